@@ -1,0 +1,318 @@
+"""Zipformer2 transducer model description, synthetic weights and on-disk format.
+
+The reference never ships the model graph: the encoder/decoder/joiner live only inside
+the `encoder-*.onnx / decoder-*.onnx / joiner-*.onnx` files that
+`core/asr_engine.py:903-1020` (`create_recognizer`) loads into onnxruntime.  Their shapes
+are pinned only by byte sizes (`offline_pwa/model_manifest.json:14-104`)
+and by icefall's Zipformer2 recipe (3P).  This module restates that
+architecture's parameter set with icefall state-dict names, so that a later
+ONNX-initializer loader only has to map names.
+
+On-disk model directory used by this build (`zasr_create` reads it):
+
+    config.json         ZipformerConfig as JSON
+    model.safetensors   every parameter below, float32, icefall names
+    tokens.txt          "piece id" per line (same format as core/asr_engine.py:980-986)
+
+Weights in this repo are always SYNTHETIC (seeded numpy PCG64): no checkpoint is
+available offline.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import os
+from collections import OrderedDict
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+BLANK_ID = 0
+UNK_ID = 2
+CONTEXT_SIZE = 2
+FEAT_DIM = 80
+
+
+@dataclasses.dataclass
+class ZipformerConfig:
+    """Zipformer2 + stateless decoder + joiner hyper-parameters."""
+    name: str = "zipformer-68m"
+    encoder_dims: Tuple[int, ...] = (192, 256, 384, 512, 384, 256)
+    num_layers: Tuple[int, ...] = (2, 2, 3, 4, 3, 2)
+    ff_dims: Tuple[int, ...] = (512, 768, 1024, 1536, 1024, 768)
+    num_heads: Tuple[int, ...] = (4, 4, 4, 8, 4, 4)
+    downsampling: Tuple[int, ...] = (1, 2, 4, 8, 4, 2)
+    cnn_kernels: Tuple[int, ...] = (31, 31, 15, 15, 15, 31)
+    query_head_dim: int = 32
+    value_head_dim: int = 12
+    pos_head_dim: int = 4
+    pos_dim: int = 48
+    vocab_size: int = 2000
+    decoder_dim: int = 512
+    joiner_dim: int = 512
+    context_size: int = CONTEXT_SIZE
+    # Conv2dSubsampling channels (icefall subsampling.py defaults)
+    layer1_channels: int = 8
+    layer2_channels: int = 32
+    layer3_channels: int = 128
+
+    @property
+    def max_dim(self) -> int:
+        return max(self.encoder_dims)
+
+    @property
+    def num_stacks(self) -> int:
+        return len(self.encoder_dims)
+
+    @property
+    def embed_out_width(self) -> int:
+        return (((FEAT_DIM - 1) // 2) - 1) // 2  # 19
+
+    def to_json(self) -> str:
+        d = dataclasses.asdict(self)
+        return json.dumps(d, indent=1)
+
+    @staticmethod
+    def from_json(text: str) -> "ZipformerConfig":
+        d = json.loads(text)
+        for k, v in list(d.items()):
+            if isinstance(v, list):
+                d[k] = tuple(v)
+        return ZipformerConfig(**d)
+
+
+def zipformer_m() -> ZipformerConfig:
+    """68M model: sherpa-onnx-zipformer-vi-2025-04-20 (core/asr_engine.py:899)."""
+    return ZipformerConfig()
+
+
+def zipformer_s() -> ZipformerConfig:
+    """30M model: zipformer-30m-rnnt-6000h (core/asr_engine.py:899)."""
+    return ZipformerConfig(
+        name="zipformer-30m",
+        encoder_dims=(192, 256, 256, 256, 256, 256),
+        num_layers=(2, 2, 2, 2, 2, 2),
+        ff_dims=(512, 768, 768, 768, 768, 768),
+        num_heads=(4, 4, 4, 8, 4, 4),
+    )
+
+
+def zipformer_tiny(vocab_size: int = 64) -> ZipformerConfig:
+    """Small test configuration (same module graph, small widths) for fast parity tests."""
+    return ZipformerConfig(
+        name="zipformer-tiny",
+        encoder_dims=(64, 96, 128, 96, 64, 64),
+        num_layers=(1, 1, 2, 1, 1, 1),
+        ff_dims=(128, 192, 256, 192, 128, 128),
+        num_heads=(2, 2, 4, 2, 2, 2),
+        cnn_kernels=(7, 7, 5, 5, 5, 7),
+        vocab_size=vocab_size,
+        decoder_dim=64,
+        joiner_dim=64,
+    )
+
+
+PRESETS = {"zipformer-68m": zipformer_m, "zipformer-30m": zipformer_s,
+           "zipformer-tiny": zipformer_tiny}
+
+
+def stack_prefix(i: int, cfg: ZipformerConfig) -> str:
+    """icefall naming: stacks with downsampling wrap the encoder in DownsampledZipformer2Encoder."""
+    return f"encoder.encoders.{i}." + ("encoder." if cfg.downsampling[i] != 1 else "")
+
+
+def param_shapes(cfg: ZipformerConfig) -> "OrderedDict[str, Tuple[int, ...]]":
+    """Parameter names/shapes of the exported transducer (encoder incl. encoder_proj,
+    decoder incl. decoder_proj, joiner output_linear)."""
+    s: "OrderedDict[str, Tuple[int, ...]]" = OrderedDict()
+    c1, c2, c3 = cfg.layer1_channels, cfg.layer2_channels, cfg.layer3_channels
+    d0 = cfg.encoder_dims[0]
+    s["encoder_embed.conv.0.weight"] = (c1, 1, 3, 3)
+    s["encoder_embed.conv.0.bias"] = (c1,)
+    s["encoder_embed.conv.4.weight"] = (c2, c1, 3, 3)
+    s["encoder_embed.conv.4.bias"] = (c2,)
+    s["encoder_embed.conv.7.weight"] = (c3, c2, 3, 3)
+    s["encoder_embed.conv.7.bias"] = (c3,)
+    s["encoder_embed.convnext.depthwise_conv.weight"] = (c3, 1, 7, 7)
+    s["encoder_embed.convnext.depthwise_conv.bias"] = (c3,)
+    s["encoder_embed.convnext.pointwise_conv1.weight"] = (3 * c3, c3, 1, 1)
+    s["encoder_embed.convnext.pointwise_conv1.bias"] = (3 * c3,)
+    s["encoder_embed.convnext.pointwise_conv2.weight"] = (c3, 3 * c3, 1, 1)
+    s["encoder_embed.convnext.pointwise_conv2.bias"] = (c3,)
+    s["encoder_embed.out.weight"] = (d0, c3 * cfg.embed_out_width)
+    s["encoder_embed.out.bias"] = (d0,)
+    s["encoder_embed.out_norm.log_scale"] = ()
+    s["encoder_embed.out_norm.bias"] = (d0,)
+    qd, vd, pd = cfg.query_head_dim, cfg.value_head_dim, cfg.pos_head_dim
+    for i in range(cfg.num_stacks):
+        d, F, h, k = cfg.encoder_dims[i], cfg.ff_dims[i], cfg.num_heads[i], cfg.cnn_kernels[i]
+        ds = cfg.downsampling[i]
+        if ds != 1:
+            s[f"encoder.encoders.{i}.downsample.bias"] = (ds,)
+            s[f"encoder.encoders.{i}.out_combiner.bypass_scale"] = (d,)
+        pre = stack_prefix(i, cfg)
+        for j in range(cfg.num_layers[i]):
+            L = f"{pre}layers.{j}."
+            s[L + "bypass.bypass_scale"] = (d,)
+            s[L + "bypass_mid.bypass_scale"] = (d,)
+            s[L + "self_attn_weights.in_proj.weight"] = ((2 * qd + pd) * h, d)
+            s[L + "self_attn_weights.in_proj.bias"] = ((2 * qd + pd) * h,)
+            s[L + "self_attn_weights.linear_pos.weight"] = (pd * h, cfg.pos_dim)
+            for a in ("self_attn1", "self_attn2"):
+                s[L + f"{a}.in_proj.weight"] = (vd * h, d)
+                s[L + f"{a}.in_proj.bias"] = (vd * h,)
+                s[L + f"{a}.out_proj.weight"] = (d, vd * h)
+                s[L + f"{a}.out_proj.bias"] = (d,)
+            for f_name, f_dim in (("feed_forward1", (F * 3) // 4), ("feed_forward2", F),
+                                  ("feed_forward3", (F * 5) // 4)):
+                s[L + f"{f_name}.in_proj.weight"] = (f_dim, d)
+                s[L + f"{f_name}.in_proj.bias"] = (f_dim,)
+                s[L + f"{f_name}.out_proj.weight"] = (d, f_dim)
+                s[L + f"{f_name}.out_proj.bias"] = (d,)
+            hid = 3 * d // 4
+            s[L + "nonlin_attention.in_proj.weight"] = (3 * hid, d)
+            s[L + "nonlin_attention.in_proj.bias"] = (3 * hid,)
+            s[L + "nonlin_attention.out_proj.weight"] = (d, hid)
+            s[L + "nonlin_attention.out_proj.bias"] = (d,)
+            for c in ("conv_module1", "conv_module2"):
+                s[L + f"{c}.in_proj.weight"] = (2 * d, d)
+                s[L + f"{c}.in_proj.bias"] = (2 * d,)
+                s[L + f"{c}.depthwise_conv.weight"] = (d, 1, k)
+                s[L + f"{c}.depthwise_conv.bias"] = (d,)
+                s[L + f"{c}.out_proj.weight"] = (d, d)
+                s[L + f"{c}.out_proj.bias"] = (d,)
+            s[L + "norm.log_scale"] = ()
+            s[L + "norm.bias"] = (d,)
+    s["encoder.downsample_output.bias"] = (2,)
+    s["encoder_proj.weight"] = (cfg.joiner_dim, cfg.max_dim)
+    s["encoder_proj.bias"] = (cfg.joiner_dim,)
+    D = cfg.decoder_dim
+    s["decoder.embedding.weight"] = (cfg.vocab_size, D)
+    s["decoder.conv.weight"] = (D, 4, cfg.context_size)  # groups = D // 4
+    s["decoder_proj.weight"] = (cfg.joiner_dim, D)
+    s["decoder_proj.bias"] = (cfg.joiner_dim,)
+    s["joiner.output_linear.weight"] = (cfg.vocab_size, cfg.joiner_dim)
+    s["joiner.output_linear.bias"] = (cfg.vocab_size,)
+    return s
+
+
+def count_params(cfg: ZipformerConfig, prefix: str = "") -> int:
+    return int(sum(int(np.prod(v)) for k, v in param_shapes(cfg).items() if k.startswith(prefix)))
+
+
+def synth_weights(cfg: ZipformerConfig, seed: int = 20261015,
+                  blank_bias: float | None = None) -> Dict[str, np.ndarray]:
+    """Seeded synthetic weights, scaled by 1/sqrt(fan_in) (SURVEY §8d "Weights").
+
+    Gains keep activations O(1) through the random network; a joiner blank-logit bias
+    makes blank win on most frames (real models emit on ~15% of encoder frames)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out: Dict[str, np.ndarray] = {}
+    qd = cfg.query_head_dim
+    for name, shape in param_shapes(cfg).items():
+        if name.endswith("log_scale"):
+            w = np.array(rng.uniform(-0.2, 0.2), dtype=np.float32).reshape(())
+        elif name.endswith("bypass_scale"):
+            w = rng.uniform(0.3, 0.9, size=shape)
+        elif name.endswith("downsample.bias") or name.endswith("downsample_output.bias"):
+            w = rng.normal(0.0, 0.5, size=shape)
+        elif name.endswith("norm.bias"):
+            w = rng.normal(0.0, 0.05, size=shape)
+        elif name.endswith(".bias"):
+            w = rng.normal(0.0, 0.02, size=shape)
+        elif name == "decoder.embedding.weight":
+            w = rng.normal(0.0, 1.0, size=shape)
+        else:
+            fan_in = int(np.prod(shape[1:]))
+            gain = 1.0
+            if ".out_proj." in name or "pointwise_conv2" in name:
+                gain = 0.5
+            if "self_attn_weights.in_proj" in name:
+                gain = qd ** -0.25 * 1.5
+            if "linear_pos" in name:
+                gain = 0.5
+            if name == "joiner.output_linear.weight":
+                gain = 1.5
+            w = rng.normal(0.0, gain / math.sqrt(fan_in), size=shape)
+        out[name] = np.ascontiguousarray(w, dtype=np.float32)
+    bb = blank_bias if blank_bias is not None else 1.0 + 0.5 * math.log(cfg.vocab_size)
+    out["joiner.output_linear.bias"][BLANK_ID] = np.float32(bb)
+    return out
+
+
+def synth_tokens(vocab_size: int, seed: int = 7) -> List[str]:
+    """Deterministic syllable-like BPE pieces; ids 0..2 are <blk>, <sos/eos>, <unk>."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    onsets = ["b", "c", "ch", "d", "đ", "g", "h", "k", "kh", "l", "m", "n", "ng", "nh", "p",
+              "ph", "qu", "r", "s", "t", "th", "tr", "v", "x", ""]
+    nuclei = ["a", "ă", "â", "e", "ê", "i", "o", "ô", "ơ", "u", "ư", "y", "ai", "ao", "ươ",
+              "iê", "uô", "oa"]
+    codas = ["", "", "n", "ng", "m", "c", "t", "nh", "ch", "p", "i", "u"]
+    toks = ["<blk>", "<sos/eos>", "<unk>"]
+    seen = set(toks)
+    while len(toks) < vocab_size:
+        p = (onsets[rng.integers(len(onsets))] + nuclei[rng.integers(len(nuclei))]
+             + codas[rng.integers(len(codas))])
+        if rng.random() < 0.6:
+            p = "▁" + p
+        if p in seen:
+            p = p + str(len(toks))
+        seen.add(p)
+        toks.append(p.upper())
+    return toks
+
+
+def save_model_dir(path: str, cfg: ZipformerConfig, weights: Dict[str, np.ndarray],
+                   tokens: List[str]) -> str:
+    from safetensors.numpy import save_file
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, "config.json"), "w") as f:
+        f.write(cfg.to_json())
+    save_file({k: np.ascontiguousarray(v, dtype=np.float32) for k, v in weights.items()},
+              os.path.join(path, "model.safetensors"))
+    with open(os.path.join(path, "tokens.txt"), "w", encoding="utf-8") as f:
+        for i, t in enumerate(tokens):
+            f.write(f"{t} {i}\n")
+    return path
+
+
+def load_model_dir(path: str):
+    from safetensors.numpy import load_file
+    with open(os.path.join(path, "config.json")) as f:
+        cfg = ZipformerConfig.from_json(f.read())
+    weights = load_file(os.path.join(path, "model.safetensors"))
+    return cfg, weights
+
+
+def make_synthetic_model_dir(path: str, preset: str = "zipformer-68m",
+                             seed: int = 20261015) -> str:
+    """Create (or reuse) a synthetic model directory for `preset`."""
+    cfg = PRESETS[preset]()
+    marker = os.path.join(path, f".synth_{preset}_{seed}")
+    if os.path.exists(marker) and os.path.exists(os.path.join(path, "model.safetensors")):
+        return path
+    save_model_dir(path, cfg, synth_weights(cfg, seed), synth_tokens(cfg.vocab_size))
+    open(marker, "w").close()
+    return path
+
+
+def seq_lengths(n_samples: int) -> Dict[str, int]:
+    """Frame-count bookkeeping for one chunk (SURVEY §8 sizes table)."""
+    T = (n_samples + 80) // 160 if n_samples > 0 else 0
+    L = (T - 7) // 2 if T >= 9 else 0
+    return {"T": T, "L": L, "T_out": (L + 1) // 2}
+
+
+def encoder_flops_per_frame(cfg: ZipformerConfig) -> Dict[str, float]:
+    """Algorithmic FLOPs of the dense projections per 50 Hz frame, per stack (for rooflines)."""
+    out = {}
+    for i in range(cfg.num_stacks):
+        d, F, h = cfg.encoder_dims[i], cfg.ff_dims[i], cfg.num_heads[i]
+        per_layer = 2.0 * ((2 * cfg.query_head_dim + cfg.pos_head_dim) * h * d
+                           + 2 * cfg.value_head_dim * h * d * 2
+                           + ((F * 3) // 4) * d * 2 + F * d * 2 + ((F * 5) // 4) * d * 2
+                           + 3 * (3 * d // 4) * d + (3 * d // 4) * d
+                           + 2 * (2 * d * d + d * d))
+        out[f"stack{i}"] = per_layer * cfg.num_layers[i] / cfg.downsampling[i]
+    return out
