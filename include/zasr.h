@@ -1,0 +1,129 @@
+/*
+ * zasr.h — C ABI of libzasr.so, the MI355X-native offline-ASR hot path
+ * (kaldi fbank -> Zipformer2 transducer encoder -> stateless decoder + joiner ->
+ *  greedy / modified-beam search with Aho-Corasick hotword biasing).
+ *
+ * Plain C types only: caller-owned input buffers are read during the call; results are
+ * library-owned until zasr_result_free (mirrors SherpaOnnxDestroyOfflineStreamResultJson,
+ * offline_pwa/static/vendor/sherpa-onnx-wasm/sherpa-onnx-asr.js:1872-1878).  Every entry
+ * point returns 0 on success and a nonzero code on failure; zasr_last_error() gives the
+ * message of the calling thread's last failure.  One handle may be used from several
+ * host threads (calls on a handle are serialised internally), matching the reference's
+ * two decode workers sharing one set of sessions (core/asr_engine.py:2291-2315).
+ *
+ * Reference interfaces each entry point replaces:
+ *   zasr_create            core/asr_engine.py:903-1020 create_recognizer (ORT sessions,
+ *                          tokens, hotword ContextGraph); sherpa-onnx
+ *                          SherpaOnnxCreateOfflineRecognizer (sherpa-onnx-asr.js:1782)
+ *   zasr_destroy           SherpaOnnxDestroyOfflineRecognizer; core/asr_engine.py:743-773
+ *                          clear_model_cache
+ *   zasr_fbank             core/asr_engine.py:698-721 compute_fbank_ort (kaldi-native-fbank)
+ *   zasr_decode_batch      core/asr_engine.py:1209-1226 decode_chunk (fbank + search) over a
+ *                          batch of chunks; SherpaOnnxAcceptWaveformOffline +
+ *                          SherpaOnnxDecodeOfflineStream (sherpa-onnx-asr.js:1799-1830)
+ *   zasr_decode_features   core/asr_engine.py:1224 _ort_beam_search with precomputed
+ *                          features (ROVER shares one fbank, core/asr_engine.py:2346-2350)
+ *   zasr_encode_features   the encoder session run, core/asr_engine.py:1045-1049
+ *   zasr_search_encoder_out  the search loop alone, core/asr_engine.py:1051-1153
+ *   zasr_result_*          the (token_ids, frames, ys_log_probs, T, emit_logits) tuple of
+ *                          core/asr_engine.py:1153 (entropy statistics instead of raw
+ *                          logits rows, reduced on device); SherpaOnnxGetOfflineStreamResult
+ */
+#ifndef ZASR_H_
+#define ZASR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct zasr_recognizer zasr_recognizer;
+typedef struct zasr_result zasr_result;
+
+enum {
+  ZASR_OK = 0,
+  ZASR_ERR_INVALID = 1,   /* bad argument */
+  ZASR_ERR_NOT_FOUND = 2, /* missing model file (reference raises FileNotFoundError) */
+  ZASR_ERR_RUNTIME = 3,   /* HIP / internal failure */
+};
+
+enum { ZASR_PRECISION_FP32 = 0, ZASR_PRECISION_BF16 = 1 };
+
+typedef struct zasr_config {
+  const char* model_dir;        /* config.json + model.safetensors (+ tokens.txt for hosts) */
+  const char* decoding_method;  /* "greedy_search" | "modified_beam_search" */
+  int32_t max_active_paths;     /* beam for modified_beam_search, 1..16 (reference: 8) */
+  float blank_penalty;          /* must be 0 (the reference applies none) */
+  /* hotwords as token-id phrases (sentencepiece encoding stays on the host,
+     core/hotword_context.py:234-248); may be NULL / 0 */
+  const int32_t* hotword_tokens;  /* concatenated phrases */
+  const int32_t* hotword_lens;    /* per-phrase token counts */
+  const float* hotword_scores;    /* per-phrase score (reference default 1.5) */
+  int32_t num_hotwords;
+  int32_t device_id;            /* HIP device ordinal */
+  int32_t precision;            /* ZASR_PRECISION_* */
+} zasr_config;
+
+int zasr_create(const zasr_config* cfg, zasr_recognizer** out);
+void zasr_destroy(zasr_recognizer* h);
+
+/* log-mel fbank of one waveform (f32 in [-1,1], 16 kHz).  out holds cap floats;
+   *n_frames = (n + 80) / 160, output row-major [n_frames][80].  h may be NULL
+   (uses device 0). */
+int zasr_fbank(zasr_recognizer* h, const float* wav, int64_t n, int32_t sample_rate, float* out,
+               int64_t cap, int64_t* n_frames);
+
+/* Decode `count` independent chunks (host buffers).  beam <= 0 uses the handle's
+   configured decoding method / max_active_paths. */
+int zasr_decode_batch(zasr_recognizer* h, const float* const* wav, const int64_t* n,
+                      int32_t count, int32_t beam, zasr_result** out);
+
+/* Same, from precomputed fbank features feats[i] of shape [n_frames[i]][80]. */
+int zasr_decode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,
+                         int32_t count, int32_t beam, zasr_result** out);
+
+/* Device-resident variant (inputs already in HBM): d_wav holds all chunks packed,
+   chunk i at element offset wav_off[i] with n[i] samples (host arrays).  stream is a
+   hipStream_t (NULL: the handle's stream).  Used by bench.py. */
+int zasr_decode_device(zasr_recognizer* h, const float* d_wav, const int64_t* wav_off,
+                       const int64_t* n, int32_t count, int32_t beam, void* stream,
+                       zasr_result** out);
+
+/* Encoder only: features -> encoder_out rows [T'_i][joiner_dim], packed in chunk order
+   into out (cap floats); t_out[i] receives T'_i. */
+int zasr_encode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,
+                         int32_t count, float* out, int64_t cap, int64_t* t_out);
+
+/* Search only, from given encoder outputs enc[i] of shape [t_out[i]][joiner_dim]. */
+int zasr_search_encoder_out(zasr_recognizer* h, const float* const* enc, const int64_t* t_out,
+                            int32_t count, int32_t beam, zasr_result** out);
+
+/* result access */
+int32_t zasr_result_count(const zasr_result* r);
+int32_t zasr_result_num_tokens(const zasr_result* r, int32_t i);
+int32_t zasr_result_num_frames(const zasr_result* r, int32_t i); /* T' of chunk i */
+const int32_t* zasr_result_tokens(const zasr_result* r, int32_t i);
+const int32_t* zasr_result_frames(const zasr_result* r, int32_t i);
+const double* zasr_result_log_probs(const zasr_result* r, int32_t i);
+/* per token 4 floats: entropy, sum p^(1/3), top1 prob, top2 prob of the emitting row */
+const float* zasr_result_token_stats(const zasr_result* r, int32_t i);
+void zasr_result_free(zasr_result* r);
+
+/* model facts */
+int32_t zasr_vocab_size(const zasr_recognizer* h);
+int32_t zasr_joiner_dim(const zasr_recognizer* h);
+
+/* profiling: per-kernel-class HIP-event timing on the handle's stream */
+int zasr_profile_enable(zasr_recognizer* h, int32_t on);
+int zasr_profile_reset(zasr_recognizer* h);
+/* writes "name count total_ms\n" lines into buf (cap bytes) */
+int zasr_profile_report(zasr_recognizer* h, char* buf, int64_t cap);
+
+const char* zasr_last_error(void);
+const char* zasr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZASR_H_ */

@@ -151,11 +151,14 @@ def parse_hotwords(path: str, default_score: float = 1.5) -> List[Tuple[str, flo
     return out
 
 
-def log_add(a: float, b: float) -> float:
+def log_add(a, b):
+    """f64 log-add.  Like the reference (core/asr_engine.py:724-728) the non-cutoff branch
+    yields an np.float64, which makes the next frame's `lp[i, :] += score` an f64 add
+    rounded to f32 (NumPy 2 / NEP 50), while a plain Python float is added in f32."""
     if a < b:
         a, b = b, a
     d = b - a
-    return a if d < -36.0 else a + float(np.log1p(np.exp(d)))
+    return a if d < -36.0 else a + np.log1p(np.exp(d))
 
 
 def beam_search(enc_out: np.ndarray, decoder: Callable[[np.ndarray], np.ndarray],

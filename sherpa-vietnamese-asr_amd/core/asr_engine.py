@@ -1,0 +1,306 @@
+"""Drop-in `core/asr_engine.py` ASR surface backed by libzasr.so on MI355X.
+
+Replaces the reference's onnxruntime + numpy hot path (`core/asr_engine.py:686-1326`)
+with the same Python names, arguments and return shapes, so the reference's callers
+(`TranscriberPipeline._run_pipeline` :2057-2494, `transcriber.py:26-34`,
+`web_service/queue_manager.py:435-443`) keep working:
+
+  get_ort()                      :686   import-compatible stub (no onnxruntime in this build)
+  compute_fbank_ort(audio, sr)   :698   kaldi fbank -> HIP kernel
+  _log_add(a, b)                 :724
+  create_recognizer(...)         :903   dict with the same keys; sessions -> one zasr handle
+  _ort_beam_search(rec, f, beam) :1023  (token_ids, frames, ys_log_probs, T, emit_stats)
+  _compute_token_entropy(x, V)   :1159  accepts device stats (or a raw logits row)
+  _finalize_word_entropy(w)      :1187
+  decode_chunk(...)              :1209  same word dicts (BPE merge, timestamps, entropy)
+  decode_chunks(...)             new    batched decode of many chunks in one GPU pass
+
+The search and the word post-processing stay semantically identical to the reference;
+the arithmetic runs in libzasr (see DESIGN.md for precision modes and tolerances).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import threading
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from zasr.binding import Recognizer
+
+logger = logging.getLogger(__name__)
+
+ROVER_MODEL_IDS = ["zipformer-30m-rnnt-6000h", "sherpa-onnx-zipformer-vi-2025-04-20"]
+ROVER_MODEL_ID = "rover-voting"
+BLANK_ID = 0
+UNK_ID = 2
+CONTEXT_SIZE = 2
+
+_recognizer_cache: Dict[tuple, dict] = {}
+_cache_lock = threading.Lock()
+_last_handle: Optional[Recognizer] = None
+
+
+def get_ort():
+    """The MI355X build has no onnxruntime; kept importable for `core/__init__.py:40-48`."""
+    raise RuntimeError("onnxruntime is not part of the MI355X build: ASR runs in libzasr.so")
+
+
+class TokenStats:
+    """Per-token joiner-row statistics computed on device: entropy, sum p^(1/3), top1, top2.
+    Stands in for the raw logits row the reference keeps per emitted token (:1125)."""
+    __slots__ = ("entropy", "s3", "top1", "top2")
+
+    def __init__(self, row):
+        self.entropy, self.s3, self.top1, self.top2 = (float(x) for x in row)
+
+
+def _default_handle() -> Recognizer:
+    if _last_handle is None:
+        raise RuntimeError("compute_fbank_ort needs a recognizer: call create_recognizer first")
+    return _last_handle
+
+
+def compute_fbank_ort(audio, sr=16000):
+    """80-bin kaldi log-mel fbank (reference :698-721) computed by the HIP fbank kernel."""
+    if sr != 16000:
+        raise ValueError("only 16 kHz input is supported (reference resamples on load)")
+    return _default_handle().fbank(np.asarray(audio, dtype=np.float32))
+
+
+def _log_add(a, b):
+    if a < b:
+        a, b = b, a
+    diff = b - a
+    return a if diff < -36.0 else a + np.log1p(np.exp(diff))
+
+
+def clear_model_cache(which="all"):
+    global _last_handle
+    if which in ("all", "recognizer"):
+        with _cache_lock:
+            for rec in _recognizer_cache.values():
+                rec["handle"].close()
+            _recognizer_cache.clear()
+            _last_handle = None
+
+
+def _load_tokens(path: str) -> Dict[int, str]:
+    id2token = {}
+    with open(path, "r", encoding="utf-8") as f:
+        for line in f:
+            parts = line.strip().split()
+            if len(parts) >= 2:
+                id2token[int(parts[-1])] = parts[0]
+    return id2token
+
+
+def _hotword_token_lists(model_path: str, hotwords_file: Optional[str], default_score: float):
+    """Hotword phrases -> token ids with the model's sentencepiece model (host side, as in
+    core/hotword_context.py:225-259).  Without bpe.model no graph is built (reference :999)."""
+    bpe = os.path.join(model_path, "bpe.model")
+    if not hotwords_file or not os.path.exists(bpe):
+        return [], []
+    from core.hotword_context import parse_hotwords_file
+    phrases = parse_hotwords_file(hotwords_file, default_score)
+    if not phrases:
+        return [], []
+    import sentencepiece as spm
+    sp = spm.SentencePieceProcessor()
+    sp.load(bpe)
+    seqs, scores = [], []
+    for text, score in phrases:
+        ids = sp.encode(text, out_type=int)
+        if ids:
+            seqs.append(ids)
+            scores.append(score)
+    return seqs, scores
+
+
+def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_provider="cpu",
+                      hotwords=None, device_id=None, precision=None):
+    """Load (or reuse) a recognizer for `model_path` (reference :903-1020).
+
+    Model directory: config.json + model.safetensors + tokens.txt (zasr/model.py).  Raises
+    FileNotFoundError when files are missing, like the reference (:927-928).
+    `hotwords` may be (token_id_lists, scores) to bypass the file + bpe.model route.
+    """
+    provider_policy = str(execution_provider or "cpu").lower()
+    dev = int(os.environ.get("ZASR_DEVICE", "0")) if device_id is None else int(device_id)
+    prec = precision or os.environ.get("ZASR_PRECISION", "fp32")
+    key = (os.path.normpath(model_path), cpu_threads, max_active_paths, provider_policy, dev, prec,
+           None if hotwords is None else repr(hotwords))
+    global _last_handle
+    with _cache_lock:
+        if key in _recognizer_cache:
+            _last_handle = _recognizer_cache[key]["handle"]
+            return _recognizer_cache[key]
+        tokens_path = os.path.join(model_path, "tokens.txt")
+        need = [os.path.join(model_path, "config.json"), os.path.join(model_path, "model.safetensors"),
+                tokens_path]
+        if not all(os.path.exists(p) for p in need):
+            raise FileNotFoundError(f"Thiếu file model trong: {model_path}")
+        if hotwords is not None:
+            seqs, scores = [list(map(int, s)) for s in hotwords[0]], list(map(float, hotwords[1]))
+        else:
+            hw_file = os.environ.get("ZASR_HOTWORDS_FILE", "")
+            seqs, scores = _hotword_token_lists(model_path, hw_file,
+                                                float(os.environ.get("ZASR_HOTWORDS_SCORE", 1.5)))
+        handle = Recognizer(model_path, "modified_beam_search", int(max_active_paths),
+                            hotwords=seqs, hotword_scores=scores, device_id=dev, precision=prec)
+        info = {"actual_provider": f"MI355X:HIP(device {dev}, {prec})"}
+        rec = {
+            "handle": handle,
+            "id2token": _load_tokens(tokens_path),
+            "vocab_size": handle.vocab_size,
+            "max_active_paths": int(max_active_paths),
+            "model_path": model_path,
+            "dec_cache": {},
+            "context_graph": {"num_phrases": len(seqs)} if seqs else None,
+            "provider_info": {"encoder": info, "decoder": info, "joiner": info},
+        }
+        _recognizer_cache[key] = rec
+        _last_handle = handle
+        return rec
+
+
+def _ort_beam_search(recognizer, features, beam_size=8):
+    """Modified beam search over one chunk's features (reference :1023-1153).
+    Returns (token_ids, frames, ys_log_probs, T, emit_stats)."""
+    r = recognizer["handle"].decode_features([np.asarray(features, np.float32)],
+                                            beam=int(beam_size))[0]
+    return (r.token_ids.tolist(), r.frames.tolist(), r.log_probs.tolist(), int(r.T),
+            [TokenStats(s) for s in r.stats])
+
+
+def _compute_token_entropy(raw_logits, V):
+    """Entropy metrics of one emitted token (reference :1159-1181).  Accepts the device
+    TokenStats (normal path) or a raw logits row (computed as the reference does)."""
+    max_entropy = math.log(V) if V > 1 else 1.0
+    alpha = 1.0 / 3.0
+    ts_max = (1.0 / (alpha - 1.0)) * (1.0 - V ** (1.0 - alpha)) if V > 1 else 1.0
+    if isinstance(raw_logits, TokenStats):
+        entropy, s3, top1, top2 = raw_logits.entropy, raw_logits.s3, raw_logits.top1, raw_logits.top2
+    else:
+        z = np.asarray(raw_logits, np.float32)
+        p = np.exp(z - np.max(z))
+        p /= np.sum(p)
+        entropy = -float(np.sum(p * np.log(p + 1e-30)))
+        s3 = float(np.sum(p ** alpha))
+        srt = np.sort(p)[::-1]
+        top1 = float(srt[0])
+        top2 = float(srt[1]) if len(srt) > 1 else 1e-10
+    tsallis = (1.0 / (alpha - 1.0)) * (1.0 - s3)
+    return {
+        "tsallis_norm": round(float(tsallis / ts_max if ts_max > 0 else 0.0), 4),
+        "margin": round(top1 - top2, 4),
+        "entropy_norm": round(entropy / max_entropy, 4),
+        "top1_prob": top1,
+    }
+
+
+_ENTROPY_FALLBACK = {"tsallis_norm": 0, "margin": 1, "entropy_norm": 0, "top1_prob": 1.0}
+
+
+def _finalize_word_entropy(w):
+    """BPE-level -> word-level aggregation (reference :1187-1206)."""
+    probs = w.pop("probs")
+    w["prob"] = sum(probs) / len(probs)
+    ents = w.pop("_ents", [])
+    if ents:
+        w["tsallis_max"] = round(float(max(e["tsallis_norm"] for e in ents)), 4)
+        w["margin_min"] = round(float(min(e["margin"] for e in ents)), 4)
+        w["entropy_norm"] = round(float(np.mean([e["entropy_norm"] for e in ents])), 4)
+        confs = [e["margin"] * (1.0 - e["tsallis_norm"]) for e in ents]
+        w["_conf"] = round(float(sum(confs) / len(confs)), 4)
+    else:
+        w["tsallis_max"] = w["margin_min"] = w["entropy_norm"] = w["_conf"] = None
+
+
+def _words_from_search(id2token, V, n_samples, time_offset, token_ids, frames, log_probs, T,
+                       emit_stats):
+    """BPE -> word dicts with timestamps, probabilities and entropy (reference :1227-1326)."""
+    if not token_ids:
+        return []
+    pieces = [id2token.get(t, "") for t in token_ids]
+    chunk_dur = n_samples / 16000.0
+    ts = [f / T * chunk_dur for f in frames] if T > 0 else []
+    if not ts:
+        return []
+    avg = (ts[-1] - ts[0]) / (len(ts) - 1) if len(ts) >= 2 else 0.08
+    ents = [_compute_token_entropy(emit_stats[j], V) if j < len(emit_stats) else _ENTROPY_FALLBACK
+            for j in range(len(token_ids))]
+    words: List[dict] = []
+    cur = None
+    for j, (t0, piece) in enumerate(zip(ts, pieces)):
+        text = piece.lower()
+        t1 = ts[j + 1] if j + 1 < len(ts) else t0 + avg
+        prob = math.exp(log_probs[j]) if j < len(log_probs) else 1.0
+        ent = ents[j]
+        starts_word = text.startswith(" ") or text.startswith("▁")
+        if starts_word or cur is None:
+            if cur is not None:
+                _finalize_word_entropy(cur)
+                words.append(cur)
+            cur = {"text": text.lstrip(" ").lstrip("▁") if starts_word else text,
+                   "start": t0 + time_offset, "end": t1 + time_offset,
+                   "local_start": t0, "local_end": t1, "last_bpe_start": t0 + time_offset,
+                   "probs": [prob], "_ents": [ent] if ent else []}
+        else:
+            cur["text"] += text
+            cur["end"] = t1 + time_offset
+            cur["local_end"] = t1
+            cur["last_bpe_start"] = t0 + time_offset
+            cur["probs"].append(prob)
+            if ent:
+                cur["_ents"].append(ent)
+    if cur is not None:
+        _finalize_word_entropy(cur)
+        words.append(cur)
+    if words:
+        words[0]["_chunk_bpe_tokens"] = list(pieces)
+        words[0]["_chunk_bpe_timestamps_local"] = list(ts)
+    for i, w in enumerate(words):
+        end = w["last_bpe_start"] + avg
+        if i + 1 < len(words):
+            end = min(end, words[i + 1]["start"])
+        w["end"] = end
+        w["local_end"] = end - time_offset
+        del w["last_bpe_start"]
+    return words
+
+
+def decode_chunk(recognizer, audio_chunk, time_offset=0.0, precomputed_features=None):
+    """Decode one chunk into merged word dicts (reference :1209-1326)."""
+    beam = recognizer.get("max_active_paths", 8)
+    h: Recognizer = recognizer["handle"]
+    if precomputed_features is not None:
+        feats = np.asarray(precomputed_features, np.float32)
+        if feats.shape[0] == 0:
+            return []
+        r = h.decode_features([feats], beam=beam)[0]
+    else:
+        a = np.asarray(audio_chunk, np.float32)
+        if a.shape[0] == 0:
+            return []
+        r = h.decode([a], beam=beam)[0]
+    return _words_from_search(recognizer["id2token"], recognizer["vocab_size"], len(audio_chunk),
+                              time_offset, r.token_ids.tolist(), r.frames.tolist(),
+                              r.log_probs.tolist(), int(r.T), [TokenStats(s) for s in r.stats])
+
+
+def decode_chunks(recognizer, chunks: Sequence[np.ndarray], time_offsets: Sequence[float],
+                  precomputed_features: Optional[Sequence[np.ndarray]] = None):
+    """Batched decode_chunk: every chunk goes through one GPU pass (fbank, encoder, search)."""
+    beam = recognizer.get("max_active_paths", 8)
+    h: Recognizer = recognizer["handle"]
+    if precomputed_features is not None:
+        res = h.decode_features([np.asarray(f, np.float32) for f in precomputed_features], beam=beam)
+    else:
+        res = h.decode([np.asarray(c, np.float32) for c in chunks], beam=beam)
+    return [_words_from_search(recognizer["id2token"], recognizer["vocab_size"], len(c), off,
+                               r.token_ids.tolist(), r.frames.tolist(), r.log_probs.tolist(),
+                               int(r.T), [TokenStats(s) for s in r.stats])
+            for c, off, r in zip(chunks, time_offsets, res)]

@@ -1,0 +1,59 @@
+// Shared helpers for libzasr (host + device).  gfx950 / CDNA4 only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#define ZASR_HIP_CHECK(expr)                                                          \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +    \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__) +   \
+                               " in " #expr);                                         \
+    }                                                                                 \
+  } while (0)
+
+#define ZASR_REQUIRE(cond, msg)                                                       \
+  do {                                                                                \
+    if (!(cond)) throw std::runtime_error(std::string("zasr: ") + (msg));             \
+  } while (0)
+
+namespace zasr {
+
+constexpr int kWave = 64;
+
+__host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ inline long cdivl(long a, long b) { return (a + b - 1) / b; }
+
+// Activation functions (icefall scaling.py SwooshL/SwooshR ONNX forms).
+__device__ __forceinline__ float softplusf(float x) {
+  // log(1 + exp(x)), stable for large |x|
+  return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x)));
+}
+__device__ __forceinline__ float swooshl(float x) { return softplusf(x - 4.f) - 0.08f * x - 0.035f; }
+__device__ __forceinline__ float swooshr(float x) {
+  return softplusf(x - 1.f) - 0.08f * x - 0.313261687f;
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace zasr

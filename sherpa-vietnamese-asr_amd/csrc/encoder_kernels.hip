@@ -1,0 +1,586 @@
+// Non-GEMM kernels of the encoder path: fbank, Conv2dSubsampling convs, attention softmax,
+// and the Zipformer2 elementwise / per-sequence operators.  All HBM-streaming kernels read
+// and write row-contiguous activations with float4 per lane where the width allows.
+#include "common.h"
+#include "kernels.h"
+
+namespace zasr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// index of the sequence that owns packed row `r`: largest b with off[b] <= r
+__device__ __forceinline__ int find_seq(const int* off, int nseq, int r) {
+  int lo = 0, hi = nseq - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= r) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// =====================================================================================
+// fbank: one wave per frame.  Samples gathered with kaldi edge reflection, DC removal,
+// pre-emphasis and povey window in f32, 512-point FFT in f64 (knf's rdft runs in double),
+// power spectrum f32, sparse mel triangles, log with FLT_EPSILON floor.
+// =====================================================================================
+constexpr int kFbWaves = 4;
+
+__global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
+    const float* __restrict__ wav, const long* __restrict__ wav_off,
+    const int* __restrict__ nsamp, const int* __restrict__ fr_off, int nseq, int total_frames,
+    FbankTables tabs, float* __restrict__ out) {
+  __shared__ float sx[kFbWaves][400];
+  __shared__ double sre[kFbWaves][512];
+  __shared__ double sim[kFbWaves][512];
+  __shared__ float spow[kFbWaves][256];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int frame = blockIdx.x * kFbWaves + w;
+  const bool active = frame < total_frames;
+  float* x = sx[w];
+  double* re = sre[w];
+  double* im = sim[w];
+  int b = 0, f = 0, n = 1;
+  if (active) {
+    b = find_seq(fr_off, nseq, frame);
+    f = frame - fr_off[b];
+    n = nsamp[b];
+    const float* base = wav + wav_off[b];
+    double part = 0.0;
+    for (int i = lane; i < 400; i += 64) {
+      long s = (long)f * 160 - 120 + i;
+      while (s < 0 || s >= n) s = (s < 0) ? (-s - 1) : (2L * n - 1 - s);
+      float v = base[s];
+      x[i] = v;
+      part += (double)v;
+    }
+    const float mean = (float)(wave_sum_d(part) / 400.0);
+    for (int i = lane; i < 400; i += 64) x[i] = x[i] - mean;
+  }
+  __syncthreads();
+  if (active) {
+    // pre-emphasis on the DC-removed frame (uses the un-emphasised left neighbour), window,
+    // scatter to bit-reversed positions
+    for (int i = lane; i < 512; i += 64) {
+      double v = 0.0;
+      if (i < 400) {
+        float cur = x[i];
+        float prev = (i == 0) ? x[0] : x[i - 1];
+        float e = __fsub_rn(cur, __fmul_rn(0.97f, prev));
+        v = (double)__fmul_rn(e, tabs.window[i]);
+      }
+      int r = __brev(i) >> 23;  // 9-bit reversal
+      re[r] = v;
+      im[r] = 0.0;
+    }
+  }
+  __syncthreads();
+  for (int half = 1; half < 512; half <<= 1) {
+    if (active) {
+      const int tstep = 256 / half;
+      for (int q = 0; q < 4; ++q) {
+        int bf = lane + 64 * q;
+        int grp = bf / half, j = bf - grp * half;
+        int i0 = grp * 2 * half + j, i1 = i0 + half;
+        double wr = tabs.twiddle[2 * (j * tstep)], wi = tabs.twiddle[2 * (j * tstep) + 1];
+        double tr = wr * re[i1] - wi * im[i1];
+        double ti = wr * im[i1] + wi * re[i1];
+        double ar = re[i0], ai = im[i0];
+        re[i1] = ar - tr;
+        im[i1] = ai - ti;
+        re[i0] = ar + tr;
+        im[i0] = ai + ti;
+      }
+    }
+    __syncthreads();
+  }
+  if (active) {
+    for (int k = lane; k < 256; k += 64) {
+      float a = (float)re[k], c = (float)im[k];
+      spow[w][k] = __fadd_rn(__fmul_rn(a, a), __fmul_rn(c, c));
+    }
+  }
+  __syncthreads();
+  if (active) {
+    for (int m = lane; m < 80; m += 64) {
+      const int st = tabs.mel_start[m], ln = tabs.mel_len[m], wo = tabs.mel_woff[m];
+      float acc = 0.f;
+      for (int k = 0; k < ln; ++k) acc = fmaf(tabs.mel_w[wo + k], spow[w][st + k], acc);
+      out[(long)frame * 80 + m] = logf(fmaxf(acc, 1.1920928955078125e-07f));
+    }
+  }
+}
+
+void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const int* fr_off,
+                  int nseq, int total_frames, const FbankTables& tabs, float* out,
+                  hipStream_t st) {
+  if (total_frames <= 0) return;
+  hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(total_frames, kFbWaves)), dim3(64 * kFbWaves), 0,
+                     st, wav, wav_off, nsamp, fr_off, nseq, total_frames, tabs, out);
+}
+
+// =====================================================================================
+// conv.0: Conv2d(1 -> 8, 3x3, padding (0, 1)) + SwooshR.  One thread per (t, f).
+// =====================================================================================
+__global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict__ fb_off,
+                             const int* __restrict__ c1_off, int nseq, int total,
+                             const float* __restrict__ w, const float* __restrict__ bias,
+                             float* __restrict__ out) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total * 80) return;
+  int row = e / 80, f = e - row * 80;
+  int b = find_seq(c1_off, nseq, row);
+  int t = row - c1_off[b];
+  const float* src = fb + (long)(fb_off[b] + t) * 80;
+  float xin[9];
+#pragma unroll
+  for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+    for (int kf = 0; kf < 3; ++kf) {
+      int ff = f + kf - 1;
+      xin[kt * 3 + kf] = (ff >= 0 && ff < 80) ? src[kt * 80 + ff] : 0.f;
+    }
+  float4 o0, o1;
+  float r[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    float acc = bias[o];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc = fmaf(w[o * 9 + k], xin[k], acc);
+    r[o] = swooshr(acc);
+  }
+  o0 = make_float4(r[0], r[1], r[2], r[3]);
+  o1 = make_float4(r[4], r[5], r[6], r[7]);
+  float4* dst = reinterpret_cast<float4*>(out + (long)e * 8);
+  dst[0] = o0;
+  dst[1] = o1;
+}
+
+void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, int nseq, int total_rows,
+                  const float* w, const float* b, float* out, hipStream_t st) {
+  if (total_rows <= 0) return;
+  long n = (long)total_rows * 80;
+  hipLaunchKernelGGL(conv1_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off, c1_off,
+                     nseq, total_rows, w, b, out);
+}
+
+// =====================================================================================
+// ConvNeXt depthwise Conv2d(128, 7x7, padding 3) over [L][19][128] per sequence.
+// One thread per output element, channel fastest (coalesced).
+// =====================================================================================
+__global__ void dwconv2d_kernel(const float* __restrict__ x, const int* __restrict__ L_off,
+                                int nseq, int total_rows, const float* __restrict__ w,
+                                const float* __restrict__ bias, float* __restrict__ out) {
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)total_rows * 19 * 128;
+  if (e >= total) return;
+  int c = e & 127;
+  long rf = e >> 7;
+  int row = (int)(rf / 19), f = (int)(rf - (long)row * 19);
+  int b = find_seq(L_off, nseq, row);
+  int t = row - L_off[b];
+  int L = L_off[b + 1] - L_off[b];
+  const float* xs = x + (long)L_off[b] * 19 * 128;
+  float acc = bias[c];
+  const float* wc = w + c * 49;
+  for (int i = 0; i < 7; ++i) {
+    int tt = t + i - 3;
+    if (tt < 0 || tt >= L) continue;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      int ff = f + j - 3;
+      if (ff < 0 || ff >= 19) continue;
+      acc = fmaf(wc[i * 7 + j], xs[((long)tt * 19 + ff) * 128 + c], acc);
+    }
+  }
+  out[e] = acc;
+}
+
+void launch_dwconv2d(const float* x, const int* L_off, int nseq, int total_rows, const float* w,
+                     const float* b, float* out, hipStream_t st) {
+  if (total_rows <= 0) return;
+  long n = (long)total_rows * 19 * 128;
+  hipLaunchKernelGGL(dwconv2d_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, L_off, nseq,
+                     total_rows, w, b, out);
+}
+
+// =====================================================================================
+// BiasNorm (+ optional bypass): one wave per row.
+// =====================================================================================
+__global__ void bias_norm_kernel(float* __restrict__ x, int rows, int d,
+                                 const float* __restrict__ bias, float scale,
+                                 const float* __restrict__ orig,
+                                 const float* __restrict__ bscale) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float* xr = x + (long)row * d;
+  float ss = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    float v = xr[c] - bias[c];
+    ss = fmaf(v, v, ss);
+  }
+  ss = wave_sum(ss);
+  float k = scale / sqrtf(ss / (float)d);
+  if (orig) {
+    const float* orow = orig + (long)row * d;
+    for (int c = lane; c < d; c += 64) {
+      float o = orow[c];
+      xr[c] = o + (xr[c] * k - o) * bscale[c];
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) xr[c] = xr[c] * k;
+  }
+}
+
+void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_scale,
+                      const float* orig, const float* bypass_scale, hipStream_t st) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(bias_norm_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, d, bias,
+                     expf(log_scale), orig, bypass_scale);
+}
+
+// =====================================================================================
+// elementwise: bypass, GLU, nonlin prep (float4 over channels; d % 4 == 0)
+// =====================================================================================
+__global__ void bypass_kernel(float* __restrict__ x, const float* __restrict__ orig,
+                              const float* __restrict__ s, long n4, int d4) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  int c4 = (int)(i % d4);
+  float4 v = reinterpret_cast<float4*>(x)[i];
+  float4 o = reinterpret_cast<const float4*>(orig)[i];
+  float4 k = reinterpret_cast<const float4*>(s)[c4];
+  v.x = o.x + (v.x - o.x) * k.x;
+  v.y = o.y + (v.y - o.y) * k.y;
+  v.z = o.z + (v.z - o.z) * k.z;
+  v.w = o.w + (v.w - o.w) * k.w;
+  reinterpret_cast<float4*>(x)[i] = v;
+}
+
+void launch_bypass(float* x, const float* orig, const float* s, long rows, int d,
+                   hipStream_t st) {
+  long n4 = rows * d / 4;
+  if (n4 <= 0) return;
+  hipLaunchKernelGGL(bypass_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, x, orig, s, n4,
+                     d / 4);
+}
+
+__global__ void glu_kernel(const float* __restrict__ x2, float* __restrict__ g, long n4,
+                           int d4) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  long r = i / d4;
+  int c4 = (int)(i - r * d4);
+  const float4* row = reinterpret_cast<const float4*>(x2) + r * 2 * d4;
+  float4 a = row[c4], s = row[d4 + c4];
+  float4 o;
+  o.x = a.x * sigmoidf_(s.x);
+  o.y = a.y * sigmoidf_(s.y);
+  o.z = a.z * sigmoidf_(s.z);
+  o.w = a.w * sigmoidf_(s.w);
+  reinterpret_cast<float4*>(g)[i] = o;
+}
+
+void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st) {
+  long n4 = rows * d / 4;
+  if (n4 <= 0) return;
+  hipLaunchKernelGGL(glu_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, x2, g, n4, d / 4);
+}
+
+__global__ void nonlin_prep_kernel(const float* __restrict__ h3, float* __restrict__ t1, long n4,
+                                   int h4) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  long r = i / h4;
+  int c4 = (int)(i - r * h4);
+  const float4* row = reinterpret_cast<const float4*>(h3) + r * 3 * h4;
+  float4 s = row[c4], x = row[h4 + c4];
+  float4 o;
+  o.x = tanhf(s.x) * x.x;
+  o.y = tanhf(s.y) * x.y;
+  o.z = tanhf(s.z) * x.z;
+  o.w = tanhf(s.w) * x.w;
+  reinterpret_cast<float4*>(t1)[i] = o;
+}
+
+void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStream_t st) {
+  long n4 = rows * hid / 4;
+  if (n4 <= 0) return;
+  hipLaunchKernelGGL(nonlin_prep_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, h3, t1, n4,
+                     hid / 4);
+}
+
+// =====================================================================================
+// depthwise conv1d over time (ConvolutionModule), zero padding per sequence, + SwooshR
+// =====================================================================================
+__global__ void dwconv1d_kernel(const float* __restrict__ x, const int* __restrict__ off,
+                                int nseq, int total_rows, int d, int K,
+                                const float* __restrict__ w, const float* __restrict__ bias,
+                                float* __restrict__ out) {
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)total_rows * d) return;
+  int row = (int)(e / d), c = (int)(e - (long)row * d);
+  int b = find_seq(off, nseq, row);
+  int lo = off[b], hi = off[b + 1];
+  int half = K >> 1;
+  float acc = bias[c];
+  const float* wc = w + (long)c * K;
+  for (int k = 0; k < K; ++k) {
+    int rr = row + k - half;
+    if (rr < lo || rr >= hi) continue;
+    acc = fmaf(wc[k], x[(long)rr * d + c], acc);
+  }
+  out[e] = swooshr(acc);
+}
+
+void launch_dwconv1d(const float* x, const int* off, int nseq, int total_rows, int d, int K,
+                     const float* w, const float* b, float* out, hipStream_t st) {
+  long n = (long)total_rows * d;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(dwconv1d_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, off, nseq,
+                     total_rows, d, K, w, b, out);
+}
+
+// =====================================================================================
+// SimpleDownsample / SimpleUpsample + bypass, convert_num_channels
+// =====================================================================================
+struct DsW {
+  float w[8];
+};
+
+__global__ void downsample_kernel(const float* __restrict__ x, const int* __restrict__ off_in,
+                                  const int* __restrict__ off_out, int nseq, int total_out,
+                                  int d, int ds, DsW wts, float* __restrict__ out) {
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)total_out * d) return;
+  int r = (int)(e / d), c = (int)(e - (long)r * d);
+  int b = find_seq(off_out, nseq, r);
+  int tp = r - off_out[b];
+  int base = off_in[b];
+  int L = off_in[b + 1] - base;
+  float acc = 0.f;
+  for (int u = 0; u < ds; ++u) {
+    int t = tp * ds + u;
+    if (t > L - 1) t = L - 1;
+    acc = fmaf(wts.w[u], x[(long)(base + t) * d + c], acc);
+  }
+  out[e] = acc;
+}
+
+void launch_downsample(const float* x, const int* off_in, const int* off_out, int nseq,
+                       int total_out, int d, int ds, const float* w_host8, float* out,
+                       hipStream_t st) {
+  long n = (long)total_out * d;
+  if (n <= 0) return;
+  DsW w{};
+  for (int i = 0; i < ds && i < 8; ++i) w.w[i] = w_host8[i];
+  hipLaunchKernelGGL(downsample_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in,
+                     off_out, nseq, total_out, d, ds, w, out);
+}
+
+__global__ void upsample_combine_kernel(const float* __restrict__ xd,
+                                        const float* __restrict__ orig,
+                                        const int* __restrict__ off_in,
+                                        const int* __restrict__ off_ds, int nseq,
+                                        int total_rows, int d, int ds,
+                                        const float* __restrict__ s, float* __restrict__ y) {
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)total_rows * d) return;
+  int r = (int)(e / d), c = (int)(e - (long)r * d);
+  int b = find_seq(off_in, nseq, r);
+  int t = r - off_in[b];
+  float up = xd[(long)(off_ds[b] + t / ds) * d + c];
+  float o = orig[e];
+  y[e] = o + (up - o) * s[c];
+}
+
+void launch_upsample_combine(const float* xd, const float* orig, const int* off_in,
+                             const int* off_ds, int nseq, int total_rows, int d, int ds,
+                             const float* s, float* y, hipStream_t st) {
+  long n = (long)total_rows * d;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(upsample_combine_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig,
+                     off_in, off_ds, nseq, total_rows, d, ds, s, y);
+}
+
+__global__ void copy_cols_kernel(const float* __restrict__ src, int lds, int c0,
+                                 float* __restrict__ dst, int ldd, int d0, int ncols, long rows,
+                                 int zero_rest, int dst_width) {
+  int width = zero_rest ? dst_width : ncols;
+  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * width) return;
+  long r = e / width;
+  int c = (int)(e - r * width);
+  float v = (c < ncols) ? src[r * lds + c0 + c] : 0.f;
+  dst[r * ldd + d0 + c] = v;
+}
+
+void launch_copy_cols(const float* src, int lds, int c0, float* dst, int ldd, int d0, int ncols,
+                      long rows, bool zero_rest, int dst_width, hipStream_t st) {
+  int width = zero_rest ? dst_width : ncols;
+  long n = rows * width;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(copy_cols_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src, lds, c0, dst,
+                     ldd, d0, ncols, rows, zero_rest ? 1 : 0, dst_width);
+}
+
+// =====================================================================================
+// Attention weights: S[i][j] = q_i . k_j (32 dims, f32 MFMA 32x32x2) + p_i . R[j - i] (4 dims),
+// softmax over j < L.  Block = 4 waves = 32 query rows of one (sequence, head); waves stride
+// over 32-key blocks.  Pass 1: per-lane online (max, sum) merged across lanes and waves.
+// Pass 2: recompute scores and write normalised weights A[h][i][j] (row stride lda = L4).
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
+  const int b = blockIdx.y;
+  const int h = blockIdx.z;
+  const int r0 = a.row_off[b];
+  const int L = a.row_off[b + 1] - r0;
+  const int i0 = blockIdx.x * 32;
+  if (i0 >= L) return;
+  const int H = a.H;
+  const int ldq = 68 * H;
+  const int lda = (L + 3) & ~3;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int hl = lane >> 5;
+  const int col = lane & 31;
+
+  __shared__ float sQ[32][33];   // [k][i]
+  __shared__ float sP[32][4];    // pos query of row i
+  __shared__ float sM[4][32], sS[4][32];
+  __shared__ float fM[32], fInv[32];
+
+  for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+    int i = e >> 5, k = e & 31;
+    float v = 0.f;
+    if (i0 + i < L) v = a.qkp[(long)(r0 + i0 + i) * ldq + h * 32 + k];
+    sQ[k][i] = v;
+  }
+  if (threadIdx.x < 128) {
+    int i = threadIdx.x >> 2, c = threadIdx.x & 3;
+    float v = 0.f;
+    if (i0 + i < L) v = a.qkp[(long)(r0 + i0 + i) * ldq + 64 * H + h * 4 + c];
+    sP[i][c] = v;
+  }
+  __syncthreads();
+
+  const float* kbase = a.qkp + (long)r0 * ldq + 32 * H + h * 32;
+  const float* pos = a.pos_tab + h * 4;
+  const int ldp = 4 * H;
+  const int nkb = (L + 31) / 32;
+
+  auto scores = [&](int j0, f32x16& acc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int j = j0 + col;
+    float kreg[16];
+    if (j < L) {
+      const float4* kp = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 * hl);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 v = kp[q];
+        kreg[4 * q] = v.x;
+        kreg[4 * q + 1] = v.y;
+        kreg[4 * q + 2] = v.z;
+        kreg[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) kreg[q] = 0.f;
+    }
+    // MFMA step s: lane half hl covers k = 16*hl + s (A: Q[i][k], B: K[j][k])
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      float av = sQ[16 * hl + s][col];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, kreg[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const int x = j - (i0 + i);
+      const float4 pr = *reinterpret_cast<const float4*>(pos + (long)(x + a.pmax - 1) * ldp);
+      float ps = sP[i][0] * pr.x;
+      ps = fmaf(sP[i][1], pr.y, ps);
+      ps = fmaf(sP[i][2], pr.z, ps);
+      ps = fmaf(sP[i][3], pr.w, ps);
+      acc[r] = (j < L) ? acc[r] + ps : -INFINITY;
+    }
+  };
+
+  float m[16], l[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+  for (int kb = wid; kb < nkb; kb += 4) {
+    f32x16 acc;
+    scores(kb * 32, acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float s = acc[r];
+      if (s == -INFINITY) continue;
+      if (s > m[r]) {
+        l[r] = l[r] * expf(m[r] - s) + 1.f;
+        m[r] = s;
+      } else {
+        l[r] += expf(s - m[r]);
+      }
+    }
+  }
+  // merge over the 32 lanes sharing a row
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      float om = __shfl_xor(m[r], o, 64);
+      float ol = __shfl_xor(l[r], o, 64);
+      float nm = fmaxf(m[r], om);
+      float nl = 0.f;
+      if (m[r] != -INFINITY) nl += l[r] * expf(m[r] - nm);
+      if (om != -INFINITY) nl += ol * expf(om - nm);
+      m[r] = nm;
+      l[r] = nl;
+    }
+    if (col == 0) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * hl;
+      sM[wid][i] = m[r];
+      sS[wid][i] = l[r];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int i = threadIdx.x;
+    float mm = -INFINITY;
+    for (int w = 0; w < 4; ++w) mm = fmaxf(mm, sM[w][i]);
+    float ss = 0.f;
+    for (int w = 0; w < 4; ++w)
+      if (sM[w][i] != -INFINITY) ss += sS[w][i] * expf(sM[w][i] - mm);
+    fM[i] = mm;
+    fInv[i] = 1.f / ss;
+  }
+  __syncthreads();
+  float* out = a.attn + a.a_off[b] + (long)h * L * lda;
+  for (int kb = wid; kb < nkb; kb += 4) {
+    f32x16 acc;
+    scores(kb * 32, acc);
+    const int j = kb * 32 + col;
+    if (j >= L) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = (r & 3) + 8 * (r >> 2) + 4 * hl;
+      if (i0 + i >= L) continue;
+      out[(long)(i0 + i) * lda + j] = expf(acc[r] - fM[i]) * fInv[i];
+    }
+  }
+}
+
+void launch_attn_softmax(const AttnArgs& a, hipStream_t st) {
+  if (a.nseq <= 0 || a.max_len <= 0) return;
+  dim3 grid(cdiv(a.max_len, 32), a.nseq, a.H);
+  hipLaunchKernelGGL(attn_softmax_kernel, grid, dim3(256), 0, st, a);
+}
+
+}  // namespace zasr

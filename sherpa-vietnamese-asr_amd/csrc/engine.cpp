@@ -1,0 +1,1197 @@
+// libzasr host runtime: model upload, fbank / encoder / search drivers.
+//
+// Reference mapping:
+//   load + session setup    core/asr_engine.py:903-1020 (create_recognizer)
+//   fbank                   core/asr_engine.py:698-721
+//   encoder run             core/asr_engine.py:1045-1049 (Zipformer2 graph, icefall 3P)
+//   search loop             core/asr_engine.py:1051-1153
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <numeric>
+#include <sstream>
+
+#include "common.h"
+#include "gemm.h"
+#include "host_io.h"
+
+namespace zasr {
+
+// ------------------------------------------------------------------------------------
+// hotwords: Aho-Corasick graph restated from core/hotword_context.py:46-184, flattened
+// to a dense (state x trie-token) transition table of (next state, score delta)
+// ------------------------------------------------------------------------------------
+namespace {
+struct HwNode {
+  int tok = -1;
+  double tok_score = 0, node_score = 0, out_score = 0;
+  bool is_end = false;
+  std::vector<std::pair<int, int>> kids;  // (token, node) in insertion order
+  int fail = 0, out = -1;
+  int child(int t) const {
+    for (auto& k : kids)
+      if (k.first == t) return k.second;
+    return -1;
+  }
+};
+}  // namespace
+
+HotwordDFA build_hotword_dfa(const std::vector<std::vector<int>>& phrases,
+                             const std::vector<float>& scores, int V) {
+  HotwordDFA dfa;
+  if (phrases.empty()) return dfa;
+  std::vector<HwNode> nd(1);
+  for (size_t p = 0; p < phrases.size(); ++p) {
+    const auto& seq = phrases[p];
+    if (seq.empty()) continue;
+    double sc = (double)scores[p];
+    int cur = 0;
+    for (size_t j = 0; j < seq.size(); ++j) {
+      int t = seq[j];
+      ZASR_REQUIRE(t >= 0 && t < V, "hotword token id out of range");
+      bool last = (j + 1 == seq.size());
+      int c = nd[cur].child(t);
+      if (c < 0) {
+        HwNode n;
+        n.tok = t;
+        n.tok_score = sc;
+        n.node_score = nd[cur].node_score + sc;
+        n.out_score = last ? n.node_score : 0.0;
+        n.is_end = last;
+        nd.push_back(n);
+        c = (int)nd.size() - 1;
+        nd[cur].kids.push_back({t, c});
+      } else {
+        HwNode& e = nd[c];
+        e.tok_score = std::max(sc, e.tok_score);
+        e.node_score = nd[cur].node_score + e.tok_score;
+        if (last) e.is_end = true;
+        if (e.is_end) e.out_score = e.node_score;
+      }
+      cur = c;
+    }
+  }
+  // BFS fail / output links
+  std::deque<int> q;
+  for (auto& k : nd[0].kids) {
+    nd[k.second].fail = 0;
+    q.push_back(k.second);
+  }
+  while (!q.empty()) {
+    int cur = q.front();
+    q.pop_front();
+    for (auto& k : nd[cur].kids) {
+      int t = k.first, kid = k.second;
+      int f = nd[cur].fail;
+      int c = nd[f].child(t);
+      if (c >= 0) {
+        f = c;
+      } else {
+        f = nd[f].fail;
+        while (nd[f].child(t) < 0) {
+          f = nd[f].fail;
+          if (nd[f].tok == -1) break;
+        }
+        int c2 = nd[f].child(t);
+        if (c2 >= 0) f = c2;
+      }
+      nd[kid].fail = f;
+      int o = f;
+      while (!nd[o].is_end) {
+        o = nd[o].fail;
+        if (nd[o].tok == -1) {
+          o = -1;
+          break;
+        }
+      }
+      nd[kid].out = o;
+      if (o >= 0) nd[kid].out_score += nd[o].out_score;
+      q.push_back(kid);
+    }
+  }
+  // token classes
+  dfa.tok2cls.assign(V, -1);
+  std::vector<int> cls_tok;
+  for (size_t i = 1; i < nd.size(); ++i) {
+    int t = nd[i].tok;
+    if (dfa.tok2cls[t] < 0) {
+      dfa.tok2cls[t] = (int)cls_tok.size();
+      cls_tok.push_back(t);
+    }
+  }
+  dfa.num_states = (int)nd.size();
+  dfa.num_cls = (int)cls_tok.size();
+  dfa.next.resize((size_t)dfa.num_states * dfa.num_cls);
+  dfa.delta.resize((size_t)dfa.num_states * dfa.num_cls);
+  dfa.node_score.resize(dfa.num_states);
+  for (int s = 0; s < dfa.num_states; ++s) {
+    dfa.node_score[s] = nd[s].node_score;
+    for (int c = 0; c < dfa.num_cls; ++c) {
+      int t = cls_tok[c];
+      int n;
+      double score;
+      int d = nd[s].child(t);
+      if (d >= 0) {
+        n = d;
+        score = nd[n].tok_score;
+      } else {
+        n = nd[s].fail;
+        while (nd[n].child(t) < 0) {
+          n = nd[n].fail;
+          if (nd[n].tok == -1) break;
+        }
+        int c2 = nd[n].child(t);
+        if (c2 >= 0) n = c2;
+        score = nd[n].node_score - nd[s].node_score;
+      }
+      if (nd[n].out_score != 0) {
+        double matched = nd[n].is_end ? nd[n].node_score
+                                      : (nd[n].out >= 0 ? nd[nd[n].out].node_score
+                                                        : nd[n].node_score);
+        score = score + matched - nd[n].node_score;
+        n = 0;
+      }
+      dfa.next[(size_t)s * dfa.num_cls + c] = n;
+      dfa.delta[(size_t)s * dfa.num_cls + c] = score;
+    }
+  }
+  return dfa;
+}
+
+// ------------------------------------------------------------------------------------
+// model loading
+// ------------------------------------------------------------------------------------
+namespace {
+
+ModelConfig parse_config(const std::string& text) {
+  Json j = Json::parse(text);
+  ModelConfig c;
+  c.name = j.has("name") ? j.at("name").str : "zipformer";
+  c.dims = j.at("encoder_dims").as_int_vec();
+  c.layers = j.at("num_layers").as_int_vec();
+  c.ff = j.at("ff_dims").as_int_vec();
+  c.heads = j.at("num_heads").as_int_vec();
+  c.ds = j.at("downsampling").as_int_vec();
+  c.kernels = j.at("cnn_kernels").as_int_vec();
+  c.qd = (int)j.at("query_head_dim").num;
+  c.vd = (int)j.at("value_head_dim").num;
+  c.pd = (int)j.at("pos_head_dim").num;
+  c.pos_dim = (int)j.at("pos_dim").num;
+  c.V = (int)j.at("vocab_size").num;
+  c.dec_dim = (int)j.at("decoder_dim").num;
+  c.joiner_dim = (int)j.at("joiner_dim").num;
+  c.context = (int)j.at("context_size").num;
+  if (j.has("layer1_channels")) c.c1 = (int)j.at("layer1_channels").num;
+  if (j.has("layer2_channels")) c.c2 = (int)j.at("layer2_channels").num;
+  if (j.has("layer3_channels")) c.c3 = (int)j.at("layer3_channels").num;
+  ZASR_REQUIRE(c.qd == 32 && c.pd == 4, "kernels are specialised for query_head_dim 32, pos_head_dim 4");
+  ZASR_REQUIRE(c.c1 == 8 && c.c2 == 32 && c.c3 == 128, "Conv2dSubsampling channels must be 8/32/128");
+  ZASR_REQUIRE(c.context == 2, "decoder context_size must be 2");
+  ZASR_REQUIRE(c.dec_dim == c.joiner_dim, "decoder_dim must equal joiner_dim");
+  size_t ns = c.dims.size();
+  ZASR_REQUIRE(c.layers.size() == ns && c.ff.size() == ns && c.heads.size() == ns &&
+                   c.ds.size() == ns && c.kernels.size() == ns,
+               "inconsistent stack config");
+  for (size_t i = 0; i < ns; ++i) {
+    ZASR_REQUIRE(c.dims[i] % 16 == 0, "encoder dims must be multiples of 16");
+    ZASR_REQUIRE(c.ds[i] >= 1 && c.ds[i] <= 8, "downsampling factor must be 1..8");
+  }
+  return c;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// Engine
+// ------------------------------------------------------------------------------------
+template <class T>
+T* Engine::ws(const std::string& name, size_t count) {
+  size_t bytes = std::max<size_t>(count * sizeof(T), 256);
+  Buf& b = ws_[name];
+  if (b.bytes < bytes) {
+    if (b.p) {
+      ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+      ZASR_HIP_CHECK(hipFree(b.p));
+    }
+    size_t alloc = bytes + bytes / 8;
+    ZASR_HIP_CHECK(hipMalloc(&b.p, alloc));
+    b.bytes = alloc;
+  }
+  return reinterpret_cast<T*>(b.p);
+}
+
+void Engine::upload(void* dst, const void* src, size_t bytes) {
+  ZASR_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st_));
+  // pageable source: HIP stages the copy before returning, so `src` may be reused
+}
+
+Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const HotwordDFA& hw,
+               int precision)
+    : device_(device), beam_(beam), greedy_(greedy), precision_(precision), hw_host_(hw) {
+  ZASR_REQUIRE(precision == 0, "only the fp32 precision mode is built in this version");
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  st_ = stream_;
+  const std::string cfg_path = dir + "/config.json";
+  const std::string st_path = dir + "/model.safetensors";
+  if (!file_exists(cfg_path) || !file_exists(st_path))
+    throw std::invalid_argument("missing model files in " + dir);
+  ModelConfig cfg = parse_config(read_file(cfg_path));
+  model_.cfg = cfg;
+  SafeTensors W;
+  W.load(st_path);
+
+  auto dev = [&](const float* src, size_t n) -> float* {
+    float* p = nullptr;
+    ZASR_HIP_CHECK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(float)));
+    ZASR_HIP_CHECK(hipMemcpy(p, src, n * sizeof(float), hipMemcpyHostToDevice));
+    model_.allocations.push_back(p);
+    return p;
+  };
+  auto tensor = [&](const std::string& name, std::initializer_list<int64_t> shape) {
+    const HostTensor& t = W.get(name);
+    std::vector<int64_t> want(shape);
+    ZASR_REQUIRE(t.shape == want, "shape mismatch for " + name);
+    return t;
+  };
+  auto lin = [&](const std::string& pre, int N, int K, bool bias = true) {
+    DLin l;
+    l.N = N;
+    l.K = K;
+    l.w = dev(tensor(pre + ".weight", {N, K}).data, (size_t)N * K);
+    if (bias) l.b = dev(tensor(pre + ".bias", {N}).data, N);
+    return l;
+  };
+  auto vec = [&](const std::string& name, int n) { return dev(tensor(name, {n}).data, n); };
+  auto scalar = [&](const std::string& name) {
+    const HostTensor& t = W.get(name);
+    ZASR_REQUIRE(t.numel == 1, name + " must be a scalar");
+    return t.data[0];
+  };
+
+  // ---- Conv2dSubsampling ----
+  {
+    const HostTensor& w0 = tensor("encoder_embed.conv.0.weight", {8, 1, 3, 3});
+    model_.conv0_w = dev(w0.data, 72);
+    model_.conv0_b = vec("encoder_embed.conv.0.bias", 8);
+    // conv.4 [32][8][3][3] -> [o][(kt*3+kf)*8 + c]
+    const HostTensor& w4 = tensor("encoder_embed.conv.4.weight", {32, 8, 3, 3});
+    std::vector<float> p4(32 * 72);
+    for (int o = 0; o < 32; ++o)
+      for (int c = 0; c < 8; ++c)
+        for (int kk = 0; kk < 9; ++kk) p4[o * 72 + kk * 8 + c] = w4.data[(o * 8 + c) * 9 + kk];
+    model_.conv4 = DLin{dev(p4.data(), p4.size()), vec("encoder_embed.conv.4.bias", 32), 32, 72};
+    const HostTensor& w7 = tensor("encoder_embed.conv.7.weight", {128, 32, 3, 3});
+    std::vector<float> p7(128 * 288);
+    for (int o = 0; o < 128; ++o)
+      for (int c = 0; c < 32; ++c)
+        for (int kk = 0; kk < 9; ++kk) p7[o * 288 + kk * 32 + c] = w7.data[(o * 32 + c) * 9 + kk];
+    model_.conv7 = DLin{dev(p7.data(), p7.size()), vec("encoder_embed.conv.7.bias", 128), 128, 288};
+    model_.dw_w = dev(tensor("encoder_embed.convnext.depthwise_conv.weight", {128, 1, 7, 7}).data,
+                      128 * 49);
+    model_.dw_b = vec("encoder_embed.convnext.depthwise_conv.bias", 128);
+    model_.pw1 = DLin{dev(tensor("encoder_embed.convnext.pointwise_conv1.weight", {384, 128, 1, 1})
+                              .data, 384 * 128),
+                      vec("encoder_embed.convnext.pointwise_conv1.bias", 384), 384, 128};
+    model_.pw2 = DLin{dev(tensor("encoder_embed.convnext.pointwise_conv2.weight", {128, 384, 1, 1})
+                              .data, 128 * 384),
+                      vec("encoder_embed.convnext.pointwise_conv2.bias", 128), 128, 384};
+    // out: input index c*19 + f  ->  f*128 + c  (our [L][19][128] layout)
+    const int d0 = cfg.dims[0];
+    const HostTensor& wo = tensor("encoder_embed.out.weight", {d0, 128 * 19});
+    std::vector<float> po((size_t)d0 * 2432);
+    for (int n = 0; n < d0; ++n)
+      for (int c = 0; c < 128; ++c)
+        for (int f = 0; f < 19; ++f) po[(size_t)n * 2432 + f * 128 + c] = wo.data[(size_t)n * 2432 + c * 19 + f];
+    model_.out = DLin{dev(po.data(), po.size()), vec("encoder_embed.out.bias", d0), d0, 2432};
+    model_.out_norm_b = vec("encoder_embed.out_norm.bias", d0);
+    model_.out_norm_ls = scalar("encoder_embed.out_norm.log_scale");
+  }
+  // ---- stacks ----
+  const int qd = cfg.qd, vd = cfg.vd, pd = cfg.pd;
+  for (size_t i = 0; i < cfg.dims.size(); ++i) {
+    DStack s;
+    s.d = cfg.dims[i];
+    s.F = cfg.ff[i];
+    s.h = cfg.heads[i];
+    s.ds = cfg.ds[i];
+    s.K = cfg.kernels[i];
+    const int d = s.d, F = s.F, h = s.h;
+    std::string pre = "encoder.encoders." + std::to_string(i) + ".";
+    if (s.ds != 1) {
+      const HostTensor& b = tensor(pre + "downsample.bias", {s.ds});
+      double mx = -1e30, sum = 0;
+      for (int u = 0; u < s.ds; ++u) mx = std::max(mx, (double)b.data[u]);
+      std::vector<double> e(s.ds);
+      for (int u = 0; u < s.ds; ++u) sum += (e[u] = std::exp((double)b.data[u] - mx));
+      for (int u = 0; u < s.ds; ++u) s.ds_w[u] = (float)(e[u] / sum);
+      s.comb = vec(pre + "out_combiner.bypass_scale", d);
+      pre += "encoder.";
+    }
+    for (int j = 0; j < cfg.layers[i]; ++j) {
+      DLayer L;
+      std::string p = pre + "layers." + std::to_string(j) + ".";
+      L.bypass = vec(p + "bypass.bypass_scale", d);
+      L.bypass_mid = vec(p + "bypass_mid.bypass_scale", d);
+      L.attn_in = lin(p + "self_attn_weights.in_proj", (2 * qd + pd) * h, d);
+      const HostTensor& pw = tensor(p + "self_attn_weights.linear_pos.weight", {pd * h, cfg.pos_dim});
+      L.pos_w.assign(pw.data, pw.data + pw.numel);
+      for (int a = 0; a < 2; ++a) {
+        std::string n = p + "self_attn" + std::to_string(a + 1);
+        L.sa_in[a] = lin(n + ".in_proj", vd * h, d);
+        L.sa_out[a] = lin(n + ".out_proj", d, vd * h);
+      }
+      const int fdims[3] = {(F * 3) / 4, F, (F * 5) / 4};
+      for (int a = 0; a < 3; ++a) {
+        std::string n = p + "feed_forward" + std::to_string(a + 1);
+        L.ff_in[a] = lin(n + ".in_proj", fdims[a], d);
+        L.ff_out[a] = lin(n + ".out_proj", d, fdims[a]);
+      }
+      const int hid = 3 * d / 4;
+      L.na_in = lin(p + "nonlin_attention.in_proj", 3 * hid, d);
+      L.na_out = lin(p + "nonlin_attention.out_proj", d, hid);
+      for (int a = 0; a < 2; ++a) {
+        std::string n = p + "conv_module" + std::to_string(a + 1);
+        L.cv_in[a] = lin(n + ".in_proj", 2 * d, d);
+        L.cv_out[a] = lin(n + ".out_proj", d, d);
+        L.cv_dw_w[a] = dev(tensor(n + ".depthwise_conv.weight", {d, 1, s.K}).data, (size_t)d * s.K);
+        L.cv_dw_b[a] = vec(n + ".depthwise_conv.bias", d);
+      }
+      L.norm_b = vec(p + "norm.bias", d);
+      L.norm_ls = scalar(p + "norm.log_scale");
+      s.layers.push_back(std::move(L));
+    }
+    model_.stacks.push_back(std::move(s));
+  }
+  {
+    const HostTensor& b = tensor("encoder.downsample_output.bias", {2});
+    double mx = std::max(b.data[0], b.data[1]);
+    double e0 = std::exp(b.data[0] - mx), e1 = std::exp(b.data[1] - mx);
+    model_.out_ds_w[0] = (float)(e0 / (e0 + e1));
+    model_.out_ds_w[1] = (float)(e1 / (e0 + e1));
+  }
+  model_.enc_proj = lin("encoder_proj", cfg.joiner_dim, cfg.max_dim());
+  const int D = cfg.dec_dim;
+  model_.dec_emb = dev(tensor("decoder.embedding.weight", {cfg.V, D}).data, (size_t)cfg.V * D);
+  model_.dec_conv = dev(tensor("decoder.conv.weight", {D, 4, 2}).data, (size_t)D * 8);
+  model_.dec_proj = lin("decoder_proj", cfg.joiner_dim, D);
+  model_.joiner = lin("joiner.output_linear", cfg.V, cfg.joiner_dim);
+  ensure_pos_tables(2048);
+
+  // ---- fbank tables ----
+  {
+    std::vector<double> tw(512);
+    for (int j = 0; j < 256; ++j) {
+      double a = -2.0 * M_PI * j / 512.0;
+      tw[2 * j] = std::cos(a);
+      tw[2 * j + 1] = std::sin(a);
+    }
+    ZASR_HIP_CHECK(hipMalloc(&d_twiddle_, 512 * sizeof(double)));
+    ZASR_HIP_CHECK(hipMemcpy(d_twiddle_, tw.data(), 512 * sizeof(double), hipMemcpyHostToDevice));
+    std::vector<float> win(400);
+    for (int i = 0; i < 400; ++i)
+      win[i] = (float)std::pow(0.5 - 0.5 * std::cos(2.0 * M_PI / 399.0 * i), 0.85);
+    d_window_ = dev(win.data(), 400);
+    auto mel = [](float f) { return 1127.0f * logf(1.0f + f / 700.0f); };
+    const float mlo = mel(20.0f), mhi = mel(7600.0f);
+    const float delta = (mhi - mlo) / 81.0f;
+    std::vector<int> meta(240);
+    std::vector<float> wts;
+    for (int b = 0; b < 80; ++b) {
+      float left = mlo + (float)b * delta, center = mlo + (float)(b + 1) * delta,
+            right = mlo + (float)(b + 2) * delta;
+      int st = -1, en = -1;
+      std::vector<float> row(256, 0.f);
+      for (int i = 0; i < 256; ++i) {
+        float m = mel(31.25f * (float)i);
+        if (m > left && m < right) {
+          row[i] = (m <= center) ? (m - left) / (center - left) : (right - m) / (right - center);
+          if (st < 0) st = i;
+          en = i;
+        }
+      }
+      if (st < 0) st = en = 0;
+      meta[b] = st;
+      meta[80 + b] = en - st + 1;
+      meta[160 + b] = (int)wts.size();
+      for (int i = st; i <= en; ++i) wts.push_back(row[i]);
+    }
+    ZASR_HIP_CHECK(hipMalloc(&d_mel_meta_, 240 * sizeof(int)));
+    ZASR_HIP_CHECK(hipMemcpy(d_mel_meta_, meta.data(), 240 * sizeof(int), hipMemcpyHostToDevice));
+    d_mel_w_ = dev(wts.data(), wts.size());
+  }
+  // ---- hotwords ----
+  hw_.num_states = hw_host_.num_states;
+  hw_.num_cls = hw_host_.num_cls;
+  if (hw_host_.num_states > 0) {
+    int *t2c = nullptr, *nx = nullptr;
+    double *dl = nullptr, *ns = nullptr;
+    ZASR_HIP_CHECK(hipMalloc(&t2c, hw_host_.tok2cls.size() * sizeof(int)));
+    ZASR_HIP_CHECK(hipMalloc(&nx, std::max<size_t>(hw_host_.next.size(), 1) * sizeof(int)));
+    ZASR_HIP_CHECK(hipMalloc(&dl, std::max<size_t>(hw_host_.delta.size(), 1) * sizeof(double)));
+    ZASR_HIP_CHECK(hipMalloc(&ns, hw_host_.node_score.size() * sizeof(double)));
+    ZASR_HIP_CHECK(hipMemcpy(t2c, hw_host_.tok2cls.data(), hw_host_.tok2cls.size() * sizeof(int), hipMemcpyHostToDevice));
+    ZASR_HIP_CHECK(hipMemcpy(nx, hw_host_.next.data(), hw_host_.next.size() * sizeof(int), hipMemcpyHostToDevice));
+    ZASR_HIP_CHECK(hipMemcpy(dl, hw_host_.delta.data(), hw_host_.delta.size() * sizeof(double), hipMemcpyHostToDevice));
+    ZASR_HIP_CHECK(hipMemcpy(ns, hw_host_.node_score.data(), hw_host_.node_score.size() * sizeof(double), hipMemcpyHostToDevice));
+    model_.allocations.push_back(t2c);
+    model_.allocations.push_back(nx);
+    model_.allocations.push_back(dl);
+    model_.allocations.push_back(ns);
+    hw_.tok2cls = t2c;
+    hw_.next = nx;
+    hw_.delta = dl;
+    hw_.node_score = ns;
+  }
+  ZASR_HIP_CHECK(hipDeviceSynchronize());
+}
+
+Engine::~Engine() {
+  // best-effort teardown: errors here cannot be reported to the caller
+  (void)hipSetDevice(device_);
+  (void)hipStreamSynchronize(stream_);
+  for (void* p : model_.allocations) (void)hipFree(p);
+  for (auto& s : model_.stacks)
+    for (auto& l : s.layers)
+      if (l.pos_tab) (void)hipFree(l.pos_tab);
+  for (auto& kv : ws_)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  if (d_twiddle_) (void)hipFree(d_twiddle_);
+  if (d_mel_meta_) (void)hipFree(d_mel_meta_);
+  for (auto e : event_pool_) (void)hipEventDestroy(e);
+  for (auto& pe : prof_pending_) {
+    (void)hipEventDestroy(pe.a);
+    (void)hipEventDestroy(pe.b);
+  }
+  (void)hipStreamDestroy(stream_);
+}
+
+// CompactRelPositionalEncoding (icefall zipformer.py, 3P) folded through linear_pos:
+// table[x + pmax - 1][n] = sum_c W_pos[n][c] * pe(x)[c]
+void Engine::ensure_pos_tables(int need) {
+  if (need <= model_.pmax) return;
+  int pmax = 1024;
+  while (pmax < need) pmax *= 2;
+  const int P = model_.cfg.pos_dim;
+  const int rows = 2 * pmax - 1;
+  std::vector<double> pe((size_t)rows * P);
+  const double cl = std::sqrt((double)P);
+  const double ls = P / (2.0 * M_PI);
+  for (int r = 0; r < rows; ++r) {
+    double x = (double)(r - (pmax - 1));
+    double sgn = (x > 0) - (x < 0);
+    double xc = cl * sgn * (std::log(std::fabs(x) + cl) - std::log(cl));
+    double xa = std::atan(xc / ls);
+    for (int i = 0; i < P / 2; ++i) {
+      pe[(size_t)r * P + 2 * i] = std::cos(xa * (i + 1));
+      pe[(size_t)r * P + 2 * i + 1] = std::sin(xa * (i + 1));
+    }
+    pe[(size_t)r * P + P - 1] = 1.0;
+  }
+  for (auto& s : model_.stacks) {
+    const int n4 = 4 * s.h;
+    for (auto& l : s.layers) {
+      std::vector<float> tab((size_t)rows * n4);
+      for (int r = 0; r < rows; ++r)
+        for (int n = 0; n < n4; ++n) {
+          double acc = 0;
+          const double* pr = &pe[(size_t)r * P];
+          const float* wr = &l.pos_w[(size_t)n * P];
+          for (int c = 0; c < P; ++c) acc += (double)wr[c] * pr[c];
+          tab[(size_t)r * n4 + n] = (float)acc;
+        }
+      if (l.pos_tab) {
+        ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+        ZASR_HIP_CHECK(hipFree(l.pos_tab));
+      }
+      ZASR_HIP_CHECK(hipMalloc(&l.pos_tab, tab.size() * sizeof(float)));
+      ZASR_HIP_CHECK(hipMemcpy(l.pos_tab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+  }
+  model_.pmax = pmax;
+}
+
+// ------------------------------------------------------------------------------------
+// profiling
+// ------------------------------------------------------------------------------------
+hipEvent_t Engine::take_event() {
+  if (!event_pool_.empty()) {
+    hipEvent_t e = event_pool_.back();
+    event_pool_.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  ZASR_HIP_CHECK(hipEventCreate(&e));
+  return e;
+}
+
+void Engine::prof_begin(const char* name) {
+  if (!prof_on_) return;
+  ProfEvent pe{name, take_event(), take_event()};
+  ZASR_HIP_CHECK(hipEventRecord(pe.a, st_));
+  prof_pending_.push_back(pe);
+}
+
+void Engine::prof_end() {
+  if (!prof_on_ || prof_pending_.empty()) return;
+  ZASR_HIP_CHECK(hipEventRecord(prof_pending_.back().b, st_));
+}
+
+void Engine::profile_reset() {
+  prof_acc_.clear();
+  for (auto& pe : prof_pending_) {
+    event_pool_.push_back(pe.a);
+    event_pool_.push_back(pe.b);
+  }
+  prof_pending_.clear();
+}
+
+std::string Engine::profile_report() {
+  for (auto& pe : prof_pending_) {
+    ZASR_HIP_CHECK(hipEventSynchronize(pe.b));
+    float ms = 0.f;
+    ZASR_HIP_CHECK(hipEventElapsedTime(&ms, pe.a, pe.b));
+    auto& acc = prof_acc_[pe.name];
+    acc.first += 1;
+    acc.second += ms;
+    event_pool_.push_back(pe.a);
+    event_pool_.push_back(pe.b);
+  }
+  prof_pending_.clear();
+  std::ostringstream os;
+  for (auto& kv : prof_acc_) os << kv.first << " " << kv.second.first << " " << kv.second.second << "\n";
+  return os.str();
+}
+
+// ------------------------------------------------------------------------------------
+// building blocks
+// ------------------------------------------------------------------------------------
+void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi) {
+  GemmParams p{};
+  p.A = A;
+  p.lda = lda;
+  p.B = l.w;
+  p.sbk = 1;
+  p.sbn = l.K;
+  p.C = C;
+  p.ldc = ldc;
+  p.bias = l.b;
+  p.M = M;
+  p.N = l.N;
+  p.K = l.K;
+  p.alpha = 1.f;
+  p.max_M = M;
+  prof_begin("gemm");
+  gemm_f32(p, epi, ALOAD_DENSE, false, st_);
+  prof_end();
+}
+
+void Engine::run_fbank(const float* d_wav, const std::vector<long>& wav_off,
+                       const std::vector<long>& n, float* d_feats, std::vector<int>& frames) {
+  const int B = (int)n.size();
+  std::vector<long> off(B);
+  std::vector<int> ns(B), fo(B + 1, 0);
+  frames.resize(B);
+  for (int b = 0; b < B; ++b) {
+    off[b] = wav_off[b];
+    ns[b] = (int)n[b];
+    frames[b] = n[b] > 0 ? (int)((n[b] + 80) / 160) : 0;
+    fo[b + 1] = fo[b] + frames[b];
+  }
+  long* d_off = ws<long>("fb_wavoff", B);
+  int* d_meta = ws<int>("fb_meta", 2 * B + 1);
+  std::vector<int> meta(ns);
+  meta.insert(meta.end(), fo.begin(), fo.end());
+  upload(d_off, off.data(), B * sizeof(long));
+  upload(d_meta, meta.data(), meta.size() * sizeof(int));
+  FbankTables t{d_twiddle_, d_window_, d_mel_meta_, d_mel_meta_ + 80, d_mel_meta_ + 160, d_mel_w_};
+  prof_begin("fbank");
+  launch_fbank(d_wav, d_off, d_meta, d_meta + B, B, fo[B], t, d_feats, st_);
+  prof_end();
+}
+
+namespace {
+struct LevelMeta {
+  std::vector<int> len;  // per sequence
+  std::vector<int> off;  // B + 1
+  int total = 0, maxlen = 0;
+};
+LevelMeta make_level(const std::vector<int>& len) {
+  LevelMeta m;
+  m.len = len;
+  m.off.assign(len.size() + 1, 0);
+  for (size_t b = 0; b < len.size(); ++b) {
+    m.off[b + 1] = m.off[b] + len[b];
+    m.maxlen = std::max(m.maxlen, len[b]);
+  }
+  m.total = m.off.back();
+  return m;
+}
+struct MetaPack {
+  std::vector<char> bytes;
+  size_t add(const void* p, size_t n) {
+    size_t at = (bytes.size() + 15) & ~size_t(15);
+    bytes.resize(at + n);
+    if (n) std::memcpy(bytes.data() + at, p, n);
+    return at;
+  }
+};
+}  // namespace
+
+void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, const int* d_off,
+                           const std::vector<int>& lens, const long* d_aoff,
+                           const void* d_slices_attn, const void* d_slices_nl, int maxL) {
+  const int d = S.d, h = S.h, B = (int)lens.size();
+  const int hid = 3 * d / 4;
+  float* O = ws<float>("ly_orig", (size_t)R * d);
+  ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
+  // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
+  float* qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
+  linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
+  float* A = ws<float>("ly_attn", 1);  // sized by caller
+  {
+    AttnArgs a{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A};
+    prof_begin("attn_softmax");
+    launch_attn_softmax(a, st_);
+    prof_end();
+  }
+  auto ff = [&](int k) {
+    const DLin& fi = Ly.ff_in[k];
+    float* H = ws<float>("ly_hid", (size_t)R * fi.N);
+    linear(fi, X, d, R, H, fi.N, EPI_SWOOSHL);
+    linear(Ly.ff_out[k], H, fi.N, R, X, d, EPI_RESADD);
+  };
+  auto self_attn = [&](int k) {
+    float* vv = ws<float>("ly_vv", (size_t)R * 12 * h);
+    float* oa = ws<float>("ly_oa", (size_t)R * 12 * h);
+    linear(Ly.sa_in[k], X, d, R, vv, 12 * h, EPI_NONE);
+    GemmParams p{};
+    p.A = A;
+    p.B = vv;
+    p.sbk = 12 * h;
+    p.sbn = 1;
+    p.C = oa;
+    p.ldc = 12 * h;
+    p.N = 12;
+    p.alpha = 1.f;
+    p.slices = reinterpret_cast<const GemmSlice*>(d_slices_attn);
+    p.num_slices = B * h;
+    p.max_M = maxL;
+    prof_begin("attn_apply");
+    gemm_f32(p, EPI_NONE, ALOAD_DENSE, true, st_);
+    prof_end();
+    linear(Ly.sa_out[k], oa, 12 * h, R, X, d, EPI_RESADD);
+  };
+  auto conv = [&](int k) {
+    float* g2 = ws<float>("ly_g2", (size_t)R * 2 * d);
+    float* g = ws<float>("ly_g", (size_t)R * d);
+    float* dc = ws<float>("ly_dc", (size_t)R * d);
+    linear(Ly.cv_in[k], X, d, R, g2, 2 * d, EPI_NONE);
+    prof_begin("elementwise");
+    launch_glu(g2, g, R, d, st_);
+    prof_end();
+    prof_begin("dwconv1d");
+    launch_dwconv1d(g, d_off, B, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+    prof_end();
+    linear(Ly.cv_out[k], dc, d, R, X, d, EPI_RESADD);
+  };
+  // 1. feed_forward1
+  ff(0);
+  // 2. nonlin_attention (attention head 0 only)
+  {
+    float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
+    float* t1 = ws<float>("ly_t1", (size_t)R * hid);
+    float* z = ws<float>("ly_z", (size_t)R * hid);
+    linear(Ly.na_in, X, d, R, h3, 3 * hid, EPI_NONE);
+    prof_begin("elementwise");
+    launch_nonlin_prep(h3, t1, R, hid, st_);
+    prof_end();
+    GemmParams p{};
+    p.A = A;
+    p.B = t1;
+    p.sbk = hid;
+    p.sbn = 1;
+    p.C = z;
+    p.ldc = hid;
+    p.N = hid;
+    p.alpha = 1.f;
+    p.aux = h3 + 2 * hid;
+    p.ldaux = 3 * hid;
+    p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
+    p.num_slices = B;
+    p.max_M = maxL;
+    prof_begin("attn_apply");
+    gemm_f32(p, EPI_MULAUX, ALOAD_DENSE, true, st_);
+    prof_end();
+    linear(Ly.na_out, z, hid, R, X, d, EPI_RESADD);
+  }
+  // 3. self_attn1, conv_module1, feed_forward2
+  self_attn(0);
+  conv(0);
+  ff(1);
+  // 4. bypass_mid
+  prof_begin("elementwise");
+  launch_bypass(X, O, Ly.bypass_mid, R, d, st_);
+  prof_end();
+  // 5. self_attn2, conv_module2, feed_forward3
+  self_attn(1);
+  conv(1);
+  ff(2);
+  // 6. BiasNorm + bypass
+  prof_begin("elementwise");
+  launch_bias_norm(X, R, d, Ly.norm_b, Ly.norm_ls, O, Ly.bypass, st_);
+  prof_end();
+}
+
+void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float* d_enc,
+                         std::vector<int>& t_out) {
+  const ModelConfig& cfg = model_.cfg;
+  const int B = (int)T.size();
+  std::vector<int> t1(B), l2(B), L(B), tout(B);
+  for (int b = 0; b < B; ++b) {
+    ZASR_REQUIRE(T[b] >= 9, "encoder needs >= 9 fbank frames per chunk");
+    t1[b] = T[b] - 2;
+    l2[b] = (T[b] - 3) / 2;
+    L[b] = (T[b] - 7) / 2;
+    tout[b] = (L[b] + 1) / 2;
+  }
+  t_out = tout;
+  LevelMeta mfb = make_level(T), mc1 = make_level(t1), mc2 = make_level(l2), mL = make_level(L),
+            mout = make_level(tout);
+  const int ns = (int)model_.stacks.size();
+  std::vector<LevelMeta> mst(ns);
+  std::vector<std::vector<long>> aoff(ns);
+  std::vector<std::vector<GemmSlice>> sl_attn(ns), sl_nl(ns);
+  size_t attn_floats = 0;
+  int maxL_all = 0;
+  for (int i = 0; i < ns; ++i) {
+    const DStack& s = model_.stacks[i];
+    std::vector<int> len(B);
+    for (int b = 0; b < B; ++b) len[b] = (L[b] + s.ds - 1) / s.ds;
+    mst[i] = make_level(len);
+    maxL_all = std::max(maxL_all, mst[i].maxlen);
+    long acc = 0;
+    const int hid = 3 * s.d / 4;
+    for (int b = 0; b < B; ++b) {
+      const int Lb = len[b], L4 = (Lb + 3) & ~3;
+      aoff[i].push_back(acc);
+      for (int hh = 0; hh < s.h; ++hh) {
+        GemmSlice g{};
+        g.a_off = acc + (long)hh * Lb * L4;
+        g.b_off = (long)mst[i].off[b] * 12 * s.h + 12 * hh;
+        g.c_off = g.b_off;
+        g.M = Lb;
+        g.K = Lb;
+        g.lda = L4;
+        sl_attn[i].push_back(g);
+      }
+      GemmSlice g{};
+      g.a_off = acc;
+      g.b_off = (long)mst[i].off[b] * hid;
+      g.c_off = g.b_off;
+      g.aux_off = (long)mst[i].off[b] * 3 * hid;
+      g.M = Lb;
+      g.K = Lb;
+      g.lda = L4;
+      sl_nl[i].push_back(g);
+      acc += (long)s.h * Lb * L4;
+    }
+    attn_floats = std::max(attn_floats, (size_t)acc);
+  }
+  ensure_pos_tables(maxL_all + 64);
+  // frontend conv slices
+  std::vector<GemmSlice> sl_c2(B), sl_c3(B);
+  for (int b = 0; b < B; ++b) {
+    sl_c2[b] = GemmSlice{(long)mc1.off[b] * 640, 0, (long)mc2.off[b] * 39 * 32, 0, l2[b] * 39, 72, 0, 0};
+    sl_c3[b] = GemmSlice{(long)mc2.off[b] * 39 * 32, 0, (long)mL.off[b] * 19 * 128, 0, L[b] * 19, 288, 0, 0};
+  }
+  // one metadata upload
+  MetaPack mp;
+  size_t o_fb = mp.add(mfb.off.data(), (B + 1) * 4), o_c1 = mp.add(mc1.off.data(), (B + 1) * 4),
+         o_L = mp.add(mL.off.data(), (B + 1) * 4), o_out = mp.add(mout.off.data(), (B + 1) * 4);
+  size_t o_c2s = mp.add(sl_c2.data(), B * sizeof(GemmSlice)),
+         o_c3s = mp.add(sl_c3.data(), B * sizeof(GemmSlice));
+  std::vector<size_t> o_st(ns), o_ao(ns), o_sa(ns), o_sn(ns);
+  for (int i = 0; i < ns; ++i) {
+    o_st[i] = mp.add(mst[i].off.data(), (B + 1) * 4);
+    o_ao[i] = mp.add(aoff[i].data(), B * sizeof(long));
+    o_sa[i] = mp.add(sl_attn[i].data(), sl_attn[i].size() * sizeof(GemmSlice));
+    o_sn[i] = mp.add(sl_nl[i].data(), sl_nl[i].size() * sizeof(GemmSlice));
+  }
+  char* d_meta = ws<char>("enc_meta", mp.bytes.size());
+  upload(d_meta, mp.bytes.data(), mp.bytes.size());
+  auto I = [&](size_t o) { return reinterpret_cast<const int*>(d_meta + o); };
+
+  // ---------------- Conv2dSubsampling ----------------
+  float* c1 = ws<float>("fe_c1", (size_t)mc1.total * 640);
+  prof_begin("frontend_conv");
+  launch_conv1(d_feats, I(o_fb), I(o_c1), B, mc1.total, model_.conv0_w, model_.conv0_b, c1, st_);
+  prof_end();
+  float* c2 = ws<float>("fe_c2", (size_t)mc2.total * 39 * 32);
+  {
+    GemmParams p{};
+    p.A = c1;
+    p.B = model_.conv4.w;
+    p.sbk = 1;
+    p.sbn = 72;
+    p.C = c2;
+    p.ldc = 32;
+    p.bias = model_.conv4.b;
+    p.N = 32;
+    p.alpha = 1.f;
+    p.slices = reinterpret_cast<const GemmSlice*>(d_meta + o_c2s);
+    p.num_slices = B;
+    p.max_M = mc2.maxlen * 39;
+    prof_begin("frontend_conv");
+    gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV2, false, st_);
+    prof_end();
+  }
+  float* x3 = ws<float>("fe_x3", (size_t)mL.total * 19 * 128);
+  {
+    GemmParams p{};
+    p.A = c2;
+    p.B = model_.conv7.w;
+    p.sbk = 1;
+    p.sbn = 288;
+    p.C = x3;
+    p.ldc = 128;
+    p.bias = model_.conv7.b;
+    p.N = 128;
+    p.alpha = 1.f;
+    p.slices = reinterpret_cast<const GemmSlice*>(d_meta + o_c3s);
+    p.num_slices = B;
+    p.max_M = mL.maxlen * 19;
+    prof_begin("frontend_conv");
+    gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
+    prof_end();
+  }
+  float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
+  prof_begin("frontend_conv");
+  launch_dwconv2d(x3, I(o_L), B, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+  prof_end();
+  float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
+  linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
+  linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
+  const int d0 = cfg.dims[0];
+  float* e0 = ws<float>("fe_e0", (size_t)mL.total * d0);
+  linear(model_.out, x3, 2432, mL.total, e0, d0, EPI_NONE);
+  prof_begin("elementwise");
+  launch_bias_norm(e0, mL.total, d0, model_.out_norm_b, model_.out_norm_ls, nullptr, nullptr, st_);
+  prof_end();
+
+  // ---------------- encoder stacks ----------------
+  ws<float>("ly_attn", std::max<size_t>(attn_floats, 1));
+  const int Dm = cfg.max_dim();
+  float* full = ws<float>("st_full", (size_t)mL.total * Dm);
+  float* prev = e0;
+  int prev_w = d0;
+  std::vector<float*> outs(ns);
+  for (int i = 0; i < ns; ++i) {
+    const DStack& s = model_.stacks[i];
+    const int d = s.d;
+    float* orig = ws<float>("st_orig" + std::to_string(i % 2), (size_t)mL.total * d);
+    prof_begin("elementwise");
+    launch_copy_cols(prev, prev_w, 0, orig, d, 0, std::min(prev_w, d), mL.total, true, d, st_);
+    prof_end();
+    float* X;
+    if (s.ds == 1) {
+      X = orig;
+    } else {
+      X = ws<float>("st_x", (size_t)mst[i].total * d);
+      prof_begin("elementwise");
+      launch_downsample(orig, I(o_L), I(o_st[i]), B, mst[i].total, d, s.ds, s.ds_w, X, st_);
+      prof_end();
+    }
+    for (const DLayer& ly : s.layers)
+      layer_forward(s, ly, X, mst[i].total, I(o_st[i]), mst[i].len,
+                    reinterpret_cast<const long*>(d_meta + o_ao[i]), d_meta + o_sa[i],
+                    d_meta + o_sn[i], mst[i].maxlen);
+    float* out = orig;
+    if (s.ds != 1) {
+      out = ws<float>("st_out" + std::to_string(i % 2), (size_t)mL.total * d);
+      prof_begin("elementwise");
+      launch_upsample_combine(X, orig, I(o_L), I(o_st[i]), B, mL.total, d, s.ds, s.comb, out, st_);
+      prof_end();
+    }
+    outs[i] = out;
+    prev = out;
+    prev_w = d;
+    // full-dim output: channel range [d_next_max, d) comes from the latest stack that has it
+    int later_max = 0;
+    for (int j = i + 1; j < ns; ++j) later_max = std::max(later_max, model_.stacks[j].d);
+    if (d > later_max) {
+      prof_begin("elementwise");
+      launch_copy_cols(out, d, later_max, full, Dm, later_max, d - later_max, mL.total, false, 0, st_);
+      prof_end();
+    }
+    // `prev` stays valid: stack i+1 only touches the buffers of the other parity
+  }
+  // ---------------- output downsample + encoder_proj ----------------
+  float* fo = ws<float>("enc_ds", (size_t)mout.total * Dm);
+  prof_begin("elementwise");
+  launch_downsample(full, I(o_L), I(o_out), B, mout.total, Dm, 2, model_.out_ds_w, fo, st_);
+  prof_end();
+  linear(model_.enc_proj, fo, Dm, mout.total, d_enc, cfg.joiner_dim, EPI_NONE);
+}
+
+std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vector<int>& t_out,
+                                            int beam) {
+  const ModelConfig& cfg = model_.cfg;
+  const int S_all = (int)t_out.size();
+  std::vector<TokenResult> res(S_all);
+  for (int s = 0; s < S_all; ++s) res[s].t_out = t_out[s];
+  // streams with T' >= 1, sorted by T' descending so active streams form a prefix
+  std::vector<int> order;
+  std::vector<int> enc_off_all(S_all + 1, 0);
+  for (int s = 0; s < S_all; ++s) enc_off_all[s + 1] = enc_off_all[s] + t_out[s];
+  for (int s = 0; s < S_all; ++s)
+    if (t_out[s] > 0) order.push_back(s);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t_out[a] > t_out[b]; });
+  const int S = (int)order.size();
+  if (S == 0) return res;
+  const int H = beam;
+  const int Tmax = t_out[order[0]];
+  const int V = cfg.V, D = cfg.joiner_dim;
+  std::vector<int> eo(S), el(S);
+  for (int i = 0; i < S; ++i) {
+    eo[i] = enc_off_all[order[i]];
+    el[i] = t_out[order[i]];
+  }
+  int* d_eo = ws<int>("se_eo", S);
+  int* d_el = ws<int>("se_el", S);
+  upload(d_eo, eo.data(), S * sizeof(int));
+  upload(d_el, el.data(), S * sizeof(int));
+  const size_t slots = (size_t)S * H;
+  SearchState st{};
+  st.lp = ws<double>("se_lp", slots);
+  st.lpf = ws<int>("se_lpf", slots);
+  st.hash = ws<unsigned long long>("se_hash", slots);
+  st.len = ws<int>("se_len", slots);
+  st.y1 = ws<int>("se_y1", slots);
+  st.y2 = ws<int>("se_y2", slots);
+  st.hw = ws<int>("se_hw", slots);
+  st.node = ws<int>("se_node", slots);
+  st.nh = ws<int>("se_nh", S);
+  st.node_cap = H * Tmax + 1;
+  const size_t ncap = (size_t)S * st.node_cap;
+  st.node_tok = ws<int>("se_ntok", ncap);
+  st.node_frame = ws<int>("se_nfr", ncap);
+  st.node_parent = ws<int>("se_npar", ncap);
+  st.node_lp = ws<double>("se_nlp", ncap);
+  st.node_stats = ws<float4>("se_nst", ncap);
+  st.node_count = ws<int>("se_ncnt", S);
+  float* dec_in = ws<float>("se_decin", slots * D);
+  float* dec_out = ws<float>("se_decout", slots * D);
+  float* logits = ws<float>("se_logits", slots * V);
+  prof_begin("search");
+  launch_search_init(st, S, H, st_);
+  prof_end();
+  int active = S;
+  for (int t = 0; t < Tmax; ++t) {
+    while (active > 0 && el[active - 1] <= t) --active;
+    const int rows = active * H;
+    prof_begin("decoder");
+    launch_decoder_prep(st, rows, model_.dec_emb, model_.dec_conv, D, dec_in, st_);
+    prof_end();
+    linear(model_.dec_proj, dec_in, D, rows, dec_out, D, EPI_NONE);
+    GemmParams p{};
+    p.lda = D;
+    p.B = model_.joiner.w;
+    p.sbk = 1;
+    p.sbn = D;
+    p.C = logits;
+    p.ldc = V;
+    p.bias = model_.joiner.b;
+    p.M = rows;
+    p.N = V;
+    p.K = D;
+    p.alpha = 1.f;
+    p.max_M = rows;
+    p.joiner = JoinerALoad{d_enc, dec_out, d_eo, d_el, H, t};
+    prof_begin("joiner");
+    gemm_f32(p, EPI_NONE, ALOAD_JOINER, false, st_);
+    prof_end();
+    prof_begin("search");
+    launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, st_);
+    prof_end();
+  }
+  const int cap = Tmax;
+  int* o_tok = ws<int>("so_tok", (size_t)S * cap);
+  int* o_fr = ws<int>("so_fr", (size_t)S * cap);
+  double* o_lp = ws<double>("so_lp", (size_t)S * cap);
+  float4* o_st = ws<float4>("so_st", (size_t)S * cap);
+  int* o_cnt = ws<int>("so_cnt", S);
+  prof_begin("search");
+  launch_search_final(st, S, H, hw_, cap, o_tok, o_fr, o_lp, o_st, o_cnt, st_);
+  prof_end();
+  std::vector<int> h_tok((size_t)S * cap), h_fr((size_t)S * cap), h_cnt(S);
+  std::vector<double> h_lp((size_t)S * cap);
+  std::vector<float> h_st((size_t)S * cap * 4);
+  ZASR_HIP_CHECK(hipMemcpyAsync(h_cnt.data(), o_cnt, S * sizeof(int), hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h_tok.data(), o_tok, h_tok.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h_fr.data(), o_fr, h_fr.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h_lp.data(), o_lp, h_lp.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h_st.data(), o_st, h_st.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+  for (int i = 0; i < S; ++i) {
+    TokenResult& r = res[order[i]];
+    const int c = h_cnt[i];
+    r.tok.assign(h_tok.begin() + (size_t)i * cap, h_tok.begin() + (size_t)i * cap + c);
+    r.frame.assign(h_fr.begin() + (size_t)i * cap, h_fr.begin() + (size_t)i * cap + c);
+    r.lp.assign(h_lp.begin() + (size_t)i * cap, h_lp.begin() + (size_t)i * cap + c);
+    r.stats.assign(h_st.begin() + (size_t)i * cap * 4, h_st.begin() + ((size_t)i * cap + c) * 4);
+  }
+  return res;
+}
+
+// ------------------------------------------------------------------------------------
+// public entry points
+// ------------------------------------------------------------------------------------
+std::vector<TokenResult> Engine::decode_device(const float* d_wav, const std::vector<long>& wav_off,
+                                               const std::vector<long>& n, int beam,
+                                               hipStream_t st) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  st_ = st ? st : stream_;
+  const int B = (int)n.size();
+  std::vector<int> frames;
+  long total_frames = 0;
+  for (int b = 0; b < B; ++b) total_frames += n[b] > 0 ? (n[b] + 80) / 160 : 0;
+  float* feats = ws<float>("feats", (size_t)std::max<long>(total_frames, 1) * 80);
+  run_fbank(d_wav, wav_off, n, feats, frames);
+  // chunks too short for the encoder produce empty results (T' = 0)
+  std::vector<int> valid, T;
+  std::vector<long> foff(B + 1, 0);
+  for (int b = 0; b < B; ++b) foff[b + 1] = foff[b] + frames[b];
+  bool all_valid = true;
+  for (int b = 0; b < B; ++b) {
+    if (frames[b] >= 9) {
+      valid.push_back(b);
+      T.push_back(frames[b]);
+    } else {
+      all_valid = false;
+    }
+  }
+  std::vector<TokenResult> out(B);
+  if (valid.empty()) {
+    st_ = stream_;
+    return out;
+  }
+  const float* fptr = feats;
+  if (!all_valid) {  // compact valid chunks' features
+    float* cf = ws<float>("feats_compact", (size_t)total_frames * 80);
+    long pos = 0;
+    for (int b : valid) {
+      ZASR_HIP_CHECK(hipMemcpyAsync(cf + pos * 80, feats + foff[b] * 80, (size_t)frames[b] * 80 * 4,
+                                    hipMemcpyDeviceToDevice, st_));
+      pos += frames[b];
+    }
+    fptr = cf;
+  }
+  long tot_out = 0;
+  for (int t : T) tot_out += ((t - 7) / 2 + 1) / 2;
+  float* enc = ws<float>("enc_out", (size_t)std::max<long>(tot_out, 1) * model_.cfg.joiner_dim);
+  std::vector<int> t_out;
+  run_encoder(fptr, T, enc, t_out);
+  std::vector<TokenResult> r = run_search(enc, t_out, beam);
+  for (size_t i = 0; i < valid.size(); ++i) out[valid[i]] = std::move(r[i]);
+  st_ = stream_;
+  return out;
+}
+
+std::vector<TokenResult> Engine::decode_features(const std::vector<const float*>& feats,
+                                                 const std::vector<long>& frames, int beam) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  st_ = stream_;
+  const int B = (int)feats.size();
+  std::vector<int> valid, T;
+  long tot = 0, tot_out = 0;
+  for (int b = 0; b < B; ++b)
+    if (frames[b] >= 9) {
+      valid.push_back(b);
+      T.push_back((int)frames[b]);
+      tot += frames[b];
+      tot_out += ((frames[b] - 7) / 2 + 1) / 2;
+    }
+  std::vector<TokenResult> out(B);
+  if (valid.empty()) return out;
+  float* d = ws<float>("feats", (size_t)tot * 80);
+  long pos = 0;
+  for (int b : valid) {
+    ZASR_HIP_CHECK(hipMemcpyAsync(d + pos * 80, feats[b], (size_t)frames[b] * 80 * 4,
+                                  hipMemcpyHostToDevice, st_));
+    pos += frames[b];
+  }
+  float* enc = ws<float>("enc_out", (size_t)tot_out * model_.cfg.joiner_dim);
+  std::vector<int> t_out;
+  run_encoder(d, T, enc, t_out);
+  std::vector<TokenResult> r = run_search(enc, t_out, beam);
+  for (size_t i = 0; i < valid.size(); ++i) out[valid[i]] = std::move(r[i]);
+  return out;
+}
+
+void Engine::fbank_host(const float* wav, long n, float* out) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  st_ = stream_;
+  const long frames = n > 0 ? (n + 80) / 160 : 0;
+  if (frames == 0) return;
+  float* dw = ws<float>("fbh_wav", n);
+  float* df = ws<float>("fbh_out", (size_t)frames * 80);
+  ZASR_HIP_CHECK(hipMemcpyAsync(dw, wav, n * 4, hipMemcpyHostToDevice, st_));
+  std::vector<int> fr;
+  run_fbank(dw, {0}, {n}, df, fr);
+  ZASR_HIP_CHECK(hipMemcpyAsync(out, df, (size_t)frames * 80 * 4, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+void Engine::encode_host(const std::vector<const float*>& feats, const std::vector<long>& frames,
+                         std::vector<float>& out, std::vector<int>& t_out) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  st_ = stream_;
+  const int B = (int)feats.size();
+  std::vector<int> T(B);
+  long tot = 0, tot_out = 0;
+  for (int b = 0; b < B; ++b) {
+    ZASR_REQUIRE(frames[b] >= 9, "encoder needs >= 9 fbank frames per chunk");
+    T[b] = (int)frames[b];
+    tot += frames[b];
+    tot_out += ((frames[b] - 7) / 2 + 1) / 2;
+  }
+  float* d = ws<float>("feats", (size_t)tot * 80);
+  long pos = 0;
+  for (int b = 0; b < B; ++b) {
+    ZASR_HIP_CHECK(hipMemcpyAsync(d + pos * 80, feats[b], (size_t)frames[b] * 80 * 4,
+                                  hipMemcpyHostToDevice, st_));
+    pos += frames[b];
+  }
+  float* enc = ws<float>("enc_out", (size_t)tot_out * model_.cfg.joiner_dim);
+  run_encoder(d, T, enc, t_out);
+  out.resize((size_t)tot_out * model_.cfg.joiner_dim);
+  ZASR_HIP_CHECK(hipMemcpyAsync(out.data(), enc, out.size() * 4, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+std::vector<TokenResult> Engine::search_host(const std::vector<const float*>& enc,
+                                             const std::vector<long>& t_out, int beam) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  st_ = stream_;
+  const int B = (int)enc.size();
+  const int D = model_.cfg.joiner_dim;
+  long tot = 0;
+  for (long t : t_out) tot += t;
+  float* d = ws<float>("enc_in", (size_t)std::max<long>(tot, 1) * D);
+  long pos = 0;
+  std::vector<int> to(B);
+  for (int b = 0; b < B; ++b) {
+    to[b] = (int)t_out[b];
+    if (t_out[b] > 0)
+      ZASR_HIP_CHECK(hipMemcpyAsync(d + pos * D, enc[b], (size_t)t_out[b] * D * 4,
+                                    hipMemcpyHostToDevice, st_));
+    pos += t_out[b];
+  }
+  return run_search(d, to, beam);
+}
+
+}  // namespace zasr

@@ -1,0 +1,164 @@
+// Host runtime of libzasr: device-resident model, per-batch workspace, and the encoder /
+// search drivers that sequence the HIP kernels on one stream.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace zasr {
+
+struct ModelConfig {
+  std::string name;
+  std::vector<int> dims, layers, ff, heads, ds, kernels;
+  int qd = 32, vd = 12, pd = 4, pos_dim = 48;
+  int V = 0, dec_dim = 0, joiner_dim = 0, context = 2;
+  int c1 = 8, c2 = 32, c3 = 128;
+  int max_dim() const {
+    int m = 0;
+    for (int d : dims) m = d > m ? d : m;
+    return m;
+  }
+};
+
+struct DLin {
+  float* w = nullptr;  // [N][K]
+  float* b = nullptr;  // [N] or null
+  int N = 0, K = 0;
+};
+
+struct DLayer {
+  DLin attn_in, sa_in[2], sa_out[2], ff_in[3], ff_out[3], na_in, na_out, cv_in[2], cv_out[2];
+  float* cv_dw_w[2] = {nullptr, nullptr};
+  float* cv_dw_b[2] = {nullptr, nullptr};
+  float* bypass = nullptr;
+  float* bypass_mid = nullptr;
+  float* norm_b = nullptr;
+  float norm_ls = 0.f;
+  std::vector<float> pos_w;  // linear_pos weight [4h][pos_dim] (host, to rebuild tables)
+  float* pos_tab = nullptr;  // [(2*pmax-1)][4h]
+};
+
+struct DStack {
+  int d = 0, F = 0, h = 0, ds = 1, K = 0;
+  float ds_w[8] = {0};
+  float* comb = nullptr;  // out_combiner bypass scale
+  std::vector<DLayer> layers;
+};
+
+struct DModel {
+  ModelConfig cfg;
+  float *conv0_w = nullptr, *conv0_b = nullptr;
+  DLin conv4, conv7, pw1, pw2, out, enc_proj, dec_proj, joiner;
+  float *dw_w = nullptr, *dw_b = nullptr;
+  float* out_norm_b = nullptr;
+  float out_norm_ls = 0.f;
+  std::vector<DStack> stacks;
+  float out_ds_w[2] = {0, 0};
+  float* dec_emb = nullptr;   // [V][D]
+  float* dec_conv = nullptr;  // [D][4][2]
+  int pmax = 0;
+  std::vector<void*> allocations;
+};
+
+struct HotwordDFA {
+  int num_states = 0, num_cls = 0;
+  std::vector<int> tok2cls, next;
+  std::vector<double> delta, node_score;
+};
+HotwordDFA build_hotword_dfa(const std::vector<std::vector<int>>& phrases,
+                             const std::vector<float>& scores, int V);
+
+struct TokenResult {
+  std::vector<int> tok, frame;
+  std::vector<double> lp;
+  std::vector<float> stats;  // 4 per token
+  int t_out = 0;
+};
+
+class Engine {
+ public:
+  Engine(const std::string& model_dir, int device, int beam, bool greedy,
+         const HotwordDFA& hw, int precision);
+  ~Engine();
+
+  int vocab() const { return model_.cfg.V; }
+  int joiner_dim() const { return model_.cfg.joiner_dim; }
+  int default_beam() const { return beam_; }
+  hipStream_t stream() const { return stream_; }
+
+  // full path from device waveforms (packed); results in chunk order
+  std::vector<TokenResult> decode_device(const float* d_wav, const std::vector<long>& wav_off,
+                                         const std::vector<long>& n, int beam, hipStream_t st);
+  std::vector<TokenResult> decode_features(const std::vector<const float*>& feats,
+                                           const std::vector<long>& frames, int beam);
+  void fbank_host(const float* wav, long n, float* out);
+  void encode_host(const std::vector<const float*>& feats, const std::vector<long>& frames,
+                   std::vector<float>& out, std::vector<int>& t_out);
+  std::vector<TokenResult> search_host(const std::vector<const float*>& enc,
+                                       const std::vector<long>& t_out, int beam);
+
+  // profiling
+  void profile_enable(bool on) { prof_on_ = on; }
+  void profile_reset();
+  std::string profile_report();
+
+  std::mutex mu;
+
+ private:
+  struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  template <class T>
+  T* ws(const std::string& name, size_t count);
+  void upload(void* dst, const void* src, size_t bytes);
+
+  // pipeline stages (all on st_)
+  void run_fbank(const float* d_wav, const std::vector<long>& wav_off, const std::vector<long>& n,
+                 float* d_feats, std::vector<int>& frames);
+  void run_encoder(const float* d_feats, const std::vector<int>& T, float* d_enc,
+                   std::vector<int>& t_out);
+  std::vector<TokenResult> run_search(const float* d_enc, const std::vector<int>& t_out, int beam);
+  void layer_forward(const DStack& stk, const DLayer& ly, float* X, int R, const int* d_off,
+                     const std::vector<int>& lens, const long* d_aoff, const void* d_slices_attn,
+                     const void* d_slices_nl, int maxL);
+  void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi);
+  void ensure_pos_tables(int max_len);
+
+  // timing
+  struct ProfEvent {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  void prof_begin(const char* name);
+  void prof_end();
+  bool prof_on_ = false;
+  std::vector<ProfEvent> prof_pending_;
+  std::map<std::string, std::pair<long, double>> prof_acc_;
+  std::vector<hipEvent_t> event_pool_;
+  hipEvent_t take_event();
+
+  DModel model_;
+  int device_ = 0;
+  int beam_ = 8;
+  [[maybe_unused]] bool greedy_ = false;
+  [[maybe_unused]] int precision_ = 0;
+  hipStream_t stream_ = nullptr;
+  hipStream_t st_ = nullptr;  // stream of the current call
+  std::map<std::string, Buf> ws_;
+  // fbank tables
+  double* d_twiddle_ = nullptr;
+  float* d_window_ = nullptr;
+  int* d_mel_meta_ = nullptr;  // start[80], len[80], woff[80]
+  float* d_mel_w_ = nullptr;
+  // hotword tables
+  HotwordDFA hw_host_;
+  HotwordTables hw_{};
+};
+
+}  // namespace zasr

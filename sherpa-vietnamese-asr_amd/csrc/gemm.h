@@ -1,0 +1,74 @@
+// Dense projection GEMMs of the Zipformer transducer on CDNA4 MFMA.
+//
+//   C[m, n] = epi( alpha * sum_k A'[m, k] * B[k, n] + bias[n] )
+//
+// A' is produced by an A-loader (plain row-major activations, the joiner's
+// tanh(enc + dec) prologue, or implicit im2col for the Conv2dSubsampling convs), B is a
+// weight matrix [N][K] (K contiguous, the nn.Linear layout) or an activation matrix [K][N]
+// (N contiguous: the attention values).  Batched launches carry one descriptor per
+// z-slice (a sequence, or a (sequence, head) pair) so ragged sequences never pad.
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace zasr {
+
+enum GemmEpi : int {
+  EPI_NONE = 0,     // C = v
+  EPI_SWOOSHL = 1,  // C = SwooshL(v)
+  EPI_SWOOSHR = 2,  // C = SwooshR(v)
+  EPI_RESADD = 3,   // C += v          (residual: src = src + module(src))
+  EPI_MULAUX = 4,   // C = v * aux[m, n]
+};
+
+enum GemmALoad : int {
+  ALOAD_DENSE = 0,   // A[m * lda + k]
+  ALOAD_JOINER = 1,  // tanh(enc[row(m)] + dec[m])     (joiner.output_linear input)
+  ALOAD_CONV2 = 2,   // im2col of conv1 output [T1][80][8]   -> conv.4 (3x3, stride 2)
+  ALOAD_CONV3 = 3,   // im2col of conv2 output [L2][39][32]  -> conv.7 (3x3, stride (1,2))
+};
+
+// Per z-slice descriptor (device array).  Offsets are in elements.
+struct GemmSlice {
+  long a_off;
+  long b_off;
+  long c_off;
+  long aux_off;
+  int M;
+  int K;
+  int lda;
+  int pad_;
+};
+
+struct JoinerALoad {
+  const float* enc;      // [sum T', D]
+  const float* dec;      // [S*H, D]
+  const int* enc_off;    // [S] first encoder row of stream s
+  const int* enc_len;    // [S] T'_s
+  int H;                 // hyp slots per stream
+  int t;                 // current frame
+};
+
+struct GemmParams {
+  const float* A;
+  int lda;
+  const float* B;
+  long sbk, sbn;         // B element (k, n) = B[k * sbk + n * sbn]
+  float* C;
+  int ldc;
+  const float* bias;     // [N] or nullptr
+  const float* aux;      // EPI_MULAUX operand
+  int ldaux;
+  int M, N, K;
+  float alpha;
+  const GemmSlice* slices;  // nullptr => single problem with the fields above
+  int num_slices;
+  int max_M;                // max M over slices (grid sizing)
+  JoinerALoad joiner;
+};
+
+// Launch; picks a tile shape from (max_M, N).  B_ncontig selects the [K][N] B layout.
+void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream_t stream);
+
+}  // namespace zasr

@@ -1,0 +1,299 @@
+// f32-in / f32-accumulate MFMA GEMM (v_mfma_f32_32x32x2_f32: exact f32 fma chains, the
+// "fp32" precision mode) for every dense projection on the Zipformer path.
+//
+// Structure: 64*WAVES threads per block, BM x BN block tile, BK = 16 K-slab staged through
+// LDS (k-major images As[k][m], Bs[k][n] so that an MFMA operand read is 32 consecutive
+// floats per lane half: conflict-free ds_read_b32), double-buffered with one barrier per
+// K-slab, next slab's global loads (float4 per lane) in flight under the MFMAs.
+// Each wave owns a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA tiles.
+#include "common.h"
+#include "gemm.h"
+
+namespace zasr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int BK = 16;
+
+template <int ALOAD>
+__device__ __forceinline__ float4 load_a4(const GemmParams& p, const float* A, int M, int K,
+                                          int lda, int gm, int gk) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (gm >= M || gk >= K) return v;
+  if constexpr (ALOAD == ALOAD_DENSE) {
+    const float* ptr = A + (long)gm * lda + gk;
+    if (gk + 3 < K) {
+      v = *reinterpret_cast<const float4*>(ptr);
+    } else {
+      v.x = ptr[0];
+      if (gk + 1 < K) v.y = ptr[1];
+      if (gk + 2 < K) v.z = ptr[2];
+    }
+  } else if constexpr (ALOAD == ALOAD_JOINER) {
+    const JoinerALoad& j = p.joiner;
+    int s = gm / j.H;
+    int len = j.enc_len[s];
+    if (len <= 0) return v;
+    int t = j.t < len ? j.t : len - 1;
+    const float4 e = *reinterpret_cast<const float4*>(j.enc + (long)(j.enc_off[s] + t) * lda + gk);
+    const float4 d = *reinterpret_cast<const float4*>(j.dec + (long)gm * lda + gk);
+    v.x = tanhf(e.x + d.x);
+    v.y = tanhf(e.y + d.y);
+    v.z = tanhf(e.z + d.z);
+    v.w = tanhf(e.w + d.w);
+  } else if constexpr (ALOAD == ALOAD_CONV2) {
+    // out (t, f) of conv.4; k = (kt*3 + kf)*8 + c over conv1 output [T1][80][8]
+    int t = gm / 39, f = gm - t * 39;
+    int kk = gk >> 3, c = gk & 7;
+    int kt = kk / 3, kf = kk - kt * 3;
+    v = *reinterpret_cast<const float4*>(A + ((long)(2 * t + kt) * 80 + 2 * f + kf) * 8 + c);
+  } else {  // ALOAD_CONV3
+    // out (t, f) of conv.7; k = (kt*3 + kf)*32 + c over conv2 output [L2][39][32]
+    int t = gm / 19, f = gm - t * 19;
+    int kk = gk >> 5, c = gk & 31;
+    int kt = kk / 3, kf = kk - kt * 3;
+    v = *reinterpret_cast<const float4*>(A + ((long)(t + kt) * 39 + 2 * f + kf) * 32 + c);
+  }
+  return v;
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, bool BNC, int EPI>
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmParams p) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int LDA_S = BM + 4;
+  constexpr int LDB_S = BN + 4;
+  constexpr int WTM = BM / WAVES_M;
+  constexpr int WTN = BN / WAVES_N;
+  constexpr int FM = WTM / 32;
+  constexpr int FN = WTN / 32;
+  static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
+  constexpr int A_F4 = BM * BK / 4;
+  constexpr int B_F4 = BN * BK / 4;
+  constexpr int A_LD = (A_F4 + NT - 1) / NT;
+  constexpr int B_LD = (B_F4 + NT - 1) / NT;
+
+  __shared__ float As[2][BK * LDA_S];
+  __shared__ float Bs[2][BK * LDB_S];
+
+  const float* A = p.A;
+  const float* B = p.B;
+  float* C = p.C;
+  const float* aux = p.aux;
+  int M = p.M, K = p.K, lda = p.lda;
+  if (p.slices) {
+    const GemmSlice s = p.slices[blockIdx.z];
+    A += s.a_off;
+    B += s.b_off;
+    C += s.c_off;
+    if (aux) aux += s.aux_off;
+    M = s.M;
+    K = s.K;
+    lda = s.lda;
+  }
+  const int m0 = blockIdx.y * BM;
+  if (m0 >= M) return;
+  const int n0 = blockIdx.x * BN;
+  const int N = p.N;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WAVES_N;
+  const int wn = wid - wm * WAVES_N;
+
+  float4 ra[A_LD];
+  float4 rb[B_LD];
+
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int idx = tid + NT * i;
+      int row = idx >> 2, k4 = idx & 3;
+      ra[i] = (idx < A_F4) ? load_a4<ALOAD>(p, A, M, K, lda, m0 + row, kt * BK + 4 * k4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int idx = tid + NT * i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < B_F4) {
+        if constexpr (!BNC) {
+          int n = idx >> 2, k4 = idx & 3;
+          int gn = n0 + n, gk = kt * BK + 4 * k4;
+          if (gn < N && gk < K) {
+            const float* ptr = B + (long)gn * p.sbn + gk;
+            if (gk + 3 < K) {
+              v = *reinterpret_cast<const float4*>(ptr);
+            } else {
+              v.x = ptr[0];
+              if (gk + 1 < K) v.y = ptr[1];
+              if (gk + 2 < K) v.z = ptr[2];
+            }
+          }
+        } else {
+          int k = idx / (BN / 4), n4 = idx - k * (BN / 4);
+          int gk = kt * BK + k, gn = n0 + 4 * n4;
+          if (gk < K && gn < N) {
+            const float* ptr = B + (long)gk * p.sbk + gn;
+            if (gn + 3 < N) {
+              v = *reinterpret_cast<const float4*>(ptr);
+            } else {
+              v.x = ptr[0];
+              if (gn + 1 < N) v.y = ptr[1];
+              if (gn + 2 < N) v.z = ptr[2];
+            }
+          }
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      int idx = tid + NT * i;
+      if (idx < A_F4) {
+        int row = idx >> 2, k4 = idx & 3;
+        float* d = &As[buf][(4 * k4) * LDA_S + row];
+        d[0] = ra[i].x;
+        d[LDA_S] = ra[i].y;
+        d[2 * LDA_S] = ra[i].z;
+        d[3 * LDA_S] = ra[i].w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      int idx = tid + NT * i;
+      if (idx < B_F4) {
+        if constexpr (!BNC) {
+          int n = idx >> 2, k4 = idx & 3;
+          float* d = &Bs[buf][(4 * k4) * LDB_S + n];
+          d[0] = rb[i].x;
+          d[LDB_S] = rb[i].y;
+          d[2 * LDB_S] = rb[i].z;
+          d[3 * LDB_S] = rb[i].w;
+        } else {
+          int k = idx / (BN / 4), n4 = idx - k * (BN / 4);
+          *reinterpret_cast<float4*>(&Bs[buf][k * LDB_S + 4 * n4]) = rb[i];
+        }
+      }
+    }
+  };
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = (K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const int kr = kk + (lane >> 5);
+      float a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = As[cur][kr * LDA_S + wm * WTM + i * 32 + (lane & 31)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = Bs[cur][kr * LDB_S + wn * WTN + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds column (lane & 31), rows (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * WTN + j * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float bcol = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        float v = acc[i][j][r] * p.alpha + bcol;
+        float* dst = C + (long)row * p.ldc + col;
+        if constexpr (EPI == EPI_SWOOSHL) v = swooshl(v);
+        if constexpr (EPI == EPI_SWOOSHR) v = swooshr(v);
+        if constexpr (EPI == EPI_MULAUX) v *= aux[(long)row * p.ldaux + col];
+        if constexpr (EPI == EPI_RESADD) v += *dst;
+        *dst = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int ALOAD, bool BNC, int EPI>
+void launch_t(const GemmParams& p, hipStream_t st) {
+  dim3 grid(cdiv(p.N, BN), cdiv(p.max_M, BM), p.slices ? p.num_slices : 1);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI>), grid,
+                     dim3(64 * WM * WN), 0, st, p);
+}
+
+template <int ALOAD, bool BNC, int EPI>
+void launch_tile(const GemmParams& p, hipStream_t st) {
+  // BN: the largest of {128, 64, 32} whose padded width is within 15% of the tightest.
+  int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
+  int best = pad32;
+  int BN = (pad128 * 100 <= best * 115) ? 128 : (pad64 * 100 <= best * 115 ? 64 : 32);
+  long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
+  bool big = blocks128 >= 512;
+  if (BN == 128) {
+    if (big) launch_t<128, 128, 2, 2, ALOAD, BNC, EPI>(p, st);
+    else launch_t<64, 128, 2, 2, ALOAD, BNC, EPI>(p, st);
+  } else if (BN == 64) {
+    if (big) launch_t<128, 64, 2, 2, ALOAD, BNC, EPI>(p, st);
+    else launch_t<64, 64, 2, 2, ALOAD, BNC, EPI>(p, st);
+  } else {
+    if (big) launch_t<128, 32, 4, 1, ALOAD, BNC, EPI>(p, st);
+    else launch_t<64, 32, 2, 1, ALOAD, BNC, EPI>(p, st);
+  }
+}
+
+}  // namespace
+
+void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream_t st) {
+  ZASR_REQUIRE(p.N > 0, "gemm: N must be positive");
+  if (p.max_M <= 0) return;
+  ZASR_REQUIRE(p.slices != nullptr || (p.lda % 4 == 0 && p.K % 4 == 0),
+               "gemm: lda and K must be multiples of 4");
+  if (aload == ALOAD_DENSE && !b_ncontig) {
+    switch (epi) {
+      case EPI_NONE: return launch_tile<ALOAD_DENSE, false, EPI_NONE>(p, st);
+      case EPI_SWOOSHL: return launch_tile<ALOAD_DENSE, false, EPI_SWOOSHL>(p, st);
+      case EPI_SWOOSHR: return launch_tile<ALOAD_DENSE, false, EPI_SWOOSHR>(p, st);
+      case EPI_RESADD: return launch_tile<ALOAD_DENSE, false, EPI_RESADD>(p, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_DENSE && b_ncontig) {
+    switch (epi) {
+      case EPI_NONE: return launch_tile<ALOAD_DENSE, true, EPI_NONE>(p, st);
+      case EPI_MULAUX: return launch_tile<ALOAD_DENSE, true, EPI_MULAUX>(p, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_JOINER && !b_ncontig && epi == EPI_NONE) {
+    return launch_tile<ALOAD_JOINER, false, EPI_NONE>(p, st);
+  } else if (aload == ALOAD_CONV2 && !b_ncontig && epi == EPI_SWOOSHR) {
+    return launch_tile<ALOAD_CONV2, false, EPI_SWOOSHR>(p, st);
+  } else if (aload == ALOAD_CONV3 && !b_ncontig && epi == EPI_SWOOSHR) {
+    return launch_tile<ALOAD_CONV3, false, EPI_SWOOSHR>(p, st);
+  }
+  throw std::runtime_error("gemm_f32: unsupported (aload, epi, layout) combination");
+}
+
+}  // namespace zasr

@@ -1,0 +1,114 @@
+// Launch wrappers for the non-GEMM kernels of the offline-ASR hot path.
+//
+// Ragged batches: every per-sequence tensor is stored packed, sequence after sequence,
+// with a device offsets array `off[b]` (size B+1) per time resolution.  Kernels that
+// need a row's sequence find it with a binary search over `off`.
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace zasr {
+
+// ---- fbank (core/asr_engine.py:698-721, kaldi semantics: SURVEY Appendix A) ----
+struct FbankTables {
+  const double* twiddle;    // [256][2]  exp(-2 pi i j / 512)
+  const float* window;      // [400]     povey
+  const int* mel_start;     // [80]
+  const int* mel_len;       // [80]
+  const int* mel_woff;      // [80] offset into mel_w
+  const float* mel_w;       // packed triangle weights
+};
+void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const int* fr_off,
+                  int nseq, int total_frames, const FbankTables& tabs, float* out,
+                  hipStream_t st);
+
+// ---- Conv2dSubsampling pieces (icefall subsampling.py, 3P) ----
+// conv.0 (1->8, 3x3, pad (0,1)) + SwooshR: fbank rows [T][80] -> [T-2][80][8]
+void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, int nseq, int total_rows,
+                  const float* w /*[8][9]*/, const float* b, float* out, hipStream_t st);
+// ConvNeXt depthwise 7x7, zero padding per sequence: [L][19][128] -> [L][19][128]
+void launch_dwconv2d(const float* x, const int* L_off, int nseq, int total_rows,
+                     const float* w /*[128][49]*/, const float* b, float* out, hipStream_t st);
+
+// ---- Zipformer2 encoder elementwise / per-sequence kernels ----
+// y = x * exp(log_scale) * rsqrt(mean((x - bias)^2));  optionally y = orig + (y - orig) * s
+void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_scale,
+                      const float* orig, const float* bypass_scale, hipStream_t st);
+// x = orig + (x - orig) * s[c]
+void launch_bypass(float* x, const float* orig, const float* s, long rows, int d, hipStream_t st);
+// g[r][c] = x2[r][c] * sigmoid(x2[r][d + c])
+void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st);
+// out[t][c] = SwooshR(b[c] + sum_k w[c][k] x[t + k - K/2][c]), zero padding per sequence
+void launch_dwconv1d(const float* x, const int* off, int nseq, int total_rows, int d, int K,
+                     const float* w, const float* b, float* out, hipStream_t st);
+// t1[r][c] = tanh(h3[r][c]) * h3[r][hid + c]
+void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStream_t st);
+// SimpleDownsample: out[t'] = sum_u w[u] x[min(ds t' + u, L - 1)]
+void launch_downsample(const float* x, const int* off_in, const int* off_out, int nseq,
+                       int total_out, int d, int ds, const float* w_host8, float* out,
+                       hipStream_t st);
+// SimpleUpsample + out_combiner bypass: y[t] = orig[t] + (xd[t / ds] - orig[t]) * s
+void launch_upsample_combine(const float* xd, const float* orig, const int* off_in,
+                             const int* off_ds, int nseq, int total_rows, int d, int ds,
+                             const float* s, float* y, hipStream_t st);
+// dst[r][0:dd] = src[r][0:min(ds, dd)], zero-padded  (convert_num_channels)
+void launch_copy_cols(const float* src, int lds, int c0, float* dst, int ldd, int d0, int ncols,
+                      long rows, bool zero_rest, int dst_width, hipStream_t st);
+
+// ---- RelPositionMultiheadAttentionWeights: scores + softmax -> attention weights ----
+struct AttnArgs {
+  const float* qkp;        // [R][ (2*32+4) * H ]
+  int H;                   // heads
+  const float* pos_tab;    // [(2*Pmax - 1)][4*H]  linear_pos(pe(x)), row x + Pmax - 1
+  int pmax;
+  const int* row_off;      // [B+1] packed rows at this resolution
+  const long* a_off;       // [B]   offset of sequence b's [H][L][ldA] block
+  int nseq;
+  int max_len;
+  float* attn;             // output
+};
+void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
+
+// ---- transducer search (core/asr_engine.py:1023-1153) ----
+struct SearchState {
+  // hypothesis slots, [S * Hmax]
+  double* lp;
+  int* lpf;           // 1: lp came from a non-cutoff log-add (np.float64 in the reference),
+                      //    so the next frame adds it in f64; 0: a Python float, added in f32
+  unsigned long long* hash;
+  int* len;
+  int* y1;            // newest context token (ys[-1], clamped >= 0)
+  int* y2;            // older context token (ys[-2], clamped >= 0)
+  int* hw;            // hotword automaton state
+  int* node;          // last emission node (-1: none)
+  int* nh;            // [S] live hypotheses
+  // emission node pool, [S * node_cap]
+  int* node_tok;
+  int* node_frame;
+  int* node_parent;
+  double* node_lp;
+  float4* node_stats;   // (entropy, sum p^(1/3), top1, top2) of the emitting joiner row
+  int* node_count;      // [S]
+  int node_cap;
+};
+struct HotwordTables {
+  int num_states;       // 0 => no hotwords
+  int num_cls;
+  const int* tok2cls;   // [V] token -> column, -1 if the token is not in the trie
+  const int* next;      // [states][cls]
+  const double* delta;  // [states][cls]
+  const double* node_score;  // [states]
+};
+void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st);
+// relu(grouped conv over (E[y2], E[y1])) for every hypothesis slot -> [S*Hmax][D]
+void launch_decoder_prep(const SearchState& s, int rows, const float* emb, const float* conv_w,
+                         int D, float* out, hipStream_t st);
+void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
+                        int beam, int t, const int* enc_len, const HotwordTables& hw,
+                        hipStream_t st);
+void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTables& hw,
+                         int out_cap, int* out_tok, int* out_frame, double* out_lp,
+                         float4* out_stats, int* out_count, hipStream_t st);
+
+}  // namespace zasr

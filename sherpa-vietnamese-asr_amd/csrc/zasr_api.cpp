@@ -1,0 +1,264 @@
+// C ABI of libzasr (include/zasr.h): argument checking, error capture, result objects.
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/zasr.h"
+#include "common.h"
+#include "engine.h"
+#include "host_io.h"
+
+using zasr::Engine;
+using zasr::TokenResult;
+
+struct zasr_recognizer {
+  std::unique_ptr<Engine> eng;
+};
+
+struct zasr_result {
+  std::vector<TokenResult> items;
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::invalid_argument& e) {
+    return fail(ZASR_ERR_NOT_FOUND, e.what());
+  } catch (const std::exception& e) {
+    return fail(ZASR_ERR_RUNTIME, e.what());
+  } catch (...) {
+    return fail(ZASR_ERR_RUNTIME, "unknown error");
+  }
+}
+
+int resolve_beam(zasr_recognizer* h, int32_t beam) {
+  return beam > 0 ? beam : h->eng->default_beam();
+}
+
+}  // namespace
+
+extern "C" {
+
+int zasr_create(const zasr_config* cfg, zasr_recognizer** out) {
+  if (!cfg || !out || !cfg->model_dir) return fail(ZASR_ERR_INVALID, "null config/model_dir/out");
+  *out = nullptr;
+  if (cfg->blank_penalty != 0.f) return fail(ZASR_ERR_INVALID, "blank_penalty must be 0");
+  std::string method = cfg->decoding_method ? cfg->decoding_method : "modified_beam_search";
+  bool greedy = (method == "greedy_search");
+  if (!greedy && method != "modified_beam_search")
+    return fail(ZASR_ERR_INVALID, "decoding_method must be greedy_search or modified_beam_search");
+  int beam = greedy ? 1 : cfg->max_active_paths;
+  if (beam < 1 || beam > 16) return fail(ZASR_ERR_INVALID, "max_active_paths must be in 1..16");
+  if (cfg->num_hotwords < 0) return fail(ZASR_ERR_INVALID, "num_hotwords < 0");
+  return guarded([&]() {
+    std::vector<std::vector<int>> phrases;
+    std::vector<float> scores;
+    const int32_t* tp = cfg->hotword_tokens;
+    for (int i = 0; i < cfg->num_hotwords; ++i) {
+      int n = cfg->hotword_lens[i];
+      if (n < 0) return fail(ZASR_ERR_INVALID, "negative hotword length");
+      phrases.emplace_back(tp, tp + n);
+      tp += n;
+      scores.push_back(cfg->hotword_scores[i]);
+    }
+    // vocab size is needed for the DFA: read it from config.json via a throwaway parse
+    std::string cfg_text = zasr::read_file(std::string(cfg->model_dir) + "/config.json");
+    int V = (int)zasr::Json::parse(cfg_text).at("vocab_size").num;
+    zasr::HotwordDFA dfa = zasr::build_hotword_dfa(phrases, scores, V);
+    auto* h = new zasr_recognizer;
+    h->eng.reset(new Engine(cfg->model_dir, cfg->device_id, beam, greedy, dfa, cfg->precision));
+    *out = h;
+    return (int)ZASR_OK;
+  });
+}
+
+void zasr_destroy(zasr_recognizer* h) { delete h; }
+
+int zasr_fbank(zasr_recognizer* h, const float* wav, int64_t n, int32_t sr, float* out,
+               int64_t cap, int64_t* n_frames) {
+  if (!n_frames || (n > 0 && !wav)) return fail(ZASR_ERR_INVALID, "null argument");
+  if (sr != 16000) return fail(ZASR_ERR_INVALID, "sample rate must be 16000");
+  int64_t frames = n > 0 ? (n + 80) / 160 : 0;
+  *n_frames = frames;
+  if (frames * 80 > cap || (frames > 0 && !out)) return fail(ZASR_ERR_INVALID, "output buffer too small");
+  if (frames == 0) return ZASR_OK;
+  return guarded([&]() {
+    Engine* e = h ? h->eng.get() : nullptr;
+    if (!e) return fail(ZASR_ERR_INVALID, "zasr_fbank needs a recognizer handle");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->fbank_host(wav, (long)n, out);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_decode_batch(zasr_recognizer* h, const float* const* wav, const int64_t* n,
+                      int32_t count, int32_t beam, zasr_result** out) {
+  if (!h || !out || count < 0 || (count > 0 && (!wav || !n))) return fail(ZASR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  return guarded([&]() {
+    Engine* e = h->eng.get();
+    std::lock_guard<std::mutex> lk(e->mu);
+    // stage host chunks into one device buffer, then run the device path
+    std::vector<long> off(count), len(count);
+    long tot = 0;
+    for (int i = 0; i < count; ++i) {
+      if (n[i] < 0) return fail(ZASR_ERR_INVALID, "negative length");
+      off[i] = tot;
+      len[i] = (long)n[i];
+      tot += (long)n[i];
+    }
+    float* d = nullptr;
+    ZASR_HIP_CHECK(hipMalloc(&d, std::max<long>(tot, 1) * sizeof(float)));
+    std::unique_ptr<float, decltype(&hipFree)> guard(d, hipFree);
+    for (int i = 0; i < count; ++i)
+      if (len[i] > 0)
+        ZASR_HIP_CHECK(hipMemcpyAsync(d + off[i], wav[i], len[i] * 4, hipMemcpyHostToDevice, e->stream()));
+    auto r = std::make_unique<zasr_result>();
+    r->items = e->decode_device(d, off, len, resolve_beam(h, beam), e->stream());
+    ZASR_HIP_CHECK(hipStreamSynchronize(e->stream()));
+    *out = r.release();
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_decode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,
+                         int32_t count, int32_t beam, zasr_result** out) {
+  if (!h || !out || count < 0 || (count > 0 && (!feats || !n_frames))) return fail(ZASR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  return guarded([&]() {
+    Engine* e = h->eng.get();
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<const float*> f(feats, feats + count);
+    std::vector<long> fr(n_frames, n_frames + count);
+    auto r = std::make_unique<zasr_result>();
+    r->items = e->decode_features(f, fr, resolve_beam(h, beam));
+    *out = r.release();
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_decode_device(zasr_recognizer* h, const float* d_wav, const int64_t* wav_off,
+                       const int64_t* n, int32_t count, int32_t beam, void* stream,
+                       zasr_result** out) {
+  if (!h || !out || count < 0 || (count > 0 && (!d_wav || !wav_off || !n))) return fail(ZASR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  return guarded([&]() {
+    Engine* e = h->eng.get();
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<long> off(wav_off, wav_off + count), len(n, n + count);
+    auto r = std::make_unique<zasr_result>();
+    r->items = e->decode_device(d_wav, off, len, resolve_beam(h, beam),
+                                reinterpret_cast<hipStream_t>(stream));
+    *out = r.release();
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_encode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,
+                         int32_t count, float* out, int64_t cap, int64_t* t_out) {
+  if (!h || !feats || !n_frames || !out || !t_out || count <= 0) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    Engine* e = h->eng.get();
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<const float*> f(feats, feats + count);
+    std::vector<long> fr(n_frames, n_frames + count);
+    long need = 0;
+    for (int i = 0; i < count; ++i) {
+      if (n_frames[i] < 9) return fail(ZASR_ERR_INVALID, "chunk shorter than 9 fbank frames");
+      need += ((n_frames[i] - 7) / 2 + 1) / 2;
+    }
+    if (need * e->joiner_dim() > cap) return fail(ZASR_ERR_INVALID, "output buffer too small");
+    std::vector<float> enc;
+    std::vector<int> to;
+    e->encode_host(f, fr, enc, to);
+    std::memcpy(out, enc.data(), enc.size() * sizeof(float));
+    for (int i = 0; i < count; ++i) t_out[i] = to[i];
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_search_encoder_out(zasr_recognizer* h, const float* const* enc, const int64_t* t_out,
+                            int32_t count, int32_t beam, zasr_result** out) {
+  if (!h || !enc || !t_out || !out || count < 0) return fail(ZASR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  return guarded([&]() {
+    Engine* e = h->eng.get();
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<const float*> p(enc, enc + count);
+    std::vector<long> t(t_out, t_out + count);
+    auto r = std::make_unique<zasr_result>();
+    r->items = e->search_host(p, t, resolve_beam(h, beam));
+    *out = r.release();
+    return (int)ZASR_OK;
+  });
+}
+
+int32_t zasr_result_count(const zasr_result* r) { return r ? (int32_t)r->items.size() : 0; }
+static const TokenResult* item(const zasr_result* r, int32_t i) {
+  return (r && i >= 0 && i < (int32_t)r->items.size()) ? &r->items[i] : nullptr;
+}
+int32_t zasr_result_num_tokens(const zasr_result* r, int32_t i) {
+  auto* t = item(r, i);
+  return t ? (int32_t)t->tok.size() : 0;
+}
+int32_t zasr_result_num_frames(const zasr_result* r, int32_t i) {
+  auto* t = item(r, i);
+  return t ? t->t_out : 0;
+}
+const int32_t* zasr_result_tokens(const zasr_result* r, int32_t i) {
+  auto* t = item(r, i);
+  return t ? t->tok.data() : nullptr;
+}
+const int32_t* zasr_result_frames(const zasr_result* r, int32_t i) {
+  auto* t = item(r, i);
+  return t ? t->frame.data() : nullptr;
+}
+const double* zasr_result_log_probs(const zasr_result* r, int32_t i) {
+  auto* t = item(r, i);
+  return t ? t->lp.data() : nullptr;
+}
+const float* zasr_result_token_stats(const zasr_result* r, int32_t i) {
+  auto* t = item(r, i);
+  return t ? t->stats.data() : nullptr;
+}
+void zasr_result_free(zasr_result* r) { delete r; }
+
+int32_t zasr_vocab_size(const zasr_recognizer* h) { return h ? h->eng->vocab() : 0; }
+int32_t zasr_joiner_dim(const zasr_recognizer* h) { return h ? h->eng->joiner_dim() : 0; }
+
+int zasr_profile_enable(zasr_recognizer* h, int32_t on) {
+  if (!h) return fail(ZASR_ERR_INVALID, "null handle");
+  h->eng->profile_enable(on != 0);
+  return ZASR_OK;
+}
+int zasr_profile_reset(zasr_recognizer* h) {
+  if (!h) return fail(ZASR_ERR_INVALID, "null handle");
+  return guarded([&]() {
+    h->eng->profile_reset();
+    return (int)ZASR_OK;
+  });
+}
+int zasr_profile_report(zasr_recognizer* h, char* buf, int64_t cap) {
+  if (!h || !buf || cap <= 0) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    std::string s = h->eng->profile_report();
+    if ((int64_t)s.size() + 1 > cap) return fail(ZASR_ERR_INVALID, "report buffer too small");
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return (int)ZASR_OK;
+  });
+}
+
+const char* zasr_last_error(void) { return g_last_error.c_str(); }
+const char* zasr_version(void) { return "zasr 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,278 @@
+"""ctypes binding of libzasr.so (include/zasr.h).
+
+This is the thin host layer the drop-in `core/asr_engine.py` sits on.  There is no CPU
+fallback: if the shared library is missing or fails to load, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEFAULT_LIB = os.path.join(_PKG, "lib", "libzasr.so")
+
+# every symbol declared in include/zasr.h (the CPU test checks the .so exports them all)
+EXPORTS = (
+    "zasr_create", "zasr_destroy", "zasr_fbank", "zasr_decode_batch", "zasr_decode_features",
+    "zasr_decode_device", "zasr_encode_features", "zasr_search_encoder_out",
+    "zasr_result_count", "zasr_result_num_tokens", "zasr_result_num_frames",
+    "zasr_result_tokens", "zasr_result_frames", "zasr_result_log_probs",
+    "zasr_result_token_stats", "zasr_result_free", "zasr_vocab_size", "zasr_joiner_dim",
+    "zasr_profile_enable", "zasr_profile_reset", "zasr_profile_report", "zasr_last_error",
+    "zasr_version",
+)
+
+
+class ZasrError(RuntimeError):
+    pass
+
+
+class _Config(C.Structure):
+    _fields_ = [
+        ("model_dir", C.c_char_p),
+        ("decoding_method", C.c_char_p),
+        ("max_active_paths", C.c_int32),
+        ("blank_penalty", C.c_float),
+        ("hotword_tokens", C.POINTER(C.c_int32)),
+        ("hotword_lens", C.POINTER(C.c_int32)),
+        ("hotword_scores", C.POINTER(C.c_float)),
+        ("num_hotwords", C.c_int32),
+        ("device_id", C.c_int32),
+        ("precision", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: Optional[str] = None) -> C.CDLL:
+    """Load libzasr.so (raises if absent: the product has no fallback path)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("ZASR_LIB", DEFAULT_LIB)
+    if not os.path.exists(p):
+        raise ZasrError(f"libzasr.so not found at {p}; build it with "
+                        f"`make -C sherpa-vietnamese-asr_amd/csrc` (or __graft_entry__.build())")
+    lib = C.CDLL(p)
+    P, I32, I64 = C.c_void_p, C.c_int32, C.c_int64
+    fp = C.POINTER(C.c_float)
+    lib.zasr_create.argtypes = [C.POINTER(_Config), C.POINTER(P)]
+    lib.zasr_create.restype = C.c_int
+    lib.zasr_destroy.argtypes = [P]
+    lib.zasr_destroy.restype = None
+    lib.zasr_fbank.argtypes = [P, fp, I64, I32, fp, I64, C.POINTER(I64)]
+    lib.zasr_fbank.restype = C.c_int
+    lib.zasr_decode_batch.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, I32, C.POINTER(P)]
+    lib.zasr_decode_batch.restype = C.c_int
+    lib.zasr_decode_features.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, I32, C.POINTER(P)]
+    lib.zasr_decode_features.restype = C.c_int
+    lib.zasr_decode_device.argtypes = [P, P, C.POINTER(I64), C.POINTER(I64), I32, I32, P,
+                                       C.POINTER(P)]
+    lib.zasr_decode_device.restype = C.c_int
+    lib.zasr_encode_features.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, fp, I64,
+                                         C.POINTER(I64)]
+    lib.zasr_encode_features.restype = C.c_int
+    lib.zasr_search_encoder_out.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, I32,
+                                            C.POINTER(P)]
+    lib.zasr_search_encoder_out.restype = C.c_int
+    for n in ("zasr_result_count",):
+        getattr(lib, n).argtypes = [P]
+        getattr(lib, n).restype = I32
+    for n in ("zasr_result_num_tokens", "zasr_result_num_frames"):
+        getattr(lib, n).argtypes = [P, I32]
+        getattr(lib, n).restype = I32
+    lib.zasr_result_tokens.argtypes = [P, I32]
+    lib.zasr_result_tokens.restype = C.POINTER(I32)
+    lib.zasr_result_frames.argtypes = [P, I32]
+    lib.zasr_result_frames.restype = C.POINTER(I32)
+    lib.zasr_result_log_probs.argtypes = [P, I32]
+    lib.zasr_result_log_probs.restype = C.POINTER(C.c_double)
+    lib.zasr_result_token_stats.argtypes = [P, I32]
+    lib.zasr_result_token_stats.restype = fp
+    lib.zasr_result_free.argtypes = [P]
+    lib.zasr_result_free.restype = None
+    lib.zasr_vocab_size.argtypes = [P]
+    lib.zasr_vocab_size.restype = I32
+    lib.zasr_joiner_dim.argtypes = [P]
+    lib.zasr_joiner_dim.restype = I32
+    lib.zasr_profile_enable.argtypes = [P, I32]
+    lib.zasr_profile_enable.restype = C.c_int
+    lib.zasr_profile_reset.argtypes = [P]
+    lib.zasr_profile_reset.restype = C.c_int
+    lib.zasr_profile_report.argtypes = [P, C.c_char_p, I64]
+    lib.zasr_profile_report.restype = C.c_int
+    lib.zasr_last_error.argtypes = []
+    lib.zasr_last_error.restype = C.c_char_p
+    lib.zasr_version.argtypes = []
+    lib.zasr_version.restype = C.c_char_p
+    if path is None:
+        _lib = lib
+    return lib
+
+
+@dataclasses.dataclass
+class SearchResult:
+    """One chunk's search output: the tuple of core/asr_engine.py:1153 with per-token
+    entropy statistics (entropy, sum p^(1/3), top1, top2) in place of raw logits rows."""
+    token_ids: np.ndarray
+    frames: np.ndarray
+    log_probs: np.ndarray
+    stats: np.ndarray
+    T: int
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _ptr_array(arrs: Sequence[np.ndarray]):
+    fp = C.POINTER(C.c_float)
+    return (fp * len(arrs))(*[a.ctypes.data_as(fp) for a in arrs])
+
+
+class Recognizer:
+    def __init__(self, model_dir: str, decoding_method: str = "modified_beam_search",
+                 max_active_paths: int = 8, hotwords: Optional[Sequence[Sequence[int]]] = None,
+                 hotword_scores: Optional[Sequence[float]] = None, device_id: int = 0,
+                 precision: str = "fp32", lib_path: Optional[str] = None):
+        self.lib = load_library(lib_path)
+        hotwords = [list(map(int, h)) for h in (hotwords or [])]
+        scores = list(hotword_scores or [1.5] * len(hotwords))
+        flat = np.array([t for h in hotwords for t in h] or [0], dtype=np.int32)
+        lens = np.array([len(h) for h in hotwords] or [0], dtype=np.int32)
+        sc = np.array(scores or [0.0], dtype=np.float32)
+        self._keep = (flat, lens, sc)
+        cfg = _Config(model_dir.encode(), decoding_method.encode(), max_active_paths, 0.0,
+                      flat.ctypes.data_as(C.POINTER(C.c_int32)),
+                      lens.ctypes.data_as(C.POINTER(C.c_int32)),
+                      sc.ctypes.data_as(C.POINTER(C.c_float)), len(hotwords), device_id,
+                      {"fp32": 0, "bf16": 1}[precision])
+        h = C.c_void_p()
+        rc = self.lib.zasr_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            msg = self.lib.zasr_last_error().decode()
+            if rc == 2:
+                raise FileNotFoundError(msg)
+            raise ZasrError(msg)
+        self.handle = h
+        self.vocab_size = self.lib.zasr_vocab_size(h)
+        self.joiner_dim = self.lib.zasr_joiner_dim(h)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.zasr_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ZasrError(self.lib.zasr_last_error().decode())
+
+    def _collect(self, res) -> List[SearchResult]:
+        out = []
+        try:
+            n = self.lib.zasr_result_count(res)
+            for i in range(n):
+                k = self.lib.zasr_result_num_tokens(res, i)
+                T = self.lib.zasr_result_num_frames(res, i)
+                if k > 0:
+                    tok = np.ctypeslib.as_array(self.lib.zasr_result_tokens(res, i), (k,)).copy()
+                    fr = np.ctypeslib.as_array(self.lib.zasr_result_frames(res, i), (k,)).copy()
+                    lp = np.ctypeslib.as_array(self.lib.zasr_result_log_probs(res, i), (k,)).copy()
+                    st = np.ctypeslib.as_array(self.lib.zasr_result_token_stats(res, i),
+                                               (k * 4,)).copy().reshape(k, 4)
+                else:
+                    tok = np.zeros(0, np.int32)
+                    fr = np.zeros(0, np.int32)
+                    lp = np.zeros(0, np.float64)
+                    st = np.zeros((0, 4), np.float32)
+                out.append(SearchResult(tok, fr, lp, st, T))
+        finally:
+            self.lib.zasr_result_free(res)
+        return out
+
+    def fbank(self, audio) -> np.ndarray:
+        a = _f32(audio)
+        n = a.shape[0]
+        frames = (n + 80) // 160 if n > 0 else 0
+        out = np.empty((max(frames, 1), 80), dtype=np.float32)
+        nf = C.c_int64()
+        fp = C.POINTER(C.c_float)
+        self._check(self.lib.zasr_fbank(self.handle, a.ctypes.data_as(fp), n, 16000,
+                                        out.ctypes.data_as(fp), out.size, C.byref(nf)))
+        return out[: nf.value]
+
+    def decode(self, chunks: Sequence, beam: int = 0) -> List[SearchResult]:
+        arrs = [_f32(c) for c in chunks]
+        ns = (C.c_int64 * len(arrs))(*[a.shape[0] for a in arrs])
+        res = C.c_void_p()
+        self._check(self.lib.zasr_decode_batch(self.handle, _ptr_array(arrs), ns, len(arrs),
+                                               beam, C.byref(res)))
+        return self._collect(res)
+
+    def decode_features(self, feats: Sequence, beam: int = 0) -> List[SearchResult]:
+        arrs = [_f32(f) for f in feats]
+        ns = (C.c_int64 * len(arrs))(*[a.shape[0] for a in arrs])
+        res = C.c_void_p()
+        self._check(self.lib.zasr_decode_features(self.handle, _ptr_array(arrs), ns, len(arrs),
+                                                  beam, C.byref(res)))
+        return self._collect(res)
+
+    def decode_device(self, d_wav_ptr: int, offsets: Sequence[int], lengths: Sequence[int],
+                      beam: int = 0, stream: int = 0) -> List[SearchResult]:
+        n = len(lengths)
+        off = (C.c_int64 * n)(*offsets)
+        ln = (C.c_int64 * n)(*lengths)
+        res = C.c_void_p()
+        self._check(self.lib.zasr_decode_device(self.handle, C.c_void_p(d_wav_ptr), off, ln, n,
+                                                beam, C.c_void_p(stream), C.byref(res)))
+        return self._collect(res)
+
+    def encode_features(self, feats: Sequence) -> List[np.ndarray]:
+        arrs = [_f32(f) for f in feats]
+        ns = (C.c_int64 * len(arrs))(*[a.shape[0] for a in arrs])
+        tot = sum(((a.shape[0] - 7) // 2 + 1) // 2 for a in arrs)
+        out = np.empty((max(tot, 1), self.joiner_dim), dtype=np.float32)
+        tout = (C.c_int64 * len(arrs))()
+        fp = C.POINTER(C.c_float)
+        self._check(self.lib.zasr_encode_features(self.handle, _ptr_array(arrs), ns, len(arrs),
+                                                  out.ctypes.data_as(fp), out.size, tout))
+        res, pos = [], 0
+        for i in range(len(arrs)):
+            res.append(out[pos: pos + tout[i]].copy())
+            pos += tout[i]
+        return res
+
+    def search(self, enc_outs: Sequence, beam: int = 0) -> List[SearchResult]:
+        arrs = [_f32(e).reshape(-1, self.joiner_dim) for e in enc_outs]
+        ns = (C.c_int64 * len(arrs))(*[a.shape[0] for a in arrs])
+        res = C.c_void_p()
+        self._check(self.lib.zasr_search_encoder_out(self.handle, _ptr_array(arrs), ns,
+                                                     len(arrs), beam, C.byref(res)))
+        return self._collect(res)
+
+    # profiling (HIP events on the library's stream)
+    def profile(self, on: bool = True):
+        self._check(self.lib.zasr_profile_enable(self.handle, 1 if on else 0))
+
+    def profile_reset(self):
+        self._check(self.lib.zasr_profile_reset(self.handle))
+
+    def profile_report(self) -> dict:
+        buf = C.create_string_buffer(1 << 16)
+        self._check(self.lib.zasr_profile_report(self.handle, buf, len(buf)))
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, cnt, ms = line.split()
+            out[name] = (int(cnt), float(ms))
+        return out
