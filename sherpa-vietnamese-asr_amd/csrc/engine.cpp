@@ -569,7 +569,8 @@ std::string Engine::profile_report() {
 // ------------------------------------------------------------------------------------
 // building blocks
 // ------------------------------------------------------------------------------------
-void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi) {
+void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
+                    const char* cls) {
   GemmParams p{};
   p.A = A;
   p.lda = lda;
@@ -584,7 +585,7 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
   p.K = l.K;
   p.alpha = 1.f;
   p.max_M = M;
-  prof_begin("gemm");
+  prof_begin(cls);
   gemm_f32(p, epi, ALOAD_DENSE, false, st_);
   prof_end();
 }
@@ -996,7 +997,7 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     prof_begin("decoder");
     launch_decoder_prep(st, rows, model_.dec_emb, model_.dec_conv, D, dec_in, st_);
     prof_end();
-    linear(model_.dec_proj, dec_in, D, rows, dec_out, D, EPI_NONE);
+    linear(model_.dec_proj, dec_in, D, rows, dec_out, D, EPI_NONE, "dec_gemm");
     GemmParams p{};
     p.lda = D;
     p.B = model_.joiner.w;

@@ -127,7 +127,8 @@ class Engine {
   void layer_forward(const DStack& stk, const DLayer& ly, float* X, int R, const int* d_off,
                      const std::vector<int>& lens, const long* d_aoff, const void* d_slices_attn,
                      const void* d_slices_nl, int maxL);
-  void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi);
+  void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
+              const char* cls = "enc_gemm");
   void ensure_pos_tables(int max_len);
 
   // timing

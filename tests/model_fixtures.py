@@ -8,14 +8,14 @@ import tempfile
 
 import numpy as np
 
-from zasr.model import (ZipformerConfig, save_model_dir, synth_tokens, synth_weights,
+from zasr.model import (WEIGHTS_VERSION, ZipformerConfig, save_model_dir, synth_tokens, synth_weights,
                         zipformer_m, zipformer_tiny)
 
 _CACHE = os.environ.get("ZASR_TEST_MODELS", os.path.join(tempfile.gettempdir(), "zasr_test_models"))
 
 
 def model_dir(name: str, cfg: ZipformerConfig, weights) -> str:
-    path = os.path.join(_CACHE, name)
+    path = os.path.join(_CACHE, f"{name}_v{WEIGHTS_VERSION}")
     if not os.path.exists(os.path.join(path, "model.safetensors")):
         save_model_dir(path, cfg, weights, synth_tokens(cfg.vocab_size))
     return path

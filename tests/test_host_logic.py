@@ -1,0 +1,43 @@
+"""Host-side word post-processing of the drop-in `decode_chunk` vs the reference's own
+output (golden fixtures from core/asr_engine.py:1209-1326), on CPU: the search result is
+the oracle's (pinned separately) with raw joiner rows, exercising the same BPE merge,
+timestamps, probabilities and entropy aggregation code the GPU path uses."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from core.asr_engine import _words_from_search
+from oracle.search import HotwordGraph, beam_search
+from synth_case import case_config, dec_joiner_weights, enc_out_for, np_decoder, np_joiner
+from zasr.model import synth_tokens
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CASES = [p for p in sorted(glob.glob(os.path.join(GOLD, "search_*.json")))
+         if "decode_chunk" in json.load(open(p))]
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(c) for c in CASES])
+def test_decode_chunk_words_match_reference(path):
+    g = json.load(open(path))
+    cfg = case_config(g["kind"])
+    w = dec_joiner_weights(g["kind"], g["seed"])
+    enc = enc_out_for(g["kind"], g["seed"], g["T"], cfg.joiner_dim)
+    graph = HotwordGraph(g["phrases"], g["scores"]) if g["hotwords"] else None
+    toks, frames, lps, T, emit = beam_search(enc, lambda y: np_decoder(w, y),
+                                             lambda e, d: np_joiner(w, e, d), g["beam"], graph)
+    id2token = dict(enumerate(synth_tokens(cfg.vocab_size)))
+    dc = g["decode_chunk"]
+    words = _words_from_search(id2token, cfg.vocab_size, dc["n_samples"], dc["time_offset"],
+                               toks, frames, lps, T, emit)
+    ref = dc["words"]
+    assert len(words) == len(ref)
+    for a, b in zip(words, ref):
+        assert set(a) == set(b)
+        for k, v in b.items():
+            if isinstance(v, float):
+                assert a[k] == pytest.approx(v, abs=1e-12), k
+            else:
+                assert a[k] == v, k
