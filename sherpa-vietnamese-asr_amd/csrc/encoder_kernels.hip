@@ -167,42 +167,65 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, int nse
 
 // =====================================================================================
 // ConvNeXt depthwise Conv2d(128, 7x7, padding 3) over [L][19][128] per sequence.
-// One thread per output element, channel fastest (coalesced).
+// Block tile: 16 packed time rows x 19 freq x 32 channels, staged with a 3-row halo in
+// LDS; zero padding outside each row's own sequence (so ragged batches == batch 1).
 // =====================================================================================
-__global__ void dwconv2d_kernel(const float* __restrict__ x, const int* __restrict__ L_off,
-                                int nseq, int total_rows, const float* __restrict__ w,
-                                const float* __restrict__ bias, float* __restrict__ out) {
-  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)total_rows * 19 * 128;
-  if (e >= total) return;
-  int c = e & 127;
-  long rf = e >> 7;
-  int row = (int)(rf / 19), f = (int)(rf - (long)row * 19);
-  int b = find_seq(L_off, nseq, row);
-  int t = row - L_off[b];
-  int L = L_off[b + 1] - L_off[b];
-  const float* xs = x + (long)L_off[b] * 19 * 128;
-  float acc = bias[c];
-  const float* wc = w + c * 49;
-  for (int i = 0; i < 7; ++i) {
-    int tt = t + i - 3;
-    if (tt < 0 || tt >= L) continue;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      int ff = f + j - 3;
-      if (ff < 0 || ff >= 19) continue;
-      acc = fmaf(wc[i * 7 + j], xs[((long)tt * 19 + ff) * 128 + c], acc);
-    }
+constexpr int kDw2T = 16;
+
+__global__ __launch_bounds__(256) void dwconv2d_kernel(const float* __restrict__ x,
+                                                       const int* __restrict__ L_off, int nseq,
+                                                       int total_rows, const float* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ out) {
+  __shared__ float tile[(kDw2T + 6) * 19 * 32];
+  const int r0 = blockIdx.x * kDw2T;
+  const int c0 = blockIdx.y * 32;
+  const int tid = threadIdx.x;
+  // stage rows r0-3 .. r0+kDw2T+2 (packed), channels c0..c0+31
+  for (int e = tid; e < (kDw2T + 6) * 19 * 8; e += 256) {
+    const int c4 = e & 7;
+    const int rf = e >> 3;
+    const int rr = rf / 19, f = rf - rr * 19;
+    const int r = r0 - 3 + rr;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= 0 && r < total_rows)
+      v = *reinterpret_cast<const float4*>(x + ((long)r * 19 + f) * 128 + c0 + 4 * c4);
+    *reinterpret_cast<float4*>(&tile[(rr * 19 + f) * 32 + 4 * c4]) = v;
   }
-  out[e] = acc;
+  __syncthreads();
+  const int c = tid & 31;
+  float wr[49];
+#pragma unroll
+  for (int k = 0; k < 49; ++k) wr[k] = w[(c0 + c) * 49 + k];
+  const float bc = bias[c0 + c];
+  for (int p = tid >> 5; p < kDw2T * 19; p += 8) {
+    const int tr = p / 19, f = p - tr * 19;
+    const int r = r0 + tr;
+    if (r >= total_rows) break;
+    const int b = find_seq(L_off, nseq, r);
+    const int lo = L_off[b] - r, hi = L_off[b + 1] - 1 - r;  // allowed time offsets
+    float acc = bc;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int dt = i - 3;
+      if (dt < lo || dt > hi) continue;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const int ff = f + j - 3;
+        if (ff < 0 || ff >= 19) continue;
+        acc = fmaf(wr[i * 7 + j], tile[((tr + 3 + dt) * 19 + ff) * 32 + c], acc);
+      }
+    }
+    out[((long)r * 19 + f) * 128 + c0 + c] = acc;
+  }
 }
 
 void launch_dwconv2d(const float* x, const int* L_off, int nseq, int total_rows, const float* w,
                      const float* b, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
-  long n = (long)total_rows * 19 * 128;
-  hipLaunchKernelGGL(dwconv2d_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, L_off, nseq,
-                     total_rows, w, b, out);
+  dim3 grid(cdiv(total_rows, kDw2T), 4);
+  hipLaunchKernelGGL(dwconv2d_kernel, grid, dim3(256), 0, st, x, L_off, nseq, total_rows, w, b,
+                     out);
 }
 
 // =====================================================================================
@@ -313,34 +336,64 @@ void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStrea
 }
 
 // =====================================================================================
-// depthwise conv1d over time (ConvolutionModule), zero padding per sequence, + SwooshR
+// ConvolutionModule core: GLU (x * sigmoid(s) of the in_proj halves) -> depthwise conv1d
+// over time (zero padding per sequence) + bias -> SwooshR.  Block tile: 64 packed rows x
+// 64 channels with a K/2 halo staged in LDS as GLU outputs.
 // =====================================================================================
-__global__ void dwconv1d_kernel(const float* __restrict__ x, const int* __restrict__ off,
-                                int nseq, int total_rows, int d, int K,
-                                const float* __restrict__ w, const float* __restrict__ bias,
-                                float* __restrict__ out) {
-  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)total_rows * d) return;
-  int row = (int)(e / d), c = (int)(e - (long)row * d);
-  int b = find_seq(off, nseq, row);
-  int lo = off[b], hi = off[b + 1];
-  int half = K >> 1;
-  float acc = bias[c];
-  const float* wc = w + (long)c * K;
-  for (int k = 0; k < K; ++k) {
-    int rr = row + k - half;
-    if (rr < lo || rr >= hi) continue;
-    acc = fmaf(wc[k], x[(long)rr * d + c], acc);
+constexpr int kDw1T = 64;
+
+__global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
+    const float* __restrict__ x2, const int* __restrict__ off, int nseq, int total_rows, int d,
+    int K, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out) {
+  extern __shared__ float tile[];  // [(kDw1T + K - 1)][64]
+  const int half = K >> 1;
+  const int r0 = blockIdx.x * kDw1T;
+  const int c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  const int nrows = kDw1T + K - 1;
+  for (int e = tid; e < nrows * 16; e += 256) {
+    const int c4 = e & 15, rr = e >> 4;
+    const int r = r0 - half + rr;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= 0 && r < total_rows && c0 + 4 * c4 < d) {
+      const float4 a = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + c0 + 4 * c4);
+      const float4 g = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + d + c0 + 4 * c4);
+      v = make_float4(a.x * sigmoidf_(g.x), a.y * sigmoidf_(g.y), a.z * sigmoidf_(g.z),
+                      a.w * sigmoidf_(g.w));
+    }
+    *reinterpret_cast<float4*>(&tile[rr * 64 + 4 * c4]) = v;
   }
-  out[e] = swooshr(acc);
+  __syncthreads();
+  const int c = tid & 63;
+  if (c0 + c >= d) return;
+  float wr[31];
+#pragma unroll
+  for (int k = 0; k < 31; ++k) wr[k] = (k < K) ? w[(long)(c0 + c) * K + k] : 0.f;
+  const float bc = bias[c0 + c];
+  for (int tr = tid >> 6; tr < kDw1T; tr += 4) {
+    const int r = r0 + tr;
+    if (r >= total_rows) break;
+    const int b = find_seq(off, nseq, r);
+    const int lo = off[b] - r, hi = off[b + 1] - 1 - r;
+    float acc = bc;
+#pragma unroll
+    for (int k = 0; k < 31; ++k) {
+      const int dt = k - half;
+      if (k >= K || dt < lo || dt > hi) continue;
+      acc = fmaf(wr[k], tile[(tr + k) * 64 + c], acc);
+    }
+    out[(long)r * d + c0 + c] = swooshr(acc);
+  }
 }
 
-void launch_dwconv1d(const float* x, const int* off, int nseq, int total_rows, int d, int K,
-                     const float* w, const float* b, float* out, hipStream_t st) {
-  long n = (long)total_rows * d;
-  if (n <= 0) return;
-  hipLaunchKernelGGL(dwconv1d_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, off, nseq,
-                     total_rows, d, K, w, b, out);
+void launch_glu_dwconv1d(const float* x2, const int* off, int nseq, int total_rows, int d, int K,
+                         const float* w, const float* b, float* out, hipStream_t st) {
+  if (total_rows <= 0) return;
+  ZASR_REQUIRE(K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
+  dim3 grid(cdiv(total_rows, kDw1T), cdiv(d, 64));
+  size_t lds = (size_t)(kDw1T + K - 1) * 64 * sizeof(float);
+  hipLaunchKernelGGL(glu_dwconv1d_kernel, grid, dim3(256), lds, st, x2, off, nseq, total_rows, d,
+                     K, w, b, out);
 }
 
 // =====================================================================================

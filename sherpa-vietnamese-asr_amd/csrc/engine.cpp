@@ -231,7 +231,7 @@ void Engine::upload(void* dst, const void* src, size_t bytes) {
 Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const HotwordDFA& hw,
                int precision)
     : device_(device), beam_(beam), greedy_(greedy), precision_(precision), hw_host_(hw) {
-  ZASR_REQUIRE(precision == 0, "only the fp32 precision mode is built in this version");
+  ZASR_REQUIRE(precision == 0 || precision == 1, "precision must be 0 (fp32) or 1 (bf16)");
   ZASR_HIP_CHECK(hipSetDevice(device_));
   ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   st_ = stream_;
@@ -377,9 +377,50 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
   const int D = cfg.dec_dim;
   model_.dec_emb = dev(tensor("decoder.embedding.weight", {cfg.V, D}).data, (size_t)cfg.V * D);
   model_.dec_conv = dev(tensor("decoder.conv.weight", {D, 4, 2}).data, (size_t)D * 8);
+  {
+    // decoder conv taps per vocabulary entry: tap_k[v][c] = sum_ci W[c][ci][k] E[v][4(c/4)+ci]
+    const HostTensor& E = tensor("decoder.embedding.weight", {cfg.V, D});
+    const HostTensor& Wc = tensor("decoder.conv.weight", {D, 4, 2});
+    std::vector<float> t0((size_t)cfg.V * D), t1((size_t)cfg.V * D);
+    for (int v = 0; v < cfg.V; ++v)
+      for (int c = 0; c < D; ++c) {
+        const float* e = E.data + (size_t)v * D + (c & ~3);
+        const float* w = Wc.data + (size_t)c * 8;
+        float a0 = 0.f, a1 = 0.f;
+        for (int ci = 0; ci < 4; ++ci) {
+          a0 = std::fma(w[ci * 2 + 0], e[ci], a0);
+          a1 = std::fma(w[ci * 2 + 1], e[ci], a1);
+        }
+        t0[(size_t)v * D + c] = a0;
+        t1[(size_t)v * D + c] = a1;
+      }
+    model_.dec_tap0 = dev(t0.data(), t0.size());
+    model_.dec_tap1 = dev(t1.data(), t1.size());
+  }
   model_.dec_proj = lin("decoder_proj", cfg.joiner_dim, D);
   model_.joiner = lin("joiner.output_linear", cfg.V, cfg.joiner_dim);
   ensure_pos_tables(2048);
+  if (precision_ == 1) {  // bf16 copies of every dense projection weight
+    auto mk = [&](DLin& l) {
+      void* p = nullptr;
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2));
+      model_.allocations.push_back(p);
+      convert_to_bf16(l.w, p, (long)l.N * l.K, stream_);
+      l.wh = p;
+    };
+    for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
+                    &model_.enc_proj})
+      mk(*l);
+    for (auto& s : model_.stacks)
+      for (auto& L : s.layers) {
+        for (DLin* l : {&L.attn_in, &L.na_in, &L.na_out}) mk(*l);
+        for (int a = 0; a < 2; ++a)
+          for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mk(*l);
+        for (int a = 0; a < 3; ++a)
+          for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mk(*l);
+      }
+    ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
 
   // ---- fbank tables ----
   {
@@ -586,7 +627,10 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
   p.alpha = 1.f;
   p.max_M = M;
   prof_begin(cls);
-  gemm_f32(p, epi, ALOAD_DENSE, false, st_);
+  if (l.wh)
+    gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_);
+  else
+    gemm_f32(p, epi, ALOAD_DENSE, false, st_);
   prof_end();
 }
 
@@ -688,14 +732,10 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   };
   auto conv = [&](int k) {
     float* g2 = ws<float>("ly_g2", (size_t)R * 2 * d);
-    float* g = ws<float>("ly_g", (size_t)R * d);
     float* dc = ws<float>("ly_dc", (size_t)R * d);
     linear(Ly.cv_in[k], X, d, R, g2, 2 * d, EPI_NONE);
-    prof_begin("elementwise");
-    launch_glu(g2, g, R, d, st_);
-    prof_end();
     prof_begin("dwconv1d");
-    launch_dwconv1d(g, d_off, B, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+    launch_glu_dwconv1d(g2, d_off, B, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
     prof_end();
     linear(Ly.cv_out[k], dc, d, R, X, d, EPI_RESADD);
   };
@@ -847,7 +887,10 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     p.num_slices = B;
     p.max_M = mc2.maxlen * 39;
     prof_begin("frontend_conv");
-    gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV2, false, st_);
+    if (model_.conv4.wh)
+      gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_);
+    else
+      gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV2, false, st_);
     prof_end();
   }
   float* x3 = ws<float>("fe_x3", (size_t)mL.total * 19 * 128);
@@ -866,7 +909,10 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     p.num_slices = B;
     p.max_M = mL.maxlen * 19;
     prof_begin("frontend_conv");
-    gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
+    if (model_.conv7.wh)
+      gemm_bf16(p, model_.conv7.wh, EPI_SWOOSHR, ALOAD_CONV3, st_);
+    else
+      gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
     prof_end();
   }
   float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
@@ -984,9 +1030,9 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   st.node_lp = ws<double>("se_nlp", ncap);
   st.node_stats = ws<float4>("se_nst", ncap);
   st.node_count = ws<int>("se_ncnt", S);
-  float* dec_in = ws<float>("se_decin", slots * D);
-  float* dec_out = ws<float>("se_decout", slots * D);
+  float* J = ws<float>("se_joinin", slots * D);
   float* logits = ws<float>("se_logits", slots * V);
+  DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
   prof_begin("search");
   launch_search_init(st, S, H, st_);
   prof_end();
@@ -994,26 +1040,13 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   for (int t = 0; t < Tmax; ++t) {
     while (active > 0 && el[active - 1] <= t) --active;
     const int rows = active * H;
+    DecJoinArgs da{dw, model_.dec_proj.w, st.y1, st.y2, d_enc, d_eo, J, rows, H, t};
     prof_begin("decoder");
-    launch_decoder_prep(st, rows, model_.dec_emb, model_.dec_conv, D, dec_in, st_);
+    launch_decjoin(da, st_);
     prof_end();
-    linear(model_.dec_proj, dec_in, D, rows, dec_out, D, EPI_NONE, "dec_gemm");
-    GemmParams p{};
-    p.lda = D;
-    p.B = model_.joiner.w;
-    p.sbk = 1;
-    p.sbn = D;
-    p.C = logits;
-    p.ldc = V;
-    p.bias = model_.joiner.b;
-    p.M = rows;
-    p.N = V;
-    p.K = D;
-    p.alpha = 1.f;
-    p.max_M = rows;
-    p.joiner = JoinerALoad{d_enc, dec_out, d_eo, d_el, H, t};
+    JoinerArgs ja{J, model_.joiner.w, model_.joiner.b, logits, rows, V, D};
     prof_begin("joiner");
-    gemm_f32(p, EPI_NONE, ALOAD_JOINER, false, st_);
+    launch_joiner(ja, st_);
     prof_end();
     prof_begin("search");
     launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, st_);

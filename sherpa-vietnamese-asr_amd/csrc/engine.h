@@ -29,6 +29,7 @@ struct DLin {
   float* w = nullptr;  // [N][K]
   float* b = nullptr;  // [N] or null
   int N = 0, K = 0;
+  void* wh = nullptr;  // bf16 copy of w (precision mode bf16)
 };
 
 struct DLayer {
@@ -61,6 +62,8 @@ struct DModel {
   float out_ds_w[2] = {0, 0};
   float* dec_emb = nullptr;   // [V][D]
   float* dec_conv = nullptr;  // [D][4][2]
+  float* dec_tap0 = nullptr;  // [V][D] conv tap 0 of each embedding row
+  float* dec_tap1 = nullptr;  // [V][D] conv tap 1
   int pmax = 0;
   std::vector<void*> allocations;
 };

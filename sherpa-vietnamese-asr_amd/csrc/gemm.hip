@@ -265,6 +265,194 @@ void launch_tile(const GemmParams& p, hipStream_t st) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// bf16 MFMA variant (the "bf16" precision mode): A converted f32 -> bf16 (RNE) while staging,
+// B = weights pre-converted to bf16 [N][K]; v_mfma_f32_32x32x16_bf16 with f32 accumulate.
+// LDS images are row-major [row][BK + 8] bf16 (80-byte rows: conflict-free ds_read_b128 of
+// the 8-element k-fragments).
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int BKH = 32;
+constexpr int LDH = BKH + 8;
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI>
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmParams p,
+                                                                          const __bf16* Bw) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WTM = BM / WAVES_M;
+  constexpr int WTN = BN / WAVES_N;
+  constexpr int FM = WTM / 32;
+  constexpr int FN = WTN / 32;
+  static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
+  constexpr int A_G = BM * BKH / 8;  // 8-element groups per stage
+  constexpr int B_G = BN * BKH / 8;
+  constexpr int A_LD = (A_G + NT - 1) / NT;
+  constexpr int B_LD = (B_G + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * LDH];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * LDH];
+
+  const float* A = p.A;
+  float* C = p.C;
+  const float* aux = p.aux;
+  int M = p.M, K = p.K, lda = p.lda;
+  long b_off = 0;
+  if (p.slices) {
+    const GemmSlice s = p.slices[blockIdx.z];
+    A += s.a_off;
+    b_off = s.b_off;
+    C += s.c_off;
+    if (aux) aux += s.aux_off;
+    M = s.M;
+    K = s.K;
+    lda = s.lda;
+  }
+  const __bf16* B = Bw + b_off;
+  const int m0 = blockIdx.y * BM;
+  if (m0 >= M) return;
+  const int n0 = blockIdx.x * BN;
+  const int N = p.N;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WAVES_N;
+  const int wn = wid - wm * WAVES_N;
+
+  bf16x8 ra[A_LD], rb[B_LD];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx >> 2, k8 = idx & 3;
+      bf16x8 v;
+      for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
+      if (idx < A_G) {
+        const int gk = kt * BKH + 8 * k8;
+        float4 x0 = load_a4<ALOAD>(p, A, M, K, lda, m0 + row, gk);
+        float4 x1 = load_a4<ALOAD>(p, A, M, K, lda, m0 + row, gk + 4);
+        v[0] = (__bf16)x0.x; v[1] = (__bf16)x0.y; v[2] = (__bf16)x0.z; v[3] = (__bf16)x0.w;
+        v[4] = (__bf16)x1.x; v[5] = (__bf16)x1.y; v[6] = (__bf16)x1.z; v[7] = (__bf16)x1.w;
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int idx = tid + NT * i;
+      const int n = idx >> 2, k8 = idx & 3;
+      bf16x8 v;
+      for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
+      if (idx < B_G) {
+        const int gn = n0 + n, gk = kt * BKH + 8 * k8;
+        if (gn < N && gk < K) {
+          const __bf16* ptr = B + (long)gn * p.sbn + gk;
+          if (gk + 7 < K) {
+            v = *reinterpret_cast<const bf16x8*>(ptr);
+          } else {
+            for (int q = 0; q < 8; ++q)
+              if (gk + q < K) v[q] = ptr[q];
+          }
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int idx = tid + NT * i;
+      if (idx < A_G) *reinterpret_cast<bf16x8*>(&As[buf][(idx >> 2) * LDH + 8 * (idx & 3)]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int idx = tid + NT * i;
+      if (idx < B_G) *reinterpret_cast<bf16x8*>(&Bs[buf][(idx >> 2) * LDH + 8 * (idx & 3)]) = rb[i];
+    }
+  };
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = (K + BKH - 1) / BKH;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);
+#pragma unroll
+    for (int ks = 0; ks < BKH / 16; ++ks) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(
+            &As[cur][(wm * WTM + i * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(
+            &Bs[cur][(wn * WTN + j * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * WTN + j * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float bcol = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        float v = acc[i][j][r] * p.alpha + bcol;
+        float* dst = C + (long)row * p.ldc + col;
+        if constexpr (EPI == EPI_SWOOSHL) v = swooshl(v);
+        if constexpr (EPI == EPI_SWOOSHR) v = swooshr(v);
+        if constexpr (EPI == EPI_MULAUX) v *= aux[(long)row * p.ldaux + col];
+        if constexpr (EPI == EPI_RESADD) v += *dst;
+        *dst = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int ALOAD, int EPI>
+void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
+  dim3 grid(cdiv(p.N, BN), cdiv(p.max_M, BM), p.slices ? p.num_slices : 1);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, ALOAD, EPI>), grid, dim3(64 * WM * WN), 0,
+                     st, p, Bw);
+}
+
+template <int ALOAD, int EPI>
+void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
+  int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
+  int best = pad32;
+  int BN = (pad128 * 100 <= best * 115) ? 128 : (pad64 * 100 <= best * 115 ? 64 : 32);
+  long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
+  bool big = blocks128 >= 512;
+  if (BN == 128) {
+    if (big) launch_h<128, 128, 2, 2, ALOAD, EPI>(p, Bw, st);
+    else launch_h<64, 128, 2, 2, ALOAD, EPI>(p, Bw, st);
+  } else if (BN == 64) {
+    if (big) launch_h<128, 64, 2, 2, ALOAD, EPI>(p, Bw, st);
+    else launch_h<64, 64, 2, 2, ALOAD, EPI>(p, Bw, st);
+  } else {
+    if (big) launch_h<128, 32, 4, 1, ALOAD, EPI>(p, Bw, st);
+    else launch_h<64, 32, 2, 1, ALOAD, EPI>(p, Bw, st);
+  }
+}
+
 }  // namespace
 
 void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream_t st) {
@@ -296,4 +484,39 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
   throw std::runtime_error("gemm_f32: unsupported (aload, epi, layout) combination");
 }
 
+}  // namespace zasr
+
+namespace zasr {
+void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t st) {
+  ZASR_REQUIRE(p.N > 0, "gemm: N must be positive");
+  if (p.max_M <= 0) return;
+  const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
+  if (aload == ALOAD_DENSE) {
+    switch (epi) {
+      case EPI_NONE: return launch_tile_h<ALOAD_DENSE, EPI_NONE>(p, B, st);
+      case EPI_SWOOSHL: return launch_tile_h<ALOAD_DENSE, EPI_SWOOSHL>(p, B, st);
+      case EPI_SWOOSHR: return launch_tile_h<ALOAD_DENSE, EPI_SWOOSHR>(p, B, st);
+      case EPI_RESADD: return launch_tile_h<ALOAD_DENSE, EPI_RESADD>(p, B, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
+    return launch_tile_h<ALOAD_CONV2, EPI_SWOOSHR>(p, B, st);
+  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR) {
+    return launch_tile_h<ALOAD_CONV3, EPI_SWOOSHR>(p, B, st);
+  }
+  throw std::runtime_error("gemm_bf16: unsupported (aload, epi) combination");
+}
+}  // namespace zasr
+
+namespace zasr {
+__global__ void f32_to_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ dst,
+                                   long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (__bf16)src[i];
+}
+void convert_to_bf16(const float* src, void* dst, long n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
+                     reinterpret_cast<__bf16*>(dst), n);
+}
 }  // namespace zasr

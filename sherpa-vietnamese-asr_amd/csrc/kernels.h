@@ -39,9 +39,10 @@ void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_sc
 void launch_bypass(float* x, const float* orig, const float* s, long rows, int d, hipStream_t st);
 // g[r][c] = x2[r][c] * sigmoid(x2[r][d + c])
 void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st);
-// out[t][c] = SwooshR(b[c] + sum_k w[c][k] x[t + k - K/2][c]), zero padding per sequence
-void launch_dwconv1d(const float* x, const int* off, int nseq, int total_rows, int d, int K,
-                     const float* w, const float* b, float* out, hipStream_t st);
+// g = x2[:, :d] * sigmoid(x2[:, d:]);  out[t][c] = SwooshR(b[c] + sum_k w[c][k] g[t+k-K/2][c]),
+// zero padding per sequence
+void launch_glu_dwconv1d(const float* x2, const int* off, int nseq, int total_rows, int d, int K,
+                         const float* w, const float* b, float* out, hipStream_t st);
 // t1[r][c] = tanh(h3[r][c]) * h3[r][hid + c]
 void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStream_t st);
 // SimpleDownsample: out[t'] = sum_u w[u] x[min(ds t' + u, L - 1)]
@@ -100,10 +101,32 @@ struct HotwordTables {
   const double* delta;  // [states][cls]
   const double* node_score;  // [states]
 };
+struct DecoderW {
+  const float* tap0;  // [V][D] grouped-conv tap 0 applied to each embedding row
+  const float* tap1;  // [V][D] tap 1
+  const float* bp;    // decoder_proj bias [D]
+  int D;
+};
+struct DecJoinArgs {
+  DecoderW dw;
+  const float* wp;       // decoder_proj weight [D][D] (K contiguous)
+  const int* y1;         // [S*H] slot contexts
+  const int* y2;
+  const float* enc;      // [sum T'][D]
+  const int* enc_off;    // [S]
+  float* J;              // [M][D] = tanh(enc[s, t] + dec[slot])
+  int M, H, t;
+};
+struct JoinerArgs {
+  const float* J;        // [M][D]
+  const float* W;        // [V][D]
+  const float* bias;     // [V]
+  float* out;            // [M][V]
+  int M, V, D;
+};
 void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st);
-// relu(grouped conv over (E[y2], E[y1])) for every hypothesis slot -> [S*Hmax][D]
-void launch_decoder_prep(const SearchState& s, int rows, const float* emb, const float* conv_w,
-                         int D, float* out, hipStream_t st);
+void launch_decjoin(const DecJoinArgs& a, hipStream_t st);
+void launch_joiner(const JoinerArgs& j, hipStream_t st);
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
                         int beam, int t, const int* enc_len, const HotwordTables& hw,
                         hipStream_t st);

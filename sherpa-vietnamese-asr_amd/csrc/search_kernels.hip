@@ -1,22 +1,27 @@
 // Transducer search on device: modified beam search (greedy = beam 1) with Aho-Corasick
 // hotword biasing, restating core/asr_engine.py:1023-1153 and core/hotword_context.py.
 //
-// Per frame t (host loop):   decoder_prep -> decoder_proj GEMM -> joiner GEMM -> search_step
-//
-// search_step: one 256-thread block per stream.
-//   1. per live hypothesis row (wave-parallel): max, second max, sum exp, entropy terms
-//      (the reference's f32 numpy log-softmax :1096-1098 and _compute_token_entropy :1159)
-//   2. candidates lp = ((logit - max) - log(sum)) + float(score_h)   (f32, :1098-1100)
-//      global top-k over H*V: per-thread sorted lists -> per-wave merge -> block merge
-//   3. thread 0 expands the k candidates in descending order: blank keeps the sequence,
-//      non-blank appends (hotword delta after top-k, :1127-1131); duplicates of the full
-//      token sequence (identified by (length, 64-bit rolling hash)) merge with an f64
-//      log-add (:1133-1138); emissions append a node {token, frame, parent, token logp,
-//      row stats} so the winning sequence is recovered at the end by backtracking.
+// Per frame t, three launches:
+//   decjoin_kernel     J[slot] = tanh(enc[s, t] + decoder(y[-2], y[-1]))  -- Embedding ->
+//                      grouped Conv1d -> ReLU -> decoder_proj (MFMA), the reference's
+//                      dec_sess/dec_cache (:1072-1088) recomputed per live slot
+//   joiner_kernel      logits[S*H, V] = W_out J + b                           (:1090-1093)
+//   search_step_kernel one block per stream:
+//     1. per live hypothesis row: max, second max, sum exp, entropy terms (the reference's
+//        f32 numpy log-softmax :1096-1098 and _compute_token_entropy :1159-1181)
+//     2. candidates lp = ((logit - max) - log(sum)) + score_h (f32 add of the Python-float
+//        score, or the f64 add of an np.float64 score, :1099-1100); global top-k over H*V
+//     3. expansion in descending order (:1110-1138): blank keeps the sequence, non-blank
+//        appends, hotword delta after top-k (:1127-1131), duplicates of the full token
+//        sequence (identified by (length, 64-bit rolling hash)) merge with an f64 log-add;
+//        emissions append a node {token, frame, parent, token logp, row stats}
+// All hypothesis state lives in LDS during the step; global memory is written once.
 #include "common.h"
 #include "kernels.h"
 
 namespace zasr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -34,7 +39,7 @@ __device__ __forceinline__ unsigned long long hash_push(unsigned long long h, in
   return x;
 }
 
-// returns the f64 log-add; *f64 = 1 when the reference's result type is np.float64
+// f64 log-add; *f64 = 1 when the reference's result type is np.float64 (non-cutoff branch)
 __device__ __forceinline__ double log_add(double a, int fa, double b, int fb, int* f64) {
   if (a < b) {
     double t = a;
@@ -58,8 +63,58 @@ __device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) {
   return v1 > v2 || (v1 == v2 && i1 < i2);
 }
 
+// relu(grouped conv(E[y2], E[y1])) for 4 channels c..c+3: the conv is linear per tap, so
+// tap0[v] = W[:, :, 0] * E[v] and tap1[v] = W[:, :, 1] * E[v] are tabulated at load time
+// (Conv1d(D, D, k=2, groups=D/4, bias=False); tap 0 = older token y[-2], tap 1 = y[-1])
+__device__ __forceinline__ float4 dec_conv4(const DecoderW& dw, int y2, int y1, int c) {
+  const float4 a = *reinterpret_cast<const float4*>(dw.tap0 + (long)y2 * dw.D + c);
+  const float4 b = *reinterpret_cast<const float4*>(dw.tap1 + (long)y1 * dw.D + c);
+  return make_float4(fmaxf(a.x + b.x, 0.f), fmaxf(a.y + b.y, 0.f), fmaxf(a.z + b.z, 0.f),
+                     fmaxf(a.w + b.w, 0.f));
+}
+
+// acc += A[32 rows][k in this wave's range] * B[32 cols][k]^T with f32 MFMA 32x32x2.
+// A in LDS ([32][lda]), B = one weight row per lane column (K contiguous), read as float4:
+// lane half h covers k = kb + 4h + j (j = 0..3).  All of the wave's B loads are issued
+// before the MFMAs (kw <= 128, i.e. D <= 512).
+template <int NQ>  // NQ = (k per wave) / 8 = D / 32
+__device__ __forceinline__ void tile32_splitk(const float* As, int lda, const float* brow,
+                                              bool bvalid, int kbeg, f32x16& acc) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 31, h = lane >> 5;
+  float4 b[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    b[q] = bvalid ? *reinterpret_cast<const float4*>(brow + kbeg + 8 * q + 4 * h)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const float4 a = *reinterpret_cast<const float4*>(As + col * lda + kbeg + 8 * q + 4 * h);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[q].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[q].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[q].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[q].w, acc, 0, 0, 0);
+  }
+}
+
+// waves 1..3 hand their partial tiles to wave 0 through LDS (red: [3][16][64])
+__device__ __forceinline__ void splitk_reduce(f32x16& acc, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (wid > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[((wid - 1) * 16 + r) * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      acc[r] += red[r * 64 + lane] + red[(16 + r) * 64 + lane] + red[(32 + r) * 64 + lane];
+  }
+}
+
 }  // namespace
 
+// --------------------------------------------------------------------------------------
 __global__ void search_init_kernel(SearchState s, int S, int Hmax) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S * Hmax) return;
@@ -84,34 +139,113 @@ void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st) {
   hipLaunchKernelGGL(search_init_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, s, S, Hmax);
 }
 
-// decoder: relu(Conv1d(D, D, k=2, groups=D/4, no bias)(E[y2], E[y1])) per slot
-__global__ void decoder_prep_kernel(const int* __restrict__ y1, const int* __restrict__ y2,
-                                    int rows, const float* __restrict__ emb,
-                                    const float* __restrict__ conv_w, int D,
-                                    float* __restrict__ out) {
-  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)rows * D) return;
-  int r = (int)(e / D), c = (int)(e - (long)r * D);
-  const float* ea = emb + (long)y2[r] * D + (c & ~3);  // tap 0: older token
-  const float* eb = emb + (long)y1[r] * D + (c & ~3);  // tap 1: newer token
-  const float* w = conv_w + (long)c * 8;                // [ci][tap]
-  float acc = 0.f;
-#pragma unroll
-  for (int ci = 0; ci < 4; ++ci) {
-    acc = fmaf(w[ci * 2 + 0], ea[ci], acc);
-    acc = fmaf(w[ci * 2 + 1], eb[ci], acc);
+// --------------------------------------------------------------------------------------
+// decoder + joiner input: block = 32 slots x 32 decoder channels, 4 waves split K.
+// --------------------------------------------------------------------------------------
+template <int NQ>
+__global__ __launch_bounds__(256) void decjoin_kernel(DecJoinArgs a) {
+  extern __shared__ float smem[];
+  const int D = a.dw.D;
+  const int lda = D + 4;
+  float* As = smem;                // relu(conv(E[y2], E[y1])) rows  [32][D + 4]
+  float* red = smem + 32 * lda;    // [3][16][64]
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int d4 = D / 4;
+  for (int e = tid; e < 32 * d4; e += 256) {
+    const int i = e / d4, c4 = e - i * d4;
+    const int r = m0 + i;
+    const float4 v = (r < a.M) ? dec_conv4(a.dw, a.y2[r], a.y1[r], 4 * c4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(As + i * lda + 4 * c4) = v;
   }
-  out[e] = fmaxf(acc, 0.f);
+  __syncthreads();
+  const int n = n0 + (lane & 31);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  tile32_splitk<NQ>(As, lda, a.wp + (long)n * D, true, wid * (D / 4), acc);
+  splitk_reduce(acc, red);
+  if (wid == 0) {
+    const float bp = a.dw.bp[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row >= a.M) continue;
+      const int s = row / a.H;
+      const float e = a.enc[(long)(a.enc_off[s] + a.t) * D + n];
+      a.J[(long)row * D + n] = tanhf(e + (acc[r] + bp));
+    }
+  }
 }
 
-void launch_decoder_prep(const SearchState& s, int rows, const float* emb, const float* conv_w,
-                         int D, float* out, hipStream_t st) {
-  long n = (long)rows * D;
-  if (n <= 0) return;
-  hipLaunchKernelGGL(decoder_prep_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, s.y1, s.y2,
-                     rows, emb, conv_w, D, out);
+void launch_decjoin(const DecJoinArgs& a, hipStream_t st) {
+  if (a.M <= 0) return;
+  ZASR_REQUIRE(a.dw.D % 32 == 0 && a.dw.D <= 512, "decoder/joiner dim must be a multiple of 32, <= 512");
+  dim3 grid(a.dw.D / 32, cdiv(a.M, 32));
+  size_t lds = (32 * (a.dw.D + 4) + 3 * 16 * 64) * sizeof(float);
+  switch (a.dw.D / 32) {
+    case 2: hipLaunchKernelGGL(decjoin_kernel<2>, grid, dim3(256), lds, st, a); break;
+    case 4: hipLaunchKernelGGL(decjoin_kernel<4>, grid, dim3(256), lds, st, a); break;
+    case 8: hipLaunchKernelGGL(decjoin_kernel<8>, grid, dim3(256), lds, st, a); break;
+    case 16: hipLaunchKernelGGL(decjoin_kernel<16>, grid, dim3(256), lds, st, a); break;
+    default: throw std::runtime_error("decoder dim must be 64, 128, 256 or 512");
+  }
 }
 
+// --------------------------------------------------------------------------------------
+// joiner: logits = W_out J + b; block = 32 rows x 32 vocab columns, 4 waves split K.
+// --------------------------------------------------------------------------------------
+template <int NQ>
+__global__ __launch_bounds__(256) void joiner_kernel(JoinerArgs j) {
+  extern __shared__ float smem[];
+  const int D = j.D;
+  const int lda = D + 4;
+  float* As = smem;
+  float* red = smem + 32 * lda;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int d4 = D / 4;
+  for (int e = tid; e < 32 * d4; e += 256) {
+    const int i = e / d4, k4 = e - i * d4;
+    const int r = m0 + i;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < j.M) v = reinterpret_cast<const float4*>(j.J + (long)r * D)[k4];
+    *reinterpret_cast<float4*>(As + i * lda + 4 * k4) = v;
+  }
+  __syncthreads();
+  const int n = n0 + (lane & 31);
+  const bool nv = n < j.V;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  tile32_splitk<NQ>(As, lda, j.W + (long)(nv ? n : 0) * D, nv, wid * (D / 4), acc);
+  splitk_reduce(acc, red);
+  if (wid == 0 && nv) {
+    const float bias = j.bias[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < j.M) j.out[(long)row * j.V + n] = acc[r] + bias;
+    }
+  }
+}
+
+void launch_joiner(const JoinerArgs& j, hipStream_t st) {
+  if (j.M <= 0) return;
+  ZASR_REQUIRE(j.D % 32 == 0 && j.D <= 512, "joiner_dim must be a multiple of 32, <= 512");
+  dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
+  size_t lds = (32 * (j.D + 4) + 3 * 16 * 64) * sizeof(float);
+  switch (j.D / 32) {
+    case 2: hipLaunchKernelGGL(joiner_kernel<2>, grid, dim3(256), lds, st, j); break;
+    case 4: hipLaunchKernelGGL(joiner_kernel<4>, grid, dim3(256), lds, st, j); break;
+    case 8: hipLaunchKernelGGL(joiner_kernel<8>, grid, dim3(256), lds, st, j); break;
+    case 16: hipLaunchKernelGGL(joiner_kernel<16>, grid, dim3(256), lds, st, j); break;
+    default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
+  }
+}
+
+// --------------------------------------------------------------------------------------
 template <int KB>
 __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const float* logits,
                                                           int V, int Hmax, int beam, int t,
@@ -123,32 +257,61 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   const int wid = tid >> 6;
   const int base = s * Hmax;
 
-  __shared__ float sMax[kMaxBeam], sLogSum[kMaxBeam], sScore[kMaxBeam];
-  __shared__ double sScoreD[kMaxBeam];
-  __shared__ int sScoreF[kMaxBeam];
+  // previous hypotheses
+  __shared__ double pLp[kMaxBeam];
+  __shared__ int pLpf[kMaxBeam], pLen[kMaxBeam], pY1[kMaxBeam], pY2[kMaxBeam], pHw[kMaxBeam],
+      pNode[kMaxBeam];
+  __shared__ unsigned long long pHash[kMaxBeam];
+  // new hypotheses
+  __shared__ double nLp[kMaxBeam];
+  __shared__ int nLpf[kMaxBeam], nLen[kMaxBeam], nY1[kMaxBeam], nY2[kMaxBeam], nHw[kMaxBeam],
+      nNode[kMaxBeam];
+  __shared__ unsigned long long nHash[kMaxBeam];
+  // row statistics
+  __shared__ float sMax[kMaxBeam], sLogSum[kMaxBeam];
   __shared__ float4 sStats[kMaxBeam];
+  __shared__ float rA[4], rB[4];
   __shared__ float cV[4 * KB];
   __shared__ int cI[4 * KB];
-  __shared__ int sN;
+  __shared__ int sN, sNN, sNodeCnt;
 
-  if (tid == 0) sN = st.nh[s];
+  if (tid == 0) {
+    sN = st.nh[s];
+    sNodeCnt = st.node_count[s];
+  }
   __syncthreads();
   const int n = sN;
+  if (tid < n) {
+    pLp[tid] = st.lp[base + tid];
+    pLpf[tid] = st.lpf[base + tid];
+    pHash[tid] = st.hash[base + tid];
+    pLen[tid] = st.len[base + tid];
+    pY1[tid] = st.y1[base + tid];
+    pY2[tid] = st.y2[base + tid];
+    pHw[tid] = st.hw[base + tid];
+    pNode[tid] = st.node[base + tid];
+  }
   const float* rows = logits + (long)base * V;
 
-  // ---- 1. per-hypothesis row statistics ----
-  for (int h = wid; h < n; h += 4) {
-    const float* row = rows + (long)h * V;
+  // ---- 1. row statistics: g waves per row (g = 4 for a single hypothesis) ----
+  const int g = n >= 4 ? 1 : (n == 1 ? 4 : 2);
+  for (int h0 = 0; h0 < n; h0 += 4 / g) {
+    const int h = h0 + wid / g;
+    const int part = wid % g;
+    const bool live = h < n;
+    const float* row = rows + (long)(live ? h : 0) * V;
+    const int stride = 64 * g, start = part * 64 + lane;
     float m1 = -INFINITY, m2 = -INFINITY;
-    for (int v = lane; v < V; v += 64) {
-      float x = row[v];
-      if (x > m1) {
-        m2 = m1;
-        m1 = x;
-      } else if (x > m2) {
-        m2 = x;
+    if (live)
+      for (int v = start; v < V; v += stride) {
+        float x = row[v];
+        if (x > m1) {
+          m2 = m1;
+          m1 = x;
+        } else if (x > m2) {
+          m2 = x;
+        }
       }
-    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
@@ -157,23 +320,87 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       m1 = hi;
       m2 = lo;
     }
+    if (g > 1) {
+      if (lane == 0) {
+        rA[wid] = m1;
+        rB[wid] = m2;
+      }
+      __syncthreads();
+      const int w0 = (wid / g) * g;
+      for (int q = 0; q < g; ++q) {
+        const int w = w0 + q;
+        if (w == wid) continue;
+        float a1 = rA[w], a2 = rB[w];
+        float hi = fmaxf(m1, a1);
+        float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
+        m1 = hi;
+        m2 = lo;
+      }
+      __syncthreads();
+    }
+    // cache e = exp(x - max) per lane (up to 32 elements; longer rows recompute)
+    constexpr int kCache = 32;
+    float ev[kCache];
+    const bool cached = (V + stride - 1) / stride <= kCache;
     float se = 0.f;
-    for (int v = lane; v < V; v += 64) se += expf(row[v] - m1);
+    if (live) {
+      if (cached) {
+#pragma unroll
+        for (int q = 0; q < kCache; ++q) {
+          const int v = start + q * stride;
+          ev[q] = (v < V) ? expf(row[v] - m1) : 0.f;
+          se += ev[q];
+        }
+      } else {
+        for (int v = start; v < V; v += stride) se += expf(row[v] - m1);
+      }
+    }
     se = wave_sum(se);
+    if (g > 1) {
+      if (lane == 0) rA[wid] = se;
+      __syncthreads();
+      const int w0 = (wid / g) * g;
+      se = 0.f;
+      for (int q = 0; q < g; ++q) se += rA[w0 + q];
+      __syncthreads();
+    }
     float ent = 0.f, s3 = 0.f;
-    for (int v = lane; v < V; v += 64) {
-      float p = expf(row[v] - m1) / se;
-      ent += p * logf(p + 1e-30f);
-      s3 += powf(p, 1.0f / 3.0f);
+    if (live) {
+      if (cached) {
+#pragma unroll
+        for (int q = 0; q < kCache; ++q) {
+          if (start + q * stride >= V) break;
+          const float p = ev[q] / se;
+          ent += p * logf(p + 1e-30f);
+          s3 += powf(p, 1.0f / 3.0f);
+        }
+      } else {
+        for (int v = start; v < V; v += stride) {
+          const float p = expf(row[v] - m1) / se;
+          ent += p * logf(p + 1e-30f);
+          s3 += powf(p, 1.0f / 3.0f);
+        }
+      }
     }
     ent = wave_sum(ent);
     s3 = wave_sum(s3);
-    if (lane == 0) {
+    if (g > 1) {
+      if (lane == 0) {
+        rA[wid] = ent;
+        rB[wid] = s3;
+      }
+      __syncthreads();
+      const int w0 = (wid / g) * g;
+      ent = s3 = 0.f;
+      for (int q = 0; q < g; ++q) {
+        ent += rA[w0 + q];
+        s3 += rB[w0 + q];
+      }
+      __syncthreads();
+    }
+    if (live && part == 0 && lane == 0) {
       sMax[h] = m1;
       sLogSum[h] = logf(se);
-      sScore[h] = (float)st.lp[base + h];
-      sScoreD[h] = st.lp[base + h];
-      sScoreF[h] = st.lpf[base + h];
       sStats[h] = make_float4(-ent, s3, 1.0f / se, expf(m2 - m1) / se);
     }
   }
@@ -188,12 +415,16 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     ti[q] = 0x7fffffff;
   }
   const int total = n * V;
-  for (int idx = tid; idx < total; idx += 256) {
-    const int h = idx / V;
-    const float x = rows[idx];
-    const float lpv = (x - sMax[h]) - sLogSum[h];
-    // reference: f32 `lp[i, :] += score` (Python float) or f64 add rounded (np.float64)
-    const float val = sScoreF[h] ? (float)((double)lpv + sScoreD[h]) : lpv + sScore[h];
+  for (int h = 0; h < n; ++h) {
+    const float mh = sMax[h], lsh = sLogSum[h];
+    const double ld = pLp[h];
+    const float lf = (float)ld;
+    const bool f64 = pLpf[h] != 0;
+    const float* row = rows + (long)h * V;
+    for (int v = tid; v < V; v += 256) {
+    const int idx = h * V + v;
+    const float lpv = (row[v] - mh) - lsh;
+    const float val = f64 ? (float)((double)lpv + ld) : lpv + lf;
     if (!better(val, idx, tv[KB - 1], ti[KB - 1])) continue;
 #pragma unroll
     for (int q = KB - 1; q >= 0; --q) {
@@ -207,8 +438,8 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
         ti[q] = idx;
       }
     }
+    }
   }
-  // per-wave merge: KB rounds of wave argmax over the lanes' list heads
   for (int round = 0; round < KB; ++round) {
     float bv = tv[0];
     int bi = ti[0];
@@ -225,7 +456,7 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       cV[wid * KB + round] = bv;
       cI[wid * KB + round] = bi;
     }
-    if (ti[0] == bi && bi != 0x7fffffff) {  // pop the winner's head (indices are unique)
+    if (ti[0] == bi && bi != 0x7fffffff) {
 #pragma unroll
       for (int q = 0; q < KB - 1; ++q) {
         tv[q] = tv[q + 1];
@@ -237,26 +468,12 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   }
   __syncthreads();
 
-  // ---- 3. expansion, hotwords, dedup (serial, <= beam candidates) ----
+  // ---- 3. expansion, hotwords, dedup (serial over <= beam candidates, all in LDS) ----
   if (tid == 0) {
     const int k = beam < total ? beam : total;
     int ptr[4] = {0, 0, 0, 0};
-    // copy previous hypotheses (read before overwrite)
-    double plp[kMaxBeam];
-    unsigned long long phash[kMaxBeam];
-    int plen[kMaxBeam], py1[kMaxBeam], py2[kMaxBeam], phw[kMaxBeam], pnode[kMaxBeam];
-    for (int h = 0; h < n; ++h) {
-      plp[h] = st.lp[base + h];
-      py2[h] = st.y2[base + h];
-      phash[h] = st.hash[base + h];
-      plen[h] = st.len[base + h];
-      py1[h] = st.y1[base + h];
-      phw[h] = st.hw[base + h];
-      pnode[h] = st.node[base + h];
-    }
     int nn = 0;
     for (int c = 0; c < k; ++c) {
-      // next best among the 4 wave lists
       int bw = -1;
       for (int w = 0; w < 4; ++w) {
         if (ptr[w] >= KB) continue;
@@ -271,18 +488,13 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       const int hi = idx / V, tok = idx - hi * V;
       double score = (double)val;
       unsigned long long key;
-      int klen, ny1, ny2, nhw, nnode = -1;
-      double tok_lp = 0.0;
+      int klen, ny1, ny2, nhw = pHw[hi];
       if (tok == 0) {
-        key = phash[hi];
-        klen = plen[hi];
-        ny1 = py1[hi];
-        ny2 = py2[hi];
-        nhw = phw[hi];
-        nnode = pnode[hi];
+        key = pHash[hi];
+        klen = pLen[hi];
+        ny1 = pY1[hi];
+        ny2 = pY2[hi];
       } else {
-        tok_lp = (double)val - plp[hi];
-        nhw = phw[hi];
         if (hw.num_states > 0 && tok != 2) {
           const int cls = hw.tok2cls[tok];
           if (cls < 0) {
@@ -294,45 +506,61 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
             nhw = hw.next[e];
           }
         }
-        key = hash_push(phash[hi], tok);
-        klen = plen[hi] + 1;
-        ny2 = py1[hi];
+        key = hash_push(pHash[hi], tok);
+        klen = pLen[hi] + 1;
+        ny2 = pY1[hi];
         ny1 = tok;
       }
       int found = -1;
-      for (int j = 0; j < nn; ++j)
-        if (st.len[base + j] == klen && st.hash[base + j] == key) {
-          found = j;
+      for (int q = 0; q < nn; ++q)
+        if (nLen[q] == klen && nHash[q] == key) {
+          found = q;
           break;
         }
       if (found >= 0) {
         int f64 = 0;
-        st.lp[base + found] = log_add(st.lp[base + found], st.lpf[base + found], score, 0, &f64);
-        st.lpf[base + found] = f64;
+        nLp[found] = log_add(nLp[found], nLpf[found], score, 0, &f64);
+        nLpf[found] = f64;
         continue;
       }
+      int nnode = pNode[hi];
       if (tok != 0) {
-        const int nid = st.node_count[s]++;
-        const long g = (long)s * st.node_cap + nid;
-        st.node_tok[g] = tok;
-        st.node_frame[g] = t;
-        st.node_parent[g] = pnode[hi];
-        st.node_lp[g] = tok_lp;
-        st.node_stats[g] = sStats[hi];
+        const int nid = sNodeCnt++;
+        const long gi = (long)s * st.node_cap + nid;
+        st.node_tok[gi] = tok;
+        st.node_frame[gi] = t;
+        st.node_parent[gi] = pNode[hi];
+        st.node_lp[gi] = (double)val - pLp[hi];
+        st.node_stats[gi] = sStats[hi];
         nnode = nid;
       }
-      st.lp[base + nn] = score;
-      st.lpf[base + nn] = 0;
-      st.hash[base + nn] = key;
-      st.len[base + nn] = klen;
-      st.y1[base + nn] = ny1;
-      st.y2[base + nn] = ny2;
-      st.hw[base + nn] = nhw;
-      st.node[base + nn] = nnode;
+      nLp[nn] = score;
+      nLpf[nn] = 0;
+      nHash[nn] = key;
+      nLen[nn] = klen;
+      nY1[nn] = ny1;
+      nY2[nn] = ny2;
+      nHw[nn] = nhw;
+      nNode[nn] = nnode;
       ++nn;
     }
+    sNN = nn;
     st.nh[s] = nn;
+    st.node_count[s] = sNodeCnt;
   }
+  __syncthreads();
+  const int nn = sNN;
+  if (tid < nn) {
+    st.lp[base + tid] = nLp[tid];
+    st.lpf[base + tid] = nLpf[tid];
+    st.hash[base + tid] = nHash[tid];
+    st.len[base + tid] = nLen[tid];
+    st.y1[base + tid] = nY1[tid];
+    st.y2[base + tid] = nY2[tid];
+    st.hw[base + tid] = nHw[tid];
+    st.node[base + tid] = nNode[tid];
+  }
+
 }
 
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
@@ -341,20 +569,17 @@ void launch_search_step(const SearchState& s, const float* logits, int V, int S,
   if (S <= 0) return;
   ZASR_REQUIRE(beam >= 1 && beam <= kMaxBeam && beam <= Hmax, "beam out of range");
   dim3 grid(S), block(256);
-  if (beam == 1)
-    hipLaunchKernelGGL(search_step_kernel<1>, grid, block, 0, st, s, logits, V, Hmax, beam, t,
-                       enc_len, hw);
-  else if (beam <= 4)
-    hipLaunchKernelGGL(search_step_kernel<4>, grid, block, 0, st, s, logits, V, Hmax, beam, t,
-                       enc_len, hw);
-  else if (beam <= 8)
-    hipLaunchKernelGGL(search_step_kernel<8>, grid, block, 0, st, s, logits, V, Hmax, beam, t,
-                       enc_len, hw);
-  else
-    hipLaunchKernelGGL(search_step_kernel<16>, grid, block, 0, st, s, logits, V, Hmax, beam, t,
-                       enc_len, hw);
+#define ZASR_STEP(KBV)                                                                      \
+  hipLaunchKernelGGL(search_step_kernel<KBV>, grid, block, 0, st, s, logits, V, Hmax, beam, t, \
+                     enc_len, hw)
+  if (beam == 1) ZASR_STEP(1);
+  else if (beam <= 4) ZASR_STEP(4);
+  else if (beam <= 8) ZASR_STEP(8);
+  else ZASR_STEP(16);
+#undef ZASR_STEP
 }
 
+// --------------------------------------------------------------------------------------
 // finalize (:1142-1148), length-normalised pick (:1151), backtrack the emission chain
 __global__ void search_final_kernel(SearchState st, int S, int Hmax, HotwordTables hw,
                                     int out_cap, int* out_tok, int* out_frame, double* out_lp,

@@ -31,7 +31,8 @@ def case_config(kind: str) -> ZipformerConfig:
 def dec_joiner_weights(kind: str, seed: int) -> Dict[str, np.ndarray]:
     cfg = case_config(kind)
     # blank bias 1 nat below the model default: ~25-40% emission, exercises merges/hotwords
-    w = synth_weights(cfg, seed, blank_bias=0.5 * math.log(cfg.vocab_size))
+    w = synth_weights(cfg, seed, blank_bias=0.5 * math.log(cfg.vocab_size), dec_gain=1.0,
+                      blank_row_gain=1.0)
     keep = ("decoder.", "decoder_proj.", "joiner.")
     return {k: v for k, v in w.items() if k.startswith(keep)}
 

@@ -191,3 +191,42 @@ def test_empty_and_short_chunks(tiny):
     assert res[0].T == 0 and res[0].token_ids.size == 0
     assert res[1].T == 0 and res[1].token_ids.size == 0
     assert res[2].T > 0
+
+
+# ------------------------------------------------------------------ bf16 precision mode
+def _token_agreement(a, b):
+    import difflib
+    sm = difflib.SequenceMatcher(a=a, b=b, autojunk=False)
+    return sum(bl.size for bl in sm.get_matching_blocks()) / max(1, max(len(a), len(b)))
+
+
+def test_bf16_mode_encoder_and_tokens(need_gpu):
+    """bf16 mode (bf16 GEMM operands, f32 accumulate/softmax/norms/search) vs the fp32 oracle:
+    encoder_out within 0.15 * max(1, |oracle|) and token agreement >= 0.9 (written to
+    gpurun_out/bf16_report.json as the measured mismatch rate)."""
+    from model_fixtures import m_model
+    from oracle.fbank import fbank
+    from oracle.zipformer import ZipformerOracle
+    from zasr.binding import Recognizer
+    cfg, w, path = m_model()
+    r32 = Recognizer(path, "greedy_search", 1, precision="fp32")
+    r16 = Recognizer(path, "greedy_search", 1, precision="bf16")
+    chunks = [_speech(s, 300 + i) for i, s in enumerate((20.0, 30.0, 12.5, 33.0))]
+    feats = [fbank(c) for c in chunks]
+    e16 = r16.encode_features(feats)
+    orc = ZipformerOracle(cfg, w)
+    errs = []
+    for f, g in zip(feats[:2], e16[:2]):
+        ref = orc.encoder(f)
+        errs.append(float(np.max(np.abs(g - ref) / np.maximum(1.0, np.abs(ref)))))
+    a32 = r32.decode(chunks)
+    a16 = r16.decode(chunks)
+    agree = [_token_agreement(x.token_ids.tolist(), y.token_ids.tolist()) for x, y in zip(a32, a16)]
+    ntok = [int(x.token_ids.size) for x in a32]
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/bf16_report.json", "w") as fh:
+        json.dump({"encoder_max_scaled_err": errs, "token_agreement": agree, "fp32_tokens": ntok}, fh)
+    assert max(errs) <= 0.15, errs
+    assert min(agree) >= 0.9 or sum(ntok) < 5, agree
+    r32.close()
+    r16.close()
