@@ -19,6 +19,19 @@ __device__ __forceinline__ int find_seq(const int* off, int nseq, int r) {
   return lo;
 }
 
+// row -> sequence map of one time resolution (built once per batch)
+__global__ void row2seq_kernel(const int* __restrict__ off, int nseq, int total,
+                               int* __restrict__ map) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < total) map[r] = find_seq(off, nseq, r);
+}
+
+void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t st) {
+  if (total <= 0) return;
+  hipLaunchKernelGGL(row2seq_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, off, nseq, total,
+                     map);
+}
+
 // =====================================================================================
 // fbank: one wave per frame.  Samples gathered with kaldi edge reflection, DC removal,
 // pre-emphasis and povey window in f32, 512-point FFT in f64 (knf's rdft runs in double),
@@ -124,13 +137,14 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
 // conv.0: Conv2d(1 -> 8, 3x3, padding (0, 1)) + SwooshR.  One thread per (t, f).
 // =====================================================================================
 __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict__ fb_off,
-                             const int* __restrict__ c1_off, int nseq, int total,
+                             const int* __restrict__ c1_off, const int* __restrict__ c1_map,
+                             int total,
                              const float* __restrict__ w, const float* __restrict__ bias,
                              float* __restrict__ out) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total * 80) return;
   int row = e / 80, f = e - row * 80;
-  int b = find_seq(c1_off, nseq, row);
+  int b = c1_map[row];
   int t = row - c1_off[b];
   const float* src = fb + (long)(fb_off[b] + t) * 80;
   float xin[9];
@@ -157,12 +171,12 @@ __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict
   dst[1] = o1;
 }
 
-void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, int nseq, int total_rows,
-                  const float* w, const float* b, float* out, hipStream_t st) {
+void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const int* c1_map,
+                  int total_rows, const float* w, const float* b, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
   long n = (long)total_rows * 80;
   hipLaunchKernelGGL(conv1_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off, c1_off,
-                     nseq, total_rows, w, b, out);
+                     c1_map, total_rows, w, b, out);
 }
 
 // =====================================================================================
@@ -173,14 +187,24 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, int nse
 constexpr int kDw2T = 16;
 
 __global__ __launch_bounds__(256) void dwconv2d_kernel(const float* __restrict__ x,
-                                                       const int* __restrict__ L_off, int nseq,
+                                                       const int* __restrict__ L_off,
+                                                       const int* __restrict__ L_map,
                                                        int total_rows, const float* __restrict__ w,
                                                        const float* __restrict__ bias,
                                                        float* __restrict__ out) {
   __shared__ float tile[(kDw2T + 6) * 19 * 32];
+  __shared__ int sLo[kDw2T], sHi[kDw2T];
   const int r0 = blockIdx.x * kDw2T;
   const int c0 = blockIdx.y * 32;
   const int tid = threadIdx.x;
+  if (tid < kDw2T) {
+    const int r = r0 + tid;
+    if (r < total_rows) {
+      const int b = L_map[r];
+      sLo[tid] = L_off[b] - r;
+      sHi[tid] = L_off[b + 1] - 1 - r;
+    }
+  }
   // stage rows r0-3 .. r0+kDw2T+2 (packed), channels c0..c0+31
   for (int e = tid; e < (kDw2T + 6) * 19 * 8; e += 256) {
     const int c4 = e & 7;
@@ -202,8 +226,7 @@ __global__ __launch_bounds__(256) void dwconv2d_kernel(const float* __restrict__
     const int tr = p / 19, f = p - tr * 19;
     const int r = r0 + tr;
     if (r >= total_rows) break;
-    const int b = find_seq(L_off, nseq, r);
-    const int lo = L_off[b] - r, hi = L_off[b + 1] - 1 - r;  // allowed time offsets
+    const int lo = sLo[tr], hi = sHi[tr];  // allowed time offsets
     float acc = bc;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
@@ -220,11 +243,11 @@ __global__ __launch_bounds__(256) void dwconv2d_kernel(const float* __restrict__
   }
 }
 
-void launch_dwconv2d(const float* x, const int* L_off, int nseq, int total_rows, const float* w,
-                     const float* b, float* out, hipStream_t st) {
+void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
+                     const float* w, const float* b, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
   dim3 grid(cdiv(total_rows, kDw2T), 4);
-  hipLaunchKernelGGL(dwconv2d_kernel, grid, dim3(256), 0, st, x, L_off, nseq, total_rows, w, b,
+  hipLaunchKernelGGL(dwconv2d_kernel, grid, dim3(256), 0, st, x, L_off, L_map, total_rows, w, b,
                      out);
 }
 
@@ -343,14 +366,24 @@ void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStrea
 constexpr int kDw1T = 64;
 
 __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
-    const float* __restrict__ x2, const int* __restrict__ off, int nseq, int total_rows, int d,
-    int K, const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out) {
+    const float* __restrict__ x2, const int* __restrict__ off, const int* __restrict__ map,
+    int total_rows, int d, int K, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out) {
   extern __shared__ float tile[];  // [(kDw1T + K - 1)][64]
+  __shared__ int sLo[kDw1T], sHi[kDw1T];
   const int half = K >> 1;
   const int r0 = blockIdx.x * kDw1T;
   const int c0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
   const int nrows = kDw1T + K - 1;
+  if (tid < kDw1T) {
+    const int r = r0 + tid;
+    if (r < total_rows) {
+      const int b = map[r];
+      sLo[tid] = off[b] - r;
+      sHi[tid] = off[b + 1] - 1 - r;
+    }
+  }
   for (int e = tid; e < nrows * 16; e += 256) {
     const int c4 = e & 15, rr = e >> 4;
     const int r = r0 - half + rr;
@@ -373,8 +406,7 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
   for (int tr = tid >> 6; tr < kDw1T; tr += 4) {
     const int r = r0 + tr;
     if (r >= total_rows) break;
-    const int b = find_seq(off, nseq, r);
-    const int lo = off[b] - r, hi = off[b + 1] - 1 - r;
+    const int lo = sLo[tr], hi = sHi[tr];
     float acc = bc;
 #pragma unroll
     for (int k = 0; k < 31; ++k) {
@@ -386,13 +418,13 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
   }
 }
 
-void launch_glu_dwconv1d(const float* x2, const int* off, int nseq, int total_rows, int d, int K,
-                         const float* w, const float* b, float* out, hipStream_t st) {
+void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
+                         int K, const float* w, const float* b, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
   ZASR_REQUIRE(K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
   dim3 grid(cdiv(total_rows, kDw1T), cdiv(d, 64));
   size_t lds = (size_t)(kDw1T + K - 1) * 64 * sizeof(float);
-  hipLaunchKernelGGL(glu_dwconv1d_kernel, grid, dim3(256), lds, st, x2, off, nseq, total_rows, d,
+  hipLaunchKernelGGL(glu_dwconv1d_kernel, grid, dim3(256), lds, st, x2, off, map, total_rows, d,
                      K, w, b, out);
 }
 
@@ -404,12 +436,13 @@ struct DsW {
 };
 
 __global__ void downsample_kernel(const float* __restrict__ x, const int* __restrict__ off_in,
-                                  const int* __restrict__ off_out, int nseq, int total_out,
+                                  const int* __restrict__ off_out, const int* __restrict__ map_out,
+                                  int total_out,
                                   int d, int ds, DsW wts, float* __restrict__ out) {
   long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long)total_out * d) return;
   int r = (int)(e / d), c = (int)(e - (long)r * d);
-  int b = find_seq(off_out, nseq, r);
+  int b = map_out[r];
   int tp = r - off_out[b];
   int base = off_in[b];
   int L = off_in[b + 1] - base;
@@ -422,7 +455,7 @@ __global__ void downsample_kernel(const float* __restrict__ x, const int* __rest
   out[e] = acc;
 }
 
-void launch_downsample(const float* x, const int* off_in, const int* off_out, int nseq,
+void launch_downsample(const float* x, const int* off_in, const int* off_out, const int* map_out,
                        int total_out, int d, int ds, const float* w_host8, float* out,
                        hipStream_t st) {
   long n = (long)total_out * d;
@@ -430,19 +463,20 @@ void launch_downsample(const float* x, const int* off_in, const int* off_out, in
   DsW w{};
   for (int i = 0; i < ds && i < 8; ++i) w.w[i] = w_host8[i];
   hipLaunchKernelGGL(downsample_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in,
-                     off_out, nseq, total_out, d, ds, w, out);
+                     off_out, map_out, total_out, d, ds, w, out);
 }
 
 __global__ void upsample_combine_kernel(const float* __restrict__ xd,
                                         const float* __restrict__ orig,
                                         const int* __restrict__ off_in,
-                                        const int* __restrict__ off_ds, int nseq,
-                                        int total_rows, int d, int ds,
+                                        const int* __restrict__ off_ds,
+                                        const int* __restrict__ map_in, int total_rows, int d,
+                                        int ds,
                                         const float* __restrict__ s, float* __restrict__ y) {
   long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long)total_rows * d) return;
   int r = (int)(e / d), c = (int)(e - (long)r * d);
-  int b = find_seq(off_in, nseq, r);
+  int b = map_in[r];
   int t = r - off_in[b];
   float up = xd[(long)(off_ds[b] + t / ds) * d + c];
   float o = orig[e];
@@ -450,12 +484,12 @@ __global__ void upsample_combine_kernel(const float* __restrict__ xd,
 }
 
 void launch_upsample_combine(const float* xd, const float* orig, const int* off_in,
-                             const int* off_ds, int nseq, int total_rows, int d, int ds,
+                             const int* off_ds, const int* map_in, int total_rows, int d, int ds,
                              const float* s, float* y, hipStream_t st) {
   long n = (long)total_rows * d;
   if (n <= 0) return;
   hipLaunchKernelGGL(upsample_combine_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig,
-                     off_in, off_ds, nseq, total_rows, d, ds, s, y);
+                     off_in, off_ds, map_in, total_rows, d, ds, s, y);
 }
 
 __global__ void copy_cols_kernel(const float* __restrict__ src, int lds, int c0,
@@ -613,8 +647,14 @@ __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
       if (sM[w][i] != -INFINITY) ss += sS[w][i] * expf(sM[w][i] - mm);
     fM[i] = mm;
     fInv[i] = 1.f / ss;
+    if (i0 + i < L) {
+      float* sp = a.stats + ((long)(r0 + i0 + i) * H + h) * 2;
+      sp[0] = mm;
+      sp[1] = 1.f / ss;
+    }
   }
   __syncthreads();
+  if (h >= a.write_heads) return;
   float* out = a.attn + a.a_off[b] + (long)h * L * lda;
   for (int kb = wid; kb < nkb; kb += 4) {
     f32x16 acc;
@@ -628,6 +668,132 @@ __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
       out[(long)(i0 + i) * lda + j] = expf(acc[r] - fM[i]) * fInv[i];
     }
   }
+}
+
+// =====================================================================================
+// Self-attention consumer fused with the score recompute (flash style, no materialised
+// weights): per (sequence, 32 queries, head), waves stride over 32-key blocks:
+//   S^T = K Q^T (f32 MFMA 32x32x2; lane = query, registers = keys) + p_i . R[j - i],
+//   P^T = exp(S^T - m_i) / l_i with the row stats of attn_softmax_kernel,
+//   O^T += V^T P^T (the S^T accumulator registers are the B operand as they stand).
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
+  const int b = blockIdx.y;
+  const int h = blockIdx.z;
+  const int r0 = a.row_off[b];
+  const int L = a.row_off[b + 1] - r0;
+  const int i0 = blockIdx.x * 32;
+  if (i0 >= L) return;
+  const int H = a.H;
+  const int ldq = 68 * H;
+  const int ldv = 12 * H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = lane & 31, h2 = lane >> 5;
+  __shared__ float4 sR[4][64];
+  __shared__ float sV[4][32][13];
+  __shared__ float red[3][16][64];
+
+  const int i = i0 + c;
+  const bool iv = i < L;
+  const int ic = iv ? i : L - 1;
+  float qreg[16];
+  {
+    const float4* qp = reinterpret_cast<const float4*>(a.qkp + (long)(r0 + ic) * ldq + h * 32 + 16 * h2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = qp[q];
+      qreg[4 * q] = v.x;
+      qreg[4 * q + 1] = v.y;
+      qreg[4 * q + 2] = v.z;
+      qreg[4 * q + 3] = v.w;
+    }
+  }
+  const float4 pq = *reinterpret_cast<const float4*>(a.qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
+  const float mi = a.stats[((long)(r0 + ic) * H + h) * 2];
+  const float li = a.stats[((long)(r0 + ic) * H + h) * 2 + 1];
+  const float* kbase = a.qkp + (long)r0 * ldq + 32 * H + h * 32;
+  const float* vbase = a.v + (long)r0 * ldv + 12 * h;
+  const int nkb = (L + 31) / 32;
+
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  for (int kb = wid; kb < nkb; kb += 4) {
+    const int j0 = kb * 32;
+    // pos rows x = j0 - i0 - 31 + l, l < 63
+    if (lane < 63) {
+      const int x = j0 - i0 - 31 + lane;
+      sR[wid][lane] = *reinterpret_cast<const float4*>(a.pos_tab + (long)(x + a.pmax - 1) * 4 * H + 4 * h);
+    }
+    // values of this key block: 32 rows x 12
+    for (int e = lane; e < 32 * 3; e += 64) {
+      const int jj = e / 3, q = e - jj * 3;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j0 + jj < L) v = *reinterpret_cast<const float4*>(vbase + (long)(j0 + jj) * ldv + 4 * q);
+      sV[wid][jj][4 * q] = v.x;
+      sV[wid][jj][4 * q + 1] = v.y;
+      sV[wid][jj][4 * q + 2] = v.z;
+      sV[wid][jj][4 * q + 3] = v.w;
+    }
+    float kreg[16];
+    const int j = j0 + c;
+    if (j < L) {
+      const float4* kp = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 * h2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = kp[q];
+        kreg[4 * q] = v.x;
+        kreg[4 * q + 1] = v.y;
+        kreg[4 * q + 2] = v.z;
+        kreg[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) kreg[q] = 0.f;
+    }
+    f32x16 sc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kreg[s], qreg[s], sc, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
+      const float4 pr = sR[wid][jr - c + 31];
+      float ps = pq.x * pr.x;
+      ps = fmaf(pq.y, pr.y, ps);
+      ps = fmaf(pq.z, pr.z, ps);
+      ps = fmaf(pq.w, pr.w, ps);
+      sc[r] = (j0 + jr < L && iv) ? expf(sc[r] + ps - mi) * li : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
+      const float av = c < 12 ? sV[wid][jr][c] : 0.f;
+      o = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sc[r], o, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (wid > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wid - 1][r][lane] = o[r];
+  }
+  __syncthreads();
+  if (wid == 0 && iv) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int v = (r & 3) + 8 * (r >> 2) + 4 * h2;
+      if (v < 12)
+        a.out[(long)(r0 + i) * ldv + 12 * h + v] = o[r] + red[0][r][lane] + red[1][r][lane] + red[2][r][lane];
+    }
+  }
+}
+
+void launch_attn_sa(const AttnSAArgs& a, hipStream_t st) {
+  if (a.nseq <= 0 || a.max_len <= 0) return;
+  dim3 grid(cdiv(a.max_len, 32), a.nseq, a.H);
+  hipLaunchKernelGGL(attn_sa_kernel, grid, dim3(256), 0, st, a);
 }
 
 void launch_attn_softmax(const AttnArgs& a, hipStream_t st) {

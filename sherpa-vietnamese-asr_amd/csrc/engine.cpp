@@ -12,6 +12,7 @@
 #include <cstring>
 #include <deque>
 #include <numeric>
+#include <cstdlib>
 #include <sstream>
 
 #include "common.h"
@@ -409,7 +410,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
       l.wh = p;
     };
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
-                    &model_.enc_proj})
+                    &model_.enc_proj, &model_.dec_proj, &model_.joiner})
       mk(*l);
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
@@ -687,8 +688,9 @@ struct MetaPack {
 }  // namespace
 
 void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, const int* d_off,
+                           const int* d_map,
                            const std::vector<int>& lens, const long* d_aoff,
-                           const void* d_slices_attn, const void* d_slices_nl, int maxL) {
+                           const void* d_slices_nl, int maxL) {
   const int d = S.d, h = S.h, B = (int)lens.size();
   const int hid = 3 * d / 4;
   float* O = ws<float>("ly_orig", (size_t)R * d);
@@ -696,9 +698,10 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
   float* qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
   linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
-  float* A = ws<float>("ly_attn", 1);  // sized by caller
+  float* A = ws<float>("ly_attn", 1);  // sized by caller: head-0 weights (nonlin_attention)
+  float* stats = ws<float>("ly_attn_stats", (size_t)R * h * 2);
   {
-    AttnArgs a{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A};
+    AttnArgs a{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A, stats, 1};
     prof_begin("attn_softmax");
     launch_attn_softmax(a, st_);
     prof_end();
@@ -713,20 +716,9 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     float* vv = ws<float>("ly_vv", (size_t)R * 12 * h);
     float* oa = ws<float>("ly_oa", (size_t)R * 12 * h);
     linear(Ly.sa_in[k], X, d, R, vv, 12 * h, EPI_NONE);
-    GemmParams p{};
-    p.A = A;
-    p.B = vv;
-    p.sbk = 12 * h;
-    p.sbn = 1;
-    p.C = oa;
-    p.ldc = 12 * h;
-    p.N = 12;
-    p.alpha = 1.f;
-    p.slices = reinterpret_cast<const GemmSlice*>(d_slices_attn);
-    p.num_slices = B * h;
-    p.max_M = maxL;
+    AttnSAArgs sa{qkp, h, Ly.pos_tab, model_.pmax, d_off, B, maxL, stats, vv, oa};
     prof_begin("attn_apply");
-    gemm_f32(p, EPI_NONE, ALOAD_DENSE, true, st_);
+    launch_attn_sa(sa, st_);
     prof_end();
     linear(Ly.sa_out[k], oa, 12 * h, R, X, d, EPI_RESADD);
   };
@@ -735,7 +727,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     float* dc = ws<float>("ly_dc", (size_t)R * d);
     linear(Ly.cv_in[k], X, d, R, g2, 2 * d, EPI_NONE);
     prof_begin("dwconv1d");
-    launch_glu_dwconv1d(g2, d_off, B, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+    launch_glu_dwconv1d(g2, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
     prof_end();
     linear(Ly.cv_out[k], dc, d, R, X, d, EPI_RESADD);
   };
@@ -805,7 +797,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   const int ns = (int)model_.stacks.size();
   std::vector<LevelMeta> mst(ns);
   std::vector<std::vector<long>> aoff(ns);
-  std::vector<std::vector<GemmSlice>> sl_attn(ns), sl_nl(ns);
+  std::vector<std::vector<GemmSlice>> sl_nl(ns);
   size_t attn_floats = 0;
   int maxL_all = 0;
   for (int i = 0; i < ns; ++i) {
@@ -819,18 +811,8 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     for (int b = 0; b < B; ++b) {
       const int Lb = len[b], L4 = (Lb + 3) & ~3;
       aoff[i].push_back(acc);
-      for (int hh = 0; hh < s.h; ++hh) {
-        GemmSlice g{};
-        g.a_off = acc + (long)hh * Lb * L4;
-        g.b_off = (long)mst[i].off[b] * 12 * s.h + 12 * hh;
-        g.c_off = g.b_off;
-        g.M = Lb;
-        g.K = Lb;
-        g.lda = L4;
-        sl_attn[i].push_back(g);
-      }
       GemmSlice g{};
-      g.a_off = acc;
+      g.a_off = acc;  // head 0 block of this sequence
       g.b_off = (long)mst[i].off[b] * hid;
       g.c_off = g.b_off;
       g.aux_off = (long)mst[i].off[b] * 3 * hid;
@@ -838,7 +820,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       g.K = Lb;
       g.lda = L4;
       sl_nl[i].push_back(g);
-      acc += (long)s.h * Lb * L4;
+      acc += (long)Lb * L4;  // only head 0 is materialised (nonlin_attention)
     }
     attn_floats = std::max(attn_floats, (size_t)acc);
   }
@@ -855,21 +837,32 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
          o_L = mp.add(mL.off.data(), (B + 1) * 4), o_out = mp.add(mout.off.data(), (B + 1) * 4);
   size_t o_c2s = mp.add(sl_c2.data(), B * sizeof(GemmSlice)),
          o_c3s = mp.add(sl_c3.data(), B * sizeof(GemmSlice));
-  std::vector<size_t> o_st(ns), o_ao(ns), o_sa(ns), o_sn(ns);
+  std::vector<size_t> o_st(ns), o_ao(ns), o_sn(ns);
   for (int i = 0; i < ns; ++i) {
     o_st[i] = mp.add(mst[i].off.data(), (B + 1) * 4);
     o_ao[i] = mp.add(aoff[i].data(), B * sizeof(long));
-    o_sa[i] = mp.add(sl_attn[i].data(), sl_attn[i].size() * sizeof(GemmSlice));
     o_sn[i] = mp.add(sl_nl[i].data(), sl_nl[i].size() * sizeof(GemmSlice));
   }
   char* d_meta = ws<char>("enc_meta", mp.bytes.size());
   upload(d_meta, mp.bytes.data(), mp.bytes.size());
   auto I = [&](size_t o) { return reinterpret_cast<const int*>(d_meta + o); };
+  // row -> sequence maps of every resolution used by per-row kernels
+  int* c1_map = ws<int>("map_c1", mc1.total);
+  int* L_map = ws<int>("map_L", mL.total);
+  int* out_map = ws<int>("map_out", mout.total);
+  launch_row2seq(I(o_c1), B, mc1.total, c1_map, st_);
+  launch_row2seq(I(o_L), B, mL.total, L_map, st_);
+  launch_row2seq(I(o_out), B, mout.total, out_map, st_);
+  std::vector<int*> st_map(ns);
+  for (int i = 0; i < ns; ++i) {
+    st_map[i] = ws<int>("map_st" + std::to_string(i), mst[i].total);
+    launch_row2seq(I(o_st[i]), B, mst[i].total, st_map[i], st_);
+  }
 
   // ---------------- Conv2dSubsampling ----------------
   float* c1 = ws<float>("fe_c1", (size_t)mc1.total * 640);
   prof_begin("frontend_conv");
-  launch_conv1(d_feats, I(o_fb), I(o_c1), B, mc1.total, model_.conv0_w, model_.conv0_b, c1, st_);
+  launch_conv1(d_feats, I(o_fb), I(o_c1), c1_map, mc1.total, model_.conv0_w, model_.conv0_b, c1, st_);
   prof_end();
   float* c2 = ws<float>("fe_c2", (size_t)mc2.total * 39 * 32);
   {
@@ -917,7 +910,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   }
   float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
   prof_begin("frontend_conv");
-  launch_dwconv2d(x3, I(o_L), B, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+  launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
   prof_end();
   float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
   linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
@@ -949,18 +942,18 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     } else {
       X = ws<float>("st_x", (size_t)mst[i].total * d);
       prof_begin("elementwise");
-      launch_downsample(orig, I(o_L), I(o_st[i]), B, mst[i].total, d, s.ds, s.ds_w, X, st_);
+      launch_downsample(orig, I(o_L), I(o_st[i]), st_map[i], mst[i].total, d, s.ds, s.ds_w, X, st_);
       prof_end();
     }
     for (const DLayer& ly : s.layers)
-      layer_forward(s, ly, X, mst[i].total, I(o_st[i]), mst[i].len,
-                    reinterpret_cast<const long*>(d_meta + o_ao[i]), d_meta + o_sa[i],
-                    d_meta + o_sn[i], mst[i].maxlen);
+      layer_forward(s, ly, X, mst[i].total, I(o_st[i]), st_map[i], mst[i].len,
+                    reinterpret_cast<const long*>(d_meta + o_ao[i]), d_meta + o_sn[i],
+                    mst[i].maxlen);
     float* out = orig;
     if (s.ds != 1) {
       out = ws<float>("st_out" + std::to_string(i % 2), (size_t)mL.total * d);
       prof_begin("elementwise");
-      launch_upsample_combine(X, orig, I(o_L), I(o_st[i]), B, mL.total, d, s.ds, s.comb, out, st_);
+      launch_upsample_combine(X, orig, I(o_L), I(o_st[i]), L_map, mL.total, d, s.ds, s.comb, out, st_);
       prof_end();
     }
     outs[i] = out;
@@ -979,7 +972,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   // ---------------- output downsample + encoder_proj ----------------
   float* fo = ws<float>("enc_ds", (size_t)mout.total * Dm);
   prof_begin("elementwise");
-  launch_downsample(full, I(o_L), I(o_out), B, mout.total, Dm, 2, model_.out_ds_w, fo, st_);
+  launch_downsample(full, I(o_L), I(o_out), out_map, mout.total, Dm, 2, model_.out_ds_w, fo, st_);
   prof_end();
   linear(model_.enc_proj, fo, Dm, mout.total, d_enc, cfg.joiner_dim, EPI_NONE);
 }
@@ -1030,27 +1023,65 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   st.node_lp = ws<double>("se_nlp", ncap);
   st.node_stats = ws<float4>("se_nst", ncap);
   st.node_count = ws<int>("se_ncnt", S);
-  float* J = ws<float>("se_joinin", slots * D);
+  st.stamps = nullptr;
+  const bool stamps = getenv("ZASR_STAMPS") != nullptr;
+  if (stamps) {
+    st.stamps = ws<unsigned long long>("se_stamps", (size_t)Tmax * 8);
+    ZASR_HIP_CHECK(hipMemsetAsync(st.stamps, 0, (size_t)Tmax * 8 * 8, st_));
+  }
   float* logits = ws<float>("se_logits", slots * V);
-  DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
-  prof_begin("search");
-  launch_search_init(st, S, H, st_);
-  prof_end();
-  int active = S;
-  for (int t = 0; t < Tmax; ++t) {
-    while (active > 0 && el[active - 1] <= t) --active;
-    const int rows = active * H;
-    DecJoinArgs da{dw, model_.dec_proj.w, st.y1, st.y2, d_enc, d_eo, J, rows, H, t};
-    prof_begin("decoder");
-    launch_decjoin(da, st_);
-    prof_end();
-    JoinerArgs ja{J, model_.joiner.w, model_.joiner.b, logits, rows, V, D};
-    prof_begin("joiner");
-    launch_joiner(ja, st_);
-    prof_end();
+  if (model_.joiner.wh) {
+    // bf16 mode: 2 launches per frame (bf16 joiner; search step + decoder for changed slots)
+    __bf16* Jh = ws<__bf16>("se_joinin_h", slots * D);
+    ZASR_HIP_CHECK(hipMemsetAsync(Jh, 0, slots * D * sizeof(__bf16), st_));
+    float* dec_a = ws<float>("se_dec_a", slots * D);
+    float* dec_b = ws<float>("se_dec_b", slots * D);
+    FusedDec fd{model_.dec_tap0, model_.dec_tap1, reinterpret_cast<const __bf16*>(model_.dec_proj.wh),
+                model_.dec_proj.b, dec_a, dec_b, d_enc, d_eo, d_el, Jh, D};
     prof_begin("search");
-    launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, st_);
+    launch_search_init(st, S, H, st_);
+    FusedDec fi = fd;
+    fi.dec_new = dec_a;
+    launch_fused_init(fi, S, H, st_);
     prof_end();
+    int active = S;
+    for (int t = 0; t < Tmax; ++t) {
+      while (active > 0 && el[active - 1] <= t) --active;
+      const int rows = active * H;
+      JoinerBf16Args ja{Jh, reinterpret_cast<const __bf16*>(model_.joiner.wh), model_.joiner.b,
+                        logits, rows, V, D};
+      prof_begin("joiner");
+      launch_joiner_bf16(ja, st_);
+      prof_end();
+      fd.dec_old = dec_a;
+      fd.dec_new = dec_b;
+      prof_begin("search");
+      launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, &fd, st_);
+      prof_end();
+      std::swap(dec_a, dec_b);
+    }
+  } else {
+    float* J = ws<float>("se_joinin", slots * D);
+    DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
+    prof_begin("search");
+    launch_search_init(st, S, H, st_);
+    prof_end();
+    int active = S;
+    for (int t = 0; t < Tmax; ++t) {
+      while (active > 0 && el[active - 1] <= t) --active;
+      const int rows = active * H;
+      DecJoinArgs da{dw, model_.dec_proj.w, st.y1, st.y2, d_enc, d_eo, J, rows, H, t};
+      prof_begin("decoder");
+      launch_decjoin(da, st_);
+      prof_end();
+      JoinerArgs ja{J, model_.joiner.w, model_.joiner.b, logits, rows, V, D};
+      prof_begin("joiner");
+      launch_joiner(ja, st_);
+      prof_end();
+      prof_begin("search");
+      launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, nullptr, st_);
+      prof_end();
+    }
   }
   const int cap = Tmax;
   int* o_tok = ws<int>("so_tok", (size_t)S * cap);
@@ -1070,6 +1101,21 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   ZASR_HIP_CHECK(hipMemcpyAsync(h_lp.data(), o_lp, h_lp.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
   ZASR_HIP_CHECK(hipMemcpyAsync(h_st.data(), o_st, h_st.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
   ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+  if (stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
+    std::vector<unsigned long long> h((size_t)Tmax * 8);
+    ZASR_HIP_CHECK(hipMemcpy(h.data(), st.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+    double acc[7] = {0};
+    int n = 0;
+    for (int t = 0; t < Tmax; ++t) {
+      const unsigned long long* p = &h[(size_t)t * 8];
+      if (!p[0] || !p[6]) continue;
+      for (int k = 1; k <= 6; ++k) acc[k] += (double)(p[k] - p[k - 1]);
+      ++n;
+    }
+    fprintf(stderr, "[zasr stamps] frames=%d mean cycles: load %.0f stats %.0f topk %.0f expand %.0f "
+            "state+dec %.0f J %.0f\n", n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n,
+            acc[5] / n, acc[6] / n);
+  }
   for (int i = 0; i < S; ++i) {
     TokenResult& r = res[order[i]];
     const int c = h_cnt[i];

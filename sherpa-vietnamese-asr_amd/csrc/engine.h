@@ -128,7 +128,7 @@ class Engine {
                    std::vector<int>& t_out);
   std::vector<TokenResult> run_search(const float* d_enc, const std::vector<int>& t_out, int beam);
   void layer_forward(const DStack& stk, const DLayer& ly, float* X, int R, const int* d_off,
-                     const std::vector<int>& lens, const long* d_aoff, const void* d_slices_attn,
+                     const int* d_map, const std::vector<int>& lens, const long* d_aoff,
                      const void* d_slices_nl, int maxL);
   void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
               const char* cls = "enc_gemm");

@@ -25,10 +25,11 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
 
 // ---- Conv2dSubsampling pieces (icefall subsampling.py, 3P) ----
 // conv.0 (1->8, 3x3, pad (0,1)) + SwooshR: fbank rows [T][80] -> [T-2][80][8]
-void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, int nseq, int total_rows,
-                  const float* w /*[8][9]*/, const float* b, float* out, hipStream_t st);
+void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const int* c1_map,
+                  int total_rows, const float* w /*[8][9]*/, const float* b, float* out,
+                  hipStream_t st);
 // ConvNeXt depthwise 7x7, zero padding per sequence: [L][19][128] -> [L][19][128]
-void launch_dwconv2d(const float* x, const int* L_off, int nseq, int total_rows,
+void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
                      const float* w /*[128][49]*/, const float* b, float* out, hipStream_t st);
 
 // ---- Zipformer2 encoder elementwise / per-sequence kernels ----
@@ -41,18 +42,20 @@ void launch_bypass(float* x, const float* orig, const float* s, long rows, int d
 void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st);
 // g = x2[:, :d] * sigmoid(x2[:, d:]);  out[t][c] = SwooshR(b[c] + sum_k w[c][k] g[t+k-K/2][c]),
 // zero padding per sequence
-void launch_glu_dwconv1d(const float* x2, const int* off, int nseq, int total_rows, int d, int K,
-                         const float* w, const float* b, float* out, hipStream_t st);
+void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
+                         int K, const float* w, const float* b, float* out, hipStream_t st);
 // t1[r][c] = tanh(h3[r][c]) * h3[r][hid + c]
 void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStream_t st);
 // SimpleDownsample: out[t'] = sum_u w[u] x[min(ds t' + u, L - 1)]
-void launch_downsample(const float* x, const int* off_in, const int* off_out, int nseq,
+void launch_downsample(const float* x, const int* off_in, const int* off_out, const int* map_out,
                        int total_out, int d, int ds, const float* w_host8, float* out,
                        hipStream_t st);
 // SimpleUpsample + out_combiner bypass: y[t] = orig[t] + (xd[t / ds] - orig[t]) * s
 void launch_upsample_combine(const float* xd, const float* orig, const int* off_in,
-                             const int* off_ds, int nseq, int total_rows, int d, int ds,
+                             const int* off_ds, const int* map_in, int total_rows, int d, int ds,
                              const float* s, float* y, hipStream_t st);
+// row -> sequence index map for one resolution (off: [nseq + 1])
+void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t st);
 // dst[r][0:dd] = src[r][0:min(ds, dd)], zero-padded  (convert_num_channels)
 void launch_copy_cols(const float* src, int lds, int c0, float* dst, int ldd, int d0, int ncols,
                       long rows, bool zero_rest, int dst_width, hipStream_t st);
@@ -67,9 +70,25 @@ struct AttnArgs {
   const long* a_off;       // [B]   offset of sequence b's [H][L][ldA] block
   int nseq;
   int max_len;
-  float* attn;             // output
+  float* attn;             // normalised weights of heads < write_heads, [h][L][L4] per seq
+  float* stats;            // [R][H][2]: row max, 1 / row sum
+  int write_heads;
 };
 void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
+// fused self-attention consumer: out[:, 12h:12h+12] = softmax(S_h) V_h, recomputing S
+struct AttnSAArgs {
+  const float* qkp;
+  int H;
+  const float* pos_tab;
+  int pmax;
+  const int* row_off;
+  int nseq;
+  int max_len;
+  const float* stats;      // from attn_softmax
+  const float* v;          // [R][12H]
+  float* out;              // [R][12H]
+};
+void launch_attn_sa(const AttnSAArgs& a, hipStream_t st);
 
 // ---- transducer search (core/asr_engine.py:1023-1153) ----
 struct SearchState {
@@ -92,6 +111,7 @@ struct SearchState {
   float4* node_stats;   // (entropy, sum p^(1/3), top1, top2) of the emitting joiner row
   int* node_count;      // [S]
   int node_cap;
+  unsigned long long* stamps;  // diagnostic phase timestamps of block 0 ([frame][8]) or null
 };
 struct HotwordTables {
   int num_states;       // 0 => no hotwords
@@ -124,12 +144,36 @@ struct JoinerArgs {
   float* out;            // [M][V]
   int M, V, D;
 };
+// bf16 search mode: decoder runs inside the search step for changed slots only
+struct FusedDec {
+  const float* tap0;        // [V][D]
+  const float* tap1;        // [V][D]
+  const __bf16* wp;         // decoder_proj weight, bf16 [D][D]
+  const float* bp;          // [D]
+  const float* dec_old;     // [S*H][D] decoder rows of the current slots
+  float* dec_new;           // [S*H][D] decoder rows of the next slots
+  const float* enc;         // [sum T'][D]
+  const int* enc_off;       // [S]
+  const int* enc_len;       // [S]
+  __bf16* J;                // [S*H][D] joiner input of the next frame
+  int D;
+};
+struct JoinerBf16Args {
+  const __bf16* J;       // [M][D]
+  const __bf16* W;       // [V][D]
+  const float* bias;     // [V]
+  float* out;            // [M][V]
+  int M, V, D;
+};
 void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st);
 void launch_decjoin(const DecJoinArgs& a, hipStream_t st);
 void launch_joiner(const JoinerArgs& j, hipStream_t st);
+void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st);
+void launch_fused_init(const FusedDec& fd, int S, int Hmax, hipStream_t st);
+// fd == nullptr: decoder handled by decjoin (fp32 mode)
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
                         int beam, int t, const int* enc_len, const HotwordTables& hw,
-                        hipStream_t st);
+                        const FusedDec* fd, hipStream_t st);
 void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTables& hw,
                          int out_cap, int* out_tok, int* out_frame, double* out_lp,
                          float4* out_stats, int* out_count, hipStream_t st);

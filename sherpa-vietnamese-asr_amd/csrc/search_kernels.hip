@@ -58,10 +58,19 @@ __device__ __forceinline__ double log_add(double a, int fa, double b, int fb, in
   return a + log1p(exp(d));
 }
 
-// candidate order: larger value first, then smaller flat index
-__device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) {
-  return v1 > v2 || (v1 == v2 && i1 < i2);
+// candidate order: larger value first, then smaller flat index, as one unsigned 64-bit key
+// (order-preserving float bits << 32 | ~index); key 0 = empty
+__device__ __forceinline__ unsigned long long make_key(float v, int idx) {
+  unsigned u = __float_as_uint(v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned)(~(unsigned)idx);
 }
+__device__ __forceinline__ float key_val(unsigned long long k) {
+  unsigned u = (unsigned)(k >> 32);
+  u = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  return __uint_as_float(u);
+}
+__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(~(unsigned)k); }
 
 // relu(grouped conv(E[y2], E[y1])) for 4 channels c..c+3: the conv is linear per tap, so
 // tap0[v] = W[:, :, 0] * E[v] and tap1[v] = W[:, :, 1] * E[v] are tabulated at load time
@@ -111,6 +120,53 @@ __device__ __forceinline__ void splitk_reduce(f32x16& acc, float* red) {
       acc[r] += red[r * 64 + lane] + red[(16 + r) * 64 + lane] + red[(32 + r) * 64 + lane];
   }
 }
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// tanh(x) = 1 - 2 / (exp(2x) + 1): saturates correctly at +-inf (bf16 joiner input only)
+__device__ __forceinline__ float fast_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
+
+// dec[j][n] = bp[n] + sum_k Wp[n][k] x[j][k] for j < nc (x: LDS [32][D + 8] bf16 rows,
+// zero past nc), bf16 MFMA 32x32x16 with f32 accumulate; waves split the output columns.
+// Results go to LDS rows out[j][D] (f32).
+__device__ __forceinline__ void dec_rows_bf16(const __bf16* xs, int nc, const __bf16* wp,
+                                              const float* bp, int D, float* out) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const int ldx = D + 8;
+  for (int ct = wid; ct < D / 32; ct += 4) {
+    const int n = ct * 32 + col;
+    const __bf16* wrow = wp + (long)n * D + 8 * h;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int k0 = 0; k0 < D; k0 += 128) {
+      bf16x8 b[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (k0 + 16 * q < D) b[q] = *reinterpret_cast<const bf16x8*>(wrow + k0 + 16 * q);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (k0 + 16 * q >= D) break;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(xs + col * ldx + k0 + 16 * q + 8 * h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[q], acc, 0, 0, 0);
+      }
+    }
+    const float bb = bp[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row < nc) out[row * D + n] = acc[r] + bb;
+    }
+  }
+}
+
+// diagnostic phase stamp (block 0, thread 0 only; st.stamps null in normal runs)
+#define ZASR_STAMP(slot)                                                                  \
+  do {                                                                                    \
+    if (st.stamps && blockIdx.x == 0 && threadIdx.x == 0)                                 \
+      st.stamps[(long)t * 8 + (slot)] = __builtin_amdgcn_s_memtime();                     \
+  } while (0)
 
 }  // namespace
 
@@ -246,10 +302,93 @@ void launch_joiner(const JoinerArgs& j, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------------------
-template <int KB>
+// bf16 joiner: logits = W_out J + b with J, W_out in bf16 (v_mfma_f32_32x32x16_bf16, f32
+// accumulate).  Block = 4 waves = 128 rows x 32 vocab columns; every wave streams its own
+// 32 J rows and the shared 32 W_out rows straight from global (no LDS, no barrier).
+// --------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void joiner_bf16_kernel(JoinerBf16Args j) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.y * 128 + wid * 32;
+  if (m0 >= j.M) return;
+  const int n = blockIdx.x * 32 + col;
+  const bool nv = n < j.V;
+  const int D = j.D;
+  const int ar = m0 + col < j.M ? m0 + col : j.M - 1;
+  const __bf16* arow = j.J + (long)ar * D + 8 * h;
+  const __bf16* brow = j.W + (long)(nv ? n : 0) * D + 8 * h;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int k0 = 0; k0 < D; k0 += 128) {
+    bf16x8 a[8], b[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (k0 + 16 * q < D) {
+        a[q] = *reinterpret_cast<const bf16x8*>(arow + k0 + 16 * q);
+        b[q] = *reinterpret_cast<const bf16x8*>(brow + k0 + 16 * q);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (k0 + 16 * q >= D) break;
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b[q], acc, 0, 0, 0);
+    }
+  }
+  if (!nv) return;
+  const float bias = j.bias[n];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < j.M) j.out[(long)row * j.V + n] = acc[r] + bias;
+  }
+}
+
+void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
+  if (j.M <= 0) return;
+  ZASR_REQUIRE(j.D % 16 == 0, "joiner_dim must be a multiple of 16");
+  dim3 grid(cdiv(j.V, 32), cdiv(j.M, 128));
+  hipLaunchKernelGGL(joiner_bf16_kernel, grid, dim3(256), 0, st, j);
+}
+
+// decoder output of context (0, 0) into slot 0 of every stream, and J for frame 0
+__global__ __launch_bounds__(256) void fused_init_kernel(FusedDec fd, int Hmax) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int D = fd.D;
+  __bf16* xs = reinterpret_cast<__bf16*>(smem_raw);                    // [32][D + 8]
+  float* dl = reinterpret_cast<float*>(smem_raw + 32 * (D + 8) * 2);  // [16][D]
+  const int s = blockIdx.x;
+  const int base = s * Hmax;
+  for (int e = threadIdx.x; e < 32 * (D + 8); e += 256) {
+    const int i = e / (D + 8), c = e - i * (D + 8);
+    float v = 0.f;
+    if (i == 0 && c < D) v = fmaxf(fd.tap0[c] + fd.tap1[c], 0.f);  // tokens (0, 0)
+    xs[e] = (__bf16)v;
+  }
+  __syncthreads();
+  dec_rows_bf16(xs, 1, fd.wp, fd.bp, D, dl);
+  __syncthreads();
+  const bool has_t = fd.enc_len[s] > 0;
+  for (int c = threadIdx.x; c < D; c += 256) {
+    const float d = dl[c];
+    fd.dec_new[(long)base * D + c] = d;
+    if (has_t)
+      fd.J[(long)base * D + c] = (__bf16)tanhf(fd.enc[(long)fd.enc_off[s] * D + c] + d);
+  }
+}
+
+void launch_fused_init(const FusedDec& fd, int S, int Hmax, hipStream_t st) {
+  if (S <= 0) return;
+  size_t lds = 32 * (fd.D + 8) * 2 + 16 * fd.D * 4;
+  hipLaunchKernelGGL(fused_init_kernel, dim3(S), dim3(256), lds, st, fd, Hmax);
+}
+
+// --------------------------------------------------------------------------------------
+template <int KB, bool FUSED>
 __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const float* logits,
                                                           int V, int Hmax, int beam, int t,
-                                                          const int* enc_len, HotwordTables hw) {
+                                                          const int* enc_len, HotwordTables hw,
+                                                          FusedDec fd) {
   const int s = blockIdx.x;
   if (t >= enc_len[s]) return;
   const int tid = threadIdx.x;
@@ -265,16 +404,17 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   // new hypotheses
   __shared__ double nLp[kMaxBeam];
   __shared__ int nLpf[kMaxBeam], nLen[kMaxBeam], nY1[kMaxBeam], nY2[kMaxBeam], nHw[kMaxBeam],
-      nNode[kMaxBeam];
+      nNode[kMaxBeam], nParent[kMaxBeam], nChanged[kMaxBeam];
   __shared__ unsigned long long nHash[kMaxBeam];
   // row statistics
   __shared__ float sMax[kMaxBeam], sLogSum[kMaxBeam];
   __shared__ float4 sStats[kMaxBeam];
-  __shared__ float rA[4], rB[4];
-  __shared__ float cV[4 * KB];
-  __shared__ int cI[4 * KB];
-  __shared__ int sN, sNN, sNodeCnt;
+  __shared__ float rA[4], rB[4], rC[4];
+  __shared__ unsigned long long cK[4 * KB];
+  __shared__ int sN, sNN, sNodeCnt, sNC;
+  __shared__ int chSlot[kMaxBeam], chIdx[kMaxBeam];
 
+  ZASR_STAMP(0);
   if (tid == 0) {
     sN = st.nh[s];
     sNodeCnt = st.node_count[s];
@@ -292,8 +432,13 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     pNode[tid] = st.node[base + tid];
   }
   const float* rows = logits + (long)base * V;
+  ZASR_STAMP(1);
 
   // ---- 1. row statistics: g waves per row (g = 4 for a single hypothesis) ----
+  // One pass for (max, second max) over register-cached logits, one for
+  //   S = sum e, E1 = sum e d, E3 = sum exp(d / 3)   (d = x - max, e = exp(d)),
+  // giving entropy = log S - E1 / S and sum p^(1/3) = S^(-1/3) E3 (the reference's
+  // f32 formulas of :1167-1171 rewritten without per-element log / pow / divide).
   const int g = n >= 4 ? 1 : (n == 1 ? 4 : 2);
   for (int h0 = 0; h0 < n; h0 += 4 / g) {
     const int h = h0 + wid / g;
@@ -301,17 +446,36 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     const bool live = h < n;
     const float* row = rows + (long)(live ? h : 0) * V;
     const int stride = 64 * g, start = part * 64 + lane;
+    constexpr int kCache = 32;
+    const bool cached = (V + stride - 1) / stride <= kCache;
+    float xv[kCache];
     float m1 = -INFINITY, m2 = -INFINITY;
-    if (live)
-      for (int v = start; v < V; v += stride) {
-        float x = row[v];
-        if (x > m1) {
-          m2 = m1;
-          m1 = x;
-        } else if (x > m2) {
-          m2 = x;
+    if (live) {
+      if (cached) {
+#pragma unroll
+        for (int q = 0; q < kCache; ++q) {
+          const int v = start + q * stride;
+          const float x = v < V ? row[v] : -INFINITY;
+          xv[q] = x;
+          if (x > m1) {
+            m2 = m1;
+            m1 = x;
+          } else if (x > m2) {
+            m2 = x;
+          }
+        }
+      } else {
+        for (int v = start; v < V; v += stride) {
+          const float x = row[v];
+          if (x > m1) {
+            m2 = m1;
+            m1 = x;
+          } else if (x > m2) {
+            m2 = x;
+          }
         }
       }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
@@ -338,83 +502,61 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       }
       __syncthreads();
     }
-    // cache e = exp(x - max) per lane (up to 32 elements; longer rows recompute)
-    constexpr int kCache = 32;
-    float ev[kCache];
-    const bool cached = (V + stride - 1) / stride <= kCache;
-    float se = 0.f;
+    float se = 0.f, e1 = 0.f, e3 = 0.f;
     if (live) {
       if (cached) {
 #pragma unroll
         for (int q = 0; q < kCache; ++q) {
-          const int v = start + q * stride;
-          ev[q] = (v < V) ? expf(row[v] - m1) : 0.f;
-          se += ev[q];
-        }
-      } else {
-        for (int v = start; v < V; v += stride) se += expf(row[v] - m1);
-      }
-    }
-    se = wave_sum(se);
-    if (g > 1) {
-      if (lane == 0) rA[wid] = se;
-      __syncthreads();
-      const int w0 = (wid / g) * g;
-      se = 0.f;
-      for (int q = 0; q < g; ++q) se += rA[w0 + q];
-      __syncthreads();
-    }
-    float ent = 0.f, s3 = 0.f;
-    if (live) {
-      if (cached) {
-#pragma unroll
-        for (int q = 0; q < kCache; ++q) {
-          if (start + q * stride >= V) break;
-          const float p = ev[q] / se;
-          ent += p * logf(p + 1e-30f);
-          s3 += powf(p, 1.0f / 3.0f);
+          const float d = xv[q] - m1;  // -inf past V -> e = 0
+          const float e = __expf(d);
+          se += e;
+          e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+          e3 += __expf(d * (1.0f / 3.0f));
         }
       } else {
         for (int v = start; v < V; v += stride) {
-          const float p = expf(row[v] - m1) / se;
-          ent += p * logf(p + 1e-30f);
-          s3 += powf(p, 1.0f / 3.0f);
+          const float d = row[v] - m1;
+          const float e = __expf(d);
+          se += e;
+          e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+          e3 += __expf(d * (1.0f / 3.0f));
         }
       }
     }
-    ent = wave_sum(ent);
-    s3 = wave_sum(s3);
+    se = wave_sum(se);
+    e1 = wave_sum(e1);
+    e3 = wave_sum(e3);
     if (g > 1) {
       if (lane == 0) {
-        rA[wid] = ent;
-        rB[wid] = s3;
+        rA[wid] = se;
+        rB[wid] = e1;
+        rC[wid] = e3;
       }
       __syncthreads();
       const int w0 = (wid / g) * g;
-      ent = s3 = 0.f;
+      se = e1 = e3 = 0.f;
       for (int q = 0; q < g; ++q) {
-        ent += rA[w0 + q];
-        s3 += rB[w0 + q];
+        se += rA[w0 + q];
+        e1 += rB[w0 + q];
+        e3 += rC[w0 + q];
       }
       __syncthreads();
     }
     if (live && part == 0 && lane == 0) {
+      const float ls = logf(se);
       sMax[h] = m1;
-      sLogSum[h] = logf(se);
-      sStats[h] = make_float4(-ent, s3, 1.0f / se, expf(m2 - m1) / se);
+      sLogSum[h] = ls;
+      sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
+                              __expf(m2 - m1) / se);
     }
   }
   __syncthreads();
+  ZASR_STAMP(2);
 
-  // ---- 2. top-k over n * V candidates ----
-  float tv[KB];
-  int ti[KB];
+  // ---- 2. top-k over n * V candidates, as packed sortable 64-bit keys ----
+  unsigned long long tk[KB];
 #pragma unroll
-  for (int q = 0; q < KB; ++q) {
-    tv[q] = -INFINITY;
-    ti[q] = 0x7fffffff;
-  }
-  const int total = n * V;
+  for (int q = 0; q < KB; ++q) tk[q] = 0ull;
   for (int h = 0; h < n; ++h) {
     const float mh = sMax[h], lsh = sLogSum[h];
     const double ld = pLp[h];
@@ -422,69 +564,47 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     const bool f64 = pLpf[h] != 0;
     const float* row = rows + (long)h * V;
     for (int v = tid; v < V; v += 256) {
-    const int idx = h * V + v;
-    const float lpv = (row[v] - mh) - lsh;
-    const float val = f64 ? (float)((double)lpv + ld) : lpv + lf;
-    if (!better(val, idx, tv[KB - 1], ti[KB - 1])) continue;
+      const float lpv = (row[v] - mh) - lsh;
+      const float val = f64 ? (float)((double)lpv + ld) : lpv + lf;
+      const unsigned long long key = make_key(val, h * V + v);
+      if (key > tk[KB - 1]) {
 #pragma unroll
-    for (int q = KB - 1; q >= 0; --q) {
-      const bool gt_prev = (q > 0) ? better(val, idx, tv[q - 1], ti[q - 1]) : false;
-      const bool gt_cur = better(val, idx, tv[q], ti[q]);
-      if (gt_prev) {
-        tv[q] = tv[q - 1];
-        ti[q] = ti[q - 1];
-      } else if (gt_cur) {
-        tv[q] = val;
-        ti[q] = idx;
+        for (int q = KB - 1; q > 0; --q) tk[q] = key > tk[q - 1] ? tk[q - 1] : (key > tk[q] ? key : tk[q]);
+        tk[0] = key > tk[0] ? key : tk[0];
       }
-    }
     }
   }
   for (int round = 0; round < KB; ++round) {
-    float bv = tv[0];
-    int bi = ti[0];
+    unsigned long long best = tk[0];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      float ov = __shfl_xor(bv, o, 64);
-      int oi = __shfl_xor(bi, o, 64);
-      if (better(ov, oi, bv, bi)) {
-        bv = ov;
-        bi = oi;
-      }
+      const unsigned long long ob = __shfl_xor(best, o, 64);
+      best = ob > best ? ob : best;
     }
-    if (lane == 0) {
-      cV[wid * KB + round] = bv;
-      cI[wid * KB + round] = bi;
-    }
-    if (ti[0] == bi && bi != 0x7fffffff) {
+    if (lane == 0) cK[wid * KB + round] = best;
+    if (best != 0ull && tk[0] == best) {
 #pragma unroll
-      for (int q = 0; q < KB - 1; ++q) {
-        tv[q] = tv[q + 1];
-        ti[q] = ti[q + 1];
-      }
-      tv[KB - 1] = -INFINITY;
-      ti[KB - 1] = 0x7fffffff;
+      for (int q = 0; q < KB - 1; ++q) tk[q] = tk[q + 1];
+      tk[KB - 1] = 0ull;
     }
   }
   __syncthreads();
-
   // ---- 3. expansion, hotwords, dedup (serial over <= beam candidates, all in LDS) ----
   if (tid == 0) {
+    const int total = n * V;
     const int k = beam < total ? beam : total;
     int ptr[4] = {0, 0, 0, 0};
-    int nn = 0;
+    int nn = 0, nc = 0;
     for (int c = 0; c < k; ++c) {
-      int bw = -1;
-      for (int w = 0; w < 4; ++w) {
-        if (ptr[w] >= KB) continue;
-        if (bw < 0 || better(cV[w * KB + ptr[w]], cI[w * KB + ptr[w]], cV[bw * KB + ptr[bw]],
-                             cI[bw * KB + ptr[bw]]))
-          bw = w;
-      }
-      const float val = cV[bw * KB + ptr[bw]];
-      const int idx = cI[bw * KB + ptr[bw]];
+      int bw = 0;
+      for (int w = 1; w < 4; ++w)
+        if (ptr[w] < KB && (ptr[bw] >= KB || cK[w * KB + ptr[w]] > cK[bw * KB + ptr[bw]])) bw = w;
+      if (ptr[bw] >= KB) break;
+      const unsigned long long key0 = cK[bw * KB + ptr[bw]];
       ++ptr[bw];
-      if (idx == 0x7fffffff) break;
+      if (key0 == 0ull) break;
+      const float val = key_val(key0);
+      const int idx = key_idx(key0);
       const int hi = idx / V, tok = idx - hi * V;
       double score = (double)val;
       unsigned long long key;
@@ -533,6 +653,8 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
         st.node_lp[gi] = (double)val - pLp[hi];
         st.node_stats[gi] = sStats[hi];
         nnode = nid;
+        chIdx[nn] = nc;
+        chSlot[nc++] = nn;
       }
       nLp[nn] = score;
       nLpf[nn] = 0;
@@ -542,13 +664,17 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       nY2[nn] = ny2;
       nHw[nn] = nhw;
       nNode[nn] = nnode;
+      nParent[nn] = hi;
+      nChanged[nn] = tok != 0;
       ++nn;
     }
     sNN = nn;
+    sNC = nc;
     st.nh[s] = nn;
     st.node_count[s] = sNodeCnt;
   }
   __syncthreads();
+  ZASR_STAMP(4);
   const int nn = sNN;
   if (tid < nn) {
     st.lp[base + tid] = nLp[tid];
@@ -560,22 +686,80 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     st.hw[base + tid] = nHw[tid];
     st.node[base + tid] = nNode[tid];
   }
+  if constexpr (FUSED) {
+    // decoder rows of the new slots (blank extensions keep the parent's row) and the
+    // joiner input of frame t + 1: J[slot] = tanh(enc[s, t + 1] + dec[slot])
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int D = fd.D;
+    __bf16* xs = reinterpret_cast<__bf16*>(smem_raw);                    // [32][D + 8]
+    float* dl = reinterpret_cast<float*>(smem_raw + 32 * (D + 8) * 2);  // [16][D]
+    const int nc = sNC;
+    if (nc > 0) {
+      for (int e = tid; e < 32 * (D + 8); e += 256) {
+        const int i = e / (D + 8), c = e - i * (D + 8);
+        float v = 0.f;
+        if (i < nc && c < D) {
+          const int q = chSlot[i];
+          v = fmaxf(fd.tap0[(long)nY2[q] * D + c] + fd.tap1[(long)nY1[q] * D + c], 0.f);
+        }
+        xs[e] = (__bf16)v;
+      }
+      __syncthreads();
+      dec_rows_bf16(xs, nc, fd.wp, fd.bp, D, dl);
+      __syncthreads();
+    }
+    ZASR_STAMP(5);
+    const bool next = t + 1 < enc_len[s];
+    const float* erow = fd.enc + (long)(fd.enc_off[s] + t + 1) * D;
+    const int d4 = D / 4;
+    for (int q = 0; q < nn; ++q) {
+      const float* src = nChanged[q] ? dl + chIdx[q] * D : fd.dec_old + (long)(base + nParent[q]) * D;
+      for (int c4 = tid; c4 < d4; c4 += 256) {
+        const float4 dv = *reinterpret_cast<const float4*>(src + 4 * c4);
+        *reinterpret_cast<float4*>(fd.dec_new + (long)(base + q) * D + 4 * c4) = dv;
+        if (next) {
+          const float4 ev = *reinterpret_cast<const float4*>(erow + 4 * c4);
+          __bf16* jo = fd.J + (long)(base + q) * D + 4 * c4;
+          jo[0] = (__bf16)fast_tanh(ev.x + dv.x);
+          jo[1] = (__bf16)fast_tanh(ev.y + dv.y);
+          jo[2] = (__bf16)fast_tanh(ev.z + dv.z);
+          jo[3] = (__bf16)fast_tanh(ev.w + dv.w);
+        }
+      }
+    }
+  }
+  ZASR_STAMP(6);
 
 }
 
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
                         int beam, int t, const int* enc_len, const HotwordTables& hw,
-                        hipStream_t st) {
+                        const FusedDec* fd, hipStream_t st) {
   if (S <= 0) return;
   ZASR_REQUIRE(beam >= 1 && beam <= kMaxBeam && beam <= Hmax, "beam out of range");
   dim3 grid(S), block(256);
+  FusedDec f{};
+  size_t lds = 0;
+  if (fd) {
+    f = *fd;
+    lds = 32 * (f.D + 8) * 2 + 16 * f.D * 4;
+  }
 #define ZASR_STEP(KBV)                                                                      \
-  hipLaunchKernelGGL(search_step_kernel<KBV>, grid, block, 0, st, s, logits, V, Hmax, beam, t, \
-                     enc_len, hw)
-  if (beam == 1) ZASR_STEP(1);
-  else if (beam <= 4) ZASR_STEP(4);
-  else if (beam <= 8) ZASR_STEP(8);
-  else ZASR_STEP(16);
+  if (fd)                                                                                   \
+    hipLaunchKernelGGL((search_step_kernel<KBV, true>), grid, block, lds, st, s, logits, V,  \
+                       Hmax, beam, t, enc_len, hw, f);                                      \
+  else                                                                                      \
+    hipLaunchKernelGGL((search_step_kernel<KBV, false>), grid, block, 0, st, s, logits, V,   \
+                       Hmax, beam, t, enc_len, hw, f)
+  if (beam == 1) {
+    ZASR_STEP(1);
+  } else if (beam <= 4) {
+    ZASR_STEP(4);
+  } else if (beam <= 8) {
+    ZASR_STEP(8);
+  } else {
+    ZASR_STEP(16);
+  }
 #undef ZASR_STEP
 }
 
