@@ -38,6 +38,17 @@ __device__ __forceinline__ float swooshl(float x) { return softplusf(x - 4.f) - 
 __device__ __forceinline__ float swooshr(float x) {
   return softplusf(x - 1.f) - 0.08f * x - 0.313261687f;
 }
+// native v_exp_f32 / v_log_f32 variants for GEMM epilogues (abs error ~1e-7 vs the
+// libm forms above)
+__device__ __forceinline__ float softplus_fast(float x) {
+  return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x)));
+}
+__device__ __forceinline__ float swooshl_fast(float x) {
+  return softplus_fast(x - 4.f) - 0.08f * x - 0.035f;
+}
+__device__ __forceinline__ float swooshr_fast(float x) {
+  return softplus_fast(x - 1.f) - 0.08f * x - 0.313261687f;
+}
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -672,11 +672,25 @@ __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnArgs a) {
 
 // =====================================================================================
 // Self-attention consumer fused with the score recompute (flash style, no materialised
-// weights): per (sequence, 32 queries, head), waves stride over 32-key blocks:
-//   S^T = K Q^T (f32 MFMA 32x32x2; lane = query, registers = keys) + p_i . R[j - i],
-//   P^T = exp(S^T - m_i) / l_i with the row stats of attn_softmax_kernel,
-//   O^T += V^T P^T (the S^T accumulator registers are the B operand as they stand).
+// weights): per (sequence, 32 queries, head), the 4 waves split the 32-key blocks:
+//   S^T = K Q^T + p_i . R[j - i]   (lane = query i, accumulator registers = 16 keys j),
+//   P^T = exp(S^T - m_i) / l_i,    O^T += V^T P^T.
+// ONLINE: m_i / l_i are running statistics (rescaled per key block, merged over waves at the
+// end) and are written out for the second self-attention of the layer; otherwise they come
+// from that output.  BF16: QK^T and PV on v_mfma_f32_32x32x16_bf16 (2 + 2 MFMAs per key
+// block; the PV k-slots are the S^T accumulator registers as they stand, with V staged in
+// the same permuted key order); else exact f32 MFMA 32x32x2 (16 + 16).
 // =====================================================================================
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8_t cvt8(const float4 x0, const float4 x1) {
+  bf16x8_t v;
+  v[0] = (__bf16)x0.x; v[1] = (__bf16)x0.y; v[2] = (__bf16)x0.z; v[3] = (__bf16)x0.w;
+  v[4] = (__bf16)x1.x; v[5] = (__bf16)x1.y; v[6] = (__bf16)x1.z; v[7] = (__bf16)x1.w;
+  return v;
+}
+
+template <bool ONLINE, bool BF16>
 __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
   const int b = blockIdx.y;
   const int h = blockIdx.z;
@@ -690,15 +704,24 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = lane & 31, h2 = lane >> 5;
   __shared__ float4 sR[4][64];
-  __shared__ float sV[4][32][13];
+  __shared__ float sV[4][32][13];                               // f32 path
+  __shared__ __attribute__((aligned(16))) __bf16 sVt[4][12][32];  // bf16 path, permuted keys
   __shared__ float red[3][16][64];
+  __shared__ float redM[4][64], redL[4][64];
 
   const int i = i0 + c;
   const bool iv = i < L;
   const int ic = iv ? i : L - 1;
+  const float* qrow = a.qkp + (long)(r0 + ic) * ldq + h * 32;
   float qreg[16];
-  {
-    const float4* qp = reinterpret_cast<const float4*>(a.qkp + (long)(r0 + ic) * ldq + h * 32 + 16 * h2);
+  bf16x8_t qf[2];
+  if constexpr (BF16) {
+    const float4* q0 = reinterpret_cast<const float4*>(qrow + 8 * h2);
+    const float4* q1 = reinterpret_cast<const float4*>(qrow + 16 + 8 * h2);
+    qf[0] = cvt8(q0[0], q0[1]);
+    qf[1] = cvt8(q1[0], q1[1]);
+  } else {
+    const float4* qp = reinterpret_cast<const float4*>(qrow + 16 * h2);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float4 v = qp[q];
@@ -709,8 +732,12 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
     }
   }
   const float4 pq = *reinterpret_cast<const float4*>(a.qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
-  const float mi = a.stats[((long)(r0 + ic) * H + h) * 2];
-  const float li = a.stats[((long)(r0 + ic) * H + h) * 2 + 1];
+  float mi = 0.f, li = 0.f;
+  if constexpr (!ONLINE) {
+    mi = a.stats[((long)(r0 + ic) * H + h) * 2];
+    li = a.stats[((long)(r0 + ic) * H + h) * 2 + 1];
+  }
+  float m_run = -INFINITY, l_run = 0.f;
   const float* kbase = a.qkp + (long)r0 * ldq + 32 * H + h * 32;
   const float* vbase = a.v + (long)r0 * ldv + 12 * h;
   const int nkb = (L + 31) / 32;
@@ -730,32 +757,58 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
       const int jj = e / 3, q = e - jj * 3;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (j0 + jj < L) v = *reinterpret_cast<const float4*>(vbase + (long)(j0 + jj) * ldv + 4 * q);
-      sV[wid][jj][4 * q] = v.x;
-      sV[wid][jj][4 * q + 1] = v.y;
-      sV[wid][jj][4 * q + 2] = v.z;
-      sV[wid][jj][4 * q + 3] = v.w;
-    }
-    float kreg[16];
-    const int j = j0 + c;
-    if (j < L) {
-      const float4* kp = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 * h2);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = kp[q];
-        kreg[4 * q] = v.x;
-        kreg[4 * q + 1] = v.y;
-        kreg[4 * q + 2] = v.z;
-        kreg[4 * q + 3] = v.w;
+      if constexpr (BF16) {
+        // key jj sits in accumulator register r = (jj&3) + 4*(jj>>3) of lane half (jj>>2)&1;
+        // MFMA m = r >> 3 takes it in k-slot 8 * half + (r & 7)
+        const int r = (jj & 3) + 4 * (jj >> 3);
+        const int slot = 16 * (r >> 3) + 8 * ((jj >> 2) & 1) + (r & 7);
+        sVt[wid][4 * q][slot] = (__bf16)v.x;
+        sVt[wid][4 * q + 1][slot] = (__bf16)v.y;
+        sVt[wid][4 * q + 2][slot] = (__bf16)v.z;
+        sVt[wid][4 * q + 3][slot] = (__bf16)v.w;
+      } else {
+        sV[wid][jj][4 * q] = v.x;
+        sV[wid][jj][4 * q + 1] = v.y;
+        sV[wid][jj][4 * q + 2] = v.z;
+        sV[wid][jj][4 * q + 3] = v.w;
       }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) kreg[q] = 0.f;
     }
+    const int j = j0 + c;
     f32x16 sc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+    if constexpr (BF16) {
+      bf16x8_t kf0, kf1;
+      if (j < L) {
+        const float4* k0 = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 8 * h2);
+        const float4* k1 = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 + 8 * h2);
+        kf0 = cvt8(k0[0], k0[1]);
+        kf1 = cvt8(k1[0], k1[1]);
+      } else {
+        kf0 = cvt8(make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f));
+        kf1 = kf0;
+      }
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf0, qf[0], sc, 0, 0, 0);
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf1, qf[1], sc, 0, 0, 0);
+    } else {
+      float kreg[16];
+      if (j < L) {
+        const float4* kp = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 * h2);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kreg[s], qreg[s], sc, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = kp[q];
+          kreg[4 * q] = v.x;
+          kreg[4 * q + 1] = v.y;
+          kreg[4 * q + 2] = v.z;
+          kreg[4 * q + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) kreg[q] = 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kreg[s], qreg[s], sc, 0, 0, 0);
+    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -765,15 +818,61 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
       ps = fmaf(pq.y, pr.y, ps);
       ps = fmaf(pq.z, pr.z, ps);
       ps = fmaf(pq.w, pr.w, ps);
-      sc[r] = (j0 + jr < L && iv) ? expf(sc[r] + ps - mi) * li : 0.f;
+      sc[r] = (j0 + jr < L && iv) ? sc[r] + ps : -INFINITY;
     }
+    if constexpr (ONLINE) {
+      float bm = sc[0];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
-      const float av = c < 12 ? sV[wid][jr][c] : 0.f;
-      o = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sc[r], o, 0, 0, 0);
+      for (int r = 1; r < 16; ++r) bm = fmaxf(bm, sc[r]);
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m_run, bm);
+      if (mn != -INFINITY) {
+        const float scale = __expf(m_run - mn);  // m_run = -inf -> 0
+        l_run *= scale;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o[r] *= scale;
+          sc[r] = __expf(sc[r] - mn);
+          l_run += sc[r];
+        }
+        m_run = mn;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = __expf(sc[r] - mi) * li;  // -inf -> 0
+    }
+    if constexpr (BF16) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        bf16x8_t pf, vf;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pf[t] = (__bf16)sc[8 * m + t];
+        if (c < 12) {
+          vf = *reinterpret_cast<const bf16x8_t*>(&sVt[wid][c][16 * m + 8 * h2]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) vf[t] = (__bf16)0.f;
+        }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
+        const float av = c < 12 ? sV[wid][jr][c] : 0.f;
+        o = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sc[r], o, 0, 0, 0);
+      }
     }
     __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (ONLINE) {
+    // this wave's row statistics: both lane halves hold the same max, partial sums
+    l_run += __shfl_xor(l_run, 32, 64);
+    redM[wid][lane] = m_run;
+    redL[wid][lane] = l_run;
   }
   if (wid > 0) {
 #pragma unroll
@@ -781,24 +880,47 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
   }
   __syncthreads();
   if (wid == 0 && iv) {
+    float wsc[4] = {1.f, 1.f, 1.f, 1.f};
+    float inv = 1.f;
+    if constexpr (ONLINE) {
+      float M = redM[0][lane];
+      for (int w = 1; w < 4; ++w) M = fmaxf(M, redM[w][lane]);
+      float Ls = 0.f;
+      for (int w = 0; w < 4; ++w) {
+        wsc[w] = redM[w][lane] == -INFINITY ? 0.f : __expf(redM[w][lane] - M);
+        Ls += redL[w][lane] * wsc[w];
+      }
+      inv = 1.f / Ls;
+      if (h2 == 0) {
+        float* sp = a.stats_out + ((long)(r0 + i) * H + h) * 2;
+        sp[0] = M;
+        sp[1] = inv;
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int v = (r & 3) + 8 * (r >> 2) + 4 * h2;
-      if (v < 12)
-        a.out[(long)(r0 + i) * ldv + 12 * h + v] = o[r] + red[0][r][lane] + red[1][r][lane] + red[2][r][lane];
+      if (v < 12) {
+        float acc = o[r] * wsc[0] + red[0][r][lane] * wsc[1] + red[1][r][lane] * wsc[2] +
+                    red[2][r][lane] * wsc[3];
+        a.out[(long)(r0 + i) * ldv + 12 * h + v] = acc * inv;
+      }
     }
   }
 }
 
-void launch_attn_sa(const AttnSAArgs& a, hipStream_t st) {
+void launch_attn_sa(const AttnSAArgs& a, bool online, bool bf16, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
   dim3 grid(cdiv(a.max_len, 32), a.nseq, a.H);
-  hipLaunchKernelGGL(attn_sa_kernel, grid, dim3(256), 0, st, a);
+  if (online && bf16) hipLaunchKernelGGL((attn_sa_kernel<true, true>), grid, dim3(256), 0, st, a);
+  else if (online) hipLaunchKernelGGL((attn_sa_kernel<true, false>), grid, dim3(256), 0, st, a);
+  else if (bf16) hipLaunchKernelGGL((attn_sa_kernel<false, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_sa_kernel<false, false>), grid, dim3(256), 0, st, a);
 }
 
 void launch_attn_softmax(const AttnArgs& a, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
-  dim3 grid(cdiv(a.max_len, 32), a.nseq, a.H);
+  dim3 grid(cdiv(a.max_len, 32), a.nseq, a.write_heads < a.H ? a.write_heads : a.H);
   hipLaunchKernelGGL(attn_softmax_kernel, grid, dim3(256), 0, st, a);
 }
 

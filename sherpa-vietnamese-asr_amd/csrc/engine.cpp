@@ -701,6 +701,8 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   float* A = ws<float>("ly_attn", 1);  // sized by caller: head-0 weights (nonlin_attention)
   float* stats = ws<float>("ly_attn_stats", (size_t)R * h * 2);
   {
+    // head 0 only: its normalised weights feed nonlin_attention; every head's statistics
+    // come from self_attn1's online softmax
     AttnArgs a{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A, stats, 1};
     prof_begin("attn_softmax");
     launch_attn_softmax(a, st_);
@@ -716,9 +718,9 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     float* vv = ws<float>("ly_vv", (size_t)R * 12 * h);
     float* oa = ws<float>("ly_oa", (size_t)R * 12 * h);
     linear(Ly.sa_in[k], X, d, R, vv, 12 * h, EPI_NONE);
-    AttnSAArgs sa{qkp, h, Ly.pos_tab, model_.pmax, d_off, B, maxL, stats, vv, oa};
+    AttnSAArgs sa{qkp, h, Ly.pos_tab, model_.pmax, d_off, B, maxL, stats, vv, oa, stats};
     prof_begin("attn_apply");
-    launch_attn_sa(sa, st_);
+    launch_attn_sa(sa, k == 0, precision_ == 1, st_);
     prof_end();
     linear(Ly.sa_out[k], oa, 12 * h, R, X, d, EPI_RESADD);
   };
@@ -756,7 +758,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
     p.num_slices = B;
     p.max_M = maxL;
-    prof_begin("attn_apply");
+    prof_begin("attn_nonlin");
     gemm_f32(p, EPI_MULAUX, ALOAD_DENSE, true, st_);
     prof_end();
     linear(Ly.na_out, z, hid, R, X, d, EPI_RESADD);

@@ -151,7 +151,7 @@ class Engine {
   int device_ = 0;
   int beam_ = 8;
   [[maybe_unused]] bool greedy_ = false;
-  [[maybe_unused]] int precision_ = 0;
+  int precision_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;

@@ -71,8 +71,11 @@ struct GemmParams {
 // Launch; picks a tile shape from (max_M, N).  B_ncontig selects the [K][N] B layout.
 void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream_t stream);
 // bf16-input variant: Bw = bf16 weights [N][K] (K contiguous, row stride p.sbn elements);
-// A (f32 activations) is rounded to bf16 while staging; f32 accumulate and epilogue.
-void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t stream);
+// A = f32 activations rounded to bf16 while staging (or bf16 when a_bf16: p.A then points
+// at __bf16 data); f32 accumulate and epilogue; C written as f32 (or bf16 when c_bf16).
+// Requires N, ldc (and ldaux for EPI_MULAUX) to be multiples of 4.
+void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t stream,
+               bool a_bf16 = false, bool c_bf16 = false);
 
 // device f32 -> bf16 (round to nearest even) copy
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t stream);

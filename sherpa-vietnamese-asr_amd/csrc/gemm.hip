@@ -6,6 +6,8 @@
 // floats per lane half: conflict-free ds_read_b32), double-buffered with one barrier per
 // K-slab, next slab's global loads (float4 per lane) in flight under the MFMAs.
 // Each wave owns a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA tiles.
+#include <type_traits>
+
 #include "common.h"
 #include "gemm.h"
 
@@ -267,33 +269,85 @@ void launch_tile(const GemmParams& p, hipStream_t st) {
 
 
 // ---------------------------------------------------------------------------------------
-// bf16 MFMA variant (the "bf16" precision mode): A converted f32 -> bf16 (RNE) while staging,
-// B = weights pre-converted to bf16 [N][K]; v_mfma_f32_32x32x16_bf16 with f32 accumulate.
-// LDS images are row-major [row][BK + 8] bf16 (80-byte rows: conflict-free ds_read_b128 of
-// the 8-element k-fragments).
+// bf16 MFMA variant (the "bf16" precision mode): v_mfma_f32_32x32x16_bf16, f32 accumulate.
+// A is f32 (rounded to bf16, RNE, while staging) or bf16; B = weights pre-converted to bf16
+// [N][K].  LDS images are row-major [row][BK + 8] bf16 (odd multiple of 16 B per row:
+// conflict-free ds_read_b128 of the 8-element k-fragments), two stages, next stage's global
+// loads in registers under the MFMAs.  The epilogue goes through LDS one 32x32 fragment per
+// wave at a time so that bias / activation / residual run on float4 rows and every global
+// access is a 16-byte vector.  Tiles are numbered so that the blocks sharing an A row-panel
+// land on the same XCD (blocks are dealt round-robin over the 8 XCDs, each with its own L2):
+// A is fetched from HBM once, not once per N tile.
 // ---------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int BKH = 32;
-constexpr int LDH = BKH + 8;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI>
+template <int ALOAD, typename TA>
+__device__ __forceinline__ bf16x8 load_a8(const GemmParams& p, const TA* A, int M, int K, int lda,
+                                          int gm, int gk) {
+  bf16x8 v;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
+  if constexpr (std::is_same<TA, __bf16>::value) {
+    if (gm < M && gk < K) {
+      const __bf16* ptr = A + (long)gm * lda + gk;
+      if (gk + 7 < K) {
+        v = *reinterpret_cast<const bf16x8*>(ptr);
+      } else {
+        for (int q = 0; q < 8; ++q)
+          if (gk + q < K) v[q] = ptr[q];
+      }
+    }
+  } else {
+    const float4 x0 = load_a4<ALOAD>(p, A, M, K, lda, gm, gk);
+    const float4 x1 = load_a4<ALOAD>(p, A, M, K, lda, gm, gk + 4);
+    v[0] = (__bf16)x0.x; v[1] = (__bf16)x0.y; v[2] = (__bf16)x0.z; v[3] = (__bf16)x0.w;
+    v[4] = (__bf16)x1.x; v[5] = (__bf16)x1.y; v[6] = (__bf16)x1.z; v[7] = (__bf16)x1.w;
+  }
+  return v;
+}
+
+// logical tile of this block (see header comment): XCD x owns tiles [x*per + min(x, rem) ...)
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+  const int per = nb >> 3, rem = nb & 7;
+  const int xcd = b & 7, slot = b >> 3;
+  return xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
+}
+
+template <int EPI>
+__device__ __forceinline__ float epi_act(float v) {
+  if constexpr (EPI == EPI_SWOOSHL) return swooshl_fast(v);
+  if constexpr (EPI == EPI_SWOOSHR) return swooshr_fast(v);
+  return v;
+}
+
+template <int BM, int BN, int BK, int WAVES_M, int WAVES_N, int ALOAD, int EPI, typename TA,
+          typename TC>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmParams p,
-                                                                          const __bf16* Bw) {
+                                                                          const __bf16* Bw,
+                                                                          int tiles_n) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WTM = BM / WAVES_M;
   constexpr int WTN = BN / WAVES_N;
   constexpr int FM = WTM / 32;
   constexpr int FN = WTN / 32;
   static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
-  constexpr int A_G = BM * BKH / 8;  // 8-element groups per stage
-  constexpr int B_G = BN * BKH / 8;
+  constexpr int LDH = BK + 8;
+  constexpr int GPR = BK / 8;         // 8-element groups per row
+  constexpr int A_G = BM * GPR;
+  constexpr int B_G = BN * GPR;
   constexpr int A_LD = (A_G + NT - 1) / NT;
   constexpr int B_LD = (B_G + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * LDH];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * LDH];
+  constexpr int STAGE = (BM + BN) * LDH;  // bf16 elements
+  constexpr int LDE = 40;                 // epilogue fragment row stride (floats)
+  constexpr int OPER_BYTES = 2 * STAGE * 2;
+  constexpr int EPI_BYTES = (NT / 64) * 32 * LDE * 4;
+  constexpr int LDS_BYTES = OPER_BYTES > EPI_BYTES ? OPER_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  __bf16* const sbase = reinterpret_cast<__bf16*>(smem);
 
-  const float* A = p.A;
-  float* C = p.C;
+  const TA* A = reinterpret_cast<const TA*>(p.A);
+  TC* C = reinterpret_cast<TC*>(p.C);
   const float* aux = p.aux;
   int M = p.M, K = p.K, lda = p.lda;
   long b_off = 0;
@@ -308,9 +362,11 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     lda = s.lda;
   }
   const __bf16* B = Bw + b_off;
-  const int m0 = blockIdx.y * BM;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int m_tile = tile / tiles_n;
+  const int m0 = m_tile * BM;
   if (m0 >= M) return;
-  const int n0 = blockIdx.x * BN;
+  const int n0 = (tile - m_tile * tiles_n) * BN;
   const int N = p.N;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -323,26 +379,18 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int idx = tid + NT * i;
-      const int row = idx >> 2, k8 = idx & 3;
-      bf16x8 v;
-      for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
-      if (idx < A_G) {
-        const int gk = kt * BKH + 8 * k8;
-        float4 x0 = load_a4<ALOAD>(p, A, M, K, lda, m0 + row, gk);
-        float4 x1 = load_a4<ALOAD>(p, A, M, K, lda, m0 + row, gk + 4);
-        v[0] = (__bf16)x0.x; v[1] = (__bf16)x0.y; v[2] = (__bf16)x0.z; v[3] = (__bf16)x0.w;
-        v[4] = (__bf16)x1.x; v[5] = (__bf16)x1.y; v[6] = (__bf16)x1.z; v[7] = (__bf16)x1.w;
-      }
-      ra[i] = v;
+      const int row = idx / GPR, k8 = idx % GPR;
+      if (idx < A_G) ra[i] = load_a8<ALOAD, TA>(p, A, M, K, lda, m0 + row, kt * BK + 8 * k8);
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
       const int idx = tid + NT * i;
-      const int n = idx >> 2, k8 = idx & 3;
+      const int n = idx / GPR, k8 = idx % GPR;
       bf16x8 v;
+#pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
       if (idx < B_G) {
-        const int gn = n0 + n, gk = kt * BKH + 8 * k8;
+        const int gn = n0 + n, gk = kt * BK + 8 * k8;
         if (gn < N && gk < K) {
           const __bf16* ptr = B + (long)gn * p.sbn + gk;
           if (gk + 7 < K) {
@@ -357,15 +405,17 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     }
   };
   auto sstore = [&](int buf) {
+    __bf16* As = sbase + buf * STAGE;
+    __bf16* Bs = As + BM * LDH;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int idx = tid + NT * i;
-      if (idx < A_G) *reinterpret_cast<bf16x8*>(&As[buf][(idx >> 2) * LDH + 8 * (idx & 3)]) = ra[i];
+      if (idx < A_G) *reinterpret_cast<bf16x8*>(&As[(idx / GPR) * LDH + 8 * (idx % GPR)]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
       const int idx = tid + NT * i;
-      if (idx < B_G) *reinterpret_cast<bf16x8*>(&Bs[buf][(idx >> 2) * LDH + 8 * (idx & 3)]) = rb[i];
+      if (idx < B_G) *reinterpret_cast<bf16x8*>(&Bs[(idx / GPR) * LDH + 8 * (idx % GPR)]) = rb[i];
     }
   };
 
@@ -377,24 +427,26 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nkt = (K + BKH - 1) / BKH;
+  const int nkt = (K + BK - 1) / BK;
   gload(0);
   sstore(0);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nkt) gload(kt + 1);
+    const __bf16* As = sbase + cur * STAGE;
+    const __bf16* Bs = As + BM * LDH;
 #pragma unroll
-    for (int ks = 0; ks < BKH / 16; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 a[FM], b[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
         a[i] = *reinterpret_cast<const bf16x8*>(
-            &As[cur][(wm * WTM + i * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+            &As[(wm * WTM + i * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         b[j] = *reinterpret_cast<const bf16x8*>(
-            &Bs[cur][(wn * WTN + j * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+            &Bs[(wn * WTN + j * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -404,37 +456,64 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
   }
+
+  // epilogue: fragment -> LDS (lane: column lane&31, rows (r&3)+8(r>>2)+4(lane>>5)) ->
+  // float4 rows (8 lanes per 32-column row)
+  float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
+  const int c4 = lane & 7;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int col = n0 + wn * WTN + j * 32 + (lane & 31);
-      if (col >= N) continue;
-      const float bcol = p.bias ? p.bias[col] : 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= M) continue;
-        float v = acc[i][j][r] * p.alpha + bcol;
-        float* dst = C + (long)row * p.ldc + col;
-        if constexpr (EPI == EPI_SWOOSHL) v = swooshl(v);
-        if constexpr (EPI == EPI_SWOOSHR) v = swooshr(v);
-        if constexpr (EPI == EPI_MULAUX) v *= aux[(long)row * p.ldaux + col];
-        if constexpr (EPI == EPI_RESADD) v += *dst;
-        *dst = v;
+      for (int r = 0; r < 16; ++r)
+        sE[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE + (lane & 31)] = acc[i][j][r];
+      __builtin_amdgcn_wave_barrier();
+      const int col = n0 + wn * WTN + j * 32 + 4 * c4;
+      float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias && col < N) bias = *reinterpret_cast<const float4*>(p.bias + col);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = (lane >> 3) + 8 * q;
+        const int row = m0 + wm * WTM + i * 32 + rl;
+        float4 v = *reinterpret_cast<const float4*>(&sE[rl * LDE + 4 * c4]);
+        if (row < M && col < N) {
+          v.x = epi_act<EPI>(fmaf(v.x, p.alpha, bias.x));
+          v.y = epi_act<EPI>(fmaf(v.y, p.alpha, bias.y));
+          v.z = epi_act<EPI>(fmaf(v.z, p.alpha, bias.z));
+          v.w = epi_act<EPI>(fmaf(v.w, p.alpha, bias.w));
+          if constexpr (EPI == EPI_MULAUX) {
+            const float4 x = *reinterpret_cast<const float4*>(aux + (long)row * p.ldaux + col);
+            v.x *= x.x; v.y *= x.y; v.z *= x.z; v.w *= x.w;
+          }
+          TC* dst = C + (long)row * p.ldc + col;
+          if constexpr (std::is_same<TC, float>::value) {
+            if constexpr (EPI == EPI_RESADD) {
+              const float4 o = *reinterpret_cast<const float4*>(dst);
+              v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            }
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            bf16x4 h;
+            h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+            *reinterpret_cast<bf16x4*>(dst) = h;
+          }
+        }
       }
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ALOAD, int EPI>
+template <int BM, int BN, int BK, int WM, int WN, int ALOAD, int EPI, typename TA, typename TC>
 void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
-  dim3 grid(cdiv(p.N, BN), cdiv(p.max_M, BM), p.slices ? p.num_slices : 1);
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, ALOAD, EPI>), grid, dim3(64 * WM * WN), 0,
-                     st, p, Bw);
+  const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
+  dim3 grid(tn * tm, 1, p.slices ? p.num_slices : 1);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC>), grid,
+                     dim3(64 * WM * WN), 0, st, p, Bw, tn);
 }
 
-template <int ALOAD, int EPI>
+template <int BK, int ALOAD, int EPI, typename TA, typename TC>
 void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
   int best = pad32;
@@ -442,15 +521,22 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
   bool big = blocks128 >= 512;
   if (BN == 128) {
-    if (big) launch_h<128, 128, 2, 2, ALOAD, EPI>(p, Bw, st);
-    else launch_h<64, 128, 2, 2, ALOAD, EPI>(p, Bw, st);
+    if (big) launch_h<128, 128, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+    else launch_h<64, 128, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
   } else if (BN == 64) {
-    if (big) launch_h<128, 64, 2, 2, ALOAD, EPI>(p, Bw, st);
-    else launch_h<64, 64, 2, 2, ALOAD, EPI>(p, Bw, st);
+    if (big) launch_h<128, 64, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+    else launch_h<64, 64, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
   } else {
-    if (big) launch_h<128, 32, 4, 1, ALOAD, EPI>(p, Bw, st);
-    else launch_h<64, 32, 2, 1, ALOAD, EPI>(p, Bw, st);
+    if (big) launch_h<128, 32, BK, 4, 1, ALOAD, EPI, TA, TC>(p, Bw, st);
+    else launch_h<64, 32, BK, 2, 1, ALOAD, EPI, TA, TC>(p, Bw, st);
   }
+}
+
+// BK = 32: at these K (72..1920) the 2-stage 64-deep variant measured 20-60 % slower (LDS
+// occupancy), tools/gemm_bench.hip
+template <int ALOAD, int EPI, typename TA, typename TC>
+void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
+  launch_tile_h<32, ALOAD, EPI, TA, TC>(p, Bw, st);
 }
 
 }  // namespace
@@ -487,24 +573,39 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
 }  // namespace zasr
 
 namespace zasr {
-void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t st) {
+void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t st,
+               bool a_bf16, bool c_bf16) {
   ZASR_REQUIRE(p.N > 0, "gemm: N must be positive");
   if (p.max_M <= 0) return;
+  ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (epi != EPI_MULAUX || p.ldaux % 4 == 0),
+               "gemm_bf16: N and the C / aux row strides must be multiples of 4");
   const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
-  if (aload == ALOAD_DENSE) {
+  if (aload == ALOAD_DENSE && !a_bf16 && !c_bf16) {
     switch (epi) {
-      case EPI_NONE: return launch_tile_h<ALOAD_DENSE, EPI_NONE>(p, B, st);
-      case EPI_SWOOSHL: return launch_tile_h<ALOAD_DENSE, EPI_SWOOSHL>(p, B, st);
-      case EPI_SWOOSHR: return launch_tile_h<ALOAD_DENSE, EPI_SWOOSHR>(p, B, st);
-      case EPI_RESADD: return launch_tile_h<ALOAD_DENSE, EPI_RESADD>(p, B, st);
+      case EPI_NONE: return launch_bk_h<ALOAD_DENSE, EPI_NONE, float, float>(p, B, st);
+      case EPI_SWOOSHL: return launch_bk_h<ALOAD_DENSE, EPI_SWOOSHL, float, float>(p, B, st);
+      case EPI_SWOOSHR: return launch_bk_h<ALOAD_DENSE, EPI_SWOOSHR, float, float>(p, B, st);
+      case EPI_RESADD: return launch_bk_h<ALOAD_DENSE, EPI_RESADD, float, float>(p, B, st);
       default: break;
     }
-  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
-    return launch_tile_h<ALOAD_CONV2, EPI_SWOOSHR>(p, B, st);
-  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR) {
-    return launch_tile_h<ALOAD_CONV3, EPI_SWOOSHR>(p, B, st);
+  } else if (aload == ALOAD_DENSE && !a_bf16 && c_bf16) {
+    switch (epi) {
+      case EPI_NONE: return launch_bk_h<ALOAD_DENSE, EPI_NONE, float, __bf16>(p, B, st);
+      case EPI_SWOOSHL: return launch_bk_h<ALOAD_DENSE, EPI_SWOOSHL, float, __bf16>(p, B, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_DENSE && a_bf16 && !c_bf16) {
+    switch (epi) {
+      case EPI_NONE: return launch_bk_h<ALOAD_DENSE, EPI_NONE, __bf16, float>(p, B, st);
+      case EPI_RESADD: return launch_bk_h<ALOAD_DENSE, EPI_RESADD, __bf16, float>(p, B, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR && !a_bf16 && !c_bf16) {
+    return launch_bk_h<ALOAD_CONV2, EPI_SWOOSHR, float, float>(p, B, st);
+  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR && !a_bf16 && !c_bf16) {
+    return launch_bk_h<ALOAD_CONV3, EPI_SWOOSHR, float, float>(p, B, st);
   }
-  throw std::runtime_error("gemm_bf16: unsupported (aload, epi) combination");
+  throw std::runtime_error("gemm_bf16: unsupported (aload, epi, operand types) combination");
 }
 }  // namespace zasr
 

@@ -84,11 +84,14 @@ struct AttnSAArgs {
   const int* row_off;
   int nseq;
   int max_len;
-  const float* stats;      // from attn_softmax
+  const float* stats;      // [R][H][2] row max, 1 / row sum (read unless online)
   const float* v;          // [R][12H]
   float* out;              // [R][12H]
+  float* stats_out;        // online: the statistics computed here, same layout
 };
-void launch_attn_sa(const AttnSAArgs& a, hipStream_t st);
+// online = running softmax statistics (first self-attention of a layer, writes stats_out);
+// bf16 = QK^T / PV on bf16 MFMA (the bf16 precision mode)
+void launch_attn_sa(const AttnSAArgs& a, bool online, bool bf16, hipStream_t st);
 
 // ---- transducer search (core/asr_engine.py:1023-1153) ----
 struct SearchState {

@@ -589,6 +589,7 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     }
   }
   __syncthreads();
+  ZASR_STAMP(3);
   // ---- 3. expansion, hotwords, dedup (serial over <= beam candidates, all in LDS) ----
   if (tid == 0) {
     const int total = n * V;
