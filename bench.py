@@ -54,39 +54,62 @@ def make_chunks(audio_sec: float, seed: int):
     return chunks
 
 
-def gemm_flops(cfg, L_list):
-    """Algorithmic FLOPs of the encoder's dense projections + frontend convs (as GEMMs)."""
-    f_enc = 0.0
-    for L in L_list:
-        T = 2 * L + 7
-        L2 = (T - 3) // 2
-        f_enc += 2.0 * (L2 * 39 * 72 * 32 + L * 19 * 288 * 128 + 2 * L * 19 * 128 * 384
-                        + L * 2432 * cfg.encoder_dims[0])
-        for i, d in enumerate(cfg.encoder_dims):
-            R = -(-L // cfg.downsampling[i])
-            F, h = cfg.ff_dims[i], cfg.num_heads[i]
-            hid = 3 * d // 4
-            per_row = ((2 * cfg.query_head_dim + cfg.pos_head_dim) * h * d
-                       + 2 * (2 * cfg.value_head_dim * h * d)
-                       + 2 * ((F * 3) // 4 + F + (F * 5) // 4) * d
-                       + 3 * hid * d + hid * d + 2 * (2 * d * d + d * d))
-            f_enc += 2.0 * R * per_row * cfg.num_layers[i]
-        f_enc += 2.0 * ((L + 1) // 2) * cfg.max_dim * cfg.joiner_dim
-    return f_enc
+def enc_gemm_work(cfg, L_list, bf16: bool):
+    """Algorithmic work of the launches in the `enc_gemm` class (every Engine::linear of the
+    encoder: ConvNeXt pw1/pw2 + embed out, the stack projections, encoder_proj), per step.
+
+    Returns (flops, bytes).  Bytes per launch = A read (f32 activations) + weights (bf16 in
+    the bf16 mode, f32 otherwise) + C write (f32) + C read for the residual epilogue."""
+    wb = 2 if bf16 else 4
+    flops = 0.0
+    nbytes = 0.0
+
+    def lin(M, K, N, resadd=False):
+        nonlocal flops, nbytes
+        if M <= 0:
+            return
+        flops += 2.0 * M * K * N
+        nbytes += 4.0 * M * K + wb * N * K + 4.0 * M * N * (2 if resadd else 1)
+
+    d0 = cfg.encoder_dims[0]
+    Ls = [L for L in L_list if L > 0]
+    Lsum = sum(Ls)
+    lin(19 * Lsum, 128, 384)
+    lin(19 * Lsum, 384, 128, True)
+    lin(Lsum, 128 * 19, d0)
+    for i, d in enumerate(cfg.encoder_dims):
+        R = sum(-(-L // cfg.downsampling[i]) for L in Ls)
+        F, h = cfg.ff_dims[i], cfg.num_heads[i]
+        hid = 3 * d // 4
+        for _ in range(cfg.num_layers[i]):
+            lin(R, d, (2 * cfg.query_head_dim + cfg.pos_head_dim) * h)
+            for f in ((F * 3) // 4, F, (F * 5) // 4):
+                lin(R, d, f)
+                lin(R, f, d, True)
+            lin(R, d, 3 * hid)
+            lin(R, hid, d, True)
+            for _ in range(2):
+                lin(R, d, cfg.value_head_dim * h)
+                lin(R, cfg.value_head_dim * h, d, True)
+                lin(R, d, 2 * d)
+                lin(R, d, d, True)
+    lin(sum((L + 1) // 2 for L in Ls), cfg.max_dim, cfg.joiner_dim)
+    return flops, nbytes
 
 
-def attn_bytes(cfg, L_list):
-    """HBM bytes of the materialised attention weights: 1 write + 3 reads (nonlin head 0,
-    self_attn1, self_attn2) per layer, f32."""
-    w = r = 0.0
-    for L in L_list:
-        for i in range(cfg.num_stacks):
-            R = -(-L // cfg.downsampling[i])
-            R4 = (R + 3) // 4 * 4
-            per = 4.0 * cfg.num_heads[i] * R * R4 * cfg.num_layers[i]
-            w += per
-            r += per * 2 + per / cfg.num_heads[i]
-    return w, r
+def pmc_traffic(kernel_class, args):
+    """HBM bytes per launch of the dominant class from a committed rocprofv3 PMC pass of this
+    same configuration (tools/pmc_traffic.py writes it: FETCH_SIZE x2 (gfx950 correction) +
+    WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return None
+    key = f"{args.model}|{args.method}|{args.beam if args.method != 'greedy_search' else 1}|" \
+          f"{args.precision}|{int(args.audio_sec)}|{kernel_class}"
+    return tab.get(key)
 
 
 def cpu_baseline(model_dir_cfg, weights, chunks, method_beam, budget_s=20.0):
@@ -131,7 +154,7 @@ def main():
     ap.add_argument("--method", default="greedy_search")
     ap.add_argument("--beam", type=int, default=8)
     ap.add_argument("--audio-sec", type=float, default=3600.0)
-    ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-out", default="")
     args = ap.parse_args()
@@ -181,9 +204,8 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=f"cuda:{local}")
         dist.barrier()
 
     # kernel-class timing: HIP events recorded by the library on its launch stream over
@@ -204,40 +226,50 @@ def main():
     tprime = sum(int(r.T) for r in res)
 
     L_list = [((n + 80) // 160 - 7) // 2 for n in lens]
-    f_gemm = gemm_flops(cfg, L_list)
-    aw, ar = attn_bytes(cfg, L_list)
+    bf16 = args.precision == "bf16"
+    f_gemm, b_gemm = enc_gemm_work(cfg, L_list, bf16)
     rows_joiner = sum(min(beam, 8) * ((L + 1) // 2) for L in L_list)
     f_join = 2.0 * rows_joiner * cfg.joiner_dim * cfg.vocab_size
     classes = {k: v for k, v in prof.items()}
     dom = max(classes.items(), key=lambda kv: kv[1][1])[0] if classes else None
-    peak_mfma = MFMA_F32_PEAK_TFLOPS if args.precision == "fp32" else MFMA_BF16_PEAK_TFLOPS
+    peak_mfma = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_F32_PEAK_TFLOPS
     roof = None
     if dom:
         cnt, ms = classes[dom]
-        per_launch_ms = ms / cnt
-        if dom in ("enc_gemm", "frontend_conv"):
-            work = f_gemm * nprof / cnt  # FLOPs per launch (class average)
-            ach = work / (per_launch_ms * 1e-3) / 1e12
-            roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2),
-                    "peak": peak_mfma, "unit": "TFLOP/s", "frac": round(ach / peak_mfma, 4),
-                    "traffic": None}
+        per_launch_s = ms / cnt * 1e-3
+        if dom == "enc_gemm":
+            # the binding roof is the larger of bytes / HBM peak and flops / MFMA peak
+            fl, by = f_gemm * nprof / cnt, b_gemm * nprof / cnt  # per launch (class mean)
+            if by / (HBM_PEAK_GBS * 1e9) >= fl / (peak_mfma * 1e12):
+                ach = by / per_launch_s / 1e9
+                roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes_per_launch": round(by),
+                        "mfma_tflops": round(fl / per_launch_s / 1e12, 2)}
+            else:
+                ach = fl / per_launch_s / 1e12
+                roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2),
+                        "peak": peak_mfma, "unit": "TFLOP/s",
+                        "frac": round(ach / peak_mfma, 4), "traffic": None,
+                        "algorithmic_flops_per_launch": round(fl),
+                        "hbm_gbs": round(by / per_launch_s / 1e9, 1)}
         elif dom == "joiner":
             work = f_join * nprof / cnt
-            ach = work / (per_launch_ms * 1e-3) / 1e12
+            ach = work / per_launch_s / 1e12
             roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2),
                     "peak": peak_mfma, "unit": "TFLOP/s", "frac": round(ach / peak_mfma, 4),
                     "traffic": None}
-        elif dom in ("attn_apply", "attn_softmax"):
-            b = (ar if dom == "attn_apply" else aw) * nprof / cnt
-            ach = b / (per_launch_ms * 1e-3) / 1e9
-            roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": None}
         else:
+            # search step / decoder: one block per stream per frame, latency-bound
             roof = {"kernel": dom, "bound": "latency", "achieved": None, "peak": None,
                     "unit": None, "frac": None, "traffic": None}
-        roof["avg_launch_ms"] = round(per_launch_ms, 4)
+        roof["avg_launch_ms"] = round(per_launch_s * 1e3, 4)
         roof["launches_per_step"] = cnt // nprof
+        tr = pmc_traffic(dom, args)
+        if tr is not None:
+            roof["traffic"] = tr["bytes_per_launch"]
+            roof["traffic_source"] = tr["source"]
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:

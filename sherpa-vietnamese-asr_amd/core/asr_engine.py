@@ -293,14 +293,28 @@ def decode_chunk(recognizer, audio_chunk, time_offset=0.0, precomputed_features=
 
 def decode_chunks(recognizer, chunks: Sequence[np.ndarray], time_offsets: Sequence[float],
                   precomputed_features: Optional[Sequence[np.ndarray]] = None):
-    """Batched decode_chunk: every chunk goes through one GPU pass (fbank, encoder, search)."""
+    """Batched decode_chunk: every chunk goes through one GPU pass (fbank, encoder, search).
+
+    Under an initialised torch.distributed group (one process per GPU) each rank decodes its
+    LPT share of the chunks and every rank receives all word lists in chunk order
+    (zasr.shard.decode_sharded; host-side gather, no GPU collective)."""
+    from zasr.shard import decode_sharded
     beam = recognizer.get("max_active_paths", 8)
     h: Recognizer = recognizer["handle"]
-    if precomputed_features is not None:
-        res = h.decode_features([np.asarray(f, np.float32) for f in precomputed_features], beam=beam)
-    else:
-        res = h.decode([np.asarray(c, np.float32) for c in chunks], beam=beam)
-    return [_words_from_search(recognizer["id2token"], recognizer["vocab_size"], len(c), off,
-                               r.token_ids.tolist(), r.frames.tolist(), r.log_probs.tolist(),
-                               int(r.T), [TokenStats(s) for s in r.stats])
-            for c, off, r in zip(chunks, time_offsets, res)]
+    id2token, V = recognizer["id2token"], recognizer["vocab_size"]
+    items = list(zip(chunks, time_offsets,
+                     precomputed_features if precomputed_features is not None else [None] * len(chunks)))
+
+    def run(part):
+        if not part:
+            return []
+        if precomputed_features is not None:
+            res = h.decode_features([np.asarray(f, np.float32) for _, _, f in part], beam=beam)
+        else:
+            res = h.decode([np.asarray(c, np.float32) for c, _, _ in part], beam=beam)
+        return [_words_from_search(id2token, V, len(c), off, r.token_ids.tolist(),
+                                   r.frames.tolist(), r.log_probs.tolist(), int(r.T),
+                                   [TokenStats(s) for s in r.stats])
+                for (c, off, _), r in zip(part, res)]
+
+    return decode_sharded(run, items, lengths=[len(c) for c in chunks])

@@ -410,7 +410,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
       l.wh = p;
     };
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
-                    &model_.enc_proj, &model_.dec_proj, &model_.joiner})
+                    &model_.enc_proj, &model_.joiner})
       mk(*l);
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
@@ -421,6 +421,21 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
           for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mk(*l);
       }
     ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  // ---- decoder-context table (kernels.h, DecTable): V^2 x D f32, built once ----
+  {
+    const double gb = (double)cfg.V * cfg.V * cfg.joiner_dim * 4.0 / 1e9;
+    double max_gb = 24.0;
+    if (const char* e = getenv("ZASR_DEC_TABLE_MAX_GB")) max_gb = atof(e);
+    if (gb <= max_gb) {
+      void* p = nullptr;
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)cfg.V * cfg.V * cfg.joiner_dim * sizeof(float)));
+      model_.allocations.push_back(p);
+      model_.dec_table = reinterpret_cast<float*>(p);
+      DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, cfg.joiner_dim};
+      launch_dec_table(dw, model_.dec_proj.w, cfg.V, model_.dec_table, stream_);
+      ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
   }
 
   // ---- fbank tables ----
@@ -1032,58 +1047,40 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     ZASR_HIP_CHECK(hipMemsetAsync(st.stamps, 0, (size_t)Tmax * 8 * 8, st_));
   }
   float* logits = ws<float>("se_logits", slots * V);
-  if (model_.joiner.wh) {
-    // bf16 mode: 2 launches per frame (bf16 joiner; search step + decoder for changed slots)
-    __bf16* Jh = ws<__bf16>("se_joinin_h", slots * D);
-    ZASR_HIP_CHECK(hipMemsetAsync(Jh, 0, slots * D * sizeof(__bf16), st_));
-    float* dec_a = ws<float>("se_dec_a", slots * D);
-    float* dec_b = ws<float>("se_dec_b", slots * D);
-    FusedDec fd{model_.dec_tap0, model_.dec_tap1, reinterpret_cast<const __bf16*>(model_.dec_proj.wh),
-                model_.dec_proj.b, dec_a, dec_b, d_enc, d_eo, d_el, Jh, D};
-    prof_begin("search");
-    launch_search_init(st, S, H, st_);
-    FusedDec fi = fd;
-    fi.dec_new = dec_a;
-    launch_fused_init(fi, S, H, st_);
-    prof_end();
-    int active = S;
-    for (int t = 0; t < Tmax; ++t) {
-      while (active > 0 && el[active - 1] <= t) --active;
-      const int rows = active * H;
-      JoinerBf16Args ja{Jh, reinterpret_cast<const __bf16*>(model_.joiner.wh), model_.joiner.b,
-                        logits, rows, V, D};
-      prof_begin("joiner");
-      launch_joiner_bf16(ja, st_);
-      prof_end();
-      fd.dec_old = dec_a;
-      fd.dec_new = dec_b;
-      prof_begin("search");
-      launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, &fd, st_);
-      prof_end();
-      std::swap(dec_a, dec_b);
-    }
-  } else {
-    float* J = ws<float>("se_joinin", slots * D);
-    DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
-    prof_begin("search");
-    launch_search_init(st, S, H, st_);
-    prof_end();
-    int active = S;
-    for (int t = 0; t < Tmax; ++t) {
-      while (active > 0 && el[active - 1] <= t) --active;
-      const int rows = active * H;
-      DecJoinArgs da{dw, model_.dec_proj.w, st.y1, st.y2, d_enc, d_eo, J, rows, H, t};
+  const bool bf16 = model_.joiner.wh != nullptr;
+  void* J = bf16 ? (void*)ws<__bf16>("se_joinin_h", slots * D) : (void*)ws<float>("se_joinin", slots * D);
+  ZASR_HIP_CHECK(hipMemsetAsync(J, 0, slots * D * (bf16 ? 2 : 4), st_));
+  DecTable dt{model_.dec_table, V, d_enc, d_eo, d_el, J, D, bf16 ? 1 : 0};
+  DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
+  prof_begin("search");
+  launch_search_init(st, S, H, st_);
+  if (model_.dec_table) launch_table_init(dt, S, H, st_);
+  prof_end();
+  // per frame: [decoder + J when there is no table] -> joiner -> search step (which writes
+  // the next frame's J from the table)
+  int active = S;
+  for (int t = 0; t < Tmax; ++t) {
+    while (active > 0 && el[active - 1] <= t) --active;
+    const int rows = active * H;
+    if (!model_.dec_table) {
+      DecJoinArgs da{dw, model_.dec_proj.w, st.y1, st.y2, d_enc, d_eo, J, rows, H, t, bf16 ? 1 : 0};
       prof_begin("decoder");
       launch_decjoin(da, st_);
       prof_end();
-      JoinerArgs ja{J, model_.joiner.w, model_.joiner.b, logits, rows, V, D};
-      prof_begin("joiner");
-      launch_joiner(ja, st_);
-      prof_end();
-      prof_begin("search");
-      launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, nullptr, st_);
-      prof_end();
     }
+    prof_begin("joiner");
+    if (bf16) {
+      JoinerBf16Args ja{reinterpret_cast<const __bf16*>(J), reinterpret_cast<const __bf16*>(model_.joiner.wh),
+                        model_.joiner.b, logits, rows, V, D};
+      launch_joiner_bf16(ja, st_);
+    } else {
+      JoinerArgs ja{reinterpret_cast<const float*>(J), model_.joiner.w, model_.joiner.b, logits, rows, V, D};
+      launch_joiner(ja, st_);
+    }
+    prof_end();
+    prof_begin("search");
+    launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, model_.dec_table ? &dt : nullptr, st_);
+    prof_end();
   }
   const int cap = Tmax;
   int* o_tok = ws<int>("so_tok", (size_t)S * cap);
@@ -1115,7 +1112,7 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
       ++n;
     }
     fprintf(stderr, "[zasr stamps] frames=%d mean cycles: load %.0f stats %.0f topk %.0f expand %.0f "
-            "state+dec %.0f J %.0f\n", n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n,
+            "state %.0f J %.0f\n", n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n,
             acc[5] / n, acc[6] / n);
   }
   for (int i = 0; i < S; ++i) {

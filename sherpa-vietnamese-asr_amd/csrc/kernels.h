@@ -137,8 +137,9 @@ struct DecJoinArgs {
   const int* y2;
   const float* enc;      // [sum T'][D]
   const int* enc_off;    // [S]
-  float* J;              // [M][D] = tanh(enc[s, t] + dec[slot])
+  void* J;               // [M][D] = tanh(enc[s, t] + dec[slot]), f32 or bf16 (j_bf16)
   int M, H, t;
+  int j_bf16;
 };
 struct JoinerArgs {
   const float* J;        // [M][D]
@@ -147,20 +148,6 @@ struct JoinerArgs {
   float* out;            // [M][V]
   int M, V, D;
 };
-// bf16 search mode: decoder runs inside the search step for changed slots only
-struct FusedDec {
-  const float* tap0;        // [V][D]
-  const float* tap1;        // [V][D]
-  const __bf16* wp;         // decoder_proj weight, bf16 [D][D]
-  const float* bp;          // [D]
-  const float* dec_old;     // [S*H][D] decoder rows of the current slots
-  float* dec_new;           // [S*H][D] decoder rows of the next slots
-  const float* enc;         // [sum T'][D]
-  const int* enc_off;       // [S]
-  const int* enc_len;       // [S]
-  __bf16* J;                // [S*H][D] joiner input of the next frame
-  int D;
-};
 struct JoinerBf16Args {
   const __bf16* J;       // [M][D]
   const __bf16* W;       // [V][D]
@@ -168,15 +155,33 @@ struct JoinerBf16Args {
   float* out;            // [M][V]
   int M, V, D;
 };
+// Decoder-context table: the stateless decoder is a pure function of the two-token context
+// (y_-2, y_-1) (core/asr_engine.py:1051-1056, 1072-1088 cache it per context), so the engine
+// evaluates it once for all V^2 contexts at model load (8.2 GB f32 at V = 2000, D = 512 --
+// small against 288 GB of HBM) and the search step turns a new hypothesis into the next
+// frame's joiner input with one row gather:  J[slot] = tanh(enc[s, t + 1] + table[y2 V + y1]).
+struct DecTable {
+  const float* table;       // [V * V][D]
+  int V;
+  const float* enc;         // [sum T'][D]
+  const int* enc_off;       // [S]
+  const int* enc_len;       // [S]
+  void* J;                  // [S*H][D] joiner input of the next frame (bf16 if j_bf16)
+  int D;
+  int j_bf16;
+};
 void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st);
 void launch_decjoin(const DecJoinArgs& a, hipStream_t st);
 void launch_joiner(const JoinerArgs& j, hipStream_t st);
 void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st);
-void launch_fused_init(const FusedDec& fd, int S, int Hmax, hipStream_t st);
-// fd == nullptr: decoder handled by decjoin (fp32 mode)
+// table[(y2 V + y1) D + n] = decoder_proj(relu(conv(E[y2], E[y1])))[n], all V^2 contexts
+void launch_dec_table(const DecoderW& dw, const float* wp, int V, float* table, hipStream_t st);
+// J of frame 0 for slot 0 of every stream (context (0, 0))
+void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st);
+// dt == nullptr: the next frame's J comes from launch_decjoin
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
                         int beam, int t, const int* enc_len, const HotwordTables& hw,
-                        const FusedDec* fd, hipStream_t st);
+                        const DecTable* dt, hipStream_t st);
 void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTables& hw,
                          int out_cap, int* out_tok, int* out_frame, double* out_lp,
                          float4* out_stats, int* out_count, hipStream_t st);

@@ -1,11 +1,8 @@
 // Transducer search on device: modified beam search (greedy = beam 1) with Aho-Corasick
 // hotword biasing, restating core/asr_engine.py:1023-1153 and core/hotword_context.py.
 //
-// Per frame t, three launches:
-//   decjoin_kernel     J[slot] = tanh(enc[s, t] + decoder(y[-2], y[-1]))  -- Embedding ->
-//                      grouped Conv1d -> ReLU -> decoder_proj (MFMA), the reference's
-//                      dec_sess/dec_cache (:1072-1088) recomputed per live slot
-//   joiner_kernel      logits[S*H, V] = W_out J + b                           (:1090-1093)
+// Per frame t, two launches:
+//   joiner             logits[S*H, V] = W_out J + b                           (:1090-1093)
 //   search_step_kernel one block per stream:
 //     1. per live hypothesis row: max, second max, sum exp, entropy terms (the reference's
 //        f32 numpy log-softmax :1096-1098 and _compute_token_entropy :1159-1181)
@@ -15,6 +12,12 @@
 //        appends, hotword delta after top-k (:1127-1131), duplicates of the full token
 //        sequence (identified by (length, 64-bit rolling hash)) merge with an f64 log-add;
 //        emissions append a node {token, frame, parent, token logp, row stats}
+//     4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + dec(y[-2], y[-1]))
+//        gathered from the decoder-context table (kernels.h, DecTable) -- the reference's
+//        dec_sess / dec_cache (:1051-1056, :1072-1088) evaluated once per context at load.
+// Without the table (vocabularies too large for it) a third launch, decjoin_kernel,
+// recomputes the decoder for every live slot (Embedding -> grouped Conv1d -> ReLU ->
+// decoder_proj on MFMA) and writes J.
 // All hypothesis state lives in LDS during the step; global memory is written once.
 #include "common.h"
 #include "kernels.h"
@@ -122,44 +125,10 @@ __device__ __forceinline__ void splitk_reduce(f32x16& acc, float* red) {
 }
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 // tanh(x) = 1 - 2 / (exp(2x) + 1): saturates correctly at +-inf (bf16 joiner input only)
 __device__ __forceinline__ float fast_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
-
-// dec[j][n] = bp[n] + sum_k Wp[n][k] x[j][k] for j < nc (x: LDS [32][D + 8] bf16 rows,
-// zero past nc), bf16 MFMA 32x32x16 with f32 accumulate; waves split the output columns.
-// Results go to LDS rows out[j][D] (f32).
-__device__ __forceinline__ void dec_rows_bf16(const __bf16* xs, int nc, const __bf16* wp,
-                                              const float* bp, int D, float* out) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int col = lane & 31, h = lane >> 5;
-  const int ldx = D + 8;
-  for (int ct = wid; ct < D / 32; ct += 4) {
-    const int n = ct * 32 + col;
-    const __bf16* wrow = wp + (long)n * D + 8 * h;
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    for (int k0 = 0; k0 < D; k0 += 128) {
-      bf16x8 b[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (k0 + 16 * q < D) b[q] = *reinterpret_cast<const bf16x8*>(wrow + k0 + 16 * q);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (k0 + 16 * q >= D) break;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(xs + col * ldx + k0 + 16 * q + 8 * h);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[q], acc, 0, 0, 0);
-      }
-    }
-    const float bb = bp[n];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (row < nc) out[row * D + n] = acc[r] + bb;
-    }
-  }
-}
 
 // diagnostic phase stamp (block 0, thread 0 only; st.stamps null in normal runs)
 #define ZASR_STAMP(slot)                                                                  \
@@ -230,7 +199,11 @@ __global__ __launch_bounds__(256) void decjoin_kernel(DecJoinArgs a) {
       if (row >= a.M) continue;
       const int s = row / a.H;
       const float e = a.enc[(long)(a.enc_off[s] + a.t) * D + n];
-      a.J[(long)row * D + n] = tanhf(e + (acc[r] + bp));
+      const float v = tanhf(e + (acc[r] + bp));
+      if (a.j_bf16)
+        reinterpret_cast<__bf16*>(a.J)[(long)row * D + n] = (__bf16)v;
+      else
+        reinterpret_cast<float*>(a.J)[(long)row * D + n] = v;
     }
   }
 }
@@ -245,6 +218,61 @@ void launch_decjoin(const DecJoinArgs& a, hipStream_t st) {
     case 4: hipLaunchKernelGGL(decjoin_kernel<4>, grid, dim3(256), lds, st, a); break;
     case 8: hipLaunchKernelGGL(decjoin_kernel<8>, grid, dim3(256), lds, st, a); break;
     case 16: hipLaunchKernelGGL(decjoin_kernel<16>, grid, dim3(256), lds, st, a); break;
+    default: throw std::runtime_error("decoder dim must be 64, 128, 256 or 512");
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// decoder-context table: rows r = y2 * V + y1, the decjoin arithmetic (same K split, same
+// reduction order) so that table rows equal the per-slot decoder bit for bit.
+// --------------------------------------------------------------------------------------
+template <int NQ>
+__global__ __launch_bounds__(256) void dec_table_kernel(DecoderW dw, const float* __restrict__ wp,
+                                                        int V, float* __restrict__ table) {
+  extern __shared__ float smem[];
+  const int D = dw.D;
+  const int lda = D + 4;
+  float* As = smem;
+  float* red = smem + 32 * lda;
+  const long M = (long)V * V;
+  const long m0 = (long)blockIdx.x * 32;
+  const int n0 = blockIdx.y * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int d4 = D / 4;
+  for (int e = tid; e < 32 * d4; e += 256) {
+    const int i = e / d4, c4 = e - i * d4;
+    const long r = m0 + i;
+    const float4 v = (r < M) ? dec_conv4(dw, (int)(r / V), (int)(r % V), 4 * c4)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(As + i * lda + 4 * c4) = v;
+  }
+  __syncthreads();
+  const int n = n0 + (lane & 31);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  tile32_splitk<NQ>(As, lda, wp + (long)n * D, true, wid * (D / 4), acc);
+  splitk_reduce(acc, red);
+  if (wid == 0) {
+    const float bp = dw.bp[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long row = m0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) table[row * D + n] = acc[r] + bp;
+    }
+  }
+}
+
+void launch_dec_table(const DecoderW& dw, const float* wp, int V, float* table, hipStream_t st) {
+  ZASR_REQUIRE(dw.D % 32 == 0 && dw.D <= 512, "decoder dim must be a multiple of 32, <= 512");
+  const long M = (long)V * V;
+  dim3 grid((unsigned)cdivl(M, 32), dw.D / 32);
+  size_t lds = (32 * (dw.D + 4) + 3 * 16 * 64) * sizeof(float);
+  switch (dw.D / 32) {
+    case 2: hipLaunchKernelGGL(dec_table_kernel<2>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 4: hipLaunchKernelGGL(dec_table_kernel<4>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 8: hipLaunchKernelGGL(dec_table_kernel<8>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 16: hipLaunchKernelGGL(dec_table_kernel<16>, grid, dim3(256), lds, st, dw, wp, V, table); break;
     default: throw std::runtime_error("decoder dim must be 64, 128, 256 or 512");
   }
 }
@@ -303,39 +331,36 @@ void launch_joiner(const JoinerArgs& j, hipStream_t st) {
 
 // --------------------------------------------------------------------------------------
 // bf16 joiner: logits = W_out J + b with J, W_out in bf16 (v_mfma_f32_32x32x16_bf16, f32
-// accumulate).  Block = 4 waves = 128 rows x 32 vocab columns; every wave streams its own
-// 32 J rows and the shared 32 W_out rows straight from global (no LDS, no barrier).
+// accumulate).  Block = 32 rows x 32 vocab columns; the 4 waves split K (each issues all of
+// its J / W_out fragment loads at once: one memory round trip), partial tiles reduced
+// through LDS.  Grid = V/32 x M/32 blocks (>= 250 at greedy batch 120: the whole chip).
 // --------------------------------------------------------------------------------------
+template <int NK>  // NK = D / 64 k16-steps per wave
 __global__ __launch_bounds__(256) void joiner_bf16_kernel(JoinerBf16Args j) {
+  __shared__ float red[3 * 16 * 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int col = lane & 31, h = lane >> 5;
-  const int m0 = blockIdx.y * 128 + wid * 32;
-  if (m0 >= j.M) return;
+  const int m0 = blockIdx.y * 32;
   const int n = blockIdx.x * 32 + col;
   const bool nv = n < j.V;
   const int D = j.D;
   const int ar = m0 + col < j.M ? m0 + col : j.M - 1;
-  const __bf16* arow = j.J + (long)ar * D + 8 * h;
-  const __bf16* brow = j.W + (long)(nv ? n : 0) * D + 8 * h;
+  const int kb = wid * (D / 4) + 8 * h;
+  const __bf16* arow = j.J + (long)ar * D + kb;
+  const __bf16* brow = j.W + (long)(nv ? n : 0) * D + kb;
+  bf16x8 a[NK], b[NK];
+#pragma unroll
+  for (int q = 0; q < NK; ++q) {
+    a[q] = *reinterpret_cast<const bf16x8*>(arow + 16 * q);
+    b[q] = *reinterpret_cast<const bf16x8*>(brow + 16 * q);
+  }
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int k0 = 0; k0 < D; k0 += 128) {
-    bf16x8 a[8], b[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (k0 + 16 * q < D) {
-        a[q] = *reinterpret_cast<const bf16x8*>(arow + k0 + 16 * q);
-        b[q] = *reinterpret_cast<const bf16x8*>(brow + k0 + 16 * q);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (k0 + 16 * q >= D) break;
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b[q], acc, 0, 0, 0);
-    }
-  }
-  if (!nv) return;
+  for (int q = 0; q < NK; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b[q], acc, 0, 0, 0);
+  splitk_reduce(acc, red);
+  if (wid != 0 || !nv) return;
   const float bias = j.bias[n];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -346,51 +371,58 @@ __global__ __launch_bounds__(256) void joiner_bf16_kernel(JoinerBf16Args j) {
 
 void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
   if (j.M <= 0) return;
-  ZASR_REQUIRE(j.D % 16 == 0, "joiner_dim must be a multiple of 16");
-  dim3 grid(cdiv(j.V, 32), cdiv(j.M, 128));
-  hipLaunchKernelGGL(joiner_bf16_kernel, grid, dim3(256), 0, st, j);
-}
-
-// decoder output of context (0, 0) into slot 0 of every stream, and J for frame 0
-__global__ __launch_bounds__(256) void fused_init_kernel(FusedDec fd, int Hmax) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int D = fd.D;
-  __bf16* xs = reinterpret_cast<__bf16*>(smem_raw);                    // [32][D + 8]
-  float* dl = reinterpret_cast<float*>(smem_raw + 32 * (D + 8) * 2);  // [16][D]
-  const int s = blockIdx.x;
-  const int base = s * Hmax;
-  for (int e = threadIdx.x; e < 32 * (D + 8); e += 256) {
-    const int i = e / (D + 8), c = e - i * (D + 8);
-    float v = 0.f;
-    if (i == 0 && c < D) v = fmaxf(fd.tap0[c] + fd.tap1[c], 0.f);  // tokens (0, 0)
-    xs[e] = (__bf16)v;
-  }
-  __syncthreads();
-  dec_rows_bf16(xs, 1, fd.wp, fd.bp, D, dl);
-  __syncthreads();
-  const bool has_t = fd.enc_len[s] > 0;
-  for (int c = threadIdx.x; c < D; c += 256) {
-    const float d = dl[c];
-    fd.dec_new[(long)base * D + c] = d;
-    if (has_t)
-      fd.J[(long)base * D + c] = (__bf16)tanhf(fd.enc[(long)fd.enc_off[s] * D + c] + d);
+  dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
+  switch (j.D) {
+    case 64: hipLaunchKernelGGL(joiner_bf16_kernel<1>, grid, dim3(256), 0, st, j); break;
+    case 128: hipLaunchKernelGGL(joiner_bf16_kernel<2>, grid, dim3(256), 0, st, j); break;
+    case 256: hipLaunchKernelGGL(joiner_bf16_kernel<4>, grid, dim3(256), 0, st, j); break;
+    case 512: hipLaunchKernelGGL(joiner_bf16_kernel<8>, grid, dim3(256), 0, st, j); break;
+    default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
   }
 }
 
-void launch_fused_init(const FusedDec& fd, int S, int Hmax, hipStream_t st) {
+__device__ __forceinline__ void store_j4(const DecTable& dt, long off, float4 e, float4 d) {
+  if (dt.j_bf16) {
+    bf16x4 v;
+    v[0] = (__bf16)fast_tanh(e.x + d.x);
+    v[1] = (__bf16)fast_tanh(e.y + d.y);
+    v[2] = (__bf16)fast_tanh(e.z + d.z);
+    v[3] = (__bf16)fast_tanh(e.w + d.w);
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(dt.J) + off) = v;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(dt.J) + off) =
+        make_float4(tanhf(e.x + d.x), tanhf(e.y + d.y), tanhf(e.z + d.z), tanhf(e.w + d.w));
+  }
+}
+
+// J of frame 0, slot 0 of stream s: context (0, 0) = table row 0
+__global__ void table_init_kernel(DecTable dt, int S, int Hmax) {
+  const int d4 = dt.D / 4;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)S * d4) return;
+  const int s = (int)(i / d4), c4 = (int)(i - (long)s * d4);
+  if (dt.enc_len[s] <= 0) return;
+  const float4 e = *reinterpret_cast<const float4*>(dt.enc + (long)dt.enc_off[s] * dt.D + 4 * c4);
+  const float4 d = *reinterpret_cast<const float4*>(dt.table + 4 * c4);
+  store_j4(dt, (long)s * Hmax * dt.D + 4 * c4, e, d);
+}
+
+void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st) {
   if (S <= 0) return;
-  size_t lds = 32 * (fd.D + 8) * 2 + 16 * fd.D * 4;
-  hipLaunchKernelGGL(fused_init_kernel, dim3(S), dim3(256), lds, st, fd, Hmax);
+  ZASR_REQUIRE(dt.D % 4 == 0, "joiner dim must be a multiple of 4");
+  const long n = (long)S * (dt.D / 4);
+  hipLaunchKernelGGL(table_init_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, dt, S, Hmax);
 }
 
 // --------------------------------------------------------------------------------------
-template <int KB, bool FUSED>
+template <int KB, bool TABLE>
 __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const float* logits,
                                                           int V, int Hmax, int beam, int t,
                                                           const int* enc_len, HotwordTables hw,
-                                                          FusedDec fd) {
+                                                          DecTable dt) {
   const int s = blockIdx.x;
-  if (t >= enc_len[s]) return;
+  const int T_s = enc_len[s];
+  if (t >= T_s) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -404,15 +436,20 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   // new hypotheses
   __shared__ double nLp[kMaxBeam];
   __shared__ int nLpf[kMaxBeam], nLen[kMaxBeam], nY1[kMaxBeam], nY2[kMaxBeam], nHw[kMaxBeam],
-      nNode[kMaxBeam], nParent[kMaxBeam], nChanged[kMaxBeam];
+      nNode[kMaxBeam], nParent[kMaxBeam];
   __shared__ unsigned long long nHash[kMaxBeam];
   // row statistics
   __shared__ float sMax[kMaxBeam], sLogSum[kMaxBeam];
   __shared__ float4 sStats[kMaxBeam];
   __shared__ float rA[4], rB[4], rC[4];
   __shared__ unsigned long long cK[4 * KB];
-  __shared__ int sN, sNN, sNodeCnt, sNC;
-  __shared__ int chSlot[kMaxBeam], chIdx[kMaxBeam];
+  __shared__ int sN, sNN, sNodeCnt, sK;
+  // candidates of this frame (after top-k), decoded in parallel
+  __shared__ unsigned long long cand[kMaxBeam], cHash[kMaxBeam];
+  __shared__ double cScore[kMaxBeam];
+  __shared__ float cVal[kMaxBeam];
+  __shared__ int cHi[kMaxBeam], cTok[kMaxBeam], cLen[kMaxBeam], cY1[kMaxBeam], cY2[kMaxBeam],
+      cHw[kMaxBeam];
 
   ZASR_STAMP(0);
   if (tid == 0) {
@@ -432,6 +469,13 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     pNode[tid] = st.node[base + tid];
   }
   const float* rows = logits + (long)base * V;
+  // the next frame's encoder row (independent of this frame's result): in flight now
+  float4 ev = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool next = t + 1 < T_s;
+  if constexpr (TABLE) {
+    if (next && tid < dt.D / 4)
+      ev = *reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + t + 1) * dt.D + 4 * tid);
+  }
   ZASR_STAMP(1);
 
   // ---- 1. row statistics: g waves per row (g = 4 for a single hypothesis) ----
@@ -590,12 +634,13 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   }
   __syncthreads();
   ZASR_STAMP(3);
-  // ---- 3. expansion, hotwords, dedup (serial over <= beam candidates, all in LDS) ----
+  // ---- 3. expansion (:1110-1138) ----
+  // 3a. merge the 4 per-wave lists: the k best candidates, best first
   if (tid == 0) {
     const int total = n * V;
     const int k = beam < total ? beam : total;
     int ptr[4] = {0, 0, 0, 0};
-    int nn = 0, nc = 0;
+    int kk = 0;
     for (int c = 0; c < k; ++c) {
       int bw = 0;
       for (int w = 1; w < 4; ++w)
@@ -604,34 +649,57 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       const unsigned long long key0 = cK[bw * KB + ptr[bw]];
       ++ptr[bw];
       if (key0 == 0ull) break;
-      const float val = key_val(key0);
-      const int idx = key_idx(key0);
-      const int hi = idx / V, tok = idx - hi * V;
-      double score = (double)val;
-      unsigned long long key;
-      int klen, ny1, ny2, nhw = pHw[hi];
-      if (tok == 0) {
-        key = pHash[hi];
-        klen = pLen[hi];
-        ny1 = pY1[hi];
-        ny2 = pY2[hi];
-      } else {
-        if (hw.num_states > 0 && tok != 2) {
-          const int cls = hw.tok2cls[tok];
-          if (cls < 0) {
-            score += -hw.node_score[nhw];
-            nhw = 0;
-          } else {
-            const long e = (long)nhw * hw.num_cls + cls;
-            score += hw.delta[e];
-            nhw = hw.next[e];
-          }
+      cand[kk++] = key0;
+    }
+    sK = kk;
+  }
+  __syncthreads();
+  // 3b. per candidate (one thread each): token, hotword transition (:1127-1131; UNK and
+  //     blank skip the graph, :1129), sequence identity
+  const int kk = sK;
+  if (tid < kk) {
+    const unsigned long long key0 = cand[tid];
+    const float val = key_val(key0);
+    const int idx = key_idx(key0);
+    const int hi = idx / V, tok = idx - hi * V;
+    double score = (double)val;
+    int nhw = pHw[hi];
+    if (tok == 0) {
+      cHash[tid] = pHash[hi];
+      cLen[tid] = pLen[hi];
+      cY1[tid] = pY1[hi];
+      cY2[tid] = pY2[hi];
+    } else {
+      if (hw.num_states > 0 && tok != 2) {
+        const int cls = hw.tok2cls[tok];
+        if (cls < 0) {
+          score += -hw.node_score[nhw];
+          nhw = 0;
+        } else {
+          const long e = (long)nhw * hw.num_cls + cls;
+          score += hw.delta[e];
+          nhw = hw.next[e];
         }
-        key = hash_push(pHash[hi], tok);
-        klen = pLen[hi] + 1;
-        ny2 = pY1[hi];
-        ny1 = tok;
       }
+      cHash[tid] = hash_push(pHash[hi], tok);
+      cLen[tid] = pLen[hi] + 1;
+      cY2[tid] = pY1[hi];
+      cY1[tid] = tok;
+    }
+    cScore[tid] = score;
+    cVal[tid] = val;
+    cHi[tid] = hi;
+    cTok[tid] = tok;
+    cHw[tid] = nhw;
+  }
+  __syncthreads();
+  // 3c. in order: merge duplicates of the full sequence with an f64 log-add (:1133-1138),
+  //     else open a slot; emissions append a node (LDS reads, global stores only)
+  if (tid == 0) {
+    int nn = 0;
+    for (int c = 0; c < kk; ++c) {
+      const unsigned long long key = cHash[c];
+      const int klen = cLen[c];
       int found = -1;
       for (int q = 0; q < nn; ++q)
         if (nLen[q] == klen && nHash[q] == key) {
@@ -640,10 +708,11 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
         }
       if (found >= 0) {
         int f64 = 0;
-        nLp[found] = log_add(nLp[found], nLpf[found], score, 0, &f64);
+        nLp[found] = log_add(nLp[found], nLpf[found], cScore[c], 0, &f64);
         nLpf[found] = f64;
         continue;
       }
+      const int hi = cHi[c], tok = cTok[c];
       int nnode = pNode[hi];
       if (tok != 0) {
         const int nid = sNodeCnt++;
@@ -651,26 +720,22 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
         st.node_tok[gi] = tok;
         st.node_frame[gi] = t;
         st.node_parent[gi] = pNode[hi];
-        st.node_lp[gi] = (double)val - pLp[hi];
+        st.node_lp[gi] = (double)cVal[c] - pLp[hi];
         st.node_stats[gi] = sStats[hi];
         nnode = nid;
-        chIdx[nn] = nc;
-        chSlot[nc++] = nn;
       }
-      nLp[nn] = score;
+      nLp[nn] = cScore[c];
       nLpf[nn] = 0;
       nHash[nn] = key;
       nLen[nn] = klen;
-      nY1[nn] = ny1;
-      nY2[nn] = ny2;
-      nHw[nn] = nhw;
+      nY1[nn] = cY1[c];
+      nY2[nn] = cY2[c];
+      nHw[nn] = cHw[c];
       nNode[nn] = nnode;
       nParent[nn] = hi;
-      nChanged[nn] = tok != 0;
       ++nn;
     }
     sNN = nn;
-    sNC = nc;
     st.nh[s] = nn;
     st.node_count[s] = sNodeCnt;
   }
@@ -687,71 +752,40 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     st.hw[base + tid] = nHw[tid];
     st.node[base + tid] = nNode[tid];
   }
-  if constexpr (FUSED) {
-    // decoder rows of the new slots (blank extensions keep the parent's row) and the
-    // joiner input of frame t + 1: J[slot] = tanh(enc[s, t + 1] + dec[slot])
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int D = fd.D;
-    __bf16* xs = reinterpret_cast<__bf16*>(smem_raw);                    // [32][D + 8]
-    float* dl = reinterpret_cast<float*>(smem_raw + 32 * (D + 8) * 2);  // [16][D]
-    const int nc = sNC;
-    if (nc > 0) {
-      for (int e = tid; e < 32 * (D + 8); e += 256) {
-        const int i = e / (D + 8), c = e - i * (D + 8);
-        float v = 0.f;
-        if (i < nc && c < D) {
-          const int q = chSlot[i];
-          v = fmaxf(fd.tap0[(long)nY2[q] * D + c] + fd.tap1[(long)nY1[q] * D + c], 0.f);
-        }
-        xs[e] = (__bf16)v;
-      }
-      __syncthreads();
-      dec_rows_bf16(xs, nc, fd.wp, fd.bp, D, dl);
-      __syncthreads();
-    }
-    ZASR_STAMP(5);
-    const bool next = t + 1 < enc_len[s];
-    const float* erow = fd.enc + (long)(fd.enc_off[s] + t + 1) * D;
-    const int d4 = D / 4;
-    for (int q = 0; q < nn; ++q) {
-      const float* src = nChanged[q] ? dl + chIdx[q] * D : fd.dec_old + (long)(base + nParent[q]) * D;
-      for (int c4 = tid; c4 < d4; c4 += 256) {
-        const float4 dv = *reinterpret_cast<const float4*>(src + 4 * c4);
-        *reinterpret_cast<float4*>(fd.dec_new + (long)(base + q) * D + 4 * c4) = dv;
-        if (next) {
-          const float4 ev = *reinterpret_cast<const float4*>(erow + 4 * c4);
-          __bf16* jo = fd.J + (long)(base + q) * D + 4 * c4;
-          jo[0] = (__bf16)fast_tanh(ev.x + dv.x);
-          jo[1] = (__bf16)fast_tanh(ev.y + dv.y);
-          jo[2] = (__bf16)fast_tanh(ev.z + dv.z);
-          jo[3] = (__bf16)fast_tanh(ev.w + dv.w);
-        }
-      }
+  ZASR_STAMP(5);
+  // ---- 4. the next frame's joiner input from the decoder-context table ----
+  if constexpr (TABLE) {
+    if (next && tid < dt.D / 4) {
+      float4 dv[KB];
+#pragma unroll
+      for (int q = 0; q < KB; ++q)
+        if (q < nn)
+          dv[q] = *reinterpret_cast<const float4*>(
+              dt.table + ((long)nY2[q] * dt.V + nY1[q]) * dt.D + 4 * tid);
+#pragma unroll
+      for (int q = 0; q < KB; ++q)
+        if (q < nn) store_j4(dt, (long)(base + q) * dt.D + 4 * tid, ev, dv[q]);
     }
   }
   ZASR_STAMP(6);
-
 }
 
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
                         int beam, int t, const int* enc_len, const HotwordTables& hw,
-                        const FusedDec* fd, hipStream_t st) {
+                        const DecTable* dt, hipStream_t st) {
   if (S <= 0) return;
   ZASR_REQUIRE(beam >= 1 && beam <= kMaxBeam && beam <= Hmax, "beam out of range");
+  ZASR_REQUIRE(!dt || (dt->D % 4 == 0 && dt->D <= 1024), "joiner dim must be a multiple of 4, <= 1024");
   dim3 grid(S), block(256);
-  FusedDec f{};
-  size_t lds = 0;
-  if (fd) {
-    f = *fd;
-    lds = 32 * (f.D + 8) * 2 + 16 * f.D * 4;
-  }
+  DecTable d{};
+  if (dt) d = *dt;
 #define ZASR_STEP(KBV)                                                                      \
-  if (fd)                                                                                   \
-    hipLaunchKernelGGL((search_step_kernel<KBV, true>), grid, block, lds, st, s, logits, V,  \
-                       Hmax, beam, t, enc_len, hw, f);                                      \
+  if (dt)                                                                                   \
+    hipLaunchKernelGGL((search_step_kernel<KBV, true>), grid, block, 0, st, s, logits, V,    \
+                       Hmax, beam, t, enc_len, hw, d);                                      \
   else                                                                                      \
     hipLaunchKernelGGL((search_step_kernel<KBV, false>), grid, block, 0, st, s, logits, V,   \
-                       Hmax, beam, t, enc_len, hw, f)
+                       Hmax, beam, t, enc_len, hw, d)
   if (beam == 1) {
     ZASR_STEP(1);
   } else if (beam <= 4) {
