@@ -1043,8 +1043,8 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   st.stamps = nullptr;
   const bool stamps = getenv("ZASR_STAMPS") != nullptr;
   if (stamps) {
-    st.stamps = ws<unsigned long long>("se_stamps", (size_t)Tmax * 8);
-    ZASR_HIP_CHECK(hipMemsetAsync(st.stamps, 0, (size_t)Tmax * 8 * 8, st_));
+    st.stamps = ws<unsigned long long>("se_stamps", (size_t)Tmax * 16);
+    ZASR_HIP_CHECK(hipMemsetAsync(st.stamps, 0, (size_t)Tmax * 16 * 8, st_));
   }
   float* logits = ws<float>("se_logits", slots * V);
   const bool bf16 = model_.joiner.wh != nullptr;
@@ -1101,19 +1101,24 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   ZASR_HIP_CHECK(hipMemcpyAsync(h_st.data(), o_st, h_st.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
   ZASR_HIP_CHECK(hipStreamSynchronize(st_));
   if (stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
-    std::vector<unsigned long long> h((size_t)Tmax * 8);
+    std::vector<unsigned long long> h((size_t)Tmax * 16);
     ZASR_HIP_CHECK(hipMemcpy(h.data(), st.stamps, h.size() * 8, hipMemcpyDeviceToHost));
-    double acc[7] = {0};
+    const int seq[] = {0, 6, 7, 8, 1, 2, 3, 4, 5};
+    const char* name[] = {"nh", "row0_loaded", "row0_stats", "rows_rest", "wave_topk", "barrier", "expand", "J"};
+    constexpr int NS = 8;
+    double acc[NS] = {0};
     int n = 0;
     for (int t = 0; t < Tmax; ++t) {
-      const unsigned long long* p = &h[(size_t)t * 8];
-      if (!p[0] || !p[6]) continue;
-      for (int k = 1; k <= 6; ++k) acc[k] += (double)(p[k] - p[k - 1]);
+      const unsigned long long* p = &h[(size_t)t * 16];
+      bool ok = true;
+      for (int k : seq) ok = ok && p[k] != 0;
+      if (!ok) continue;
+      for (int k = 0; k < NS; ++k) acc[k] += (double)(p[seq[k + 1]] - p[seq[k]]);
       ++n;
     }
-    fprintf(stderr, "[zasr stamps] frames=%d mean cycles: load %.0f stats %.0f topk %.0f expand %.0f "
-            "state %.0f J %.0f\n", n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n,
-            acc[5] / n, acc[6] / n);
+    fprintf(stderr, "[zasr stamps] frames=%d mean cycles:", n);
+    for (int k = 0; k < NS; ++k) fprintf(stderr, " %s %.0f", name[k], n ? acc[k] / n : 0.0);
+    fprintf(stderr, "\n");
   }
   for (int i = 0; i < S; ++i) {
     TokenResult& r = res[order[i]];

@@ -134,7 +134,7 @@ __device__ __forceinline__ float fast_tanh(float x) { return 1.f - 2.f / (__expf
 #define ZASR_STAMP(slot)                                                                  \
   do {                                                                                    \
     if (st.stamps && blockIdx.x == 0 && threadIdx.x == 0)                                 \
-      st.stamps[(long)t * 8 + (slot)] = __builtin_amdgcn_s_memtime();                     \
+      st.stamps[(long)t * 16 + (slot)] = __builtin_amdgcn_s_memtime();                     \
   } while (0)
 
 }  // namespace
@@ -415,7 +415,12 @@ void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------------------
-template <int KB, bool TABLE>
+// One block per stream.  Hypothesis row h belongs to wave h % 4: the wave loads the row
+// (float4 per lane, Q per lane), reduces its statistics with shuffles and inserts its
+// candidates into per-thread top-KB lists -- no block barrier until the four wave lists
+// meet.  Everything after the top-k (ranking, hotwords, dedup, slot and node writes, the
+// next frame's joiner input) runs in wave 0 with lane-parallel LDS work.
+template <int KB, int Q, bool TABLE>
 __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const float* logits,
                                                           int V, int Hmax, int beam, int t,
                                                           const int* enc_len, HotwordTables hw,
@@ -428,39 +433,31 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   const int wid = tid >> 6;
   const int base = s * Hmax;
 
-  // previous hypotheses
   __shared__ double pLp[kMaxBeam];
-  __shared__ int pLpf[kMaxBeam], pLen[kMaxBeam], pY1[kMaxBeam], pY2[kMaxBeam], pHw[kMaxBeam],
-      pNode[kMaxBeam];
+  __shared__ int pLen[kMaxBeam], pY1[kMaxBeam], pY2[kMaxBeam], pHw[kMaxBeam], pNode[kMaxBeam];
   __shared__ unsigned long long pHash[kMaxBeam];
-  // new hypotheses
-  __shared__ double nLp[kMaxBeam];
-  __shared__ int nLpf[kMaxBeam], nLen[kMaxBeam], nY1[kMaxBeam], nY2[kMaxBeam], nHw[kMaxBeam],
-      nNode[kMaxBeam], nParent[kMaxBeam];
-  __shared__ unsigned long long nHash[kMaxBeam];
-  // row statistics
-  __shared__ float sMax[kMaxBeam], sLogSum[kMaxBeam];
   __shared__ float4 sStats[kMaxBeam];
-  __shared__ float rA[4], rB[4], rC[4];
   __shared__ unsigned long long cK[4 * KB];
-  __shared__ int sN, sNN, sNodeCnt, sK;
-  // candidates of this frame (after top-k), decoded in parallel
   __shared__ unsigned long long cand[kMaxBeam], cHash[kMaxBeam];
   __shared__ double cScore[kMaxBeam];
-  __shared__ float cVal[kMaxBeam];
-  __shared__ int cHi[kMaxBeam], cTok[kMaxBeam], cLen[kMaxBeam], cY1[kMaxBeam], cY2[kMaxBeam],
-      cHw[kMaxBeam];
+  __shared__ int cLen[kMaxBeam], cY1[kMaxBeam], cY2[kMaxBeam], cDup[kMaxBeam];
 
   ZASR_STAMP(0);
-  if (tid == 0) {
-    sN = st.nh[s];
-    sNodeCnt = st.node_count[s];
+  const int V4 = V >> 2;
+  const float4* rows4 = reinterpret_cast<const float4*>(logits + (long)base * V);
+  // first row of this wave: issued before anything else (rows >= nh hold stale but valid data)
+  float4 xa[Q], xb[Q];
+  if (wid < Hmax) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane + 64 * q;
+      xa[q] = i < V4 ? rows4[(long)wid * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    }
   }
-  __syncthreads();
-  const int n = sN;
+  const int n = st.nh[s];
+  if (n != 12345) ZASR_STAMP(6);
   if (tid < n) {
     pLp[tid] = st.lp[base + tid];
-    pLpf[tid] = st.lpf[base + tid];
     pHash[tid] = st.hash[base + tid];
     pLen[tid] = st.len[base + tid];
     pY1[tid] = st.y1[base + tid];
@@ -468,156 +465,111 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     pHw[tid] = st.hw[base + tid];
     pNode[tid] = st.node[base + tid];
   }
-  const float* rows = logits + (long)base * V;
-  // the next frame's encoder row (independent of this frame's result): in flight now
-  float4 ev = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the next frame's encoder row (wave 0 writes J): in flight now
+  float4 ev[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
   const bool next = t + 1 < T_s;
   if constexpr (TABLE) {
-    if (next && tid < dt.D / 4)
-      ev = *reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + t + 1) * dt.D + 4 * tid);
-  }
-  ZASR_STAMP(1);
-
-  // ---- 1. row statistics: g waves per row (g = 4 for a single hypothesis) ----
-  // One pass for (max, second max) over register-cached logits, one for
-  //   S = sum e, E1 = sum e d, E3 = sum exp(d / 3)   (d = x - max, e = exp(d)),
-  // giving entropy = log S - E1 / S and sum p^(1/3) = S^(-1/3) E3 (the reference's
-  // f32 formulas of :1167-1171 rewritten without per-element log / pow / divide).
-  const int g = n >= 4 ? 1 : (n == 1 ? 4 : 2);
-  for (int h0 = 0; h0 < n; h0 += 4 / g) {
-    const int h = h0 + wid / g;
-    const int part = wid % g;
-    const bool live = h < n;
-    const float* row = rows + (long)(live ? h : 0) * V;
-    const int stride = 64 * g, start = part * 64 + lane;
-    constexpr int kCache = 32;
-    const bool cached = (V + stride - 1) / stride <= kCache;
-    float xv[kCache];
-    float m1 = -INFINITY, m2 = -INFINITY;
-    if (live) {
-      if (cached) {
+    if (wid == 0 && next) {
 #pragma unroll
-        for (int q = 0; q < kCache; ++q) {
-          const int v = start + q * stride;
-          const float x = v < V ? row[v] : -INFINITY;
-          xv[q] = x;
-          if (x > m1) {
-            m2 = m1;
-            m1 = x;
-          } else if (x > m2) {
-            m2 = x;
-          }
-        }
-      } else {
-        for (int v = start; v < V; v += stride) {
-          const float x = row[v];
-          if (x > m1) {
-            m2 = m1;
-            m1 = x;
-          } else if (x > m2) {
-            m2 = x;
-          }
-        }
+      for (int j = 0; j < 2; ++j) {
+        const int c4 = lane + 64 * j;
+        if (c4 < dt.D / 4)
+          ev[j] = *reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + t + 1) * dt.D + 4 * c4);
       }
     }
+  }
+
+  // ---- 1 + 2. per row: statistics (:1096-1098, :1159-1181) and candidate insertion ----
+  //   max / second max; S = sum e, E1 = sum e d, E3 = sum exp(d / 3) (d = x - max):
+  //   entropy = log S - E1 / S, sum p^(1/3) = S^(-1/3) E3, top1 = 1 / S, top2 = e^(m2-m1) / S
+  //   candidate lp = ((x - max) - log S) + score_h (f32 add, or f64 for an np.float64 score)
+  unsigned long long tk[KB];
+#pragma unroll
+  for (int q = 0; q < KB; ++q) tk[q] = 0ull;
+  for (int h = wid; h < n; h += 4) {
+    const bool more = h + 4 < n;
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int i = lane + 64 * q;
+        xb[q] = i < V4 ? rows4[(long)(h + 4) * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      }
+    }
+    const double ld = st.lp[base + h];
+    const bool f64 = st.lpf[base + h] != 0;
+    float m1 = -INFINITY, m2 = -INFINITY;
+    auto upd = [&](float x) {  // branch-free (a branchy form put m1/m2 in scratch)
+      m2 = fmaxf(m2, fminf(m1, x));
+      m1 = fmaxf(m1, x);
+    };
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      upd(xa[q].x);
+      upd(xa[q].y);
+      upd(xa[q].z);
+      upd(xa[q].w);
+    }
+    if (h == 0 && m1 != 12345.f) ZASR_STAMP(7);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
-      float hi = fmaxf(m1, a1);
-      float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
+      const float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
+      const float hi = fmaxf(m1, a1);
+      const float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
       m1 = hi;
       m2 = lo;
     }
-    if (g > 1) {
-      if (lane == 0) {
-        rA[wid] = m1;
-        rB[wid] = m2;
-      }
-      __syncthreads();
-      const int w0 = (wid / g) * g;
-      for (int q = 0; q < g; ++q) {
-        const int w = w0 + q;
-        if (w == wid) continue;
-        float a1 = rA[w], a2 = rB[w];
-        float hi = fmaxf(m1, a1);
-        float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
-        m1 = hi;
-        m2 = lo;
-      }
-      __syncthreads();
-    }
     float se = 0.f, e1 = 0.f, e3 = 0.f;
-    if (live) {
-      if (cached) {
+    auto acc = [&](float x) {
+      const float d = x - m1;  // -inf past V -> e = 0
+      const float e = __expf(d);
+      se += e;
+      e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+      e3 += __expf(d * (1.0f / 3.0f));
+    };
 #pragma unroll
-        for (int q = 0; q < kCache; ++q) {
-          const float d = xv[q] - m1;  // -inf past V -> e = 0
-          const float e = __expf(d);
-          se += e;
-          e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
-          e3 += __expf(d * (1.0f / 3.0f));
-        }
-      } else {
-        for (int v = start; v < V; v += stride) {
-          const float d = row[v] - m1;
-          const float e = __expf(d);
-          se += e;
-          e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
-          e3 += __expf(d * (1.0f / 3.0f));
-        }
-      }
+    for (int q = 0; q < Q; ++q) {
+      acc(xa[q].x);
+      acc(xa[q].y);
+      acc(xa[q].z);
+      acc(xa[q].w);
     }
     se = wave_sum(se);
     e1 = wave_sum(e1);
     e3 = wave_sum(e3);
-    if (g > 1) {
-      if (lane == 0) {
-        rA[wid] = se;
-        rB[wid] = e1;
-        rC[wid] = e3;
-      }
-      __syncthreads();
-      const int w0 = (wid / g) * g;
-      se = e1 = e3 = 0.f;
-      for (int q = 0; q < g; ++q) {
-        se += rA[w0 + q];
-        e1 += rB[w0 + q];
-        e3 += rC[w0 + q];
-      }
-      __syncthreads();
-    }
-    if (live && part == 0 && lane == 0) {
-      const float ls = logf(se);
-      sMax[h] = m1;
-      sLogSum[h] = ls;
+    const float ls = logf(se);
+    if (h == 0 && ls != 12345.f) ZASR_STAMP(8);
+    if (lane == 0)
       sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
                               __expf(m2 - m1) / se);
-    }
-  }
-  __syncthreads();
-  ZASR_STAMP(2);
-
-  // ---- 2. top-k over n * V candidates, as packed sortable 64-bit keys ----
-  unsigned long long tk[KB];
-#pragma unroll
-  for (int q = 0; q < KB; ++q) tk[q] = 0ull;
-  for (int h = 0; h < n; ++h) {
-    const float mh = sMax[h], lsh = sLogSum[h];
-    const double ld = pLp[h];
     const float lf = (float)ld;
-    const bool f64 = pLpf[h] != 0;
-    const float* row = rows + (long)h * V;
-    for (int v = tid; v < V; v += 256) {
-      const float lpv = (row[v] - mh) - lsh;
+    auto ins = [&](float x, int idx) {
+      const float lpv = (x - m1) - ls;
       const float val = f64 ? (float)((double)lpv + ld) : lpv + lf;
-      const unsigned long long key = make_key(val, h * V + v);
+      const unsigned long long key = make_key(val, idx);
       if (key > tk[KB - 1]) {
 #pragma unroll
         for (int q = KB - 1; q > 0; --q) tk[q] = key > tk[q - 1] ? tk[q - 1] : (key > tk[q] ? key : tk[q]);
         tk[0] = key > tk[0] ? key : tk[0];
       }
+    };
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane + 64 * q;
+      if (i < V4) {
+        const int b0 = h * V + 4 * i;
+        ins(xa[q].x, b0);
+        ins(xa[q].y, b0 + 1);
+        ins(xa[q].z, b0 + 2);
+        ins(xa[q].w, b0 + 3);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) xa[q] = xb[q];
     }
   }
+  ZASR_STAMP(1);
+  // per-wave top-KB
   for (int round = 0; round < KB; ++round) {
     unsigned long long best = tk[0];
 #pragma unroll
@@ -632,43 +584,45 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       tk[KB - 1] = 0ull;
     }
   }
+  ZASR_STAMP(2);
   __syncthreads();
   ZASR_STAMP(3);
-  // ---- 3. expansion (:1110-1138) ----
-  // 3a. merge the 4 per-wave lists: the k best candidates, best first
-  if (tid == 0) {
-    const int total = n * V;
-    const int k = beam < total ? beam : total;
-    int ptr[4] = {0, 0, 0, 0};
-    int kk = 0;
-    for (int c = 0; c < k; ++c) {
-      int bw = 0;
-      for (int w = 1; w < 4; ++w)
-        if (ptr[w] < KB && (ptr[bw] >= KB || cK[w * KB + ptr[w]] > cK[bw * KB + ptr[bw]])) bw = w;
-      if (ptr[bw] >= KB) break;
-      const unsigned long long key0 = cK[bw * KB + ptr[bw]];
-      ++ptr[bw];
-      if (key0 == 0ull) break;
-      cand[kk++] = key0;
-    }
-    sK = kk;
+  if (wid != 0) return;
+
+  // ---- 3. expansion (:1110-1138), wave 0 ----
+  // 3a. global rank of each wave-list key (keys are distinct): the k best, best first
+  const int total = n * V;
+  const int k = beam < total ? beam : total;
+  {
+    const unsigned long long key = lane < 4 * KB ? cK[lane] : 0ull;
+    int rank = 0;
+    for (int j = 0; j < 4 * KB; ++j) rank += cK[j] > key ? 1 : 0;
+    if (key != 0ull && rank < k) cand[rank] = key;
   }
-  __syncthreads();
-  // 3b. per candidate (one thread each): token, hotword transition (:1127-1131; UNK and
-  //     blank skip the graph, :1129), sequence identity
-  const int kk = sK;
-  if (tid < kk) {
-    const unsigned long long key0 = cand[tid];
-    const float val = key_val(key0);
+  const unsigned long long nzmask = __ballot(lane < 4 * KB && cK[lane < 4 * KB ? lane : 0] != 0ull);
+  const int nz = __popcll(nzmask);
+  const int kk = k < nz ? k : nz;
+  __builtin_amdgcn_wave_barrier();
+  // 3b. lane c decodes candidate c: token, hotword transition (:1127-1131; blank and UNK
+  //     skip the graph, :1129), sequence identity
+  const bool lv = lane < kk;
+  int hi = 0, tok = 0, nhw = 0, klen = 0, ny1 = 0, ny2 = 0;
+  float val = 0.f;
+  double score = 0.0;
+  unsigned long long key = 0ull;
+  if (lv) {
+    const unsigned long long key0 = cand[lane];
+    val = key_val(key0);
     const int idx = key_idx(key0);
-    const int hi = idx / V, tok = idx - hi * V;
-    double score = (double)val;
-    int nhw = pHw[hi];
+    hi = idx / V;
+    tok = idx - hi * V;
+    score = (double)val;
+    nhw = pHw[hi];
     if (tok == 0) {
-      cHash[tid] = pHash[hi];
-      cLen[tid] = pLen[hi];
-      cY1[tid] = pY1[hi];
-      cY2[tid] = pY2[hi];
+      key = pHash[hi];
+      klen = pLen[hi];
+      ny1 = pY1[hi];
+      ny2 = pY2[hi];
     } else {
       if (hw.num_states > 0 && tok != 2) {
         const int cls = hw.tok2cls[tok];
@@ -681,93 +635,121 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
           nhw = hw.next[e];
         }
       }
-      cHash[tid] = hash_push(pHash[hi], tok);
-      cLen[tid] = pLen[hi] + 1;
-      cY2[tid] = pY1[hi];
-      cY1[tid] = tok;
+      key = hash_push(pHash[hi], tok);
+      klen = pLen[hi] + 1;
+      ny2 = pY1[hi];
+      ny1 = tok;
     }
-    cScore[tid] = score;
-    cVal[tid] = val;
-    cHi[tid] = hi;
-    cTok[tid] = tok;
-    cHw[tid] = nhw;
+    cHash[lane] = key;
+    cLen[lane] = klen;
+    cScore[lane] = score;
+    cY1[lane] = ny1;
+    cY2[lane] = ny2;
   }
-  __syncthreads();
-  // 3c. in order: merge duplicates of the full sequence with an f64 log-add (:1133-1138),
-  //     else open a slot; emissions append a node (LDS reads, global stores only)
-  if (tid == 0) {
-    int nn = 0;
-    for (int c = 0; c < kk; ++c) {
-      const unsigned long long key = cHash[c];
-      const int klen = cLen[c];
-      int found = -1;
-      for (int q = 0; q < nn; ++q)
-        if (nLen[q] == klen && nHash[q] == key) {
-          found = q;
-          break;
+  __builtin_amdgcn_wave_barrier();
+  // the next frame's decoder rows of every candidate context (table gather), in flight
+  // while duplicates are resolved
+  constexpr int KP = KB < 8 ? KB : 8;
+  float4 dv[KP][2];
+  if constexpr (TABLE) {
+    if (next) {
+#pragma unroll
+      for (int c = 0; c < KP; ++c) {
+        if (c < kk) {
+          const float* row = dt.table + ((long)cY2[c] * dt.V + cY1[c]) * dt.D;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int c4 = lane + 64 * j;
+            if (c4 < dt.D / 4) dv[c][j] = *reinterpret_cast<const float4*>(row + 4 * c4);
+          }
         }
-      if (found >= 0) {
-        int f64 = 0;
-        nLp[found] = log_add(nLp[found], nLpf[found], cScore[c], 0, &f64);
-        nLpf[found] = f64;
-        continue;
       }
-      const int hi = cHi[c], tok = cTok[c];
-      int nnode = pNode[hi];
-      if (tok != 0) {
-        const int nid = sNodeCnt++;
-        const long gi = (long)s * st.node_cap + nid;
-        st.node_tok[gi] = tok;
-        st.node_frame[gi] = t;
-        st.node_parent[gi] = pNode[hi];
-        st.node_lp[gi] = (double)cVal[c] - pLp[hi];
-        st.node_stats[gi] = sStats[hi];
-        nnode = nid;
-      }
-      nLp[nn] = cScore[c];
-      nLpf[nn] = 0;
-      nHash[nn] = key;
-      nLen[nn] = klen;
-      nY1[nn] = cY1[c];
-      nY2[nn] = cY2[c];
-      nHw[nn] = cHw[c];
-      nNode[nn] = nnode;
-      nParent[nn] = hi;
-      ++nn;
     }
-    sNN = nn;
-    st.nh[s] = nn;
-    st.node_count[s] = sNodeCnt;
   }
-  __syncthreads();
+  // 3c. duplicates of the full sequence merge into their first occurrence, in candidate
+  //     order, with an f64 log-add (:1133-1138)
+  int dup = -1;
+  if (lv) {
+    for (int c = 0; c < lane; ++c)
+      if (cLen[c] == klen && cHash[c] == key) {
+        dup = c;
+        break;
+      }
+    cDup[lane] = dup;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const bool first = lv && dup < 0;
+  const unsigned long long fmask = __ballot(first);
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int slot = __popcll(fmask & below);
+  const bool emit = first && tok != 0;
+  const unsigned long long emask = __ballot(emit);
+  const int node_base = st.node_count[s];
+  if (first) {
+    double lp = score;
+    int f64 = 0;
+    for (int c = lane + 1; c < kk; ++c)
+      if (cDup[c] == lane) lp = log_add(lp, f64, cScore[c], 0, &f64);
+    int nnode = pNode[hi];
+    if (emit) {
+      const int nid = node_base + __popcll(emask & below);
+      const long gi = (long)s * st.node_cap + nid;
+      st.node_tok[gi] = tok;
+      st.node_frame[gi] = t;
+      st.node_parent[gi] = pNode[hi];
+      st.node_lp[gi] = (double)val - pLp[hi];
+      st.node_stats[gi] = sStats[hi];
+      nnode = nid;
+    }
+    const int o = base + slot;
+    st.lp[o] = lp;
+    st.lpf[o] = f64;
+    st.hash[o] = key;
+    st.len[o] = klen;
+    st.y1[o] = ny1;
+    st.y2[o] = ny2;
+    st.hw[o] = nhw;
+    st.node[o] = nnode;
+  }
+  if (lane == 0) {
+    st.nh[s] = __popcll(fmask);
+    st.node_count[s] = node_base + __popcll(emask);
+  }
   ZASR_STAMP(4);
-  const int nn = sNN;
-  if (tid < nn) {
-    st.lp[base + tid] = nLp[tid];
-    st.lpf[base + tid] = nLpf[tid];
-    st.hash[base + tid] = nHash[tid];
-    st.len[base + tid] = nLen[tid];
-    st.y1[base + tid] = nY1[tid];
-    st.y2[base + tid] = nY2[tid];
-    st.hw[base + tid] = nHw[tid];
-    st.node[base + tid] = nNode[tid];
+  // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]) ----
+  if constexpr (TABLE) {
+    if (next) {
+#pragma unroll
+      for (int c0 = 0; c0 < KB; c0 += KP) {
+        if (c0 > 0) {  // beams above 8: the next batch of candidate rows
+#pragma unroll
+          for (int c = 0; c < KP; ++c) {
+            if (c0 + c < kk && ((fmask >> (c0 + c)) & 1ull)) {
+              const float* row = dt.table + ((long)cY2[c0 + c] * dt.V + cY1[c0 + c]) * dt.D;
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const int c4 = lane + 64 * j;
+                if (c4 < dt.D / 4) dv[c][j] = *reinterpret_cast<const float4*>(row + 4 * c4);
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < KP; ++c) {
+          const int cc = c0 + c;
+          if (cc < kk && ((fmask >> cc) & 1ull)) {
+            const int sl = __popcll(fmask & ((1ull << cc) - 1ull));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int c4 = lane + 64 * j;
+              if (c4 < dt.D / 4) store_j4(dt, (long)(base + sl) * dt.D + 4 * c4, ev[j], dv[c][j]);
+            }
+          }
+        }
+      }
+    }
   }
   ZASR_STAMP(5);
-  // ---- 4. the next frame's joiner input from the decoder-context table ----
-  if constexpr (TABLE) {
-    if (next && tid < dt.D / 4) {
-      float4 dv[KB];
-#pragma unroll
-      for (int q = 0; q < KB; ++q)
-        if (q < nn)
-          dv[q] = *reinterpret_cast<const float4*>(
-              dt.table + ((long)nY2[q] * dt.V + nY1[q]) * dt.D + 4 * tid);
-#pragma unroll
-      for (int q = 0; q < KB; ++q)
-        if (q < nn) store_j4(dt, (long)(base + q) * dt.D + 4 * tid, ev, dv[q]);
-    }
-  }
-  ZASR_STAMP(6);
 }
 
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
@@ -775,17 +757,29 @@ void launch_search_step(const SearchState& s, const float* logits, int V, int S,
                         const DecTable* dt, hipStream_t st) {
   if (S <= 0) return;
   ZASR_REQUIRE(beam >= 1 && beam <= kMaxBeam && beam <= Hmax, "beam out of range");
-  ZASR_REQUIRE(!dt || (dt->D % 4 == 0 && dt->D <= 1024), "joiner dim must be a multiple of 4, <= 1024");
+  ZASR_REQUIRE(V % 4 == 0 && V <= 4096, "vocabulary size must be a multiple of 4, <= 4096");
+  ZASR_REQUIRE(!dt || (dt->D % 4 == 0 && dt->D <= 512), "joiner dim must be a multiple of 4, <= 512");
   dim3 grid(S), block(256);
   DecTable d{};
   if (dt) d = *dt;
-#define ZASR_STEP(KBV)                                                                      \
-  if (dt)                                                                                   \
-    hipLaunchKernelGGL((search_step_kernel<KBV, true>), grid, block, 0, st, s, logits, V,    \
-                       Hmax, beam, t, enc_len, hw, d);                                      \
-  else                                                                                      \
-    hipLaunchKernelGGL((search_step_kernel<KBV, false>), grid, block, 0, st, s, logits, V,   \
-                       Hmax, beam, t, enc_len, hw, d)
+#define ZASR_STEP3(KBV, QV)                                                                 \
+  do {                                                                                      \
+    if (dt)                                                                                 \
+      hipLaunchKernelGGL((search_step_kernel<KBV, QV, true>), grid, block, 0, st, s, logits, \
+                         V, Hmax, beam, t, enc_len, hw, d);                                 \
+    else                                                                                    \
+      hipLaunchKernelGGL((search_step_kernel<KBV, QV, false>), grid, block, 0, st, s,        \
+                         logits, V, Hmax, beam, t, enc_len, hw, d);                         \
+  } while (0)
+#define ZASR_STEP(KBV)             \
+  do {                             \
+    if (V <= 512)                  \
+      ZASR_STEP3(KBV, 2);          \
+    else if (V <= 2048)            \
+      ZASR_STEP3(KBV, 8);          \
+    else                           \
+      ZASR_STEP3(KBV, 16);         \
+  } while (0)
   if (beam == 1) {
     ZASR_STEP(1);
   } else if (beam <= 4) {
@@ -796,6 +790,7 @@ void launch_search_step(const SearchState& s, const float* logits, int V, int S,
     ZASR_STEP(16);
   }
 #undef ZASR_STEP
+#undef ZASR_STEP3
 }
 
 // --------------------------------------------------------------------------------------
