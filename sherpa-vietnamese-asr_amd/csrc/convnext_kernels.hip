@@ -1,0 +1,251 @@
+// Fused ConvNeXt block of Conv2dSubsampling (bf16 mode):
+//   out = x + pw2(SwooshL(pw1(dwconv7x7(x) + b_dw) + b1)) + b2
+// x, out: [rows (50 Hz frames, packed over sequences)][19 freq][128 ch] f32.
+//
+// One block = 5 frames x 19 freq = 95 positions (one 96-row MFMA M tile).  The 7x7 window's
+// 11 input frames are staged once in LDS as bf16; the depthwise conv runs on packed f32 FMAs
+// (two channels per lane) into the bf16 A tile; pw1 (128 -> 384) and pw2 (384 -> 128) run on
+// v_mfma_f32_32x32x16_bf16 in three 128-wide slices of the hidden layer, each slice's SwooshL
+// output living only in LDS.  The 384-wide hidden activation (11.5 GB per hour of audio in the
+// unfused form) never reaches HBM.  Zero padding outside each frame's own sequence (time) and
+// outside [0, 19) (freq), as the unfused path.
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace zasr {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kT = 5;            // output frames per block
+constexpr int kH = kT + 6;       // staged input frames
+constexpr int kP = kT * 19;      // 95 positions
+constexpr int kLdA = 136;        // A / H tile row stride (bf16): 272 B = odd multiple of 16 B
+constexpr int kHaloBytes = kH * 19 * 128 * 2;   // 53 504
+constexpr int kTileBytes = 96 * kLdA * 2;       // 26 112
+
+__device__ __forceinline__ int xcd_tile_cn(int b, int nb) {
+  const int per = nb >> 3, rem = nb & 7;
+  const int xcd = b & 7, slot = b >> 3;
+  return xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
+}
+
+// depthwise 7x7 for one (freq f, channel pair) column of the 5 output frames
+template <bool MASKED>
+__device__ __forceinline__ void dw_column(const __bf16* halo, int f, int c2, const float2 (&w)[49],
+                                          float2 bias, const int* lo, const int* hi,
+                                          __bf16* A) {
+  float2 acc[kT];
+#pragma unroll
+  for (int i = 0; i < kT; ++i) acc[i] = bias;
+#pragma unroll
+  for (int rr = 0; rr < kH; ++rr) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int ff = f + j - 3;
+      float2 v = make_float2(0.f, 0.f);
+      if (ff >= 0 && ff < 19) {
+        const bf16x2 h = *reinterpret_cast<const bf16x2*>(halo + ((rr * 19 + ff) * 128 + 2 * c2));
+        v = make_float2((float)h[0], (float)h[1]);
+      }
+#pragma unroll
+      for (int i = 0; i < kT; ++i) {
+        const int ti = rr - i;  // tap row 0..6 <-> time offset ti - 3
+        if (ti < 0 || ti > 6) continue;
+        if (MASKED && (ti - 3 < lo[i] || ti - 3 > hi[i])) continue;
+        acc[i].x = fmaf(w[ti * 7 + j].x, v.x, acc[i].x);
+        acc[i].y = fmaf(w[ti * 7 + j].y, v.y, acc[i].y);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kT; ++i) {
+    bf16x2 o;
+    o[0] = (__bf16)acc[i].x;
+    o[1] = (__bf16)acc[i].y;
+    *reinterpret_cast<bf16x2*>(A + (i * 19 + f) * kLdA + 2 * c2) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void convnext_fused_kernel(
+    const float* __restrict__ x, const int* __restrict__ L_off, const int* __restrict__ L_map,
+    int total_rows, const float* __restrict__ dw_w, const float* __restrict__ dw_b,
+    const __bf16* __restrict__ w1, const float* __restrict__ b1, const __bf16* __restrict__ w2,
+    const float* __restrict__ b2, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kHaloBytes + kTileBytes];
+  __shared__ int sLo[kT], sHi[kT], sMasked;
+  __bf16* const halo = reinterpret_cast<__bf16*>(smem);
+  __bf16* const Hs = reinterpret_cast<__bf16*>(smem);  // aliases the halo after the dwconv
+  __bf16* const As = reinterpret_cast<__bf16*>(smem + kHaloBytes);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int t0 = xcd_tile_cn(blockIdx.x, gridDim.x) * kT;
+  if (t0 >= total_rows) return;
+
+  // ---- stage frames t0-3 .. t0+7 as bf16 (zero outside [0, total_rows)) ----
+  // the 11 frames are contiguous in memory: a linear float4 copy, all of a batch's loads in
+  // flight before its LDS stores (a load -> store loop serialises on every load)
+  constexpr int kF4 = kH * 19 * 32;
+  constexpr int kIt = (kF4 + 255) / 256;  // 27
+  constexpr int kBatch = 14;
+  const float4* src = reinterpret_cast<const float4*>(x + ((long)t0 - 3) * 19 * 128);
+  const long lo4 = (long)(3 - t0) * 19 * 32;           // first valid float4 (frame 0)
+  const long hi4 = (long)(total_rows - t0 + 3) * 19 * 32;  // end (frame total_rows)
+#pragma unroll
+  for (int b0 = 0; b0 < kIt; b0 += kBatch) {
+    float4 v[kBatch];
+    // unconditional loads from clamped addresses, zero selected afterwards (a guarded load
+    // becomes a branch with a vmcnt(0) wait per element)
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) {
+      const int e = tid + 256 * (b0 + q);
+      long ec = e < lo4 ? lo4 : e;
+      ec = ec >= hi4 ? hi4 - 1 : ec;
+      ec = ec >= kF4 ? kF4 - 1 : ec;
+      const float4 t = src[ec];
+      const bool ok = b0 + q < kIt && e < kF4 && e >= lo4 && e < hi4;
+      v[q] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < kBatch; ++q) {
+      const int e = tid + 256 * (b0 + q);
+      if (b0 + q < kIt && e < kF4) {
+        bf16x2 a, b;
+        a[0] = (__bf16)v[q].x;
+        a[1] = (__bf16)v[q].y;
+        b[0] = (__bf16)v[q].z;
+        b[1] = (__bf16)v[q].w;
+        bf16x2* d = reinterpret_cast<bf16x2*>(halo + 4 * e);
+        d[0] = a;
+        d[1] = b;
+      }
+    }
+  }
+  if (tid < kT) {
+    const int r = t0 + tid;
+    int lo = -3, hi = 3;
+    if (r < total_rows) {
+      const int b = L_map[r];
+      lo = max(L_off[b] - r, -3);
+      hi = min(L_off[b + 1] - 1 - r, 3);
+    }
+    sLo[tid] = lo;
+    sHi[tid] = hi;
+  }
+  if (tid == 0) sMasked = 0;
+  // padding row 95 of the A tile
+  if (tid < kLdA / 2) reinterpret_cast<unsigned*>(As + 95 * kLdA)[tid] = 0u;
+  __syncthreads();
+  if (tid < kT && (sLo[tid] != -3 || sHi[tid] != 3)) atomicOr(&sMasked, 1);
+  __syncthreads();
+
+  // ---- depthwise 7x7: lane owns channels (2 c2, 2 c2 + 1), freq f = fg + 4 k ----
+  {
+    const int c2 = tid & 63, fg = tid >> 6;
+    float2 w[49];
+#pragma unroll
+    for (int k = 0; k < 49; ++k) w[k] = make_float2(dw_w[(2 * c2) * 49 + k], dw_w[(2 * c2 + 1) * 49 + k]);
+    const float2 bias = make_float2(dw_b[2 * c2], dw_b[2 * c2 + 1]);
+    const bool masked = sMasked != 0;
+    int lo[kT], hi[kT];
+#pragma unroll
+    for (int i = 0; i < kT; ++i) {
+      lo[i] = sLo[i];
+      hi[i] = sHi[i];
+    }
+    for (int f = fg; f < 19; f += 4) {
+      if (masked)
+        dw_column<true>(halo, f, c2, w, bias, lo, hi, As);
+      else
+        dw_column<false>(halo, f, c2, w, bias, lo, hi, As);
+    }
+  }
+  __syncthreads();
+
+  // ---- pw1 -> SwooshL -> pw2, three 128-wide slices of the hidden layer ----
+  const int col = lane & 31, half = lane >> 5;
+  f32x16 acc2[3];
+#pragma unroll
+  for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc2[rt][r] = 0.f;
+  for (int n3 = 0; n3 < 3; ++n3) {
+    // pw1: this wave's 32 hidden columns of the slice, all 96 rows, K = 128
+    const int hn = n3 * 128 + wid * 32 + col;
+    bf16x8 bw[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) bw[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
+    f32x16 acc1[3];
+#pragma unroll
+    for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[rt][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + (rt * 32 + col) * kLdA + ks * 16 + 8 * half);
+        acc1[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc1[rt], 0, 0, 0);
+      }
+    }
+    const float bb = b1[hn];
+    if (n3 > 0) __syncthreads();  // previous slice's pw2 is done reading Hs
+#pragma unroll
+    for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        Hs[row * kLdA + wid * 32 + col] = (__bf16)swooshl_fast(acc1[rt][r] + bb);
+      }
+    __syncthreads();
+    // pw2: this wave's 32 output channels, K = this slice's 128 hidden units
+    const int on = wid * 32 + col;
+    bf16x8 bw2[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      bw2[ks] = *reinterpret_cast<const bf16x8*>(w2 + (long)on * 384 + n3 * 128 + ks * 16 + 8 * half);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Hs + (rt * 32 + col) * kLdA + ks * 16 + 8 * half);
+        acc2[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw2[ks], acc2[rt], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- out = x + pw2 + b2 (f32) ----
+  const int on = wid * 32 + col;
+  const float bo = b2[on];
+  const long p0 = (long)t0 * 19;
+  const long pend = (long)total_rows * 19;
+#pragma unroll
+  for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const long p = p0 + row;
+      if (row < kP && p < pend) {
+        const long o = p * 128 + on;
+        out[o] = x[o] + (acc2[rt][r] + bo);
+      }
+    }
+}
+
+}  // namespace
+
+void launch_convnext_fused(const float* x, const int* L_off, const int* L_map, int total_rows,
+                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
+                           const void* w2, const float* b2, float* out, hipStream_t st) {
+  if (total_rows <= 0) return;
+  const int nb = cdiv(total_rows, kT);
+  hipLaunchKernelGGL(convnext_fused_kernel, dim3(nb), dim3(256), 0, st, x, L_off, L_map,
+                     total_rows, dw_w, dw_b, reinterpret_cast<const __bf16*>(w1), b1,
+                     reinterpret_cast<const __bf16*>(w2), b2, out);
+}
+
+}  // namespace zasr

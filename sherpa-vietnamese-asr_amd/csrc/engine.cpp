@@ -925,13 +925,23 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
     prof_end();
   }
-  float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
-  prof_begin("frontend_conv");
-  launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
-  prof_end();
-  float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
-  linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
-  linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
+  if (model_.pw1.wh) {
+    // bf16 mode: the whole ConvNeXt block in one kernel, hidden layer kept on chip
+    float* x4 = ws<float>("fe_x4", (size_t)mL.total * 19 * 128);
+    prof_begin("frontend_conv");
+    launch_convnext_fused(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, model_.pw1.wh,
+                          model_.pw1.b, model_.pw2.wh, model_.pw2.b, x4, st_);
+    prof_end();
+    x3 = x4;
+  } else {
+    float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
+    prof_begin("frontend_conv");
+    launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+    prof_end();
+    float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
+    linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
+    linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
+  }
   const int d0 = cfg.dims[0];
   float* e0 = ws<float>("fe_e0", (size_t)mL.total * d0);
   linear(model_.out, x3, 2432, mL.total, e0, d0, EPI_NONE);

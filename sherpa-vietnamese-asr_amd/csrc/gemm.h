@@ -24,7 +24,7 @@ enum GemmEpi : int {
 
 enum GemmALoad : int {
   ALOAD_DENSE = 0,   // A[m * lda + k]
-  ALOAD_JOINER = 1,  // tanh(enc[row(m)] + dec[m])     (joiner.output_linear input)
+  ALOAD_JOINER = 1,  // retired (the joiner has its own split-K kernels)
   ALOAD_CONV2 = 2,   // im2col of conv1 output [T1][80][8]   -> conv.4 (3x3, stride 2)
   ALOAD_CONV3 = 3,   // im2col of conv2 output [L2][39][32]  -> conv.7 (3x3, stride (1,2))
 };

@@ -19,46 +19,32 @@ namespace {
 
 constexpr int BK = 16;
 
+// A operand, 4 consecutive k of row gm.  Loads are unconditional (clamped into the valid
+// range, zero selected afterwards): a guarded load compiles to a branch with a vmcnt(0) wait,
+// which serialises the tile's memory round trips.  Requires M >= 1 and K % 4 == 0.
 template <int ALOAD>
 __device__ __forceinline__ float4 load_a4(const GemmParams& p, const float* A, int M, int K,
                                           int lda, int gm, int gk) {
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (gm >= M || gk >= K) return v;
+  const bool ok = gm < M && gk < K;
+  const int m = gm < M ? gm : M - 1;
+  const int k = gk < K ? gk : K - 4;
+  float4 v;
   if constexpr (ALOAD == ALOAD_DENSE) {
-    const float* ptr = A + (long)gm * lda + gk;
-    if (gk + 3 < K) {
-      v = *reinterpret_cast<const float4*>(ptr);
-    } else {
-      v.x = ptr[0];
-      if (gk + 1 < K) v.y = ptr[1];
-      if (gk + 2 < K) v.z = ptr[2];
-    }
-  } else if constexpr (ALOAD == ALOAD_JOINER) {
-    const JoinerALoad& j = p.joiner;
-    int s = gm / j.H;
-    int len = j.enc_len[s];
-    if (len <= 0) return v;
-    int t = j.t < len ? j.t : len - 1;
-    const float4 e = *reinterpret_cast<const float4*>(j.enc + (long)(j.enc_off[s] + t) * lda + gk);
-    const float4 d = *reinterpret_cast<const float4*>(j.dec + (long)gm * lda + gk);
-    v.x = tanhf(e.x + d.x);
-    v.y = tanhf(e.y + d.y);
-    v.z = tanhf(e.z + d.z);
-    v.w = tanhf(e.w + d.w);
+    v = *reinterpret_cast<const float4*>(A + (long)m * lda + k);
   } else if constexpr (ALOAD == ALOAD_CONV2) {
     // out (t, f) of conv.4; k = (kt*3 + kf)*8 + c over conv1 output [T1][80][8]
-    int t = gm / 39, f = gm - t * 39;
-    int kk = gk >> 3, c = gk & 7;
-    int kt = kk / 3, kf = kk - kt * 3;
+    const int t = m / 39, f = m - t * 39;
+    const int kk = k >> 3, c = k & 7;
+    const int kt = kk / 3, kf = kk - kt * 3;
     v = *reinterpret_cast<const float4*>(A + ((long)(2 * t + kt) * 80 + 2 * f + kf) * 8 + c);
   } else {  // ALOAD_CONV3
     // out (t, f) of conv.7; k = (kt*3 + kf)*32 + c over conv2 output [L2][39][32]
-    int t = gm / 19, f = gm - t * 19;
-    int kk = gk >> 5, c = gk & 31;
-    int kt = kk / 3, kf = kk - kt * 3;
+    const int t = m / 19, f = m - t * 19;
+    const int kk = k >> 5, c = k & 31;
+    const int kt = kk / 3, kf = kk - kt * 3;
     v = *reinterpret_cast<const float4*>(A + ((long)(t + kt) * 39 + 2 * f + kf) * 32 + c);
   }
-  return v;
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, bool BNC, int EPI>
@@ -112,41 +98,27 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
     for (int i = 0; i < A_LD; ++i) {
       int idx = tid + NT * i;
       int row = idx >> 2, k4 = idx & 3;
-      ra[i] = (idx < A_F4) ? load_a4<ALOAD>(p, A, M, K, lda, m0 + row, kt * BK + 4 * k4)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v = load_a4<ALOAD>(p, A, M, K, lda, m0 + (idx < A_F4 ? row : 0), kt * BK + 4 * k4);
+      ra[i] = (idx < A_F4) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
       int idx = tid + NT * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < B_F4) {
-        if constexpr (!BNC) {
-          int n = idx >> 2, k4 = idx & 3;
-          int gn = n0 + n, gk = kt * BK + 4 * k4;
-          if (gn < N && gk < K) {
-            const float* ptr = B + (long)gn * p.sbn + gk;
-            if (gk + 3 < K) {
-              v = *reinterpret_cast<const float4*>(ptr);
-            } else {
-              v.x = ptr[0];
-              if (gk + 1 < K) v.y = ptr[1];
-              if (gk + 2 < K) v.z = ptr[2];
-            }
-          }
-        } else {
-          int k = idx / (BN / 4), n4 = idx - k * (BN / 4);
-          int gk = kt * BK + k, gn = n0 + 4 * n4;
-          if (gk < K && gn < N) {
-            const float* ptr = B + (long)gk * p.sbk + gn;
-            if (gn + 3 < N) {
-              v = *reinterpret_cast<const float4*>(ptr);
-            } else {
-              v.x = ptr[0];
-              if (gn + 1 < N) v.y = ptr[1];
-              if (gn + 2 < N) v.z = ptr[2];
-            }
-          }
-        }
+      float4 v;
+      if constexpr (!BNC) {
+        const int n = idx >> 2, k4 = idx & 3;
+        const int gn = n0 + n, gk = kt * BK + 4 * k4;
+        const bool ok = idx < B_F4 && gn < N && gk < K;
+        const int nc = gn < N ? gn : N - 1, kc = gk < K ? gk : K - 4;
+        v = *reinterpret_cast<const float4*>(B + (long)nc * p.sbn + kc);
+        if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const int k = idx / (BN / 4), n4 = idx - k * (BN / 4);
+        const int gk = kt * BK + k, gn = n0 + 4 * n4;
+        const bool ok = idx < B_F4 && gk < K && gn < N;
+        const int kc = gk < K ? gk : K - 1, nc = gn < N ? gn : N - 4;
+        v = *reinterpret_cast<const float4*>(B + (long)kc * p.sbk + nc);
+        if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       rb[i] = v;
     }
@@ -286,17 +258,15 @@ template <int ALOAD, typename TA>
 __device__ __forceinline__ bf16x8 load_a8(const GemmParams& p, const TA* A, int M, int K, int lda,
                                           int gm, int gk) {
   bf16x8 v;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
   if constexpr (std::is_same<TA, __bf16>::value) {
-    if (gm < M && gk < K) {
-      const __bf16* ptr = A + (long)gm * lda + gk;
-      if (gk + 7 < K) {
-        v = *reinterpret_cast<const bf16x8*>(ptr);
-      } else {
-        for (int q = 0; q < 8; ++q)
-          if (gk + q < K) v[q] = ptr[q];
-      }
+    // unconditional, clamped (K % 8 == 0)
+    const bool ok = gm < M && gk < K;
+    const int m = gm < M ? gm : M - 1;
+    const int k = gk < K ? gk : K - 8;
+    v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
+    if (!ok) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
     }
   } else {
     const float4 x0 = load_a4<ALOAD>(p, A, M, K, lda, gm, gk);
@@ -380,26 +350,19 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     for (int i = 0; i < A_LD; ++i) {
       const int idx = tid + NT * i;
       const int row = idx / GPR, k8 = idx % GPR;
-      if (idx < A_G) ra[i] = load_a8<ALOAD, TA>(p, A, M, K, lda, m0 + row, kt * BK + 8 * k8);
+      ra[i] = load_a8<ALOAD, TA>(p, A, M, K, lda, m0 + (idx < A_G ? row : 0), kt * BK + 8 * k8);
     }
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
       const int idx = tid + NT * i;
       const int n = idx / GPR, k8 = idx % GPR;
-      bf16x8 v;
+      const int gn = n0 + n, gk = kt * BK + 8 * k8;
+      const bool ok = idx < B_G && gn < N && gk < K;
+      const int nc = gn < N ? gn : N - 1, kc = gk < K ? gk : K - 8;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(B + (long)nc * p.sbn + kc);
+      if (!ok) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
-      if (idx < B_G) {
-        const int gn = n0 + n, gk = kt * BK + 8 * k8;
-        if (gn < N && gk < K) {
-          const __bf16* ptr = B + (long)gn * p.sbn + gk;
-          if (gk + 7 < K) {
-            v = *reinterpret_cast<const bf16x8*>(ptr);
-          } else {
-            for (int q = 0; q < 8; ++q)
-              if (gk + q < K) v[q] = ptr[q];
-          }
-        }
+        for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
       }
       rb[i] = v;
     }
@@ -560,8 +523,6 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
       case EPI_MULAUX: return launch_tile<ALOAD_DENSE, true, EPI_MULAUX>(p, st);
       default: break;
     }
-  } else if (aload == ALOAD_JOINER && !b_ncontig && epi == EPI_NONE) {
-    return launch_tile<ALOAD_JOINER, false, EPI_NONE>(p, st);
   } else if (aload == ALOAD_CONV2 && !b_ncontig && epi == EPI_SWOOSHR) {
     return launch_tile<ALOAD_CONV2, false, EPI_SWOOSHR>(p, st);
   } else if (aload == ALOAD_CONV3 && !b_ncontig && epi == EPI_SWOOSHR) {
@@ -579,6 +540,7 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
   if (p.max_M <= 0) return;
   ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (epi != EPI_MULAUX || p.ldaux % 4 == 0),
                "gemm_bf16: N and the C / aux row strides must be multiples of 4");
+  ZASR_REQUIRE(p.slices != nullptr || p.K % 8 == 0, "gemm_bf16: K must be a multiple of 8");
   const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
   if (aload == ALOAD_DENSE && !a_bf16 && !c_bf16) {
     switch (epi) {

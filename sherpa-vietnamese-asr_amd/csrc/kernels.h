@@ -29,6 +29,11 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const i
                   int total_rows, const float* w /*[8][9]*/, const float* b, float* out,
                   hipStream_t st);
 // ConvNeXt depthwise 7x7, zero padding per sequence: [L][19][128] -> [L][19][128]
+// bf16 mode: out = x + pw2(SwooshL(pw1(dwconv7x7(x)))) in one kernel (convnext_kernels.hip);
+// w1 / w2 are the bf16 pw weights, out must not alias x
+void launch_convnext_fused(const float* x, const int* L_off, const int* L_map, int total_rows,
+                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
+                           const void* w2, const float* b2, float* out, hipStream_t st);
 void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
                      const float* w /*[128][49]*/, const float* b, float* out, hipStream_t st);
 
