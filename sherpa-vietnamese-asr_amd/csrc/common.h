@@ -49,6 +49,7 @@ __device__ __forceinline__ float swooshl_fast(float x) {
 __device__ __forceinline__ float swooshr_fast(float x) {
   return softplus_fast(x - 1.f) - 0.08f * x - 0.313261687f;
 }
+__device__ __forceinline__ float sigmoid_fast(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -72,6 +72,9 @@ __device__ __forceinline__ void dw_column(const __bf16* halo, int f, int c2, con
   }
 }
 
+// PHASES: bit 0 staging, bit 1 depthwise conv, bit 2 pointwise MLP (all = 7; subsets are
+// for tools/convnext_bench.hip)
+template <int PHASES>
 __global__ __launch_bounds__(256) void convnext_fused_kernel(
     const float* __restrict__ x, const int* __restrict__ L_off, const int* __restrict__ L_map,
     int total_rows, const float* __restrict__ dw_w, const float* __restrict__ dw_b,
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void convnext_fused_kernel(
   __syncthreads();
 
   // ---- depthwise 7x7: lane owns channels (2 c2, 2 c2 + 1), freq f = fg + 4 k ----
-  {
+  if constexpr ((PHASES & 2) != 0) {
     const int c2 = tid & 63, fg = tid >> 6;
     float2 w[49];
 #pragma unroll
@@ -167,6 +170,10 @@ __global__ __launch_bounds__(256) void convnext_fused_kernel(
   __syncthreads();
 
   // ---- pw1 -> SwooshL -> pw2, three 128-wide slices of the hidden layer ----
+  if constexpr ((PHASES & 4) == 0) {
+    if (tid == 0 && (float)As[tid] == 12345.f) out[0] = 0.f;  // keep the earlier phases live
+    return;
+  }
   const int col = lane & 31, half = lane >> 5;
   f32x16 acc2[3];
 #pragma unroll
@@ -243,7 +250,7 @@ void launch_convnext_fused(const float* x, const int* L_off, const int* L_map, i
                            const void* w2, const float* b2, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
   const int nb = cdiv(total_rows, kT);
-  hipLaunchKernelGGL(convnext_fused_kernel, dim3(nb), dim3(256), 0, st, x, L_off, L_map,
+  hipLaunchKernelGGL(convnext_fused_kernel<7>, dim3(nb), dim3(256), 0, st, x, L_off, L_map,
                      total_rows, dw_w, dw_b, reinterpret_cast<const __bf16*>(w1), b1,
                      reinterpret_cast<const __bf16*>(w2), b2, out);
 }

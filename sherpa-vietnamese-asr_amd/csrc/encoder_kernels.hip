@@ -254,37 +254,59 @@ void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int tot
 // =====================================================================================
 // BiasNorm (+ optional bypass): one wave per row.
 // =====================================================================================
-__global__ void bias_norm_kernel(float* __restrict__ x, int rows, int d,
-                                 const float* __restrict__ bias, float scale,
-                                 const float* __restrict__ orig,
-                                 const float* __restrict__ bscale) {
-  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  int lane = threadIdx.x & 63;
+template <int NQ>  // float4 per lane: d <= 256 * NQ
+__global__ __launch_bounds__(256) void bias_norm_kernel(float* __restrict__ x, int rows, int d,
+                                                        const float* __restrict__ bias, float scale,
+                                                        const float* __restrict__ orig,
+                                                        const float* __restrict__ bscale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  float* xr = x + (long)row * d;
+  const int d4 = d >> 2;
+  float4* xr = reinterpret_cast<float4*>(x + (long)row * d);
+  float4 v[NQ], o[NQ];
   float ss = 0.f;
-  for (int c = lane; c < d; c += 64) {
-    float v = xr[c] - bias[c];
-    ss = fmaf(v, v, ss);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = lane + 64 * q;
+    const int ic = i < d4 ? i : d4 - 1;
+    v[q] = xr[ic];
+    if (orig) o[q] = reinterpret_cast<const float4*>(orig + (long)row * d)[ic];
+    const float4 bq = reinterpret_cast<const float4*>(bias)[ic];
+    float4 t = make_float4(v[q].x - bq.x, v[q].y - bq.y, v[q].z - bq.z, v[q].w - bq.w);
+    if (i >= d4) t = make_float4(0.f, 0.f, 0.f, 0.f);
+    ss = fmaf(t.x, t.x, fmaf(t.y, t.y, fmaf(t.z, t.z, fmaf(t.w, t.w, ss))));
   }
   ss = wave_sum(ss);
-  float k = scale / sqrtf(ss / (float)d);
-  if (orig) {
-    const float* orow = orig + (long)row * d;
-    for (int c = lane; c < d; c += 64) {
-      float o = orow[c];
-      xr[c] = o + (xr[c] * k - o) * bscale[c];
+  const float k = scale / sqrtf(ss / (float)d);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = lane + 64 * q;
+    if (i >= d4) continue;
+    float4 r = make_float4(v[q].x * k, v[q].y * k, v[q].z * k, v[q].w * k);
+    if (orig) {
+      const float4 s4 = reinterpret_cast<const float4*>(bscale)[i];
+      r = make_float4(o[q].x + (r.x - o[q].x) * s4.x, o[q].y + (r.y - o[q].y) * s4.y,
+                      o[q].z + (r.z - o[q].z) * s4.z, o[q].w + (r.w - o[q].w) * s4.w);
     }
-  } else {
-    for (int c = lane; c < d; c += 64) xr[c] = xr[c] * k;
+    xr[i] = r;
   }
 }
 
 void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_scale,
                       const float* orig, const float* bypass_scale, hipStream_t st) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(bias_norm_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, rows, d, bias,
-                     expf(log_scale), orig, bypass_scale);
+  ZASR_REQUIRE(d % 4 == 0 && d <= 1024, "BiasNorm width must be a multiple of 4, <= 1024");
+  const dim3 grid(cdiv(rows, 4));
+  if (d <= 256)
+    hipLaunchKernelGGL(bias_norm_kernel<1>, grid, dim3(256), 0, st, x, rows, d, bias,
+                       expf(log_scale), orig, bypass_scale);
+  else if (d <= 512)
+    hipLaunchKernelGGL(bias_norm_kernel<2>, grid, dim3(256), 0, st, x, rows, d, bias,
+                       expf(log_scale), orig, bypass_scale);
+  else
+    hipLaunchKernelGGL(bias_norm_kernel<4>, grid, dim3(256), 0, st, x, rows, d, bias,
+                       expf(log_scale), orig, bypass_scale);
 }
 
 // =====================================================================================
@@ -361,71 +383,130 @@ void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStrea
 // =====================================================================================
 // ConvolutionModule core: GLU (x * sigmoid(s) of the in_proj halves) -> depthwise conv1d
 // over time (zero padding per sequence) + bias -> SwooshR.  Block tile: 64 packed rows x
-// 64 channels with a K/2 halo staged in LDS as GLU outputs.
+// 64 channels with a K/2 halo staged in LDS as GLU outputs (loads unconditional and batched:
+// one memory round trip).  Each lane owns one channel and 16 consecutive rows, so every
+// staged value is read from LDS once per lane and feeds up to K FMAs from registers.
+// Rows whose window crosses a sequence edge take the masked path (per-row tap range).
 // =====================================================================================
 constexpr int kDw1T = 64;
 
+// K = compiled window (7, 15, 31); a smaller odd kernel Kr runs with zero taps padded
+// symmetrically (adds exact zeros only)
+template <int K>
 __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
     const float* __restrict__ x2, const int* __restrict__ off, const int* __restrict__ map,
-    int total_rows, int d, int K, const float* __restrict__ w, const float* __restrict__ bias,
+    int total_rows, int d, int Kr, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ out) {
-  extern __shared__ float tile[];  // [(kDw1T + K - 1)][64]
-  __shared__ int sLo[kDw1T], sHi[kDw1T];
-  const int half = K >> 1;
+  constexpr int half = K / 2;
+  constexpr int nrows = kDw1T + K - 1;
+  constexpr int nf4 = nrows * 16;
+  constexpr int kIt = (nf4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float tile[nrows * 64];
+  __shared__ int sLo[kDw1T], sHi[kDw1T], sMasked;
   const int r0 = blockIdx.x * kDw1T;
   const int c0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
-  const int nrows = kDw1T + K - 1;
-  if (tid < kDw1T) {
-    const int r = r0 + tid;
-    if (r < total_rows) {
-      const int b = map[r];
-      sLo[tid] = off[b] - r;
-      sHi[tid] = off[b + 1] - 1 - r;
+  if (tid == 0) sMasked = 0;
+  {
+    float4 a[kIt], g[kIt];
+#pragma unroll
+    for (int q = 0; q < kIt; ++q) {
+      const int e = tid + 256 * q;
+      const int c4 = e & 15, rr = e >> 4;
+      int r = r0 - half + rr;
+      r = r < 0 ? 0 : (r >= total_rows ? total_rows - 1 : r);
+      const int cc = c0 + 4 * c4 < d ? c0 + 4 * c4 : d - 4;
+      a[q] = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + cc);
+      g[q] = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + d + cc);
+    }
+#pragma unroll
+    for (int q = 0; q < kIt; ++q) {
+      const int e = tid + 256 * q;
+      const int c4 = e & 15, rr = e >> 4;
+      const int r = r0 - half + rr;
+      const bool ok = e < nf4 && r >= 0 && r < total_rows && c0 + 4 * c4 < d;
+      float4 v = make_float4(a[q].x * sigmoid_fast(g[q].x), a[q].y * sigmoid_fast(g[q].y),
+                             a[q].z * sigmoid_fast(g[q].z), a[q].w * sigmoid_fast(g[q].w));
+      if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < nf4) *reinterpret_cast<float4*>(&tile[rr * 64 + 4 * c4]) = v;
     }
   }
-  for (int e = tid; e < nrows * 16; e += 256) {
-    const int c4 = e & 15, rr = e >> 4;
-    const int r = r0 - half + rr;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r >= 0 && r < total_rows && c0 + 4 * c4 < d) {
-      const float4 a = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + c0 + 4 * c4);
-      const float4 g = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + d + c0 + 4 * c4);
-      v = make_float4(a.x * sigmoidf_(g.x), a.y * sigmoidf_(g.y), a.z * sigmoidf_(g.z),
-                      a.w * sigmoidf_(g.w));
+  __syncthreads();
+  if (tid < kDw1T) {
+    const int r = r0 + tid;
+    int lo = -half, hi = half;
+    if (r < total_rows) {
+      const int b = map[r];
+      lo = max(off[b] - r, -half);
+      hi = min(off[b + 1] - 1 - r, half);
     }
-    *reinterpret_cast<float4*>(&tile[rr * 64 + 4 * c4]) = v;
+    sLo[tid] = lo;
+    sHi[tid] = hi;
+    if (lo != -half || hi != half) atomicOr(&sMasked, 1);
   }
   __syncthreads();
   const int c = tid & 63;
   if (c0 + c >= d) return;
-  float wr[31];
+  const int tr0 = (tid >> 6) * 16;
+  float wr[K];
+  const int pad = (K - Kr) / 2;
 #pragma unroll
-  for (int k = 0; k < 31; ++k) wr[k] = (k < K) ? w[(long)(c0 + c) * K + k] : 0.f;
+  for (int k = 0; k < K; ++k) {
+    const int kk = k - pad;
+    const bool ok = kk >= 0 && kk < Kr;
+    const float wv = w[(long)(c0 + c) * Kr + (ok ? kk : 0)];
+    wr[k] = ok ? wv : 0.f;
+  }
   const float bc = bias[c0 + c];
-  for (int tr = tid >> 6; tr < kDw1T; tr += 4) {
-    const int r = r0 + tr;
-    if (r >= total_rows) break;
-    const int lo = sLo[tr], hi = sHi[tr];
-    float acc = bc;
+  float acc[16];
 #pragma unroll
-    for (int k = 0; k < 31; ++k) {
-      const int dt = k - half;
-      if (k >= K || dt < lo || dt > hi) continue;
-      acc = fmaf(wr[k], tile[(tr + k) * 64 + c], acc);
+  for (int i = 0; i < 16; ++i) acc[i] = bc;
+  if (!sMasked) {
+#pragma unroll
+    for (int rr = 0; rr < 16 + K - 1; ++rr) {
+      const float v = tile[(tr0 + rr) * 64 + c];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k = rr - i;
+        if (k >= 0 && k < K) acc[i] = fmaf(wr[k], v, acc[i]);
+      }
     }
-    out[(long)r * d + c0 + c] = swooshr(acc);
+  } else {
+    int lo[16], hi[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      lo[i] = sLo[tr0 + i];
+      hi[i] = sHi[tr0 + i];
+    }
+#pragma unroll
+    for (int rr = 0; rr < 16 + K - 1; ++rr) {
+      const float v = tile[(tr0 + rr) * 64 + c];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k = rr - i;
+        if (k >= 0 && k < K && k - half >= lo[i] && k - half <= hi[i]) acc[i] = fmaf(wr[k], v, acc[i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + tr0 + i;
+    if (r < total_rows) out[(long)r * d + c0 + c] = swooshr_fast(acc[i]);
   }
 }
 
 void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
                          int K, const float* w, const float* b, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
-  ZASR_REQUIRE(K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
+  ZASR_REQUIRE(d % 4 == 0, "conv module channels must be a multiple of 4");
   dim3 grid(cdiv(total_rows, kDw1T), cdiv(d, 64));
-  size_t lds = (size_t)(kDw1T + K - 1) * 64 * sizeof(float);
-  hipLaunchKernelGGL(glu_dwconv1d_kernel, grid, dim3(256), lds, st, x2, off, map, total_rows, d,
-                     K, w, b, out);
+  ZASR_REQUIRE(K >= 1 && K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
+  if (K <= 7)
+    hipLaunchKernelGGL(glu_dwconv1d_kernel<7>, grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+  else if (K <= 15)
+    hipLaunchKernelGGL(glu_dwconv1d_kernel<15>, grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+  else
+    hipLaunchKernelGGL(glu_dwconv1d_kernel<31>, grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
 }
 
 // =====================================================================================
@@ -446,12 +527,17 @@ __global__ void downsample_kernel(const float* __restrict__ x, const int* __rest
   int tp = r - off_out[b];
   int base = off_in[b];
   int L = off_in[b + 1] - base;
-  float acc = 0.f;
-  for (int u = 0; u < ds; ++u) {
-    int t = tp * ds + u;
-    if (t > L - 1) t = L - 1;
-    acc = fmaf(wts.w[u], x[(long)(base + t) * d + c], acc);
+  float xv[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {  // all loads in flight (ds <= 8)
+    int t = tp * ds + (u < ds ? u : 0);
+    if (t > L - 1) t = L - 1;  // SimpleDownsample pads with the last frame
+    xv[u] = x[(long)(base + t) * d + c];
   }
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (u < ds) acc = fmaf(wts.w[u], xv[u], acc);
   out[e] = acc;
 }
 
@@ -747,16 +833,28 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
   for (int kb = wid; kb < nkb; kb += 4) {
     const int j0 = kb * 32;
-    // pos rows x = j0 - i0 - 31 + l, l < 63
-    if (lane < 63) {
-      const int x = j0 - i0 - 31 + lane;
-      sR[wid][lane] = *reinterpret_cast<const float4*>(a.pos_tab + (long)(x + a.pmax - 1) * 4 * H + 4 * h);
+    // pos rows x = j0 - i0 - 31 + l, l < 63 (loads unconditional, clamped: a guarded load
+    // becomes a branch with its own vmcnt(0) wait)
+    {
+      const int x = j0 - i0 - 31 + (lane < 63 ? lane : 62);
+      const float4 pr = *reinterpret_cast<const float4*>(a.pos_tab + (long)(x + a.pmax - 1) * 4 * H + 4 * h);
+      if (lane < 63) sR[wid][lane] = pr;
     }
     // values of this key block: 32 rows x 12
-    for (int e = lane; e < 32 * 3; e += 64) {
+    float4 vv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = lane + 64 * u;
+      const int jj = (e < 96 ? e : 95) / 3, q = (e < 96 ? e : 95) - jj * 3;
+      const int jr = j0 + jj < L ? j0 + jj : L - 1;
+      vv[u] = *reinterpret_cast<const float4*>(vbase + (long)jr * ldv + 4 * q);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = lane + 64 * u;
+      if (e >= 96) continue;
       const int jj = e / 3, q = e - jj * 3;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j0 + jj < L) v = *reinterpret_cast<const float4*>(vbase + (long)(j0 + jj) * ldv + 4 * q);
+      float4 v = j0 + jj < L ? vv[u] : make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (BF16) {
         // key jj sits in accumulator register r = (jj&3) + 4*(jj>>3) of lane half (jj>>2)&1;
         // MFMA m = r >> 3 takes it in k-slot 8 * half + (r & 7)
@@ -778,22 +876,19 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = 0.f;
     if constexpr (BF16) {
-      bf16x8_t kf0, kf1;
-      if (j < L) {
-        const float4* k0 = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 8 * h2);
-        const float4* k1 = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 + 8 * h2);
-        kf0 = cvt8(k0[0], k0[1]);
-        kf1 = cvt8(k1[0], k1[1]);
-      } else {
-        kf0 = cvt8(make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f));
-        kf1 = kf0;
-      }
+      // keys past L are masked to -inf below, so their (clamped) values do not matter
+      const int jc = j < L ? j : L - 1;
+      const float4* k0 = reinterpret_cast<const float4*>(kbase + (long)jc * ldq + 8 * h2);
+      const float4* k1 = reinterpret_cast<const float4*>(kbase + (long)jc * ldq + 16 + 8 * h2);
+      const bf16x8_t kf0 = cvt8(k0[0], k0[1]);
+      const bf16x8_t kf1 = cvt8(k1[0], k1[1]);
       sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf0, qf[0], sc, 0, 0, 0);
       sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf1, qf[1], sc, 0, 0, 0);
     } else {
       float kreg[16];
-      if (j < L) {
-        const float4* kp = reinterpret_cast<const float4*>(kbase + (long)j * ldq + 16 * h2);
+      {
+        const int jc = j < L ? j : L - 1;  // masked below
+        const float4* kp = reinterpret_cast<const float4*>(kbase + (long)jc * ldq + 16 * h2);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 v = kp[q];
@@ -802,9 +897,6 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
           kreg[4 * q + 2] = v.z;
           kreg[4 * q + 3] = v.w;
         }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) kreg[q] = 0.f;
       }
 #pragma unroll
       for (int s = 0; s < 16; ++s) sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kreg[s], qreg[s], sc, 0, 0, 0);

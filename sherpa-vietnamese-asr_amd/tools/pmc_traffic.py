@@ -1,0 +1,72 @@
+"""HBM traffic per launch of a kernel class from two rocprofv3 PMC passes (FETCH_SIZE and
+WRITE_SIZE collected separately: together they exceed the gfx950 counter budget).
+
+bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE / WRITE_SIZE are in KiB, and on
+gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM).
+
+  python tools/pmc_traffic.py FETCH.csv WRITE.csv --key "zipformer-68m|greedy_search|1|bf16|3600|enc_gemm"
+          [--out profiles/pmc_traffic.json]
+
+Kernel classes: enc_gemm = gemm_bf16_kernel / gemm_f32_kernel with the dense A loader
+(template argument ALOAD = 0) and a [N][K] weight operand, the launches Engine::linear makes.
+"""
+import argparse
+import csv
+import json
+import os
+import re
+
+
+def in_class(name: str, cls: str) -> bool:
+    if cls == "enc_gemm":
+        m = re.search(r"gemm_(bf16|f32)_kernel<([^>]*)>", name)
+        if not m:
+            return False
+        args = [a.strip() for a in m.group(2).split(",")]
+        if m.group(1) == "bf16":
+            return args[5] == "0"
+        return args[4] == "0" and args[5] == "false"  # B n-contiguous = nonlin_attention
+
+    return cls in name
+
+
+def total(path: str, counter: str, cls: str):
+    s, n = 0.0, 0
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter and in_class(r["Kernel_Name"], cls):
+                s += float(r["Counter_Value"])
+                n += 1
+    return s, n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("--key", required=True)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    cls = a.key.split("|")[-1]
+    f, nf = total(a.fetch_csv, "FETCH_SIZE", cls)
+    w, nw = total(a.write_csv, "WRITE_SIZE", cls)
+    if nf == 0 or nf != nw:
+        raise SystemExit("dispatch counts differ or are zero: %d vs %d" % (nf, nw))
+    per = (2.0 * f + w) * 1024.0 / nf
+    rec = {"bytes_per_launch": round(per), "launches": nf,
+           "fetch_kib_x2": round(2 * f), "write_kib": round(w),
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                     "FETCH_SIZE x2 gfx950 correction; " + os.path.basename(os.path.dirname(a.fetch_csv))}
+    print(json.dumps({a.key: rec}, indent=1))
+    if a.out:
+        tab = {}
+        if os.path.exists(a.out):
+            with open(a.out) as fh:
+                tab = json.load(fh)
+        tab[a.key] = rec
+        with open(a.out, "w") as fh:
+            json.dump(tab, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
