@@ -392,11 +392,21 @@ constexpr int kDw1T = 64;
 
 // K = compiled window (7, 15, 31); a smaller odd kernel Kr runs with zero taps padded
 // symmetrically (adds exact zeros only)
-template <int K>
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const __bf16* p) {
+  const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(p);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(__bf16* p, float v) { *p = (__bf16)v; }
+
+template <int K, typename TI, typename TO>
 __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
-    const float* __restrict__ x2, const int* __restrict__ off, const int* __restrict__ map,
+    const TI* __restrict__ x2, const int* __restrict__ off, const int* __restrict__ map,
     int total_rows, int d, int Kr, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ out) {
+    TO* __restrict__ out) {
   constexpr int half = K / 2;
   constexpr int nrows = kDw1T + K - 1;
   constexpr int nf4 = nrows * 16;
@@ -416,8 +426,8 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
       int r = r0 - half + rr;
       r = r < 0 ? 0 : (r >= total_rows ? total_rows - 1 : r);
       const int cc = c0 + 4 * c4 < d ? c0 + 4 * c4 : d - 4;
-      a[q] = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + cc);
-      g[q] = *reinterpret_cast<const float4*>(x2 + (long)r * 2 * d + d + cc);
+      a[q] = ld4(x2 + (long)r * 2 * d + cc);
+      g[q] = ld4(x2 + (long)r * 2 * d + d + cc);
     }
 #pragma unroll
     for (int q = 0; q < kIt; ++q) {
@@ -491,22 +501,36 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int r = r0 + tr0 + i;
-    if (r < total_rows) out[(long)r * d + c0 + c] = swooshr_fast(acc[i]);
+    if (r < total_rows) st1(out + (long)r * d + c0 + c, swooshr_fast(acc[i]));
   }
 }
 
-void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
-                         int K, const float* w, const float* b, float* out, hipStream_t st) {
+template <typename TI, typename TO>
+static void launch_glu_dwconv1d_t(const TI* x2, const int* off, const int* map, int total_rows,
+                                  int d, int K, const float* w, const float* b, TO* out,
+                                  hipStream_t st) {
   if (total_rows <= 0) return;
   ZASR_REQUIRE(d % 4 == 0, "conv module channels must be a multiple of 4");
   dim3 grid(cdiv(total_rows, kDw1T), cdiv(d, 64));
   ZASR_REQUIRE(K >= 1 && K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
   if (K <= 7)
-    hipLaunchKernelGGL(glu_dwconv1d_kernel<7>, grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    hipLaunchKernelGGL((glu_dwconv1d_kernel<7, TI, TO>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
   else if (K <= 15)
-    hipLaunchKernelGGL(glu_dwconv1d_kernel<15>, grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    hipLaunchKernelGGL((glu_dwconv1d_kernel<15, TI, TO>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
   else
-    hipLaunchKernelGGL(glu_dwconv1d_kernel<31>, grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    hipLaunchKernelGGL((glu_dwconv1d_kernel<31, TI, TO>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+}
+
+void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
+                         int K, const float* w, const float* b, float* out, hipStream_t st) {
+  launch_glu_dwconv1d_t(x2, off, map, total_rows, d, K, w, b, out, st);
+}
+
+void launch_glu_dwconv1d_bf16(const void* x2, const int* off, const int* map, int total_rows,
+                              int d, int K, const float* w, const float* b, void* out,
+                              hipStream_t st) {
+  launch_glu_dwconv1d_t(reinterpret_cast<const __bf16*>(x2), off, map, total_rows, d, K, w, b,
+                        reinterpret_cast<__bf16*>(out), st);
 }
 
 // =====================================================================================

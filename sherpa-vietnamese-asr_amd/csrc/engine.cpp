@@ -650,6 +650,28 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
   prof_end();
 }
 
+void Engine::linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M, void* C,
+                      bool c_bf16, int ldc, int epi) {
+  ZASR_REQUIRE(l.wh != nullptr, "linear_h needs bf16 weights");
+  GemmParams p{};
+  p.A = reinterpret_cast<const float*>(A);
+  p.lda = lda;
+  p.B = l.w;
+  p.sbk = 1;
+  p.sbn = l.K;
+  p.C = reinterpret_cast<float*>(C);
+  p.ldc = ldc;
+  p.bias = l.b;
+  p.M = M;
+  p.N = l.N;
+  p.K = l.K;
+  p.alpha = 1.f;
+  p.max_M = M;
+  prof_begin("enc_gemm");
+  gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_, a_bf16, c_bf16);
+  prof_end();
+}
+
 void Engine::run_fbank(const float* d_wav, const std::vector<long>& wav_off,
                        const std::vector<long>& n, float* d_feats, std::vector<int>& frames) {
   const int B = (int)n.size();
@@ -725,9 +747,15 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   }
   auto ff = [&](int k) {
     const DLin& fi = Ly.ff_in[k];
-    float* H = ws<float>("ly_hid", (size_t)R * fi.N);
-    linear(fi, X, d, R, H, fi.N, EPI_SWOOSHL);
-    linear(Ly.ff_out[k], H, fi.N, R, X, d, EPI_RESADD);
+    if (fi.wh) {  // bf16 mode: the hidden activation crosses HBM in bf16
+      __bf16* H = ws<__bf16>("ly_hid_h", (size_t)R * fi.N);
+      linear_h(fi, X, false, d, R, H, true, fi.N, EPI_SWOOSHL);
+      linear_h(Ly.ff_out[k], H, true, fi.N, R, X, false, d, EPI_RESADD);
+    } else {
+      float* H = ws<float>("ly_hid", (size_t)R * fi.N);
+      linear(fi, X, d, R, H, fi.N, EPI_SWOOSHL);
+      linear(Ly.ff_out[k], H, fi.N, R, X, d, EPI_RESADD);
+    }
   };
   auto self_attn = [&](int k) {
     float* vv = ws<float>("ly_vv", (size_t)R * 12 * h);
@@ -740,6 +768,16 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     linear(Ly.sa_out[k], oa, 12 * h, R, X, d, EPI_RESADD);
   };
   auto conv = [&](int k) {
+    if (Ly.cv_in[k].wh) {  // bf16 mode: in_proj output and out_proj input in bf16
+      __bf16* g2 = ws<__bf16>("ly_g2_h", (size_t)R * 2 * d);
+      __bf16* dc = ws<__bf16>("ly_dc_h", (size_t)R * d);
+      linear_h(Ly.cv_in[k], X, false, d, R, g2, true, 2 * d, EPI_NONE);
+      prof_begin("dwconv1d");
+      launch_glu_dwconv1d_bf16(g2, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+      prof_end();
+      linear_h(Ly.cv_out[k], dc, true, d, R, X, false, d, EPI_RESADD);
+      return;
+    }
     float* g2 = ws<float>("ly_g2", (size_t)R * 2 * d);
     float* dc = ws<float>("ly_dc", (size_t)R * d);
     linear(Ly.cv_in[k], X, d, R, g2, 2 * d, EPI_NONE);

@@ -133,6 +133,10 @@ class Engine {
                      const void* d_slices_nl, int maxL);
   void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
               const char* cls = "enc_gemm");
+  // bf16 mode only: A and/or C in bf16 (GEMM -> GEMM intermediates; the GEMM rounds A to
+  // bf16 on load anyway, so storing it rounded changes nothing numerically)
+  void linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M, void* C, bool c_bf16,
+                int ldc, int epi);
   void ensure_pos_tables(int max_len);
 
   // timing

@@ -49,6 +49,10 @@ void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st);
 // zero padding per sequence
 void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
                          int K, const float* w, const float* b, float* out, hipStream_t st);
+// bf16 in (the conv in_proj output) / bf16 out (the conv out_proj input), bf16 mode
+void launch_glu_dwconv1d_bf16(const void* x2, const int* off, const int* map, int total_rows,
+                              int d, int K, const float* w, const float* b, void* out,
+                              hipStream_t st);
 // t1[r][c] = tanh(h3[r][c]) * h3[r][hid + c]
 void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStream_t st);
 // SimpleDownsample: out[t'] = sum_u w[u] x[min(ds t' + u, L - 1)]
