@@ -257,3 +257,29 @@ def test_bf16_search_path_beam_hotwords(need_gpu):
     with open("gpurun_out/bf16_search_report.json", "w") as fh:
         json.dump({"cases": [os.path.basename(c) for c in CASES], "token_agreement": agree}, fh)
     assert sum(agree) / len(agree) >= 0.75, agree
+
+
+# ------------------------------------------------------------------ ROVER (row L)
+def test_rover_shared_fbank_equals_separate_decodes(need_gpu):
+    """decode_chunks_rover (one GPU fbank per chunk shared by both models) == each model
+    decoding on its own + the block vote (the vote itself is pinned on CPU by
+    tests/test_host_plan_rover.py)."""
+    import copy
+    from core.asr_engine import create_recognizer, decode_chunks
+    from model_fixtures import tiny_model
+    from zasr.rover import decode_chunks_rover, rover_merge
+    _, _, pa = tiny_model(3)
+    _, _, pb = tiny_model(4)
+    ra = create_recognizer(pa, max_active_paths=4)
+    rb = create_recognizer(pb, max_active_paths=4)
+    chunks = [_speech(s, 500 + i) for i, s in enumerate((4.0, 2.2, 6.5))]
+    offs = [0.0, 3.7, 7.1]
+    got = decode_chunks_rover(ra, rb, chunks, offs, ["xin chào"])
+    wa = decode_chunks(ra, chunks, offs)
+    wb = decode_chunks(rb, chunks, offs)
+    ref = [rover_merge(copy.deepcopy(a), copy.deepcopy(b), ["xin chào"]) for a, b in zip(wa, wb)]
+    assert len(got) == len(ref)
+    for (m1, d1), (m2, d2) in zip(got, ref):
+        assert d1 == d2
+        assert [w["text"] for w in m1] == [w["text"] for w in m2]
+        assert [w["start"] for w in m1] == [w["start"] for w in m2]

@@ -41,3 +41,22 @@ def test_decode_chunk_words_match_reference(path):
                 assert a[k] == pytest.approx(v, abs=1e-12), k
             else:
                 assert a[k] == v, k
+
+
+def test_dropin_install_rebinds_hot_path_names():
+    """zasr.dropin.install rebinds the reference module's hot-path names to this build and
+    leaves the rest (pipeline, merges) alone; checked on a stand-in module object."""
+    import types
+    import core.asr_engine as ours
+    from zasr.dropin import ENGINE_NAMES, install
+    ref = types.ModuleType("core_asr_engine_standin")
+    ref.TranscriberPipeline = object
+    ref.rover_merge_words = lambda a, b: (a, set())
+    for n in ENGINE_NAMES:
+        setattr(ref, n, None)
+    done = install(ref)
+    assert ref.create_recognizer is ours.create_recognizer
+    assert ref.decode_chunk is ours.decode_chunk
+    assert ref.compute_fbank_ort is ours.compute_fbank_ort
+    assert ref.TranscriberPipeline is object
+    assert "asr_engine.decode_chunk" in done
