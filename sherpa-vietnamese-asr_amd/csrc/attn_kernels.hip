@@ -1,0 +1,371 @@
+// bf16-mode kernels of NonlinAttention (icefall zipformer.py NonlinAttention, 3P; the
+// reference runs it inside the exported encoder, core/asr_engine.py:1045-1049):
+//
+//   z = (A0 @ (tanh(s) * x)) * y,   (s, x, y) = chunk(in_proj(src), 3),
+//   A0 = softmax over keys of head 0 of RelPositionMultiheadAttentionWeights.
+//
+// The product A0 @ t1 is a per-sequence GEMM with K = L (up to ~1700 keys): it runs on the
+// bf16 MFMA GEMM (gemm.hip, one z-slice per sequence) with
+//   A = A0 in bf16, [L][L8] per sequence (L8 = L rounded up to 8, columns >= L zero),
+//   B = t1 transposed in bf16, [hid][R8] (sequence b in columns [o8_b, o8_b + L8_b), zero
+//       padded), i.e. the [N][K] "weight" layout the GEMM streams with 16-byte loads,
+// and the `* y` factor in its epilogue.  The kernels here produce A0 and t1^T.
+#include "common.h"
+#include "kernels.h"
+
+namespace zasr {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+}  // namespace
+
+// =====================================================================================
+// bf16-mode attention (RelPositionMultiheadAttentionWeights + SelfAttention, icefall
+// zipformer.py, 3P), flash style: scores are recomputed where they are consumed and never
+// reach HBM except head 0's normalised weights (NonlinAttention's GEMM operand).
+//
+// Block = 4 waves = 128 queries of one (sequence, head); wave w owns queries
+// i0 + 32 w + (lane & 31) and walks every 32-key block of the sequence.  Per key block the
+// block stages K (32 keys x 32 dims) and V^T (12 dims x 32 keys, permuted into the
+// accumulator order of the scores) in LDS once for all 4 waves, double-buffered with the
+// next block's global loads in registers.  The positional rows R[x] (x = j - i) the block
+// touches (L + 127 of them) are staged once at the start.
+//
+//   S^T = K Q^T     v_mfma_f32_32x32x16_bf16: lane = query, registers = 16 keys (q, k and
+//                   the pos queries p stay f32 in HBM; q and k are rounded to bf16 once)
+//         + p_i . R[j - i]
+//   P^T = exp2(S^T - c_i)     (log2 domain: q and p are pre-scaled by log2 e)
+//   O^T += V^T P^T            (the accumulator registers are the MFMA k-slots as they stand)
+//
+// MODE 0 (W0): head 0, pass 1 = row statistics, pass 2 = normalised weights in bf16.
+// MODE 1 (SA online): running max / sum, O rescaled when the max moves; writes the output
+//   and the row statistic c_i = max + log2(sum) for the second self-attention.
+// MODE 2 (SA stats): c_i from MODE 1, P normalised directly.
+// =====================================================================================
+namespace {
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kKLd = 40;  // LDS row stride (bf16) of the K / V^T images: 80 B
+constexpr int kPosPad = 160;  // staged positional rows beyond L (the last key block's tail)
+
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 8 consecutive f32 -> bf16 (RNE), optionally scaled first (one rounding)
+__device__ __forceinline__ bf16x8 load8_bf16(const float* p, float scale) {
+  const float4 x0 = reinterpret_cast<const float4*>(p)[0];
+  const float4 x1 = reinterpret_cast<const float4*>(p)[1];
+  bf16x8 v;
+  v[0] = (__bf16)(x0.x * scale); v[1] = (__bf16)(x0.y * scale);
+  v[2] = (__bf16)(x0.z * scale); v[3] = (__bf16)(x0.w * scale);
+  v[4] = (__bf16)(x1.x * scale); v[5] = (__bf16)(x1.y * scale);
+  v[6] = (__bf16)(x1.z * scale); v[7] = (__bf16)(x1.w * scale);
+  return v;
+}
+}  // namespace
+
+template <int MODE>
+__global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
+  extern __shared__ float4 sPos[];  // [L + kPosPad] positional rows of this head, x = xlo + t
+  __shared__ __attribute__((aligned(16))) __bf16 sK[2][32 * kKLd];
+  __shared__ __attribute__((aligned(16))) __bf16 sVt[2][12 * kKLd];
+  const int b = blockIdx.y;
+  const int h = MODE == 0 ? 0 : blockIdx.z;
+  const int r0 = a.row_off[b];
+  const int L = a.row_off[b + 1] - r0;
+  const int i0b = blockIdx.x * 128;
+  if (i0b >= L) return;
+  const int H = a.H;
+  const long ldq = 68L * H;
+  const long ldv = 12L * H;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c = lane & 31, h2 = lane >> 5;
+  const int i0 = i0b + 32 * wid;
+  const bool live = i0 < L;  // wave-uniform
+  const int i = i0 + c;
+  const int ic = i < L ? i : L - 1;
+
+  // ---- positional rows: x in [xlo, xlo + L + kPosPad) (p_i carries the log2 e scale) ----
+  {
+    const int xlo = -(i0b + 127);
+    const int n = L + kPosPad;
+    const int rmax = 2 * a.pmax - 2;
+    for (int t = tid; t < n; t += 256) {
+      int row = xlo + t + a.pmax - 1;
+      row = row < 0 ? 0 : (row > rmax ? rmax : row);
+      sPos[t] = *reinterpret_cast<const float4*>(a.pos_tab + (long)row * 4 * H + 4 * h);
+    }
+  }
+  // ---- this lane's query, pre-scaled by log2 e and rounded once ----
+  const float* qrow = a.qkp + (long)(r0 + ic) * ldq + 32 * h;
+  const bf16x8 qf0 = load8_bf16(qrow + 8 * h2, kLog2e);
+  const bf16x8 qf1 = load8_bf16(qrow + 16 + 8 * h2, kLog2e);
+  float4 pq = *reinterpret_cast<const float4*>(a.qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
+  pq.x *= kLog2e; pq.y *= kLog2e; pq.z *= kLog2e; pq.w *= kLog2e;
+  // pos index of (this query, key j0 + jr): j0 + jr - 32 wid - c + 127
+  const int pbase = 127 - 32 * wid - c;
+
+  const int nkb = (L + 31) / 32;
+  // staging roles: threads 0..127 load K (key tid>>2, 16-byte chunk tid&3); threads
+  // 128..223 load V (key (tid-128)/3, 4 dims (tid-128)%3); MODE 0 needs no V
+  const float* kbase = a.qkp + (long)r0 * ldq + 32 * H + 32 * h;
+  const __bf16* vbase = MODE == 0 ? nullptr : a.v + (long)r0 * ldv + 12 * h;
+  const int vt = tid - 128;
+  const int vkey = vt / 3, vq = vt - 3 * (vt / 3);
+  float4 kraw0, kraw1;
+  bf16x4 vreg;
+  auto gload = [&](int kb) {
+    const int j0 = kb * 32;
+    if (tid < 128) {
+      int j = j0 + (tid >> 2);
+      j = j < L ? j : L - 1;
+      kraw0 = *reinterpret_cast<const float4*>(kbase + (long)j * ldq + 8 * (tid & 3));
+      kraw1 = *reinterpret_cast<const float4*>(kbase + (long)j * ldq + 8 * (tid & 3) + 4);
+    } else if (MODE != 0 && vt < 96) {
+      int j = j0 + vkey;
+      j = j < L ? j : L - 1;
+      vreg = *reinterpret_cast<const bf16x4*>(vbase + (long)j * ldv + 4 * vq);
+    }
+  };
+  auto sstore = [&](int buf) {
+    if (tid < 128) {
+      bf16x8 kv;
+      kv[0] = (__bf16)kraw0.x; kv[1] = (__bf16)kraw0.y; kv[2] = (__bf16)kraw0.z; kv[3] = (__bf16)kraw0.w;
+      kv[4] = (__bf16)kraw1.x; kv[5] = (__bf16)kraw1.y; kv[6] = (__bf16)kraw1.z; kv[7] = (__bf16)kraw1.w;
+      *reinterpret_cast<bf16x8*>(&sK[buf][(tid >> 2) * kKLd + 8 * (tid & 3)]) = kv;
+    } else if (MODE != 0 && vt < 96) {
+      // key jj sits in score register r = (jj&3) + 4 (jj>>3) of lane half (jj>>2)&1, which
+      // the PV MFMA m = r >> 3 takes in k-slot 8 half + (r & 7)
+      const int jj = vkey;
+      const int r = (jj & 3) + 4 * (jj >> 3);
+      const int slot = 16 * (r >> 3) + 8 * ((jj >> 2) & 1) + (r & 7);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sVt[buf][(4 * vq + e) * kKLd + slot] = vreg[e];
+    }
+  };
+  // scores of key block kb (log2 domain), keys >= L masked to -inf
+  auto scores = [&](int kb, int buf, f32x16& s) {
+    const int j0 = kb * 32;
+    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(&sK[buf][c * kKLd + 8 * h2]);
+    const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(&sK[buf][c * kKLd + 16 + 8 * h2]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, s, 0, 0, 0);
+    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf1, s, 0, 0, 0);
+    const int pb = j0 + pbase;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
+      const float4 pr = sPos[pb + jr];
+      float ps = fmaf(pq.x, pr.x, s[r]);
+      ps = fmaf(pq.y, pr.y, ps);
+      ps = fmaf(pq.z, pr.z, ps);
+      s[r] = fmaf(pq.w, pr.w, ps);
+    }
+    if (j0 + 32 > L) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
+        s[r] = j0 + jr < L ? s[r] : -INFINITY;
+      }
+    }
+  };
+
+  // ---- key-block loop(s) ----
+  float m = -INFINITY, l = 0.f, cst = 0.f;
+  if constexpr (MODE == 2) cst = a.stats_in[(long)(r0 + ic) * H + h];
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+
+  constexpr int NPASS = MODE == 0 ? 2 : 1;
+  __bf16* const a0 = MODE == 0 ? a.attn + a.a_off[b] : nullptr;
+#pragma unroll 1
+  for (int pass = 0; pass < NPASS; ++pass) {
+    if (MODE == 0 && pass == 1) {
+      // row statistic from the two lane halves (same query, disjoint keys)
+      const float mo = __shfl_xor(m, 32, 64), lo = __shfl_xor(l, 32, 64);
+      const float M = fmaxf(m, mo);
+      const float Ls = l * fexp2(m - M) + lo * fexp2(mo - M);
+      cst = M + __log2f(Ls);
+    }
+    gload(0);
+    __syncthreads();  // previous pass's readers are done with buffer 0 (and sPos is staged)
+    sstore(0);
+    __syncthreads();
+#pragma unroll 1
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int cur = kb & 1;
+      if (kb + 1 < nkb) gload(kb + 1);
+      if (live) {
+        f32x16 s;
+        scores(kb, cur, s);
+        if constexpr (MODE == 0) {
+          if (pass == 0) {
+            float bm = s[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) bm = fmaxf(bm, s[r]);
+            const float mn = fmaxf(m, bm);
+            if (mn != -INFINITY) {  // a lane half can see only masked keys (L <= 4)
+              float acc = 0.f;
+#pragma unroll
+              for (int r = 0; r < 16; ++r) acc += fexp2(s[r] - mn);
+              l = l * fexp2(m - mn) + acc;
+              m = mn;
+            }
+          } else if (i < L) {
+            const int L8 = (L + 7) & ~7;
+            const int j0 = kb * 32;
+            __bf16* dst = a0 + (long)i * L8 + j0 + 4 * h2;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if (j0 + 8 * g + 4 * h2 < L8) {
+                bf16x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (__bf16)fexp2(s[4 * g + e] - cst);
+                *reinterpret_cast<bf16x4*>(dst + 8 * g) = v;
+              }
+            }
+          }
+        } else {
+          if constexpr (MODE == 1) {
+            float bm = s[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) bm = fmaxf(bm, s[r]);
+            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+            const float mn = fmaxf(m, bm);
+            if (__any(mn > m)) {
+              const float sc = fexp2(m - mn);  // m = -inf -> 0
+#pragma unroll
+              for (int r = 0; r < 16; ++r) o[r] *= sc;
+              l *= sc;
+              m = mn;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              s[r] = fexp2(s[r] - m);
+              l += s[r];
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = fexp2(s[r] - cst);
+          }
+#pragma unroll
+          for (int mm = 0; mm < 2; ++mm) {
+            bf16x8 pf, vf;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) pf[t] = (__bf16)s[8 * mm + t];
+            if (c < 12) {
+              vf = *reinterpret_cast<const bf16x8*>(&sVt[cur][c * kKLd + 16 * mm + 8 * h2]);
+            } else {
+#pragma unroll
+              for (int t = 0; t < 8; ++t) vf[t] = (__bf16)0.f;
+            }
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
+          }
+        }
+      }
+      if (kb + 1 < nkb) sstore(cur ^ 1);
+      __syncthreads();
+    }
+  }
+  if constexpr (MODE != 0) {
+    if (!live || i >= L) return;
+    float inv = 1.f;
+    if constexpr (MODE == 1) {
+      const float lt = l + __shfl_xor(l, 32, 64);
+      inv = 1.f / lt;
+      if (h2 == 0) a.stats_out[(long)(r0 + i) * H + h] = m + __log2f(lt);
+    }
+    // O^T rows = value dims d = (r&3) + 8 (r>>2) + 4 h2; d < 12 valid
+    __bf16* dst = a.out + (long)(r0 + i) * ldv + 12 * h;
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = (__bf16)(o[e] * inv);
+      v1[e] = (__bf16)(o[4 + e] * inv);
+    }
+    *reinterpret_cast<bf16x4*>(dst + 4 * h2) = v0;  // d 0..3 (h2 = 0) / 4..7 (h2 = 1)
+    if (h2 == 0) *reinterpret_cast<bf16x4*>(dst + 8) = v1;  // d 8..11
+  }
+}
+
+void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
+  if (a.nseq <= 0 || a.max_len <= 0) return;
+  const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
+  ZASR_REQUIRE(lds <= 140 * 1024, "attention: sequence too long for the bf16 kernel's LDS");
+  const dim3 grid(cdiv(a.max_len, 128), a.nseq, mode == 0 ? 1 : a.H);
+  if (mode == 0)
+    hipLaunchKernelGGL(attn_flash_kernel<0>, grid, dim3(256), lds, st, a);
+  else if (mode == 1)
+    hipLaunchKernelGGL(attn_flash_kernel<1>, grid, dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(attn_flash_kernel<2>, grid, dim3(256), lds, st, a);
+}
+
+// =====================================================================================
+// t1^T = (tanh(s) * x)^T in bf16: h3 [R][3 hid] f32 -> t1t [hid][R8].  Tile 64 rows x 64
+// channels transposed through LDS; packed row r of sequence b goes to column
+// r + (o8_b - off_b); the last row of a sequence also writes the zero padding up to
+// o8_b + L8_b.
+// =====================================================================================
+__global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const float* __restrict__ h3,
+                                                            const int* __restrict__ off,
+                                                            const int* __restrict__ o8,
+                                                            const int* __restrict__ map, int R,
+                                                            int hid, int R8,
+                                                            __bf16* __restrict__ t1t) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  // load: 64 rows x 16 float4 per tile, 4 per thread, all loads in flight first
+  float4 sv[4], xv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int idx = tid + 256 * k;
+    const int rl = idx >> 4, c4 = idx & 15;
+    const int r = r0 + rl < R ? r0 + rl : R - 1;
+    const int cc = c0 + 4 * c4 < hid ? c0 + 4 * c4 : hid - 4;
+    const float* row = h3 + (long)r * 3 * hid;
+    sv[k] = *reinterpret_cast<const float4*>(row + cc);
+    xv[k] = *reinterpret_cast<const float4*>(row + hid + cc);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int idx = tid + 256 * k;
+    const int rl = idx >> 4, c4 = idx & 15;
+    tile[4 * c4 + 0][rl] = tanhf(sv[k].x) * xv[k].x;
+    tile[4 * c4 + 1][rl] = tanhf(sv[k].y) * xv[k].y;
+    tile[4 * c4 + 2][rl] = tanhf(sv[k].z) * xv[k].z;
+    tile[4 * c4 + 3][rl] = tanhf(sv[k].w) * xv[k].w;
+  }
+  __syncthreads();
+  const int rl = tid & 63;
+  const int r = r0 + rl;
+  if (r >= R) return;
+  const int b = map[r];
+  const int shift = o8[b] - off[b];
+  const int col = r + shift;
+  const bool last = r == off[b + 1] - 1;
+  const int pad_end = o8[b] + ((off[b + 1] - off[b] + 7) & ~7);
+  for (int cl = tid >> 6; cl < 64; cl += 4) {
+    const int ch = c0 + cl;
+    if (ch >= hid) break;
+    __bf16* dst = t1t + (long)ch * R8;
+    dst[col] = (__bf16)tile[cl][rl];
+    if (last)
+      for (int z = col + 1; z < pad_end; ++z) dst[z] = (__bf16)0.f;
+  }
+}
+
+void launch_nonlin_prep_t(const float* h3, const int* off, const int* o8, const int* map, int R,
+                          int hid, int R8, void* t1t, hipStream_t st) {
+  if (R <= 0) return;
+  ZASR_REQUIRE(hid % 4 == 0, "nonlin_prep_t: hid must be a multiple of 4");
+  hipLaunchKernelGGL(nonlin_prep_t_kernel, dim3(cdiv(R, 64), cdiv(hid, 64)), dim3(256), 0, st,
+                     h3, off, o8, map, R, hid, R8, reinterpret_cast<__bf16*>(t1t));
+}
+
+}  // namespace zasr

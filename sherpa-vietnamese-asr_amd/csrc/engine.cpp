@@ -727,19 +727,37 @@ struct MetaPack {
 void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, const int* d_off,
                            const int* d_map,
                            const std::vector<int>& lens, const long* d_aoff,
-                           const void* d_slices_nl, int maxL) {
+                           const void* d_slices_nl, int maxL, const int* d_o8, int R8) {
   const int d = S.d, h = S.h, B = (int)lens.size();
   const int hid = 3 * d / 4;
   float* O = ws<float>("ly_orig", (size_t)R * d);
   ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
   // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
-  float* qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
-  linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
-  float* A = ws<float>("ly_attn", 1);  // sized by caller: head-0 weights (nonlin_attention)
-  float* stats = ws<float>("ly_attn_stats", (size_t)R * h * 2);
-  {
+  const bool bf16 = precision_ == 1;
+  float* qkp = nullptr;
+  float* A = nullptr;
+  __bf16* A16 = nullptr;
+  float* stats = nullptr;
+  AttnFlashArgs fa{};
+  if (bf16) {
+    // flash-style attention on bf16 q / k / v (attn_kernels.hip): head 0's normalised weights
+    // for the NonlinAttention GEMM; every head's statistics come from self_attn1
+    qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
+    linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
+    A16 = ws<__bf16>("ly_attn_h", 1);  // sized by the caller
+    stats = ws<float>("ly_attn_stats", (size_t)R * h);
+    fa = AttnFlashArgs{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A16,
+                       nullptr, nullptr, stats, stats};
+    prof_begin("attn_softmax");
+    launch_attn_flash(fa, 0, st_);
+    prof_end();
+  } else {
     // head 0 only: its normalised weights feed nonlin_attention; every head's statistics
     // come from self_attn1's online softmax
+    qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
+    linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
+    A = ws<float>("ly_attn", 1);  // sized by the caller
+    stats = ws<float>("ly_attn_stats", (size_t)R * h * 2);
     AttnArgs a{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A, stats, 1};
     prof_begin("attn_softmax");
     launch_attn_softmax(a, st_);
@@ -758,12 +776,25 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     }
   };
   auto self_attn = [&](int k) {
+    if (bf16) {
+      __bf16* vv = ws<__bf16>("ly_vv_h", (size_t)R * 12 * h);
+      __bf16* oa = ws<__bf16>("ly_oa_h", (size_t)R * 12 * h);
+      linear_h(Ly.sa_in[k], X, false, d, R, vv, true, 12 * h, EPI_NONE);
+      AttnFlashArgs a = fa;
+      a.v = vv;
+      a.out = oa;
+      prof_begin("attn_apply");
+      launch_attn_flash(a, k == 0 ? 1 : 2, st_);
+      prof_end();
+      linear_h(Ly.sa_out[k], oa, true, 12 * h, R, X, false, d, EPI_RESADD);
+      return;
+    }
     float* vv = ws<float>("ly_vv", (size_t)R * 12 * h);
     float* oa = ws<float>("ly_oa", (size_t)R * 12 * h);
     linear(Ly.sa_in[k], X, d, R, vv, 12 * h, EPI_NONE);
     AttnSAArgs sa{qkp, h, Ly.pos_tab, model_.pmax, d_off, B, maxL, stats, vv, oa, stats};
     prof_begin("attn_apply");
-    launch_attn_sa(sa, k == 0, precision_ == 1, st_);
+    launch_attn_sa(sa, k == 0, false, st_);
     prof_end();
     linear(Ly.sa_out[k], oa, 12 * h, R, X, d, EPI_RESADD);
   };
@@ -789,7 +820,34 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   // 1. feed_forward1
   ff(0);
   // 2. nonlin_attention (attention head 0 only)
-  {
+  if (bf16) {
+    // z = (A0 @ t1) * y on bf16 MFMA: A0 [L][L8] bf16, t1^T [hid][R8] bf16, z bf16
+    float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
+    __bf16* t1t = ws<__bf16>("ly_t1t", (size_t)hid * R8);
+    __bf16* z = ws<__bf16>("ly_z_h", (size_t)R * hid);
+    linear(Ly.na_in, X, d, R, h3, 3 * hid, EPI_NONE);
+    prof_begin("elementwise");
+    launch_nonlin_prep_t(h3, d_off, d_o8, d_map, R, hid, R8, t1t, st_);
+    prof_end();
+    GemmParams p{};
+    p.A = reinterpret_cast<const float*>(A16);
+    p.B = nullptr;
+    p.sbk = 1;
+    p.sbn = R8;
+    p.C = reinterpret_cast<float*>(z);
+    p.ldc = hid;
+    p.N = hid;
+    p.alpha = 1.f;
+    p.aux = h3 + 2 * hid;
+    p.ldaux = 3 * hid;
+    p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
+    p.num_slices = B;
+    p.max_M = maxL;
+    prof_begin("attn_nonlin");
+    gemm_bf16(p, t1t, EPI_MULAUX, ALOAD_DENSE, st_, true, true);
+    prof_end();
+    linear_h(Ly.na_out, z, true, hid, R, X, false, d, EPI_RESADD);
+  } else {
     float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
     float* t1 = ws<float>("ly_t1", (size_t)R * hid);
     float* z = ws<float>("ly_z", (size_t)R * hid);
@@ -853,6 +911,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   std::vector<LevelMeta> mst(ns);
   std::vector<std::vector<long>> aoff(ns);
   std::vector<std::vector<GemmSlice>> sl_nl(ns);
+  std::vector<std::vector<int>> o8(ns);
+  std::vector<int> R8(ns, 0);
+  const bool bf16 = precision_ == 1;
   size_t attn_floats = 0;
   int maxL_all = 0;
   for (int i = 0; i < ns; ++i) {
@@ -863,23 +924,29 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     maxL_all = std::max(maxL_all, mst[i].maxlen);
     long acc = 0;
     const int hid = 3 * s.d / 4;
+    int c8 = 0;
     for (int b = 0; b < B; ++b) {
-      const int Lb = len[b], L4 = (Lb + 3) & ~3;
+      const int Lb = len[b], L4 = (Lb + 3) & ~3, L8 = (Lb + 7) & ~7;
+      const int Lp = bf16 ? L8 : L4;  // weight row stride (bf16: the GEMM's K padding)
       aoff[i].push_back(acc);
+      o8[i].push_back(c8);
       GemmSlice g{};
       g.a_off = acc;  // head 0 block of this sequence
-      g.b_off = (long)mst[i].off[b] * hid;
-      g.c_off = g.b_off;
+      g.b_off = bf16 ? (long)c8 : (long)mst[i].off[b] * hid;  // bf16: column of t1^T
+      g.c_off = (long)mst[i].off[b] * hid;
       g.aux_off = (long)mst[i].off[b] * 3 * hid;
       g.M = Lb;
-      g.K = Lb;
-      g.lda = L4;
+      g.K = bf16 ? L8 : Lb;
+      g.lda = Lp;
       sl_nl[i].push_back(g);
-      acc += (long)Lb * L4;  // only head 0 is materialised (nonlin_attention)
+      acc += (long)Lb * Lp;  // only head 0 is materialised (nonlin_attention)
+      c8 += L8;
     }
+    o8[i].push_back(c8);
+    R8[i] = c8;
     attn_floats = std::max(attn_floats, (size_t)acc);
   }
-  ensure_pos_tables(maxL_all + 64);
+  ensure_pos_tables(maxL_all + 192);  // the bf16 attention stages rows up to L + 160
   // frontend conv slices
   std::vector<GemmSlice> sl_c2(B), sl_c3(B);
   for (int b = 0; b < B; ++b) {
@@ -892,9 +959,10 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
          o_L = mp.add(mL.off.data(), (B + 1) * 4), o_out = mp.add(mout.off.data(), (B + 1) * 4);
   size_t o_c2s = mp.add(sl_c2.data(), B * sizeof(GemmSlice)),
          o_c3s = mp.add(sl_c3.data(), B * sizeof(GemmSlice));
-  std::vector<size_t> o_st(ns), o_ao(ns), o_sn(ns);
+  std::vector<size_t> o_st(ns), o_ao(ns), o_sn(ns), o_o8(ns);
   for (int i = 0; i < ns; ++i) {
     o_st[i] = mp.add(mst[i].off.data(), (B + 1) * 4);
+    o_o8[i] = mp.add(o8[i].data(), (B + 1) * 4);
     o_ao[i] = mp.add(aoff[i].data(), B * sizeof(long));
     o_sn[i] = mp.add(sl_nl[i].data(), sl_nl[i].size() * sizeof(GemmSlice));
   }
@@ -988,7 +1056,10 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   prof_end();
 
   // ---------------- encoder stacks ----------------
-  ws<float>("ly_attn", std::max<size_t>(attn_floats, 1));
+  if (bf16)
+    ws<__bf16>("ly_attn_h", std::max<size_t>(attn_floats, 1));
+  else
+    ws<float>("ly_attn", std::max<size_t>(attn_floats, 1));
   const int Dm = cfg.max_dim();
   float* full = ws<float>("st_full", (size_t)mL.total * Dm);
   float* prev = e0;
@@ -1013,7 +1084,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     for (const DLayer& ly : s.layers)
       layer_forward(s, ly, X, mst[i].total, I(o_st[i]), st_map[i], mst[i].len,
                     reinterpret_cast<const long*>(d_meta + o_ao[i]), d_meta + o_sn[i],
-                    mst[i].maxlen);
+                    mst[i].maxlen, I(o_o8[i]), R8[i]);
     float* out = orig;
     if (s.ds != 1) {
       out = ws<float>("st_out" + std::to_string(i % 2), (size_t)mL.total * d);

@@ -562,6 +562,12 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
       case EPI_RESADD: return launch_bk_h<ALOAD_DENSE, EPI_RESADD, __bf16, float>(p, B, st);
       default: break;
     }
+  } else if (aload == ALOAD_DENSE && a_bf16 && c_bf16) {
+    switch (epi) {
+      case EPI_NONE: return launch_bk_h<ALOAD_DENSE, EPI_NONE, __bf16, __bf16>(p, B, st);
+      case EPI_MULAUX: return launch_bk_h<ALOAD_DENSE, EPI_MULAUX, __bf16, __bf16>(p, B, st);
+      default: break;
+    }
   } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR && !a_bf16 && !c_bf16) {
     return launch_bk_h<ALOAD_CONV2, EPI_SWOOSHR, float, float>(p, B, st);
   } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR && !a_bf16 && !c_bf16) {

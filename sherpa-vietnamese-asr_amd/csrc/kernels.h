@@ -84,6 +84,32 @@ struct AttnArgs {
   int write_heads;
 };
 void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
+// bf16 mode, flash-style attention (attn_kernels.hip): qkp f32, v / out in bf16.
+//   mode 0: head-0 normalised weights in bf16, [L][L8] per sequence at a_off[b] (columns
+//           [L, L8) zero; L8 = L rounded up to 8), the NonlinAttention GEMM operand
+//   mode 1: self-attention with running statistics; writes out and stats_out
+//   mode 2: self-attention with the statistics of mode 1 (stats_in)
+// stats: [R][H] c = row max + log2(row sum), log2 domain
+struct AttnFlashArgs {
+  const float* qkp;        // [R][68 H]
+  int H;
+  const float* pos_tab;    // [(2 pmax - 1)][4 H]
+  int pmax;
+  const int* row_off;      // [B+1]
+  const long* a_off;       // [B] (mode 0)
+  int nseq;
+  int max_len;
+  __bf16* attn;            // mode 0
+  const __bf16* v;         // [R][12 H]
+  __bf16* out;             // [R][12 H]
+  const float* stats_in;   // mode 2
+  float* stats_out;        // mode 1
+};
+void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st);
+// t1t[c][o8_b + j] = bf16(tanh(h3[r][c]) * h3[r][hid + c]) for packed row r = off_b + j;
+// columns [o8_b + L_b, o8_b + L8_b) zero; t1t row stride R8 = sum_b L8_b
+void launch_nonlin_prep_t(const float* h3, const int* off, const int* o8, const int* map, int R,
+                          int hid, int R8, void* t1t, hipStream_t st);
 // fused self-attention consumer: out[:, 12h:12h+12] = softmax(S_h) V_h, recomputing S
 struct AttnSAArgs {
   const float* qkp;

@@ -202,7 +202,8 @@ def _token_agreement(a, b):
 
 def test_bf16_mode_encoder_and_tokens(need_gpu):
     """bf16 mode (bf16 GEMM/joiner/decoder operands, f32 accumulate/softmax/norms/search) vs
-    the fp32 path: encoder_out within 0.15 * max(1, |oracle|); greedy token agreement with
+    the fp32 path: encoder_out within 0.05 * max(1, |oracle|) (measured 0.015; a double-scaled
+    positional term measured 0.03, so the bound is kept tight); greedy token agreement with
     fp32 >= 0.85 mean, >= 0.7 worst chunk (measured rates in gpurun_out/bf16_report.json)."""
     from model_fixtures import m_model
     from oracle.fbank import fbank
@@ -226,11 +227,36 @@ def test_bf16_mode_encoder_and_tokens(need_gpu):
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/bf16_report.json", "w") as fh:
         json.dump({"encoder_max_scaled_err": errs, "token_agreement": agree, "fp32_tokens": ntok}, fh)
-    assert max(errs) <= 0.15, errs
+    assert max(errs) <= 0.05, errs
     # greedy drift: one flipped near-tie changes the decoder context for the rest of a chunk
     assert sum(agree) / len(agree) >= 0.85 and min(agree) >= 0.7, agree
     r32.close()
     r16.close()
+
+
+def test_bf16_encoder_tiny_ragged(tiny):
+    """bf16 mode on ragged batches incl. the shortest valid chunk (stacks with L <= 4, where a
+    32-key block is mostly masked): encoder_out within 0.05 * max(1, |oracle|), and batched
+    == unbatched bit-exactly (no padding, per-sequence attention)."""
+    from oracle.fbank import fbank
+    from oracle.zipformer import ZipformerOracle
+    from zasr.binding import Recognizer
+    cfg, w, path, _ = tiny
+    rec = Recognizer(path, "greedy_search", 1, precision="bf16")
+    orc = ZipformerOracle(cfg, w)
+    lens = [0.095, 0.2, 1.37, 4.0, 7.9, 21.0]
+    feats = [fbank(_speech(s, 600 + i)) for i, s in enumerate(lens)]
+    feats[0] = feats[0][:9]
+    got = rec.encode_features(feats)
+    for f, g in zip(feats, got):
+        ref = orc.encoder(f)
+        assert g.shape == ref.shape
+        err = float(np.max(np.abs(g - ref) / np.maximum(1.0, np.abs(ref))))
+        assert err <= 0.05, err
+    for f, g in zip(feats, got):
+        alone = rec.encode_features([f])[0]
+        np.testing.assert_array_equal(alone, g)
+    rec.close()
 
 
 def test_bf16_search_path_beam_hotwords(need_gpu):
