@@ -1,16 +1,21 @@
-// Fused ConvNeXt block of Conv2dSubsampling (bf16 mode):
-//   out = x + pw2(SwooshL(pw1(dwconv7x7(x) + b_dw) + b1)) + b2
-// x, out: [rows (50 Hz frames, packed over sequences)][19 freq][128 ch] f32.
+// ConvNeXt block of Conv2dSubsampling in the bf16 mode (icefall subsampling.py ConvNeXt, 3P;
+// runs inside the reference's exported encoder, core/asr_engine.py:1045-1049):
 //
-// One block = 5 frames x 19 freq = 95 positions (one 96-row MFMA M tile).  The 7x7 window's
-// 11 input frames are staged once in LDS as bf16; the depthwise conv runs on packed f32 FMAs
-// (two channels per lane) into the bf16 A tile; pw1 (128 -> 384) and pw2 (384 -> 128) run on
-// v_mfma_f32_32x32x16_bf16 in three 128-wide slices of the hidden layer, each slice's SwooshL
-// output living only in LDS.  The 384-wide hidden activation (11.5 GB per hour of audio in the
-// unfused form) never reaches HBM.  Zero padding outside each frame's own sequence (time) and
-// outside [0, 19) (freq), as the unfused path.
-#include <type_traits>
-
+//   out = x + pw2(SwooshL(pw1(dwconv7x7(x) + b_dw) + b1)) + b2
+//
+// x, out: [rows (50 Hz frames, packed over sequences)][19 freq][128 ch] bf16.  Two kernels:
+//
+// 1. convnext_dw_kernel: depthwise 7x7 with zero padding outside each frame's own sequence
+//    (time) and outside [0, 19) (freq).  Tile = 16 frames x 19 freq x 64 channels with a
+//    3-frame halo staged in LDS (bf16, 53.5 KB: two blocks per CU, one staging while the
+//    other computes).  A thread owns a channel pair (packed f32 FMAs, weights in registers)
+//    and 8 consecutive frames of one freq: every staged value read from LDS feeds up to 7
+//    output frames.  Output y = dwconv + bias in bf16.
+// 2. convnext_mlp_kernel: 128 positions (frame, freq) per block; the 384-wide hidden layer
+//    is produced in three 128-wide slices, each living only in LDS: H^T = W1 Y^T on
+//    v_mfma_f32_32x32x16_bf16 (so one lane holds 4 consecutive hidden units of one position
+//    per register group: 8-byte LDS stores), SwooshL, then O^T += W2 H^T.  Epilogue adds b2
+//    and the residual x and writes bf16.
 #include "common.h"
 #include "kernels.h"
 
@@ -20,115 +25,101 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kT = 5;            // output frames per block
-constexpr int kH = kT + 6;       // staged input frames
-constexpr int kP = kT * 19;      // 95 positions
-constexpr int kLdA = 136;        // A / H tile row stride (bf16): 272 B = odd multiple of 16 B
-constexpr int kHaloBytes = kH * 19 * 128 * 2;   // 53 504
-constexpr int kTileBytes = 96 * kLdA * 2;       // 26 112
+constexpr int kDwT = 16;                // output frames per block
+constexpr int kDwH = kDwT + 6;          // staged frames
+constexpr int kDwC = 64;                // channels per block
+constexpr int kDwItems = 2 * 19 * 32;   // (segment, freq, channel pair) work items
 
-__device__ __forceinline__ int xcd_tile_cn(int b, int nb) {
-  const int per = nb >> 3, rem = nb & 7;
-  const int xcd = b & 7, slot = b >> 3;
-  return xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
-}
+}  // namespace
 
-// depthwise 7x7 for one (freq f, channel pair) column of the 5 output frames
+// staged tile: [kDwH frames][25 = 3 + 19 + 3 freq, zero columns at the edges][kDwC] bf16
+constexpr int kDwF = 25;
+
 template <bool MASKED>
-__device__ __forceinline__ void dw_column(const __bf16* halo, int f, int c2, const float2 (&w)[49],
-                                          float2 bias, const int* lo, const int* hi,
-                                          __bf16* A) {
-  float2 acc[kT];
+__device__ __forceinline__ void dw_item(const __bf16* __restrict__ tile, int seg, int f, int p,
+                                        const float2 (&w)[49], float2 bias, const int* sLo,
+                                        const int* sHi, float2 (&acc)[8]) {
 #pragma unroll
-  for (int i = 0; i < kT; ++i) acc[i] = bias;
+  for (int i = 0; i < 8; ++i) acc[i] = bias;
+  const __bf16* base = tile + ((seg * 8) * kDwF + f) * kDwC + 2 * p;
 #pragma unroll
-  for (int rr = 0; rr < kH; ++rr) {
+  for (int rr = 0; rr < 14; ++rr) {  // staged frame seg*8 + rr <-> tap row rr - i
+    float2 v[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int ff = f + j - 3;
-      float2 v = make_float2(0.f, 0.f);
-      if (ff >= 0 && ff < 19) {
-        const bf16x2 h = *reinterpret_cast<const bf16x2*>(halo + ((rr * 19 + ff) * 128 + 2 * c2));
-        v = make_float2((float)h[0], (float)h[1]);
+    for (int j = 0; j < 7; ++j) {  // freq tap j <-> staged column f + j
+      const bf16x2 hv = *reinterpret_cast<const bf16x2*>(base + (rr * kDwF + j) * kDwC);
+      v[j] = make_float2((float)hv[0], (float)hv[1]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ti = rr - i;
+      if (ti < 0 || ti > 6) continue;
+      if (MASKED) {
+        const int dt = ti - 3;
+        if (dt < sLo[seg * 8 + i] || dt > sHi[seg * 8 + i]) continue;
       }
 #pragma unroll
-      for (int i = 0; i < kT; ++i) {
-        const int ti = rr - i;  // tap row 0..6 <-> time offset ti - 3
-        if (ti < 0 || ti > 6) continue;
-        if (MASKED && (ti - 3 < lo[i] || ti - 3 > hi[i])) continue;
-        acc[i].x = fmaf(w[ti * 7 + j].x, v.x, acc[i].x);
-        acc[i].y = fmaf(w[ti * 7 + j].y, v.y, acc[i].y);
+      for (int j = 0; j < 7; ++j) {
+        acc[i].x = fmaf(w[ti * 7 + j].x, v[j].x, acc[i].x);
+        acc[i].y = fmaf(w[ti * 7 + j].y, v[j].y, acc[i].y);
       }
     }
-  }
-#pragma unroll
-  for (int i = 0; i < kT; ++i) {
-    bf16x2 o;
-    o[0] = (__bf16)acc[i].x;
-    o[1] = (__bf16)acc[i].y;
-    *reinterpret_cast<bf16x2*>(A + (i * 19 + f) * kLdA + 2 * c2) = o;
+    // keep each frame's 7 LDS reads next to their FMAs (hoisting all 98 reads spills)
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// PHASES: bit 0 staging, bit 1 depthwise conv, bit 2 pointwise MLP (all = 7; subsets are
-// for tools/convnext_bench.hip)
-template <int PHASES>
-__global__ __launch_bounds__(256) void convnext_fused_kernel(
-    const float* __restrict__ x, const int* __restrict__ L_off, const int* __restrict__ L_map,
+__global__ __launch_bounds__(256) void convnext_dw_kernel(
+    const __bf16* __restrict__ x, const int* __restrict__ L_off, const int* __restrict__ L_map,
     int total_rows, const float* __restrict__ dw_w, const float* __restrict__ dw_b,
-    const __bf16* __restrict__ w1, const float* __restrict__ b1, const __bf16* __restrict__ w2,
-    const float* __restrict__ b2, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kHaloBytes + kTileBytes];
-  __shared__ int sLo[kT], sHi[kT], sMasked;
-  __bf16* const halo = reinterpret_cast<__bf16*>(smem);
-  __bf16* const Hs = reinterpret_cast<__bf16*>(smem);  // aliases the halo after the dwconv
-  __bf16* const As = reinterpret_cast<__bf16*>(smem + kHaloBytes);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int t0 = xcd_tile_cn(blockIdx.x, gridDim.x) * kT;
-  if (t0 >= total_rows) return;
-
-  // ---- stage frames t0-3 .. t0+7 as bf16 (zero outside [0, total_rows)) ----
-  // the 11 frames are contiguous in memory: a linear float4 copy, all of a batch's loads in
-  // flight before its LDS stores (a load -> store loop serialises on every load)
-  constexpr int kF4 = kH * 19 * 32;
-  constexpr int kIt = (kF4 + 255) / 256;  // 27
-  constexpr int kBatch = 14;
-  const float4* src = reinterpret_cast<const float4*>(x + ((long)t0 - 3) * 19 * 128);
-  const long lo4 = (long)(3 - t0) * 19 * 32;           // first valid float4 (frame 0)
-  const long hi4 = (long)(total_rows - t0 + 3) * 19 * 32;  // end (frame total_rows)
+    __bf16* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) __bf16 tile[kDwH * kDwF * kDwC];
+  __shared__ int sLo[kDwT], sHi[kDwT], sMasked;
+  const int t0 = blockIdx.x * kDwT;
+  const int c0 = blockIdx.y * kDwC;
+  const int tid = threadIdx.x;
+  if (tid == 0) sMasked = 0;
+  // ---- zero freq padding columns (3 + 3 per staged frame, 8 pieces of 16 B each) ----
+  for (int e = tid; e < kDwH * 6 * 8; e += 256) {
+    const int q = e & 7, cf = (e >> 3) % 6, rr = (e >> 3) / 6;
+    const int fcol = cf < 3 ? cf : 19 + cf;
+    bf16x8 z;
 #pragma unroll
-  for (int b0 = 0; b0 < kIt; b0 += kBatch) {
-    float4 v[kBatch];
-    // unconditional loads from clamped addresses, zero selected afterwards (a guarded load
-    // becomes a branch with a vmcnt(0) wait per element)
+    for (int t = 0; t < 8; ++t) z[t] = (__bf16)0.f;
+    *reinterpret_cast<bf16x8*>(tile + (rr * kDwF + fcol) * kDwC + 8 * q) = z;
+  }
+  // ---- stage frames t0-3 .. t0+18, channels c0..c0+63: 22 x 19 x 8 16-byte pieces ----
+  constexpr int kPieces = kDwH * 19 * 8;  // 3344
+  constexpr int kIt = (kPieces + 255) / 256;
+  bf16x8 v[kIt];
 #pragma unroll
-    for (int q = 0; q < kBatch; ++q) {
-      const int e = tid + 256 * (b0 + q);
-      long ec = e < lo4 ? lo4 : e;
-      ec = ec >= hi4 ? hi4 - 1 : ec;
-      ec = ec >= kF4 ? kF4 - 1 : ec;
-      const float4 t = src[ec];
-      const bool ok = b0 + q < kIt && e < kF4 && e >= lo4 && e < hi4;
-      v[q] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  for (int k = 0; k < kIt; ++k) {
+    const int e = tid + 256 * k;
+    const int ec = e < kPieces ? e : kPieces - 1;
+    const int rf = ec >> 3, q = ec & 7;
+    const int rr = rf / 19, f = rf - rr * 19;
+    int r = t0 - 3 + rr;
+    const bool ok = e < kPieces && r >= 0 && r < total_rows;
+    r = r < 0 ? 0 : (r >= total_rows ? total_rows - 1 : r);
+    v[k] = *reinterpret_cast<const bf16x8*>(x + ((long)r * 19 + f) * 128 + c0 + 8 * q);
+    if (!ok) {
 #pragma unroll
-    for (int q = 0; q < kBatch; ++q) {
-      const int e = tid + 256 * (b0 + q);
-      if (b0 + q < kIt && e < kF4) {
-        bf16x2 a, b;
-        a[0] = (__bf16)v[q].x;
-        a[1] = (__bf16)v[q].y;
-        b[0] = (__bf16)v[q].z;
-        b[1] = (__bf16)v[q].w;
-        bf16x2* d = reinterpret_cast<bf16x2*>(halo + 4 * e);
-        d[0] = a;
-        d[1] = b;
-      }
+      for (int t = 0; t < 8; ++t) v[k][t] = (__bf16)0.f;
     }
   }
-  if (tid < kT) {
+#pragma unroll
+  for (int k = 0; k < kIt; ++k) {
+    const int e = tid + 256 * k;
+    if (e < kPieces) {
+      const int rf = e >> 3, q = e & 7;
+      const int rr = rf / 19, f = rf - rr * 19;
+      *reinterpret_cast<bf16x8*>(tile + (rr * kDwF + 3 + f) * kDwC + 8 * q) = v[k];
+    }
+  }
+  if (tid < kDwT) {
     const int r = t0 + tid;
     int lo = -3, hi = 3;
     if (r < total_rows) {
@@ -139,120 +130,166 @@ __global__ __launch_bounds__(256) void convnext_fused_kernel(
     sLo[tid] = lo;
     sHi[tid] = hi;
   }
-  if (tid == 0) sMasked = 0;
-  // padding row 95 of the A tile
-  if (tid < kLdA / 2) reinterpret_cast<unsigned*>(As + 95 * kLdA)[tid] = 0u;
   __syncthreads();
-  if (tid < kT && (sLo[tid] != -3 || sHi[tid] != 3)) atomicOr(&sMasked, 1);
+  if (tid < kDwT && (sLo[tid] != -3 || sHi[tid] != 3)) atomicOr(&sMasked, 1);
   __syncthreads();
 
-  // ---- depthwise 7x7: lane owns channels (2 c2, 2 c2 + 1), freq f = fg + 4 k ----
-  if constexpr ((PHASES & 2) != 0) {
-    const int c2 = tid & 63, fg = tid >> 6;
-    float2 w[49];
+  const int p = tid & 31;  // channel pair c0 + 2p, c0 + 2p + 1 (fixed per thread)
+  float2 w[49];
 #pragma unroll
-    for (int k = 0; k < 49; ++k) w[k] = make_float2(dw_w[(2 * c2) * 49 + k], dw_w[(2 * c2 + 1) * 49 + k]);
-    const float2 bias = make_float2(dw_b[2 * c2], dw_b[2 * c2 + 1]);
-    const bool masked = sMasked != 0;
-    int lo[kT], hi[kT];
+  for (int k = 0; k < 49; ++k)
+    w[k] = make_float2(dw_w[(c0 + 2 * p) * 49 + k], dw_w[(c0 + 2 * p + 1) * 49 + k]);
+  const float2 bias = make_float2(dw_b[c0 + 2 * p], dw_b[c0 + 2 * p + 1]);
+  const bool masked = sMasked != 0;
+  for (int it = tid; it < kDwItems; it += 256) {
+    const int q = it >> 5;  // (segment, freq)
+    const int seg = q / 19, f = q - seg * 19;
+    float2 acc[8];
+    if (masked)
+      dw_item<true>(tile, seg, f, p, w, bias, sLo, sHi, acc);
+    else
+      dw_item<false>(tile, seg, f, p, w, bias, sLo, sHi, acc);
 #pragma unroll
-    for (int i = 0; i < kT; ++i) {
-      lo[i] = sLo[i];
-      hi[i] = sHi[i];
-    }
-    for (int f = fg; f < 19; f += 4) {
-      if (masked)
-        dw_column<true>(halo, f, c2, w, bias, lo, hi, As);
-      else
-        dw_column<false>(halo, f, c2, w, bias, lo, hi, As);
-    }
-  }
-  __syncthreads();
-
-  // ---- pw1 -> SwooshL -> pw2, three 128-wide slices of the hidden layer ----
-  if constexpr ((PHASES & 4) == 0) {
-    if (tid == 0 && (float)As[tid] == 12345.f) out[0] = 0.f;  // keep the earlier phases live
-    return;
-  }
-  const int col = lane & 31, half = lane >> 5;
-  f32x16 acc2[3];
-#pragma unroll
-  for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc2[rt][r] = 0.f;
-  for (int n3 = 0; n3 < 3; ++n3) {
-    // pw1: this wave's 32 hidden columns of the slice, all 96 rows, K = 128
-    const int hn = n3 * 128 + wid * 32 + col;
-    bf16x8 bw[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) bw[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
-    f32x16 acc1[3];
-#pragma unroll
-    for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc1[rt][r] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-      for (int rt = 0; rt < 3; ++rt) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + (rt * 32 + col) * kLdA + ks * 16 + 8 * half);
-        acc1[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc1[rt], 0, 0, 0);
-      }
-    }
-    const float bb = b1[hn];
-    if (n3 > 0) __syncthreads();  // previous slice's pw2 is done reading Hs
-#pragma unroll
-    for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        Hs[row * kLdA + wid * 32 + col] = (__bf16)swooshl_fast(acc1[rt][r] + bb);
-      }
-    __syncthreads();
-    // pw2: this wave's 32 output channels, K = this slice's 128 hidden units
-    const int on = wid * 32 + col;
-    bf16x8 bw2[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      bw2[ks] = *reinterpret_cast<const bf16x8*>(w2 + (long)on * 384 + n3 * 128 + ks * 16 + 8 * half);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-      for (int rt = 0; rt < 3; ++rt) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Hs + (rt * 32 + col) * kLdA + ks * 16 + 8 * half);
-        acc2[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw2[ks], acc2[rt], 0, 0, 0);
+    for (int i = 0; i < 8; ++i) {
+      const int r = t0 + seg * 8 + i;
+      if (r < total_rows) {
+        bf16x2 o;
+        o[0] = (__bf16)acc[i].x;
+        o[1] = (__bf16)acc[i].y;
+        *reinterpret_cast<bf16x2*>(y + ((long)r * 19 + f) * 128 + c0 + 2 * p) = o;
       }
     }
   }
-
-  // ---- out = x + pw2 + b2 (f32) ----
-  const int on = wid * 32 + col;
-  const float bo = b2[on];
-  const long p0 = (long)t0 * 19;
-  const long pend = (long)total_rows * 19;
-#pragma unroll
-  for (int rt = 0; rt < 3; ++rt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const long p = p0 + row;
-      if (row < kP && p < pend) {
-        const long o = p * 128 + on;
-        out[o] = x[o] + (acc2[rt][r] + bo);
-      }
-    }
 }
 
+// =====================================================================================
+// pointwise MLP + residual.  Y / H tiles in LDS: [128 positions][136] bf16 (272-byte rows:
+// conflict-free 16-byte fragment reads).  Wave w owns hidden (pw1) / output (pw2) columns
+// 32 w .. 32 w + 31 of each 128-wide slice, for all 128 positions (4 MFMA tiles).
+// =====================================================================================
+namespace {
+constexpr int kMlpM = 128;
+constexpr int kMlpLd = 136;
 }  // namespace
 
-void launch_convnext_fused(const float* x, const int* L_off, const int* L_map, int total_rows,
-                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
-                           const void* w2, const float* b2, float* out, hipStream_t st) {
+__global__ __launch_bounds__(256) void convnext_mlp_kernel(
+    const __bf16* __restrict__ yin, const __bf16* __restrict__ x, long npos,
+    const __bf16* __restrict__ w1, const float* __restrict__ b1, const __bf16* __restrict__ w2,
+    const float* __restrict__ b2, __bf16* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) __bf16 Ys[kMlpM * kMlpLd];
+  __shared__ __attribute__((aligned(16))) __bf16 Hs[kMlpM * kMlpLd];
+  const long p0 = (long)blockIdx.x * kMlpM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int col = lane & 31, half = lane >> 5;
+  // ---- Y tile: 128 x 128 bf16 = 2048 16-byte pieces, 8 per thread ----
+  {
+    bf16x8 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = tid + 256 * k;
+      long pp = p0 + (e >> 4);
+      pp = pp < npos ? pp : npos - 1;
+      v[k] = *reinterpret_cast<const bf16x8*>(yin + pp * 128 + 8 * (e & 15));
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = tid + 256 * k;
+      *reinterpret_cast<bf16x8*>(Ys + (e >> 4) * kMlpLd + 8 * (e & 15)) = v[k];
+    }
+  }
+  __syncthreads();
+
+  f32x16 acc2[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc2[t][r] = 0.f;
+
+  for (int n3 = 0; n3 < 3; ++n3) {
+    // ---- H^T slice: rows = hidden units n3*128 + 32 wid + (0..31), cols = positions ----
+    const int hn = n3 * 128 + wid * 32 + col;
+    bf16x8 wf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      wf[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
+    f32x16 acc1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[t][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 yf =
+            *reinterpret_cast<const bf16x8*>(Ys + (t * 32 + col) * kMlpLd + ks * 16 + 8 * half);
+        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], yf, acc1[t], 0, 0, 0);
+      }
+    }
+    // bias of the 16 hidden rows this lane holds: wid*32 + (r&3) + 8 (r>>2) + 4 half
+    float bb[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bb[r] = b1[n3 * 128 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+    if (n3 > 0) __syncthreads();  // the previous slice's pw2 is done reading Hs
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 hv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[e] = (__bf16)swooshl_fast(acc1[t][4 * g + e] + bb[4 * g + e]);
+        *reinterpret_cast<bf16x4*>(Hs + (t * 32 + col) * kMlpLd + wid * 32 + 8 * g + 4 * half) = hv;
+      }
+    __syncthreads();
+    // ---- O^T += W2[:, slice] H^T: rows = output channels 32 wid + (0..31) ----
+    const int on = wid * 32 + col;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      wf[ks] = *reinterpret_cast<const bf16x8*>(w2 + (long)on * 384 + n3 * 128 + ks * 16 + 8 * half);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 hf =
+            *reinterpret_cast<const bf16x8*>(Hs + (t * 32 + col) * kMlpLd + ks * 16 + 8 * half);
+        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], hf, acc2[t], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- out = x + O + b2: lane holds position t*32 + col, channels 32 wid + 8 g + 4 half + e ----
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int ch = wid * 32 + 8 * g + 4 * half;
+    const float4 bo = *reinterpret_cast<const float4*>(b2 + ch);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const long pp = p0 + t * 32 + col;
+      if (pp >= npos) continue;
+      const bf16x4 xr = *reinterpret_cast<const bf16x4*>(x + pp * 128 + ch);
+      bf16x4 o;
+      o[0] = (__bf16)((float)xr[0] + (acc2[t][4 * g + 0] + bo.x));
+      o[1] = (__bf16)((float)xr[1] + (acc2[t][4 * g + 1] + bo.y));
+      o[2] = (__bf16)((float)xr[2] + (acc2[t][4 * g + 2] + bo.z));
+      o[3] = (__bf16)((float)xr[3] + (acc2[t][4 * g + 3] + bo.w));
+      *reinterpret_cast<bf16x4*>(out + pp * 128 + ch) = o;
+    }
+  }
+}
+
+void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int total_rows,
+                          const float* dw_w, const float* dw_b, const void* w1, const float* b1,
+                          const void* w2, const float* b2, void* ytmp, void* out,
+                          hipStream_t st) {
   if (total_rows <= 0) return;
-  const int nb = cdiv(total_rows, kT);
-  hipLaunchKernelGGL(convnext_fused_kernel<7>, dim3(nb), dim3(256), 0, st, x, L_off, L_map,
-                     total_rows, dw_w, dw_b, reinterpret_cast<const __bf16*>(w1), b1,
-                     reinterpret_cast<const __bf16*>(w2), b2, out);
+  const __bf16* xb = reinterpret_cast<const __bf16*>(x);
+  __bf16* yb = reinterpret_cast<__bf16*>(ytmp);
+  hipLaunchKernelGGL(convnext_dw_kernel, dim3(cdiv(total_rows, kDwT), 128 / kDwC), dim3(256), 0,
+                     st, xb, L_off, L_map, total_rows, dw_w, dw_b, yb);
+  const long npos = (long)total_rows * 19;
+  hipLaunchKernelGGL(convnext_mlp_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
+                     yb, xb, npos, reinterpret_cast<const __bf16*>(w1), b1,
+                     reinterpret_cast<const __bf16*>(w2), b2, reinterpret_cast<__bf16*>(out));
 }
 
 }  // namespace zasr

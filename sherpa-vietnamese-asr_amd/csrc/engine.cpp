@@ -503,6 +503,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
     hw_.delta = dl;
     hw_.node_score = ns;
   }
+  ZASR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_pinned_), 64, hipHostMallocDefault));
   ZASR_HIP_CHECK(hipDeviceSynchronize());
 }
 
@@ -523,6 +524,7 @@ Engine::~Engine() {
     (void)hipEventDestroy(pe.a);
     (void)hipEventDestroy(pe.b);
   }
+  if (h_pinned_) (void)hipHostFree(h_pinned_);
   (void)hipStreamDestroy(stream_);
 }
 
@@ -1009,14 +1011,14 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV2, false, st_);
     prof_end();
   }
-  float* x3 = ws<float>("fe_x3", (size_t)mL.total * 19 * 128);
+  const int d0 = cfg.dims[0];
+  float* e0 = ws<float>("fe_e0", (size_t)mL.total * d0);
   {
     GemmParams p{};
     p.A = c2;
     p.B = model_.conv7.w;
     p.sbk = 1;
     p.sbn = 288;
-    p.C = x3;
     p.ldc = 128;
     p.bias = model_.conv7.b;
     p.N = 128;
@@ -1024,33 +1026,36 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     p.slices = reinterpret_cast<const GemmSlice*>(d_meta + o_c3s);
     p.num_slices = B;
     p.max_M = mL.maxlen * 19;
-    prof_begin("frontend_conv");
-    if (model_.conv7.wh)
-      gemm_bf16(p, model_.conv7.wh, EPI_SWOOSHR, ALOAD_CONV3, st_);
-    else
+    if (model_.pw1.wh) {
+      // bf16 mode: conv.7 output, the ConvNeXt block and its output stay bf16
+      __bf16* x3 = ws<__bf16>("fe_x3_h", (size_t)mL.total * 19 * 128);
+      __bf16* y3 = ws<__bf16>("fe_y3_h", (size_t)mL.total * 19 * 128);
+      __bf16* x4 = ws<__bf16>("fe_x4_h", (size_t)mL.total * 19 * 128);
+      p.C = reinterpret_cast<float*>(x3);
+      prof_begin("frontend_conv");
+      gemm_bf16(p, model_.conv7.wh, EPI_SWOOSHR, ALOAD_CONV3, st_, false, true);
+      prof_end();
+      prof_begin("frontend_conv");
+      launch_convnext_bf16(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, model_.pw1.wh,
+                           model_.pw1.b, model_.pw2.wh, model_.pw2.b, y3, x4, st_);
+      prof_end();
+      linear_h(model_.out, x4, true, 2432, mL.total, e0, false, d0, EPI_NONE);
+    } else {
+      float* x3 = ws<float>("fe_x3", (size_t)mL.total * 19 * 128);
+      p.C = x3;
+      prof_begin("frontend_conv");
       gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
-    prof_end();
+      prof_end();
+      float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
+      prof_begin("frontend_conv");
+      launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+      prof_end();
+      float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
+      linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
+      linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
+      linear(model_.out, x3, 2432, mL.total, e0, d0, EPI_NONE);
+    }
   }
-  if (model_.pw1.wh) {
-    // bf16 mode: the whole ConvNeXt block in one kernel, hidden layer kept on chip
-    float* x4 = ws<float>("fe_x4", (size_t)mL.total * 19 * 128);
-    prof_begin("frontend_conv");
-    launch_convnext_fused(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, model_.pw1.wh,
-                          model_.pw1.b, model_.pw2.wh, model_.pw2.b, x4, st_);
-    prof_end();
-    x3 = x4;
-  } else {
-    float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
-    prof_begin("frontend_conv");
-    launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
-    prof_end();
-    float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
-    linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
-    linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
-  }
-  const int d0 = cfg.dims[0];
-  float* e0 = ws<float>("fe_e0", (size_t)mL.total * d0);
-  linear(model_.out, x3, 2432, mL.total, e0, d0, EPI_NONE);
   prof_begin("elementwise");
   launch_bias_norm(e0, mL.total, d0, model_.out_norm_b, model_.out_norm_ls, nullptr, nullptr, st_);
   prof_end();
@@ -1171,6 +1176,48 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   ZASR_HIP_CHECK(hipMemsetAsync(J, 0, slots * D * (bf16 ? 2 : 4), st_));
   DecTable dt{model_.dec_table, V, d_enc, d_eo, d_el, J, D, bf16 ? 1 : 0};
   DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
+  // greedy with the decoder-context table: speculative windows (kernels.h, greedy_spec)
+  const char* spec_env = getenv("ZASR_GREEDY_WINDOW");
+  const int F = spec_env ? atoi(spec_env) : 8;
+  if (H == 1 && model_.dec_table && (F == 4 || F == 8)) {
+    void* Js = bf16 ? (void*)ws<__bf16>("gs_joinin_h", (size_t)S * F * D)
+                    : (void*)ws<float>("gs_joinin", (size_t)S * F * D);
+    float* lg = ws<float>("gs_logits", (size_t)S * F * V);
+    int* d_t = ws<int>("gs_t", S);
+    int* d_active = ws<int>("gs_active", 2);
+    DecTable ds{model_.dec_table, V, d_enc, d_eo, d_el, Js, D, bf16 ? 1 : 0};
+    prof_begin("search");
+    launch_search_init(st, S, 1, st_);
+    launch_greedy_spec_init(ds, S, F, d_t, d_active, st_);
+    prof_end();
+    // every super-step advances each live stream by >= 1 frame: Tmax steps at most; the
+    // host checks the live-stream count every kSync steps (one small D2H copy)
+    constexpr int kSync = 16;
+    int k = 0;
+    while (k < Tmax) {
+      for (int b = 0; b < kSync && k < Tmax; ++b, ++k) {
+        prof_begin("joiner");
+        if (bf16) {
+          JoinerBf16Args ja{reinterpret_cast<const __bf16*>(Js),
+                            reinterpret_cast<const __bf16*>(model_.joiner.wh), model_.joiner.b, lg,
+                            S * F, V, D, d_t, d_el, F};
+          launch_joiner_bf16(ja, st_);
+        } else {
+          JoinerArgs ja{reinterpret_cast<const float*>(Js), model_.joiner.w, model_.joiner.b, lg,
+                        S * F, V, D, d_t, d_el, F};
+          launch_joiner(ja, st_);
+        }
+        prof_end();
+        prof_begin("search");
+        launch_greedy_spec(st, lg, V, S, F, d_t, d_el, hw_, ds, d_active, k & 1, st_);
+        prof_end();
+      }
+      ZASR_HIP_CHECK(hipMemcpyAsync(h_pinned_, d_active + ((k - 1) & 1), sizeof(int),
+                                    hipMemcpyDeviceToHost, st_));
+      ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+      if (*h_pinned_ == 0) break;
+    }
+  } else {
   prof_begin("search");
   launch_search_init(st, S, H, st_);
   if (model_.dec_table) launch_table_init(dt, S, H, st_);
@@ -1200,6 +1247,7 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     prof_begin("search");
     launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, model_.dec_table ? &dt : nullptr, st_);
     prof_end();
+  }
   }
   const int cap = Tmax;
   int* o_tok = ws<int>("so_tok", (size_t)S * cap);

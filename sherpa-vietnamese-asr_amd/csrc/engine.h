@@ -165,6 +165,7 @@ class Engine {
   float* d_window_ = nullptr;
   int* d_mel_meta_ = nullptr;  // start[80], len[80], woff[80]
   float* d_mel_w_ = nullptr;
+  int* h_pinned_ = nullptr;  // pinned host word (live-stream count of the greedy search)
   // hotword tables
   HotwordDFA hw_host_;
   HotwordTables hw_{};

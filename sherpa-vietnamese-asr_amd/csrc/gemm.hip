@@ -572,6 +572,8 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
     return launch_bk_h<ALOAD_CONV2, EPI_SWOOSHR, float, float>(p, B, st);
   } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR && !a_bf16 && !c_bf16) {
     return launch_bk_h<ALOAD_CONV3, EPI_SWOOSHR, float, float>(p, B, st);
+  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR && !a_bf16 && c_bf16) {
+    return launch_bk_h<ALOAD_CONV3, EPI_SWOOSHR, float, __bf16>(p, B, st);
   }
   throw std::runtime_error("gemm_bf16: unsupported (aload, epi, operand types) combination");
 }

@@ -29,11 +29,12 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const i
                   int total_rows, const float* w /*[8][9]*/, const float* b, float* out,
                   hipStream_t st);
 // ConvNeXt depthwise 7x7, zero padding per sequence: [L][19][128] -> [L][19][128]
-// bf16 mode: out = x + pw2(SwooshL(pw1(dwconv7x7(x)))) in one kernel (convnext_kernels.hip);
-// w1 / w2 are the bf16 pw weights, out must not alias x
-void launch_convnext_fused(const float* x, const int* L_off, const int* L_map, int total_rows,
-                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
-                           const void* w2, const float* b2, float* out, hipStream_t st);
+// bf16 mode: out = x + pw2(SwooshL(pw1(dwconv7x7(x)))) (convnext_kernels.hip), x / out /
+// ytmp (the depthwise output) bf16 [rows][19][128]; w1 / w2 the bf16 pw weights
+void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int total_rows,
+                          const float* dw_w, const float* dw_b, const void* w1, const float* b1,
+                          const void* w2, const float* b2, void* ytmp, void* out,
+                          hipStream_t st);
 void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
                      const float* w /*[128][49]*/, const float* b, float* out, hipStream_t st);
 
@@ -176,12 +177,17 @@ struct DecJoinArgs {
   int M, H, t;
   int j_bf16;
 };
+// live_t / live_len / live_f (optional): rows are (stream, window frame) = (r / live_f,
+// r % live_f); a 32-row tile whose streams are all finished (live_t >= live_len) is skipped
 struct JoinerArgs {
   const float* J;        // [M][D]
   const float* W;        // [V][D]
   const float* bias;     // [V]
   float* out;            // [M][V]
   int M, V, D;
+  const int* live_t = nullptr;
+  const int* live_len = nullptr;
+  int live_f = 0;
 };
 struct JoinerBf16Args {
   const __bf16* J;       // [M][D]
@@ -189,6 +195,9 @@ struct JoinerBf16Args {
   const float* bias;     // [V]
   float* out;            // [M][V]
   int M, V, D;
+  const int* live_t = nullptr;
+  const int* live_len = nullptr;
+  int live_f = 0;
 };
 // Decoder-context table: the stateless decoder is a pure function of the two-token context
 // (y_-2, y_-1) (core/asr_engine.py:1051-1056, 1072-1088 cache it per context), so the engine
@@ -217,6 +226,20 @@ void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st);
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
                         int beam, int t, const int* enc_len, const HotwordTables& hw,
                         const DecTable* dt, hipStream_t st);
+// ---- speculative greedy search (beam 1 with the decoder-context table) ----
+// Greedy keeps the decoder context across blank frames, so the joiner rows of the next F
+// frames of a stream are all known until the first emission.  One super-step = the joiner
+// over [S][F] rows (J rows written by the previous super-step) + greedy_spec: per stream,
+// the exact per-frame top-1 of the frame-by-frame step (same f32 score arithmetic, same
+// smaller-index tie break) for every frame of the window under the all-blank-so-far
+// hypothesis, then the first non-blank frame (if any) is the emission; t_cur advances past
+// it (or by the window).  Streams still running after the step add 1 to active[parity].
+// J layout: [S][F][D] (row s * F + f = frame t_cur[s] + f).
+void launch_greedy_spec_init(const DecTable& dt, int S, int F, int* t_cur, int* active,
+                             hipStream_t st);
+void launch_greedy_spec(const SearchState& s, const float* logits, int V, int S, int F,
+                        int* t_cur, const int* enc_len, const HotwordTables& hw,
+                        const DecTable& dt, int* active, int parity, hipStream_t st);
 void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTables& hw,
                          int out_cap, int* out_tok, int* out_frame, double* out_lp,
                          float4* out_stats, int* out_count, hipStream_t st);

@@ -127,6 +127,16 @@ __device__ __forceinline__ void splitk_reduce(f32x16& acc, float* red) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// all streams of joiner rows m0 .. m0 + 31 finished (speculative greedy windows)
+__device__ __forceinline__ bool tile_done(const int* live_t, const int* live_len, int F, int m0,
+                                          int M) {
+  if (!live_t) return false;
+  const int s0 = m0 / F, s1 = (min(m0 + 32, M) - 1) / F;
+  for (int s = s0; s <= s1; ++s)
+    if (live_t[s] < live_len[s]) return false;
+  return true;
+}
+
 // tanh(x) = 1 - 2 / (exp(2x) + 1): saturates correctly at +-inf (bf16 joiner input only)
 __device__ __forceinline__ float fast_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
 
@@ -288,6 +298,7 @@ __global__ __launch_bounds__(256) void joiner_kernel(JoinerArgs j) {
   float* As = smem;
   float* red = smem + 32 * lda;
   const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M)) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int d4 = D / 4;
   for (int e = tid; e < 32 * d4; e += 256) {
@@ -341,6 +352,7 @@ __global__ __launch_bounds__(256) void joiner_bf16_kernel(JoinerBf16Args j) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int col = lane & 31, h = lane >> 5;
   const int m0 = blockIdx.y * 32;
+  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M)) return;
   const int n = blockIdx.x * 32 + col;
   const bool nv = n < j.V;
   const int D = j.D;
@@ -791,6 +803,261 @@ void launch_search_step(const SearchState& s, const float* logits, int V, int S,
   }
 #undef ZASR_STEP
 #undef ZASR_STEP3
+}
+
+// --------------------------------------------------------------------------------------
+// speculative greedy (kernels.h).  J of the first window: frames 0 .. F-1, context (0, 0).
+// --------------------------------------------------------------------------------------
+__global__ void greedy_spec_init_kernel(DecTable dt, int S, int F, int* t_cur, int* active) {
+  const int d4 = dt.D / 4;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 2) active[i] = 0;
+  if (i >= (long)S * F * d4) return;
+  const int c4 = (int)(i % d4);
+  const long sf = i / d4;
+  const int s = (int)(sf / F), f = (int)(sf - (long)s * F);
+  if (f == 0 && c4 == 0) t_cur[s] = 0;
+  if (f >= dt.enc_len[s]) return;
+  const float4 e = *reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + f) * dt.D + 4 * c4);
+  const float4 d = *reinterpret_cast<const float4*>(dt.table + 4 * c4);
+  store_j4(dt, sf * dt.D + 4 * c4, e, d);
+}
+
+void launch_greedy_spec_init(const DecTable& dt, int S, int F, int* t_cur, int* active,
+                             hipStream_t st) {
+  if (S <= 0) return;
+  ZASR_REQUIRE(dt.D % 4 == 0, "joiner dim must be a multiple of 4");
+  const long n = std::max<long>((long)S * F * (dt.D / 4), 2);
+  hipLaunchKernelGGL(greedy_spec_init_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st,
+                     dt, S, F, t_cur, active);
+}
+
+// One block per stream, wave w owns window rows w, w + 4, ... (register resident).
+//   A. per row: max, second max, S = sum e, E1, E3 (the statistics of search_step_kernel),
+//      log S, and d0 = fl(x_blank - max)
+//   B. lf_f = the score before frame f if frames 0 .. f-1 were all blank: the reference's
+//      f32 recurrence lp <- fl(fl(d0 - log S) + fl(lp)) (a one-thread scan)
+//   C. per row, the exact top-1 of key(fl(fl(x - max) - log S) + lf_f, index) -- the
+//      candidate order of search_step_kernel at beam 1 -- so the first row whose top-1 is
+//      not blank is exactly the frame-by-frame emission
+//   D. wave 0: state, emission node, hotword transition (:1127-1131), next window's J
+template <int F, int Q>
+__global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const float* logits,
+                                                          int V, int* t_cur, const int* enc_len,
+                                                          HotwordTables hw, DecTable dt,
+                                                          int* active, int parity) {
+  constexpr int RPW = F / 4;  // rows per wave
+  const int s = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (s == 0 && tid == 0) active[parity ^ 1] = 0;  // the next super-step's counter
+  const int T_s = enc_len[s];
+  const int t0 = t_cur[s];
+  if (t0 >= T_s) return;
+  const int nf = T_s - t0 < F ? T_s - t0 : F;
+  const int V4 = V >> 2;
+  __shared__ float sLs[F], sD0[F], sLf[F], sM1[F];
+  __shared__ double sLp[F + 1];
+  __shared__ float4 sStats[F];
+  __shared__ unsigned long long sKey[F];
+
+  // ---- A. rows in registers + statistics ----
+  const float4* rows4 = reinterpret_cast<const float4*>(logits + (long)s * F * V);
+  float4 x[RPW][Q];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int f = wid + 4 * r;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane + 64 * q;
+      x[r][q] = (f < nf && i < V4) ? rows4[(long)f * V4 + i]
+                                   : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    }
+  }
+  // the current hypothesis (one slot) and, for wave 0, nothing else yet
+  const int base = s * 1;  // Hmax = 1 at beam 1 (launch_greedy_spec checks)
+  float m1r[RPW], lsr[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int f = wid + 4 * r;
+    float m1 = -INFINITY, m2 = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float4 v = x[r][q];
+      m2 = fmaxf(m2, fminf(m1, v.x)); m1 = fmaxf(m1, v.x);
+      m2 = fmaxf(m2, fminf(m1, v.y)); m1 = fmaxf(m1, v.y);
+      m2 = fmaxf(m2, fminf(m1, v.z)); m1 = fmaxf(m1, v.z);
+      m2 = fmaxf(m2, fminf(m1, v.w)); m1 = fmaxf(m1, v.w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
+      const float hi = fmaxf(m1, a1);
+      const float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
+      m1 = hi;
+      m2 = lo;
+    }
+    float se = 0.f, e1 = 0.f, e3 = 0.f;
+    auto acc = [&](float v) {
+      const float d = v - m1;
+      const float e = __expf(d);
+      se += e;
+      e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+      e3 += __expf(d * (1.0f / 3.0f));
+    };
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      acc(x[r][q].x);
+      acc(x[r][q].y);
+      acc(x[r][q].z);
+      acc(x[r][q].w);
+    }
+    se = wave_sum(se);
+    e1 = wave_sum(e1);
+    e3 = wave_sum(e3);
+    const float ls = logf(se);
+    m1r[r] = m1;
+    lsr[r] = ls;
+    if (lane == 0 && f < nf) {
+      sLs[f] = ls;
+      sM1[f] = m1;
+      sD0[f] = x[r][0].x - m1;  // blank = token 0 = lane 0's first element
+      sStats[f] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
+                              __expf(m2 - m1) / se);
+    }
+  }
+  __syncthreads();
+  // ---- B. scores before each frame under the all-blank hypothesis (f32 adds) ----
+  if (tid == 0) {
+    double lp = st.lp[base];
+    sLp[0] = lp;
+    for (int f = 0; f < nf; ++f) {
+      const float lf = (float)lp;
+      sLf[f] = lf;
+      const float lpv = sD0[f] - sLs[f];
+      lp = (double)(lpv + lf);
+      sLp[f + 1] = lp;
+    }
+  }
+  __syncthreads();
+  // ---- C. exact top-1 per row ----
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int f = wid + 4 * r;
+    if (f >= nf) continue;  // wave-uniform
+    const float lf = sLf[f], m1 = m1r[r], ls = lsr[r];
+    unsigned long long best = 0ull;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane + 64 * q;
+      if (i < V4) {
+        const float4 v = x[r][q];
+        const unsigned long long k0 = make_key(((v.x - m1) - ls) + lf, 4 * i);
+        const unsigned long long k1 = make_key(((v.y - m1) - ls) + lf, 4 * i + 1);
+        const unsigned long long k2 = make_key(((v.z - m1) - ls) + lf, 4 * i + 2);
+        const unsigned long long k3 = make_key(((v.w - m1) - ls) + lf, 4 * i + 3);
+        best = k0 > best ? k0 : best;
+        best = k1 > best ? k1 : best;
+        best = k2 > best ? k2 : best;
+        best = k3 > best ? k3 : best;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long ob = __shfl_xor(best, o, 64);
+      best = ob > best ? ob : best;
+    }
+    if (lane == 0) sKey[f] = best;
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  // ---- D. the first emission of the window (wave 0) ----
+  int fe = -1;
+  for (int f = 0; f < nf; ++f)
+    if (key_idx(sKey[f]) != 0) {
+      fe = f;
+      break;
+    }
+  const int t_new = t0 + (fe >= 0 ? fe + 1 : nf);
+  int y1 = st.y1[base], y2 = st.y2[base];
+  if (fe >= 0) {
+    const unsigned long long key = sKey[fe];
+    const float val = key_val(key);
+    const int tok = key_idx(key);
+    double score = (double)val;
+    int nhw = st.hw[base];
+    if (hw.num_states > 0 && tok != 2) {
+      const int cls = hw.tok2cls[tok];
+      if (cls < 0) {
+        score += -hw.node_score[nhw];
+        nhw = 0;
+      } else {
+        const long e = (long)nhw * hw.num_cls + cls;
+        score += hw.delta[e];
+        nhw = hw.next[e];
+      }
+    }
+    if (lane == 0) {
+      const int nid = st.node_count[s];
+      const long gi = (long)s * st.node_cap + nid;
+      const int parent = st.node[base];
+      st.node_tok[gi] = tok;
+      st.node_frame[gi] = t0 + fe;
+      st.node_parent[gi] = parent;
+      st.node_lp[gi] = (double)val - sLp[fe];
+      st.node_stats[gi] = sStats[fe];
+      st.node_count[s] = nid + 1;
+      st.lp[base] = score;
+      st.lpf[base] = 0;
+      st.hash[base] = hash_push(st.hash[base], tok);
+      st.len[base] = st.len[base] + 1;
+      st.y2[base] = y1;
+      st.y1[base] = tok;
+      st.hw[base] = nhw;
+      st.node[base] = nid;
+    }
+    y2 = y1;
+    y1 = tok;
+  } else if (lane == 0) {
+    st.lp[base] = sLp[nf];
+    st.lpf[base] = 0;
+  }
+  if (lane == 0) {
+    t_cur[s] = t_new;
+    if (t_new < T_s) atomicAdd(&active[parity], 1);
+  }
+  // ---- the next window's joiner input: J[s][f] = tanh(enc[t_new + f] + table[y2, y1]) ----
+  if (t_new < T_s) {
+    const int nf2 = T_s - t_new < F ? T_s - t_new : F;
+    const float* trow = dt.table + ((long)y2 * dt.V + y1) * dt.D;
+    const int d4 = dt.D / 4;
+    for (int c4 = lane; c4 < d4; c4 += 64) {
+      const float4 d = *reinterpret_cast<const float4*>(trow + 4 * c4);
+      for (int f = 0; f < nf2; ++f) {
+        const float4 e = *reinterpret_cast<const float4*>(
+            dt.enc + (long)(dt.enc_off[s] + t_new + f) * dt.D + 4 * c4);
+        store_j4(dt, ((long)s * F + f) * dt.D + 4 * c4, e, d);
+      }
+    }
+  }
+}
+
+void launch_greedy_spec(const SearchState& s, const float* logits, int V, int S, int F,
+                        int* t_cur, const int* enc_len, const HotwordTables& hw,
+                        const DecTable& dt, int* active, int parity, hipStream_t st) {
+  if (S <= 0) return;
+  ZASR_REQUIRE(V % 4 == 0 && V <= 4096, "vocabulary size must be a multiple of 4, <= 4096");
+  ZASR_REQUIRE(dt.D % 4 == 0 && dt.D <= 512, "joiner dim must be a multiple of 4, <= 512");
+#define ZASR_GS(FV, QV)                                                                      \
+  hipLaunchKernelGGL((greedy_spec_kernel<FV, QV>), dim3(S), dim3(256), 0, st, s, logits, V, \
+                     t_cur, enc_len, hw, dt, active, parity)
+  if (F == 4) {
+    if (V <= 512) ZASR_GS(4, 2); else if (V <= 2048) ZASR_GS(4, 8); else ZASR_GS(4, 16);
+  } else if (F == 8) {
+    if (V <= 512) ZASR_GS(8, 2); else if (V <= 2048) ZASR_GS(8, 8); else ZASR_GS(8, 16);
+  } else {
+    throw std::runtime_error("greedy_spec: window must be 4 or 8 frames");
+  }
+#undef ZASR_GS
 }
 
 // --------------------------------------------------------------------------------------

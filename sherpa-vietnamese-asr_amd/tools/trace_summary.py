@@ -9,9 +9,9 @@ from collections import OrderedDict
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name)
     name = name.replace("zasr::", "").replace("(anonymous namespace)::", "")
-    return name[:70]
+    name = re.sub(r"\(.*", "", name).replace("void ", "")
+    return name[:80]
 
 
 def main():

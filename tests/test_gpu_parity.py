@@ -193,6 +193,31 @@ def test_empty_and_short_chunks(tiny):
     assert res[2].T > 0
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_speculative_greedy_equals_frame_by_frame(need_gpu, precision, monkeypatch):
+    """Greedy with the decoder-context table runs speculative windows of F frames
+    (kernels.h greedy_spec); results must be bit-identical to the frame-by-frame search step
+    (ZASR_GREEDY_WINDOW=0) -- tokens, frames, log-probs and entropy statistics."""
+    from model_fixtures import m_model
+    from zasr.binding import Recognizer
+    cfg, w, path = m_model()
+    rec = Recognizer(path, "greedy_search", 1, precision=precision)
+    chunks = [_speech(s, 700 + i) for i, s in enumerate((0.3, 2.0, 7.5, 21.0, 33.0, 0.0))]
+    out = {}
+    for win in ("0", "4", "8"):
+        monkeypatch.setenv("ZASR_GREEDY_WINDOW", win)
+        out[win] = rec.decode(chunks)
+    for win in ("4", "8"):
+        for a, b in zip(out["0"], out[win]):
+            assert a.T == b.T
+            assert a.token_ids.tolist() == b.token_ids.tolist()
+            assert a.frames.tolist() == b.frames.tolist()
+            np.testing.assert_array_equal(a.log_probs, b.log_probs)
+            np.testing.assert_array_equal(a.stats, b.stats)
+    assert sum(r.token_ids.size for r in out["8"]) > 20
+    rec.close()
+
+
 # ------------------------------------------------------------------ bf16 precision mode
 def _token_agreement(a, b):
     import difflib
