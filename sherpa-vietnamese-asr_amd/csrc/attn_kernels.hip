@@ -35,10 +35,9 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // next block's global loads in registers.  The positional rows R[x] (x = j - i) the block
 // touches (L + 127 of them) are staged once at the start.
 //
-//   S^T = K Q^T     v_mfma_f32_32x32x16_bf16: lane = query, registers = 16 keys (q, k and
-//                   the pos queries p stay f32 in HBM; q and k are rounded to bf16 once)
+//   S^T = K Q^T     v_mfma_f32_32x32x16_bf16: lane = query, registers = 16 keys
 //         + p_i . R[j - i]
-//   P^T = exp2(S^T - c_i)     (log2 domain: q and p are pre-scaled by log2 e)
+//   P^T = exp2(S^T - c_i)     (log2 domain: q and p carry log2 e from attn_in's weights)
 //   O^T += V^T P^T            (the accumulator registers are the MFMA k-slots as they stand)
 //
 // MODE 0 (W0): head 0, pass 1 = row statistics, pass 2 = normalised weights in bf16.
@@ -47,23 +46,11 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // MODE 2 (SA stats): c_i from MODE 1, P normalised directly.
 // =====================================================================================
 namespace {
-constexpr float kLog2e = 1.4426950408889634f;
 constexpr int kKLd = 40;  // LDS row stride (bf16) of the K / V^T images: 80 B
 constexpr int kPosPad = 160;  // staged positional rows beyond L (the last key block's tail)
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// 8 consecutive f32 -> bf16 (RNE), optionally scaled first (one rounding)
-__device__ __forceinline__ bf16x8 load8_bf16(const float* p, float scale) {
-  const float4 x0 = reinterpret_cast<const float4*>(p)[0];
-  const float4 x1 = reinterpret_cast<const float4*>(p)[1];
-  bf16x8 v;
-  v[0] = (__bf16)(x0.x * scale); v[1] = (__bf16)(x0.y * scale);
-  v[2] = (__bf16)(x0.z * scale); v[3] = (__bf16)(x0.w * scale);
-  v[4] = (__bf16)(x1.x * scale); v[5] = (__bf16)(x1.y * scale);
-  v[6] = (__bf16)(x1.z * scale); v[7] = (__bf16)(x1.w * scale);
-  return v;
-}
 }  // namespace
 
 template <int MODE>
@@ -98,31 +85,33 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       sPos[t] = *reinterpret_cast<const float4*>(a.pos_tab + (long)row * 4 * H + 4 * h);
     }
   }
-  // ---- this lane's query, pre-scaled by log2 e and rounded once ----
-  const float* qrow = a.qkp + (long)(r0 + ic) * ldq + 32 * h;
-  const bf16x8 qf0 = load8_bf16(qrow + 8 * h2, kLog2e);
-  const bf16x8 qf1 = load8_bf16(qrow + 16 + 8 * h2, kLog2e);
-  float4 pq = *reinterpret_cast<const float4*>(a.qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
-  pq.x *= kLog2e; pq.y *= kLog2e; pq.z *= kLog2e; pq.w *= kLog2e;
+  // ---- this lane's query and positional query (log2 e already folded in) ----
+  const __bf16* qrow = a.qkp + (long)(r0 + ic) * ldq + 32 * h;
+  const bf16x8 qf0 = *reinterpret_cast<const bf16x8*>(qrow + 8 * h2);
+  const bf16x8 qf1 = *reinterpret_cast<const bf16x8*>(qrow + 16 + 8 * h2);
+  float4 pq;
+  {
+    const bf16x4 pv = *reinterpret_cast<const bf16x4*>(a.qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
+    pq = make_float4((float)pv[0], (float)pv[1], (float)pv[2], (float)pv[3]);
+  }
   // pos index of (this query, key j0 + jr): j0 + jr - 32 wid - c + 127
   const int pbase = 127 - 32 * wid - c;
 
   const int nkb = (L + 31) / 32;
   // staging roles: threads 0..127 load K (key tid>>2, 16-byte chunk tid&3); threads
   // 128..223 load V (key (tid-128)/3, 4 dims (tid-128)%3); MODE 0 needs no V
-  const float* kbase = a.qkp + (long)r0 * ldq + 32 * H + 32 * h;
+  const __bf16* kbase = a.qkp + (long)r0 * ldq + 32 * H + 32 * h;
   const __bf16* vbase = MODE == 0 ? nullptr : a.v + (long)r0 * ldv + 12 * h;
   const int vt = tid - 128;
   const int vkey = vt / 3, vq = vt - 3 * (vt / 3);
-  float4 kraw0, kraw1;
+  bf16x8 kreg;
   bf16x4 vreg;
   auto gload = [&](int kb) {
     const int j0 = kb * 32;
     if (tid < 128) {
       int j = j0 + (tid >> 2);
       j = j < L ? j : L - 1;
-      kraw0 = *reinterpret_cast<const float4*>(kbase + (long)j * ldq + 8 * (tid & 3));
-      kraw1 = *reinterpret_cast<const float4*>(kbase + (long)j * ldq + 8 * (tid & 3) + 4);
+      kreg = *reinterpret_cast<const bf16x8*>(kbase + (long)j * ldq + 8 * (tid & 3));
     } else if (MODE != 0 && vt < 96) {
       int j = j0 + vkey;
       j = j < L ? j : L - 1;
@@ -131,10 +120,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   };
   auto sstore = [&](int buf) {
     if (tid < 128) {
-      bf16x8 kv;
-      kv[0] = (__bf16)kraw0.x; kv[1] = (__bf16)kraw0.y; kv[2] = (__bf16)kraw0.z; kv[3] = (__bf16)kraw0.w;
-      kv[4] = (__bf16)kraw1.x; kv[5] = (__bf16)kraw1.y; kv[6] = (__bf16)kraw1.z; kv[7] = (__bf16)kraw1.w;
-      *reinterpret_cast<bf16x8*>(&sK[buf][(tid >> 2) * kKLd + 8 * (tid & 3)]) = kv;
+      *reinterpret_cast<bf16x8*>(&sK[buf][(tid >> 2) * kKLd + 8 * (tid & 3)]) = kreg;
     } else if (MODE != 0 && vt < 96) {
       // key jj sits in score register r = (jj&3) + 4 (jj>>3) of lane half (jj>>2)&1, which
       // the PV MFMA m = r >> 3 takes in k-slot 8 half + (r & 7)
@@ -294,6 +280,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
+  ZASR_REQUIRE(a.H % 2 == 0, "attention: the bf16 kernels need an even head count (16-byte q/k rows)");
   const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
   ZASR_REQUIRE(lds <= 140 * 1024, "attention: sequence too long for the bf16 kernel's LDS");
   const dim3 grid(cdiv(a.max_len, 128), a.nseq, mode == 0 ? 1 : a.H);

@@ -414,7 +414,26 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
       mk(*l);
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
-        for (DLin* l : {&L.attn_in, &L.na_in, &L.na_out}) mk(*l);
+        // attn_in: the query and positional-query rows carry log2(e) in the bf16 path (the
+        // flash attention works in the log2 domain), folded before the single rounding
+        {
+          DLin& l = L.attn_in;
+          const int h = s.h;
+          std::vector<float> rs(l.N, 1.f), bias(l.N);
+          const float kLog2e = 1.4426950408889634f;
+          for (int r = 0; r < l.N; ++r)
+            if (r < 32 * h || r >= 64 * h) rs[r] = kLog2e;
+          ZASR_HIP_CHECK(hipMemcpy(bias.data(), l.b, l.N * sizeof(float), hipMemcpyDeviceToHost));
+          for (int r = 0; r < l.N; ++r) bias[r] *= rs[r];
+          float* d_rs = dev(rs.data(), rs.size());
+          l.bh = dev(bias.data(), bias.size());
+          void* p = nullptr;
+          ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2));
+          model_.allocations.push_back(p);
+          convert_rows_to_bf16(l.w, d_rs, p, l.N, l.K, stream_);
+          l.wh = p;
+        }
+        for (DLin* l : {&L.na_in, &L.na_out}) mk(*l);
         for (int a = 0; a < 2; ++a)
           for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mk(*l);
         for (int a = 0; a < 3; ++a)
@@ -663,7 +682,7 @@ void Engine::linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M,
   p.sbn = l.K;
   p.C = reinterpret_cast<float*>(C);
   p.ldc = ldc;
-  p.bias = l.b;
+  p.bias = l.bh ? l.bh : l.b;
   p.M = M;
   p.N = l.N;
   p.K = l.K;
@@ -744,11 +763,11 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   if (bf16) {
     // flash-style attention on bf16 q / k / v (attn_kernels.hip): head 0's normalised weights
     // for the NonlinAttention GEMM; every head's statistics come from self_attn1
-    qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
-    linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
+    __bf16* qkp16 = ws<__bf16>("ly_qkp_h", (size_t)R * 68 * h);
+    linear_h(Ly.attn_in, X, false, d, R, qkp16, true, 68 * h, EPI_NONE);
     A16 = ws<__bf16>("ly_attn_h", 1);  // sized by the caller
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
-    fa = AttnFlashArgs{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A16,
+    fa = AttnFlashArgs{qkp16, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A16,
                        nullptr, nullptr, stats, stats};
     prof_begin("attn_softmax");
     launch_attn_flash(fa, 0, st_);
@@ -1178,7 +1197,7 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
   // greedy with the decoder-context table: speculative windows (kernels.h, greedy_spec)
   const char* spec_env = getenv("ZASR_GREEDY_WINDOW");
-  const int F = spec_env ? atoi(spec_env) : 8;
+  const int F = spec_env ? atoi(spec_env) : 4;
   if (H == 1 && model_.dec_table && (F == 4 || F == 8)) {
     void* Js = bf16 ? (void*)ws<__bf16>("gs_joinin_h", (size_t)S * F * D)
                     : (void*)ws<float>("gs_joinin", (size_t)S * F * D);

@@ -30,6 +30,7 @@ struct DLin {
   float* b = nullptr;  // [N] or null
   int N = 0, K = 0;
   void* wh = nullptr;  // bf16 copy of w (precision mode bf16)
+  float* bh = nullptr; // bias of the bf16 path when it differs from b (folded row scales)
 };
 
 struct DLayer {

@@ -79,5 +79,8 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
 
 // device f32 -> bf16 (round to nearest even) copy
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
+// dst[r][k] = bf16(src[r][k] * row_scale[r]) (one rounding), src / dst [N][K]
+void convert_rows_to_bf16(const float* src, const float* row_scale, void* dst, long N, int K,
+                          hipStream_t stream);
 
 }  // namespace zasr

@@ -585,6 +585,18 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ src, __bf16* __rest
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = (__bf16)src[i];
 }
+__global__ void rows_to_bf16_kernel(const float* __restrict__ src, const float* __restrict__ rs,
+                                    __bf16* __restrict__ dst, long n, int K) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (__bf16)(src[i] * rs[i / K]);
+}
+void convert_rows_to_bf16(const float* src, const float* row_scale, void* dst, long N, int K,
+                          hipStream_t st) {
+  const long n = N * K;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(rows_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src, row_scale,
+                     reinterpret_cast<__bf16*>(dst), n, K);
+}
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,

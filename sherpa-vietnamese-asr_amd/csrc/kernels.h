@@ -85,14 +85,16 @@ struct AttnArgs {
   int write_heads;
 };
 void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
-// bf16 mode, flash-style attention (attn_kernels.hip): qkp f32, v / out in bf16.
+// bf16 mode, flash-style attention (attn_kernels.hip): qkp / v / out in bf16; the query
+// and positional-query columns of qkp carry a log2(e) factor (folded into attn_in's bf16
+// weights and bias at load).
 //   mode 0: head-0 normalised weights in bf16, [L][L8] per sequence at a_off[b] (columns
 //           [L, L8) zero; L8 = L rounded up to 8), the NonlinAttention GEMM operand
 //   mode 1: self-attention with running statistics; writes out and stats_out
 //   mode 2: self-attention with the statistics of mode 1 (stats_in)
 // stats: [R][H] c = row max + log2(row sum), log2 domain
 struct AttnFlashArgs {
-  const float* qkp;        // [R][68 H]
+  const __bf16* qkp;       // [R][68 H]
   int H;
   const float* pos_tab;    // [(2 pmax - 1)][4 H]
   int pmax;

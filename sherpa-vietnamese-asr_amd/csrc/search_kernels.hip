@@ -833,20 +833,24 @@ void launch_greedy_spec_init(const DecTable& dt, int S, int F, int* t_cur, int* 
 }
 
 // One block per stream, wave w owns window rows w, w + 4, ... (register resident).
-//   A. per row: max, second max, S = sum e, E1, E3 (the statistics of search_step_kernel),
-//      log S, and d0 = fl(x_blank - max)
+//   A. per row: max, second max, log S (S = sum e), and d0 = fl(x_blank - max); the
+//      encoder rows of every frame the next window can start at (t0 + 1 .. t0 + 2F - 1) and
+//      the current context's table row are staged in LDS meanwhile
 //   B. lf_f = the score before frame f if frames 0 .. f-1 were all blank: the reference's
-//      f32 recurrence lp <- fl(fl(d0 - log S) + fl(lp)) (a one-thread scan)
-//   C. per row, the exact top-1 of key(fl(fl(x - max) - log S) + lf_f, index) -- the
-//      candidate order of search_step_kernel at beam 1 -- so the first row whose top-1 is
-//      not blank is exactly the frame-by-frame emission
-//   D. wave 0: state, emission node, hotword transition (:1127-1131), next window's J
+//      f32 recurrence lp <- fl(fl(d0 - log S) + fl(lp)) (one thread)
+//   C. per row, the top-1 of search_step_kernel's candidate order: the value
+//      fl(fl(fl(x - max) - log S) + lf_f) is monotone in x, so the top value is that of x =
+//      max and the winner is the smallest index reaching it (a float compare per element)
+//   D. the first non-blank row is the emission: its owning wave adds the entropy terms of
+//      that row and writes node + state (hotword transition :1127-1131); all waves write the
+//      next window's J rows from the staged encoder rows and the (new) context's table row
 template <int F, int Q>
 __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const float* logits,
                                                           int V, int* t_cur, const int* enc_len,
                                                           HotwordTables hw, DecTable dt,
                                                           int* active, int parity) {
   constexpr int RPW = F / 4;  // rows per wave
+  constexpr int DMAX = 512;
   const int s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (s == 0 && tid == 0) active[parity ^ 1] = 0;  // the next super-step's counter
@@ -855,12 +859,16 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
   if (t0 >= T_s) return;
   const int nf = T_s - t0 < F ? T_s - t0 : F;
   const int V4 = V >> 2;
-  __shared__ float sLs[F], sD0[F], sLf[F], sM1[F];
+  const int D = dt.D, d4 = D >> 2;
+  __shared__ float sLs[F], sD0[F], sLf[F];
   __shared__ double sLp[F + 1];
-  __shared__ float4 sStats[F];
-  __shared__ unsigned long long sKey[F];
+  __shared__ int sTok[F];
+  __shared__ float4 sEnc[(2 * F - 1) * (DMAX / 4)];
+  __shared__ float4 sTab[DMAX / 4];
+  const int base = s;  // Hmax = 1 at beam 1
+  const int y1 = st.y1[base], y2 = st.y2[base];
 
-  // ---- A. rows in registers + statistics ----
+  // ---- A. rows in registers; encoder rows t0 + 1 .. and the context row into LDS ----
   const float4* rows4 = reinterpret_cast<const float4*>(logits + (long)s * F * V);
   float4 x[RPW][Q];
 #pragma unroll
@@ -873,9 +881,29 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
                                    : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     }
   }
-  // the current hypothesis (one slot) and, for wave 0, nothing else yet
-  const int base = s * 1;  // Hmax = 1 at beam 1 (launch_greedy_spec checks)
-  float m1r[RPW], lsr[RPW];
+  {
+    const float4* enc4 = reinterpret_cast<const float4*>(dt.enc + (long)dt.enc_off[s] * D);
+    const float4* tab4 = reinterpret_cast<const float4*>(dt.table + ((long)y2 * dt.V + y1) * D);
+    constexpr int NE = (2 * F - 1) * (DMAX / 4);
+    constexpr int IT = (NE + 255) / 256;
+    float4 ev[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int e = tid + 256 * k;
+      const int fr = e / d4, c4 = e - fr * d4;
+      int t = t0 + 1 + fr;
+      t = t < T_s ? t : T_s - 1;
+      ev[k] = (fr < 2 * F - 1) ? enc4[(long)t * d4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float4 tv = tid < d4 ? tab4[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int e = tid + 256 * k;
+      if (e < (2 * F - 1) * d4) sEnc[e] = ev[k];
+    }
+    if (tid < d4) sTab[tid] = tv;
+  }
+  float m1r[RPW], m2r[RPW], lsr[RPW], ser[RPW];
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int f = wid + 4 * r;
@@ -896,33 +924,23 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
       m1 = hi;
       m2 = lo;
     }
-    float se = 0.f, e1 = 0.f, e3 = 0.f;
-    auto acc = [&](float v) {
-      const float d = v - m1;
-      const float e = __expf(d);
-      se += e;
-      e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
-      e3 += __expf(d * (1.0f / 3.0f));
-    };
+    float se = 0.f;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      acc(x[r][q].x);
-      acc(x[r][q].y);
-      acc(x[r][q].z);
-      acc(x[r][q].w);
+      se += __expf(x[r][q].x - m1);
+      se += __expf(x[r][q].y - m1);
+      se += __expf(x[r][q].z - m1);
+      se += __expf(x[r][q].w - m1);
     }
     se = wave_sum(se);
-    e1 = wave_sum(e1);
-    e3 = wave_sum(e3);
     const float ls = logf(se);
     m1r[r] = m1;
+    m2r[r] = m2;
     lsr[r] = ls;
+    ser[r] = se;
     if (lane == 0 && f < nf) {
       sLs[f] = ls;
-      sM1[f] = m1;
       sD0[f] = x[r][0].x - m1;  // blank = token 0 = lane 0's first element
-      sStats[f] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
-                              __expf(m2 - m1) / se);
     }
   }
   __syncthreads();
@@ -933,111 +951,138 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
     for (int f = 0; f < nf; ++f) {
       const float lf = (float)lp;
       sLf[f] = lf;
-      const float lpv = sD0[f] - sLs[f];
-      lp = (double)(lpv + lf);
+      lp = (double)((sD0[f] - sLs[f]) + lf);
       sLp[f + 1] = lp;
     }
   }
   __syncthreads();
-  // ---- C. exact top-1 per row ----
+  // ---- C. top-1 token per row ----
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int f = wid + 4 * r;
     if (f >= nf) continue;  // wave-uniform
     const float lf = sLf[f], m1 = m1r[r], ls = lsr[r];
-    unsigned long long best = 0ull;
+    const float vmax = (0.f - ls) + lf;
+    int bq = 0x7fffffff;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int i = lane + 64 * q;
-      if (i < V4) {
-        const float4 v = x[r][q];
-        const unsigned long long k0 = make_key(((v.x - m1) - ls) + lf, 4 * i);
-        const unsigned long long k1 = make_key(((v.y - m1) - ls) + lf, 4 * i + 1);
-        const unsigned long long k2 = make_key(((v.z - m1) - ls) + lf, 4 * i + 2);
-        const unsigned long long k3 = make_key(((v.w - m1) - ls) + lf, 4 * i + 3);
-        best = k0 > best ? k0 : best;
-        best = k1 > best ? k1 : best;
-        best = k2 > best ? k2 : best;
-        best = k3 > best ? k3 : best;
-      }
+    for (int q = Q - 1; q >= 0; --q) {
+      const int i = 4 * (lane + 64 * q);
+      const float4 v = x[r][q];
+      const int c = (((v.x - m1) - ls) + lf == vmax) ? i
+                  : (((v.y - m1) - ls) + lf == vmax) ? i + 1
+                  : (((v.z - m1) - ls) + lf == vmax) ? i + 2
+                  : (((v.w - m1) - ls) + lf == vmax) ? i + 3 : 0x7fffffff;
+      bq = c < bq ? c : bq;
     }
+    int best = bq;  // the smallest index of this lane reaching the top value
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long ob = __shfl_xor(best, o, 64);
-      best = ob > best ? ob : best;
+      const int ob = __shfl_xor(best, o, 64);
+      best = ob < best ? ob : best;
     }
-    if (lane == 0) sKey[f] = best;
+    if (lane == 0) sTok[f] = best;
   }
   __syncthreads();
-  if (wid != 0) return;
-  // ---- D. the first emission of the window (wave 0) ----
+  // ---- D. the first emission of the window ----
   int fe = -1;
   for (int f = 0; f < nf; ++f)
-    if (key_idx(sKey[f]) != 0) {
+    if (sTok[f] != 0) {
       fe = f;
       break;
     }
   const int t_new = t0 + (fe >= 0 ? fe + 1 : nf);
-  int y1 = st.y1[base], y2 = st.y2[base];
+  int ny1 = y1, ny2 = y2;
   if (fe >= 0) {
-    const unsigned long long key = sKey[fe];
-    const float val = key_val(key);
-    const int tok = key_idx(key);
-    double score = (double)val;
-    int nhw = st.hw[base];
-    if (hw.num_states > 0 && tok != 2) {
-      const int cls = hw.tok2cls[tok];
-      if (cls < 0) {
-        score += -hw.node_score[nhw];
-        nhw = 0;
-      } else {
-        const long e = (long)nhw * hw.num_cls + cls;
-        score += hw.delta[e];
-        nhw = hw.next[e];
+    const int tok = sTok[fe];
+    ny2 = y1;
+    ny1 = tok;
+    if ((fe & 3) == wid) {
+      // owner wave: the entropy terms of row fe (search_step_kernel's statistics)
+      const int r = fe >> 2;
+      float m1 = 0.f, m2 = 0.f, se = 1.f, ls = 0.f;
+      float e1 = 0.f, e3 = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        if (rr != r) continue;
+        m1 = m1r[rr];
+        m2 = m2r[rr];
+        se = ser[rr];
+        ls = lsr[rr];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const float4 v = x[rr][q];
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float d = vv[c] - m1;
+            const float e = __expf(d);
+            e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+            e3 += __expf(d * (1.0f / 3.0f));
+          }
+        }
+      }
+      e1 = wave_sum(e1);
+      e3 = wave_sum(e3);
+      if (lane == 0) {
+        const float val = (0.f - ls) + sLf[fe];
+        double score = (double)val;
+        int nhw = st.hw[base];
+        if (hw.num_states > 0 && tok != 2) {
+          const int cls = hw.tok2cls[tok];
+          if (cls < 0) {
+            score += -hw.node_score[nhw];
+            nhw = 0;
+          } else {
+            const long e = (long)nhw * hw.num_cls + cls;
+            score += hw.delta[e];
+            nhw = hw.next[e];
+          }
+        }
+        const int nid = st.node_count[s];
+        const long gi = (long)s * st.node_cap + nid;
+        st.node_tok[gi] = tok;
+        st.node_frame[gi] = t0 + fe;
+        st.node_parent[gi] = st.node[base];
+        st.node_lp[gi] = (double)val - sLp[fe];
+        st.node_stats[gi] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)),
+                                        1.0f / se, __expf(m2 - m1) / se);
+        st.node_count[s] = nid + 1;
+        st.lp[base] = score;
+        st.lpf[base] = 0;
+        st.hash[base] = hash_push(st.hash[base], tok);
+        st.len[base] = st.len[base] + 1;
+        st.y2[base] = y1;
+        st.y1[base] = tok;
+        st.hw[base] = nhw;
+        st.node[base] = nid;
       }
     }
-    if (lane == 0) {
-      const int nid = st.node_count[s];
-      const long gi = (long)s * st.node_cap + nid;
-      const int parent = st.node[base];
-      st.node_tok[gi] = tok;
-      st.node_frame[gi] = t0 + fe;
-      st.node_parent[gi] = parent;
-      st.node_lp[gi] = (double)val - sLp[fe];
-      st.node_stats[gi] = sStats[fe];
-      st.node_count[s] = nid + 1;
-      st.lp[base] = score;
-      st.lpf[base] = 0;
-      st.hash[base] = hash_push(st.hash[base], tok);
-      st.len[base] = st.len[base] + 1;
-      st.y2[base] = y1;
-      st.y1[base] = tok;
-      st.hw[base] = nhw;
-      st.node[base] = nid;
-    }
-    y2 = y1;
-    y1 = tok;
-  } else if (lane == 0) {
+  } else if (tid == 0) {
     st.lp[base] = sLp[nf];
     st.lpf[base] = 0;
   }
-  if (lane == 0) {
+  if (tid == 0) {
     t_cur[s] = t_new;
     if (t_new < T_s) atomicAdd(&active[parity], 1);
   }
-  // ---- the next window's joiner input: J[s][f] = tanh(enc[t_new + f] + table[y2, y1]) ----
-  if (t_new < T_s) {
-    const int nf2 = T_s - t_new < F ? T_s - t_new : F;
-    const float* trow = dt.table + ((long)y2 * dt.V + y1) * dt.D;
-    const int d4 = dt.D / 4;
-    for (int c4 = lane; c4 < d4; c4 += 64) {
-      const float4 d = *reinterpret_cast<const float4*>(trow + 4 * c4);
-      for (int f = 0; f < nf2; ++f) {
-        const float4 e = *reinterpret_cast<const float4*>(
-            dt.enc + (long)(dt.enc_off[s] + t_new + f) * dt.D + 4 * c4);
-        store_j4(dt, ((long)s * F + f) * dt.D + 4 * c4, e, d);
-      }
-    }
+  // ---- the next window's joiner input: J[s][f] = tanh(enc[t_new + f] + table[ny2, ny1]) ----
+  if (t_new >= T_s) return;
+  const int nf2 = T_s - t_new < F ? T_s - t_new : F;
+  float4 tv;
+  if (fe >= 0) {
+    if (tid < d4) tv = reinterpret_cast<const float4*>(dt.table + ((long)ny2 * dt.V + ny1) * D)[tid];
+  } else {
+    if (tid < d4) tv = sTab[tid];
+  }
+  if (fe >= 0) {
+    __syncthreads();  // every wave is done reading sTab: reuse it for the new context row
+    if (tid < d4) sTab[tid] = tv;
+  }
+  __syncthreads();
+  const int fo = t_new - t0 - 1;  // staged row of frame t_new
+  for (int e = tid; e < nf2 * d4; e += 256) {
+    const int f = e / d4, c4 = e - f * d4;
+    store_j4(dt, ((long)s * F + f) * D + 4 * c4, sEnc[(fo + f) * d4 + c4], sTab[c4]);
   }
 }
 

@@ -39,9 +39,27 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void k(GemmParams p, const _
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WAVES_N, wn = wid - wm * WAVES_N;
   bf16x8 ra[A_LD], rb[B_LD];
+  constexpr bool FULLA = (DBG & 8) != 0 && sizeof(TA) == 4;
+  constexpr int PPR = BK / 4;                 // 16-byte f32 pieces per row slab
+  constexpr int A_P = BM * PPR;
+  constexpr int A_LP = (A_P + NT - 1) / NT;
+  float4 rf[FULLA ? A_LP : 1];
   auto gload = [&](int kt) {
+    if constexpr (FULLA) {
 #pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
+      for (int i = 0; i < A_LP; ++i) {
+        const int idx = tid + NT * i;
+        const int row = idx / PPR, k4 = idx % PPR;
+        int gm = m0 + row, gk = kt * BK + 4 * k4;
+        const bool ok = gm < M && gk < K;
+        gm = gm < M ? gm : M - 1;
+        gk = gk < K ? gk : K - 4;
+        const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(A) + (long)gm * lda + gk);
+        rf[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (FULLA ? 0 : A_LD); ++i) {
       const int idx = tid + NT * i;
       const int row = idx / GPR, k8 = idx % GPR;
       if constexpr ((DBG & 4) != 0) {
@@ -63,8 +81,19 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void k(GemmParams p, const _
   auto sstore = [&](int buf) {
     __bf16* As = sbase + buf * STAGE;
     __bf16* Bs = As + BM * LDH;
+    if constexpr (FULLA) {
 #pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
+      for (int i = 0; i < A_LP; ++i) {
+        const int idx = tid + NT * i;
+        if (idx < A_P) {
+          bf16x4 h;
+          h[0] = (__bf16)rf[i].x; h[1] = (__bf16)rf[i].y; h[2] = (__bf16)rf[i].z; h[3] = (__bf16)rf[i].w;
+          *reinterpret_cast<bf16x4*>(&As[(idx / PPR) * LDH + 4 * (idx % PPR)]) = h;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (FULLA ? 0 : A_LD); ++i) {
       const int idx = tid + NT * i;
       if (idx < A_G) *reinterpret_cast<bf16x8*>(&As[(idx / GPR) * LDH + 8 * (idx % GPR)]) = ra[i];
     }
@@ -114,6 +143,35 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void k(GemmParams p, const _
   }
   float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
   const int c4 = lane & 7;
+  if constexpr ((DBG & 16) != 0 && !std::is_same<TC, float>::value) {
+    // 16-byte bf16 stores: lane -> row (lane >> 2) + 16 q, columns 8 (lane & 3) .. + 7
+    const int c8 = lane & 3;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sE[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE + (lane & 31)] = acc[i][j][r];
+        __builtin_amdgcn_wave_barrier();
+        const int col = n0 + wn * WTN + j * 32 + 8 * c8;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int rl = (lane >> 2) + 16 * q;
+          const int row = m0 + wm * WTM + i * 32 + rl;
+          const float4 v0 = *reinterpret_cast<const float4*>(&sE[rl * LDE + 8 * c8]);
+          const float4 v1 = *reinterpret_cast<const float4*>(&sE[rl * LDE + 8 * c8 + 4]);
+          if (row < M && col < N) {
+            bf16x8 h;
+            h[0] = (__bf16)v0.x; h[1] = (__bf16)v0.y; h[2] = (__bf16)v0.z; h[3] = (__bf16)v0.w;
+            h[4] = (__bf16)v1.x; h[5] = (__bf16)v1.y; h[6] = (__bf16)v1.z; h[7] = (__bf16)v1.w;
+            *reinterpret_cast<bf16x8*>(C + (long)row * p.ldc + col) = h;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -421,6 +479,137 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void kf(GemmParams p, const 
       __builtin_amdgcn_wave_barrier();
     }
 }
+
+// two K-steps of global loads in flight: register sets alternate, the loads of step kt + 2
+// are issued while step kt computes and step kt + 1 (loaded an iteration earlier) is stored
+template <int BM, int BN, int BK, int WAVES_M, int WAVES_N, typename TA, typename TC>
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void k2(GemmParams p, const __bf16* Bw,
+                                                            int tiles_n) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N, FM = WTM / 32, FN = WTN / 32;
+  constexpr int LDH = BK + 8, GPR = BK / 8, A_G = BM * GPR, B_G = BN * GPR;
+  constexpr int A_LD = (A_G + NT - 1) / NT, B_LD = (B_G + NT - 1) / NT;
+  constexpr int STAGE = (BM + BN) * LDH;
+  constexpr int LDE = 40;
+  constexpr int OPER_BYTES = 2 * STAGE * 2, EPI_BYTES = (NT / 64) * 32 * LDE * 4;
+  constexpr int LDS_BYTES = OPER_BYTES > EPI_BYTES ? OPER_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  __bf16* const sbase = reinterpret_cast<__bf16*>(smem);
+  const TA* A = reinterpret_cast<const TA*>(p.A);
+  TC* C = reinterpret_cast<TC*>(p.C);
+  const int M = p.M, K = p.K, lda = p.lda, N = p.N;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int m_tile = tile / tiles_n;
+  const int m0 = m_tile * BM;
+  if (m0 >= M) return;
+  const int n0 = (tile - m_tile * tiles_n) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WAVES_N, wn = wid - wm * WAVES_N;
+  bf16x8 ra[2][A_LD], rb[2][B_LD];
+  auto gload = [&](int kt, int set) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx / GPR, k8 = idx % GPR;
+      ra[set][i] = load_a8<ALOAD_DENSE, TA>(p, A, M, K, lda, m0 + (idx < A_G ? row : 0), kt * BK + 8 * k8);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int idx = tid + NT * i;
+      const int n = idx / GPR, k8 = idx % GPR;
+      const int gn = n0 + n, gk = kt * BK + 8 * k8;
+      const int nc = gn < N ? gn : N - 1, kc = gk < K ? gk : K - 8;
+      rb[set][i] = *reinterpret_cast<const bf16x8*>(Bw + (long)nc * p.sbn + kc);
+    }
+  };
+  auto sstore = [&](int buf, int set) {
+    __bf16* As = sbase + buf * STAGE;
+    __bf16* Bs = As + BM * LDH;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int idx = tid + NT * i;
+      if (idx < A_G) *reinterpret_cast<bf16x8*>(&As[(idx / GPR) * LDH + 8 * (idx % GPR)]) = ra[set][i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int idx = tid + NT * i;
+      if (idx < B_G) *reinterpret_cast<bf16x8*>(&Bs[(idx / GPR) * LDH + 8 * (idx % GPR)]) = rb[set][i];
+    }
+  };
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto compute = [&](int buf) {
+    const __bf16* As = sbase + buf * STAGE;
+    const __bf16* Bs = As + BM * LDH;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * WTM + i * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wn * WTN + j * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  const int nkt = (K + BK - 1) / BK;
+  gload(0, 0);
+  if (nkt > 1) gload(1, 1);
+  sstore(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; kt += 2) {
+    // even step: compute buf 0; set 0 is free -> loads of kt + 2; store set 1 (kt + 1)
+    if (kt + 2 < nkt) gload(kt + 2, 0);
+    compute(0);
+    if (kt + 1 < nkt) sstore(1, 1);
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    // odd step
+    if (kt + 3 < nkt) gload(kt + 3, 1);
+    compute(1);
+    if (kt + 2 < nkt) sstore(0, 0);
+    __syncthreads();
+  }
+  float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
+  const int c4 = lane & 7;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sE[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE + (lane & 31)] = acc[i][j][r];
+      __builtin_amdgcn_wave_barrier();
+      const int col = n0 + wn * WTN + j * 32 + 4 * c4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = (lane >> 3) + 8 * q;
+        const int row = m0 + wm * WTM + i * 32 + rl;
+        float4 v = *reinterpret_cast<const float4*>(&sE[rl * LDE + 4 * c4]);
+        if (row < M && col < N) {
+          TC* dst = C + (long)row * p.ldc + col;
+          if constexpr (std::is_same<TC, float>::value) {
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            bf16x4 h;
+            h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+            *reinterpret_cast<bf16x4*>(dst) = h;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+}
 }  // namespace lab
 
 struct Shape {
@@ -465,6 +654,14 @@ static double run_persist(const GemmParams& p, const __bf16* B, int G) {
   });
 }
 
+template <int BM, int BN, int BK, int WM, int WN, typename TA, typename TC>
+static double run_k2(const GemmParams& p, const __bf16* B) {
+  const int tn = cdiv(p.N, BN), tm = cdiv(p.M, BM);
+  return time_it([&] {
+    hipLaunchKernelGGL((lab::k2<BM, BN, BK, WM, WN, TA, TC>), dim3(tn * tm), dim3(64 * WM * WN), 0, 0, p, B, tn);
+  });
+}
+
 template <int BM, int BN, int WM, int WN, typename TA, typename TC>
 static double run_full(const GemmParams& p, const __bf16* B) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.M, BM);
@@ -493,16 +690,13 @@ static void run_shape(const Shape& s, void* dA, __bf16* dB, void* dC) {
   double full = run_lab<TA, TC, 0>(p, dB);
   double nost = run_lab<TA, TC, 1>(p, dB);
   double nomf = run_lab<TA, TC, 2>(p, dB);
-  double noa = run_lab<TA, TC, 4>(p, dB);
+  double noa = run_lab<TA, TC, 16>(p, dB);  // 16-byte bf16 epilogue stores
   double only_ld = run_lab<TA, TC, 3>(p, dB);
-  double p512 = 0, p768 = 0, p1024 = 0;
-  if (s.K <= 256) {
-    p512 = run_full<64, 64, 2, 2, TA, TC>(p, dB);
-    p768 = run_full<64, 128, 2, 2, TA, TC>(p, dB);
-    p1024 = run_full<128, 64, 2, 2, TA, TC>(p, dB);
-  }
+  double p512 = run_k2<128, 128, 32, 2, 2, TA, TC>(p, dB);
+  double p768 = run_k2<128, 128, 64, 2, 2, TA, TC>(p, dB);
+  double p1024 = run_k2<256, 128, 32, 4, 2, TA, TC>(p, dB);
   printf("%-8s M=%7d K=%5d N=%5d %s%s  prod %7.1f us (%5.0f GB/s %5.0f TF/s) | lab128 %7.1f  "
-         "no-store %7.1f  no-mfma %7.1f  no-A %7.1f  loads-only %7.1f | full64x64 %7.1f 64x128 %7.1f 128x64 %7.1f (%5.0f GB/s)\n",
+         "no-store %7.1f  no-mfma %7.1f  st16 %7.1f  loads-only %7.1f | pf2 128x128x32 %7.1f 128x128x64 %7.1f 256x128x32 %7.1f (best %5.0f GB/s)\n",
          s.name, s.M, s.K, s.N, s.a16 ? "A16" : "A32", s.c16 ? "C16" : "C32", prod,
          bytes / prod * 1e-3, flops / prod * 1e-6, full, nost, nomf, noa, only_ld, p512, p768, p1024,
          bytes / std::max(1e-9, std::min(p512, std::min(p768, p1024))) * 1e-3);

@@ -202,7 +202,8 @@ def test_speculative_greedy_equals_frame_by_frame(need_gpu, precision, monkeypat
     from zasr.binding import Recognizer
     cfg, w, path = m_model()
     rec = Recognizer(path, "greedy_search", 1, precision=precision)
-    chunks = [_speech(s, 700 + i) for i, s in enumerate((0.3, 2.0, 7.5, 21.0, 33.0, 0.0))]
+    chunks = [_speech(s, 700 + i) for i, s in enumerate((0.3, 2.0, 7.5, 21.0, 33.0))]
+    chunks.append(np.zeros(0, np.float32))
     out = {}
     for win in ("0", "4", "8"):
         monkeypatch.setenv("ZASR_GREEDY_WINDOW", win)
