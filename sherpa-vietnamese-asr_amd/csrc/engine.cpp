@@ -784,8 +784,16 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     launch_attn_softmax(a, st_);
     prof_end();
   }
+  static const bool ffn_unfused = getenv("ZASR_FFN_UNFUSED") != nullptr;
   auto ff = [&](int k) {
     const DLin& fi = Ly.ff_in[k];
+    if (fi.wh && !ffn_unfused && ffn_fused_supported(d)) {
+      // bf16 mode: in_proj -> SwooshL -> out_proj + residual in one kernel, hidden on chip
+      prof_begin("ffn_fused");
+      launch_ffn_fused(X, R, d, fi.N, fi.wh, fi.b, Ly.ff_out[k].wh, Ly.ff_out[k].b, st_);
+      prof_end();
+      return;
+    }
     if (fi.wh) {  // bf16 mode: the hidden activation crosses HBM in bf16
       __bf16* H = ws<__bf16>("ly_hid_h", (size_t)R * fi.N);
       linear_h(fi, X, false, d, R, H, true, fi.N, EPI_SWOOSHL);
