@@ -54,47 +54,60 @@ def make_chunks(audio_sec: float, seed: int):
     return chunks
 
 
-def enc_gemm_work(cfg, L_list, bf16: bool):
-    """Algorithmic work of the launches in the `enc_gemm` class (every Engine::linear of the
-    encoder: ConvNeXt pw1/pw2 + embed out, the stack projections, encoder_proj), per step.
+FFN_FUSED_DIMS = (64, 96, 128, 192)  # ffn_kernels.hip ffn_fused_supported
 
-    Returns (flops, bytes).  Bytes per launch = A read (f32 activations) + weights (bf16 in
-    the bf16 mode, f32 otherwise) + C write (f32) + C read for the residual epilogue."""
+
+def gemm_class_work(cfg, L_list, bf16: bool):
+    """Algorithmic work per step of the GEMM-class launches, mirroring Engine::run_encoder /
+    layer_forward: {"enc_gemm": (flops, bytes), "ffn_fused": (flops, bytes)}.
+
+    enc_gemm = every Engine::linear / linear_h (stack projections, embed out, encoder_proj;
+    in the fp32 mode also the ConvNeXt pointwise convs).  Bytes per launch = A read + weights
+    + C write (+ C read for the residual epilogue), each at the dtype the launch really uses
+    (bf16 mode: GEMM -> GEMM intermediates, q/k/v and the hidden activations in bf16; the
+    residual stream f32).  ffn_fused (bf16 mode, model dim in FFN_FUSED_DIMS) = X read + X
+    written (f32) + both weight matrices (bf16), 4 R d F flops."""
     wb = 2 if bf16 else 4
-    flops = 0.0
-    nbytes = 0.0
+    acc = {"enc_gemm": [0.0, 0.0], "ffn_fused": [0.0, 0.0]}
 
-    def lin(M, K, N, resadd=False):
-        nonlocal flops, nbytes
+    def lin(M, K, N, a=4, c=4, resadd=False):
         if M <= 0:
             return
-        flops += 2.0 * M * K * N
-        nbytes += 4.0 * M * K + wb * N * K + 4.0 * M * N * (2 if resadd else 1)
+        acc["enc_gemm"][0] += 2.0 * M * K * N
+        acc["enc_gemm"][1] += a * M * K + wb * N * K + c * M * N * (2 if resadd else 1)
 
+    h16 = 2 if bf16 else 4  # intermediates stored in bf16 in the bf16 mode
     d0 = cfg.encoder_dims[0]
     Ls = [L for L in L_list if L > 0]
     Lsum = sum(Ls)
-    lin(19 * Lsum, 128, 384)
-    lin(19 * Lsum, 384, 128, True)
-    lin(Lsum, 128 * 19, d0)
+    if bf16:
+        lin(Lsum, 128 * 19, d0, a=2)  # embed out over the bf16 ConvNeXt output
+    else:
+        lin(19 * Lsum, 128, 384)
+        lin(19 * Lsum, 384, 128, resadd=True)
+        lin(Lsum, 128 * 19, d0)
     for i, d in enumerate(cfg.encoder_dims):
         R = sum(-(-L // cfg.downsampling[i]) for L in Ls)
         F, h = cfg.ff_dims[i], cfg.num_heads[i]
         hid = 3 * d // 4
         for _ in range(cfg.num_layers[i]):
-            lin(R, d, (2 * cfg.query_head_dim + cfg.pos_head_dim) * h)
+            lin(R, d, (2 * cfg.query_head_dim + cfg.pos_head_dim) * h, c=h16)
             for f in ((F * 3) // 4, F, (F * 5) // 4):
-                lin(R, d, f)
-                lin(R, f, d, True)
+                if bf16 and d in FFN_FUSED_DIMS:
+                    acc["ffn_fused"][0] += 4.0 * R * d * f
+                    acc["ffn_fused"][1] += 8.0 * R * d + 2 * 2.0 * f * d
+                else:
+                    lin(R, d, f, c=h16)
+                    lin(R, f, d, a=h16, resadd=True)
             lin(R, d, 3 * hid)
-            lin(R, hid, d, True)
+            lin(R, hid, d, a=h16, resadd=True)
             for _ in range(2):
-                lin(R, d, cfg.value_head_dim * h)
-                lin(R, cfg.value_head_dim * h, d, True)
-                lin(R, d, 2 * d)
-                lin(R, d, d, True)
+                lin(R, d, cfg.value_head_dim * h, c=h16)
+                lin(R, cfg.value_head_dim * h, d, a=h16, resadd=True)
+                lin(R, d, 2 * d, c=h16)
+                lin(R, d, d, a=h16, resadd=True)
     lin(sum((L + 1) // 2 for L in Ls), cfg.max_dim, cfg.joiner_dim)
-    return flops, nbytes
+    return {k: (v[0], v[1]) for k, v in acc.items()}
 
 
 def pmc_traffic(kernel_class, args):
@@ -227,7 +240,7 @@ def main():
 
     L_list = [((n + 80) // 160 - 7) // 2 for n in lens]
     bf16 = args.precision == "bf16"
-    f_gemm, b_gemm = enc_gemm_work(cfg, L_list, bf16)
+    work = gemm_class_work(cfg, L_list, bf16)
     rows_joiner = sum(min(beam, 8) * ((L + 1) // 2) for L in L_list)
     f_join = 2.0 * rows_joiner * cfg.joiner_dim * cfg.vocab_size
     classes = {k: v for k, v in prof.items()}
@@ -237,9 +250,10 @@ def main():
     if dom:
         cnt, ms = classes[dom]
         per_launch_s = ms / cnt * 1e-3
-        if dom == "enc_gemm":
+        if dom in work:
             # the binding roof is the larger of bytes / HBM peak and flops / MFMA peak
-            fl, by = f_gemm * nprof / cnt, b_gemm * nprof / cnt  # per launch (class mean)
+            f_cls, b_cls = work[dom]
+            fl, by = f_cls * nprof / cnt, b_cls * nprof / cnt  # per launch (class mean)
             if by / (HBM_PEAK_GBS * 1e9) >= fl / (peak_mfma * 1e12):
                 ach = by / per_launch_s / 1e9
                 roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1),

@@ -159,6 +159,8 @@ class Engine {
   [[maybe_unused]] bool greedy_ = false;
   int precision_ = 0;
   hipStream_t stream_ = nullptr;
+  hipStream_t stream2_ = nullptr;  // searches of a pipelined decode (decode_device)
+  hipEvent_t part_ev_[3] = {nullptr, nullptr, nullptr};
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;
   // fbank tables
