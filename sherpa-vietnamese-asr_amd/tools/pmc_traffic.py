@@ -8,7 +8,9 @@ gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads (MI355X_MICROAR
           [--out profiles/pmc_traffic.json]
 
 Kernel classes: enc_gemm = gemm_bf16_kernel / gemm_f32_kernel with the dense A loader
-(template argument ALOAD = 0) and a [N][K] weight operand, the launches Engine::linear makes.
+(template argument ALOAD = 0) and a [N][K] weight operand, the launches Engine::linear /
+linear_h make (the NonlinAttention GEMM, EPI_MULAUX, is class attn_nonlin); any other class
+name matches kernels whose name contains it (e.g. ffn_fused).
 """
 import argparse
 import csv
@@ -17,14 +19,27 @@ import os
 import re
 
 
+def gemm_args(name: str):
+    """(kind, template integer args) of a gemm kernel name, demangled or (for instantiations
+    with __bf16 arguments, which rocprofv3 leaves mangled) mangled."""
+    m = re.search(r"gemm_(bf16|f32)_kernel<([^>]*)>", name)
+    if m:
+        return m.group(1), [a.strip() for a in m.group(2).split(",")]
+    m = re.search(r"gemm_(bf16|f32)_kernelI((?:Li\d+E|Lb[01]E)+)", name)
+    if m:
+        vals = re.findall(r"L(i|b)(\d+)E", m.group(2))
+        return m.group(1), [("false" if v == "0" else "true") if t == "b" else v for t, v in vals]
+    return None, None
+
+
 def in_class(name: str, cls: str) -> bool:
     if cls == "enc_gemm":
-        m = re.search(r"gemm_(bf16|f32)_kernel<([^>]*)>", name)
-        if not m:
+        kind, args = gemm_args(name)
+        if kind is None:
             return False
-        args = [a.strip() for a in m.group(2).split(",")]
-        if m.group(1) == "bf16":
-            return args[5] == "0"
+        m = re.match(r"(bf16|f32)", kind)
+        if kind == "bf16":
+            return args[5] == "0" and args[6] != "4"  # EPI_MULAUX = the NonlinAttention GEMM
         return args[4] == "0" and args[5] == "false"  # B n-contiguous = nonlin_attention
 
     return cls in name
