@@ -33,95 +33,138 @@ void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t s
 }
 
 // =====================================================================================
-// fbank: one wave per frame.  Samples gathered with kaldi edge reflection, DC removal,
-// pre-emphasis and povey window in f32, 512-point FFT in f64 (knf's rdft runs in double),
-// power spectrum f32, sparse mel triangles, log with FLT_EPSILON floor.
+// fbank: one wave per frame, 4 frames per block.  Samples gathered with kaldi edge
+// reflection (one round trip: all 7 loads per lane in flight), DC removal, pre-emphasis
+// (left neighbour by lane shuffle) and povey window in f32; the 512-point real FFT in f64
+// (knf's rdft runs in double) as a 256-point complex FFT of z[n] = x[2n] + i x[2n+1]:
+// four radix-4 Stockham passes, one butterfly per lane per pass, ping-ponging two per-wave
+// LDS images (no bit reversal, wave-local barriers only), then the even/odd split
+// X[k] = E[k] + W512^k O[k]; power spectrum f32, mel triangles (tables in LDS), log with
+// FLT_EPSILON floor.
 // =====================================================================================
 constexpr int kFbWaves = 4;
+constexpr int kMelWMax = 512;  // each FFT bin lies in at most two triangles
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
 
 __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
     const float* __restrict__ wav, const long* __restrict__ wav_off,
     const int* __restrict__ nsamp, const int* __restrict__ fr_off, int nseq, int total_frames,
     FbankTables tabs, float* __restrict__ out) {
-  __shared__ float sx[kFbWaves][400];
-  __shared__ double sre[kFbWaves][512];
-  __shared__ double sim[kFbWaves][512];
-  __shared__ float spow[kFbWaves][256];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  __shared__ double2 sTw[256];  // exp(-2 pi i u / 512), u < 256
+  __shared__ float sWin[400];
+  __shared__ int sMeta[240];
+  __shared__ float sMelW[kMelWMax];
+  __shared__ double2 sA[kFbWaves][256], sB[kFbWaves][256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < 256; i += 64 * kFbWaves)
+    sTw[i] = make_double2(tabs.twiddle[2 * i], tabs.twiddle[2 * i + 1]);
+  for (int i = tid; i < 400; i += 64 * kFbWaves) sWin[i] = tabs.window[i];
+  if (tid < 80) {
+    sMeta[tid] = tabs.mel_start[tid];
+    sMeta[80 + tid] = tabs.mel_len[tid];
+    sMeta[160 + tid] = tabs.mel_woff[tid];
+  }
+  {
+    const int nw = tabs.mel_woff[79] + tabs.mel_len[79];
+    for (int i = tid; i < nw && i < kMelWMax; i += 64 * kFbWaves) sMelW[i] = tabs.mel_w[i];
+  }
   const int frame = blockIdx.x * kFbWaves + w;
   const bool active = frame < total_frames;
-  float* x = sx[w];
-  double* re = sre[w];
-  double* im = sim[w];
-  int b = 0, f = 0, n = 1;
+  float xv[7];
   if (active) {
-    b = find_seq(fr_off, nseq, frame);
-    f = frame - fr_off[b];
-    n = nsamp[b];
+    const int b = find_seq(fr_off, nseq, frame);
+    const int f = frame - fr_off[b];
+    const long n = nsamp[b];
     const float* base = wav + wav_off[b];
-    double part = 0.0;
-    for (int i = lane; i < 400; i += 64) {
-      long s = (long)f * 160 - 120 + i;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int i = lane + 64 * k;
+      long s = (long)f * 160 - 120 + (i < 400 ? i : 399);
       while (s < 0 || s >= n) s = (s < 0) ? (-s - 1) : (2L * n - 1 - s);
-      float v = base[s];
-      x[i] = v;
-      part += (double)v;
+      xv[k] = base[s];
     }
+    double part = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      if (lane + 64 * k < 400) part += (double)xv[k];
     const float mean = (float)(wave_sum_d(part) / 400.0);
-    for (int i = lane; i < 400; i += 64) x[i] = x[i] - mean;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) xv[k] = xv[k] - mean;
   }
-  __syncthreads();
-  if (active) {
-    // pre-emphasis on the DC-removed frame (uses the un-emphasised left neighbour), window,
-    // scatter to bit-reversed positions
-    for (int i = lane; i < 512; i += 64) {
-      double v = 0.0;
-      if (i < 400) {
-        float cur = x[i];
-        float prev = (i == 0) ? x[0] : x[i - 1];
-        float e = __fsub_rn(cur, __fmul_rn(0.97f, prev));
-        v = (double)__fmul_rn(e, tabs.window[i]);
-      }
-      int r = __brev(i) >> 23;  // 9-bit reversal
-      re[r] = v;
-      im[r] = 0.0;
+  __syncthreads();  // tables staged
+  if (!active) return;
+  double2* A = sA[w];
+  double2* B = sB[w];
+  {
+    // pre-emphasis (left neighbour of sample i = lane + 64k: lane - 1, or lane 63 of chunk
+    // k - 1; sample 0 uses itself), window; real samples into A viewed as double[512]
+    double* xr = reinterpret_cast<double*>(A);
+    float carry = 0.f;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const float up = __shfl(xv[k], lane == 0 ? 0 : lane - 1, 64);
+      const float prev = lane != 0 ? up : (k == 0 ? xv[0] : carry);
+      carry = __shfl(xv[k], 63, 64);
+      const int i = lane + 64 * k;
+      const float e = __fsub_rn(xv[k], __fmul_rn(0.97f, prev));
+      xr[i] = i < 400 ? (double)__fmul_rn(e, sWin[i < 400 ? i : 0]) : 0.0;
     }
+    xr[lane + 448] = 0.0;
   }
-  __syncthreads();
-  for (int half = 1; half < 512; half <<= 1) {
-    if (active) {
-      const int tstep = 256 / half;
-      for (int q = 0; q < 4; ++q) {
-        int bf = lane + 64 * q;
-        int grp = bf / half, j = bf - grp * half;
-        int i0 = grp * 2 * half + j, i1 = i0 + half;
-        double wr = tabs.twiddle[2 * (j * tstep)], wi = tabs.twiddle[2 * (j * tstep) + 1];
-        double tr = wr * re[i1] - wi * im[i1];
-        double ti = wr * im[i1] + wi * re[i1];
-        double ar = re[i0], ai = im[i0];
-        re[i1] = ar - tr;
-        im[i1] = ai - ti;
-        re[i0] = ar + tr;
-        im[i0] = ai + ti;
-      }
+  __builtin_amdgcn_wave_barrier();
+  // 256-point complex FFT (Stockham radix-4): pass s with Ns = 4^s, lane j = one butterfly
+  const int j = lane;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const double2* X = (s & 1) ? B : A;
+    double2* Y = (s & 1) ? A : B;
+    const int ns_log = 2 * s, Ns = 1 << ns_log;
+    const int k = j & (Ns - 1);
+    double2 v0 = X[j], v1 = X[j + 64], v2 = X[j + 128], v3 = X[j + 192];
+    if (s > 0) {
+      // twiddle exp(-2 pi i k r / (4 Ns)) = W512^(u r), u = k * 128 / Ns
+      const int u = k << (7 - ns_log);
+      const int u2 = 2 * u, u3 = 3 * u;
+      const double2 t1 = sTw[u];
+      const double2 t2 = u2 < 256 ? sTw[u2] : make_double2(-sTw[u2 - 256].x, -sTw[u2 - 256].y);
+      const double2 t3 = u3 < 256 ? sTw[u3] : make_double2(-sTw[u3 - 256].x, -sTw[u3 - 256].y);
+      v1 = cmul(v1, t1);
+      v2 = cmul(v2, t2);
+      v3 = cmul(v3, t3);
     }
-    __syncthreads();
+    const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
+    const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
+    const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
+    const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);  // (v1 - v3) * (-i)
+    const int o = ((j >> ns_log) << (ns_log + 2)) + k;
+    Y[o] = make_double2(a0.x + a2.x, a0.y + a2.y);
+    Y[o + Ns] = make_double2(a1.x + a3.x, a1.y + a3.y);
+    Y[o + 2 * Ns] = make_double2(a0.x - a2.x, a0.y - a2.y);
+    Y[o + 3 * Ns] = make_double2(a1.x - a3.x, a1.y - a3.y);
+    __builtin_amdgcn_wave_barrier();
   }
-  if (active) {
-    for (int k = lane; k < 256; k += 64) {
-      float a = (float)re[k], c = (float)im[k];
-      spow[w][k] = __fadd_rn(__fmul_rn(a, a), __fmul_rn(c, c));
-    }
+  // Z = FFT256(z) is in A; X[k] = E[k] + W512^k O[k], E = (Z_k + conj Z_-k) / 2,
+  // O = (Z_k - conj Z_-k) / 2i; power of bins 0..255 (f32) into B viewed as float[256]
+  float* pw = reinterpret_cast<float*>(B);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int kb = lane + 64 * q;
+    const double2 zk = A[kb], zm = A[(256 - kb) & 255];
+    const double2 E = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+    const double2 O = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+    const double2 X = cmul(O, sTw[kb]);
+    const float re = (float)(E.x + X.x), im = (float)(E.y + X.y);
+    pw[kb] = __fadd_rn(__fmul_rn(re, re), __fmul_rn(im, im));
   }
-  __syncthreads();
-  if (active) {
-    for (int m = lane; m < 80; m += 64) {
-      const int st = tabs.mel_start[m], ln = tabs.mel_len[m], wo = tabs.mel_woff[m];
-      float acc = 0.f;
-      for (int k = 0; k < ln; ++k) acc = fmaf(tabs.mel_w[wo + k], spow[w][st + k], acc);
-      out[(long)frame * 80 + m] = logf(fmaxf(acc, 1.1920928955078125e-07f));
-    }
+  __builtin_amdgcn_wave_barrier();
+  for (int m = lane; m < 80; m += 64) {
+    const int st = sMeta[m], ln = sMeta[80 + m], wo = sMeta[160 + m];
+    float acc = 0.f;
+    for (int k = 0; k < ln; ++k) acc = fmaf(sMelW[wo + k], pw[st + k], acc);
+    out[(long)frame * 80 + m] = logf(fmaxf(acc, 1.1920928955078125e-07f));
   }
 }
 
@@ -540,40 +583,97 @@ struct DsW {
   float w[8];
 };
 
+// float4 per thread, 32-bit index math (rows * d / 4 < 2^31 at any batch the engine forms)
 __global__ void downsample_kernel(const float* __restrict__ x, const int* __restrict__ off_in,
                                   const int* __restrict__ off_out, const int* __restrict__ map_out,
                                   int total_out,
-                                  int d, int ds, DsW wts, float* __restrict__ out) {
-  long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)total_out * d) return;
-  int r = (int)(e / d), c = (int)(e - (long)r * d);
-  int b = map_out[r];
-  int tp = r - off_out[b];
-  int base = off_in[b];
-  int L = off_in[b + 1] - base;
-  float xv[8];
+                                  int d4, int ds, DsW wts, float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total_out * d4) return;
+  const int r = e / d4, c4 = e - r * d4;
+  const int b = map_out[r];
+  const int tp = r - off_out[b];
+  const int base = off_in[b];
+  const int L = off_in[b + 1] - base;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  float4 xv[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {  // all loads in flight (ds <= 8)
     int t = tp * ds + (u < ds ? u : 0);
     if (t > L - 1) t = L - 1;  // SimpleDownsample pads with the last frame
-    xv[u] = x[(long)(base + t) * d + c];
+    xv[u] = x4[(base + t) * d4 + c4];
   }
-  float acc = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int u = 0; u < 8; ++u)
-    if (u < ds) acc = fmaf(wts.w[u], xv[u], acc);
-  out[e] = acc;
+    if (u < ds) {
+      acc.x = fmaf(wts.w[u], xv[u].x, acc.x);
+      acc.y = fmaf(wts.w[u], xv[u].y, acc.y);
+      acc.z = fmaf(wts.w[u], xv[u].z, acc.z);
+      acc.w = fmaf(wts.w[u], xv[u].w, acc.w);
+    }
+  reinterpret_cast<float4*>(out)[e] = acc;
 }
 
 void launch_downsample(const float* x, const int* off_in, const int* off_out, const int* map_out,
                        int total_out, int d, int ds, const float* w_host8, float* out,
                        hipStream_t st) {
-  long n = (long)total_out * d;
+  const long n = (long)total_out * (d / 4);
   if (n <= 0) return;
+  ZASR_REQUIRE(d % 4 == 0 && n < (1L << 31), "downsample: width must be a multiple of 4");
   DsW w{};
   for (int i = 0; i < ds && i < 8; ++i) w.w[i] = w_host8[i];
   hipLaunchKernelGGL(downsample_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in,
-                     off_out, map_out, total_out, d, ds, w, out);
+                     off_out, map_out, total_out, d / 4, ds, w, out);
+}
+
+// The seam between encoder stacks (icefall Zipformer2Encoder / DownsampledZipformer2Encoder,
+// 3P): y = orig + (SimpleUpsample(xd) - orig) * s (out_combiner bypass; ds == 1: y = orig),
+// written once as
+//   * the next stack's input, convert_num_channels'd to width dn (truncate / zero-pad), and
+//   * columns [c0, d) of the full-dim encoder output (_get_full_dim_output),
+// so the stack output never makes a separate round trip through HBM.  float4 per thread.
+__global__ void stack_glue_kernel(const float* __restrict__ xd, const float* __restrict__ orig,
+                                  const int* __restrict__ off_in, const int* __restrict__ off_ds,
+                                  const int* __restrict__ map_in, int rows, int d4, int ds_shift,
+                                  const float* __restrict__ s, float* __restrict__ next, int dn4,
+                                  float* __restrict__ full, int ldf4, int c04) {
+  const int w4 = d4 > dn4 ? d4 : dn4;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * w4) return;
+  const int r = e / w4, c4 = e - r * w4;
+  float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < d4) {
+    const float4 o = reinterpret_cast<const float4*>(orig)[r * d4 + c4];
+    y = o;
+    if (ds_shift > 0) {
+      const int b = map_in[r];
+      const int t = r - off_in[b];
+      const float4 up = reinterpret_cast<const float4*>(xd)[(off_ds[b] + (t >> ds_shift)) * d4 + c4];
+      const float4 k = reinterpret_cast<const float4*>(s)[c4];
+      y.x = o.x + (up.x - o.x) * k.x;
+      y.y = o.y + (up.y - o.y) * k.y;
+      y.z = o.z + (up.z - o.z) * k.z;
+      y.w = o.w + (up.w - o.w) * k.w;
+    }
+    if (full != nullptr && c4 >= c04) reinterpret_cast<float4*>(full)[r * ldf4 + c4] = y;
+  }
+  if (next != nullptr && c4 < dn4) reinterpret_cast<float4*>(next)[r * dn4 + c4] = y;
+}
+
+void launch_stack_glue(const float* xd, const float* orig, const int* off_in, const int* off_ds,
+                       const int* map_in, int rows, int d, int ds, const float* s, float* next,
+                       int dn, float* full, int ldf, int c0, hipStream_t st) {
+  const int w = d > dn ? d : dn;
+  const long n = (long)rows * (w / 4);
+  if (n <= 0) return;
+  ZASR_REQUIRE(d % 4 == 0 && dn % 4 == 0 && ldf % 4 == 0 && c0 % 4 == 0 && n < (1L << 31),
+               "stack glue: widths must be multiples of 4");
+  int shift = 0;
+  while ((1 << shift) < ds) ++shift;
+  ZASR_REQUIRE((1 << shift) == ds, "stack glue: downsampling factor must be a power of 2");
+  hipLaunchKernelGGL(stack_glue_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig, off_in,
+                     off_ds, map_in, rows, d / 4, shift, s, next, dn / 4, full, ldf / 4, c0 / 4);
 }
 
 __global__ void upsample_combine_kernel(const float* __restrict__ xd,

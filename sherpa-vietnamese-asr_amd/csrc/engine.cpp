@@ -414,6 +414,13 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
                     &model_.enc_proj, &model_.joiner})
       mk(*l);
+    if (cfg.joiner_dim == 256 || cfg.joiner_dim == 512) {  // speculative-greedy joiner operand
+      void* p = nullptr;
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)gemm_rp_packed_elems(cfg.V, cfg.joiner_dim) * 2));
+      model_.allocations.push_back(p);
+      gemm_rp_pack_weights(model_.joiner.wh, cfg.V, cfg.joiner_dim, p, stream_);
+      model_.joiner_packed = p;
+    }
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
         // attn_in: the query and positional-query rows carry log2(e) in the bf16 path (the
@@ -1099,16 +1106,16 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     ws<float>("ly_attn", std::max<size_t>(attn_floats, 1));
   const int Dm = cfg.max_dim();
   float* full = ws<float>("st_full", (size_t)mL.total * Dm);
-  float* prev = e0;
-  int prev_w = d0;
-  std::vector<float*> outs(ns);
+  // stack i's input (50 Hz, width d_i): stack 0 takes the embed output, every later one is
+  // written by the previous seam's stack_glue
+  float* orig = ws<float>("st_orig0", (size_t)mL.total * model_.stacks[0].d);
+  prof_begin("elementwise");
+  launch_copy_cols(e0, d0, 0, orig, model_.stacks[0].d, 0, std::min(d0, model_.stacks[0].d),
+                   mL.total, true, model_.stacks[0].d, st_);
+  prof_end();
   for (int i = 0; i < ns; ++i) {
     const DStack& s = model_.stacks[i];
     const int d = s.d;
-    float* orig = ws<float>("st_orig" + std::to_string(i % 2), (size_t)mL.total * d);
-    prof_begin("elementwise");
-    launch_copy_cols(prev, prev_w, 0, orig, d, 0, std::min(prev_w, d), mL.total, true, d, st_);
-    prof_end();
     float* X;
     if (s.ds == 1) {
       X = orig;
@@ -1122,25 +1129,18 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       layer_forward(s, ly, X, mst[i].total, I(o_st[i]), st_map[i], mst[i].len,
                     reinterpret_cast<const long*>(d_meta + o_ao[i]), d_meta + o_sn[i],
                     mst[i].maxlen, I(o_o8[i]), R8[i]);
-    float* out = orig;
-    if (s.ds != 1) {
-      out = ws<float>("st_out" + std::to_string(i % 2), (size_t)mL.total * d);
-      prof_begin("elementwise");
-      launch_upsample_combine(X, orig, I(o_L), I(o_st[i]), L_map, mL.total, d, s.ds, s.comb, out, st_);
-      prof_end();
-    }
-    outs[i] = out;
-    prev = out;
-    prev_w = d;
-    // full-dim output: channel range [d_next_max, d) comes from the latest stack that has it
+    // seam: upsample + bypass combine, written as stack i+1's input and into the full-dim
+    // output's channel range [d_later_max, d) (the latest stack that has those channels)
     int later_max = 0;
     for (int j = i + 1; j < ns; ++j) later_max = std::max(later_max, model_.stacks[j].d);
-    if (d > later_max) {
-      prof_begin("elementwise");
-      launch_copy_cols(out, d, later_max, full, Dm, later_max, d - later_max, mL.total, false, 0, st_);
-      prof_end();
-    }
-    // `prev` stays valid: stack i+1 only touches the buffers of the other parity
+    const int dn = i + 1 < ns ? model_.stacks[i + 1].d : 0;
+    float* next = i + 1 < ns ? ws<float>("st_orig" + std::to_string((i + 1) % 2), (size_t)mL.total * dn)
+                             : nullptr;
+    prof_begin("elementwise");
+    launch_stack_glue(X, orig, I(o_L), I(o_st[i]), L_map, mL.total, d, s.ds, s.comb, next, dn,
+                      d > later_max ? full : nullptr, Dm, later_max, st_);
+    prof_end();
+    orig = next;
   }
   // ---------------- output downsample + encoder_proj ----------------
   float* fo = ws<float>("enc_ds", (size_t)mout.total * Dm);
@@ -1204,20 +1204,27 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   }
   float* logits = ws<float>("se_logits", slots * V);
   const bool bf16 = model_.joiner.wh != nullptr;
-  void* J = bf16 ? (void*)ws<__bf16>("se_joinin_h", slots * D) : (void*)ws<float>("se_joinin", slots * D);
-  ZASR_HIP_CHECK(hipMemsetAsync(J, 0, slots * D * (bf16 ? 2 : 4), st_));
+  // bf16 with the decoder-context table: J in fragment order for the packed joiner (every
+  // J writer goes through store_j4); without the table decjoin writes row-major J
+  static const bool no_pack = getenv("ZASR_JOINER_UNPACKED") != nullptr;
+  const bool packed = bf16 && model_.joiner_packed && model_.dec_table && !no_pack;
+  const size_t jrows = (size_t)joiner_packed_rows((long)slots);
+  void* J = bf16 ? (void*)ws<__bf16>("se_joinin_h", jrows * D) : (void*)ws<float>("se_joinin", slots * D);
+  ZASR_HIP_CHECK(hipMemsetAsync(J, 0, (bf16 ? jrows * 2 : slots * 4) * D, st_));
   DecTable dt{model_.dec_table, V, d_enc, d_eo, d_el, J, D, bf16 ? 1 : 0};
+  dt.j_packed = packed ? 1 : 0;
   DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
   // greedy with the decoder-context table: speculative windows (kernels.h, greedy_spec)
   const char* spec_env = getenv("ZASR_GREEDY_WINDOW");
   const int F = spec_env ? atoi(spec_env) : 4;
   if (H == 1 && model_.dec_table && (F == 4 || F == 8)) {
-    void* Js = bf16 ? (void*)ws<__bf16>("gs_joinin_h", (size_t)S * F * D)
+    void* Js = bf16 ? (void*)ws<__bf16>("gs_joinin_h", (size_t)joiner_packed_rows((long)S * F) * D)
                     : (void*)ws<float>("gs_joinin", (size_t)S * F * D);
     float* lg = ws<float>("gs_logits", (size_t)S * F * V);
     int* d_t = ws<int>("gs_t", S);
     int* d_active = ws<int>("gs_active", 2);
     DecTable ds{model_.dec_table, V, d_enc, d_eo, d_el, Js, D, bf16 ? 1 : 0};
+    ds.j_packed = packed ? 1 : 0;
     prof_begin("search");
     launch_search_init(st, S, 1, st_);
     launch_greedy_spec_init(ds, S, F, d_t, d_active, st_);
@@ -1229,7 +1236,10 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     while (k < Tmax) {
       for (int b = 0; b < kSync && k < Tmax; ++b, ++k) {
         prof_begin("joiner");
-        if (bf16) {
+        if (packed) {
+          JoinerPackedArgs ja{Js, model_.joiner_packed, model_.joiner.b, lg, S * F, V, D, d_t, d_el, F};
+          launch_joiner_packed(ja, st_);
+        } else if (bf16) {
           JoinerBf16Args ja{reinterpret_cast<const __bf16*>(Js),
                             reinterpret_cast<const __bf16*>(model_.joiner.wh), model_.joiner.b, lg,
                             S * F, V, D, d_t, d_el, F};
@@ -1267,7 +1277,10 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
       prof_end();
     }
     prof_begin("joiner");
-    if (bf16) {
+    if (packed) {
+      JoinerPackedArgs ja{J, model_.joiner_packed, model_.joiner.b, logits, rows, V, D};
+      launch_joiner_packed(ja, st_);
+    } else if (bf16) {
       JoinerBf16Args ja{reinterpret_cast<const __bf16*>(J), reinterpret_cast<const __bf16*>(model_.joiner.wh),
                         model_.joiner.b, logits, rows, V, D};
       launch_joiner_bf16(ja, st_);

@@ -63,6 +63,7 @@ struct DModel {
   float out_ds_w[2] = {0, 0};
   float* dec_emb = nullptr;   // [V][D]
   float* dec_conv = nullptr;  // [D][4][2]
+  void* joiner_packed = nullptr;  // bf16 joiner weights in MFMA-fragment order (bf16 mode)
   float* dec_table = nullptr;  // [V*V][D] decoder output per context (null: too large)
   float* dec_tap0 = nullptr;  // [V][D] conv tap 0 of each embedding row
   float* dec_tap1 = nullptr;  // [V][D] conv tap 1

@@ -77,6 +77,17 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
 void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t stream,
                bool a_bf16 = false, bool c_bf16 = false);
 
+// Row-panel GEMM (gemm_rp.hip) for K in {48, 64, 96, 128, 144, 192, 256, 288, 384, 512}:
+// C = epi(A W^T + bias) with W pre-packed by gemm_rp_pack_weights (bf16 [N][K] ->
+// MFMA-fragment order, gemm_rp_packed_elems(N, K) bf16 elements).  Combinations: A f32 -> C
+// bf16 (EPI_NONE / EPI_SWOOSHL), A f32 -> C f32 (EPI_NONE), A bf16 -> C f32 (EPI_RESADD).
+// Returns false (nothing launched) for any other combination or shape.
+bool gemm_rp_supported_k(int K);
+long gemm_rp_packed_elems(int N, int K);
+void gemm_rp_pack_weights(const void* W_bf16, int N, int K, void* out, hipStream_t stream);
+bool gemm_rp(const void* A, bool a_bf16, int lda, const void* Bp, const float* bias, void* C,
+             bool c_bf16, int ldc, int M, int N, int K, int epi, hipStream_t stream);
+
 // device f32 -> bf16 (round to nearest even) copy
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
 // dst[r][k] = bf16(src[r][k] * row_scale[r]) (one rounding), src / dst [N][K]

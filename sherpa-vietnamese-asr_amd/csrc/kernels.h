@@ -64,6 +64,12 @@ void launch_downsample(const float* x, const int* off_in, const int* off_out, co
 void launch_upsample_combine(const float* xd, const float* orig, const int* off_in,
                              const int* off_ds, const int* map_in, int total_rows, int d, int ds,
                              const float* s, float* y, hipStream_t st);
+// seam between stacks: y = orig + (xd[t / ds] - orig) * s (ds == 1: y = orig) written as the
+// next stack's input of width dn (truncated / zero-padded; null: none) and into columns
+// [c0, d) of the full-dim output (null or c0 >= d: none); xd / off_ds unused when ds == 1
+void launch_stack_glue(const float* xd, const float* orig, const int* off_in, const int* off_ds,
+                       const int* map_in, int rows, int d, int ds, const float* s, float* next,
+                       int dn, float* full, int ldf, int c0, hipStream_t st);
 // row -> sequence index map for one resolution (off: [nseq + 1])
 void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t st);
 // dst[r][0:dd] = src[r][0:min(ds, dd)], zero-padded  (convert_num_channels)
@@ -221,7 +227,26 @@ struct DecTable {
   void* J;                  // [S*H][D] joiner input of the next frame (bf16 if j_bf16)
   int D;
   int j_bf16;
+  int j_packed = 0;         // bf16 J in MFMA-fragment order (joiner_packed_kernel's A operand)
 };
+// Speculative-greedy joiner on fragment-packed operands: J packed by the greedy search
+// kernels ([row/32][D/16][64 lanes][8] bf16, rows padded to a multiple of 64), W packed once
+// at load by gemm_rp_pack_weights ([col/32][D/16][64][8], zero beyond V).  One block per
+// 64 x 64 output tile: both 64 KB operand tiles cross into LDS once with coalesced 16-byte
+// loads (every load of the block in flight together), 4 waves x one 32 x 32 tile over all of D.
+struct JoinerPackedArgs {
+  const void* Jp;
+  const void* Wp;
+  const float* bias;   // [V]
+  float* out;          // [M][V]
+  int M, V, D;
+  const int* live_t = nullptr;
+  const int* live_len = nullptr;
+  int live_f = 0;
+};
+void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st);
+// rows the packed J buffer must hold for M joiner rows
+inline long joiner_packed_rows(long M) { return (M + 63) / 64 * 64; }
 void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st);
 void launch_decjoin(const DecJoinArgs& a, hipStream_t st);
 void launch_joiner(const JoinerArgs& j, hipStream_t st);

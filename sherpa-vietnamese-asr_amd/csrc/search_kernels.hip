@@ -393,8 +393,82 @@ void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
   }
 }
 
+// --------------------------------------------------------------------------------------
+// speculative-greedy joiner on fragment-packed J / W (kernels.h JoinerPackedArgs)
+template <int QK>
+__global__ __launch_bounds__(256) void joiner_packed_kernel(JoinerPackedArgs j) {
+  __shared__ bf16x8 sJ[2 * QK * 64];
+  __shared__ bf16x8 sW[2 * QK * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.y * 64;
+  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M) &&
+      (m0 + 32 >= j.M || tile_done(j.live_t, j.live_len, j.live_f, m0 + 32, j.M)))
+    return;  // block-uniform: every stream of these 64 rows has finished
+  const int g0 = blockIdx.x * 2;
+  const bf16x8* srcJ = reinterpret_cast<const bf16x8*>(j.Jp) + (long)(m0 >> 5) * QK * 64;
+  const bf16x8* srcW = reinterpret_cast<const bf16x8*>(j.Wp) + (long)g0 * QK * 64;
+  constexpr int PER = 2 * QK * 64 / 256;
+  bf16x8 vj[PER], vw[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    vj[i] = srcJ[tid + 256 * i];
+    vw[i] = srcW[tid + 256 * i];
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    sJ[tid + 256 * i] = vj[i];
+    sW[tid + 256 * i] = vw[i];
+  }
+  __syncthreads();
+  const int rt = wid >> 1, gc = wid & 1;
+  const int row0 = m0 + 32 * rt;
+  if (row0 >= j.M) return;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int q = 0; q < QK; ++q)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sJ[(rt * QK + q) * 64 + lane],
+                                                  sW[(gc * QK + q) * 64 + lane], acc, 0, 0, 0);
+  const int col = (g0 + gc) * 32 + (lane & 31);
+  if (col >= j.V) return;
+  const float bb = j.bias[col];
+  const int h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < j.M) j.out[(long)row * j.V + col] = acc[r] + bb;
+  }
+}
+
+void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st) {
+  if (j.M <= 0) return;
+  dim3 grid(cdiv(j.V, 64), cdiv(j.M, 64));
+  switch (j.D) {
+    case 256: hipLaunchKernelGGL(joiner_packed_kernel<16>, grid, dim3(256), 0, st, j); break;
+    case 512: hipLaunchKernelGGL(joiner_packed_kernel<32>, grid, dim3(256), 0, st, j); break;
+    default: throw std::runtime_error("packed joiner: joiner dim must be 256 or 512");
+  }
+}
+
+// element offset of J[row][k] in the fragment-packed image (kernels.h JoinerPackedArgs)
+__device__ __forceinline__ long packed_j_off(long row, int k, int D) {
+  const long rt = row >> 5;
+  const int r = (int)(row & 31), q = k >> 4, hh = (k >> 3) & 1, j = k & 7;
+  return ((rt * (D >> 4) + q) * 64 + r + 32 * hh) * 8 + j;
+}
+
 __device__ __forceinline__ void store_j4(const DecTable& dt, long off, float4 e, float4 d) {
-  if (dt.j_bf16) {
+  if (dt.j_packed) {  // 4 consecutive k stay inside one 8-element fragment slot
+    bf16x4 v;
+    v[0] = (__bf16)fast_tanh(e.x + d.x);
+    v[1] = (__bf16)fast_tanh(e.y + d.y);
+    v[2] = (__bf16)fast_tanh(e.z + d.z);
+    v[3] = (__bf16)fast_tanh(e.w + d.w);
+    const long row = off / dt.D;
+    const int k = (int)(off - row * dt.D);
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(dt.J) + packed_j_off(row, k, dt.D)) = v;
+  } else if (dt.j_bf16) {
     bf16x4 v;
     v[0] = (__bf16)fast_tanh(e.x + d.x);
     v[1] = (__bf16)fast_tanh(e.y + d.y);
