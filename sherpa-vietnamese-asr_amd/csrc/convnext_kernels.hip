@@ -172,7 +172,7 @@ constexpr int kMlpM = 128;
 constexpr int kMlpLd = 136;
 }  // namespace
 
-__global__ __launch_bounds__(256) void convnext_mlp_kernel(
+__global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
     const __bf16* __restrict__ yin, const __bf16* __restrict__ x, long npos,
     const __bf16* __restrict__ w1, const float* __restrict__ b1, const __bf16* __restrict__ w2,
     const float* __restrict__ b2, __bf16* __restrict__ out) {
@@ -205,13 +205,22 @@ __global__ __launch_bounds__(256) void convnext_mlp_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[t][r] = 0.f;
 
-  for (int n3 = 0; n3 < 3; ++n3) {
-    // ---- H^T slice: rows = hidden units n3*128 + 32 wid + (0..31), cols = positions ----
-    const int hn = n3 * 128 + wid * 32 + col;
-    bf16x8 wf[8];
+  // weight fragments straight from L2 (96 KB each, shared by every block): W1 of slice n3 + 1
+  // is fetched under slice n3's pw2 MFMAs and W2 of slice n3 under its pw1 MFMAs, so only the
+  // first slice's W1 round trip is exposed
+  bf16x8 wf1[8], wf2[8];
+  {
+    const int hn = wid * 32 + col;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks)
-      wf[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
+      wf1[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
+  }
+  for (int n3 = 0; n3 < 3; ++n3) {
+    // ---- H^T slice: rows = hidden units n3*128 + 32 wid + (0..31), cols = positions ----
+    const int on = wid * 32 + col;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      wf2[ks] = *reinterpret_cast<const bf16x8*>(w2 + (long)on * 384 + n3 * 128 + ks * 16 + 8 * half);
     f32x16 acc1[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -223,8 +232,14 @@ __global__ __launch_bounds__(256) void convnext_mlp_kernel(
       for (int t = 0; t < 4; ++t) {
         const bf16x8 yf =
             *reinterpret_cast<const bf16x8*>(Ys + (t * 32 + col) * kMlpLd + ks * 16 + 8 * half);
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], yf, acc1[t], 0, 0, 0);
+        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf1[ks], yf, acc1[t], 0, 0, 0);
       }
+    }
+    if (n3 < 2) {
+      const int hn = (n3 + 1) * 128 + wid * 32 + col;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        wf1[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
     }
     // bias of the 16 hidden rows this lane holds: wid*32 + (r&3) + 8 (r>>2) + 4 half
     float bb[16];
@@ -242,22 +257,28 @@ __global__ __launch_bounds__(256) void convnext_mlp_kernel(
       }
     __syncthreads();
     // ---- O^T += W2[:, slice] H^T: rows = output channels 32 wid + (0..31) ----
-    const int on = wid * 32 + col;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      wf[ks] = *reinterpret_cast<const bf16x8*>(w2 + (long)on * 384 + n3 * 128 + ks * 16 + 8 * half);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bf16x8 hf =
             *reinterpret_cast<const bf16x8*>(Hs + (t * 32 + col) * kMlpLd + ks * 16 + 8 * half);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], hf, acc2[t], 0, 0, 0);
+        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf2[ks], hf, acc2[t], 0, 0, 0);
       }
     }
   }
 
   // ---- out = x + O + b2: lane holds position t*32 + col, channels 32 wid + 8 g + 4 half + e ----
+  // residual loads unconditional (clamped) and all in flight together; stores guarded
+  bf16x4 xr[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      long pp = p0 + t * 32 + col;
+      pp = pp < npos ? pp : npos - 1;
+      xr[g][t] = *reinterpret_cast<const bf16x4*>(x + pp * 128 + wid * 32 + 8 * g + 4 * half);
+    }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int ch = wid * 32 + 8 * g + 4 * half;
@@ -265,14 +286,12 @@ __global__ __launch_bounds__(256) void convnext_mlp_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const long pp = p0 + t * 32 + col;
-      if (pp >= npos) continue;
-      const bf16x4 xr = *reinterpret_cast<const bf16x4*>(x + pp * 128 + ch);
       bf16x4 o;
-      o[0] = (__bf16)((float)xr[0] + (acc2[t][4 * g + 0] + bo.x));
-      o[1] = (__bf16)((float)xr[1] + (acc2[t][4 * g + 1] + bo.y));
-      o[2] = (__bf16)((float)xr[2] + (acc2[t][4 * g + 2] + bo.z));
-      o[3] = (__bf16)((float)xr[3] + (acc2[t][4 * g + 3] + bo.w));
-      *reinterpret_cast<bf16x4*>(out + pp * 128 + ch) = o;
+      o[0] = (__bf16)((float)xr[g][t][0] + (acc2[t][4 * g + 0] + bo.x));
+      o[1] = (__bf16)((float)xr[g][t][1] + (acc2[t][4 * g + 1] + bo.y));
+      o[2] = (__bf16)((float)xr[g][t][2] + (acc2[t][4 * g + 2] + bo.z));
+      o[3] = (__bf16)((float)xr[g][t][3] + (acc2[t][4 * g + 3] + bo.w));
+      if (pp < npos) *reinterpret_cast<bf16x4*>(out + pp * 128 + ch) = o;
     }
   }
 }

@@ -6,6 +6,7 @@
 // floats per lane half: conflict-free ds_read_b32), double-buffered with one barrier per
 // K-slab, next slab's global loads (float4 per lane) in flight under the MFMAs.
 // Each wave owns a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA tiles.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -495,10 +496,226 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Multi-stage LDS-DMA variant (K % 32 == 0, dense A, no z-slices).  The register-staged
+// kernel above keeps one 32-deep K slab in flight, so every slab pays a full memory round
+// trip behind 8 MFMAs per wave (tools/gemm_lab.hip: the MFMA-heavy FFN shapes run at
+// ~15 % of peak).  Here each wave issues global_load_lds (16 B per lane, no VGPR destination)
+// for its share of the slab NS - 1 slabs ahead; the loop waits with a counted vmcnt for the
+// slab it is about to read, so NS - 2 slabs stay in flight across the raw s_barrier.
+// LDS images are lane-linear per 1 KB wave instruction (the DMA destination is base +
+// 16 * lane), bank-conflict-free for the fragment ds_read_b128 by an XOR swizzle applied to
+// the per-lane GLOBAL address:
+//   bf16 rows (64 B):  16-byte chunk c of row r stored at chunk c ^ ((r >> 2) & 3)
+//   f32 rows (128 B):  chunk c of row r stored at chunk c ^ ((r >> 1) & 7)
+// f32 A (the residual stream) is staged as f32 and rounded to bf16 at the fragment read.
+// All LDS is one __shared__ array and the loop has no ordinary global loads (either would
+// make hipcc drain the DMA queue with vmcnt(0)).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_base) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(g), (lds_ptr_t)(lds_base), 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NS, int EPI, typename TA, typename TC>
+__global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf16* Bw,
+                                                        int tiles_n) {
+  constexpr int BM = 128, BN = 128, BK = 32;
+  constexpr bool AF32 = std::is_same<TA, float>::value;
+  constexpr int A_BYTES = BM * BK * (AF32 ? 4 : 2);
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int GA = A_BYTES / 1024 / 4;  // DMA instructions per wave per slab
+  constexpr int GB = B_BYTES / 1024 / 4;
+  constexpr int G = GA + GB;
+  constexpr int LDE = 40;
+  constexpr int EPI_BYTES = 4 * 32 * LDE * 4;
+  constexpr int LDS_BYTES = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
+  static_assert(NS >= 2 && NS <= 4, "stages");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS_BYTES];
+
+  const TA* A = reinterpret_cast<const TA*>(p.A);
+  TC* C = reinterpret_cast<TC*>(p.C);
+  const int M = p.M, K = p.K, lda = p.lda;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int m_tile = tile / tiles_n;
+  const int m0 = m_tile * BM;
+  const int n0 = (tile - m_tile * tiles_n) * BN;
+  const int N = p.N;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nkt = K / BK;
+
+  // per-lane global source pointers of this wave's DMA instructions (slab 0)
+  const TA* asrc[GA];
+  const __bf16* bsrc[GB];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int ins = wid * GA + g;
+    if constexpr (AF32) {
+      const int row = ins * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ ((row >> 1) & 7);
+      const int gr = m0 + row < M ? m0 + row : M - 1;
+      asrc[g] = A + (long)gr * lda + 4 * lc;
+    } else {
+      const int row = ins * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((row >> 2) & 3);
+      const int gr = m0 + row < M ? m0 + row : M - 1;
+      asrc[g] = A + (long)gr * lda + 8 * lc;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < GB; ++g) {
+    const int ins = wid * GB + g;
+    const int row = ins * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ ((row >> 2) & 3);
+    const int gn = n0 + row < N ? n0 + row : N - 1;
+    bsrc[g] = Bw + (long)gn * p.sbn + 8 * lc;
+  }
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NS) * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int g = 0; g < GA; ++g) glds16(asrc[g] + k0, st + (wid * GA + g) * 1024);
+#pragma unroll
+    for (int g = 0; g < GB; ++g) glds16(bsrc[g] + k0, st + A_BYTES + (wid * GB + g) * 1024);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkt) issue(s);
+  const int r32 = lane & 31, h = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int ahead = nkt - 1 - kt < NS - 2 ? nkt - 1 - kt : NS - 2;
+    if (ahead >= 2) wait_vmcnt<2 * G>();
+    else if (ahead == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nkt) issue(kt + NS - 1);  // the buffer every wave finished reading
+    const unsigned char* st = smem + (kt % NS) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 2 * ks + h;  // 16-byte bf16 chunk of the fragment's k range
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + r32;
+        if constexpr (AF32) {
+          const int sw = (row >> 1) & 7;
+          const float4 x0 = *reinterpret_cast<const float4*>(st + row * 128 + (((2 * ch) ^ sw) << 4));
+          const float4 x1 = *reinterpret_cast<const float4*>(st + row * 128 + (((2 * ch + 1) ^ sw) << 4));
+          a[i][0] = (__bf16)x0.x; a[i][1] = (__bf16)x0.y; a[i][2] = (__bf16)x0.z; a[i][3] = (__bf16)x0.w;
+          a[i][4] = (__bf16)x1.x; a[i][5] = (__bf16)x1.y; a[i][6] = (__bf16)x1.z; a[i][7] = (__bf16)x1.w;
+        } else {
+          a[i] = *reinterpret_cast<const bf16x8*>(st + row * 64 + ((ch ^ ((row >> 2) & 3)) << 4));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * 64 + j * 32 + r32;
+        b[j] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + row * 64 + ((ch ^ ((row >> 2) & 3)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every DMA retired (vmcnt(0) above) and every stage read: reuse smem
+
+  // epilogue: as gemm_bf16_kernel (fragment -> LDS -> float4 rows)
+  float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
+  const int c4 = lane & 7;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sE[((r & 3) + 8 * (r >> 2) + 4 * h) * LDE + r32] = acc[i][j][r];
+      __builtin_amdgcn_wave_barrier();
+      const int col = n0 + wn * 64 + j * 32 + 4 * c4;
+      float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias && col < N) bias = *reinterpret_cast<const float4*>(p.bias + col);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = (lane >> 3) + 8 * q;
+        const int row = m0 + wm * 64 + i * 32 + rl;
+        float4 v = *reinterpret_cast<const float4*>(&sE[rl * LDE + 4 * c4]);
+        if (row < M && col < N) {
+          v.x = epi_act<EPI>(fmaf(v.x, p.alpha, bias.x));
+          v.y = epi_act<EPI>(fmaf(v.y, p.alpha, bias.y));
+          v.z = epi_act<EPI>(fmaf(v.z, p.alpha, bias.z));
+          v.w = epi_act<EPI>(fmaf(v.w, p.alpha, bias.w));
+          TC* dst = C + (long)row * p.ldc + col;
+          if constexpr (std::is_same<TC, float>::value) {
+            if constexpr (EPI == EPI_RESADD) {
+              const float4 o = *reinterpret_cast<const float4*>(dst);
+              v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            }
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            bf16x4 hv;
+            hv[0] = (__bf16)v.x; hv[1] = (__bf16)v.y; hv[2] = (__bf16)v.z; hv[3] = (__bf16)v.w;
+            *reinterpret_cast<bf16x4*>(dst) = hv;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <int NS, int EPI, typename TA, typename TC>
+void launch_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
+  const int tn = cdiv(p.N, 128), tm = cdiv(p.M, 128);
+  hipLaunchKernelGGL((gemm_glds_kernel<NS, EPI, TA, TC>), dim3(tn * tm), dim3(256), 0, st, p, Bw,
+                     tn);
+}
+
+int glds_mode() {  // ZASR_GEMM_GLDS=0 selects the register-staged kernel (A/B runs)
+  const char* e = getenv("ZASR_GEMM_GLDS");
+  return e ? atoi(e) : 1;
+}
+
+// the multi-stage kernel for the long-K / wide-N projections (dense, K % 32 == 0)
+template <int EPI, typename TA, typename TC>
+bool try_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
+  // measured (tools/rp_bench.hip): ahead of the register-staged kernel only on the long-K
+  // bf16-A output projections (K >= 1024: +11 %); behind it on the short-K / f32-A shapes
+  const int mode = glds_mode();
+  if (mode == 0 || p.slices != nullptr || p.K % 32 != 0 || p.K < 128 || p.M < 128) return false;
+  if (mode == 1 && (std::is_same<TA, float>::value || p.K < 1024)) return false;
+  if (p.lda % (std::is_same<TA, float>::value ? 4 : 8) != 0 || p.sbn % 8 != 0) return false;
+  if (std::is_same<TA, float>::value)
+    launch_glds<3, EPI, TA, TC>(p, Bw, st);
+  else
+    launch_glds<4, EPI, TA, TC>(p, Bw, st);
+  return true;
+}
+
 // BK = 32: at these K (72..1920) the 2-stage 64-deep variant measured 20-60 % slower (LDS
 // occupancy), tools/gemm_bench.hip
 template <int ALOAD, int EPI, typename TA, typename TC>
 void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
+  if constexpr (ALOAD == ALOAD_DENSE && EPI != EPI_MULAUX)
+    if (try_glds<EPI, TA, TC>(p, Bw, st)) return;
   launch_tile_h<32, ALOAD, EPI, TA, TC>(p, Bw, st);
 }
 

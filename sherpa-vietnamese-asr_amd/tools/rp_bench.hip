@@ -1,4 +1,5 @@
-// Row-panel GEMM (csrc/gemm_rp.hip) vs the 128x128-tile bf16 GEMM (csrc/gemm.hip) on the
+// Multi-stage LDS-DMA GEMM (gemm.hip gemm_glds_kernel) vs the register-staged 128x128-tile
+// bf16 GEMM on the
 // Zipformer-68M projection shapes (development tool, not part of libzasr).
 // Build: make -C tools rp_bench ; run on the GPU box: tools/rp_bench
 // Per shape: us per launch and algorithmic GB/s of both kernels, and the max |diff| between
@@ -66,6 +67,10 @@ int main() {
       {"ff_in3", 24671, 512, 1536, EPI_SWOOSHL, false, true},
       {"na_out3", 24671, 384, 512, EPI_RESADD, true, false},
       {"enc_proj", 98685, 512, 512, EPI_NONE, false, false},
+      {"ff_out1", 98685, 768, 256, EPI_RESADD, true, false},
+      {"ff_out2", 49342, 1280, 384, EPI_RESADD, true, false},
+      {"ff_out3", 24671, 1920, 512, EPI_RESADD, true, false},
+      {"ff_in1b", 98685, 256, 960, EPI_SWOOSHL, false, true},
   };
   size_t maxA = 0, maxC = 0, maxB = 0;
   for (auto& s : shapes) {
@@ -73,7 +78,7 @@ int main() {
     maxC = std::max(maxC, (size_t)s.M * s.N);
     maxB = std::max(maxB, (size_t)gemm_rp_packed_elems(s.N, s.K));
   }
-  void *dA, *dC0, *dC1, *dB, *dBp;
+  void *dA, *dA16, *dC0, *dC1, *dB, *dBp;
   float* dbias;
   hipMalloc(&dA, maxA * 4);
   hipMalloc(&dC0, maxC * 4);
@@ -87,6 +92,10 @@ int main() {
     std::vector<float> h(maxA);
     for (auto& x : h) x = nd(rng);
     hipMemcpy(dA, h.data(), maxA * 4, hipMemcpyHostToDevice);
+    std::vector<__bf16> h16(maxA);
+    for (size_t i = 0; i < maxA; ++i) h16[i] = (__bf16)h[i];
+    hipMalloc(&dA16, maxA * 2);
+    hipMemcpy(dA16, h16.data(), maxA * 2, hipMemcpyHostToDevice);
     std::vector<__bf16> hb(maxB);
     for (auto& x : hb) x = (__bf16)(nd(rng) * 0.06f);
     hipMemcpy(dB, hb.data(), maxB * 2, hipMemcpyHostToDevice);
@@ -97,7 +106,7 @@ int main() {
   for (auto& s : shapes) {
     gemm_rp_pack_weights(dB, s.N, s.K, dBp, 0);
     GemmParams p{};
-    p.A = reinterpret_cast<const float*>(dA);
+    p.A = reinterpret_cast<const float*>(s.a16 ? dA16 : dA);
     p.lda = s.K;
     p.sbk = 1;
     p.sbn = s.K;
@@ -113,25 +122,24 @@ int main() {
     hipMemset(dC0, 0, nC * 4);
     hipMemset(dC1, 0, nC * 4);
     p.C = reinterpret_cast<float*>(dC0);
+    setenv("ZASR_GEMM_GLDS", "0", 1);
     gemm_bf16(p, dB, s.epi, ALOAD_DENSE, 0, s.a16, s.c16);
-    const bool ok = gemm_rp(dA, s.a16, s.K, dBp, dbias, dC1, s.c16, s.N, s.M, s.N, s.K, s.epi, 0);
+    setenv("ZASR_GEMM_GLDS", "2", 1);
+    p.C = reinterpret_cast<float*>(dC1);
+    gemm_bf16(p, dB, s.epi, ALOAD_DENSE, 0, s.a16, s.c16);
     hipDeviceSynchronize();
-    if (!ok) {
-      printf("%-9s unsupported by gemm_rp\n", s.name);
-      continue;
-    }
     auto r0 = fetch(dC0, nC, s.c16), r1 = fetch(dC1, nC, s.c16);
     double err = 0;
     for (size_t i = 0; i < nC; ++i)
       err = std::max(err, (double)std::fabs(r0[i] - r1[i]) / std::max(1.0, (double)std::fabs(r0[i])));
+    setenv("ZASR_GEMM_GLDS", "0", 1);
     const double t_old = time_it([&] { gemm_bf16(p, dB, s.epi, ALOAD_DENSE, 0, s.a16, s.c16); });
-    const double t_rp = time_it([&] {
-      gemm_rp(dA, s.a16, s.K, dBp, dbias, dC1, s.c16, s.N, s.M, s.N, s.K, s.epi, 0);
-    });
+    setenv("ZASR_GEMM_GLDS", "2", 1);
+    const double t_rp = time_it([&] { gemm_bf16(p, dB, s.epi, ALOAD_DENSE, 0, s.a16, s.c16); });
     const double bytes = (double)s.M * s.K * (s.a16 ? 2 : 4) + (double)s.N * s.K * 2 +
                          (double)nC * (s.c16 ? 2 : 4) * (s.epi == EPI_RESADD ? 2 : 1);
     const double fl = 2.0 * s.M * s.K * s.N;
-    printf("%-9s M=%7d K=%4d N=%5d %s%s  tile128 %7.1f us %5.0f GB/s | rowpanel %7.1f us %5.0f GB/s %5.0f TF/s  x%.2f  diff %.2e\n",
+    printf("%-9s M=%7d K=%4d N=%5d %s%s  tile128 %7.1f us %5.0f GB/s | glds %7.1f us %5.0f GB/s %5.0f TF/s  x%.2f  diff %.2e\n",
            s.name, s.M, s.K, s.N, s.a16 ? "A16" : "A32", s.c16 ? "C16" : "C32", t_old,
            bytes / t_old * 1e-3, t_rp, bytes / t_rp * 1e-3, fl / t_rp * 1e-6, t_old / t_rp, err);
   }
