@@ -346,7 +346,47 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
   const int wn = wid - wm * WAVES_N;
 
   bf16x8 ra[A_LD], rb[B_LD];
+  // dense operands: the per-thread row pointers are k-invariant (rows past M / N are clamped
+  // to a valid row: they only feed outputs that are never stored), so a full slab costs one
+  // pointer add per load; only a K tail slab takes the clamped, zero-filling path
+  const TA* arow[A_LD];
+  const __bf16* brow[B_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int idx = tid + NT * i;
+    const int row = (idx < A_G ? idx : 0) / GPR, k8 = idx % GPR;
+    const int gm = m0 + row < M ? m0 + row : M - 1;
+    arow[i] = A + (long)gm * lda + 8 * k8;
+  }
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    const int idx = tid + NT * i;
+    const int n = (idx < B_G ? idx : 0) / GPR, k8 = idx % GPR;
+    const int gn = n0 + n < N ? n0 + n : N - 1;
+    brow[i] = B + (long)gn * p.sbn + 8 * k8;
+  }
+  auto to_bf16x8 = [](float4 x0, float4 x1) {
+    bf16x8 v;
+    v[0] = (__bf16)x0.x; v[1] = (__bf16)x0.y; v[2] = (__bf16)x0.z; v[3] = (__bf16)x0.w;
+    v[4] = (__bf16)x1.x; v[5] = (__bf16)x1.y; v[6] = (__bf16)x1.z; v[7] = (__bf16)x1.w;
+    return v;
+  };
   auto gload = [&](int kt) {
+    const int k0 = kt * BK;
+    if (ALOAD == ALOAD_DENSE && k0 + BK <= K) {
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        if constexpr (std::is_same<TA, __bf16>::value) {
+          ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + k0);
+        } else {
+          const float* a = reinterpret_cast<const float*>(arow[i]) + k0;
+          ra[i] = to_bf16x8(*reinterpret_cast<const float4*>(a), *reinterpret_cast<const float4*>(a + 4));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) rb[i] = *reinterpret_cast<const bf16x8*>(brow[i] + k0);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int idx = tid + NT * i;
