@@ -34,6 +34,8 @@ def gemm_args(name: str):
 
 def in_class(name: str, cls: str) -> bool:
     if cls == "enc_gemm":
+        if "gemm_glds_kernel" in name:  # multi-stage LDS-DMA variant: dense projections only
+            return True
         kind, args = gemm_args(name)
         if kind is None:
             return False
