@@ -1233,6 +1233,10 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     // host checks the live-stream count every kSync steps (one small D2H copy)
     constexpr int kSync = 16;
     int k = 0;
+    hipEvent_t live_ev[2];
+    for (auto& e : live_ev) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int slot = 0;
+    bool have_prev = false;
     while (k < Tmax) {
       for (int b = 0; b < kSync && k < Tmax; ++b, ++k) {
         prof_begin("joiner");
@@ -1254,11 +1258,20 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
         launch_greedy_spec(st, lg, V, S, F, d_t, d_el, hw_, ds, d_active, k & 1, st_);
         prof_end();
       }
-      ZASR_HIP_CHECK(hipMemcpyAsync(h_pinned_, d_active + ((k - 1) & 1), sizeof(int),
+      // the live count after this batch lands in pinned slot `slot`; the host then waits only
+      // for the PREVIOUS batch's count, so the GPU always has the next kSync steps queued (a
+      // batch enqueued after the last stream finished exits in every kernel's first lines)
+      ZASR_HIP_CHECK(hipMemcpyAsync(h_pinned_ + slot, d_active + ((k - 1) & 1), sizeof(int),
                                     hipMemcpyDeviceToHost, st_));
-      ZASR_HIP_CHECK(hipStreamSynchronize(st_));
-      if (*h_pinned_ == 0) break;
+      ZASR_HIP_CHECK(hipEventRecord(live_ev[slot], st_));
+      if (have_prev) {
+        ZASR_HIP_CHECK(hipEventSynchronize(live_ev[slot ^ 1]));
+        if (h_pinned_[slot ^ 1] == 0) break;
+      }
+      have_prev = true;
+      slot ^= 1;
     }
+    for (auto e : live_ev) (void)hipEventDestroy(e);
   } else {
   prof_begin("search");
   launch_search_init(st, S, H, st_);

@@ -296,7 +296,8 @@ template <int BM, int BN, int BK, int WAVES_M, int WAVES_N, int ALOAD, int EPI, 
           typename TC>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmParams p,
                                                                           const __bf16* Bw,
-                                                                          int tiles_n) {
+                                                                          int tiles_n,
+                                                                          int tiles_m) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WTM = BM / WAVES_M;
   constexpr int WTN = BN / WAVES_N;
@@ -322,8 +323,13 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
   const float* aux = p.aux;
   int M = p.M, K = p.K, lda = p.lda;
   long b_off = 0;
+  // one linear grid over (slice, tile): the XCD grouping below then keeps the N tiles of
+  // one (slice, row panel) on one XCD for every slice, not only when tiles % 8 == 0
+  const int tiles = tiles_n * tiles_m;
+  const int lin = xcd_tile(blockIdx.x, gridDim.x);
+  const int zs = lin / tiles;
   if (p.slices) {
-    const GemmSlice s = p.slices[blockIdx.z];
+    const GemmSlice s = p.slices[zs];
     A += s.a_off;
     b_off = s.b_off;
     C += s.c_off;
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     lda = s.lda;
   }
   const __bf16* B = Bw + b_off;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = lin - zs * tiles;
   const int m_tile = tile / tiles_n;
   const int m0 = m_tile * BM;
   if (m0 >= M) return;
@@ -512,9 +518,9 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
 template <int BM, int BN, int BK, int WM, int WN, int ALOAD, int EPI, typename TA, typename TC>
 void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
-  dim3 grid(tn * tm, 1, p.slices ? p.num_slices : 1);
+  dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
   hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC>), grid,
-                     dim3(64 * WM * WN), 0, st, p, Bw, tn);
+                     dim3(64 * WM * WN), 0, st, p, Bw, tn, tm);
 }
 
 template <int BK, int ALOAD, int EPI, typename TA, typename TC>
@@ -522,6 +528,9 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
   int best = pad32;
   int BN = (pad128 * 100 <= best * 115) ? 128 : (pad64 * 100 <= best * 115 ? 64 : 32);
+  // the sliced NonlinAttention GEMM streams a K = L-deep A panel per N tile: a 32-wide tile
+  // re-reads it N/32 times at one MFMA per wave per k-step -- take 64 despite the padding
+  if (EPI == EPI_MULAUX && BN == 32 && p.N > 64) BN = 64;
   long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
   bool big = blocks128 >= 512;
   if (BN == 128) {

@@ -1031,6 +1031,7 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
   }
   __syncthreads();
   // ---- C. top-1 token per row ----
+  float4 pre[RPW][2];
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int f = wid + 4 * r;
@@ -1055,6 +1056,16 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
       best = ob < best ? ob : best;
     }
     if (lane == 0) sTok[f] = best;
+    // a non-blank top-1 may be the window's emission: fetch the decoder-table row of the
+    // context it would create now, under the block-wide decision below
+    if (best != 0) {
+      const float4* nrow = reinterpret_cast<const float4*>(dt.table + ((long)y1 * dt.V + best) * D);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c4 = lane + 64 * j;
+        pre[r][j] = nrow[c4 < d4 ? c4 : d4 - 1];
+      }
+    }
   }
   __syncthreads();
   // ---- D. the first emission of the window ----
@@ -1142,15 +1153,18 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
   // ---- the next window's joiner input: J[s][f] = tanh(enc[t_new + f] + table[ny2, ny1]) ----
   if (t_new >= T_s) return;
   const int nf2 = T_s - t_new < F ? T_s - t_new : F;
-  float4 tv;
-  if (fe >= 0) {
-    if (tid < d4) tv = reinterpret_cast<const float4*>(dt.table + ((long)ny2 * dt.V + ny1) * D)[tid];
-  } else {
-    if (tid < d4) tv = sTab[tid];
-  }
-  if (fe >= 0) {
-    __syncthreads();  // every wave is done reading sTab: reuse it for the new context row
-    if (tid < d4) sTab[tid] = tv;
+  if (fe >= 0 && (fe & 3) == wid) {
+    // the emitting row's wave holds the new context's table row (prefetched in C)
+    const int r = fe >> 2;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      if (rr != r) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c4 = lane + 64 * j;
+        if (c4 < d4) sTab[c4] = pre[rr][j];
+      }
+    }
   }
   __syncthreads();
   const int fo = t_new - t0 - 1;  // staged row of frame t_new
