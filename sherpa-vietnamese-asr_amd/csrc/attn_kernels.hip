@@ -298,7 +298,14 @@ void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
 // r + (o8_b - off_b); the last row of a sequence also writes the zero padding up to
 // o8_b + L8_b.
 // =====================================================================================
-__global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const float* __restrict__ h3,
+__device__ __forceinline__ float4 h3_load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 h3_load4(const __bf16* p) {
+  const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+
+template <typename TH>
+__global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict__ h3,
                                                             const int* __restrict__ off,
                                                             const int* __restrict__ o8,
                                                             const int* __restrict__ map, int R,
@@ -315,9 +322,9 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const float* __restr
     const int rl = idx >> 4, c4 = idx & 15;
     const int r = r0 + rl < R ? r0 + rl : R - 1;
     const int cc = c0 + 4 * c4 < hid ? c0 + 4 * c4 : hid - 4;
-    const float* row = h3 + (long)r * 3 * hid;
-    sv[k] = *reinterpret_cast<const float4*>(row + cc);
-    xv[k] = *reinterpret_cast<const float4*>(row + hid + cc);
+    const TH* row = h3 + (long)r * 3 * hid;
+    sv[k] = h3_load4(row + cc);
+    xv[k] = h3_load4(row + hid + cc);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -347,12 +354,19 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const float* __restr
   }
 }
 
-void launch_nonlin_prep_t(const float* h3, const int* off, const int* o8, const int* map, int R,
-                          int hid, int R8, void* t1t, hipStream_t st) {
+void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const int* o8,
+                          const int* map, int R, int hid, int R8, void* t1t, hipStream_t st) {
   if (R <= 0) return;
   ZASR_REQUIRE(hid % 4 == 0, "nonlin_prep_t: hid must be a multiple of 4");
-  hipLaunchKernelGGL(nonlin_prep_t_kernel, dim3(cdiv(R, 64), cdiv(hid, 64)), dim3(256), 0, st,
-                     h3, off, o8, map, R, hid, R8, reinterpret_cast<__bf16*>(t1t));
+  const dim3 grid(cdiv(R, 64), cdiv(hid, 64));
+  if (h3_bf16)
+    hipLaunchKernelGGL(nonlin_prep_t_kernel<__bf16>, grid, dim3(256), 0, st,
+                       reinterpret_cast<const __bf16*>(h3), off, o8, map, R, hid, R8,
+                       reinterpret_cast<__bf16*>(t1t));
+  else
+    hipLaunchKernelGGL(nonlin_prep_t_kernel<float>, grid, dim3(256), 0, st,
+                       reinterpret_cast<const float*>(h3), off, o8, map, R, hid, R8,
+                       reinterpret_cast<__bf16*>(t1t));
 }
 
 }  // namespace zasr

@@ -863,12 +863,14 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   // 2. nonlin_attention (attention head 0 only)
   if (bf16) {
     // z = (A0 @ t1) * y on bf16 MFMA: A0 [L][L8] bf16, t1^T [hid][R8] bf16, z bf16
-    float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
+    // (s, x, y) = chunk(in_proj(src), 3) in bf16: read by the transpose kernel (s, x) and
+    // by the GEMM epilogue (y)
+    __bf16* h3 = ws<__bf16>("ly_h3_h", (size_t)R * 3 * hid);
     __bf16* t1t = ws<__bf16>("ly_t1t", (size_t)hid * R8);
     __bf16* z = ws<__bf16>("ly_z_h", (size_t)R * hid);
-    linear(Ly.na_in, X, d, R, h3, 3 * hid, EPI_NONE);
+    linear_h(Ly.na_in, X, false, d, R, h3, true, 3 * hid, EPI_NONE);
     prof_begin("elementwise");
-    launch_nonlin_prep_t(h3, d_off, d_o8, d_map, R, hid, R8, t1t, st_);
+    launch_nonlin_prep_t(h3, true, d_off, d_o8, d_map, R, hid, R8, t1t, st_);
     prof_end();
     GemmParams p{};
     p.A = reinterpret_cast<const float*>(A16);
@@ -879,13 +881,13 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     p.ldc = hid;
     p.N = hid;
     p.alpha = 1.f;
-    p.aux = h3 + 2 * hid;
+    p.aux = reinterpret_cast<const float*>(h3 + 2 * hid);  // bf16 (EPI_MULAUX16)
     p.ldaux = 3 * hid;
     p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
     p.num_slices = B;
     p.max_M = maxL;
     prof_begin("attn_nonlin");
-    gemm_bf16(p, t1t, EPI_MULAUX, ALOAD_DENSE, st_, true, true);
+    gemm_bf16(p, t1t, EPI_MULAUX16, ALOAD_DENSE, st_, true, true);
     prof_end();
     linear_h(Ly.na_out, z, true, hid, R, X, false, d, EPI_RESADD);
   } else {

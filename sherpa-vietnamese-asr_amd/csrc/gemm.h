@@ -20,6 +20,7 @@ enum GemmEpi : int {
   EPI_SWOOSHR = 2,  // C = SwooshR(v)
   EPI_RESADD = 3,   // C += v          (residual: src = src + module(src))
   EPI_MULAUX = 4,   // C = v * aux[m, n]
+  EPI_MULAUX16 = 5, // C = v * aux[m, n], aux bf16 (gemm_bf16 only)
 };
 
 enum GemmALoad : int {

@@ -321,6 +321,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
   const TA* A = reinterpret_cast<const TA*>(p.A);
   TC* C = reinterpret_cast<TC*>(p.C);
   const float* aux = p.aux;
+  const __bf16* aux16 = EPI == EPI_MULAUX16 ? reinterpret_cast<const __bf16*>(p.aux) : nullptr;
   int M = p.M, K = p.K, lda = p.lda;
   long b_off = 0;
   // one linear grid over (slice, tile): the XCD grouping below then keeps the N tiles of
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     b_off = s.b_off;
     C += s.c_off;
     if (aux) aux += s.aux_off;
+    if (aux16) aux16 += s.aux_off;
     M = s.M;
     K = s.K;
     lda = s.lda;
@@ -496,6 +498,10 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
             const float4 x = *reinterpret_cast<const float4*>(aux + (long)row * p.ldaux + col);
             v.x *= x.x; v.y *= x.y; v.z *= x.z; v.w *= x.w;
           }
+          if constexpr (EPI == EPI_MULAUX16) {
+            const bf16x4 x = *reinterpret_cast<const bf16x4*>(aux16 + (long)row * p.ldaux + col);
+            v.x *= (float)x[0]; v.y *= (float)x[1]; v.z *= (float)x[2]; v.w *= (float)x[3];
+          }
           TC* dst = C + (long)row * p.ldc + col;
           if constexpr (std::is_same<TC, float>::value) {
             if constexpr (EPI == EPI_RESADD) {
@@ -530,7 +536,7 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   int BN = (pad128 * 100 <= best * 115) ? 128 : (pad64 * 100 <= best * 115 ? 64 : 32);
   // the sliced NonlinAttention GEMM streams a K = L-deep A panel per N tile: a 32-wide tile
   // re-reads it N/32 times at one MFMA per wave per k-step -- take 64 despite the padding
-  if (EPI == EPI_MULAUX && BN == 32 && p.N > 64) BN = 64;
+  if ((EPI == EPI_MULAUX || EPI == EPI_MULAUX16) && BN == 32 && p.N > 64) BN = 64;
   long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
   bool big = blocks128 >= 512;
   if (BN == 128) {
@@ -763,7 +769,7 @@ bool try_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
 // occupancy), tools/gemm_bench.hip
 template <int ALOAD, int EPI, typename TA, typename TC>
 void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
-  if constexpr (ALOAD == ALOAD_DENSE && EPI != EPI_MULAUX)
+  if constexpr (ALOAD == ALOAD_DENSE && EPI != EPI_MULAUX && EPI != EPI_MULAUX16)
     if (try_glds<EPI, TA, TC>(p, Bw, st)) return;
   launch_tile_h<32, ALOAD, EPI, TA, TC>(p, Bw, st);
 }
@@ -804,7 +810,7 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
                bool a_bf16, bool c_bf16) {
   ZASR_REQUIRE(p.N > 0, "gemm: N must be positive");
   if (p.max_M <= 0) return;
-  ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (epi != EPI_MULAUX || p.ldaux % 4 == 0),
+  ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && ((epi != EPI_MULAUX && epi != EPI_MULAUX16) || p.ldaux % 4 == 0),
                "gemm_bf16: N and the C / aux row strides must be multiples of 4");
   ZASR_REQUIRE(p.slices != nullptr || p.K % 8 == 0, "gemm_bf16: K must be a multiple of 8");
   const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
@@ -832,6 +838,7 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
     switch (epi) {
       case EPI_NONE: return launch_bk_h<ALOAD_DENSE, EPI_NONE, __bf16, __bf16>(p, B, st);
       case EPI_MULAUX: return launch_bk_h<ALOAD_DENSE, EPI_MULAUX, __bf16, __bf16>(p, B, st);
+      case EPI_MULAUX16: return launch_bk_h<ALOAD_DENSE, EPI_MULAUX16, __bf16, __bf16>(p, B, st);
       default: break;
     }
   } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR && !a_bf16 && !c_bf16) {

@@ -117,8 +117,8 @@ struct AttnFlashArgs {
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st);
 // t1t[c][o8_b + j] = bf16(tanh(h3[r][c]) * h3[r][hid + c]) for packed row r = off_b + j;
 // columns [o8_b + L_b, o8_b + L8_b) zero; t1t row stride R8 = sum_b L8_b
-void launch_nonlin_prep_t(const float* h3, const int* off, const int* o8, const int* map, int R,
-                          int hid, int R8, void* t1t, hipStream_t st);
+void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const int* o8,
+                          const int* map, int R, int hid, int R8, void* t1t, hipStream_t st);
 // fused self-attention consumer: out[:, 12h:12h+12] = softmax(S_h) V_h, recomputing S
 struct AttnSAArgs {
   const float* qkp;

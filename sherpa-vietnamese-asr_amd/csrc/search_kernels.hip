@@ -397,8 +397,10 @@ void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
 // speculative-greedy joiner on fragment-packed J / W (kernels.h JoinerPackedArgs)
 template <int QK>
 __global__ __launch_bounds__(256) void joiner_packed_kernel(JoinerPackedArgs j) {
-  __shared__ bf16x8 sJ[2 * QK * 64];
-  __shared__ bf16x8 sW[2 * QK * 64];
+  // one LDS array: [J tile: 2 row tiles][W tile: 2 column groups], each QK x 1 KB
+  __shared__ __attribute__((aligned(1024))) bf16x8 sOp[4 * QK * 64];
+  bf16x8* const sJ = sOp;
+  bf16x8* const sW = sOp + 2 * QK * 64;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m0 = blockIdx.y * 64;
   if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M) &&
@@ -407,18 +409,18 @@ __global__ __launch_bounds__(256) void joiner_packed_kernel(JoinerPackedArgs j) 
   const int g0 = blockIdx.x * 2;
   const bf16x8* srcJ = reinterpret_cast<const bf16x8*>(j.Jp) + (long)(m0 >> 5) * QK * 64;
   const bf16x8* srcW = reinterpret_cast<const bf16x8*>(j.Wp) + (long)g0 * QK * 64;
-  constexpr int PER = 2 * QK * 64 / 256;
-  bf16x8 vj[PER], vw[PER];
+  // both tiles are lane-linear 1 KB fragments: LDS-DMA (global_load_lds, 16 B per lane), no
+  // VGPR staging and no ds_write pass; wave w moves chunks [w * 2QK/4, (w + 1) * 2QK/4)
+  constexpr int CPW = 2 * QK / 4;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    vj[i] = srcJ[tid + 256 * i];
-    vw[i] = srcW[tid + 256 * i];
+  for (int c = 0; c < CPW; ++c) {
+    const int ch = wid * CPW + c;
+    __builtin_amdgcn_global_load_lds(const_cast<bf16x8*>(srcJ + ch * 64 + lane),
+                                     (__attribute__((address_space(3))) void*)(sJ + ch * 64), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(const_cast<bf16x8*>(srcW + ch * 64 + lane),
+                                     (__attribute__((address_space(3))) void*)(sW + ch * 64), 16, 0, 0);
   }
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    sJ[tid + 256 * i] = vj[i];
-    sW[tid + 256 * i] = vw[i];
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int rt = wid >> 1, gc = wid & 1;
   const int row0 = m0 + 32 * rt;
