@@ -179,11 +179,14 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
 // =====================================================================================
 // conv.0: Conv2d(1 -> 8, 3x3, padding (0, 1)) + SwooshR.  One thread per (t, f).
 // =====================================================================================
+// BF16: bf16 output and the native-exp/log SwooshR (the bf16 mode; conv.4 reads it through
+// its bf16 implicit-im2col loader); f32: the libm form (the fp32 parity mode)
+template <bool BF16>
 __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict__ fb_off,
                              const int* __restrict__ c1_off, const int* __restrict__ c1_map,
                              int total,
                              const float* __restrict__ w, const float* __restrict__ bias,
-                             float* __restrict__ out) {
+                             void* __restrict__ out) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total * 80) return;
   int row = e / 80, f = e - row * 80;
@@ -195,31 +198,42 @@ __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict
   for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
     for (int kf = 0; kf < 3; ++kf) {
-      int ff = f + kf - 1;
-      xin[kt * 3 + kf] = (ff >= 0 && ff < 80) ? src[kt * 80 + ff] : 0.f;
+      const int ff = f + kf - 1;
+      const float v = src[kt * 80 + (ff < 0 ? 0 : (ff > 79 ? 79 : ff))];  // unconditional
+      xin[kt * 3 + kf] = (ff >= 0 && ff < 80) ? v : 0.f;
     }
-  float4 o0, o1;
   float r[8];
 #pragma unroll
   for (int o = 0; o < 8; ++o) {
     float acc = bias[o];
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc = fmaf(w[o * 9 + k], xin[k], acc);
-    r[o] = swooshr(acc);
+    r[o] = BF16 ? swooshr_fast(acc) : swooshr(acc);
   }
-  o0 = make_float4(r[0], r[1], r[2], r[3]);
-  o1 = make_float4(r[4], r[5], r[6], r[7]);
-  float4* dst = reinterpret_cast<float4*>(out + (long)e * 8);
-  dst[0] = o0;
-  dst[1] = o1;
+  if constexpr (BF16) {
+    typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+    bf16x8_t h;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) h[o] = (__bf16)r[o];
+    reinterpret_cast<bf16x8_t*>(out)[e] = h;
+  } else {
+    float4* dst = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (long)e * 8);
+    dst[0] = make_float4(r[0], r[1], r[2], r[3]);
+    dst[1] = make_float4(r[4], r[5], r[6], r[7]);
+  }
 }
 
 void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const int* c1_map,
-                  int total_rows, const float* w, const float* b, float* out, hipStream_t st) {
+                  int total_rows, const float* w, const float* b, void* out, bool out_bf16,
+                  hipStream_t st) {
   if (total_rows <= 0) return;
   long n = (long)total_rows * 80;
-  hipLaunchKernelGGL(conv1_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off, c1_off,
-                     c1_map, total_rows, w, b, out);
+  if (out_bf16)
+    hipLaunchKernelGGL(conv1_kernel<true>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
+                       c1_off, c1_map, total_rows, w, b, out);
+  else
+    hipLaunchKernelGGL(conv1_kernel<false>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
+                       c1_off, c1_map, total_rows, w, b, out);
 }
 
 // =====================================================================================

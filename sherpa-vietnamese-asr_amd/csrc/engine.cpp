@@ -1026,18 +1026,24 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   }
 
   // ---------------- Conv2dSubsampling ----------------
-  float* c1 = ws<float>("fe_c1", (size_t)mc1.total * 640);
+  // bf16 mode: conv.0 and conv.4 outputs in bf16 (read back through the GEMM's bf16
+  // implicit-im2col loaders)
+  const bool fe16 = model_.conv4.wh != nullptr && model_.conv7.wh != nullptr;
+  void* c1 = fe16 ? (void*)ws<__bf16>("fe_c1_h", (size_t)mc1.total * 640)
+                  : (void*)ws<float>("fe_c1", (size_t)mc1.total * 640);
   prof_begin("frontend_conv");
-  launch_conv1(d_feats, I(o_fb), I(o_c1), c1_map, mc1.total, model_.conv0_w, model_.conv0_b, c1, st_);
+  launch_conv1(d_feats, I(o_fb), I(o_c1), c1_map, mc1.total, model_.conv0_w, model_.conv0_b, c1,
+               fe16, st_);
   prof_end();
-  float* c2 = ws<float>("fe_c2", (size_t)mc2.total * 39 * 32);
+  void* c2 = fe16 ? (void*)ws<__bf16>("fe_c2_h", (size_t)mc2.total * 39 * 32)
+                  : (void*)ws<float>("fe_c2", (size_t)mc2.total * 39 * 32);
   {
     GemmParams p{};
-    p.A = c1;
+    p.A = reinterpret_cast<const float*>(c1);
     p.B = model_.conv4.w;
     p.sbk = 1;
     p.sbn = 72;
-    p.C = c2;
+    p.C = reinterpret_cast<float*>(c2);
     p.ldc = 32;
     p.bias = model_.conv4.b;
     p.N = 32;
@@ -1046,7 +1052,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     p.num_slices = B;
     p.max_M = mc2.maxlen * 39;
     prof_begin("frontend_conv");
-    if (model_.conv4.wh)
+    if (fe16)
+      gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_, true, true);
+    else if (model_.conv4.wh)
       gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_);
     else
       gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV2, false, st_);
@@ -1056,7 +1064,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   float* e0 = ws<float>("fe_e0", (size_t)mL.total * d0);
   {
     GemmParams p{};
-    p.A = c2;
+    p.A = reinterpret_cast<const float*>(c2);
     p.B = model_.conv7.w;
     p.sbk = 1;
     p.sbn = 288;
@@ -1074,7 +1082,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       __bf16* x4 = ws<__bf16>("fe_x4_h", (size_t)mL.total * 19 * 128);
       p.C = reinterpret_cast<float*>(x3);
       prof_begin("frontend_conv");
-      gemm_bf16(p, model_.conv7.wh, EPI_SWOOSHR, ALOAD_CONV3, st_, false, true);
+      gemm_bf16(p, model_.conv7.wh, EPI_SWOOSHR, ALOAD_CONV3, st_, fe16, true);
       prof_end();
       prof_begin("frontend_conv");
       launch_convnext_bf16(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, model_.pw1.wh,

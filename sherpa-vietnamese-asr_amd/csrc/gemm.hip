@@ -260,11 +260,24 @@ __device__ __forceinline__ bf16x8 load_a8(const GemmParams& p, const TA* A, int 
                                           int gm, int gk) {
   bf16x8 v;
   if constexpr (std::is_same<TA, __bf16>::value) {
-    // unconditional, clamped (K % 8 == 0)
+    // unconditional, clamped (K % 8 == 0); the implicit-im2col loaders take the 8 channels
+    // of one (time, freq) input position (k % 8 == 0 keeps them contiguous)
     const bool ok = gm < M && gk < K;
     const int m = gm < M ? gm : M - 1;
     const int k = gk < K ? gk : K - 8;
-    v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
+    if constexpr (ALOAD == ALOAD_DENSE) {
+      v = *reinterpret_cast<const bf16x8*>(A + (long)m * lda + k);
+    } else if constexpr (ALOAD == ALOAD_CONV2) {
+      const int t = m / 39, f = m - t * 39;
+      const int kk = k >> 3;
+      const int kt = kk / 3, kf = kk - kt * 3;
+      v = *reinterpret_cast<const bf16x8*>(A + ((long)(2 * t + kt) * 80 + 2 * f + kf) * 8);
+    } else {  // ALOAD_CONV3
+      const int t = m / 19, f = m - t * 19;
+      const int kk = k >> 5, c = k & 31;
+      const int kt = kk / 3, kf = kk - kt * 3;
+      v = *reinterpret_cast<const bf16x8*>(A + ((long)(t + kt) * 39 + 2 * f + kf) * 32 + c);
+    }
     if (!ok) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = (__bf16)0.f;
@@ -847,6 +860,10 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
     return launch_bk_h<ALOAD_CONV3, EPI_SWOOSHR, float, float>(p, B, st);
   } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR && !a_bf16 && c_bf16) {
     return launch_bk_h<ALOAD_CONV3, EPI_SWOOSHR, float, __bf16>(p, B, st);
+  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR && a_bf16 && c_bf16) {
+    return launch_bk_h<ALOAD_CONV2, EPI_SWOOSHR, __bf16, __bf16>(p, B, st);
+  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR && a_bf16 && c_bf16) {
+    return launch_bk_h<ALOAD_CONV3, EPI_SWOOSHR, __bf16, __bf16>(p, B, st);
   }
   throw std::runtime_error("gemm_bf16: unsupported (aload, epi, operand types) combination");
 }
