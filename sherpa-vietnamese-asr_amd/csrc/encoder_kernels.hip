@@ -315,7 +315,8 @@ template <int NQ>  // float4 per lane: d <= 256 * NQ
 __global__ __launch_bounds__(256) void bias_norm_kernel(float* __restrict__ x, int rows, int d,
                                                         const float* __restrict__ bias, float scale,
                                                         const float* __restrict__ orig,
-                                                        const float* __restrict__ bscale) {
+                                                        const float* __restrict__ bscale,
+                                                        float* __restrict__ copy_out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -347,23 +348,27 @@ __global__ __launch_bounds__(256) void bias_norm_kernel(float* __restrict__ x, i
                       o[q].z + (r.z - o[q].z) * s4.z, o[q].w + (r.w - o[q].w) * s4.w);
     }
     xr[i] = r;
+    // the next layer's bypass input (its copy of src): the row is complete in this thread's
+    // registers, so writing it over `orig` (read above by the same lane) is safe
+    if (copy_out) reinterpret_cast<float4*>(copy_out + (long)row * d)[i] = r;
   }
 }
 
 void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_scale,
-                      const float* orig, const float* bypass_scale, hipStream_t st) {
+                      const float* orig, const float* bypass_scale, hipStream_t st,
+                      float* copy_out) {
   if (rows <= 0) return;
   ZASR_REQUIRE(d % 4 == 0 && d <= 1024, "BiasNorm width must be a multiple of 4, <= 1024");
   const dim3 grid(cdiv(rows, 4));
   if (d <= 256)
     hipLaunchKernelGGL(bias_norm_kernel<1>, grid, dim3(256), 0, st, x, rows, d, bias,
-                       expf(log_scale), orig, bypass_scale);
+                       expf(log_scale), orig, bypass_scale, copy_out);
   else if (d <= 512)
     hipLaunchKernelGGL(bias_norm_kernel<2>, grid, dim3(256), 0, st, x, rows, d, bias,
-                       expf(log_scale), orig, bypass_scale);
+                       expf(log_scale), orig, bypass_scale, copy_out);
   else
     hipLaunchKernelGGL(bias_norm_kernel<4>, grid, dim3(256), 0, st, x, rows, d, bias,
-                       expf(log_scale), orig, bypass_scale);
+                       expf(log_scale), orig, bypass_scale, copy_out);
 }
 
 // =====================================================================================

@@ -684,7 +684,8 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
 }
 
 void Engine::linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M, void* C,
-                      bool c_bf16, int ldc, int epi) {
+                      bool c_bf16, int ldc, int epi, const float* byp_orig,
+                      const float* byp_scale) {
   ZASR_REQUIRE(l.wh != nullptr, "linear_h needs bf16 weights");
   GemmParams p{};
   p.A = reinterpret_cast<const float*>(A);
@@ -700,6 +701,8 @@ void Engine::linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M,
   p.K = l.K;
   p.alpha = 1.f;
   p.max_M = M;
+  p.byp_orig = byp_orig;
+  p.byp_scale = byp_scale;
   prof_begin("enc_gemm");
   gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_, a_bf16, c_bf16);
   prof_end();
@@ -760,11 +763,12 @@ struct MetaPack {
 void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, const int* d_off,
                            const int* d_map,
                            const std::vector<int>& lens, const long* d_aoff,
-                           const void* d_slices_nl, int maxL, const int* d_o8, int R8) {
+                           const void* d_slices_nl, int maxL, const int* d_o8, int R8, bool orig_ready, bool last_layer) {
   const int d = S.d, h = S.h, B = (int)lens.size();
   const int hid = 3 * d / 4;
   float* O = ws<float>("ly_orig", (size_t)R * d);
-  ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
+  if (!orig_ready)  // else the previous layer's BiasNorm already wrote src here
+    ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
   // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
   const bool bf16 = precision_ == 1;
   float* qkp = nullptr;
@@ -797,19 +801,23 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_end();
   }
   static const bool ffn_unfused = getenv("ZASR_FFN_UNFUSED") != nullptr;
+  // bf16 mode: feed_forward2's residual epilogue also applies bypass_mid (same formula as
+  // launch_bypass, one pass over X fewer)
   auto ff = [&](int k) {
     const DLin& fi = Ly.ff_in[k];
+    const float* bo = (bf16 && k == 1) ? O : nullptr;
+    const float* bs = (bf16 && k == 1) ? Ly.bypass_mid : nullptr;
     if (fi.wh && !ffn_unfused && ffn_fused_supported(d)) {
       // bf16 mode: in_proj -> SwooshL -> out_proj + residual in one kernel, hidden on chip
       prof_begin("ffn_fused");
-      launch_ffn_fused(X, R, d, fi.N, fi.wh, fi.b, Ly.ff_out[k].wh, Ly.ff_out[k].b, st_);
+      launch_ffn_fused(X, R, d, fi.N, fi.wh, fi.b, Ly.ff_out[k].wh, Ly.ff_out[k].b, st_, bo, bs);
       prof_end();
       return;
     }
     if (fi.wh) {  // bf16 mode: the hidden activation crosses HBM in bf16
       __bf16* H = ws<__bf16>("ly_hid_h", (size_t)R * fi.N);
       linear_h(fi, X, false, d, R, H, true, fi.N, EPI_SWOOSHL);
-      linear_h(Ly.ff_out[k], H, true, fi.N, R, X, false, d, EPI_RESADD);
+      linear_h(Ly.ff_out[k], H, true, fi.N, R, X, false, d, EPI_RESADD, bo, bs);
     } else {
       float* H = ws<float>("ly_hid", (size_t)R * fi.N);
       linear(fi, X, d, R, H, fi.N, EPI_SWOOSHL);
@@ -921,17 +929,19 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   self_attn(0);
   conv(0);
   ff(1);
-  // 4. bypass_mid
-  prof_begin("elementwise");
-  launch_bypass(X, O, Ly.bypass_mid, R, d, st_);
-  prof_end();
+  // 4. bypass_mid (bf16 mode: folded into feed_forward2's epilogue)
+  if (!bf16) {
+    prof_begin("elementwise");
+    launch_bypass(X, O, Ly.bypass_mid, R, d, st_);
+    prof_end();
+  }
   // 5. self_attn2, conv_module2, feed_forward3
   self_attn(1);
   conv(1);
   ff(2);
   // 6. BiasNorm + bypass
   prof_begin("elementwise");
-  launch_bias_norm(X, R, d, Ly.norm_b, Ly.norm_ls, O, Ly.bypass, st_);
+  launch_bias_norm(X, R, d, Ly.norm_b, Ly.norm_ls, O, Ly.bypass, st_, last_layer ? nullptr : O);
   prof_end();
 }
 
@@ -1135,10 +1145,10 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       launch_downsample(orig, I(o_L), I(o_st[i]), st_map[i], mst[i].total, d, s.ds, s.ds_w, X, st_);
       prof_end();
     }
-    for (const DLayer& ly : s.layers)
-      layer_forward(s, ly, X, mst[i].total, I(o_st[i]), st_map[i], mst[i].len,
+    for (size_t li = 0; li < s.layers.size(); ++li)
+      layer_forward(s, s.layers[li], X, mst[i].total, I(o_st[i]), st_map[i], mst[i].len,
                     reinterpret_cast<const long*>(d_meta + o_ao[i]), d_meta + o_sn[i],
-                    mst[i].maxlen, I(o_o8[i]), R8[i]);
+                    mst[i].maxlen, I(o_o8[i]), R8[i], li > 0, li + 1 == s.layers.size());
     // seam: upsample + bypass combine, written as stack i+1's input and into the full-dim
     // output's channel range [d_later_max, d) (the latest stack that has those channels)
     int later_max = 0;

@@ -132,13 +132,15 @@ class Engine {
   std::vector<TokenResult> run_search(const float* d_enc, const std::vector<int>& t_out, int beam);
   void layer_forward(const DStack& stk, const DLayer& ly, float* X, int R, const int* d_off,
                      const int* d_map, const std::vector<int>& lens, const long* d_aoff,
-                     const void* d_slices_nl, int maxL, const int* d_o8, int R8);
+                     const void* d_slices_nl, int maxL, const int* d_o8, int R8, bool orig_ready = false,
+                     bool last_layer = true);
   void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
               const char* cls = "enc_gemm");
   // bf16 mode only: A and/or C in bf16 (GEMM -> GEMM intermediates; the GEMM rounds A to
   // bf16 on load anyway, so storing it rounded changes nothing numerically)
   void linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M, void* C, bool c_bf16,
-                int ldc, int epi);
+                int ldc, int epi, const float* byp_orig = nullptr,
+                const float* byp_scale = nullptr);
   void ensure_pos_tables(int max_len);
 
   // timing

@@ -39,7 +39,9 @@ __global__ __launch_bounds__(256, (D <= 192 ? 2 : 1)) void ffn_fused_kernel(floa
                                                            const __bf16* __restrict__ W1,
                                                            const float* __restrict__ b1,
                                                            const __bf16* __restrict__ W2,
-                                                           const float* __restrict__ b2) {
+                                                           const float* __restrict__ b2,
+                                                           const float* __restrict__ byp_orig,
+                                                           const float* __restrict__ byp_scale) {
   constexpr int KS = D / 16;     // k-steps of the first product
   constexpr int OT = D / 32;     // output row tiles of the second
   constexpr int W1LD = D + 8;    // W1 chunk row stride (bf16): odd multiple of 16 B
@@ -176,6 +178,14 @@ __global__ __launch_bounds__(256, (D <= 192 ? 2 : 1)) void ffn_fused_kernel(floa
       v.y += o[t][4 * g + 1] + bb.y;
       v.z += o[t][4 * g + 2] + bb.z;
       v.w += o[t][4 * g + 3] + bb.w;
+      if (byp_orig != nullptr) {  // bypass_mid folded in (launch_bypass's formula)
+        const float4 b0 = *reinterpret_cast<const float4*>(byp_orig + (long)tok * D + ch);
+        const float4 k = *reinterpret_cast<const float4*>(byp_scale + ch);
+        v.x = b0.x + (v.x - b0.x) * k.x;
+        v.y = b0.y + (v.y - b0.y) * k.y;
+        v.z = b0.z + (v.z - b0.z) * k.z;
+        v.w = b0.w + (v.w - b0.w) * k.w;
+      }
       *reinterpret_cast<float4*>(xr + ch) = v;
     }
 }
@@ -185,14 +195,15 @@ __global__ __launch_bounds__(256, (D <= 192 ? 2 : 1)) void ffn_fused_kernel(floa
 bool ffn_fused_supported(int D) { return D == 64 || D == 96 || D == 128 || D == 192; }
 
 void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float* b1,
-                      const void* W2, const float* b2, hipStream_t st) {
+                      const void* W2, const float* b2, hipStream_t st, const float* byp_orig,
+                      const float* byp_scale) {
   if (R <= 0) return;
   ZASR_REQUIRE(ffn_fused_supported(D), "ffn_fused: unsupported model dim");
   ZASR_REQUIRE(F % 8 == 0, "ffn_fused: feed-forward dim must be a multiple of 8");
   const dim3 grid(cdiv(R, kTok));
   const __bf16* w1 = reinterpret_cast<const __bf16*>(W1);
   const __bf16* w2 = reinterpret_cast<const __bf16*>(W2);
-#define ZASR_FFN(DV) hipLaunchKernelGGL(ffn_fused_kernel<DV>, grid, dim3(256), 0, st, X, R, F, w1, b1, w2, b2)
+#define ZASR_FFN(DV) hipLaunchKernelGGL(ffn_fused_kernel<DV>, grid, dim3(256), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
   switch (D) {
     case 64: ZASR_FFN(64); break;
     case 96: ZASR_FFN(96); break;

@@ -497,6 +497,20 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
       const int col = n0 + wn * WTN + j * 32 + 4 * c4;
       float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
       if (p.bias && col < N) bias = *reinterpret_cast<const float4*>(p.bias + col);
+      // residual-epilogue side inputs: unconditional (clamped) loads, all in flight before
+      // the guarded stores (a guarded load compiles to a branch with its own vmcnt(0))
+      float4 pre_o[4], pre_b[4], pre_k = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (EPI == EPI_RESADD && std::is_same<TC, float>::value) {
+        const int cc = col < N ? col : N - 4;
+        if (p.byp_orig != nullptr) pre_k = *reinterpret_cast<const float4*>(p.byp_scale + cc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + wm * WTM + i * 32 + (lane >> 3) + 8 * q;
+          const long off = (long)(row < M ? row : M - 1) * p.ldc + cc;
+          pre_o[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + off);
+          if (p.byp_orig != nullptr) pre_b[q] = *reinterpret_cast<const float4*>(p.byp_orig + off);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int rl = (lane >> 3) + 8 * q;
@@ -518,8 +532,15 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
           TC* dst = C + (long)row * p.ldc + col;
           if constexpr (std::is_same<TC, float>::value) {
             if constexpr (EPI == EPI_RESADD) {
-              const float4 o = *reinterpret_cast<const float4*>(dst);
+              const float4 o = pre_o[q];
               v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+              if (p.byp_orig != nullptr) {  // bypass_mid folded in (launch_bypass's formula)
+                const float4 b0 = pre_b[q];
+                v.x = b0.x + (v.x - b0.x) * pre_k.x;
+                v.y = b0.y + (v.y - b0.y) * pre_k.y;
+                v.z = b0.z + (v.z - b0.z) * pre_k.z;
+                v.w = b0.w + (v.w - b0.w) * pre_k.w;
+              }
             }
             *reinterpret_cast<float4*>(dst) = v;
           } else {
@@ -721,6 +742,20 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
       const int col = n0 + wn * 64 + j * 32 + 4 * c4;
       float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
       if (p.bias && col < N) bias = *reinterpret_cast<const float4*>(p.bias + col);
+      // residual-epilogue side inputs: unconditional (clamped) loads, all in flight before
+      // the guarded stores (a guarded load compiles to a branch with its own vmcnt(0))
+      float4 pre_o[4], pre_b[4], pre_k = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (EPI == EPI_RESADD && std::is_same<TC, float>::value) {
+        const int cc = col < N ? col : N - 4;
+        if (p.byp_orig != nullptr) pre_k = *reinterpret_cast<const float4*>(p.byp_scale + cc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + wm * 64 + i * 32 + (lane >> 3) + 8 * q;
+          const long off = (long)(row < M ? row : M - 1) * p.ldc + cc;
+          pre_o[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + off);
+          if (p.byp_orig != nullptr) pre_b[q] = *reinterpret_cast<const float4*>(p.byp_orig + off);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int rl = (lane >> 3) + 8 * q;
@@ -734,8 +769,15 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
           TC* dst = C + (long)row * p.ldc + col;
           if constexpr (std::is_same<TC, float>::value) {
             if constexpr (EPI == EPI_RESADD) {
-              const float4 o = *reinterpret_cast<const float4*>(dst);
+              const float4 o = pre_o[q];
               v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+              if (p.byp_orig != nullptr) {  // bypass_mid folded in (launch_bypass's formula)
+                const float4 b0 = pre_b[q];
+                v.x = b0.x + (v.x - b0.x) * pre_k.x;
+                v.y = b0.y + (v.y - b0.y) * pre_k.y;
+                v.z = b0.z + (v.z - b0.z) * pre_k.z;
+                v.w = b0.w + (v.w - b0.w) * pre_k.w;
+              }
             }
             *reinterpret_cast<float4*>(dst) = v;
           } else {

@@ -41,8 +41,11 @@ void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int tot
 
 // ---- Zipformer2 encoder elementwise / per-sequence kernels ----
 // y = x * exp(log_scale) * rsqrt(mean((x - bias)^2));  optionally y = orig + (y - orig) * s
+// copy_out (nullable): the result also written there (the next layer's bypass input; may
+// alias orig)
 void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_scale,
-                      const float* orig, const float* bypass_scale, hipStream_t st);
+                      const float* orig, const float* bypass_scale, hipStream_t st,
+                      float* copy_out = nullptr);
 // x = orig + (x - orig) * s[c]
 void launch_bypass(float* x, const float* orig, const float* s, long rows, int d, hipStream_t st);
 // g[r][c] = x2[r][c] * sigmoid(x2[r][d + c])
@@ -142,7 +145,8 @@ void launch_attn_sa(const AttnSAArgs& a, bool online, bool bf16, hipStream_t st)
 // X[R][D] += W2 SwooshL(W1 X + b1) + b2; W1 [F][D], W2 [D][F] bf16; D in {64, 96, 128, 192, 256}
 bool ffn_fused_supported(int D);
 void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float* b1,
-                      const void* W2, const float* b2, hipStream_t st);
+                      const void* W2, const float* b2, hipStream_t st,
+                      const float* byp_orig = nullptr, const float* byp_scale = nullptr);
 
 // ---- transducer search (core/asr_engine.py:1023-1153) ----
 struct SearchState {
