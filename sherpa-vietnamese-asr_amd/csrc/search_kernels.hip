@@ -529,6 +529,8 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   __shared__ unsigned long long cand[kMaxBeam], cHash[kMaxBeam];
   __shared__ double cScore[kMaxBeam];
   __shared__ int cLen[kMaxBeam], cY1[kMaxBeam], cY2[kMaxBeam], cDup[kMaxBeam];
+  __shared__ int sKK;
+  __shared__ unsigned long long sFmask;
 
   ZASR_STAMP(0);
   const int V4 = V >> 2;
@@ -557,7 +559,7 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   float4 ev[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
   const bool next = t + 1 < T_s;
   if constexpr (TABLE) {
-    if (wid == 0 && next) {
+    if (next) {  // every wave writes J rows of its candidates (step 4)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c4 = lane + 64 * j;
@@ -675,163 +677,159 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   ZASR_STAMP(2);
   __syncthreads();
   ZASR_STAMP(3);
-  if (wid != 0) return;
-
-  // ---- 3. expansion (:1110-1138), wave 0 ----
+  // ---- 3. expansion (:1110-1138): ranking and candidate decode in wave 0 ----
   // 3a. global rank of each wave-list key (keys are distinct): the k best, best first
   const int total = n * V;
   const int k = beam < total ? beam : total;
-  {
-    const unsigned long long key = lane < 4 * KB ? cK[lane] : 0ull;
-    int rank = 0;
-    for (int j = 0; j < 4 * KB; ++j) rank += cK[j] > key ? 1 : 0;
-    if (key != 0ull && rank < k) cand[rank] = key;
-  }
-  const unsigned long long nzmask = __ballot(lane < 4 * KB && cK[lane < 4 * KB ? lane : 0] != 0ull);
-  const int nz = __popcll(nzmask);
-  const int kk = k < nz ? k : nz;
-  __builtin_amdgcn_wave_barrier();
-  // 3b. lane c decodes candidate c: token, hotword transition (:1127-1131; blank and UNK
-  //     skip the graph, :1129), sequence identity
-  const bool lv = lane < kk;
+  const bool lv_any = wid == 0;
+  int kk = 0;
   int hi = 0, tok = 0, nhw = 0, klen = 0, ny1 = 0, ny2 = 0;
   float val = 0.f;
   double score = 0.0;
   unsigned long long key = 0ull;
-  if (lv) {
-    const unsigned long long key0 = cand[lane];
-    val = key_val(key0);
-    const int idx = key_idx(key0);
-    hi = idx / V;
-    tok = idx - hi * V;
-    score = (double)val;
-    nhw = pHw[hi];
-    if (tok == 0) {
-      key = pHash[hi];
-      klen = pLen[hi];
-      ny1 = pY1[hi];
-      ny2 = pY2[hi];
-    } else {
-      if (hw.num_states > 0 && tok != 2) {
-        const int cls = hw.tok2cls[tok];
-        if (cls < 0) {
-          score += -hw.node_score[nhw];
-          nhw = 0;
-        } else {
-          const long e = (long)nhw * hw.num_cls + cls;
-          score += hw.delta[e];
-          nhw = hw.next[e];
-        }
-      }
-      key = hash_push(pHash[hi], tok);
-      klen = pLen[hi] + 1;
-      ny2 = pY1[hi];
-      ny1 = tok;
+  bool lv = false;
+  if (lv_any) {
+    {
+      const unsigned long long key = lane < 4 * KB ? cK[lane] : 0ull;
+      int rank = 0;
+      for (int j = 0; j < 4 * KB; ++j) rank += cK[j] > key ? 1 : 0;
+      if (key != 0ull && rank < k) cand[rank] = key;
     }
-    cHash[lane] = key;
-    cLen[lane] = klen;
-    cScore[lane] = score;
-    cY1[lane] = ny1;
-    cY2[lane] = ny2;
+    const unsigned long long nzmask = __ballot(lane < 4 * KB && cK[lane < 4 * KB ? lane : 0] != 0ull);
+    const int nz = __popcll(nzmask);
+    kk = k < nz ? k : nz;
+    __builtin_amdgcn_wave_barrier();
+    // 3b. lane c decodes candidate c: token, hotword transition (:1127-1131; blank and UNK
+    //     skip the graph, :1129), sequence identity
+    lv = lane < kk;
+    if (lv) {
+      const unsigned long long key0 = cand[lane];
+      val = key_val(key0);
+      const int idx = key_idx(key0);
+      hi = idx / V;
+      tok = idx - hi * V;
+      score = (double)val;
+      nhw = pHw[hi];
+      if (tok == 0) {
+        key = pHash[hi];
+        klen = pLen[hi];
+        ny1 = pY1[hi];
+        ny2 = pY2[hi];
+      } else {
+        if (hw.num_states > 0 && tok != 2) {
+          const int cls = hw.tok2cls[tok];
+          if (cls < 0) {
+            score += -hw.node_score[nhw];
+            nhw = 0;
+          } else {
+            const long e = (long)nhw * hw.num_cls + cls;
+            score += hw.delta[e];
+            nhw = hw.next[e];
+          }
+        }
+        key = hash_push(pHash[hi], tok);
+        klen = pLen[hi] + 1;
+        ny2 = pY1[hi];
+        ny1 = tok;
+      }
+      cHash[lane] = key;
+      cLen[lane] = klen;
+      cScore[lane] = score;
+      cY1[lane] = ny1;
+      cY2[lane] = ny2;
+    }
+    if (lane == 0) sKK = kk;
   }
-  __builtin_amdgcn_wave_barrier();
-  // the next frame's decoder rows of every candidate context (table gather), in flight
-  // while duplicates are resolved
-  constexpr int KP = KB < 8 ? KB : 8;
-  float4 dv[KP][2];
+  __syncthreads();  // candidate contexts visible to every wave
+  // every wave: the next frame's decoder rows of its candidates c = wid + 4 m (table gather),
+  // in flight while wave 0 resolves duplicates
+  constexpr int KW = (KB + 3) / 4;
+  float4 dv[KW][2];
+  const int kk_all = sKK;
   if constexpr (TABLE) {
     if (next) {
 #pragma unroll
-      for (int c = 0; c < KP; ++c) {
-        if (c < kk) {
+      for (int m = 0; m < KW; ++m) {
+        const int c = wid + 4 * m;
+        if (c < kk_all) {
           const float* row = dt.table + ((long)cY2[c] * dt.V + cY1[c]) * dt.D;
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int c4 = lane + 64 * j;
-            if (c4 < dt.D / 4) dv[c][j] = *reinterpret_cast<const float4*>(row + 4 * c4);
+            if (c4 < dt.D / 4) dv[m][j] = *reinterpret_cast<const float4*>(row + 4 * c4);
           }
         }
       }
     }
   }
-  // 3c. duplicates of the full sequence merge into their first occurrence, in candidate
-  //     order, with an f64 log-add (:1133-1138)
-  int dup = -1;
-  if (lv) {
-    for (int c = 0; c < lane; ++c)
-      if (cLen[c] == klen && cHash[c] == key) {
-        dup = c;
-        break;
-      }
-    cDup[lane] = dup;
-  }
-  __builtin_amdgcn_wave_barrier();
-  const bool first = lv && dup < 0;
-  const unsigned long long fmask = __ballot(first);
-  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int slot = __popcll(fmask & below);
-  const bool emit = first && tok != 0;
-  const unsigned long long emask = __ballot(emit);
-  const int node_base = st.node_count[s];
-  if (first) {
-    double lp = score;
-    int f64 = 0;
-    for (int c = lane + 1; c < kk; ++c)
-      if (cDup[c] == lane) lp = log_add(lp, f64, cScore[c], 0, &f64);
-    int nnode = pNode[hi];
-    if (emit) {
-      const int nid = node_base + __popcll(emask & below);
-      const long gi = (long)s * st.node_cap + nid;
-      st.node_tok[gi] = tok;
-      st.node_frame[gi] = t;
-      st.node_parent[gi] = pNode[hi];
-      st.node_lp[gi] = (double)val - pLp[hi];
-      st.node_stats[gi] = sStats[hi];
-      nnode = nid;
+  if (lv_any) {
+    // 3c. duplicates of the full sequence merge into their first occurrence, in candidate
+    //     order, with an f64 log-add (:1133-1138)
+    int dup = -1;
+    if (lv) {
+      for (int c = 0; c < lane; ++c)
+        if (cLen[c] == klen && cHash[c] == key) {
+          dup = c;
+          break;
+        }
+      cDup[lane] = dup;
     }
-    const int o = base + slot;
-    st.lp[o] = lp;
-    st.lpf[o] = f64;
-    st.hash[o] = key;
-    st.len[o] = klen;
-    st.y1[o] = ny1;
-    st.y2[o] = ny2;
-    st.hw[o] = nhw;
-    st.node[o] = nnode;
-  }
-  if (lane == 0) {
-    st.nh[s] = __popcll(fmask);
-    st.node_count[s] = node_base + __popcll(emask);
+    __builtin_amdgcn_wave_barrier();
+    const bool first = lv && dup < 0;
+    const unsigned long long fmask = __ballot(first);
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int slot = __popcll(fmask & below);
+    const bool emit = first && tok != 0;
+    const unsigned long long emask = __ballot(emit);
+    const int node_base = st.node_count[s];
+    if (first) {
+      double lp = score;
+      int f64 = 0;
+      for (int c = lane + 1; c < kk; ++c)
+        if (cDup[c] == lane) lp = log_add(lp, f64, cScore[c], 0, &f64);
+      int nnode = pNode[hi];
+      if (emit) {
+        const int nid = node_base + __popcll(emask & below);
+        const long gi = (long)s * st.node_cap + nid;
+        st.node_tok[gi] = tok;
+        st.node_frame[gi] = t;
+        st.node_parent[gi] = pNode[hi];
+        st.node_lp[gi] = (double)val - pLp[hi];
+        st.node_stats[gi] = sStats[hi];
+        nnode = nid;
+      }
+      const int o = base + slot;
+      st.lp[o] = lp;
+      st.lpf[o] = f64;
+      st.hash[o] = key;
+      st.len[o] = klen;
+      st.y1[o] = ny1;
+      st.y2[o] = ny2;
+      st.hw[o] = nhw;
+      st.node[o] = nnode;
+    }
+    if (lane == 0) {
+      st.nh[s] = __popcll(fmask);
+      st.node_count[s] = node_base + __popcll(emask);
+      sFmask = fmask;
+    }
   }
   ZASR_STAMP(4);
-  // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]) ----
+  // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]),
+  //         one candidate per wave at a time ----
   if constexpr (TABLE) {
     if (next) {
+      __syncthreads();  // sFmask
+      const unsigned long long fm = sFmask;
 #pragma unroll
-      for (int c0 = 0; c0 < KB; c0 += KP) {
-        if (c0 > 0) {  // beams above 8: the next batch of candidate rows
+      for (int m = 0; m < KW; ++m) {
+        const int cc = wid + 4 * m;
+        if (cc < kk_all && ((fm >> cc) & 1ull)) {
+          const int sl = __popcll(fm & ((1ull << cc) - 1ull));
 #pragma unroll
-          for (int c = 0; c < KP; ++c) {
-            if (c0 + c < kk && ((fmask >> (c0 + c)) & 1ull)) {
-              const float* row = dt.table + ((long)cY2[c0 + c] * dt.V + cY1[c0 + c]) * dt.D;
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const int c4 = lane + 64 * j;
-                if (c4 < dt.D / 4) dv[c][j] = *reinterpret_cast<const float4*>(row + 4 * c4);
-              }
-            }
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < KP; ++c) {
-          const int cc = c0 + c;
-          if (cc < kk && ((fmask >> cc) & 1ull)) {
-            const int sl = __popcll(fmask & ((1ull << cc) - 1ull));
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int c4 = lane + 64 * j;
-              if (c4 < dt.D / 4) store_j4(dt, (long)(base + sl) * dt.D + 4 * c4, ev[j], dv[c][j]);
-            }
+          for (int j = 0; j < 2; ++j) {
+            const int c4 = lane + 64 * j;
+            if (c4 < dt.D / 4) store_j4(dt, (long)(base + sl) * dt.D + 4 * c4, ev[j], dv[m][j]);
           }
         }
       }
