@@ -90,6 +90,16 @@ int zasr_decode_device(zasr_recognizer* h, const float* d_wav, const int64_t* wa
                        const int64_t* n, int32_t count, int32_t beam, void* stream,
                        zasr_result** out);
 
+/* Several device-resident batches back to back: chunks as in zasr_decode_device, grouped
+   into n_batches consecutive batches of batch_sizes[i] chunks (sum = count).  Batch k+1's
+   fbank + encoder overlap batch k's search on the GPU; results for all count chunks, in
+   chunk order, identical to decoding each batch with zasr_decode_device.  Replaces the
+   reference's 2-worker chunk dispatch, whose point is that one worker's beam search runs
+   while the other's encoder does (core/asr_engine.py:2250-2276). */
+int zasr_decode_device_batches(zasr_recognizer* h, const float* d_wav, const int64_t* wav_off,
+                               const int64_t* n, int32_t count, const int32_t* batch_sizes,
+                               int32_t n_batches, int32_t beam, void* stream, zasr_result** out);
+
 /* Encoder only: features -> encoder_out rows [T'_i][joiner_dim], packed in chunk order
    into out (cap floats); t_out[i] receives T'_i. */
 int zasr_encode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,

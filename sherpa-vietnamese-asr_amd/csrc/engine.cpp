@@ -225,8 +225,35 @@ T* Engine::ws(const std::string& name, size_t count) {
 }
 
 void Engine::upload(void* dst, const void* src, size_t bytes) {
-  ZASR_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st_));
+  // staged through the current pinned arena: a copy from pinned memory is truly
+  // asynchronous, so enqueueing the next batch's encoder never waits for the stream (the
+  // arena of a pipeline slot is reset only after that slot's previous batch has completed)
+  PinArena& a = pin_[pin_cur_];
+  const size_t need = (bytes + 255) & ~size_t(255);
+  if (a.used + need <= a.cap) {
+    char* h = a.p + a.used;
+    a.used += need;
+    std::memcpy(h, src, bytes);
+    ZASR_HIP_CHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st_));
+    return;
+  }
+  a.want += need;  // grown at the arena's next reset
   // pageable source: HIP stages the copy before returning, so `src` may be reused
+  ZASR_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st_));
+}
+
+void Engine::pin_reset(int arena) {
+  // callers guarantee every earlier copy out of this arena has executed
+  PinArena& a = pin_[arena];
+  const size_t want = std::max(a.want + a.used, a.cap);
+  if (want > a.cap) {
+    if (a.p) ZASR_HIP_CHECK(hipHostFree(a.p));
+    a.cap = want + want / 4 + 4096;
+    ZASR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&a.p), a.cap, hipHostMallocDefault));
+  }
+  a.used = 0;
+  a.want = 0;
+  pin_cur_ = arena;
 }
 
 Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const HotwordDFA& hw,
@@ -235,7 +262,11 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
   ZASR_REQUIRE(precision == 0 || precision == 1, "precision must be 0 (fp32) or 1 (bf16)");
   ZASR_HIP_CHECK(hipSetDevice(device_));
   ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+  {
+    int least = 0, greatest = 0;
+    ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
+  }
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   st_ = stream_;
   const std::string cfg_path = dir + "/config.json";
@@ -552,8 +583,10 @@ Engine::~Engine() {
     (void)hipEventDestroy(pe.a);
     (void)hipEventDestroy(pe.b);
   }
-  if (h_pinned_) (void)hipHostFree(h_pinned_);
   (void)hipStreamSynchronize(stream2_);
+  if (h_pinned_) (void)hipHostFree(h_pinned_);
+  for (auto& a : pin_)
+    if (a.p) (void)hipHostFree(a.p);
   for (auto e : part_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(stream2_);
   (void)hipStreamDestroy(stream_);
@@ -1379,92 +1412,104 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
 // ------------------------------------------------------------------------------------
 // public entry points
 // ------------------------------------------------------------------------------------
-std::vector<TokenResult> Engine::decode_device(const float* d_wav, const std::vector<long>& wav_off,
-                                               const std::vector<long>& n, int beam,
-                                               hipStream_t st) {
-  ZASR_HIP_CHECK(hipSetDevice(device_));
-  st_ = st ? st : stream_;
+void Engine::encode_stage(const float* d_wav, const std::vector<long>& wav_off,
+                          const std::vector<long>& n, int slot, Pending& pd) {
+  pin_reset(slot);
   const int B = (int)n.size();
+  pd = Pending{};
+  pd.B = B;
+  pd.ready = part_ev_[slot];
   std::vector<int> frames;
   long total_frames = 0;
   for (int b = 0; b < B; ++b) total_frames += n[b] > 0 ? (n[b] + 80) / 160 : 0;
   float* feats = ws<float>("feats", (size_t)std::max<long>(total_frames, 1) * 80);
   run_fbank(d_wav, wav_off, n, feats, frames);
   // chunks too short for the encoder produce empty results (T' = 0)
-  std::vector<int> valid, T;
+  std::vector<int> T;
   std::vector<long> foff(B + 1, 0);
   for (int b = 0; b < B; ++b) foff[b + 1] = foff[b] + frames[b];
-  bool all_valid = true;
-  for (int b = 0; b < B; ++b) {
+  for (int b = 0; b < B; ++b)
     if (frames[b] >= 9) {
-      valid.push_back(b);
+      pd.valid.push_back(b);
       T.push_back(frames[b]);
-    } else {
-      all_valid = false;
     }
-  }
-  std::vector<TokenResult> out(B);
-  if (valid.empty()) {
-    st_ = stream_;
-    return out;
-  }
+  if (pd.valid.empty()) return;
   const float* fptr = feats;
-  if (!all_valid) {  // compact valid chunks' features
+  if ((int)pd.valid.size() != B) {  // compact valid chunks' features
     float* cf = ws<float>("feats_compact", (size_t)total_frames * 80);
     long pos = 0;
-    for (int b : valid) {
+    for (int b : pd.valid) {
       ZASR_HIP_CHECK(hipMemcpyAsync(cf + pos * 80, feats + foff[b] * 80, (size_t)frames[b] * 80 * 4,
                                     hipMemcpyDeviceToDevice, st_));
       pos += frames[b];
     }
     fptr = cf;
   }
-  // Optionally two halves, pipelined: half B's encoder on the call's stream while half A's
-  // search runs on the engine's second stream (ordered by an event per half).
-  const int nv = (int)valid.size();
-  // Measured neutral-to-negative at the bench's 120 chunks (each half's search takes as long
-  // as the whole batch's: the step count is set by the densest stream, not by the stream
-  // count), so it is opt-in (ZASR_PIPELINE=1).
-  static const bool pipe = getenv("ZASR_PIPELINE") != nullptr;
-  const int parts = (nv >= 8 && pipe) ? 2 : 1;
-  int split = nv;
-  if (parts == 2) {  // balance the halves by frames
-    long tot = 0, run = 0;
-    for (int t : T) tot += t;
-    split = 1;
-    for (int i = 0; i < nv - 1; ++i) {
-      run += T[i];
-      split = i + 1;
-      if (2 * run >= tot) break;
-    }
-  }
-  const int bounds[3] = {0, parts == 2 ? split : nv, nv};
-  std::vector<std::vector<int>> tp(parts), tout(parts);
-  std::vector<float*> encp(parts);
-  long frame0 = 0;
-  for (int p = 0; p < parts; ++p) {
-    tp[p].assign(T.begin() + bounds[p], T.begin() + bounds[p + 1]);
-    long tot_out = 0, fr = 0;
-    for (int t : tp[p]) {
-      tot_out += ((t - 7) / 2 + 1) / 2;
-      fr += t;
-    }
-    encp[p] = ws<float>("enc_out" + std::to_string(p),
-                        (size_t)std::max<long>(tot_out, 1) * model_.cfg.joiner_dim);
-    run_encoder(fptr + frame0 * 80, tp[p], encp[p], tout[p]);
-    ZASR_HIP_CHECK(hipEventRecord(part_ev_[p], st_));
-    frame0 += fr;
-  }
+  long tot_out = 0;
+  for (int t : T) tot_out += ((t - 7) / 2 + 1) / 2;
+  // the encoder output is the only buffer the search reads: one per pipeline slot
+  pd.enc = ws<float>(slot ? "enc_out1" : "enc_out0",
+                     (size_t)std::max<long>(tot_out, 1) * model_.cfg.joiner_dim);
+  run_encoder(fptr, T, pd.enc, pd.t_out);
+  ZASR_HIP_CHECK(hipEventRecord(pd.ready, st_));
+}
+
+std::vector<TokenResult> Engine::search_stage(Pending& pd, int beam) {
+  std::vector<TokenResult> out(pd.B);
+  if (pd.valid.empty()) return out;
   hipStream_t main_st = st_;
   st_ = stream2_;
-  for (int p = 0; p < parts; ++p) {
-    ZASR_HIP_CHECK(hipStreamWaitEvent(stream2_, part_ev_[p], 0));
-    std::vector<TokenResult> r = run_search(encp[p], tout[p], beam);
-    for (int i = bounds[p]; i < bounds[p + 1]; ++i) out[valid[i]] = std::move(r[i - bounds[p]]);
-  }
-  // the call's stream sees the whole decode complete (the results are already on the host)
+  pin_reset(2);
+  ZASR_HIP_CHECK(hipStreamWaitEvent(stream2_, pd.ready, 0));
+  std::vector<TokenResult> r = run_search(pd.enc, pd.t_out, beam);
+  for (size_t i = 0; i < pd.valid.size(); ++i) out[pd.valid[i]] = std::move(r[i]);
+  // the call's stream sees the search complete (its results are already on the host)
   ZASR_HIP_CHECK(hipEventRecord(part_ev_[2], stream2_));
   ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[2], 0));
+  st_ = main_st;
+  return out;
+}
+
+std::vector<TokenResult> Engine::decode_device(const float* d_wav, const std::vector<long>& wav_off,
+                                               const std::vector<long>& n, int beam,
+                                               hipStream_t st) {
+  return decode_device_batches(d_wav, wav_off, n, {(int)n.size()}, beam, st);
+}
+
+std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
+                                                       const std::vector<long>& wav_off,
+                                                       const std::vector<long>& n,
+                                                       const std::vector<int>& batch_sizes,
+                                                       int beam, hipStream_t st) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  long total = 0;
+  for (int c : batch_sizes) {
+    ZASR_REQUIRE(c >= 0, "negative batch size");
+    total += c;
+  }
+  ZASR_REQUIRE(total == (long)n.size() && wav_off.size() == n.size(),
+               "batch sizes must sum to the chunk count");
+  st_ = st ? st : stream_;
+  std::vector<TokenResult> out;
+  out.reserve(n.size());
+  // batch k's encoder is enqueued (slot k % 2) before batch k-1's search runs, so the GPU
+  // overlaps them; batch k+1 reuses slot (k-1) % 2 only after batch k-1's search returned
+  Pending pd[2];
+  long first = 0;
+  const int nb = (int)batch_sizes.size();
+  for (int k = 0; k <= nb; ++k) {
+    if (k < nb) {
+      const int c = batch_sizes[k];
+      std::vector<long> o(wav_off.begin() + first, wav_off.begin() + first + c);
+      std::vector<long> l(n.begin() + first, n.begin() + first + c);
+      encode_stage(d_wav, o, l, k & 1, pd[k & 1]);
+      first += c;
+    }
+    if (k > 0) {
+      std::vector<TokenResult> r = search_stage(pd[(k - 1) & 1], beam);
+      for (auto& x : r) out.push_back(std::move(x));
+    }
+  }
   st_ = stream_;
   return out;
 }
@@ -1473,6 +1518,7 @@ std::vector<TokenResult> Engine::decode_features(const std::vector<const float*>
                                                  const std::vector<long>& frames, int beam) {
   ZASR_HIP_CHECK(hipSetDevice(device_));
   st_ = stream_;
+  pin_reset(0);
   const int B = (int)feats.size();
   std::vector<int> valid, T;
   long tot = 0, tot_out = 0;
@@ -1503,6 +1549,7 @@ std::vector<TokenResult> Engine::decode_features(const std::vector<const float*>
 void Engine::fbank_host(const float* wav, long n, float* out) {
   ZASR_HIP_CHECK(hipSetDevice(device_));
   st_ = stream_;
+  pin_reset(0);
   const long frames = n > 0 ? (n + 80) / 160 : 0;
   if (frames == 0) return;
   float* dw = ws<float>("fbh_wav", n);
@@ -1518,6 +1565,7 @@ void Engine::encode_host(const std::vector<const float*>& feats, const std::vect
                          std::vector<float>& out, std::vector<int>& t_out) {
   ZASR_HIP_CHECK(hipSetDevice(device_));
   st_ = stream_;
+  pin_reset(0);
   const int B = (int)feats.size();
   std::vector<int> T(B);
   long tot = 0, tot_out = 0;
@@ -1545,6 +1593,7 @@ std::vector<TokenResult> Engine::search_host(const std::vector<const float*>& en
                                              const std::vector<long>& t_out, int beam) {
   ZASR_HIP_CHECK(hipSetDevice(device_));
   st_ = stream_;
+  pin_reset(0);
   const int B = (int)enc.size();
   const int D = model_.cfg.joiner_dim;
   long tot = 0;

@@ -100,6 +100,14 @@ class Engine {
   // full path from device waveforms (packed); results in chunk order
   std::vector<TokenResult> decode_device(const float* d_wav, const std::vector<long>& wav_off,
                                          const std::vector<long>& n, int beam, hipStream_t st);
+  // several batches back to back (results in chunk order, batch_sizes[i] chunks per batch):
+  // batch k+1's fbank + encoder run on the call's stream while batch k's search runs on the
+  // engine's high-priority search stream -- the search loop is latency-bound on few CUs, so
+  // the encoder of the next batch fills the rest of the chip
+  std::vector<TokenResult> decode_device_batches(const float* d_wav, const std::vector<long>& wav_off,
+                                                 const std::vector<long>& n,
+                                                 const std::vector<int>& batch_sizes, int beam,
+                                                 hipStream_t st);
   std::vector<TokenResult> decode_features(const std::vector<const float*>& feats,
                                            const std::vector<long>& frames, int beam);
   void fbank_host(const float* wav, long n, float* out);
@@ -123,6 +131,26 @@ class Engine {
   template <class T>
   T* ws(const std::string& name, size_t count);
   void upload(void* dst, const void* src, size_t bytes);
+
+  // a batch whose encoder output is enqueued (enc_out slot `slot`), waiting for its search
+  struct Pending {
+    int B = 0;
+    std::vector<int> valid, t_out;
+    float* enc = nullptr;
+    hipEvent_t ready = nullptr;
+  };
+  void encode_stage(const float* d_wav, const std::vector<long>& wav_off, const std::vector<long>& n,
+                    int slot, Pending& p);
+  std::vector<TokenResult> search_stage(Pending& p, int beam);
+  // pinned staging for host->device metadata uploads: one arena per pipeline slot (0, 1)
+  // plus one for the search (2), so an upload never waits for the stream to drain
+  struct PinArena {
+    char* p = nullptr;
+    size_t cap = 0, used = 0, want = 0;
+  };
+  PinArena pin_[3];
+  int pin_cur_ = 0;
+  void pin_reset(int arena);
 
   // pipeline stages (all on st_)
   void run_fbank(const float* d_wav, const std::vector<long>& wav_off, const std::vector<long>& n,
@@ -162,7 +190,7 @@ class Engine {
   [[maybe_unused]] bool greedy_ = false;
   int precision_ = 0;
   hipStream_t stream_ = nullptr;
-  hipStream_t stream2_ = nullptr;  // searches of a pipelined decode (decode_device)
+  hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
   hipEvent_t part_ev_[3] = {nullptr, nullptr, nullptr};
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;

@@ -18,7 +18,7 @@ DEFAULT_LIB = os.path.join(_PKG, "lib", "libzasr.so")
 # every symbol declared in include/zasr.h (the CPU test checks the .so exports them all)
 EXPORTS = (
     "zasr_create", "zasr_destroy", "zasr_fbank", "zasr_decode_batch", "zasr_decode_features",
-    "zasr_decode_device", "zasr_encode_features", "zasr_search_encoder_out",
+    "zasr_decode_device", "zasr_decode_device_batches", "zasr_encode_features", "zasr_search_encoder_out",
     "zasr_result_count", "zasr_result_num_tokens", "zasr_result_num_frames",
     "zasr_result_tokens", "zasr_result_frames", "zasr_result_log_probs",
     "zasr_result_token_stats", "zasr_result_free", "zasr_vocab_size", "zasr_joiner_dim",
@@ -74,6 +74,9 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_decode_device.argtypes = [P, P, C.POINTER(I64), C.POINTER(I64), I32, I32, P,
                                        C.POINTER(P)]
     lib.zasr_decode_device.restype = C.c_int
+    lib.zasr_decode_device_batches.argtypes = [P, P, C.POINTER(I64), C.POINTER(I64), I32,
+                                               C.POINTER(I32), I32, I32, P, C.POINTER(P)]
+    lib.zasr_decode_device_batches.restype = C.c_int
     lib.zasr_encode_features.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, fp, I64,
                                          C.POINTER(I64)]
     lib.zasr_encode_features.restype = C.c_int
@@ -236,6 +239,21 @@ class Recognizer:
         res = C.c_void_p()
         self._check(self.lib.zasr_decode_device(self.handle, C.c_void_p(d_wav_ptr), off, ln, n,
                                                 beam, C.c_void_p(stream), C.byref(res)))
+        return self._collect(res)
+
+    def decode_device_batches(self, d_wav_ptr: int, offsets: Sequence[int],
+                              lengths: Sequence[int], batch_sizes: Sequence[int],
+                              beam: int = 0, stream: int = 0) -> List[SearchResult]:
+        """Consecutive batches (batch_sizes[i] chunks each) decoded with batch k+1's encoder
+        overlapping batch k's search; results for every chunk, in chunk order."""
+        n = len(lengths)
+        off = (C.c_int64 * n)(*offsets)
+        ln = (C.c_int64 * n)(*lengths)
+        bs = (C.c_int32 * len(batch_sizes))(*batch_sizes)
+        res = C.c_void_p()
+        self._check(self.lib.zasr_decode_device_batches(
+            self.handle, C.c_void_p(d_wav_ptr), off, ln, n, bs, len(batch_sizes), beam,
+            C.c_void_p(stream), C.byref(res)))
         return self._collect(res)
 
     def encode_features(self, feats: Sequence) -> List[np.ndarray]:

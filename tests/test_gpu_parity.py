@@ -335,3 +335,38 @@ def test_rover_shared_fbank_equals_separate_decodes(need_gpu):
         assert d1 == d2
         assert [w["text"] for w in m1] == [w["text"] for w in m2]
         assert [w["start"] for w in m1] == [w["start"] for w in m2]
+
+
+@pytest.mark.parametrize("method,beam", [("greedy_search", 1), ("modified_beam_search", 4)])
+def test_pipelined_batches_equal_per_batch_decode(need_gpu, method, beam):
+    """zasr_decode_device_batches: batch k+1's encoder overlaps batch k's search on two
+    streams; every chunk's result must be bit-identical to decoding its batch alone
+    (batches of different sizes, an empty batch, short and empty chunks, a batch whose
+    chunks are all too short)."""
+    import torch
+    from model_fixtures import m_model
+    from zasr.binding import Recognizer
+    cfg, w, path = m_model()
+    rec = Recognizer(path, method, beam, precision="bf16")
+    secs = [[2.0, 7.5, 0.3], [], [21.0], [0.0, 0.004], [3.3, 1.1, 12.0, 5.0], [9.0]]
+    batches = [[_speech(s, 900 + 10 * i + j) if s > 0 else np.zeros(0, np.float32)
+                for j, s in enumerate(b)] for i, b in enumerate(secs)]
+    flat = [c for b in batches for c in b]
+    lens = [c.shape[0] for c in flat]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    d = torch.from_numpy(np.concatenate(flat)).cuda()
+    torch.cuda.synchronize()
+    piped = rec.decode_device_batches(d.data_ptr(), offs, lens, [len(b) for b in batches])
+    assert len(piped) == len(flat)
+    i = 0
+    for b in batches:
+        alone = rec.decode_device(d.data_ptr(), offs[i:i + len(b)], lens[i:i + len(b)]) if b else []
+        for a, p in zip(alone, piped[i:i + len(b)]):
+            assert a.T == p.T
+            assert a.token_ids.tolist() == p.token_ids.tolist()
+            assert a.frames.tolist() == p.frames.tolist()
+            np.testing.assert_array_equal(a.log_probs, p.log_probs)
+            np.testing.assert_array_equal(a.stats, p.stats)
+        i += len(b)
+    assert sum(r.token_ids.size for r in piped) > 20
+    rec.close()
