@@ -22,6 +22,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace zasr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -443,12 +445,75 @@ __global__ __launch_bounds__(256) void joiner_packed_kernel(JoinerPackedArgs j) 
   }
 }
 
+// Register-staged variant: no LDS.  Each wave streams its own J row tile and W column group
+// (1 KB coalesced fragment loads, 8 fragments of each in flight ahead of the MFMAs) -- twice
+// the L2 reads of the LDS-shared kernel, but a block needs no LDS and few VGPRs, so under the
+// batch pipeline it co-resides with the next batch's encoder GEMM blocks instead of waiting
+// for whole CUs to drain (the LDS kernel's 128 KB per block fits only on an empty CU).
+// Same fragments, same MFMA order: bit-identical logits.
+template <int QK>
+__global__ __launch_bounds__(256) void joiner_reg_kernel(JoinerPackedArgs j) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.y * 64;
+  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M) &&
+      (m0 + 32 >= j.M || tile_done(j.live_t, j.live_len, j.live_f, m0 + 32, j.M)))
+    return;  // block-uniform: every stream of these 64 rows has finished
+  const int rt = wid >> 1, gc = wid & 1;
+  const int row0 = m0 + 32 * rt;
+  const int g = blockIdx.x * 2 + gc;
+  if (row0 >= j.M || g * 32 >= j.V) return;
+  const bf16x8* srcJ = reinterpret_cast<const bf16x8*>(j.Jp) + (long)(row0 >> 5) * QK * 64 + lane;
+  const bf16x8* srcW = reinterpret_cast<const bf16x8*>(j.Wp) + (long)g * QK * 64 + lane;
+  constexpr int CH = 8;
+  constexpr int NCH = QK / CH;
+  bf16x8 a[2][CH], b[2][CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    a[0][c] = srcJ[c * 64];
+    b[0][c] = srcW[c * 64];
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int h = 0; h < NCH; ++h) {
+    const int cur = h & 1;
+    if (h + 1 < NCH) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        a[cur ^ 1][c] = srcJ[((h + 1) * CH + c) * 64];
+        b[cur ^ 1][c] = srcW[((h + 1) * CH + c) * 64];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cur][c], b[cur][c], acc, 0, 0, 0);
+  }
+  const int col = g * 32 + (lane & 31);
+  if (col >= j.V) return;
+  const float bb = j.bias[col];
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    if (row < j.M) j.out[(long)row * j.V + col] = acc[r] + bb;
+  }
+}
+
 void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st) {
   if (j.M <= 0) return;
   dim3 grid(cdiv(j.V, 64), cdiv(j.M, 64));
+  // ZASR_JOINER_LDS=1: the LDS-shared kernel (lowest latency on an idle GPU)
+  static const bool lds = getenv("ZASR_JOINER_LDS") != nullptr && atoi(getenv("ZASR_JOINER_LDS")) != 0;
   switch (j.D) {
-    case 256: hipLaunchKernelGGL(joiner_packed_kernel<16>, grid, dim3(256), 0, st, j); break;
-    case 512: hipLaunchKernelGGL(joiner_packed_kernel<32>, grid, dim3(256), 0, st, j); break;
+    case 256:
+      if (lds) hipLaunchKernelGGL(joiner_packed_kernel<16>, grid, dim3(256), 0, st, j);
+      else hipLaunchKernelGGL(joiner_reg_kernel<16>, grid, dim3(256), 0, st, j);
+      break;
+    case 512:
+      if (lds) hipLaunchKernelGGL(joiner_packed_kernel<32>, grid, dim3(256), 0, st, j);
+      else hipLaunchKernelGGL(joiner_reg_kernel<32>, grid, dim3(256), 0, st, j);
+      break;
     default: throw std::runtime_error("packed joiner: joiner dim must be 256 or 512");
   }
 }
