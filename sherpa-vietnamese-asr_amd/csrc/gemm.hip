@@ -573,6 +573,30 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   if ((EPI == EPI_MULAUX || EPI == EPI_MULAUX16) && BN == 32 && p.N > 64) BN = 64;
   long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
   bool big = blocks128 >= 512;
+  // wide tiles: 128 x 256 on 8 waves (2 x 4, 64 x 64 each) for N >= 256 -- twice the MFMAs
+  // per A slab and per barrier of the 128 x 128 kernel, each A row panel read by half as many
+  // blocks; measured -5 % enc_gemm time at the bench's shapes (profiles/r01/v15_gemm_tiles.txt).
+  // ZASR_GEMM_TILE: 0 = 128 x 128 only, 1 = 256 x 128 (8 waves), 2 = 128 x 256 (default),
+  // 3 = 256 x 256, 4 = 128 x 256 for N >= 512 else 256 x 128
+  static const int tile_mode = getenv("ZASR_GEMM_TILE") ? atoi(getenv("ZASR_GEMM_TILE")) : 2;
+  if (BN == 128 && big && tile_mode == 1 && blocks128 >= 1024) {
+    launch_h<256, 128, BK, 4, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+    return;
+  }
+  if (BN == 128 && big && tile_mode == 3 && p.N >= 256 && blocks128 >= 1024) {
+    launch_h<256, 256, BK, 2, 4, ALOAD, EPI, TA, TC>(p, Bw, st);
+    return;
+  }
+  if (BN == 128 && big && tile_mode == 4) {
+    if (p.N >= 512) launch_h<128, 256, BK, 2, 4, ALOAD, EPI, TA, TC>(p, Bw, st);
+    else if (blocks128 >= 1024) launch_h<256, 128, BK, 4, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+    else launch_h<128, 128, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+    return;
+  }
+  if (BN == 128 && big && tile_mode == 2 && p.N >= 256) {
+    launch_h<128, 256, BK, 2, 4, ALOAD, EPI, TA, TC>(p, Bw, st);
+    return;
+  }
   if (BN == 128) {
     if (big) launch_h<128, 128, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
     else launch_h<64, 128, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
