@@ -211,7 +211,7 @@ ModelConfig parse_config(const std::string& text) {
 template <class T>
 T* Engine::ws(const std::string& name, size_t count) {
   size_t bytes = std::max<size_t>(count * sizeof(T), 256);
-  Buf& b = ws_[name];
+  Buf& b = ws_tag_.empty() ? ws_[name] : ws_[ws_tag_ + name];
   if (b.bytes < bytes) {
     if (b.p) {
       ZASR_HIP_CHECK(hipStreamSynchronize(st_));
@@ -267,6 +267,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
     ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
   }
+  ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream3_, hipStreamNonBlocking));
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   st_ = stream_;
   const std::string cfg_path = dir + "/config.json";
@@ -589,6 +590,8 @@ Engine::~Engine() {
     if (a.p) (void)hipHostFree(a.p);
   for (auto e : part_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(stream2_);
+  (void)hipStreamSynchronize(stream3_);
+  (void)hipStreamDestroy(stream3_);
   (void)hipStreamDestroy(stream_);
 }
 
@@ -596,6 +599,8 @@ Engine::~Engine() {
 // table[x + pmax - 1][n] = sum_c W_pos[n][c] * pe(x)[c]
 void Engine::ensure_pos_tables(int need) {
   if (need <= model_.pmax) return;
+  // the tables are shared by every encoder stream: replace them only on an idle device
+  ZASR_HIP_CHECK(hipDeviceSynchronize());
   int pmax = 1024;
   while (pmax < need) pmax *= 2;
   const int P = model_.cfg.pos_dim;
@@ -1413,12 +1418,15 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
 // public entry points
 // ------------------------------------------------------------------------------------
 void Engine::encode_stage(const float* d_wav, const std::vector<long>& wav_off,
-                          const std::vector<long>& n, int slot, Pending& pd) {
-  pin_reset(slot);
+                          const std::vector<long>& n, int out_slot, int ws_slot,
+                          hipStream_t stream, Pending& pd) {
+  st_ = stream;
+  pin_reset(out_slot);
+  ws_tag_ = ws_slot ? "w1/" : "";
   const int B = (int)n.size();
   pd = Pending{};
   pd.B = B;
-  pd.ready = part_ev_[slot];
+  pd.ready = part_ev_[out_slot];
   std::vector<int> frames;
   long total_frames = 0;
   for (int b = 0; b < B; ++b) total_frames += n[b] > 0 ? (n[b] + 80) / 160 : 0;
@@ -1433,7 +1441,10 @@ void Engine::encode_stage(const float* d_wav, const std::vector<long>& wav_off,
       pd.valid.push_back(b);
       T.push_back(frames[b]);
     }
-  if (pd.valid.empty()) return;
+  if (pd.valid.empty()) {
+    ws_tag_.clear();
+    return;
+  }
   const float* fptr = feats;
   if ((int)pd.valid.size() != B) {  // compact valid chunks' features
     float* cf = ws<float>("feats_compact", (size_t)total_frames * 80);
@@ -1448,10 +1459,11 @@ void Engine::encode_stage(const float* d_wav, const std::vector<long>& wav_off,
   long tot_out = 0;
   for (int t : T) tot_out += ((t - 7) / 2 + 1) / 2;
   // the encoder output is the only buffer the search reads: one per pipeline slot
-  pd.enc = ws<float>(slot ? "enc_out1" : "enc_out0",
+  pd.enc = ws<float>("enc_out" + std::to_string(out_slot),
                      (size_t)std::max<long>(tot_out, 1) * model_.cfg.joiner_dim);
   run_encoder(fptr, T, pd.enc, pd.t_out);
   ZASR_HIP_CHECK(hipEventRecord(pd.ready, st_));
+  ws_tag_.clear();
 }
 
 std::vector<TokenResult> Engine::search_stage(Pending& pd, int beam) {
@@ -1459,13 +1471,13 @@ std::vector<TokenResult> Engine::search_stage(Pending& pd, int beam) {
   if (pd.valid.empty()) return out;
   hipStream_t main_st = st_;
   st_ = stream2_;
-  pin_reset(2);
+  pin_reset(3);
   ZASR_HIP_CHECK(hipStreamWaitEvent(stream2_, pd.ready, 0));
   std::vector<TokenResult> r = run_search(pd.enc, pd.t_out, beam);
   for (size_t i = 0; i < pd.valid.size(); ++i) out[pd.valid[i]] = std::move(r[i]);
   // the call's stream sees the search complete (its results are already on the host)
-  ZASR_HIP_CHECK(hipEventRecord(part_ev_[2], stream2_));
-  ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[2], 0));
+  ZASR_HIP_CHECK(hipEventRecord(part_ev_[3], stream2_));
+  ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[3], 0));
   st_ = main_st;
   return out;
 }
@@ -1489,26 +1501,38 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   }
   ZASR_REQUIRE(total == (long)n.size() && wav_off.size() == n.size(),
                "batch sizes must sum to the chunk count");
-  st_ = st ? st : stream_;
+  hipStream_t main_st = st ? st : stream_;
+  st_ = main_st;
   std::vector<TokenResult> out;
   out.reserve(n.size());
-  // batch k's encoder is enqueued (slot k % 2) before batch k-1's search runs, so the GPU
-  // overlaps them; batch k+1 reuses slot (k-1) % 2 only after batch k-1's search returned
-  Pending pd[2];
-  long first = 0;
+  // E encoder streams; L = E batches' encoders are enqueued ahead of the search in flight.
+  // Batch k: encoder output / event / pinned arena slot k % (L + 1), stream + workspace set
+  // k % E.  When batch k + L is enqueued, the previous user of its output slot (batch k - 1)
+  // has been searched (the search returns on the host), and its stream's previous batch
+  // (k + L - E) is ordered before it on the same stream.
+  static const int env_e = getenv("ZASR_ENC_STREAMS") ? atoi(getenv("ZASR_ENC_STREAMS")) : 2;
   const int nb = (int)batch_sizes.size();
-  for (int k = 0; k <= nb; ++k) {
-    if (k < nb) {
-      const int c = batch_sizes[k];
-      std::vector<long> o(wav_off.begin() + first, wav_off.begin() + first + c);
-      std::vector<long> l(n.begin() + first, n.begin() + first + c);
-      encode_stage(d_wav, o, l, k & 1, pd[k & 1]);
-      first += c;
-    }
-    if (k > 0) {
-      std::vector<TokenResult> r = search_stage(pd[(k - 1) & 1], beam);
-      for (auto& x : r) out.push_back(std::move(x));
-    }
+  const int E = (env_e == 1 || nb < 3) ? 1 : 2;
+  const int L = E;
+  hipStream_t enc_st[2] = {main_st, stream3_};
+  if (E == 2) {  // the second encoder stream starts after the caller's prior work
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[4], main_st));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(stream3_, part_ev_[4], 0));
+  }
+  std::vector<long> first(nb + 1, 0);
+  for (int k = 0; k < nb; ++k) first[k + 1] = first[k] + batch_sizes[k];
+  Pending pd[3];
+  auto enqueue = [&](int k) {
+    std::vector<long> o(wav_off.begin() + first[k], wav_off.begin() + first[k + 1]);
+    std::vector<long> l(n.begin() + first[k], n.begin() + first[k + 1]);
+    encode_stage(d_wav, o, l, k % (L + 1), k % E, enc_st[k % E], pd[k % (L + 1)]);
+    st_ = main_st;
+  };
+  for (int k = 0; k < std::min(L, nb); ++k) enqueue(k);
+  for (int k = 0; k < nb; ++k) {
+    if (k + L < nb) enqueue(k + L);
+    std::vector<TokenResult> r = search_stage(pd[k % (L + 1)], beam);
+    for (auto& x : r) out.push_back(std::move(x));
   }
   st_ = stream_;
   return out;

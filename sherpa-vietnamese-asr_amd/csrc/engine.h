@@ -139,16 +139,19 @@ class Engine {
     float* enc = nullptr;
     hipEvent_t ready = nullptr;
   };
+  // out_slot: encoder output buffer, completion event and pinned arena (0..2); ws_slot:
+  // encoder workspace set (0, 1) -- two batches' encoders may run at once on two streams
   void encode_stage(const float* d_wav, const std::vector<long>& wav_off, const std::vector<long>& n,
-                    int slot, Pending& p);
+                    int out_slot, int ws_slot, hipStream_t stream, Pending& p);
   std::vector<TokenResult> search_stage(Pending& p, int beam);
-  // pinned staging for host->device metadata uploads: one arena per pipeline slot (0, 1)
-  // plus one for the search (2), so an upload never waits for the stream to drain
+  // pinned staging for host->device metadata uploads: one arena per encoder output slot
+  // (0..2) plus one for the search (3), so an upload never waits for the stream to drain
   struct PinArena {
     char* p = nullptr;
     size_t cap = 0, used = 0, want = 0;
   };
-  PinArena pin_[3];
+  PinArena pin_[4];
+  std::string ws_tag_;  // workspace-name prefix of the encoder workspace set in use
   int pin_cur_ = 0;
   void pin_reset(int arena);
 
@@ -191,7 +194,9 @@ class Engine {
   int precision_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
-  hipEvent_t part_ev_[3] = {nullptr, nullptr, nullptr};
+  hipStream_t stream3_ = nullptr;  // second encoder stream of the batch pipeline
+  hipEvent_t part_ev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // 0..2 encoder
+                                                                           // outputs, 3 search, 4 start
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;
   // fbank tables
