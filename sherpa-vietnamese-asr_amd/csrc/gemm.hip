@@ -577,14 +577,12 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   // per A slab and per barrier of the 128 x 128 kernel, each A row panel read by half as many
   // blocks; measured -5 % enc_gemm time at the bench's shapes (profiles/r01/v15_gemm_tiles.txt).
   // ZASR_GEMM_TILE: 0 = 128 x 128 only, 1 = 256 x 128 (8 waves), 2 = 128 x 256 (default),
-  // 3 = 256 x 256, 4 = 128 x 256 for N >= 512 else 256 x 128
+  // 4 = 128 x 256 for N >= 512 else 256 x 128 (256 x 256 measured 7 % slower: removed).
+  // A two-slab register prefetch (two K slabs in flight in two register sets behind the LDS
+  // slab) measured enc_gemm 16.7 -> 21.1 ms per step and was dropped (v17)
   static const int tile_mode = getenv("ZASR_GEMM_TILE") ? atoi(getenv("ZASR_GEMM_TILE")) : 2;
   if (BN == 128 && big && tile_mode == 1 && blocks128 >= 1024) {
     launch_h<256, 128, BK, 4, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
-    return;
-  }
-  if (BN == 128 && big && tile_mode == 3 && p.N >= 256 && blocks128 >= 1024) {
-    launch_h<256, 256, BK, 2, 4, ALOAD, EPI, TA, TC>(p, Bw, st);
     return;
   }
   if (BN == 128 && big && tile_mode == 4) {
