@@ -169,6 +169,9 @@ def main():
     ap.add_argument("--audio-sec", type=float, default=3600.0)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hotwords", type=int, default=0,
+                    help="N synthetic hotwords (2-4 tokens each, score 1.5 as the reference's "
+                         "hotwords_score default, core/asr_engine.py:1000); beam search only")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="steps as separate decode_device calls (no cross-batch overlap)")
     ap.add_argument("--profile-out", default="")
@@ -192,7 +195,13 @@ def main():
     mdir = os.path.join(tempfile.gettempdir(), f"zasr_bench_{args.model}_{os.getpid()}")
     save_model_dir(mdir, cfg, weights, synth_tokens(cfg.vocab_size))
     beam = 1 if args.method == "greedy_search" else args.beam
-    rec = Recognizer(mdir, args.method, beam, device_id=local, precision=args.precision)
+    hotwords = None
+    if args.hotwords:
+        hr = np.random.default_rng(20261016)
+        hotwords = [hr.integers(1, cfg.vocab_size, size=int(hr.integers(2, 5))).tolist()
+                    for _ in range(args.hotwords)]
+    rec = Recognizer(mdir, args.method, beam, hotwords=hotwords, device_id=local,
+                     precision=args.precision)
 
     # per-rank shard: the same hour of synthetic audio, seeded by rank
     chunks = make_chunks(args.audio_sec, 20261015 + rank)
@@ -317,7 +326,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded 16 kHz speech-like audio, random-init Zipformer weights)",
             "config": {"workload": f"{args.model} {args.method}"
-                                   f"{'' if beam == 1 else ' beam %d' % beam}, batched VAD-style chunks",
+                                   f"{'' if beam == 1 else ' beam %d' % beam}"
+                                   f"{' + %d hotwords' % args.hotwords if args.hotwords else ''}"
+                                   ", batched VAD-style chunks",
                        "model": args.model, "chunks_per_gpu": len(chunks),
                        "audio_sec_per_gpu": audio_sec_rank,
                        "decoded_sec_per_gpu_incl_overlap": round(decoded_sec_rank, 1),
