@@ -665,6 +665,16 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       upd(xa[q].w);
     }
     if (h == 0 && m1 != 12345.f) ZASR_STAMP(7);
+    // insertion threshold: split the wave into KB lane groups and take the smallest group
+    // maximum.  Every group holds an element at least that large, so the row's top KB are
+    // all >= it, and the scores are monotone in x: elements below it are never inserted
+    // (exact; the wave runs the insertion network only where some lane passes it).  Six
+    // shuffles (KB-th largest lane maximum by rounds: measured 2.5k cycles, too slow).
+    float thr_x = m1;
+#pragma unroll
+    for (int o = 1; o < 64 / KB; o <<= 1) thr_x = fmaxf(thr_x, __shfl_xor(thr_x, o, 64));
+#pragma unroll
+    for (int o = 64 / KB; o < 64; o <<= 1) thr_x = fminf(thr_x, __shfl_xor(thr_x, o, 64));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
@@ -697,11 +707,15 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
                               __expf(m2 - m1) / se);
     const float lf = (float)ld;
-    auto ins = [&](float x, int idx) {
+    auto score = [&](float x) {
       const float lpv = (x - m1) - ls;
-      const float val = f64 ? (float)((double)lpv + ld) : lpv + lf;
+      return f64 ? (float)((double)lpv + ld) : lpv + lf;
+    };
+    const float thr_val = score(thr_x);
+    auto ins = [&](float x, int idx) {
+      const float val = score(x);
       const unsigned long long key = make_key(val, idx);
-      if (key > tk[KB - 1]) {
+      if (val >= thr_val && key > tk[KB - 1]) {
 #pragma unroll
         for (int q = KB - 1; q > 0; --q) tk[q] = key > tk[q - 1] ? tk[q - 1] : (key > tk[q] ? key : tk[q]);
         tk[0] = key > tk[0] ? key : tk[0];
