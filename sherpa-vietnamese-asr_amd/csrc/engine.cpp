@@ -1510,9 +1510,13 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   // k % E.  When batch k + L is enqueued, the previous user of its output slot (batch k - 1)
   // has been searched (the search returns on the host), and its stream's previous batch
   // (k + L - E) is ordered before it on the same stream.
-  static const int env_e = getenv("ZASR_ENC_STREAMS") ? atoi(getenv("ZASR_ENC_STREAMS")) : 2;
+  // Greedy: the encoder is the critical path, a second encoder stream fills its kernel tails
+  // (98.4k vs 95.3k xRT).  Beam search: the search is the critical path and a second encoder
+  // stream only adds contention for it (69.9k vs 68.3k xRT at beam 8 + 20 hotwords).
+  static const int env_e = getenv("ZASR_ENC_STREAMS") ? atoi(getenv("ZASR_ENC_STREAMS")) : 0;
   const int nb = (int)batch_sizes.size();
-  const int E = (env_e == 1 || nb < 3) ? 1 : 2;
+  const int want_e = env_e ? env_e : (beam > 1 ? 1 : 2);
+  const int E = (want_e == 1 || nb < 3) ? 1 : 2;
   const int L = E;
   hipStream_t enc_st[2] = {main_st, stream3_};
   if (E == 2) {  // the second encoder stream starts after the caller's prior work
