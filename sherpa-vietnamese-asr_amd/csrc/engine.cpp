@@ -267,7 +267,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
     ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
   }
-  ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream3_, hipStreamNonBlocking));
+  for (auto& x : enc_extra_) ZASR_HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   st_ = stream_;
   const std::string cfg_path = dir + "/config.json";
@@ -590,8 +590,10 @@ Engine::~Engine() {
     if (a.p) (void)hipHostFree(a.p);
   for (auto e : part_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(stream2_);
-  (void)hipStreamSynchronize(stream3_);
-  (void)hipStreamDestroy(stream3_);
+  for (auto x : enc_extra_) {
+    (void)hipStreamSynchronize(x);
+    (void)hipStreamDestroy(x);
+  }
   (void)hipStreamDestroy(stream_);
 }
 
@@ -1422,7 +1424,7 @@ void Engine::encode_stage(const float* d_wav, const std::vector<long>& wav_off,
                           hipStream_t stream, Pending& pd) {
   st_ = stream;
   pin_reset(out_slot);
-  ws_tag_ = ws_slot ? "w1/" : "";
+  ws_tag_ = ws_slot ? "w" + std::to_string(ws_slot) + "/" : "";
   const int B = (int)n.size();
   pd = Pending{};
   pd.B = B;
@@ -1471,13 +1473,13 @@ std::vector<TokenResult> Engine::search_stage(Pending& pd, int beam) {
   if (pd.valid.empty()) return out;
   hipStream_t main_st = st_;
   st_ = stream2_;
-  pin_reset(3);
+  pin_reset(kMaxEnc + 1);
   ZASR_HIP_CHECK(hipStreamWaitEvent(stream2_, pd.ready, 0));
   std::vector<TokenResult> r = run_search(pd.enc, pd.t_out, beam);
   for (size_t i = 0; i < pd.valid.size(); ++i) out[pd.valid[i]] = std::move(r[i]);
   // the call's stream sees the search complete (its results are already on the host)
-  ZASR_HIP_CHECK(hipEventRecord(part_ev_[3], stream2_));
-  ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[3], 0));
+  ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 1], stream2_));
+  ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[kMaxEnc + 1], 0));
   st_ = main_st;
   return out;
 }
@@ -1516,16 +1518,17 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   static const int env_e = getenv("ZASR_ENC_STREAMS") ? atoi(getenv("ZASR_ENC_STREAMS")) : 0;
   const int nb = (int)batch_sizes.size();
   const int want_e = env_e ? env_e : (beam > 1 ? 1 : 2);
-  const int E = (want_e == 1 || nb < 3) ? 1 : 2;
+  const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
   const int L = E;
-  hipStream_t enc_st[2] = {main_st, stream3_};
-  if (E == 2) {  // the second encoder stream starts after the caller's prior work
-    ZASR_HIP_CHECK(hipEventRecord(part_ev_[4], main_st));
-    ZASR_HIP_CHECK(hipStreamWaitEvent(stream3_, part_ev_[4], 0));
+  hipStream_t enc_st[kMaxEnc] = {main_st};
+  for (int e = 1; e < kMaxEnc; ++e) enc_st[e] = enc_extra_[e - 1];
+  if (E > 1) {  // the other encoder streams start after the caller's prior work
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 2], main_st));
+    for (int e = 1; e < E; ++e) ZASR_HIP_CHECK(hipStreamWaitEvent(enc_st[e], part_ev_[kMaxEnc + 2], 0));
   }
   std::vector<long> first(nb + 1, 0);
   for (int k = 0; k < nb; ++k) first[k + 1] = first[k] + batch_sizes[k];
-  Pending pd[3];
+  Pending pd[kMaxEnc + 1];
   auto enqueue = [&](int k) {
     std::vector<long> o(wav_off.begin() + first[k], wav_off.begin() + first[k + 1]);
     std::vector<long> l(n.begin() + first[k], n.begin() + first[k + 1]);

@@ -139,18 +139,20 @@ class Engine {
     float* enc = nullptr;
     hipEvent_t ready = nullptr;
   };
-  // out_slot: encoder output buffer, completion event and pinned arena (0..2); ws_slot:
-  // encoder workspace set (0, 1) -- two batches' encoders may run at once on two streams
+  // out_slot: encoder output buffer, completion event and pinned arena (0..kMaxEnc);
+  // ws_slot: encoder workspace set (0..kMaxEnc-1) -- several batches' encoders may run at
+  // once on separate streams
   void encode_stage(const float* d_wav, const std::vector<long>& wav_off, const std::vector<long>& n,
                     int out_slot, int ws_slot, hipStream_t stream, Pending& p);
   std::vector<TokenResult> search_stage(Pending& p, int beam);
   // pinned staging for host->device metadata uploads: one arena per encoder output slot
-  // (0..2) plus one for the search (3), so an upload never waits for the stream to drain
+  // plus one for the search, so an upload never waits for the stream to drain
   struct PinArena {
     char* p = nullptr;
     size_t cap = 0, used = 0, want = 0;
   };
-  PinArena pin_[4];
+  static constexpr int kMaxEnc = 3;  // encoder streams of the batch pipeline
+  PinArena pin_[kMaxEnc + 2];       // kMaxEnc + 1 output slots, then the search's
   std::string ws_tag_;  // workspace-name prefix of the encoder workspace set in use
   int pin_cur_ = 0;
   void pin_reset(int arena);
@@ -194,9 +196,9 @@ class Engine {
   int precision_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
-  hipStream_t stream3_ = nullptr;  // second encoder stream of the batch pipeline
-  hipEvent_t part_ev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // 0..2 encoder
-                                                                           // outputs, 3 search, 4 start
+  hipStream_t enc_extra_[kMaxEnc - 1] = {};  // encoder streams 1.. of the batch pipeline
+  // [0, kMaxEnc]: encoder output slots; kMaxEnc + 1: search done; kMaxEnc + 2: start
+  hipEvent_t part_ev_[kMaxEnc + 3] = {};
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;
   // fbank tables
