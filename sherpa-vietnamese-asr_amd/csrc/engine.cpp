@@ -1388,15 +1388,22 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   if (stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
     std::vector<unsigned long long> h((size_t)Tmax * 16);
     ZASR_HIP_CHECK(hipMemcpy(h.data(), st.stamps, h.size() * 8, hipMemcpyDeviceToHost));
-    const int seq[] = {0, 6, 7, 8, 1, 2, 3, 4, 5};
-    const char* name[] = {"nh", "row0_loaded", "row0_stats", "rows_rest", "wave_topk", "barrier", "expand", "J"};
-    constexpr int NS = 8;
-    double acc[NS] = {0};
+    // beam >= 5 (a second row per wave): row 4's phases are stamped too
+    const bool two = H > 4;
+    const int seq2[] = {0, 6, 7, 8, 9, 10, 11, 1, 2, 3, 4, 5};
+    const int seq1[] = {0, 6, 7, 8, 1, 2, 3, 4, 5};
+    const char* name2[] = {"nh", "row0_loaded", "row0_stats", "row0_insert", "row4_loaded",
+                           "row4_stats", "row4_insert", "wave_topk", "barrier", "expand", "J"};
+    const char* name1[] = {"nh", "row0_loaded", "row0_stats", "rows_rest", "wave_topk", "barrier", "expand", "J"};
+    const int* seq = two ? seq2 : seq1;
+    const char* const* name = two ? name2 : name1;
+    const int NS = two ? 11 : 8;
+    double acc[16] = {0};
     int n = 0;
     for (int t = 0; t < Tmax; ++t) {
       const unsigned long long* p = &h[(size_t)t * 16];
       bool ok = true;
-      for (int k : seq) ok = ok && p[k] != 0;
+      for (int k = 0; k <= NS; ++k) ok = ok && p[seq[k]] != 0;
       if (!ok) continue;
       for (int k = 0; k < NS; ++k) acc[k] += (double)(p[seq[k + 1]] - p[seq[k]]);
       ++n;

@@ -139,6 +139,100 @@ __device__ __forceinline__ bool tile_done(const int* live_t, const int* live_len
   return true;
 }
 
+// ---- wave reductions on DPP + readlane (no LDS round trips) ----
+// The search kernels run one block per stream, one wave per SIMD: every cross-lane step is
+// exposed latency.  __shfl_xor lowers to ds_bpermute_b32 (an LDS round trip per step, six per
+// reduction); here a 16-lane row reduces in four DPP steps (quad_perm 1-0-3-2, 2-3-0-1,
+// row_ror 4, row_ror 8) and the four row results are combined as scalars via v_readlane.
+// Max / min / the (max, second max) merge are exact in any order.  The float sum is
+// deterministic (every lane gets the same value) but associates differently from a
+// butterfly: every search kernel uses this one function, so the frame-by-frame and the
+// speculative greedy kernels still agree bit for bit.
+constexpr int kDppQuad1 = 0xB1, kDppQuad2 = 0x4E, kDppRor4 = 0x124, kDppRor8 = 0x128;
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<kDppQuad1>(v);
+  v += dpp_f<kDppQuad2>(v);
+  v += dpp_f<kDppRor4>(v);
+  v += dpp_f<kDppRor8>(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+__device__ __forceinline__ float row_max_dpp(float v) {  // every lane: its 16-lane row's max
+  v = fmaxf(v, dpp_f<kDppQuad1>(v));
+  v = fmaxf(v, dpp_f<kDppQuad2>(v));
+  v = fmaxf(v, dpp_f<kDppRor4>(v));
+  return fmaxf(v, dpp_f<kDppRor8>(v));
+}
+__device__ __forceinline__ float wave_min_dpp(float v) {
+  v = fminf(v, dpp_f<kDppQuad1>(v));
+  v = fminf(v, dpp_f<kDppQuad2>(v));
+  v = fminf(v, dpp_f<kDppRor4>(v));
+  v = fminf(v, dpp_f<kDppRor8>(v));
+  return fminf(fminf(lane_f(v, 0), lane_f(v, 16)), fminf(lane_f(v, 32), lane_f(v, 48)));
+}
+// (max, second max) over the wave's (m1, m2) pairs
+template <int CTRL>
+__device__ __forceinline__ void max2_step(float& m1, float& m2, float a1, float a2) {
+  const float hi = fmaxf(m1, a1);
+  const float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
+  m1 = hi;
+  m2 = lo;
+}
+__device__ __forceinline__ void wave_max2_dpp(float& m1, float& m2) {
+  max2_step<0>(m1, m2, dpp_f<kDppQuad1>(m1), dpp_f<kDppQuad1>(m2));
+  max2_step<0>(m1, m2, dpp_f<kDppQuad2>(m1), dpp_f<kDppQuad2>(m2));
+  max2_step<0>(m1, m2, dpp_f<kDppRor4>(m1), dpp_f<kDppRor4>(m2));
+  max2_step<0>(m1, m2, dpp_f<kDppRor8>(m1), dpp_f<kDppRor8>(m2));
+  float r1 = lane_f(m1, 0), r2 = lane_f(m2, 0);
+#pragma unroll
+  for (int l = 16; l < 64; l += 16) max2_step<0>(r1, r2, lane_f(m1, l), lane_f(m2, l));
+  m1 = r1;
+  m2 = r2;
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const int lo = dpp_i<CTRL>((int)(unsigned)v), hi = dpp_i<CTRL>((int)(unsigned)(v >> 32));
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long lane_u64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64_dpp(unsigned long long v) {
+  unsigned long long o;
+  o = dpp_u64<kDppQuad1>(v); v = o > v ? o : v;
+  o = dpp_u64<kDppQuad2>(v); v = o > v ? o : v;
+  o = dpp_u64<kDppRor4>(v); v = o > v ? o : v;
+  o = dpp_u64<kDppRor8>(v); v = o > v ? o : v;
+  unsigned long long r = lane_u64(v, 0);
+#pragma unroll
+  for (int l = 16; l < 64; l += 16) {
+    const unsigned long long x = lane_u64(v, l);
+    r = x > r ? x : r;
+  }
+  return r;
+}
+__device__ __forceinline__ int wave_min_i_dpp(int v) {
+  v = min(v, dpp_i<kDppQuad1>(v));
+  v = min(v, dpp_i<kDppQuad2>(v));
+  v = min(v, dpp_i<kDppRor4>(v));
+  v = min(v, dpp_i<kDppRor8>(v));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
 // tanh(x) = 1 - 2 / (exp(2x) + 1): saturates correctly at +-inf (bf16 joiner input only)
 __device__ __forceinline__ float fast_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
 
@@ -609,6 +703,14 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       xa[q] = i < V4 ? rows4[(long)wid * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     }
   }
+  // the score of this wave's first row, in flight with its logits (slots >= nh hold stale
+  // but valid data and are never used); later rows' scores are prefetched one row ahead
+  double ld_cur = 0.0;
+  int lpf_cur = 0;
+  if (wid < Hmax) {
+    ld_cur = st.lp[base + wid];
+    lpf_cur = st.lpf[base + wid];
+  }
   const int n = st.nh[s];
   if (n != 12345) ZASR_STAMP(6);
   if (tid < n) {
@@ -643,15 +745,19 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   for (int q = 0; q < KB; ++q) tk[q] = 0ull;
   for (int h = wid; h < n; h += 4) {
     const bool more = h + 4 < n;
+    double ld_nx = 0.0;
+    int lpf_nx = 0;
     if (more) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int i = lane + 64 * q;
         xb[q] = i < V4 ? rows4[(long)(h + 4) * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
       }
+      ld_nx = st.lp[base + h + 4];
+      lpf_nx = st.lpf[base + h + 4];
     }
-    const double ld = st.lp[base + h];
-    const bool f64 = st.lpf[base + h] != 0;
+    const double ld = ld_cur;
+    const bool f64 = lpf_cur != 0;
     float m1 = -INFINITY, m2 = -INFINITY;
     auto upd = [&](float x) {  // branch-free (a branchy form put m1/m2 in scratch)
       m2 = fmaxf(m2, fminf(m1, x));
@@ -665,24 +771,21 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       upd(xa[q].w);
     }
     if (h == 0 && m1 != 12345.f) ZASR_STAMP(7);
+    if (h == 4 && m1 != 12345.f) ZASR_STAMP(10);
     // insertion threshold: split the wave into KB lane groups and take the smallest group
     // maximum.  Every group holds an element at least that large, so the row's top KB are
     // all >= it, and the scores are monotone in x: elements below it are never inserted
     // (exact; the wave runs the insertion network only where some lane passes it).  Six
     // shuffles (KB-th largest lane maximum by rounds: measured 2.5k cycles, too slow).
-    float thr_x = m1;
-#pragma unroll
-    for (int o = 1; o < 64 / KB; o <<= 1) thr_x = fmaxf(thr_x, __shfl_xor(thr_x, o, 64));
-#pragma unroll
-    for (int o = 64 / KB; o < 64; o <<= 1) thr_x = fminf(thr_x, __shfl_xor(thr_x, o, 64));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
-      const float hi = fmaxf(m1, a1);
-      const float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
-      m1 = hi;
-      m2 = lo;
-    }
+    // groups (DPP): KB >= 16: the 16 quads; KB = 8: overlapping quad pairs (q, q - 1), of
+    // which the 8 pairs (2i, 2i + 1) are disjoint, so the minimum over all of them is still
+    // a bound; KB <= 4: the four 16-lane rows
+    float thr_x = fmaxf(m1, dpp_f<kDppQuad1>(m1));
+    thr_x = fmaxf(thr_x, dpp_f<kDppQuad2>(thr_x));
+    if constexpr (KB <= 8) thr_x = fmaxf(thr_x, dpp_f<kDppRor4>(thr_x));
+    if constexpr (KB <= 4) thr_x = fmaxf(thr_x, dpp_f<kDppRor8>(thr_x));
+    thr_x = wave_min_dpp(thr_x);
+    wave_max2_dpp(m1, m2);
     float se = 0.f, e1 = 0.f, e3 = 0.f;
     auto acc = [&](float x) {
       const float d = x - m1;  // -inf past V -> e = 0
@@ -698,11 +801,12 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       acc(xa[q].z);
       acc(xa[q].w);
     }
-    se = wave_sum(se);
-    e1 = wave_sum(e1);
-    e3 = wave_sum(e3);
+    se = wave_sum_dpp(se);
+    e1 = wave_sum_dpp(e1);
+    e3 = wave_sum_dpp(e3);
     const float ls = logf(se);
     if (h == 0 && ls != 12345.f) ZASR_STAMP(8);
+    if (h == 4 && ls != 12345.f) ZASR_STAMP(11);
     if (lane == 0)
       sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
                               __expf(m2 - m1) / se);
@@ -732,20 +836,18 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
         ins(xa[q].w, b0 + 3);
       }
     }
+    if (h == 0 && tk[0] != 12345ull) ZASR_STAMP(9);
     if (more) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) xa[q] = xb[q];
+      ld_cur = ld_nx;
+      lpf_cur = lpf_nx;
     }
   }
   ZASR_STAMP(1);
   // per-wave top-KB
   for (int round = 0; round < KB; ++round) {
-    unsigned long long best = tk[0];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long ob = __shfl_xor(best, o, 64);
-      best = ob > best ? ob : best;
-    }
+    const unsigned long long best = wave_max_u64_dpp(tk[0]);
     if (lane == 0) cK[wid * KB + round] = best;
     if (best != 0ull && tk[0] == best) {
 #pragma unroll
@@ -1069,14 +1171,7 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
       m2 = fmaxf(m2, fminf(m1, v.z)); m1 = fmaxf(m1, v.z);
       m2 = fmaxf(m2, fminf(m1, v.w)); m1 = fmaxf(m1, v.w);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float a1 = __shfl_xor(m1, o, 64), a2 = __shfl_xor(m2, o, 64);
-      const float hi = fmaxf(m1, a1);
-      const float lo = fmaxf(fminf(m1, a1), fmaxf(m2, a2));
-      m1 = hi;
-      m2 = lo;
-    }
+    wave_max2_dpp(m1, m2);
     float se = 0.f;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -1085,7 +1180,7 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
       se += __expf(x[r][q].z - m1);
       se += __expf(x[r][q].w - m1);
     }
-    se = wave_sum(se);
+    se = wave_sum_dpp(se);
     const float ls = logf(se);
     m1r[r] = m1;
     m2r[r] = m2;
@@ -1128,12 +1223,7 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
                   : (((v.w - m1) - ls) + lf == vmax) ? i + 3 : 0x7fffffff;
       bq = c < bq ? c : bq;
     }
-    int best = bq;  // the smallest index of this lane reaching the top value
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const int ob = __shfl_xor(best, o, 64);
-      best = ob < best ? ob : best;
-    }
+    const int best = wave_min_i_dpp(bq);  // smallest index reaching the top value
     if (lane == 0) sTok[f] = best;
     // a non-blank top-1 may be the window's emission: fetch the decoder-table row of the
     // context it would create now, under the block-wide decision below
@@ -1185,8 +1275,8 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
           }
         }
       }
-      e1 = wave_sum(e1);
-      e3 = wave_sum(e3);
+      e1 = wave_sum_dpp(e1);
+      e3 = wave_sum_dpp(e3);
       if (lane == 0) {
         const float val = (0.f - ls) + sLf[fe];
         double score = (double)val;
