@@ -161,7 +161,7 @@ def cpu_baseline(model_dir_cfg, weights, chunks, method_beam, budget_s=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="zipformer-68m")
     ap.add_argument("--method", default="greedy_search")
