@@ -1252,27 +1252,30 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
     ny1 = tok;
     if ((fe & 3) == wid) {
       // owner wave: the entropy terms of row fe (search_step_kernel's statistics)
+      // row r = fe >> 2 of this wave, chosen by selects (a dynamic register-array index
+      // would put the arrays in scratch)
       const int r = fe >> 2;
-      float m1 = 0.f, m2 = 0.f, se = 1.f, ls = 0.f;
+      float m1 = m1r[0], m2 = m2r[0], se = ser[0], ls = lsr[0];
+#pragma unroll
+      for (int rr = 1; rr < RPW; ++rr) {
+        m1 = rr == r ? m1r[rr] : m1;
+        m2 = rr == r ? m2r[rr] : m2;
+        se = rr == r ? ser[rr] : se;
+        ls = rr == r ? lsr[rr] : ls;
+      }
       float e1 = 0.f, e3 = 0.f;
 #pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        if (rr != r) continue;
-        m1 = m1r[rr];
-        m2 = m2r[rr];
-        se = ser[rr];
-        ls = lsr[rr];
+      for (int q = 0; q < Q; ++q) {
+        float4 v = x[0][q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const float4 v = x[rr][q];
-          const float vv[4] = {v.x, v.y, v.z, v.w};
+        for (int rr = 1; rr < RPW; ++rr) v = rr == r ? x[rr][q] : v;
+        const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float d = vv[c] - m1;
-            const float e = __expf(d);
-            e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
-            e3 += __expf(d * (1.0f / 3.0f));
-          }
+        for (int c = 0; c < 4; ++c) {
+          const float d = vv[c] - m1;
+          const float e = __expf(d);
+          e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+          e3 += __expf(d * (1.0f / 3.0f));
         }
       }
       e1 = wave_sum_dpp(e1);
@@ -1326,13 +1329,12 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
     // the emitting row's wave holds the new context's table row (prefetched in C)
     const int r = fe >> 2;
 #pragma unroll
-    for (int rr = 0; rr < RPW; ++rr) {
-      if (rr != r) continue;
+    for (int j = 0; j < 2; ++j) {
+      float4 v = pre[0][j];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c4 = lane + 64 * j;
-        if (c4 < d4) sTab[c4] = pre[rr][j];
-      }
+      for (int rr = 1; rr < RPW; ++rr) v = rr == r ? pre[rr][j] : v;
+      const int c4 = lane + 64 * j;
+      if (c4 < d4) sTab[c4] = v;
     }
   }
   __syncthreads();
