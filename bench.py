@@ -167,7 +167,7 @@ def main():
     ap.add_argument("--method", default="greedy_search")
     ap.add_argument("--beam", type=int, default=8)
     ap.add_argument("--audio-sec", type=float, default=3600.0)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hotwords", type=int, default=0,
                     help="N synthetic hotwords (2-4 tokens each, score 1.5 as the reference's "

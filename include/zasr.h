@@ -48,7 +48,10 @@ enum {
   ZASR_ERR_RUNTIME = 3,   /* HIP / internal failure */
 };
 
-enum { ZASR_PRECISION_FP32 = 0, ZASR_PRECISION_BF16 = 1 };
+/* FP32: exact-f32 MFMA everywhere (parity mode).  BF16: bf16 MFMA operands for the encoder
+   projections / attention and the joiner, f32 accumulate, norms and search.  BF16_ENC: the
+   BF16 encoder with the f32 joiner and search of FP32 (no bf16 rounding of the joiner input). */
+enum { ZASR_PRECISION_FP32 = 0, ZASR_PRECISION_BF16 = 1, ZASR_PRECISION_BF16_ENC = 2 };
 
 typedef struct zasr_config {
   const char* model_dir;        /* config.json + model.safetensors (+ tokens.txt for hosts) */

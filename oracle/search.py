@@ -169,12 +169,17 @@ def beam_search(enc_out: np.ndarray, decoder: Callable[[np.ndarray], np.ndarray]
     cache: Dict[Tuple[int, int], np.ndarray] = {}
 
     def dec_rows(ctxs):
-        miss = [c for c in dict.fromkeys(ctxs) if c not in cache]
+        # cache misses go to the decoder as one batch, duplicates included, each hypothesis
+        # taking the row of its own batch position and the cache keeping the last one
+        # (core/asr_engine.py:1073-1088): row values can depend on the batch shape in BLAS
+        rows = [cache.get(c) for c in ctxs]
+        miss = [i for i, r in enumerate(rows) if r is None]
         if miss:
-            res = decoder(np.array(miss, dtype=np.int64))
-            for c, r in zip(miss, res):
-                cache[c] = r.copy()
-        return np.stack([cache[c] for c in ctxs])
+            res = decoder(np.array([ctxs[i] for i in miss], dtype=np.int64))
+            for j, i in enumerate(miss):
+                rows[i] = res[j]
+                cache[ctxs[i]] = res[j].copy()
+        return np.stack(rows)
 
     # hyp record: [ys(list), logp(f64), frames, tok_logps, emit_logits, ctx_state]
     hyps: Dict[tuple, list] = {(-1, BLANK): [[-1, BLANK], 0.0, [], [], [],

@@ -259,7 +259,8 @@ void Engine::pin_reset(int arena) {
 Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const HotwordDFA& hw,
                int precision)
     : device_(device), beam_(beam), greedy_(greedy), precision_(precision), hw_host_(hw) {
-  ZASR_REQUIRE(precision == 0 || precision == 1, "precision must be 0 (fp32) or 1 (bf16)");
+  ZASR_REQUIRE(precision >= 0 && precision <= 2,
+               "precision must be 0 (fp32), 1 (bf16) or 2 (bf16 encoder, f32 joiner + search)");
   ZASR_HIP_CHECK(hipSetDevice(device_));
   ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   {
@@ -435,7 +436,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
   model_.dec_proj = lin("decoder_proj", cfg.joiner_dim, D);
   model_.joiner = lin("joiner.output_linear", cfg.V, cfg.joiner_dim);
   ensure_pos_tables(2048);
-  if (precision_ == 1) {  // bf16 copies of every dense projection weight
+  if (precision_ != 0) {  // bf16 copies of every dense projection weight
     auto mk = [&](DLin& l) {
       void* p = nullptr;
       ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2));
@@ -444,9 +445,11 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
       l.wh = p;
     };
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
-                    &model_.enc_proj, &model_.joiner})
+                    &model_.enc_proj})
       mk(*l);
-    if (cfg.joiner_dim == 256 || cfg.joiner_dim == 512) {  // speculative-greedy joiner operand
+    // precision 2 keeps the joiner (and with it J, the logits and the search) in f32
+    if (precision_ == 1) mk(model_.joiner);
+    if (precision_ == 1 && (cfg.joiner_dim == 256 || cfg.joiner_dim == 512)) {  // speculative-greedy joiner operand
       void* p = nullptr;
       ZASR_HIP_CHECK(hipMalloc(&p, (size_t)gemm_rp_packed_elems(cfg.V, cfg.joiner_dim) * 2));
       model_.allocations.push_back(p);
@@ -810,7 +813,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   if (!orig_ready)  // else the previous layer's BiasNorm already wrote src here
     ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
   // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
-  const bool bf16 = precision_ == 1;
+  const bool bf16 = precision_ != 0;
   float* qkp = nullptr;
   float* A = nullptr;
   __bf16* A16 = nullptr;
@@ -1006,7 +1009,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   std::vector<std::vector<GemmSlice>> sl_nl(ns);
   std::vector<std::vector<int>> o8(ns);
   std::vector<int> R8(ns, 0);
-  const bool bf16 = precision_ == 1;
+  const bool bf16 = precision_ != 0;
   size_t attn_floats = 0;
   int maxL_all = 0;
   for (int i = 0; i < ns; ++i) {

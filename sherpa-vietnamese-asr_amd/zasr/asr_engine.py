@@ -1,5 +1,9 @@
 """Drop-in `core/asr_engine.py` ASR surface backed by libzasr.so on MI355X.
 
+This module lives under the `zasr` package (not under a `core` package) so that it never
+shadows the reference's own `core` package: `zasr.dropin.install(core.asr_engine, ...)`
+rebinds the reference module's hot-path names to the functions below.
+
 Replaces the reference's onnxruntime + numpy hot path (`core/asr_engine.py:686-1326`)
 with the same Python names, arguments and return shapes, so the reference's callers
 (`TranscriberPipeline._run_pipeline` :2057-2494, `transcriber.py:26-34`,
@@ -41,6 +45,15 @@ CONTEXT_SIZE = 2
 _recognizer_cache: Dict[tuple, dict] = {}
 _cache_lock = threading.Lock()
 _last_handle: Optional[Recognizer] = None
+# the reference's core.asr_engine module once zasr.dropin.install() ran: its
+# get_hotwords_config (core/config.py:385-408, imported at core/asr_engine.py top level)
+# is where the hotword file and score come from, as in create_recognizer (:993-1003)
+_HOST = None
+
+
+def set_host_module(module) -> None:
+    global _HOST
+    _HOST = module
 
 
 def get_ort():
@@ -78,11 +91,14 @@ def _log_add(a, b):
 
 
 def clear_model_cache(which="all"):
+    """Drops this build's recognizer cache (reference :743-768, the 'recognizer' part).  The
+    native engines are released by reference count: copies of a recognizer dict
+    (`dict(recognizer_2)`, core/asr_engine.py:2306) share the handle, and the last one to
+    go frees it (Recognizer.__del__).  After install() the reference's own clear_model_cache
+    still runs for the punctuation restorer and diarizer (zasr.dropin)."""
     global _last_handle
     if which in ("all", "recognizer"):
         with _cache_lock:
-            for rec in _recognizer_cache.values():
-                rec["handle"].close()
             _recognizer_cache.clear()
             _last_handle = None
 
@@ -103,7 +119,7 @@ def _hotword_token_lists(model_path: str, hotwords_file: Optional[str], default_
     bpe = os.path.join(model_path, "bpe.model")
     if not hotwords_file or not os.path.exists(bpe):
         return [], []
-    from core.hotword_context import parse_hotwords_file
+    from zasr.hotword_context import parse_hotwords_file
     phrases = parse_hotwords_file(hotwords_file, default_score)
     if not phrases:
         return [], []
@@ -119,13 +135,32 @@ def _hotword_token_lists(model_path: str, hotwords_file: Optional[str], default_
     return seqs, scores
 
 
+def _hotword_config(model_path: str):
+    """(hotwords_file, hotwords_score) the way the reference's create_recognizer finds them
+    (:993-1003): `get_hotwords_config(model_path)` of the installed reference module.  The
+    env vars ZASR_HOTWORDS_FILE / ZASR_HOTWORDS_SCORE override it (standalone use)."""
+    env_file = os.environ.get("ZASR_HOTWORDS_FILE")
+    if env_file is not None:
+        return env_file, float(os.environ.get("ZASR_HOTWORDS_SCORE", 1.5))
+    get_cfg = getattr(_HOST, "get_hotwords_config", None) if _HOST is not None else None
+    if get_cfg is None:
+        return "", 1.5
+    try:
+        cfg = get_cfg(model_path) or {}
+    except Exception as e:  # the reference logs and continues without a graph (:1002-1003)
+        print(f"[Hotwords] Failed to build context graph: {e}")
+        return "", 1.5
+    return cfg.get("hotwords_file", ""), float(cfg.get("hotwords_score", 1.5))
+
+
 def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_provider="cpu",
                       hotwords=None, device_id=None, precision=None):
     """Load (or reuse) a recognizer for `model_path` (reference :903-1020).
 
     Model directory: config.json + model.safetensors + tokens.txt (zasr/model.py).  Raises
     FileNotFoundError when files are missing, like the reference (:927-928).
-    `hotwords` may be (token_id_lists, scores) to bypass the file + bpe.model route.
+    Hotwords: the reference's hotword config (see _hotword_config) tokenized with the model's
+    bpe.model; `hotwords` may be (token_id_lists, scores) to bypass the file + bpe route.
     """
     provider_policy = str(execution_provider or "cpu").lower()
     dev = int(os.environ.get("ZASR_DEVICE", "0")) if device_id is None else int(device_id)
@@ -145,9 +180,8 @@ def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_p
         if hotwords is not None:
             seqs, scores = [list(map(int, s)) for s in hotwords[0]], list(map(float, hotwords[1]))
         else:
-            hw_file = os.environ.get("ZASR_HOTWORDS_FILE", "")
-            seqs, scores = _hotword_token_lists(model_path, hw_file,
-                                                float(os.environ.get("ZASR_HOTWORDS_SCORE", 1.5)))
+            hw_file, hw_score = _hotword_config(model_path)
+            seqs, scores = _hotword_token_lists(model_path, hw_file, hw_score)
         handle = Recognizer(model_path, "modified_beam_search", int(max_active_paths),
                             hotwords=seqs, hotword_scores=scores, device_id=dev, precision=prec)
         info = {"actual_provider": f"MI355X:HIP(device {dev}, {prec})"}
@@ -272,6 +306,14 @@ def _words_from_search(id2token, V, n_samples, time_offset, token_ids, frames, l
     return words
 
 
+def result_words(recognizer, r, n_samples: int, time_offset: float):
+    """Word dicts of one device search result (reference :1227-1326): the tail of
+    decode_chunk, shared by decode_chunk / decode_chunks / the ROVER path."""
+    return _words_from_search(recognizer["id2token"], recognizer["vocab_size"], n_samples,
+                              time_offset, r.token_ids.tolist(), r.frames.tolist(),
+                              r.log_probs.tolist(), int(r.T), [TokenStats(s) for s in r.stats])
+
+
 def decode_chunk(recognizer, audio_chunk, time_offset=0.0, precomputed_features=None):
     """Decode one chunk into merged word dicts (reference :1209-1326)."""
     beam = recognizer.get("max_active_paths", 8)
@@ -286,9 +328,7 @@ def decode_chunk(recognizer, audio_chunk, time_offset=0.0, precomputed_features=
         if a.shape[0] == 0:
             return []
         r = h.decode([a], beam=beam)[0]
-    return _words_from_search(recognizer["id2token"], recognizer["vocab_size"], len(audio_chunk),
-                              time_offset, r.token_ids.tolist(), r.frames.tolist(),
-                              r.log_probs.tolist(), int(r.T), [TokenStats(s) for s in r.stats])
+    return result_words(recognizer, r, len(audio_chunk), time_offset)
 
 
 def decode_chunks(recognizer, chunks: Sequence[np.ndarray], time_offsets: Sequence[float],
@@ -301,7 +341,6 @@ def decode_chunks(recognizer, chunks: Sequence[np.ndarray], time_offsets: Sequen
     from zasr.shard import decode_sharded
     beam = recognizer.get("max_active_paths", 8)
     h: Recognizer = recognizer["handle"]
-    id2token, V = recognizer["id2token"], recognizer["vocab_size"]
     items = list(zip(chunks, time_offsets,
                      precomputed_features if precomputed_features is not None else [None] * len(chunks)))
 
@@ -312,9 +351,6 @@ def decode_chunks(recognizer, chunks: Sequence[np.ndarray], time_offsets: Sequen
             res = h.decode_features([np.asarray(f, np.float32) for _, _, f in part], beam=beam)
         else:
             res = h.decode([np.asarray(c, np.float32) for c, _, _ in part], beam=beam)
-        return [_words_from_search(id2token, V, len(c), off, r.token_ids.tolist(),
-                                   r.frames.tolist(), r.log_probs.tolist(), int(r.T),
-                                   [TokenStats(s) for s in r.stats])
-                for (c, off, _), r in zip(part, res)]
+        return [result_words(recognizer, r, len(c), off) for (c, off, _), r in zip(part, res)]
 
     return decode_sharded(run, items, lengths=[len(c) for c in chunks])

@@ -27,6 +27,10 @@ EXPORTS = (
 )
 
 
+# include/zasr.h ZASR_PRECISION_*: "bf16_enc" = the bf16 encoder with the f32 joiner + search
+PRECISIONS = {"fp32": 0, "bf16": 1, "bf16_enc": 2}
+
+
 class ZasrError(RuntimeError):
     pass
 
@@ -154,7 +158,7 @@ class Recognizer:
                       flat.ctypes.data_as(C.POINTER(C.c_int32)),
                       lens.ctypes.data_as(C.POINTER(C.c_int32)),
                       sc.ctypes.data_as(C.POINTER(C.c_float)), len(hotwords), device_id,
-                      {"fp32": 0, "bf16": 1}[precision])
+                      PRECISIONS[precision])
         h = C.c_void_p()
         rc = self.lib.zasr_create(C.byref(cfg), C.byref(h))
         if rc != 0:

@@ -1,38 +1,69 @@
 """Install this build under the reference's module names without editing its source.
 
-    import core.asr_engine, core.hardware_accel           # the reference's modules
+    import sys; sys.path.insert(0, "/path/to/reference")          # the reference's tree
+    sys.path.insert(0, "/path/to/sherpa-vietnamese-asr_amd")       # this package: zasr only
+    import core.asr_engine, core.hardware_accel, core.calibration  # the reference's modules
     from zasr.dropin import install
-    install(core.asr_engine, core.hardware_accel)          # before TranscriberPipeline runs
+    install(core.asr_engine, core.hardware_accel, core.calibration)  # before the pipeline runs
 
-Every hot-path entry point of the reference module is rebound to the HIP implementation
-(core/asr_engine.py:686-1326 + core/hardware_accel.py), so the reference's own
-TranscriberPipeline, overlap merge and ROVER vote run unchanged on top of libzasr.  Names the
-reference defines but this build does not replace (pipeline, merges, VAD, UI glue) are left
-alone.  Returns the list of names rebound.
+This build's modules live in the `zasr` package, so importing them never shadows the
+reference's `core` package (both trees can be on sys.path in any order).
+
+What is rebound (the ASR hot path, core/asr_engine.py:698-1326):
+  asr_engine      compute_fbank_ort, _log_add, create_recognizer, _ort_beam_search,
+                  _compute_token_entropy, _finalize_word_entropy, decode_chunk, and
+                  clear_model_cache wrapped so the reference's own version still unloads
+                  the punctuation restorer and the diarizer (:743-768)
+  hardware_accel  configure_gpu_addon_paths only (the DirectML / OpenVINO add-on dispatch is
+                  removed per the north star); create_ort_session, is_gpu_provider and
+                  auto_batch_size stay the reference's, so the stages outside ASR (diarization,
+                  punctuation, DNSMOS) keep running on onnxruntime as before
+  calibration     detect_calibration_status / run_device_calibration (the provider picker is
+                  removed per the north star; ASR always runs on MI355X)
+
+get_ort, TranscriberPipeline, the overlap merge, ROVER vote, VAD and UI glue stay the
+reference's.  create_recognizer reads the hotword file and score through the reference
+module's own get_hotwords_config (core/config.py:385-408), as the reference does (:993-1003).
+Returns the list of names rebound.
 """
 from __future__ import annotations
 
 from types import ModuleType
 from typing import List, Optional
 
-ENGINE_NAMES = ("get_ort", "compute_fbank_ort", "_log_add", "clear_model_cache",
-                "create_recognizer", "_ort_beam_search", "_compute_token_entropy",
-                "_finalize_word_entropy", "decode_chunk", "ROVER_MODEL_IDS", "ROVER_MODEL_ID")
-ACCEL_NAMES = ("configure_gpu_addon_paths", "detect_hardware", "is_gpu_provider",
-               "create_ort_session", "auto_batch_size", "hardware_summary")
+ENGINE_NAMES = ("compute_fbank_ort", "_log_add", "create_recognizer", "_ort_beam_search",
+                "_compute_token_entropy", "_finalize_word_entropy", "decode_chunk")
+ACCEL_NAMES = ("configure_gpu_addon_paths",)
+CALIBRATION_NAMES = ("detect_calibration_status", "run_device_calibration")
 
 
-def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None) -> List[str]:
-    from core import asr_engine as ours
-    from core import hardware_accel as ours_hw
+def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None,
+            calibration_module: Optional[ModuleType] = None) -> List[str]:
+    from zasr import asr_engine as ours
+    from zasr import calibration as ours_cal
+    from zasr import hardware_accel as ours_hw
+    if engine_module is ours:
+        raise ValueError("install() needs the reference's core.asr_engine module, got zasr's own")
     done = []
     for n in ENGINE_NAMES:
-        if hasattr(ours, n):
-            setattr(engine_module, n, getattr(ours, n))
-            done.append("asr_engine." + n)
+        setattr(engine_module, n, getattr(ours, n))
+        done.append("asr_engine." + n)
+    orig_clear = getattr(engine_module, "clear_model_cache", None)
+    if orig_clear is not None and not getattr(orig_clear, "_zasr_wrapped", False):
+        def clear_model_cache(which="all"):
+            ours.clear_model_cache(which)
+            return orig_clear(which)
+        clear_model_cache._zasr_wrapped = True
+        clear_model_cache.__doc__ = orig_clear.__doc__
+        engine_module.clear_model_cache = clear_model_cache
+        done.append("asr_engine.clear_model_cache")
+    ours.set_host_module(engine_module)
     if accel_module is not None:
         for n in ACCEL_NAMES:
-            if hasattr(ours_hw, n):
-                setattr(accel_module, n, getattr(ours_hw, n))
-                done.append("hardware_accel." + n)
+            setattr(accel_module, n, getattr(ours_hw, n))
+            done.append("hardware_accel." + n)
+    if calibration_module is not None:
+        for n in CALIBRATION_NAMES:
+            setattr(calibration_module, n, getattr(ours_cal, n))
+            done.append("calibration." + n)
     return done

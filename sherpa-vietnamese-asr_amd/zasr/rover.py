@@ -141,7 +141,7 @@ def decode_chunks_rover(rec_a, rec_b, chunks, time_offsets, hotword_phrases: Seq
     through model A's handle), then the block vote per chunk.  Returns a list of
     (merged_words, disagree_indices) per chunk."""
     import numpy as np
-    from core.asr_engine import decode_chunks
+    from zasr.asr_engine import decode_chunks
     ha = rec_a["handle"]
     feats = [ha.fbank(np.asarray(c, np.float32)) for c in chunks]
     words_a = decode_chunks(rec_a, chunks, time_offsets, precomputed_features=feats)

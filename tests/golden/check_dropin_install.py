@@ -1,0 +1,115 @@
+"""Build-container check that zasr.dropin.install really rebinds the REFERENCE's modules.
+
+Run here only (the reference never travels to the GPU box):
+
+    python tests/golden/check_dropin_install.py [/root/reference]
+
+It puts the reference tree and this build's package on sys.path together (reference first,
+then ours, then the other order in a second process), imports the reference's own
+`core.asr_engine`, `core.hardware_accel` and `core.calibration`, runs install(), and asserts:
+  * the hot-path names of the reference module object are now this build's functions;
+  * the names this build must NOT take over (get_ort, TranscriberPipeline, rover_merge_words,
+    merge_chunks_with_overlap, create_ort_session, is_gpu_provider, auto_batch_size) are
+    still the reference's;
+  * clear_model_cache is wrapped: this build's cache is dropped AND the reference's own
+    function still runs (it unloads the punctuation restorer / diarizer);
+  * create_recognizer's hotword route goes through the reference's get_hotwords_config
+    (core/config.py:385-408): the file it prepares from the reference's hotword.txt and its
+    score 1.5 are what this build uses.
+Prints "dropin install ok" and exits 0 on success.
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(os.path.dirname(HERE)), "sherpa-vietnamese-asr_amd")
+
+
+def check(ref_root: str, ours_first: bool) -> None:
+    paths = [PKG, ref_root] if ours_first else [ref_root, PKG]
+    for p in reversed(paths):
+        sys.path.insert(0, p)
+    with contextlib.redirect_stdout(io.StringIO()):
+        import core.asr_engine as ref
+        import core.calibration as ref_cal
+        import core.hardware_accel as ref_hw
+    assert os.path.realpath(ref.__file__).startswith(os.path.realpath(ref_root)), ref.__file__
+    import zasr.asr_engine as ours
+    import zasr.calibration as ours_cal
+    import zasr.hardware_accel as ours_hw
+    from zasr.dropin import ACCEL_NAMES, CALIBRATION_NAMES, ENGINE_NAMES, install
+
+    keep = {n: getattr(ref, n) for n in ("get_ort", "TranscriberPipeline", "rover_merge_words",
+                                          "merge_chunks_with_overlap")}
+    keep_hw = {n: getattr(ref_hw, n) for n in ("create_ort_session", "is_gpu_provider",
+                                                "auto_batch_size")}
+    orig_clear = ref.clear_model_cache
+    done = install(ref, ref_hw, ref_cal)
+
+    for n in ENGINE_NAMES:
+        assert getattr(ref, n) is getattr(ours, n), n
+    for n in ACCEL_NAMES:
+        assert getattr(ref_hw, n) is getattr(ours_hw, n), n
+    for n in CALIBRATION_NAMES:
+        assert getattr(ref_cal, n) is getattr(ours_cal, n), n
+    for n, f in keep.items():
+        assert getattr(ref, n) is f, n
+    for n, f in keep_hw.items():
+        assert getattr(ref_hw, n) is f, n
+    assert "asr_engine.create_recognizer" in done and "asr_engine.decode_chunk" in done
+
+    # clear_model_cache: ours drops its cache, the reference's still runs
+    assert ref.clear_model_cache is not orig_clear
+    ours._recognizer_cache[("sentinel",)] = {"handle": None}
+    calls = []
+    real = orig_clear
+
+    def spy(which="all"):
+        calls.append(which)
+        return real(which)
+    # re-install over a spy to observe the call-through without touching the module's state
+    ref.clear_model_cache = spy
+    install(ref)
+    with contextlib.redirect_stdout(io.StringIO()):
+        ref.clear_model_cache("all")
+    assert calls == ["all"], calls
+    assert not ours._recognizer_cache
+
+    # hotword route: the reference's get_hotwords_config decides file and score
+    model_dir = os.path.join(ref_root, "models")  # bpe.model absent: the config still resolves
+    with contextlib.redirect_stdout(io.StringIO()):
+        hw_file, hw_score = ours._hotword_config(model_dir)
+    assert hw_file and os.path.exists(hw_file), hw_file
+    assert hw_score == 1.5, hw_score
+    from zasr.hotword_context import parse_hotwords_file
+    phrases = parse_hotwords_file(hw_file)
+    assert len(phrases) > 200, len(phrases)
+    os.remove(hw_file)  # prepare_hotwords_file writes a temp copy
+    print("dropin install ok (%s first): %d names rebound, %d hotword phrases via "
+          "get_hotwords_config" % ("zasr" if ours_first else "reference", len(done), len(phrases)))
+
+
+def main():
+    ref_root = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/root/reference"
+    if "--ours-first" in sys.argv:
+        check(ref_root, True)
+        return
+    if "--ref-first" in sys.argv:
+        check(ref_root, False)
+        return
+    for flag in ("--ref-first", "--ours-first"):  # fresh interpreter per sys.path order
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), ref_root, flag],
+                           capture_output=True, text=True)
+        sys.stdout.write(r.stdout)
+        if r.returncode != 0:
+            sys.stderr.write(r.stderr)
+            sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()

@@ -29,8 +29,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from synth_case import (HOTWORD_FILE, boosted_phrases_from_case, case_config,  # noqa: E402
-                        dec_joiner_weights, enc_out_for, hotword_token_ids, np_decoder,
-                        np_joiner)
+                        dec_joiner_weights, enc_out_for, hotword_token_ids, ngram_phrases,
+                        np_decoder, np_joiner)
 
 REF = "/root/reference"
 
@@ -62,20 +62,40 @@ def case_inputs(kind, seed, T):
     return cfg, w, enc
 
 
-def phrases_for(hc, kind, seed, V, with_hw):
+def phrases_for(hc, kind, seed, V, with_hw, emitted=None):
     if not with_hw:
         return [], []
     seqs, scores = hotword_token_ids(hc.parse_hotwords_file(HOTWORD_FILE, 1.5), V)
     extra = boosted_phrases_from_case(0, V, seed)
     seqs = seqs + extra
     scores = scores + [2.0 + 0.25 * (i % 3) for i in range(len(extra))]
+    if emitted:  # n-grams the model emits without hotwords: full matches at V = 2000
+        ng = ngram_phrases(emitted)
+        seqs = seqs + ng
+        scores = scores + [1.5 + 0.5 * (i % 2) for i in range(len(ng))]
     return seqs, scores
 
 
-def run_case(ae, hc, kind, seed, T, beam, with_hw, dump_chunk=False):
+def full_matches(hc, seqs, scores, toks):
+    """Completed phrases along the decoded tokens (the reference's non-strict walk: a full
+    match returns the root with a positive delta)."""
+    if not seqs:
+        return 0
+    g = hc.ContextGraph()
+    g.build(seqs, scores)
+    st, n = g.root, 0
+    for t in toks:
+        if t == 2:
+            continue
+        d, st = g.forward_one_step(st, t)
+        n += int(st is g.root and d > 0)
+    return n
+
+
+def run_case(ae, hc, kind, seed, T, beam, with_hw, dump_chunk=False, emitted=None):
     cfg, w, enc = case_inputs(kind, seed, T)
     V = cfg.vocab_size
-    seqs, scores = phrases_for(hc, kind, seed, V, with_hw)
+    seqs, scores = phrases_for(hc, kind, seed, V, with_hw, emitted)
     graph = None
     if seqs:
         graph = hc.ContextGraph()
@@ -97,6 +117,7 @@ def run_case(ae, hc, kind, seed, T, beam, with_hw, dump_chunk=False):
         "token_ids": [int(t) for t in toks], "frames": [int(f) for f in frames],
         "ys_log_probs": [float(x) for x in lps], "T_out": int(Tn),
         "entropy": ent,
+        "hotword_full_matches": full_matches(hc, seqs, scores, toks),
     }
     if dump_chunk:
         rec["dec_cache"] = {}
@@ -146,9 +167,29 @@ def hotword_walks(hc, V=64, seed=5):
     return {"V": V, "phrases": seqs, "scores": scores, "walks": walks}
 
 
+def dense_cases(ae, hc, outdir):
+    """V = 2000, T' = 320, blank bias tuned for ~150 beam-8 emissions; the hotword graph is
+    hotword.txt + random phrases + n-grams of the no-hotword output (full matches)."""
+    for beam in (4, 8):
+        seed = 3001 + beam
+        base = run_case(ae, hc, "dense", seed, 320, beam, False, dump_chunk=True)
+        hw = run_case(ae, hc, "dense", seed, 320, beam, True, dump_chunk=True,
+                      emitted=base["token_ids"])
+        for res, tag in ((base, "nohw"), (hw, "hw")):
+            name = f"search_dense_b{beam}_{tag}.json"
+            with open(os.path.join(outdir, name), "w") as f:
+                json.dump(res, f)
+            print(name, "tokens:", len(res["token_ids"]), "T':", res["T_out"],
+                  "full hotword matches:", res["hotword_full_matches"])
+
+
 def main():
     ae, hc = _import_reference()
     outdir = HERE
+    if "--dense-only" in sys.argv:
+        dense_cases(ae, hc, outdir)
+        return
+    dense_cases(ae, hc, outdir)
     cases = []
     for kind, T in (("small", 60), ("full", 100)):
         for beam in (1, 4, 8):

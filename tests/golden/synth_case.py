@@ -28,10 +28,16 @@ def case_config(kind: str) -> ZipformerConfig:
     return zipformer_tiny(64) if kind == "small" else zipformer_m()
 
 
+# joiner blank-logit bias per case kind: "small"/"full" sit 1 nat below the model default
+# (~25-40 % emission at beam 1, sparse at beam 8); "dense" (V = 2000, T' = 320) is tuned so
+# that beam 8 emits ~150 tokens -- dedup, log-add merges and hotword matches at the real shape
+def case_blank_bias(kind: str, V: int) -> float:
+    return 2.2 if kind == "dense" else 0.5 * math.log(V)
+
+
 def dec_joiner_weights(kind: str, seed: int) -> Dict[str, np.ndarray]:
     cfg = case_config(kind)
-    # blank bias 1 nat below the model default: ~25-40% emission, exercises merges/hotwords
-    w = synth_weights(cfg, seed, blank_bias=0.5 * math.log(cfg.vocab_size), dec_gain=1.0,
+    w = synth_weights(cfg, seed, blank_bias=case_blank_bias(kind, cfg.vocab_size), dec_gain=1.0,
                       blank_row_gain=1.0)
     keep = ("decoder.", "decoder_proj.", "joiner.")
     return {k: v for k, v in w.items() if k.startswith(keep)}
@@ -79,6 +85,18 @@ def hotword_token_ids(phrases: List[Tuple[str, float]], V: int):
             seqs.append(ids)
             scores.append(sc)
     return seqs, scores
+
+
+def ngram_phrases(token_ids: List[int], every: int = 6, n_max: int = 3) -> List[List[int]]:
+    """Phrases cut from a decoded token sequence (2..n_max consecutive tokens every `every`
+    positions): hotwords the model actually emits, so full Aho-Corasick matches happen."""
+    out = []
+    for i in range(0, max(0, len(token_ids) - 1), every):
+        n = 2 + (i // every) % (n_max - 1)
+        ph = [int(t) for t in token_ids[i:i + n]]
+        if len(ph) >= 2 and ph not in out:
+            out.append(ph)
+    return out
 
 
 def boosted_phrases_from_case(enc_T: int, V: int, seed: int, n: int = 12):

@@ -9,7 +9,7 @@ import tempfile
 import numpy as np
 
 from zasr.model import (WEIGHTS_VERSION, ZipformerConfig, save_model_dir, synth_tokens, synth_weights,
-                        zipformer_m, zipformer_tiny)
+                        zipformer_m, zipformer_s, zipformer_tiny)
 
 _CACHE = os.environ.get("ZASR_TEST_MODELS", os.path.join(tempfile.gettempdir(), "zasr_test_models"))
 
@@ -43,3 +43,10 @@ def search_case_model(kind: str, seed: int):
     w = synth_weights(cfg, 1)
     w.update(dec_joiner_weights(kind, seed))
     return cfg, model_dir(f"search_{kind}_{seed}", cfg, w)
+
+
+def s_model(seed: int = 20261016):
+    """Zipformer-30M (ROVER model A, zipformer-30m-rnnt-6000h shapes), random init."""
+    cfg = zipformer_s()
+    w = synth_weights(cfg, seed)
+    return cfg, w, model_dir(f"s_{seed}", cfg, w)

@@ -46,10 +46,10 @@ def test_create_reports_missing_model(tmp_path):
 
 
 def test_drop_in_modules_import():
-    import core.asr_engine as ae
-    import core.calibration as cal
-    import core.hardware_accel as ha
-    import core.hotword_context as hc
+    import zasr.asr_engine as ae
+    import zasr.calibration as cal
+    import zasr.hardware_accel as ha
+    import zasr.hotword_context as hc
     for name in ("create_recognizer", "compute_fbank_ort", "_ort_beam_search", "decode_chunk",
                  "get_ort", "_log_add", "_compute_token_entropy", "ROVER_MODEL_ID"):
         assert hasattr(ae, name)
@@ -63,6 +63,6 @@ def test_drop_in_modules_import():
 
 
 def test_create_recognizer_missing_files(tmp_path):
-    import core.asr_engine as ae
+    import zasr.asr_engine as ae
     with pytest.raises(FileNotFoundError):
         ae.create_recognizer(str(tmp_path))

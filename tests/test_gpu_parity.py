@@ -3,7 +3,9 @@
 Tolerances (floating point, stated here as the north_star asks):
   fbank log-mel           |diff| <= 2e-3 absolute (log domain; f64 FFT on both sides)
   encoder_out             max |diff| <= 2e-3 * max(1, |oracle|), fp32 mode
-  search token ids/frames exact; token log-probs within 1e-4; entropy stats within 2e-4
+  search token ids/frames exact; token log-probs within 5e-4 (a token log-prob is the
+  difference of two f32 hypothesis scores, core/asr_engine.py:1099-1100,1121: at the dense
+  cases' T' = 320 the scores reach ~1000, f32 ulp 6e-5 .. 1.2e-4); entropy stats within 2e-4
 """
 import glob
 import json
@@ -125,13 +127,52 @@ def test_search_matches_reference_golden(need_gpu, path):
     assert r.T == g["T_out"]
     assert r.token_ids.tolist() == g["token_ids"]
     assert r.frames.tolist() == g["frames"]
-    np.testing.assert_allclose(r.log_probs, g["ys_log_probs"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(r.log_probs, g["ys_log_probs"], atol=5e-4, rtol=0)
     for st, ref in zip(r.stats, g["entropy"]):
         got = _entropy_dict(st, g["V"])
         for k in ("tsallis_norm", "margin", "entropy_norm"):
             assert abs(got[k] - ref[k]) <= 2e-4, (k, got[k], ref[k])
         assert abs(got["top1_prob"] - ref["top1_prob"]) <= 1e-5
     rec.close()
+
+
+DC_CASES = [c for c in CASES if "decode_chunk" in json.load(open(c))]
+
+
+@pytest.mark.parametrize("path", DC_CASES, ids=[os.path.basename(c) for c in DC_CASES])
+def test_dropin_words_from_device_search_match_reference(need_gpu, path):
+    """The drop-in decode_chunk tail (zasr.asr_engine.result_words: BPE merge, timestamps,
+    probabilities, entropy aggregation from the DEVICE TokenStats) vs the word dicts the
+    reference's own decode_chunk returned (core/asr_engine.py:1209-1326).  Texts, pieces and
+    timestamps exact; probabilities within 1e-4 relative; the 4-dp rounded entropy fields
+    within 1.01e-4 (one rounding step: device f32 vs numpy f32 statistics)."""
+    from model_fixtures import search_case_model
+    from synth_case import case_config, enc_out_for
+    from zasr.asr_engine import create_recognizer, result_words
+    with open(path) as f:
+        g = json.load(f)
+    cfg, mdir = search_case_model(g["kind"], g["seed"])
+    enc = enc_out_for(g["kind"], g["seed"], g["T"], case_config(g["kind"]).joiner_dim)
+    hw = (g["phrases"], g["scores"]) if g["hotwords"] else ([], [])
+    rec = create_recognizer(mdir, max_active_paths=g["beam"], hotwords=hw, precision="fp32")
+    r = rec["handle"].search([enc], beam=g["beam"])[0]
+    dc = g["decode_chunk"]
+    words = result_words(rec, r, dc["n_samples"], dc["time_offset"])
+    ref = dc["words"]
+    assert len(words) == len(ref)
+    for a, b in zip(words, ref):
+        assert set(a) == set(b)
+        for k, v in b.items():
+            if k == "_chunk_bpe_timestamps_local":
+                np.testing.assert_allclose(a[k], v, atol=1e-9, rtol=0)
+            elif k in ("tsallis_max", "margin_min", "entropy_norm", "_conf") and v is not None:
+                assert abs(a[k] - v) <= 1.01e-4, (k, a[k], v)
+            elif k == "prob":
+                assert a[k] == pytest.approx(v, rel=1e-4), k
+            elif isinstance(v, float):
+                assert a[k] == pytest.approx(v, abs=1e-9), k
+            else:
+                assert a[k] == v, k
 
 
 # ------------------------------------------------------------------ end to end
@@ -317,7 +358,7 @@ def test_rover_shared_fbank_equals_separate_decodes(need_gpu):
     decoding on its own + the block vote (the vote itself is pinned on CPU by
     tests/test_host_plan_rover.py)."""
     import copy
-    from core.asr_engine import create_recognizer, decode_chunks
+    from zasr.asr_engine import create_recognizer, decode_chunks
     from model_fixtures import tiny_model
     from zasr.rover import decode_chunks_rover, rover_merge
     _, _, pa = tiny_model(3)

@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from core.asr_engine import _words_from_search
+from zasr.asr_engine import _words_from_search
 from oracle.search import HotwordGraph, beam_search
 from synth_case import case_config, dec_joiner_weights, enc_out_for, np_decoder, np_joiner
 from zasr.model import synth_tokens
@@ -44,14 +44,18 @@ def test_decode_chunk_words_match_reference(path):
 
 
 def test_dropin_install_rebinds_hot_path_names():
-    """zasr.dropin.install rebinds the reference module's hot-path names to this build and
-    leaves the rest (pipeline, merges) alone; checked on a stand-in module object."""
+    """zasr.dropin.install on a stand-in module object: hot-path names rebound, the rest
+    (pipeline, merges, get_ort) left alone, clear_model_cache wrapped (call-through)."""
     import types
-    import core.asr_engine as ours
+    import zasr.asr_engine as ours
     from zasr.dropin import ENGINE_NAMES, install
     ref = types.ModuleType("core_asr_engine_standin")
     ref.TranscriberPipeline = object
     ref.rover_merge_words = lambda a, b: (a, set())
+    sentinel_get_ort = lambda: "ort"
+    ref.get_ort = sentinel_get_ort
+    calls = []
+    ref.clear_model_cache = lambda which="all": calls.append(which)
     for n in ENGINE_NAMES:
         setattr(ref, n, None)
     done = install(ref)
@@ -59,4 +63,10 @@ def test_dropin_install_rebinds_hot_path_names():
     assert ref.decode_chunk is ours.decode_chunk
     assert ref.compute_fbank_ort is ours.compute_fbank_ort
     assert ref.TranscriberPipeline is object
+    assert ref.get_ort is sentinel_get_ort
+    ref.clear_model_cache("restorer")
+    assert calls == ["restorer"]
     assert "asr_engine.decode_chunk" in done
+    with pytest.raises(ValueError):
+        install(ours)
+    ours.set_host_module(None)

@@ -47,7 +47,7 @@ def _worker(rank, world, port, out_dir):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from zasr.shard import decode_sharded, lpt_partition, max_over_ranks
-    from core.asr_engine import decode_chunks
+    from zasr.asr_engine import decode_chunks
     lens = [16000 * s + 37 * i for i, s in enumerate((30, 22, 33, 5, 28, 31, 20))]
     chunks = [np.full(n, 0.01 * i, np.float32) for i, n in enumerate(lens)]
     # ordered gather of an identity decode
