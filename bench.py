@@ -2,23 +2,31 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model zipformer-68m]
                     [--method greedy_search|modified_beam_search] [--beam 8]
-                    [--audio-sec 3600] [--no-cpu-baseline]
+                    [--hotwords-file default|PATH] [--audio-sec 3600]
+                    [--precision bf16|bf16_enc|fp32] [--no-cpu-baseline] [--shape-table]
 
 One step = one pass of the hot path (fbank -> Conv2dSubsampling -> Zipformer2 encoder ->
-decoder/joiner -> search) over one batch of synthetic 16 kHz speech: `--audio-sec` seconds
-(default 1 h) cut by the reference planner into ~30 s chunks with 3 s overlap
-(core/asr_engine.py:2137-2161), all chunks decoded in one batched pass per GPU.  The
-waveforms are resident in HBM before the timed region.  N > 1: one process per GPU
-(torch.distributed.run), each rank decodes its own 1 h shard (weak scaling, no data-path
-collective); the time is the max over ranks.
+decoder/joiner -> search) over one batch: `--audio-sec` seconds (default 1 h) of seeded
+synthetic 16 kHz speech cut by the reference planner (zasr/plan.py: silence-aligned ~30 s
+chunks with a 3 s overlap, core/asr_engine.py:2137-2161), all chunks decoded in one batched
+pass.  The waveforms are resident in HBM before the timed region; K steps are K consecutive
+batches through the engine's batch pipeline (zasr_decode_device_batches).
 
-Prints one JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline accounting.
+--gpus N > 1 without RANK in the environment: this process starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child (before touching
+the GPU) and exits with its return code.  Under torch.distributed each rank decodes its own
+hour (seed + rank; weak scaling, no collective on the data path); the timed region is
+bracketed by barriers and the time is the max over ranks.
+
+Prints one JSON line (rank 0).  DESIGN.md §7 has the roofline accounting.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -35,23 +43,78 @@ SR = 16000
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (f32-input MFMA)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense
 HBM_PEAK_GBS = 8000.0
+WEIGHT_SEED = 20261015
+AUDIO_SEED = 20261015
+DEFAULT_HOTWORDS = os.path.join(REPO, "tests", "golden", "hotword_sample.txt")
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="zipformer-68m")
+    ap.add_argument("--method", default="greedy_search")
+    ap.add_argument("--beam", type=int, default=8)
+    ap.add_argument("--audio-sec", type=float, default=3600.0)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-repeats", type=int, default=5,
+                    help="CPU baseline: 1 warm-up then the mean of this many repeats "
+                         "(core/calibration.py:822-830)")
+    ap.add_argument("--hotwords-file", default="",
+                    help="hotword phrases (reference hotword.txt format, score 1.5 default, "
+                         "core/config.py:405-408); tokenized by the syllable hash (bpe.model is "
+                         "absent).  'default' = tests/golden/hotword_sample.txt (the "
+                         "reference's hotword.txt).  Beam search only.")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="steps as separate decode_device calls (no cross-batch overlap)")
+    ap.add_argument("--shape-table", action="store_true",
+                    help="also time every encoder GEMM shape (HIP events) and emit the "
+                         "per-shape roofline table")
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="no GPU: exercise the launcher / rank / timing / JSON path with gloo "
+                         "and a CPU stand-in step (tests/test_bench_launcher.py)")
+    ap.add_argument("--profile-out", default="")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 outside torch.distributed: run N ranks under torch.distributed.run as a
+    CHILD process (this process never initialised the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------ workload
 def make_chunks(audio_sec: float, seed: int):
-    """~30 s chunks (+3 s overlap) of seeded synthetic speech: windows of a 5-minute base
-    signal with per-chunk gain and noise (cheap to build for an hour of audio)."""
-    from zasr.synth_audio import chunk_plan, synth_speech
-    total = int(audio_sec * SR)
-    base = synth_speech(min(audio_sec, 300.0) + 40.0, seed)
-    rng = np.random.Generator(np.random.PCG64(seed + 1))
-    chunks = []
-    for a, e, _ in chunk_plan(total):
-        n = e - a
-        s = int(rng.integers(0, base.shape[0] - n))
-        c = base[s:s + n] * np.float32(rng.uniform(0.7, 1.1))
-        c = c + np.float32(1e-3) * rng.standard_normal(n).astype(np.float32)
-        chunks.append(np.ascontiguousarray(c, dtype=np.float32))
-    return chunks
+    """`audio_sec` of seeded synthetic speech cut by the reference planner (silence-aligned
+    ~30 s boundaries, 3 s overlap; zasr/plan.py restates core/asr_engine.py:2137-2161).  The
+    synthetic pauses (0.3-2 s) are shorter than the 5 s VAD merge gap (:2117), so the whole
+    signal is one VAD group and the concatenated speech is the signal itself."""
+    from zasr.plan import plan_chunks
+    from zasr.synth_audio import synth_speech
+    audio = synth_speech(audio_sec, seed)
+    return [np.ascontiguousarray(audio[a:e]) for a, e, _ in plan_chunks(audio)]
+
+
+def load_hotwords(path: str, V: int):
+    from zasr.hotword_context import parse_hotwords_file
+    from zasr.model import hash_tokenize_phrases
+    return hash_tokenize_phrases(parse_hotwords_file(path, 1.5), V)
 
 
 FFN_FUSED_DIMS = (64, 96, 128, 192)  # ffn_kernels.hip ffn_fused_supported
@@ -99,7 +162,7 @@ def gemm_class_work(cfg, L_list, bf16: bool):
                 else:
                     lin(R, d, f, c=h16)
                     lin(R, f, d, a=h16, resadd=True)
-            lin(R, d, 3 * hid)
+            lin(R, d, 3 * hid, c=h16)
             lin(R, hid, d, a=h16, resadd=True)
             for _ in range(2):
                 lin(R, d, cfg.value_head_dim * h, c=h16)
@@ -108,6 +171,39 @@ def gemm_class_work(cfg, L_list, bf16: bool):
                 lin(R, d, d, a=h16, resadd=True)
     lin(sum((L + 1) // 2 for L in Ls), cfg.max_dim, cfg.joiner_dim)
     return {k: (v[0], v[1]) for k, v in acc.items()}
+
+
+EPI_NAMES = ["none", "swooshl", "swooshr", "resadd", "mulaux", "mulaux16"]
+
+
+def shape_table(prof: dict, nprof: int, bf16_peak: float, f32_peak: float):
+    """Per-shape roofline rows from profile mode 2's "enc_gemm|M|K|N|w16|a16|c16|epi" classes:
+    algorithmic bytes (A + W + C [+ C read for EPI_RESADD] at the launch's dtypes) and flops,
+    the binding roof (larger of bytes / HBM peak and flops / MFMA peak), and the fraction of
+    that roof the measured mean launch time reaches."""
+    rows = []
+    for name, (cnt, ms) in prof.items():
+        parts = name.split("|")
+        if len(parts) != 8:
+            continue
+        M, K, N, w16, a16, c16, epi = map(int, parts[1:])
+        by = (2 if a16 else 4) * M * K + (2 if w16 else 4) * N * K + \
+            (2 if c16 else 4) * M * N * (2 if epi == 3 else 1)
+        fl = 2.0 * M * K * N
+        t = ms / cnt * 1e-3
+        peak_f = bf16_peak if w16 else f32_peak
+        t_hbm, t_mfma = by / (HBM_PEAK_GBS * 1e9), fl / (peak_f * 1e12)
+        bound = "hbm" if t_hbm >= t_mfma else "mfma"
+        rows.append({"M": M, "K": K, "N": N, "a": "bf16" if a16 else "f32",
+                     "w": "bf16" if w16 else "f32", "c": "bf16" if c16 else "f32",
+                     "epi": EPI_NAMES[epi], "launches_per_step": cnt // nprof,
+                     "us": round(t * 1e6, 2), "bytes": by, "flops": fl, "bound": bound,
+                     "achieved": round((by / t / 1e9) if bound == "hbm" else (fl / t / 1e12), 1),
+                     "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
+                     "frac": round(max(t_hbm, t_mfma) / t, 4),
+                     "ms_per_step": round(ms / nprof, 4)})
+    rows.sort(key=lambda r: -r["ms_per_step"])
+    return rows
 
 
 def pmc_traffic(kernel_class, args):
@@ -120,160 +216,225 @@ def pmc_traffic(kernel_class, args):
             tab = json.load(f)
     except (OSError, ValueError):
         return None
+    hw = "|hw" if (args.hotwords_file and args.method != "greedy_search") else ""
     key = f"{args.model}|{args.method}|{args.beam if args.method != 'greedy_search' else 1}|" \
-          f"{args.precision}|{int(args.audio_sec)}|{kernel_class}"
+          f"{args.precision}|{int(args.audio_sec)}|{kernel_class}{hw}"
     return tab.get(key)
 
 
-def cpu_baseline(model_dir_cfg, weights, chunks, method_beam, budget_s=20.0):
-    """Oracle (fp32 torch encoder + numpy fbank + Python search) on a bounded sample."""
+# ------------------------------------------------------------------ CPU baseline
+_CPU = {}
+
+
+def _cpu_worker_init(model, seed, threads, hotwords):
     import torch
+    from oracle.search import HotwordGraph
+    from oracle.zipformer import ZipformerOracle
+    from zasr.model import PRESETS, synth_weights
+    torch.set_num_threads(threads)
+    cfg = PRESETS[model]()
+    _CPU["orc"] = ZipformerOracle(cfg, synth_weights(cfg, seed))
+    _CPU["graph"] = HotwordGraph(*hotwords) if hotwords and hotwords[0] else None
+
+
+def _cpu_worker_run(job):
     from oracle.fbank import fbank
     from oracle.search import beam_search
-    from oracle.zipformer import ZipformerOracle
+    chunks, beam = job
+    orc = _CPU["orc"]
+    t0 = time.perf_counter()
+    for c in chunks:
+        enc = orc.encoder(fbank(c))
+        beam_search(enc, orc.decoder, orc.joiner, beam, _CPU["graph"] if beam > 1 else None)
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(args, chunks, beam, hotwords, n_chunks=4):
+    """The oracle (torch fp32 encoder + numpy fbank + the reference's search restated) on a
+    bounded sample, with the reference's CPU policy (BASELINE.md "CPU-baseline plan"):
+      * 2 chunk workers when >= 4 chunks and >= 4 physical cores, chunks split even/odd
+        (core/asr_engine.py:2262-2276, 2388-2397), one process each;
+      * encoder threads = physical cores shared between the workers (:946-955), capped at
+        the box's CPU share (16 threads per GPU);
+      * 1 warm-up pass then the mean of `--cpu-repeats` timed passes (core/calibration.py:
+        822-830).
+    Runs before this process touches the GPU (the workers are spawned children)."""
+    import multiprocessing as mp
     try:
         import psutil
         phys = psutil.cpu_count(logical=False) or os.cpu_count()
     except Exception:
         phys = os.cpu_count()
-    threads = max(1, min(phys, 16))  # reference policy: encoder Z = physical cores
-    torch.set_num_threads(threads)
-    orc = ZipformerOracle(model_dir_cfg, weights)
-    done_sec, t0, used = 0.0, time.time(), 0
-    # warm-up (reference calibration: 1 warmup then measured runs, core/calibration.py:822-830)
-    orc.encoder(fbank(chunks[0][: SR * 3]))
-    t0 = time.time()
-    for c in chunks:
-        enc = orc.encoder(fbank(c))
-        beam_search(enc, orc.decoder, orc.joiner, method_beam)
-        done_sec += c.shape[0] / SR
-        used += 1
-        if time.time() - t0 > budget_s:
-            break
-    el = time.time() - t0
-    return {"value": round(done_sec / el, 3), "unit": "audio-sec/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"{used} chunk(s), {done_sec:.1f} s of the same synthetic audio, "
-                      f"oracle fbank+encoder+{'greedy' if method_beam == 1 else 'beam %d' % method_beam}"
-                      f" search, torch fp32 {threads} threads"}
+    nproc = os.cpu_count()
+    share = min(16, phys)
+    sample = chunks[:n_chunks]
+    workers = 2 if (len(sample) >= 4 and phys >= 4) else 1
+    threads = max(1, share // workers)
+    jobs = [(sample[w::workers], beam) for w in range(workers)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers, initializer=_cpu_worker_init,
+                  initargs=(args.model, WEIGHT_SEED, threads, hotwords)) as pool:
+        pool.map(_cpu_worker_run, [([c[: SR * 4] for c in j[0][:1]], j[1]) for j in jobs])
+        times = []
+        for _ in range(max(1, args.cpu_repeats)):
+            t0 = time.perf_counter()
+            pool.map(_cpu_worker_run, jobs)
+            times.append(time.perf_counter() - t0)
+    sec = sum(c.shape[0] for c in sample) / SR
+    mean = float(np.mean(times))
+    return {"value": round(sec / mean, 3), "unit": "audio-sec/sec", "cores": workers * threads,
+            "kind": "port", "nproc": nproc, "physical_cores": phys, "workers": workers,
+            "threads_per_worker": threads, "repeats": len(times),
+            "repeat_s": [round(t, 3) for t in times],
+            "sample": f"{len(sample)} planner chunks ({sec:.1f} s) of the benched audio; oracle "
+                      f"fbank + torch fp32 encoder + reference search "
+                      f"({'greedy' if beam == 1 else 'beam %d' % beam}"
+                      f"{' + hotwords' if hotwords and hotwords[0] and beam > 1 else ''}), "
+                      f"{workers} worker process(es) x {threads} threads, 1 warm-up + mean of "
+                      f"{len(times)}"}
 
 
+# ------------------------------------------------------------------ main
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="zipformer-68m")
-    ap.add_argument("--method", default="greedy_search")
-    ap.add_argument("--beam", type=int, default=8)
-    ap.add_argument("--audio-sec", type=float, default=3600.0)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--hotwords", type=int, default=0,
-                    help="N synthetic hotwords (2-4 tokens each, score 1.5 as the reference's "
-                         "hotwords_score default, core/asr_engine.py:1000); beam search only")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="steps as separate decode_device calls (no cross-batch overlap)")
-    ap.add_argument("--profile-out", default="")
-    args = ap.parse_args()
+    args = parse_args()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args))
 
-    import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    from zasr.model import PRESETS, chunk_flops
+    cfg = PRESETS[args.model]()
+    beam = 1 if args.method == "greedy_search" else args.beam
+    hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
+    hotwords = load_hotwords(hw_path, cfg.vocab_size) if (hw_path and beam > 1) else None
+
+    # each rank: its own hour of audio (weak scaling), planned like the reference
+    chunks = make_chunks(args.audio_sec, AUDIO_SEED + rank)
+    lens = [c.shape[0] for c in chunks]
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_dry_run:
+        cpu = cpu_baseline(args, chunks, beam, hotwords)
+
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
+        dist.init_process_group("gloo" if args.cpu_dry_run else "nccl", init_method="env://")
 
-    from zasr.binding import Recognizer
-    from zasr.model import PRESETS, save_model_dir, synth_tokens, synth_weights
-
-    cfg = PRESETS[args.model]()
-    weights = synth_weights(cfg, 20261015)
-    mdir = os.path.join(tempfile.gettempdir(), f"zasr_bench_{args.model}_{os.getpid()}")
-    save_model_dir(mdir, cfg, weights, synth_tokens(cfg.vocab_size))
-    beam = 1 if args.method == "greedy_search" else args.beam
-    hotwords = None
-    if args.hotwords:
-        hr = np.random.default_rng(20261016)
-        hotwords = [hr.integers(1, cfg.vocab_size, size=int(hr.integers(2, 5))).tolist()
-                    for _ in range(args.hotwords)]
-    rec = Recognizer(mdir, args.method, beam, hotwords=hotwords, device_id=local,
-                     precision=args.precision)
-
-    # per-rank shard: the same hour of synthetic audio, seeded by rank
-    chunks = make_chunks(args.audio_sec, 20261015 + rank)
-    lens = [c.shape[0] for c in chunks]
-    offs = np.cumsum([0] + lens[:-1]).tolist()
-    d_wav = torch.from_numpy(np.concatenate(chunks)).to(f"cuda:{local}")
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream().cuda_stream
-
-    def step():
-        return rec.decode_device(d_wav.data_ptr(), offs, lens, beam=beam, stream=stream)
-
-    def steps(k):
-        # k steps = k consecutive batches (each the hour of chunks) through the engine's
-        # batch pipeline: batch i+1's fbank + encoder overlap batch i's search on the GPU
-        # (zasr_decode_device_batches); every batch's results are complete on return
-        if args.no_pipeline:
+    rec, dev = None, None
+    if args.cpu_dry_run:
+        # launcher / rank / timing path only: a CPU stand-in for the decode
+        def steps(k):
             for _ in range(k):
-                r = step()
-            return r
-        n = len(lens)
-        r = rec.decode_device_batches(d_wav.data_ptr(), offs * k, lens * k, [n] * k,
-                                      beam=beam, stream=stream)
-        return r[-n:]
+                sum(float(np.abs(c[::97]).sum()) for c in chunks)
+            return []
+    else:
+        torch.cuda.set_device(local)
+        dev = f"cuda:{local}"
+        from zasr.binding import Recognizer
+        from zasr.model import save_model_dir, synth_tokens, synth_weights
+        weights = synth_weights(cfg, WEIGHT_SEED)
+        mdir = os.path.join(tempfile.gettempdir(), f"zasr_bench_{args.model}_{os.getpid()}")
+        save_model_dir(mdir, cfg, weights, synth_tokens(cfg.vocab_size))
+        del weights
+        rec = Recognizer(mdir, args.method, beam, hotwords=hotwords[0] if hotwords else None,
+                         hotword_scores=hotwords[1] if hotwords else None, device_id=local,
+                         precision=args.precision)
+        offs = np.cumsum([0] + lens[:-1]).tolist()
+        d_wav = torch.from_numpy(np.concatenate(chunks)).to(dev)
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream().cuda_stream
+
+        def step():
+            return rec.decode_device(d_wav.data_ptr(), offs, lens, beam=beam, stream=stream)
+
+        def steps(k):
+            # k steps = k consecutive batches (each the hour of chunks) through the engine's
+            # batch pipeline: batch i+1's fbank + encoder overlap batch i's search on the GPU
+            # (zasr_decode_device_batches); every batch's results are complete on return
+            if args.no_pipeline:
+                for _ in range(k):
+                    r = step()
+                return r
+            n = len(lens)
+            r = rec.decode_device_batches(d_wav.data_ptr(), offs * k, lens * k, [n] * k,
+                                          beam=beam, stream=stream)
+            return r[-n:]
+
+    def sync():
+        if dev is not None:
+            torch.cuda.synchronize()
 
     if args.warmup:
-        res = steps(args.warmup)
-    torch.cuda.synchronize()
-    # single-batch latency (one hour of chunks, nothing to overlap with): reported beside
-    t1 = time.perf_counter()
-    step()
-    torch.cuda.synchronize()
-    batch_latency_ms = 1000 * (time.perf_counter() - t1)
+        steps(args.warmup)
+    sync()
+    batch_latency_ms = None
+    if rec is not None:  # one batch alone (nothing to overlap with): reported beside
+        t1 = time.perf_counter()
+        step()
+        sync()
+        batch_latency_ms = 1000 * (time.perf_counter() - t1)
 
     # timed region: barrier + sync on both sides, max over ranks
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     res = steps(args.steps)
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     if dist:
         from zasr.shard import max_over_ranks
-        el = max_over_ranks(el, device=f"cuda:{local}")
+        el = max_over_ranks(el, device=dev)
         dist.barrier()
 
     # kernel-class timing: HIP events recorded by the library on its launch stream over
-    # K profiled steps (separate from the wall-clock region above)
-    rec.profile(True)
-    rec.profile_reset()
-    for _ in range(max(1, min(args.steps, 3))):
-        step()
-    torch.cuda.synchronize()
-    prof = rec.profile_report()
-    rec.profile(False)
-    nprof = max(1, min(args.steps, 3))
+    # profiled steps (separate from the wall-clock region above)
+    classes, shapes, nprof = {}, None, max(1, min(args.steps, 3))
+    if rec is not None:
+        rec.profile(1)
+        rec.profile_reset()
+        for _ in range(nprof):
+            step()
+        sync()
+        classes = rec.profile_report()
+        if args.shape_table:
+            rec.profile(2)
+            rec.profile_reset()
+            step()
+            sync()
+            shapes = shape_table(rec.profile_report(), 1, MFMA_BF16_PEAK_TFLOPS,
+                                 MFMA_F32_PEAK_TFLOPS)
+        rec.profile(0)
 
-    audio_sec_rank = args.audio_sec
-    decoded_sec_rank = sum(lens) / SR
-    value = audio_sec_rank * world * args.steps / el
+    value = args.audio_sec * world * args.steps / el
     emitted = sum(int(r.token_ids.size) for r in res)
     tprime = sum(int(r.T) for r in res)
 
     L_list = [((n + 80) // 160 - 7) // 2 for n in lens]
-    bf16 = args.precision == "bf16"
-    work = gemm_class_work(cfg, L_list, bf16)
-    rows_joiner = sum(min(beam, 8) * ((L + 1) // 2) for L in L_list)
-    f_join = 2.0 * rows_joiner * cfg.joiner_dim * cfg.vocab_size
-    classes = {k: v for k, v in prof.items()}
-    dom = max(classes.items(), key=lambda kv: kv[1][1])[0] if classes else None
+    bf16 = args.precision != "fp32"
     peak_mfma = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_F32_PEAK_TFLOPS
+    # end-to-end roofline (SURVEY §8d): algorithmic FLOPs of the whole path per step
+    # (zasr.model.chunk_flops over the step's chunks) / step time / MFMA peak
+    fl_parts = {}
+    for n in lens:
+        for k, v in chunk_flops(cfg, n, beam).items():
+            fl_parts[k] = fl_parts.get(k, 0.0) + v
+    fl_step = sum(fl_parts.values())
+    t_step = el / args.steps
+    e2e = {"flops_per_step": fl_step, "flops_per_audio_sec": round(fl_step / args.audio_sec),
+           "breakdown_gflop_per_step": {k: round(v / 1e9, 2) for k, v in fl_parts.items()},
+           "achieved": round(fl_step / t_step / 1e12, 2), "unit": "TFLOP/s", "peak": peak_mfma,
+           "frac": round(fl_step / t_step / 1e12 / peak_mfma, 4)}
+
+    work = gemm_class_work(cfg, L_list, bf16)
+    f_join = 2.0 * beam * tprime * cfg.joiner_dim * cfg.vocab_size  # per step
+    dom = max(classes.items(), key=lambda kv: kv[1][1])[0] if classes else None
     roof = None
     if dom:
         cnt, ms = classes[dom]
@@ -297,8 +458,7 @@ def main():
                         "algorithmic_flops_per_launch": round(fl),
                         "hbm_gbs": round(by / per_launch_s / 1e9, 1)}
         elif dom == "joiner":
-            work = f_join * nprof / cnt
-            ach = work / per_launch_s / 1e12
+            ach = f_join * nprof / cnt / per_launch_s / 1e12
             roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2),
                     "peak": peak_mfma, "unit": "TFLOP/s", "frac": round(ach / peak_mfma, 4),
                     "traffic": None}
@@ -313,11 +473,9 @@ def main():
             roof["traffic"] = tr["bytes_per_launch"]
             roof["traffic_source"] = tr["source"]
 
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, weights, chunks[:6], beam)
-
     if rank == 0:
+        hw_tag = (f" + hotwords ({len(hotwords[0])} phrases of {os.path.basename(hw_path)})"
+                  if hotwords else "")
         line = {
             "metric": "audio-sec/sec (xRT) Zipformer-68M offline decode",
             "value": round(value, 2), "unit": "audio-sec/sec", "n_gpus": world,
@@ -326,26 +484,34 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic (seeded 16 kHz speech-like audio, random-init Zipformer weights)",
             "config": {"workload": f"{args.model} {args.method}"
-                                   f"{'' if beam == 1 else ' beam %d' % beam}"
-                                   f"{' + %d hotwords' % args.hotwords if args.hotwords else ''}"
-                                   ", batched VAD-style chunks",
+                                   f"{'' if beam == 1 else ' beam %d' % beam}{hw_tag}"
+                                   ", batched planner chunks, 1 h per GPU",
                        "model": args.model, "chunks_per_gpu": len(chunks),
-                       "audio_sec_per_gpu": audio_sec_rank,
-                       "decoded_sec_per_gpu_incl_overlap": round(decoded_sec_rank, 1),
-                       "parallelism": f"dp{world} (chunk shards, no collective)",
+                       "chunk_sec_min_max": [round(min(lens) / SR, 2), round(max(lens) / SR, 2)],
+                       "audio_sec_per_gpu": args.audio_sec,
+                       "decoded_sec_per_gpu_incl_overlap": round(sum(lens) / SR, 1),
+                       "parallelism": f"dp{world} (each rank its own hour, seed + rank; weak "
+                                      f"scaling, no collective on the data path)",
                        "batch_pipeline": not args.no_pipeline,
-                       "single_batch_latency_ms": round(batch_latency_ms, 3),
-                       "rtf": round(1.0 / (value / world), 6),
+                       "single_batch_latency_ms": (round(batch_latency_ms, 3)
+                                                   if batch_latency_ms is not None else None),
+                       "rtf": round(1.0 / (value / world), 8),
                        "tokens_emitted_per_gpu": emitted, "encoder_frames_per_gpu": tprime},
             "roofline": roof,
+            "roofline_e2e": e2e,
             "kernel_classes_ms_per_step": {k: round(v[1] / nprof, 3) for k, v in classes.items()},
             "cpu_baseline": cpu,
         }
+        if args.cpu_dry_run:
+            line["dry_run"] = True
+        if shapes is not None:
+            line["gemm_shapes"] = shapes
         print(json.dumps(line))
         if args.profile_out:
             with open(args.profile_out, "w") as f:
                 json.dump(line, f, indent=1)
-    rec.close()
+    if rec is not None:
+        rec.close()
     if dist:
         dist.destroy_process_group()
 

@@ -127,7 +127,9 @@ void zasr_result_free(zasr_result* r);
 int32_t zasr_vocab_size(const zasr_recognizer* h);
 int32_t zasr_joiner_dim(const zasr_recognizer* h);
 
-/* profiling: per-kernel-class HIP-event timing on the handle's stream */
+/* profiling: per-kernel-class HIP-event timing on the handle's stream.  on = 0 off,
+   1 kernel classes, 2 kernel classes with the encoder GEMMs split by shape
+   ("enc_gemm|M|K|N|w16|a16|c16|epi" class names, for the per-shape roofline table) */
 int zasr_profile_enable(zasr_recognizer* h, int32_t on);
 int zasr_profile_reset(zasr_recognizer* h);
 /* writes "name count total_ms\n" lines into buf (cap bytes) */

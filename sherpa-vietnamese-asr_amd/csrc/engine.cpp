@@ -661,7 +661,9 @@ hipEvent_t Engine::take_event() {
   return e;
 }
 
-void Engine::prof_begin(const char* name) {
+void Engine::prof_begin(const char* name) { prof_begin(std::string(name)); }
+
+void Engine::prof_begin(const std::string& name) {
   if (!prof_on_) return;
   ProfEvent pe{name, take_event(), take_event()};
   ZASR_HIP_CHECK(hipEventRecord(pe.a, st_));
@@ -699,6 +701,16 @@ std::string Engine::profile_report() {
   return os.str();
 }
 
+// per-shape GEMM class names (profile mode 2): "<class>|M|K|N|w16|a16|c16|epi", parsed by
+// bench.py into the per-shape roofline table
+std::string Engine::shape_key(const char* cls, int M, int K, int N, bool w16, bool a16, bool c16,
+                              int epi) {
+  std::ostringstream os;
+  os << cls << "|" << M << "|" << K << "|" << N << "|" << (int)w16 << "|" << (int)a16 << "|"
+     << (int)c16 << "|" << epi;
+  return os.str();
+}
+
 // ------------------------------------------------------------------------------------
 // building blocks
 // ------------------------------------------------------------------------------------
@@ -718,7 +730,10 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
   p.K = l.K;
   p.alpha = 1.f;
   p.max_M = M;
-  prof_begin(cls);
+  if (prof_shapes_ && prof_on_)
+    prof_begin(shape_key(cls, M, l.K, l.N, l.wh != nullptr, false, false, epi));
+  else
+    prof_begin(cls);
   if (l.wh)
     gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_);
   else
@@ -746,7 +761,10 @@ void Engine::linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M,
   p.max_M = M;
   p.byp_orig = byp_orig;
   p.byp_scale = byp_scale;
-  prof_begin("enc_gemm");
+  if (prof_shapes_ && prof_on_)
+    prof_begin(shape_key("enc_gemm", M, l.K, l.N, true, a_bf16, c_bf16, epi));
+  else
+    prof_begin("enc_gemm");
   gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_, a_bf16, c_bf16);
   prof_end();
 }

@@ -117,7 +117,11 @@ class Engine {
                                        const std::vector<long>& t_out, int beam);
 
   // profiling
-  void profile_enable(bool on) { prof_on_ = on; }
+  // mode 0: off, 1: kernel classes, 2: classes with the GEMMs split by shape
+  void profile_enable(int mode) {
+    prof_on_ = mode > 0;
+    prof_shapes_ = mode == 2;
+  }
   void profile_reset();
   std::string profile_report();
 
@@ -182,8 +186,12 @@ class Engine {
     hipEvent_t a, b;
   };
   void prof_begin(const char* name);
+  void prof_begin(const std::string& name);
   void prof_end();
+  static std::string shape_key(const char* cls, int M, int K, int N, bool w16, bool a16,
+                               bool c16, int epi);
   bool prof_on_ = false;
+  bool prof_shapes_ = false;  // GEMM classes split by shape (profile mode 2)
   std::vector<ProfEvent> prof_pending_;
   std::map<std::string, std::pair<long, double>> prof_acc_;
   std::vector<hipEvent_t> event_pool_;

@@ -264,7 +264,8 @@ int32_t zasr_joiner_dim(const zasr_recognizer* h) { return h ? h->eng->joiner_di
 
 int zasr_profile_enable(zasr_recognizer* h, int32_t on) {
   if (!h) return fail(ZASR_ERR_INVALID, "null handle");
-  h->eng->profile_enable(on != 0);
+  if (on < 0 || on > 2) return fail(ZASR_ERR_INVALID, "profile mode must be 0, 1 or 2");
+  h->eng->profile_enable((int)on);
   return ZASR_OK;
 }
 int zasr_profile_reset(zasr_recognizer* h) {

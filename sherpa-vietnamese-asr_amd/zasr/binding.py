@@ -284,8 +284,9 @@ class Recognizer:
         return self._collect(res)
 
     # profiling (HIP events on the library's stream)
-    def profile(self, on: bool = True):
-        self._check(self.lib.zasr_profile_enable(self.handle, 1 if on else 0))
+    def profile(self, on=True):
+        """on: False/0 off, True/1 kernel classes, 2 = GEMMs split by shape."""
+        self._check(self.lib.zasr_profile_enable(self.handle, int(on)))
 
     def profile_reset(self):
         self._check(self.lib.zasr_profile_reset(self.handle))

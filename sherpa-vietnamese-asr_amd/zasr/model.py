@@ -201,12 +201,14 @@ def count_params(cfg: ZipformerConfig, prefix: str = "") -> int:
     return int(sum(int(np.prod(v)) for k, v in param_shapes(cfg).items() if k.startswith(prefix)))
 
 
-# Joiner blank-logit bias giving ~5-15 % greedy emission on the bench's synthetic speech
-# through the synthetic encoder (calibrated with the oracle).  decoder_proj is scaled down
+# Joiner blank-logit bias giving ~15 % greedy emission (SURVEY §8d "Weights") on the bench's
+# planner chunks of synthetic speech through the synthetic encoder, calibrated with the
+# oracle (68M seed 20261015: -1.6 -> 26 %, -1.4 -> 15 %, -1.2 -> 10 %; 30M seed 20261016:
+# 5.7 -> 30 %, 6.0 -> 11 %).  decoder_proj is scaled down
 # (dec_gain) and the blank row of output_linear up (blank_row_gain) so that emission is
 # driven by the encoder frames rather than by the (random) decoder context.
-SYNTH_BLANK_BIAS = {"zipformer-68m": -2.0, "zipformer-30m": 0.8, "zipformer-tiny": 1.8}
-WEIGHTS_VERSION = 3
+SYNTH_BLANK_BIAS = {"zipformer-68m": -1.4, "zipformer-30m": 5.9, "zipformer-tiny": 1.8}
+WEIGHTS_VERSION = 4
 
 
 def synth_weights(cfg: ZipformerConfig, seed: int = 20261015,
@@ -276,6 +278,27 @@ def synth_tokens(vocab_size: int, seed: int = 7) -> List[str]:
     return toks
 
 
+def syllable_token_id(syllable: str, V: int) -> int:
+    """Deterministic syllable -> token id in [3, V) (md5): stands in for the model's
+    sentencepiece encoding of hotword phrases (bpe.model is absent offline; SURVEY §8d
+    config 3)."""
+    import hashlib
+    h = hashlib.md5(syllable.encode("utf-8")).digest()
+    return 3 + int.from_bytes(h[:4], "little") % (V - 3)
+
+
+def hash_tokenize_phrases(phrases, V: int):
+    """[(phrase, score)] (hotword file entries, core/hotword_context.py:191-222) ->
+    (token id lists, scores), one token per space-separated syllable."""
+    seqs, scores = [], []
+    for text, sc in phrases:
+        ids = [syllable_token_id(s, V) for s in text.split()]
+        if ids:
+            seqs.append(ids)
+            scores.append(float(sc))
+    return seqs, scores
+
+
 def save_model_dir(path: str, cfg: ZipformerConfig, weights: Dict[str, np.ndarray],
                    tokens: List[str]) -> str:
     from safetensors.numpy import save_file
@@ -315,6 +338,36 @@ def seq_lengths(n_samples: int) -> Dict[str, int]:
     T = (n_samples + 80) // 160 if n_samples > 0 else 0
     L = (T - 7) // 2 if T >= 9 else 0
     return {"T": T, "L": L, "T_out": (L + 1) // 2}
+
+
+def chunk_flops(cfg: ZipformerConfig, n_samples: int, beam: int = 1) -> Dict[str, float]:
+    """Algorithmic FLOPs of one chunk through the path (SURVEY §8d "F_enc"): frontend convs,
+    every stack projection, attention (scores incl. the positional term, both value
+    products, NonlinAttention), depthwise convs, encoder_proj, and the joiner at `beam` rows
+    per encoder frame (the decoder is a table lookup).  Elementwise work is not counted."""
+    T = (n_samples + 80) // 160 if n_samples > 0 else 0
+    if T < 9:
+        return {"frontend": 0.0, "projections": 0.0, "attention": 0.0, "conv1d": 0.0,
+                "joiner": 0.0}
+    L = (T - 7) // 2
+    l1, l2 = T - 2, (T - 3) // 2
+    fe = 2.0 * (72 * 8 * l1 * 80 + 72 * 32 * l2 * 39 + 288 * 128 * L * 19
+                + 49 * 128 * L * 19 + 2 * 128 * 384 * L * 19) + 2.0 * 2432 * cfg.encoder_dims[0] * L
+    proj = att = cv = 0.0
+    qd, vd, pd = cfg.query_head_dim, cfg.value_head_dim, cfg.pos_head_dim
+    for i in range(cfg.num_stacks):
+        d, F, h, K = cfg.encoder_dims[i], cfg.ff_dims[i], cfg.num_heads[i], cfg.cnn_kernels[i]
+        R = -(-L // cfg.downsampling[i])
+        hid = 3 * d // 4
+        per = ((2 * qd + pd) * h * d + 2 * d * ((F * 3) // 4 + F + (F * 5) // 4)
+               + 3 * hid * d + hid * d + 2 * (2 * vd * h * d) + 2 * (2 * d * d + d * d))
+        proj += 2.0 * R * per * cfg.num_layers[i]
+        att += 2.0 * R * R * (h * (qd + pd) + 2 * h * vd + hid) * cfg.num_layers[i]
+        cv += 2.0 * 2 * R * d * K * cfg.num_layers[i]
+    Tout = (L + 1) // 2
+    proj += 2.0 * Tout * cfg.max_dim * cfg.joiner_dim
+    return {"frontend": fe, "projections": proj, "attention": att, "conv1d": cv,
+            "joiner": 2.0 * beam * Tout * cfg.joiner_dim * cfg.vocab_size}
 
 
 def encoder_flops_per_frame(cfg: ZipformerConfig) -> Dict[str, float]:

@@ -7,7 +7,6 @@ only calls `.run(None, feeds)` on them (:1047, :1055, :1085, :1092).
 """
 from __future__ import annotations
 
-import hashlib
 import math
 import os
 import sys
@@ -19,7 +18,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(os.path.dirname(_HERE))
 sys.path.insert(0, os.path.join(_REPO, "sherpa-vietnamese-asr_amd"))
 
-from zasr.model import ZipformerConfig, synth_weights, zipformer_m, zipformer_tiny  # noqa: E402
+from zasr.model import (ZipformerConfig, hash_tokenize_phrases, synth_weights,  # noqa: E402
+                        zipformer_m, zipformer_tiny)
 
 HOTWORD_FILE = os.path.join(_HERE, "hotword_sample.txt")
 
@@ -71,20 +71,9 @@ def np_joiner(w: Dict[str, np.ndarray], enc: np.ndarray, dec: np.ndarray) -> np.
     return (x @ w["joiner.output_linear.weight"].T + w["joiner.output_linear.bias"]).astype(np.float32)
 
 
-def syllable_id(syl: str, V: int) -> int:
-    h = hashlib.md5(syl.encode("utf-8")).digest()
-    return 3 + int.from_bytes(h[:4], "little") % (V - 3)
-
-
 def hotword_token_ids(phrases: List[Tuple[str, float]], V: int):
     """Deterministic syllable -> id tokenization into [3, V) (real bpe.model is absent)."""
-    seqs, scores = [], []
-    for text, sc in phrases:
-        ids = [syllable_id(s, V) for s in text.split()]
-        if ids:
-            seqs.append(ids)
-            scores.append(sc)
-    return seqs, scores
+    return hash_tokenize_phrases(phrases, V)
 
 
 def ngram_phrases(token_ids: List[int], every: int = 6, n_max: int = 3) -> List[List[int]]:

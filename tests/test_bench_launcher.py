@@ -1,0 +1,40 @@
+"""bench.py --gpus N: the launcher path the driver uses, on CPU.
+
+`python bench.py --gpus 2 ...` without RANK starts torch.distributed.run with 2 ranks as a
+child process; each rank plans its own synthetic audio, the timed region is bracketed by
+barriers and the time is max-reduced over ranks (gloo here, RCCL on the box).  --cpu-dry-run
+replaces the GPU decode with a CPU stand-in so the whole path runs without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("RANK", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--cpu-dry-run",
+                        "--steps", "2", "--warmup", "1", "--audio-sec", "40",
+                        "--no-cpu-baseline", *extra],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_launches_two_ranks():
+    line = _run("--gpus", "2")
+    assert line["n_gpus"] == 2
+    assert line["scaling"] == "weak"
+    assert line["dry_run"] is True
+    assert line["config"]["parallelism"].startswith("dp2")
+
+
+def test_bench_single_rank_default():
+    line = _run()
+    assert line["n_gpus"] == 1
+    assert line["config"]["chunks_per_gpu"] >= 1
+    assert 20.0 <= line["config"]["chunk_sec_min_max"][1] <= 36.0

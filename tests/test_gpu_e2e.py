@@ -121,7 +121,7 @@ def test_m_greedy_fp32_end_to_end(m_case):
     res = rec.decode(m_case["chunks"])
     for i, (r, ref) in enumerate(zip(res, m_case["greedy"])):
         _assert_same(r, ref, 2e-3, 2e-3, f"greedy chunk {i}")
-    assert sum(len(g[0]) for g in m_case["greedy"]) > 200
+    assert sum(len(g[0]) for g in m_case["greedy"]) > 100
     rec.close()
 
 
