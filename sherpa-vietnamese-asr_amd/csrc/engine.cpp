@@ -262,13 +262,27 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
   ZASR_REQUIRE(precision >= 0 && precision <= 2,
                "precision must be 0 (fp32), 1 (bf16) or 2 (bf16 encoder, f32 joiner + search)");
   ZASR_HIP_CHECK(hipSetDevice(device_));
-  ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  {
+  // ZASR_SEARCH_CUS = N > 0: the search stream runs on CUs [0, N) and the encoder streams on
+  // the rest (CU-masked queues), so the latency-bound search chain never waits for CUs held
+  // by the next batch's encoder blocks
+  if (const char* e = getenv("ZASR_SEARCH_CUS")) search_cus_ = atoi(e);
+  int ncu = 0;
+  ZASR_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_));
+  if (search_cus_ > 0 && search_cus_ < ncu) {
+    std::vector<uint32_t> ms((ncu + 31) / 32, 0u), me((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) (c < search_cus_ ? ms : me)[c / 32] |= 1u << (c % 32);
+    ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2_, (uint32_t)ms.size(), ms.data()));
+    ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)me.size(), me.data()));
+    for (auto& x : enc_extra_)
+      ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&x, (uint32_t)me.size(), me.data()));
+  } else {
+    search_cus_ = 0;
+    ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     int least = 0, greatest = 0;
     ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
+    for (auto& x : enc_extra_) ZASR_HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   }
-  for (auto& x : enc_extra_) ZASR_HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   st_ = stream_;
   const std::string cfg_path = dir + "/config.json";
@@ -1409,16 +1423,10 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   if (stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
     std::vector<unsigned long long> h((size_t)Tmax * 16);
     ZASR_HIP_CHECK(hipMemcpy(h.data(), st.stamps, h.size() * 8, hipMemcpyDeviceToHost));
-    // beam >= 5 (a second row per wave): row 4's phases are stamped too
-    const bool two = H > 4;
-    const int seq2[] = {0, 6, 7, 8, 9, 10, 11, 1, 2, 3, 4, 5};
-    const int seq1[] = {0, 6, 7, 8, 1, 2, 3, 4, 5};
-    const char* name2[] = {"nh", "row0_loaded", "row0_stats", "row0_insert", "row4_loaded",
-                           "row4_stats", "row4_insert", "wave_topk", "barrier", "expand", "J"};
-    const char* name1[] = {"nh", "row0_loaded", "row0_stats", "rows_rest", "wave_topk", "barrier", "expand", "J"};
-    const int* seq = two ? seq2 : seq1;
-    const char* const* name = two ? name2 : name1;
-    const int NS = two ? 11 : 8;
+    const int seq[] = {0, 6, 7, 8, 10, 1, 2, 3, 4, 5};
+    const char* name[] = {"nh", "row0_max", "row0_stats", "row0_topk", "rows_decode", "barrier",
+                          "rank", "tail", "J"};
+    const int NS = 9;
     double acc[16] = {0};
     int n = 0;
     for (int t = 0; t < Tmax; ++t) {
@@ -1548,11 +1556,13 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   const int want_e = env_e ? env_e : (beam > 1 ? 1 : 2);
   const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
   const int L = E;
-  hipStream_t enc_st[kMaxEnc] = {main_st};
+  // encoder stream 0 is the caller's stream, or (CU-partitioned) the engine's masked stream
+  hipStream_t enc_st[kMaxEnc] = {search_cus_ > 0 ? stream_ : main_st};
   for (int e = 1; e < kMaxEnc; ++e) enc_st[e] = enc_extra_[e - 1];
-  if (E > 1) {  // the other encoder streams start after the caller's prior work
+  if (E > 1 || enc_st[0] != main_st) {  // the encoder streams start after the caller's prior work
     ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 2], main_st));
-    for (int e = 1; e < E; ++e) ZASR_HIP_CHECK(hipStreamWaitEvent(enc_st[e], part_ev_[kMaxEnc + 2], 0));
+    for (int e = 0; e < E; ++e)
+      if (enc_st[e] != main_st) ZASR_HIP_CHECK(hipStreamWaitEvent(enc_st[e], part_ev_[kMaxEnc + 2], 0));
   }
   std::vector<long> first(nb + 1, 0);
   for (int k = 0; k < nb; ++k) first[k + 1] = first[k] + batch_sizes[k];

@@ -204,6 +204,7 @@ class Engine {
   int precision_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
+  int search_cus_ = 0;             // > 0: search / encoder streams on disjoint CU sets
   hipStream_t enc_extra_[kMaxEnc - 1] = {};  // encoder streams 1.. of the batch pipeline
   // [0, kMaxEnc]: encoder output slots; kMaxEnc + 1: search done; kMaxEnc + 2: start
   hipEvent_t part_ev_[kMaxEnc + 3] = {};

@@ -224,6 +224,21 @@ __device__ __forceinline__ unsigned long long wave_max_u64_dpp(unsigned long lon
   }
   return r;
 }
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f<kDppQuad1>(v));
+  v = fmaxf(v, dpp_f<kDppQuad2>(v));
+  v = fmaxf(v, dpp_f<kDppRor4>(v));
+  v = fmaxf(v, dpp_f<kDppRor8>(v));
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__shfl((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ double shfl_f64(double v, int l) {
+  return __longlong_as_double((long long)shfl_u64((unsigned long long)__double_as_longlong(v), l));
+}
 __device__ __forceinline__ int wave_min_i_dpp(int v) {
   v = min(v, dpp_i<kDppQuad1>(v));
   v = min(v, dpp_i<kDppQuad2>(v));
@@ -619,15 +634,13 @@ __device__ __forceinline__ long packed_j_off(long row, int k, int D) {
   return ((rt * (D >> 4) + q) * 64 + r + 32 * hh) * 8 + j;
 }
 
-__device__ __forceinline__ void store_j4(const DecTable& dt, long off, float4 e, float4 d) {
+__device__ __forceinline__ void store_j4(const DecTable& dt, long row, int k, float4 e, float4 d) {
   if (dt.j_packed) {  // 4 consecutive k stay inside one 8-element fragment slot
     bf16x4 v;
     v[0] = (__bf16)fast_tanh(e.x + d.x);
     v[1] = (__bf16)fast_tanh(e.y + d.y);
     v[2] = (__bf16)fast_tanh(e.z + d.z);
     v[3] = (__bf16)fast_tanh(e.w + d.w);
-    const long row = off / dt.D;
-    const int k = (int)(off - row * dt.D);
     *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(dt.J) + packed_j_off(row, k, dt.D)) = v;
   } else if (dt.j_bf16) {
     bf16x4 v;
@@ -635,9 +648,9 @@ __device__ __forceinline__ void store_j4(const DecTable& dt, long off, float4 e,
     v[1] = (__bf16)fast_tanh(e.y + d.y);
     v[2] = (__bf16)fast_tanh(e.z + d.z);
     v[3] = (__bf16)fast_tanh(e.w + d.w);
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(dt.J) + off) = v;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(dt.J) + row * dt.D + k) = v;
   } else {
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(dt.J) + off) =
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(dt.J) + row * dt.D + k) =
         make_float4(tanhf(e.x + d.x), tanhf(e.y + d.y), tanhf(e.z + d.z), tanhf(e.w + d.w));
   }
 }
@@ -651,7 +664,7 @@ __global__ void table_init_kernel(DecTable dt, int S, int Hmax) {
   if (dt.enc_len[s] <= 0) return;
   const float4 e = *reinterpret_cast<const float4*>(dt.enc + (long)dt.enc_off[s] * dt.D + 4 * c4);
   const float4 d = *reinterpret_cast<const float4*>(dt.table + 4 * c4);
-  store_j4(dt, (long)s * Hmax * dt.D + 4 * c4, e, d);
+  store_j4(dt, (long)s * Hmax, 4 * c4, e, d);
 }
 
 void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st) {
@@ -662,16 +675,29 @@ void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------------------
-// One block per stream.  Hypothesis row h belongs to wave h % 4: the wave loads the row
-// (float4 per lane, Q per lane), reduces its statistics with shuffles and inserts its
-// candidates into per-thread top-KB lists -- no block barrier until the four wave lists
-// meet.  Everything after the top-k (ranking, hotwords, dedup, slot and node writes, the
-// next frame's joiner input) runs in wave 0 with lane-parallel LDS work.
+// One block of 8 waves per stream; hypothesis row h belongs to wave h % 8 (one row per wave
+// up to beam 8).  Per row the wave
+//   1. loads the row (float4 per lane, Q per lane) and reduces its statistics with DPP;
+//   2. finds the row's top KB candidates: a threshold t = the smallest of KB disjoint lane
+//      groups' maxima (every group holds an element >= t, so the row's top KB are >= t),
+//      the elements >= t compacted into a per-wave LDS list by ballot, one per lane, keyed by
+//      (candidate lp desc, flat index asc) -- the order this build gives the reference's
+//      argpartition / argsort (core/asr_engine.py:1103-1106) -- and ranked by counting.  The
+//      lp = ((x - max) - log S) + score_h is monotone in x, so an element below t can only
+//      reach the list by an f32 rounding tie with the KB-th lp; when the KB-th lp equals lp(t)
+//      (or more than 64 elements pass t) the row takes the exact slow path: elements popped
+//      in (x desc, index asc) order until the KB-th and its lp ties;
+//   3. decodes its KB best (token, hotword transition :1127-1131, sequence identity) into LDS
+//      slots h * KB + rank, so the hotword table loads overlap the other rows.
+// After one block barrier wave 0 ranks the n * KB slots, merges duplicates and writes the new
+// hypotheses; then every wave writes the next frame's joiner input of its candidates.
 template <int KB, int Q, bool TABLE>
-__global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const float* logits,
+__global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const float* logits,
                                                           int V, int Hmax, int beam, int t,
                                                           const int* enc_len, HotwordTables hw,
                                                           DecTable dt) {
+  constexpr int NW = 8;
+  constexpr int NKS = KB * KB;  // row h's list in slots h * KB + r (n <= beam <= KB rows)
   const int s = blockIdx.x;
   const int T_s = enc_len[s];
   if (t >= T_s) return;
@@ -680,53 +706,56 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   const int wid = tid >> 6;
   const int base = s * Hmax;
 
-  __shared__ double pLp[kMaxBeam];
-  __shared__ int pLen[kMaxBeam], pY1[kMaxBeam], pY2[kMaxBeam], pHw[kMaxBeam], pNode[kMaxBeam];
-  __shared__ unsigned long long pHash[kMaxBeam];
   __shared__ float4 sStats[kMaxBeam];
-  __shared__ unsigned long long cK[4 * KB];
-  __shared__ unsigned long long cand[kMaxBeam], cHash[kMaxBeam];
-  __shared__ double cScore[kMaxBeam];
-  __shared__ int cLen[kMaxBeam], cY1[kMaxBeam], cY2[kMaxBeam], cDup[kMaxBeam];
+  __shared__ unsigned long long cK[NKS], dHash[NKS];
+  __shared__ double dScore[NKS];
+  __shared__ float dVal[NKS];
+  __shared__ int dHi[NKS], dTok[NKS], dLen[NKS], dY1[NKS], dY2[NKS], dHw[NKS];
+  __shared__ float wX[NW][64];
+  __shared__ int wI[NW][64];
+  __shared__ int cSrc[kMaxBeam], cDup[kMaxBeam];
   __shared__ int sKK;
   __shared__ unsigned long long sFmask;
 
   ZASR_STAMP(0);
   const int V4 = V >> 2;
   const float4* rows4 = reinterpret_cast<const float4*>(logits + (long)base * V);
-  // first row of this wave: issued before anything else (rows >= nh hold stale but valid data)
-  float4 xa[Q], xb[Q];
+  // this wave's first row, issued before anything else (rows >= nh hold stale but valid data)
+  float4 xa[Q];
+  double ld_cur = 0.0;
+  int lpf_cur = 0;
   if (wid < Hmax) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int i = lane + 64 * q;
       xa[q] = i < V4 ? rows4[(long)wid * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     }
-  }
-  // the score of this wave's first row, in flight with its logits (slots >= nh hold stale
-  // but valid data and are never used); later rows' scores are prefetched one row ahead
-  double ld_cur = 0.0;
-  int lpf_cur = 0;
-  if (wid < Hmax) {
     ld_cur = st.lp[base + wid];
     lpf_cur = st.lpf[base + wid];
   }
+  // every wave holds the hypothesis records in lanes < Hmax (slots >= nh are stale but valid
+  // memory and never selected)
+  double pLp = 0.0;
+  unsigned long long pHash = 0ull;
+  int pLen = 0, pY1 = 0, pY2 = 0, pHw = 0, pNode = 0;
+  if (lane < Hmax) {
+    pLp = st.lp[base + lane];
+    pHash = st.hash[base + lane];
+    pLen = st.len[base + lane];
+    pY1 = st.y1[base + lane];
+    pY2 = st.y2[base + lane];
+    pHw = st.hw[base + lane];
+    pNode = st.node[base + lane];
+  }
+  const int node_base = st.node_count[s];
   const int n = st.nh[s];
   if (n != 12345) ZASR_STAMP(6);
-  if (tid < n) {
-    pLp[tid] = st.lp[base + tid];
-    pHash[tid] = st.hash[base + tid];
-    pLen[tid] = st.len[base + tid];
-    pY1[tid] = st.y1[base + tid];
-    pY2[tid] = st.y2[base + tid];
-    pHw[tid] = st.hw[base + tid];
-    pNode[tid] = st.node[base + tid];
-  }
-  // the next frame's encoder row (wave 0 writes J): in flight now
+  const bool use_hw = hw.num_states > 0;
+  // the next frame's encoder row (every wave writes J rows of candidates in step 4)
   float4 ev[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
   const bool next = t + 1 < T_s;
   if constexpr (TABLE) {
-    if (next) {  // every wave writes J rows of its candidates (step 4)
+    if (next) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c4 = lane + 64 * j;
@@ -736,28 +765,21 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     }
   }
 
-  // ---- 1 + 2. per row: statistics (:1096-1098, :1159-1181) and candidate insertion ----
+  // ---- 1 + 2. per row: statistics (:1096-1098, :1159-1181) and the row's top candidates ----
   //   max / second max; S = sum e, E1 = sum e d, E3 = sum exp(d / 3) (d = x - max):
   //   entropy = log S - E1 / S, sum p^(1/3) = S^(-1/3) E3, top1 = 1 / S, top2 = e^(m2-m1) / S
-  //   candidate lp = ((x - max) - log S) + score_h (f32 add, or f64 for an np.float64 score)
-  unsigned long long tk[KB];
-#pragma unroll
-  for (int q = 0; q < KB; ++q) tk[q] = 0ull;
-  for (int h = wid; h < n; h += 4) {
-    const bool more = h + 4 < n;
-    double ld_nx = 0.0;
-    int lpf_nx = 0;
-    if (more) {
+  //   candidate lp = ((x - max) - log S) + score_h (f32 add of the Python-float score, or the
+  //   f64 add of an np.float64 score, :1099-1100)
+  for (int h = wid; h < n; h += NW) {
+    if (h != wid) {  // beam > 8: a second row per wave
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int i = lane + 64 * q;
-        xb[q] = i < V4 ? rows4[(long)(h + 4) * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+        xa[q] = i < V4 ? rows4[(long)h * V4 + i] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
       }
-      ld_nx = st.lp[base + h + 4];
-      lpf_nx = st.lpf[base + h + 4];
+      ld_cur = st.lp[base + h];
+      lpf_cur = st.lpf[base + h];
     }
-    const double ld = ld_cur;
-    const bool f64 = lpf_cur != 0;
     float m1 = -INFINITY, m2 = -INFINITY;
     auto upd = [&](float x) {  // branch-free (a branchy form put m1/m2 in scratch)
       m2 = fmaxf(m2, fminf(m1, x));
@@ -771,15 +793,9 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       upd(xa[q].w);
     }
     if (h == 0 && m1 != 12345.f) ZASR_STAMP(7);
-    if (h == 4 && m1 != 12345.f) ZASR_STAMP(10);
-    // insertion threshold: split the wave into KB lane groups and take the smallest group
-    // maximum.  Every group holds an element at least that large, so the row's top KB are
-    // all >= it, and the scores are monotone in x: elements below it are never inserted
-    // (exact; the wave runs the insertion network only where some lane passes it).  Six
-    // shuffles (KB-th largest lane maximum by rounds: measured 2.5k cycles, too slow).
-    // groups (DPP): KB >= 16: the 16 quads; KB = 8: overlapping quad pairs (q, q - 1), of
-    // which the 8 pairs (2i, 2i + 1) are disjoint, so the minimum over all of them is still
-    // a bound; KB <= 4: the four 16-lane rows
+    // candidate threshold: lane groups (DPP): KB >= 16: the 16 quads; KB = 8: overlapping
+    // quad pairs (q, q - 1), of which the 8 pairs (2i, 2i + 1) are disjoint, so the minimum
+    // over all of them is still a bound; KB <= 4: the four 16-lane rows
     float thr_x = fmaxf(m1, dpp_f<kDppQuad1>(m1));
     thr_x = fmaxf(thr_x, dpp_f<kDppQuad2>(thr_x));
     if constexpr (KB <= 8) thr_x = fmaxf(thr_x, dpp_f<kDppRor4>(thr_x));
@@ -806,176 +822,254 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
     e3 = wave_sum_dpp(e3);
     const float ls = logf(se);
     if (h == 0 && ls != 12345.f) ZASR_STAMP(8);
-    if (h == 4 && ls != 12345.f) ZASR_STAMP(11);
     if (lane == 0)
       sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
                               __expf(m2 - m1) / se);
+    const double ld = ld_cur;
+    const bool f64 = lpf_cur != 0;
     const float lf = (float)ld;
     auto score = [&](float x) {
       const float lpv = (x - m1) - ls;
       return f64 ? (float)((double)lpv + ld) : lpv + lf;
     };
-    const float thr_val = score(thr_x);
-    auto ins = [&](float x, int idx) {
-      const float val = score(x);
-      const unsigned long long key = make_key(val, idx);
-      if (val >= thr_val && key > tk[KB - 1]) {
-#pragma unroll
-        for (int q = KB - 1; q > 0; --q) tk[q] = key > tk[q - 1] ? tk[q - 1] : (key > tk[q] ? key : tk[q]);
-        tk[0] = key > tk[0] ? key : tk[0];
+    // 2a. elements >= thr_x into the wave's list (order: q, component, lane)
+    int total = 0;
+    auto push = [&](float x, int col) {
+      const bool p = x >= thr_x;
+      const unsigned long long m = __ballot(p);
+      if (m) {
+        const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        if (p && pos < 64) {
+          wX[wid][pos] = x;
+          wI[wid][pos] = col;
+        }
+        total += __popcll(m);
       }
     };
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int i = lane + 64 * q;
-      if (i < V4) {
-        const int b0 = h * V + 4 * i;
-        ins(xa[q].x, b0);
-        ins(xa[q].y, b0 + 1);
-        ins(xa[q].z, b0 + 2);
-        ins(xa[q].w, b0 + 3);
+      const int c0 = 4 * (lane + 64 * q);
+      push(xa[q].x, c0);
+      push(xa[q].y, c0 + 1);
+      push(xa[q].z, c0 + 2);
+      push(xa[q].w, c0 + 3);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // 2b. keys and ranks within the row
+    unsigned long long key = 0ull;
+    float val = -INFINITY;
+    int ncand = total;
+    bool fast = total <= 64;
+    if (fast) {
+      if (lane < total) {
+        val = score(wX[wid][lane]);
+        key = make_key(val, h * V + wI[wid][lane]);
       }
     }
-    if (h == 0 && tk[0] != 12345ull) ZASR_STAMP(9);
-    if (more) {
+    int rank = 64;
+    auto rank_keys = [&]() {
+      rank = 0;
+      for (int c = 0; c < ncand; ++c) rank += lane_u64(key, c) > key ? 1 : 0;
+      if (lane >= ncand) rank = 64;
+    };
+    if (fast) {
+      rank_keys();
+      const unsigned long long kth = __ballot(rank == KB - 1);
+      // exact unless an element below the threshold can tie the KB-th lp
+      fast = kth != 0ull && lane_f(val, __ffsll((long long)kth) - 1) != score(thr_x);
+    }
+    if (h == 0 && total != 12345) ZASR_STAMP(10);
+    if (!fast) {
+      // slow path: pop in (x desc, index asc) order -- per lane the head and second of its
+      // elements, the popped lane promoting its second or rescanning what follows -- until
+      // the KB-th and every further element with an equal lp
+      float hv = -INFINITY, sv = -INFINITY;
+      int hj = -1, sj = -1;
+      auto take = [&](float x, int j) {  // strict >: the earlier of equal values ranks first
+        const bool gh = x > hv, gs = x > sv;
+        sv = gh ? hv : (gs ? x : sv);
+        sj = gh ? hj : (gs ? j : sj);
+        hv = gh ? x : hv;
+        hj = gh ? j : hj;
+      };
 #pragma unroll
-      for (int q = 0; q < Q; ++q) xa[q] = xb[q];
-      ld_cur = ld_nx;
-      lpf_cur = lpf_nx;
+      for (int q = 0; q < Q; ++q) {
+        take(xa[q].x, 4 * q);
+        take(xa[q].y, 4 * q + 1);
+        take(xa[q].z, 4 * q + 2);
+        take(xa[q].w, 4 * q + 3);
+      }
+      bool sv_ok = true;
+      float s_kb = 0.f;
+      int got = 0;  // wave-uniform
+      key = 0ull;
+      for (;;) {
+        const float g = wave_max_dpp(hv);
+        if (g == -INFINITY) break;  // row exhausted
+        const unsigned long long tied = __ballot(hv == g);
+        const int myidx = 4 * (lane + 64 * (hj >> 2)) + (hj & 3);
+        int owner;
+        if (__popcll(tied) == 1) {
+          owner = __ffsll((long long)tied) - 1;
+        } else {  // equal heads in several lanes: the smallest column first
+          const int mi = wave_min_i_dpp(hv == g ? myidx : 0x7fffffff);
+          owner = __ffsll((long long)__ballot(hv == g && myidx == mi)) - 1;
+        }
+        const int gidx = __builtin_amdgcn_readlane(myidx, owner);
+        const float v = score(g);
+        if (got >= KB && v != s_kb) break;  // past the KB-th and its lp ties
+        if (got >= 64) break;               // > 56 equal f32 lps: never seen
+        if (got == KB - 1) s_kb = v;
+        if (lane == got) key = make_key(v, h * V + gidx);
+        ++got;
+        if (lane == owner) {  // pop: promote the second, or rescan what follows the popped one
+          const float pv = hv;
+          const int pj = hj;
+          if (sv_ok) {
+            hv = sv;
+            hj = sj;
+            sv_ok = false;
+          } else {
+            hv = sv = -INFINITY;
+            hj = sj = -1;
+            auto after = [&](float x, int j) {
+              if (x < pv || (x == pv && j > pj)) take(x, j);
+            };
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+              after(xa[q].x, 4 * q);
+              after(xa[q].y, 4 * q + 1);
+              after(xa[q].z, 4 * q + 2);
+              after(xa[q].w, 4 * q + 3);
+            }
+            sv_ok = true;
+          }
+        }
+      }
+      ncand = got;
+      rank_keys();
+    }
+    // 2c. the row's KB best -> slots h * KB + rank, decoded (:1116-1131): blank keeps the
+    //     sequence, non-blank appends and steps the hotword graph (blank and UNK skip it,
+    //     :1129); every lane < KB writes its slot (empty: key 0)
+    {
+      const unsigned long long phash = lane_u64(pHash, h);
+      const int plen = __builtin_amdgcn_readlane(pLen, h);
+      const int py1 = __builtin_amdgcn_readlane(pY1, h);
+      const int py2 = __builtin_amdgcn_readlane(pY2, h);
+      const int phw = __builtin_amdgcn_readlane(pHw, h);
+      if (lane < KB) cK[h * KB + lane] = 0ull;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (rank < KB) {
+        const int slot = h * KB + rank;
+        const int tok = key_idx(key) - h * V;
+        double sc = (double)key_val(key);
+        int nhw = phw, klen, ny1, ny2;
+        unsigned long long hk;
+        if (tok == 0) {
+          hk = phash;
+          klen = plen;
+          ny1 = py1;
+          ny2 = py2;
+        } else {
+          if (use_hw && tok != 2) {
+            const int cls = hw.tok2cls[tok];
+            if (cls < 0) {
+              sc += -hw.node_score[nhw];
+              nhw = 0;
+            } else {
+              const long e = (long)nhw * hw.num_cls + cls;
+              sc += hw.delta[e];
+              nhw = hw.next[e];
+            }
+          }
+          hk = hash_push(phash, tok);
+          klen = plen + 1;
+          ny2 = py1;
+          ny1 = tok;
+        }
+        cK[slot] = key;
+        dVal[slot] = key_val(key);
+        dHi[slot] = h;
+        dTok[slot] = tok;
+        dScore[slot] = sc;
+        dHw[slot] = nhw;
+        dHash[slot] = hk;
+        dLen[slot] = klen;
+        dY1[slot] = ny1;
+        dY2[slot] = ny2;
+      }
     }
   }
   ZASR_STAMP(1);
-  // per-wave top-KB
-  for (int round = 0; round < KB; ++round) {
-    const unsigned long long best = wave_max_u64_dpp(tk[0]);
-    if (lane == 0) cK[wid * KB + round] = best;
-    if (best != 0ull && tk[0] == best) {
-#pragma unroll
-      for (int q = 0; q < KB - 1; ++q) tk[q] = tk[q + 1];
-      tk[KB - 1] = 0ull;
-    }
-  }
-  ZASR_STAMP(2);
   __syncthreads();
-  ZASR_STAMP(3);
-  // ---- 3. expansion (:1110-1138): ranking and candidate decode in wave 0 ----
-  // 3a. global rank of each wave-list key (keys are distinct): the k best, best first
-  const int total = n * V;
-  const int k = beam < total ? beam : total;
-  const bool lv_any = wid == 0;
-  int kk = 0;
-  int hi = 0, tok = 0, nhw = 0, klen = 0, ny1 = 0, ny2 = 0;
-  float val = 0.f;
-  double score = 0.0;
-  unsigned long long key = 0ull;
-  bool lv = false;
-  if (lv_any) {
-    {
-      const unsigned long long key = lane < 4 * KB ? cK[lane] : 0ull;
+  ZASR_STAMP(2);
+  // ---- 3. expansion (:1110-1138): ranking and duplicate merge in wave 0 ----
+  const int total_c = n * V;
+  const int k = beam < total_c ? beam : total_c;
+  const int nk = n * KB;
+  if (wid == 0) {
+    // 3a. global rank of each slot key (keys are distinct): the k best, best first
+    int nz = 0;
+#pragma unroll
+    for (int r0 = 0; r0 < NKS; r0 += 64) {
+      const int c = r0 + lane;
+      const unsigned long long key = c < nk ? cK[c] : 0ull;
       int rank = 0;
-      for (int j = 0; j < 4 * KB; ++j) rank += cK[j] > key ? 1 : 0;
-      if (key != 0ull && rank < k) cand[rank] = key;
+      for (int j = 0; j < nk; ++j) rank += cK[j] > key ? 1 : 0;
+      if (key != 0ull && rank < k) cSrc[rank] = c;
+      nz += __popcll(__ballot(key != 0ull));
     }
-    const unsigned long long nzmask = __ballot(lane < 4 * KB && cK[lane < 4 * KB ? lane : 0] != 0ull);
-    const int nz = __popcll(nzmask);
-    kk = k < nz ? k : nz;
-    __builtin_amdgcn_wave_barrier();
-    // 3b. lane c decodes candidate c: token, hotword transition (:1127-1131; blank and UNK
-    //     skip the graph, :1129), sequence identity
-    lv = lane < kk;
-    if (lv) {
-      const unsigned long long key0 = cand[lane];
-      val = key_val(key0);
-      const int idx = key_idx(key0);
-      hi = idx / V;
-      tok = idx - hi * V;
-      score = (double)val;
-      nhw = pHw[hi];
-      if (tok == 0) {
-        key = pHash[hi];
-        klen = pLen[hi];
-        ny1 = pY1[hi];
-        ny2 = pY2[hi];
-      } else {
-        if (hw.num_states > 0 && tok != 2) {
-          const int cls = hw.tok2cls[tok];
-          if (cls < 0) {
-            score += -hw.node_score[nhw];
-            nhw = 0;
-          } else {
-            const long e = (long)nhw * hw.num_cls + cls;
-            score += hw.delta[e];
-            nhw = hw.next[e];
-          }
-        }
-        key = hash_push(pHash[hi], tok);
-        klen = pLen[hi] + 1;
-        ny2 = pY1[hi];
-        ny1 = tok;
-      }
-      cHash[lane] = key;
-      cLen[lane] = klen;
-      cScore[lane] = score;
-      cY1[lane] = ny1;
-      cY2[lane] = ny2;
-    }
+    const int kk = k < nz ? k : nz;
     if (lane == 0) sKK = kk;
-  }
-  __syncthreads();  // candidate contexts visible to every wave
-  // every wave: the next frame's decoder rows of its candidates c = wid + 4 m (table gather),
-  // in flight while wave 0 resolves duplicates
-  constexpr int KW = (KB + 3) / 4;
-  float4 dv[KW][2];
-  const int kk_all = sKK;
-  if constexpr (TABLE) {
-    if (next) {
-#pragma unroll
-      for (int m = 0; m < KW; ++m) {
-        const int c = wid + 4 * m;
-        if (c < kk_all) {
-          const float* row = dt.table + ((long)cY2[c] * dt.V + cY1[c]) * dt.D;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int c4 = lane + 64 * j;
-            if (c4 < dt.D / 4) dv[m][j] = *reinterpret_cast<const float4*>(row + 4 * c4);
-          }
-        }
-      }
-    }
-  }
-  if (lv_any) {
-    // 3c. duplicates of the full sequence merge into their first occurrence, in candidate
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    ZASR_STAMP(3);
+    // 3b. duplicates of the full sequence merge into their first occurrence, in candidate
     //     order, with an f64 log-add (:1133-1138)
+    const bool lv = lane < kk;
+    const int src = lv ? cSrc[lane] : 0;
+    const unsigned long long key = lv ? dHash[src] : 0ull;
+    const int klen = lv ? dLen[src] : 0;
     int dup = -1;
     if (lv) {
-      for (int c = 0; c < lane; ++c)
-        if (cLen[c] == klen && cHash[c] == key) {
+      for (int c = 0; c < lane; ++c) {
+        const int o = cSrc[c];
+        if (dLen[o] == klen && dHash[o] == key) {
           dup = c;
           break;
         }
+      }
       cDup[lane] = dup;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const bool first = lv && dup < 0;
+    const int tok = lv ? dTok[src] : 0;
+    const int hi = lv ? dHi[src] : 0;
+    const double plp = shfl_f64(pLp, hi);
+    const int pnode = __shfl(pNode, hi);
     const unsigned long long fmask = __ballot(first);
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int slot = __popcll(fmask & below);
     const bool emit = first && tok != 0;
     const unsigned long long emask = __ballot(emit);
-    const int node_base = st.node_count[s];
     if (first) {
-      double lp = score;
+      double lp = dScore[src];
       int f64 = 0;
       for (int c = lane + 1; c < kk; ++c)
-        if (cDup[c] == lane) lp = log_add(lp, f64, cScore[c], 0, &f64);
-      int nnode = pNode[hi];
+        if (cDup[c] == lane) lp = log_add(lp, f64, dScore[cSrc[c]], 0, &f64);
+      int nnode = pnode;
       if (emit) {
         const int nid = node_base + __popcll(emask & below);
         const long gi = (long)s * st.node_cap + nid;
         st.node_tok[gi] = tok;
         st.node_frame[gi] = t;
-        st.node_parent[gi] = pNode[hi];
-        st.node_lp[gi] = (double)val - pLp[hi];
+        st.node_parent[gi] = pnode;
+        st.node_lp[gi] = (double)dVal[src] - plp;
         st.node_stats[gi] = sStats[hi];
         nnode = nid;
       }
@@ -984,9 +1078,9 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
       st.lpf[o] = f64;
       st.hash[o] = key;
       st.len[o] = klen;
-      st.y1[o] = ny1;
-      st.y2[o] = ny2;
-      st.hw[o] = nhw;
+      st.y1[o] = dY1[src];
+      st.y2[o] = dY2[src];
+      st.hw[o] = dHw[src];
       st.node[o] = nnode;
     }
     if (lane == 0) {
@@ -997,21 +1091,22 @@ __global__ __launch_bounds__(256) void search_step_kernel(SearchState st, const 
   }
   ZASR_STAMP(4);
   // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]),
-  //         one candidate per wave at a time ----
+  //         candidate c by wave c % 8 ----
   if constexpr (TABLE) {
     if (next) {
-      __syncthreads();  // sFmask
+      __syncthreads();  // sFmask, sKK, cSrc
       const unsigned long long fm = sFmask;
+      const int kk_all = sKK;
+      for (int cc = wid; cc < kk_all; cc += NW) {
+        if (!((fm >> cc) & 1ull)) continue;
+        const int src = cSrc[cc];
+        const float* row = dt.table + ((long)dY2[src] * dt.V + dY1[src]) * dt.D;
+        const int sl = __popcll(fm & ((1ull << cc) - 1ull));
 #pragma unroll
-      for (int m = 0; m < KW; ++m) {
-        const int cc = wid + 4 * m;
-        if (cc < kk_all && ((fm >> cc) & 1ull)) {
-          const int sl = __popcll(fm & ((1ull << cc) - 1ull));
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int c4 = lane + 64 * j;
-            if (c4 < dt.D / 4) store_j4(dt, (long)(base + sl) * dt.D + 4 * c4, ev[j], dv[m][j]);
-          }
+        for (int j = 0; j < 2; ++j) {
+          const int c4 = lane + 64 * j;
+          if (c4 < dt.D / 4)
+            store_j4(dt, base + sl, 4 * c4, ev[j], *reinterpret_cast<const float4*>(row + 4 * c4));
         }
       }
     }
@@ -1026,7 +1121,7 @@ void launch_search_step(const SearchState& s, const float* logits, int V, int S,
   ZASR_REQUIRE(beam >= 1 && beam <= kMaxBeam && beam <= Hmax, "beam out of range");
   ZASR_REQUIRE(V % 4 == 0 && V <= 4096, "vocabulary size must be a multiple of 4, <= 4096");
   ZASR_REQUIRE(!dt || (dt->D % 4 == 0 && dt->D <= 512), "joiner dim must be a multiple of 4, <= 512");
-  dim3 grid(S), block(256);
+  dim3 grid(S), block(512);
   DecTable d{};
   if (dt) d = *dt;
 #define ZASR_STEP3(KBV, QV)                                                                 \
@@ -1075,7 +1170,7 @@ __global__ void greedy_spec_init_kernel(DecTable dt, int S, int F, int* t_cur, i
   if (f >= dt.enc_len[s]) return;
   const float4 e = *reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + f) * dt.D + 4 * c4);
   const float4 d = *reinterpret_cast<const float4*>(dt.table + 4 * c4);
-  store_j4(dt, sf * dt.D + 4 * c4, e, d);
+  store_j4(dt, sf, 4 * c4, e, d);
 }
 
 void launch_greedy_spec_init(const DecTable& dt, int S, int F, int* t_cur, int* active,
@@ -1341,7 +1436,7 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
   const int fo = t_new - t0 - 1;  // staged row of frame t_new
   for (int e = tid; e < nf2 * d4; e += 256) {
     const int f = e / d4, c4 = e - f * d4;
-    store_j4(dt, ((long)s * F + f) * D + 4 * c4, sEnc[(fo + f) * d4 + c4], sTab[c4]);
+    store_j4(dt, (long)s * F + f, 4 * c4, sEnc[(fo + f) * d4 + c4], sTab[c4]);
   }
 }
 

@@ -17,8 +17,8 @@ Tolerances (stated as the north star asks):
                  after 800 frames, core/asr_engine.py:1099-1100,1121: f32 ulp 1.2e-4)
   bf16 modes     statistical: the token error rate (edit distance / reference tokens) vs the
                  fp32 oracle is measured, written to gpurun_out/bf16_token_error.json (kept
-                 under profiles/) and bounded by 0.30 (the bound only catches a broken path;
-                 the measured rates are what DESIGN.md §5 reports)
+                 under profiles/) and bounded by 0.15 pooled over the chunks (measured
+                 0.03-0.10; the bound catches a broken path, DESIGN.md §5 reports the rates)
 """
 import json
 import os
@@ -180,7 +180,7 @@ def test_m_bf16_token_error_rate(m_case):
     assert report["fp32/greedy"]["token_error_rate"] == 0.0
     assert report["fp32/beam8_hotwords"]["token_error_rate"] == 0.0
     for k, v in report.items():
-        assert v["token_error_rate"] <= 0.30, (k, v)
+        assert v["token_error_rate"] <= 0.15, (k, v)
 
 
 # ------------------------------------------------------------------ Zipformer-30M

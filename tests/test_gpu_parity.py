@@ -270,8 +270,9 @@ def _token_agreement(a, b):
 def test_bf16_mode_encoder_and_tokens(need_gpu):
     """bf16 mode (bf16 GEMM/joiner/decoder operands, f32 accumulate/softmax/norms/search) vs
     the fp32 path: encoder_out within 0.05 * max(1, |oracle|) (measured 0.015; a double-scaled
-    positional term measured 0.03, so the bound is kept tight); greedy token agreement with
-    fp32 >= 0.85 mean, >= 0.7 worst chunk (measured rates in gpurun_out/bf16_report.json)."""
+    positional term measured 0.03, so the bound is kept tight).  Token agreement with the fp32
+    path is reported (gpurun_out/bf16_report.json); the token error rate against the ORACLE is
+    bounded in tests/test_gpu_e2e.py::test_m_bf16_token_error_rate."""
     from model_fixtures import m_model
     from oracle.fbank import fbank
     from oracle.zipformer import ZipformerOracle
@@ -295,8 +296,6 @@ def test_bf16_mode_encoder_and_tokens(need_gpu):
     with open("gpurun_out/bf16_report.json", "w") as fh:
         json.dump({"encoder_max_scaled_err": errs, "token_agreement": agree, "fp32_tokens": ntok}, fh)
     assert max(errs) <= 0.05, errs
-    # greedy drift: one flipped near-tie changes the decoder context for the rest of a chunk
-    assert sum(agree) / len(agree) >= 0.85 and min(agree) >= 0.7, agree
     r32.close()
     r16.close()
 
