@@ -54,7 +54,8 @@ enum {
 enum { ZASR_PRECISION_FP32 = 0, ZASR_PRECISION_BF16 = 1, ZASR_PRECISION_BF16_ENC = 2 };
 
 typedef struct zasr_config {
-  const char* model_dir;        /* config.json + model.safetensors (+ tokens.txt for hosts) */
+  const char* model_dir;        /* config.json + model.safetensors, or the reference's
+                                   encoder-/decoder-/joiner-*.onnx (+ tokens.txt for hosts) */
   const char* decoding_method;  /* "greedy_search" | "modified_beam_search" */
   int32_t max_active_paths;     /* beam for modified_beam_search, 1..16 (reference: 8) */
   float blank_penalty;          /* must be 0 (the reference applies none) */
@@ -70,6 +71,14 @@ typedef struct zasr_config {
 
 int zasr_create(const zasr_config* cfg, zasr_recognizer** out);
 void zasr_destroy(zasr_recognizer* h);
+
+/* Host-only (no GPU): load a model directory the way zasr_create does -- config.json +
+   model.safetensors, or the reference's encoder-/decoder-/joiner-*.onnx set chosen like
+   create_recognizer (core/asr_engine.py:913-928: non-int8 preferred, int8 dequantized when it
+   is the only file) with the architecture inferred from the initializer shapes -- and write
+   out_dir/config.json + out_dir/model.safetensors (float32, the engine's tensor names).
+   Replaces the ORT session load's file handling; ZASR_ERR_NOT_FOUND when files are missing. */
+int zasr_convert_model(const char* model_dir, const char* out_dir);
 
 /* log-mel fbank of one waveform (f32 in [-1,1], 16 kHz).  out holds cap floats;
    *n_frames = (n + 80) / 160, output row-major [n_frames][80].  h may be NULL

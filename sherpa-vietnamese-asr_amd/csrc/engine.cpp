@@ -18,6 +18,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "host_io.h"
+#include "onnx_io.h"
 
 namespace zasr {
 
@@ -256,11 +257,19 @@ void Engine::pin_reset(int arena) {
   pin_cur_ = arena;
 }
 
-Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const HotwordDFA& hw,
+Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
+               const std::vector<std::vector<int>>& hotwords, const std::vector<float>& hotword_scores,
                int precision)
-    : device_(device), beam_(beam), greedy_(greedy), precision_(precision), hw_host_(hw) {
+    : device_(device), beam_(beam), greedy_(greedy), precision_(precision) {
   ZASR_REQUIRE(precision >= 0 && precision <= 2,
                "precision must be 0 (fp32), 1 (bf16) or 2 (bf16 encoder, f32 joiner + search)");
+  // host side first (no GPU state to unwind when the files are bad): config.json +
+  // model.safetensors, or the reference's encoder-/decoder-/joiner-*.onnx (onnx_io.h;
+  // core/asr_engine.py:913-928)
+  SafeTensors W;
+  ModelConfig cfg = parse_config(load_model_dir(dir, W));
+  model_.cfg = cfg;
+  hw_host_ = build_hotword_dfa(hotwords, hotword_scores, cfg.V);
   ZASR_HIP_CHECK(hipSetDevice(device_));
   // ZASR_SEARCH_CUS = N > 0: the search stream runs on CUs [0, N) and the encoder streams on
   // the rest (CU-masked queues), so the latency-bound search chain never waits for CUs held
@@ -285,14 +294,6 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy, const 
   }
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   st_ = stream_;
-  const std::string cfg_path = dir + "/config.json";
-  const std::string st_path = dir + "/model.safetensors";
-  if (!file_exists(cfg_path) || !file_exists(st_path))
-    throw std::invalid_argument("missing model files in " + dir);
-  ModelConfig cfg = parse_config(read_file(cfg_path));
-  model_.cfg = cfg;
-  SafeTensors W;
-  W.load(st_path);
 
   auto dev = [&](const float* src, size_t n) -> float* {
     float* p = nullptr;

@@ -88,8 +88,11 @@ struct TokenResult {
 
 class Engine {
  public:
+  // model_dir: config.json + model.safetensors or the reference's ONNX files (onnx_io.h);
+  // hotwords: token-id phrases + scores, compiled into the device automaton once V is known
   Engine(const std::string& model_dir, int device, int beam, bool greedy,
-         const HotwordDFA& hw, int precision);
+         const std::vector<std::vector<int>>& hotwords, const std::vector<float>& hotword_scores,
+         int precision);
   ~Engine();
 
   int vocab() const { return model_.cfg.V; }

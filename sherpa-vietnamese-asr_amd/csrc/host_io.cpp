@@ -204,6 +204,18 @@ void SafeTensors::load(const std::string& path) {
   }
 }
 
+void SafeTensors::put(const std::string& name, std::vector<int64_t> shape, std::vector<float>&& data) {
+  size_t n = 1;
+  for (auto d : shape) n *= (size_t)d;
+  if (n != data.size()) throw std::runtime_error("tensor " + name + ": shape / data size mismatch");
+  owned_.push_back(std::move(data));
+  HostTensor ht;
+  ht.shape = std::move(shape);
+  ht.numel = n;
+  ht.data = owned_.back().data();
+  tensors_[name] = ht;
+}
+
 const HostTensor& SafeTensors::get(const std::string& name) const {
   auto it = tensors_.find(name);
   if (it == tensors_.end()) throw std::runtime_error("model: missing tensor " + name);

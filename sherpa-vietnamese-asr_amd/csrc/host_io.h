@@ -2,6 +2,7 @@
 // safetensors loader.  No third-party dependencies.
 #pragma once
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -30,9 +31,11 @@ struct HostTensor {
   size_t numel = 0;
 };
 
+// A named f32 tensor set: a safetensors file (load) and/or tensors added by put (owned).
 class SafeTensors {
  public:
   void load(const std::string& path);
+  void put(const std::string& name, std::vector<int64_t> shape, std::vector<float>&& data);
   bool has(const std::string& name) const { return tensors_.count(name) != 0; }
   const HostTensor& get(const std::string& name) const;
   const std::map<std::string, HostTensor>& all() const { return tensors_; }
@@ -40,6 +43,7 @@ class SafeTensors {
  private:
   std::vector<char> buf_;
   std::vector<float> converted_;
+  std::deque<std::vector<float>> owned_;
   std::map<std::string, HostTensor> tensors_;
 };
 

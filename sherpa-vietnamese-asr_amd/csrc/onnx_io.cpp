@@ -1,0 +1,574 @@
+// ONNX initializer reader (protobuf wire format, onnx.proto field numbers) and the mapping of
+// a reference model directory onto the engine's weight names.  See onnx_io.h.
+#include "onnx_io.h"
+
+#include <dirent.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <set>
+#include <sstream>
+#include <stdexcept>
+
+namespace zasr {
+
+namespace {
+
+// ---------------------------------------------------------------- protobuf wire format
+struct Span {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  std::string str() const { return std::string(reinterpret_cast<const char*>(p), n); }
+};
+
+struct Pb {
+  const uint8_t* p;
+  const uint8_t* end;
+  explicit Pb(Span s) : p(s.p), end(s.p + s.n) {}
+  bool more() const { return p < end; }
+  uint64_t varint() {
+    uint64_t v = 0;
+    for (int sh = 0; sh < 64; sh += 7) {
+      if (p >= end) throw std::runtime_error("onnx: truncated varint");
+      const uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7f) << sh;
+      if (!(b & 0x80)) return v;
+    }
+    throw std::runtime_error("onnx: bad varint");
+  }
+  void key(uint32_t& field, uint32_t& wire) {
+    const uint64_t k = varint();
+    field = (uint32_t)(k >> 3);
+    wire = (uint32_t)(k & 7);
+  }
+  Span bytes() {
+    const uint64_t n = varint();
+    if (n > (uint64_t)(end - p)) throw std::runtime_error("onnx: truncated field");
+    Span s{p, (size_t)n};
+    p += n;
+    return s;
+  }
+  void skip(uint32_t wire) {
+    switch (wire) {
+      case 0: varint(); break;
+      case 1: p += 8; break;
+      case 2: bytes(); break;
+      case 5: p += 4; break;
+      default: throw std::runtime_error("onnx: unsupported wire type");
+    }
+    if (p > end) throw std::runtime_error("onnx: truncated field");
+  }
+};
+
+// onnx.proto TensorProto.DataType
+enum { T_FLOAT = 1, T_UINT8 = 2, T_INT8 = 3, T_INT32 = 6, T_INT64 = 7, T_FLOAT16 = 10,
+       T_DOUBLE = 11, T_BFLOAT16 = 16 };
+
+struct RawTensor {
+  std::string name;
+  std::vector<int64_t> dims;
+  int dtype = 0;
+  Span raw;                  // raw_data (field 9)
+  std::vector<float> f32;    // float_data (field 4)
+  std::vector<int64_t> ints; // int32_data (5) / int64_data (7)
+  std::string ext_location;  // external data (fields 13 / 14)
+  long ext_offset = 0, ext_length = -1;
+};
+
+struct Node {
+  std::string name, op;
+  std::vector<std::string> in, out;
+};
+
+struct OnnxFile {
+  std::string bytes;  // the whole file
+  std::vector<RawTensor> inits;
+  std::vector<Node> nodes;
+};
+
+float half_to_float(uint16_t h) {
+  const uint32_t s = (uint32_t)(h & 0x8000) << 16, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+  uint32_t bits;
+  if (e == 0) {
+    if (m == 0) {
+      bits = s;
+    } else {  // subnormal
+      int ee = -1;
+      uint32_t mm = m;
+      do {
+        ++ee;
+        mm <<= 1;
+      } while (!(mm & 0x400));
+      bits = s | ((uint32_t)(127 - 15 - ee) << 23) | ((mm & 0x3ff) << 13);
+    }
+  } else if (e == 31) {
+    bits = s | 0x7f800000u | (m << 13);
+  } else {
+    bits = s | ((e + 127 - 15) << 23) | (m << 13);
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+
+RawTensor parse_tensor(Span s) {
+  RawTensor t;
+  Pb pb(s);
+  while (pb.more()) {
+    uint32_t f, w;
+    pb.key(f, w);
+    if (f == 1) {  // dims (packed or not)
+      if (w == 2) {
+        Pb q(pb.bytes());
+        while (q.more()) t.dims.push_back((int64_t)q.varint());
+      } else {
+        t.dims.push_back((int64_t)pb.varint());
+      }
+    } else if (f == 2 && w == 0) {
+      t.dtype = (int)pb.varint();
+    } else if (f == 4) {  // float_data
+      if (w == 2) {
+        Span b = pb.bytes();
+        const size_t k = b.n / 4;
+        t.f32.resize(k);
+        std::memcpy(t.f32.data(), b.p, k * 4);
+      } else if (w == 5) {
+        float v;
+        std::memcpy(&v, pb.p, 4);
+        pb.p += 4;
+        t.f32.push_back(v);
+      } else {
+        pb.skip(w);
+      }
+    } else if ((f == 5 || f == 7) && (w == 2 || w == 0)) {  // int32_data / int64_data
+      if (w == 2) {
+        Pb q(pb.bytes());
+        while (q.more()) t.ints.push_back((int64_t)q.varint());
+      } else {
+        t.ints.push_back((int64_t)pb.varint());
+      }
+    } else if (f == 8 && w == 2) {
+      t.name = pb.bytes().str();
+    } else if (f == 9 && w == 2) {
+      t.raw = pb.bytes();
+    } else if (f == 13 && w == 2) {  // external_data: StringStringEntryProto {1 key, 2 value}
+      Pb q(pb.bytes());
+      std::string k, v;
+      while (q.more()) {
+        uint32_t f2, w2;
+        q.key(f2, w2);
+        if (f2 == 1 && w2 == 2) k = q.bytes().str();
+        else if (f2 == 2 && w2 == 2) v = q.bytes().str();
+        else q.skip(w2);
+      }
+      if (k == "location") t.ext_location = v;
+      else if (k == "offset") t.ext_offset = std::stol(v);
+      else if (k == "length") t.ext_length = std::stol(v);
+    } else {
+      pb.skip(w);
+    }
+  }
+  return t;
+}
+
+Node parse_node(Span s) {
+  Node n;
+  Pb pb(s);
+  while (pb.more()) {
+    uint32_t f, w;
+    pb.key(f, w);
+    if (w == 2 && f == 1) n.in.push_back(pb.bytes().str());
+    else if (w == 2 && f == 2) n.out.push_back(pb.bytes().str());
+    else if (w == 2 && f == 3) n.name = pb.bytes().str();
+    else if (w == 2 && f == 4) n.op = pb.bytes().str();
+    else pb.skip(w);
+  }
+  return n;
+}
+
+void parse_file(const std::string& path, OnnxFile& of) {
+  of.bytes = read_file(path);
+  Span all{reinterpret_cast<const uint8_t*>(of.bytes.data()), of.bytes.size()};
+  Pb model(all);
+  bool have_graph = false;
+  while (model.more()) {
+    uint32_t f, w;
+    model.key(f, w);
+    if (f == 7 && w == 2) {  // ModelProto.graph
+      have_graph = true;
+      Pb g(model.bytes());
+      while (g.more()) {
+        uint32_t gf, gw;
+        g.key(gf, gw);
+        if (gf == 1 && gw == 2) of.nodes.push_back(parse_node(g.bytes()));
+        else if (gf == 5 && gw == 2) of.inits.push_back(parse_tensor(g.bytes()));
+        else g.skip(gw);
+      }
+    } else {
+      model.skip(w);
+    }
+  }
+  if (!have_graph) throw std::runtime_error("onnx: no graph in " + path);
+}
+
+size_t numel_of(const std::vector<int64_t>& d) {
+  size_t n = 1;
+  for (int64_t x : d) n *= (size_t)x;
+  return n;
+}
+
+// the tensor's values as f32 (float / double / half / bfloat16 / int8 / uint8 / int32 / int64)
+std::vector<float> to_f32(const RawTensor& t, const std::string& dir) {
+  const size_t n = numel_of(t.dims);
+  std::vector<float> out(n);
+  std::string ext;
+  Span raw = t.raw;
+  if (!t.ext_location.empty()) {
+    ext = read_file(dir + "/" + t.ext_location);
+    const long len = t.ext_length >= 0 ? t.ext_length : (long)ext.size() - t.ext_offset;
+    if (t.ext_offset < 0 || t.ext_offset + len > (long)ext.size())
+      throw std::runtime_error("onnx: external data out of range for " + t.name);
+    raw = Span{reinterpret_cast<const uint8_t*>(ext.data()) + t.ext_offset, (size_t)len};
+  }
+  auto need = [&](size_t bytes) {
+    if (raw.n != bytes)
+      throw std::runtime_error("onnx: raw_data size mismatch for " + t.name);
+  };
+  if (raw.n > 0) {
+    switch (t.dtype) {
+      case T_FLOAT: need(n * 4); std::memcpy(out.data(), raw.p, n * 4); break;
+      case T_DOUBLE:
+        need(n * 8);
+        for (size_t i = 0; i < n; ++i) {
+          double v;
+          std::memcpy(&v, raw.p + 8 * i, 8);
+          out[i] = (float)v;
+        }
+        break;
+      case T_FLOAT16:
+        need(n * 2);
+        for (size_t i = 0; i < n; ++i) {
+          uint16_t h;
+          std::memcpy(&h, raw.p + 2 * i, 2);
+          out[i] = half_to_float(h);
+        }
+        break;
+      case T_BFLOAT16:
+        need(n * 2);
+        for (size_t i = 0; i < n; ++i) {
+          uint16_t h;
+          std::memcpy(&h, raw.p + 2 * i, 2);
+          const uint32_t bits = (uint32_t)h << 16;
+          std::memcpy(&out[i], &bits, 4);
+        }
+        break;
+      case T_INT8: need(n); for (size_t i = 0; i < n; ++i) out[i] = (float)(int8_t)raw.p[i]; break;
+      case T_UINT8: need(n); for (size_t i = 0; i < n; ++i) out[i] = (float)raw.p[i]; break;
+      case T_INT32:
+        need(n * 4);
+        for (size_t i = 0; i < n; ++i) {
+          int32_t v;
+          std::memcpy(&v, raw.p + 4 * i, 4);
+          out[i] = (float)v;
+        }
+        break;
+      case T_INT64:
+        need(n * 8);
+        for (size_t i = 0; i < n; ++i) {
+          int64_t v;
+          std::memcpy(&v, raw.p + 8 * i, 8);
+          out[i] = (float)v;
+        }
+        break;
+      default:
+        throw std::runtime_error("onnx: unsupported data type " + std::to_string(t.dtype) + " for " + t.name);
+    }
+  } else if (!t.f32.empty()) {
+    if (t.f32.size() != n) throw std::runtime_error("onnx: float_data size mismatch for " + t.name);
+    out = t.f32;
+  } else if (!t.ints.empty()) {
+    if (t.ints.size() != n) throw std::runtime_error("onnx: int data size mismatch for " + t.name);
+    for (size_t i = 0; i < n; ++i) out[i] = (float)t.ints[i];
+  } else if (n != 0) {
+    throw std::runtime_error("onnx: tensor without data: " + t.name);
+  }
+  return out;
+}
+
+bool ends_with(const std::string& s, const std::string& x) {
+  return s.size() >= x.size() && s.compare(s.size() - x.size(), x.size(), x) == 0;
+}
+
+// torch.onnx scope path of a node ("/encoder/encoders.0/layers.1/feed_forward1/in_proj/MatMul")
+// -> module path ("encoder.encoders.0.layers.1.feed_forward1.in_proj")
+std::string scope_module(const std::string& node_name) {
+  if (node_name.empty() || node_name[0] != '/') return "";
+  std::string s = node_name.substr(1);
+  const size_t last = s.rfind('/');
+  if (last == std::string::npos) return "";
+  s = s.substr(0, last);
+  std::replace(s.begin(), s.end(), '/', '.');
+  return s;
+}
+
+struct Loaded {
+  std::vector<int64_t> dims;
+  std::vector<float> data;
+};
+
+// one file's initializers under the names the engine uses; MatMul weights that neither a scope
+// name nor a following bias names are appended to `unnamed` in graph (execution) order
+void map_file(const OnnxFile& of, const std::string& dir, const std::string& prefix,
+              std::map<std::string, Loaded>& out, std::vector<Loaded>* unnamed) {
+  std::map<std::string, const RawTensor*> byname;
+  for (const auto& t : of.inits) byname[t.name] = &t;
+  // 1. dequantize "<w>_quantized" (int8 / uint8) with "<w>_scale" and "<w>_zero_point"
+  //    (onnxruntime quantize_dynamic: per-tensor scale; per-channel along the last axis)
+  std::map<std::string, Loaded> vals;
+  std::set<std::string> consumed;
+  for (const auto& t : of.inits) {
+    if (!ends_with(t.name, "_quantized")) continue;
+    const std::string b = t.name.substr(0, t.name.size() - 10);
+    auto sc = byname.find(b + "_scale"), zp = byname.find(b + "_zero_point");
+    if (sc == byname.end()) continue;
+    std::vector<float> q = to_f32(t, dir), s = to_f32(*sc->second, dir);
+    std::vector<float> z = zp != byname.end() ? to_f32(*zp->second, dir) : std::vector<float>(s.size(), 0.f);
+    if (s.empty() || z.size() != s.size()) throw std::runtime_error("onnx: bad quantization parameters for " + b);
+    const size_t last = t.dims.empty() ? 1 : (size_t)t.dims.back();
+    if (s.size() != 1 && s.size() != last)
+      throw std::runtime_error("onnx: unsupported quantization axis for " + b);
+    for (size_t i = 0; i < q.size(); ++i) {
+      const size_t c = s.size() == 1 ? 0 : i % last;
+      q[i] = (q[i] - z[c]) * s[c];
+    }
+    vals[b] = Loaded{t.dims, std::move(q)};
+    consumed.insert(t.name);
+    consumed.insert(b + "_scale");
+    if (zp != byname.end()) consumed.insert(b + "_zero_point");
+  }
+  for (const auto& t : of.inits)
+    if (!consumed.count(t.name) && !vals.count(t.name)) vals[t.name] = Loaded{t.dims, to_f32(t, dir)};
+  // 2. MatMul / MatMulInteger weight operands: the exporter stores nn.Linear weights
+  //    transposed ([in][out]) under generated names; name them from the node's scope path, or
+  //    from the bias of the Add that follows (through Cast / Mul for MatMulInteger)
+  std::map<std::string, std::vector<const Node*>> consumers;
+  for (const auto& n : of.nodes)
+    for (const auto& i : n.in) consumers[i].push_back(&n);
+  auto base_of = [](const std::string& x) {
+    return ends_with(x, "_quantized") ? x.substr(0, x.size() - 10) : x;
+  };
+  std::map<std::string, std::string> rename;  // generated name -> module weight name
+  for (const auto& n : of.nodes) {
+    if ((n.op != "MatMul" && n.op != "MatMulInteger") || n.in.size() < 2) continue;
+    const std::string w = base_of(n.in[1]);
+    if (!vals.count(w) || vals[w].dims.size() != 2 || ends_with(w, ".weight")) continue;
+    std::string mod = scope_module(n.name);
+    if (mod.empty() && !n.out.empty()) {  // follow the output to an Add with a named bias
+      std::string cur = n.out[0];
+      for (int hop = 0; hop < 4 && mod.empty(); ++hop) {
+        const Node* nxt = nullptr;
+        for (const Node* c : consumers[cur]) {
+          if (c->op == "Add") {
+            for (const auto& i : c->in)
+              if (ends_with(i, ".bias") && vals.count(i)) mod = i.substr(0, i.size() - 5);
+          }
+          if (c->op == "Cast" || c->op == "Mul") nxt = c;
+        }
+        if (!nxt || nxt->out.empty()) break;
+        cur = nxt->out[0];
+      }
+    }
+    if (!mod.empty()) {
+      rename[w] = mod + ".weight";
+    } else if (unnamed) {
+      unnamed->push_back(vals[w]);
+      vals.erase(w);
+    }
+  }
+  for (const auto& kv : rename) {
+    Loaded& l = vals[kv.first];
+    const int64_t K = l.dims[0], N = l.dims[1];
+    Loaded t{{N, K}, std::vector<float>(l.data.size())};
+    for (int64_t k = 0; k < K; ++k)
+      for (int64_t c = 0; c < N; ++c) t.data[(size_t)c * K + k] = l.data[(size_t)k * N + c];
+    out[prefix + kv.second] = std::move(t);
+  }
+  for (auto& kv : vals) {
+    if (rename.count(kv.first)) continue;
+    if (kv.first.rfind("onnx::", 0) == 0 || kv.first.empty()) continue;  // graph constants
+    std::string name = kv.first;
+    if (name.rfind(prefix, 0) != 0) name = prefix + name;
+    if (!out.count(name)) out[name] = std::move(kv.second);
+  }
+}
+
+int dim(const std::map<std::string, Loaded>& w, const std::string& name, size_t axis) {
+  auto it = w.find(name);
+  if (it == w.end()) throw std::runtime_error("onnx model: missing tensor " + name);
+  if (axis >= it->second.dims.size()) throw std::runtime_error("onnx model: bad rank for " + name);
+  return (int)it->second.dims[axis];
+}
+
+std::string ivec(const std::vector<int>& v) {
+  std::ostringstream os;
+  os << "[";
+  for (size_t i = 0; i < v.size(); ++i) os << (i ? ", " : "") << v[i];
+  os << "]";
+  return os.str();
+}
+
+// ZipformerConfig (zasr/model.py) from the tensor shapes; query / positional head dims are the
+// kernels' 32 / 4
+std::string infer_config(const std::map<std::string, Loaded>& w) {
+  std::vector<int> dims, layers, ff, heads, ds, kernels;
+  int vd = 0, pos_dim = 0;
+  for (int i = 0;; ++i) {
+    const std::string s = "encoder.encoders." + std::to_string(i) + ".";
+    const bool down = w.count(s + "downsample.bias") != 0;
+    const std::string pre = s + (down ? "encoder." : "");
+    if (!w.count(pre + "layers.0.norm.bias")) break;
+    int nl = 0;
+    while (w.count(pre + "layers." + std::to_string(nl) + ".norm.bias")) ++nl;
+    const std::string L = pre + "layers.0.";
+    const int d = dim(w, L + "norm.bias", 0);
+    const int h = dim(w, L + "self_attn_weights.in_proj.weight", 0) / (2 * 32 + 4);
+    dims.push_back(d);
+    layers.push_back(nl);
+    ff.push_back(dim(w, L + "feed_forward2.in_proj.weight", 0));
+    heads.push_back(h);
+    ds.push_back(down ? dim(w, s + "downsample.bias", 0) : 1);
+    kernels.push_back(dim(w, L + "conv_module1.depthwise_conv.weight", 2));
+    vd = dim(w, L + "self_attn1.in_proj.weight", 0) / h;
+    pos_dim = dim(w, L + "self_attn_weights.linear_pos.weight", 1);
+  }
+  if (dims.empty()) throw std::runtime_error("onnx model: no Zipformer2 encoder stacks found");
+  std::ostringstream os;
+  os << "{\"name\": \"zipformer-onnx\", \"encoder_dims\": " << ivec(dims)
+     << ", \"num_layers\": " << ivec(layers) << ", \"ff_dims\": " << ivec(ff)
+     << ", \"num_heads\": " << ivec(heads) << ", \"downsampling\": " << ivec(ds)
+     << ", \"cnn_kernels\": " << ivec(kernels) << ", \"query_head_dim\": 32"
+     << ", \"value_head_dim\": " << vd << ", \"pos_head_dim\": 4, \"pos_dim\": " << pos_dim
+     << ", \"vocab_size\": " << dim(w, "joiner.output_linear.weight", 0)
+     << ", \"decoder_dim\": " << dim(w, "decoder.embedding.weight", 1)
+     << ", \"joiner_dim\": " << dim(w, "joiner.output_linear.weight", 1)
+     << ", \"context_size\": " << dim(w, "decoder.conv.weight", 2)
+     << ", \"layer1_channels\": " << dim(w, "encoder_embed.conv.0.weight", 0)
+     << ", \"layer2_channels\": " << dim(w, "encoder_embed.conv.4.weight", 0)
+     << ", \"layer3_channels\": " << dim(w, "encoder_embed.conv.7.weight", 0) << "}";
+  return os.str();
+}
+
+}  // namespace
+
+OnnxFiles find_onnx_files(const std::string& dir) {
+  // core/asr_engine.py:913-928: the first directory entry starting with the pattern and ending
+  // in .onnx whose name does not contain "int8"; else the first such file
+  std::vector<std::string> names;
+  if (DIR* d = opendir(dir.c_str())) {
+    while (dirent* e = readdir(d)) names.push_back(e->d_name);
+    closedir(d);
+  }
+  auto pick = [&](const std::string& pat) -> std::string {
+    std::string any, flt;
+    for (const auto& f : names) {
+      if (f.rfind(pat, 0) != 0 || !ends_with(f, ".onnx")) continue;
+      if (any.empty()) any = f;
+      if (flt.empty() && f.find("int8") == std::string::npos) flt = f;
+    }
+    const std::string f = !flt.empty() ? flt : any;
+    return f.empty() ? "" : dir + "/" + f;
+  };
+  return OnnxFiles{pick("encoder-"), pick("decoder-"), pick("joiner-")};
+}
+
+std::string load_onnx_model(const OnnxFiles& files, SafeTensors& out) {
+  std::map<std::string, Loaded> w;
+  std::vector<Loaded> unnamed;  // encoder MatMul weights without a scope name or bias
+  const std::pair<const std::string*, const char*> parts[] = {
+      {&files.encoder, ""}, {&files.decoder, ""}, {&files.joiner, "joiner."}};
+  for (const auto& pr : parts) {
+    OnnxFile of;
+    parse_file(*pr.first, of);
+    const std::string dir = pr.first->substr(0, pr.first->rfind('/'));
+    std::map<std::string, Loaded> part;
+    map_file(of, dir, pr.second, part, pr.first == &files.encoder ? &unnamed : nullptr);
+    for (auto& kv : part) {
+      // an exporter may keep encoder_proj / decoder_proj in the joiner graph
+      std::string name = kv.first;
+      if (name.rfind("joiner.encoder_proj.", 0) == 0 || name.rfind("joiner.decoder_proj.", 0) == 0)
+        name = name.substr(7);
+      if (!w.count(name)) w[name] = std::move(kv.second);
+    }
+  }
+  // bias-free linears (self_attn_weights.linear_pos) of an export without scope names: in
+  // execution order, layer by layer, each the next unnamed weight of shape [pos_dim][4 h]
+  size_t next_unnamed = 0;
+  for (int i = 0;; ++i) {
+    const std::string s = "encoder.encoders." + std::to_string(i) + ".";
+    const std::string pre = s + (w.count(s + "downsample.bias") ? "encoder." : "");
+    if (!w.count(pre + "layers.0.norm.bias")) break;
+    for (int j = 0; w.count(pre + "layers." + std::to_string(j) + ".norm.bias"); ++j) {
+      const std::string L = pre + "layers." + std::to_string(j) + ".self_attn_weights.";
+      if (w.count(L + "linear_pos.weight") || !w.count(L + "in_proj.weight")) continue;
+      const int64_t n4 = 4 * (w[L + "in_proj.weight"].dims[0] / (2 * 32 + 4));
+      while (next_unnamed < unnamed.size() && unnamed[next_unnamed].dims[1] != n4) ++next_unnamed;
+      if (next_unnamed == unnamed.size()) break;
+      const Loaded& u = unnamed[next_unnamed++];
+      const int64_t K = u.dims[0], N = u.dims[1];
+      Loaded t{{N, K}, std::vector<float>(u.data.size())};
+      for (int64_t k = 0; k < K; ++k)
+        for (int64_t c = 0; c < N; ++c) t.data[(size_t)c * K + k] = u.data[(size_t)k * N + c];
+      w[L + "linear_pos.weight"] = std::move(t);
+    }
+  }
+  const std::string cfg = infer_config(w);
+  for (auto& kv : w) out.put(kv.first, kv.second.dims, std::move(kv.second.data));
+  return cfg;
+}
+
+std::string load_model_dir(const std::string& dir, SafeTensors& out) {
+  const std::string cfg_path = dir + "/config.json", st_path = dir + "/model.safetensors";
+  if (file_exists(cfg_path) && file_exists(st_path)) {
+    out.load(st_path);
+    return read_file(cfg_path);
+  }
+  const OnnxFiles f = find_onnx_files(dir);
+  if (f.complete()) {
+    std::string cfg = load_onnx_model(f, out);
+    if (file_exists(cfg_path)) cfg = read_file(cfg_path);  // an explicit config wins
+    return cfg;
+  }
+  throw std::invalid_argument("missing model files in " + dir +
+                              " (config.json + model.safetensors, or encoder-/decoder-/joiner-*.onnx)");
+}
+
+void write_safetensors(const std::string& path, const SafeTensors& t) {
+  std::ostringstream hdr;
+  hdr << "{";
+  size_t off = 0;
+  bool first = true;
+  for (const auto& kv : t.all()) {
+    hdr << (first ? "" : ",") << "\"" << kv.first << "\":{\"dtype\":\"F32\",\"shape\":[";
+    for (size_t i = 0; i < kv.second.shape.size(); ++i) hdr << (i ? "," : "") << kv.second.shape[i];
+    hdr << "],\"data_offsets\":[" << off << "," << off + kv.second.numel * 4 << "]}";
+    off += kv.second.numel * 4;
+    first = false;
+  }
+  hdr << "}";
+  std::string h = hdr.str();
+  while ((8 + h.size()) % 8) h += ' ';
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  const uint64_t hl = h.size();
+  f.write(reinterpret_cast<const char*>(&hl), 8);
+  f.write(h.data(), (std::streamsize)h.size());
+  for (const auto& kv : t.all())
+    f.write(reinterpret_cast<const char*>(kv.second.data), (std::streamsize)(kv.second.numel * 4));
+  if (!f) throw std::runtime_error("write failed: " + path);
+}
+
+}  // namespace zasr

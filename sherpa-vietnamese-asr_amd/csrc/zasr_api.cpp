@@ -8,6 +8,7 @@
 #include "common.h"
 #include "engine.h"
 #include "host_io.h"
+#include "onnx_io.h"
 
 using zasr::Engine;
 using zasr::TokenResult;
@@ -71,18 +72,35 @@ int zasr_create(const zasr_config* cfg, zasr_recognizer** out) {
       tp += n;
       scores.push_back(cfg->hotword_scores[i]);
     }
-    // vocab size is needed for the DFA: read it from config.json via a throwaway parse
-    std::string cfg_text = zasr::read_file(std::string(cfg->model_dir) + "/config.json");
-    int V = (int)zasr::Json::parse(cfg_text).at("vocab_size").num;
-    zasr::HotwordDFA dfa = zasr::build_hotword_dfa(phrases, scores, V);
     auto* h = new zasr_recognizer;
-    h->eng.reset(new Engine(cfg->model_dir, cfg->device_id, beam, greedy, dfa, cfg->precision));
+    try {
+      h->eng.reset(new Engine(cfg->model_dir, cfg->device_id, beam, greedy, phrases, scores,
+                              cfg->precision));
+    } catch (...) {
+      delete h;
+      throw;
+    }
     *out = h;
     return (int)ZASR_OK;
   });
 }
 
 void zasr_destroy(zasr_recognizer* h) { delete h; }
+
+int zasr_convert_model(const char* model_dir, const char* out_dir) {
+  if (!model_dir || !out_dir) return fail(ZASR_ERR_INVALID, "null model_dir/out_dir");
+  return guarded([&]() {
+    zasr::SafeTensors w;
+    const std::string cfg = zasr::load_model_dir(model_dir, w);
+    zasr::write_safetensors(std::string(out_dir) + "/model.safetensors", w);
+    FILE* f = fopen((std::string(out_dir) + "/config.json").c_str(), "wb");
+    if (!f) return fail(ZASR_ERR_RUNTIME, std::string("cannot write config.json in ") + out_dir);
+    const size_t wr = fwrite(cfg.data(), 1, cfg.size(), f);
+    fclose(f);
+    if (wr != cfg.size()) return fail(ZASR_ERR_RUNTIME, "short write of config.json");
+    return (int)ZASR_OK;
+  });
+}
 
 int zasr_fbank(zasr_recognizer* h, const float* wav, int64_t n, int32_t sr, float* out,
                int64_t cap, int64_t* n_frames) {

@@ -103,6 +103,30 @@ def clear_model_cache(which="all"):
             _last_handle = None
 
 
+def _onnx_file(model_path: str, pattern: str) -> Optional[str]:
+    """The reference's find_file (core/asr_engine.py:913-920): the first entry starting with
+    `pattern` and ending in .onnx without "int8" in its name, else the first such file."""
+    try:
+        names = os.listdir(model_path)
+    except OSError:
+        return None
+    files = [f for f in names if f.startswith(pattern) and f.endswith(".onnx")]
+    floats = [f for f in files if "int8" not in f]
+    if floats:
+        return os.path.join(model_path, floats[0])
+    return os.path.join(model_path, files[0]) if files else None
+
+
+def model_files_present(model_path: str) -> bool:
+    """tokens.txt plus either this build's config.json + model.safetensors or the reference's
+    encoder-/decoder-/joiner-*.onnx set (libzasr reads their initializers, csrc/onnx_io.cpp)."""
+    if not os.path.exists(os.path.join(model_path, "tokens.txt")):
+        return False
+    if all(os.path.exists(os.path.join(model_path, f)) for f in ("config.json", "model.safetensors")):
+        return True
+    return all(_onnx_file(model_path, p) for p in ("encoder-", "decoder-", "joiner-"))
+
+
 def _load_tokens(path: str) -> Dict[int, str]:
     id2token = {}
     with open(path, "r", encoding="utf-8") as f:
@@ -157,8 +181,9 @@ def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_p
                       hotwords=None, device_id=None, precision=None):
     """Load (or reuse) a recognizer for `model_path` (reference :903-1020).
 
-    Model directory: config.json + model.safetensors + tokens.txt (zasr/model.py).  Raises
-    FileNotFoundError when files are missing, like the reference (:927-928).
+    Model directory: tokens.txt + either config.json + model.safetensors (zasr/model.py) or the
+    reference's encoder-/decoder-/joiner-*.onnx files (read by libzasr, non-int8 preferred like
+    :913-928).  Raises FileNotFoundError when files are missing, like the reference (:927-928).
     Hotwords: the reference's hotword config (see _hotword_config) tokenized with the model's
     bpe.model; `hotwords` may be (token_id_lists, scores) to bypass the file + bpe route.
     """
@@ -173,9 +198,7 @@ def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_p
             _last_handle = _recognizer_cache[key]["handle"]
             return _recognizer_cache[key]
         tokens_path = os.path.join(model_path, "tokens.txt")
-        need = [os.path.join(model_path, "config.json"), os.path.join(model_path, "model.safetensors"),
-                tokens_path]
-        if not all(os.path.exists(p) for p in need):
+        if not model_files_present(model_path):
             raise FileNotFoundError(f"Thiếu file model trong: {model_path}")
         if hotwords is not None:
             seqs, scores = [list(map(int, s)) for s in hotwords[0]], list(map(float, hotwords[1]))

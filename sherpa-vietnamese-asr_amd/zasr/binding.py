@@ -17,7 +17,7 @@ DEFAULT_LIB = os.path.join(_PKG, "lib", "libzasr.so")
 
 # every symbol declared in include/zasr.h (the CPU test checks the .so exports them all)
 EXPORTS = (
-    "zasr_create", "zasr_destroy", "zasr_fbank", "zasr_decode_batch", "zasr_decode_features",
+    "zasr_create", "zasr_destroy", "zasr_convert_model", "zasr_fbank", "zasr_decode_batch", "zasr_decode_features",
     "zasr_decode_device", "zasr_decode_device_batches", "zasr_encode_features", "zasr_search_encoder_out",
     "zasr_result_count", "zasr_result_num_tokens", "zasr_result_num_frames",
     "zasr_result_tokens", "zasr_result_frames", "zasr_result_log_probs",
@@ -69,6 +69,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_create.restype = C.c_int
     lib.zasr_destroy.argtypes = [P]
     lib.zasr_destroy.restype = None
+    lib.zasr_convert_model.argtypes = [C.c_char_p, C.c_char_p]
+    lib.zasr_convert_model.restype = C.c_int
     lib.zasr_fbank.argtypes = [P, fp, I64, I32, fp, I64, C.POINTER(I64)]
     lib.zasr_fbank.restype = C.c_int
     lib.zasr_decode_batch.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, I32, C.POINTER(P)]
@@ -120,6 +122,20 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def convert_model(model_dir: str, out_dir: str, lib_path: Optional[str] = None) -> None:
+    """Host-only load of a model directory (config.json + model.safetensors, or the
+    reference's encoder-/decoder-/joiner-*.onnx) through libzasr's loader, written as
+    out_dir/config.json + out_dir/model.safetensors (include/zasr.h zasr_convert_model)."""
+    lib = load_library(lib_path)
+    os.makedirs(out_dir, exist_ok=True)
+    rc = lib.zasr_convert_model(model_dir.encode(), out_dir.encode())
+    if rc != 0:
+        msg = lib.zasr_last_error().decode()
+        if rc == 2:
+            raise FileNotFoundError(msg)
+        raise ZasrError(msg)
 
 
 @dataclasses.dataclass

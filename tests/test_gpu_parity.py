@@ -351,6 +351,28 @@ def test_bf16_search_path_beam_hotwords(need_gpu):
     assert sum(agree) / len(agree) >= 0.75, agree
 
 
+# ------------------------------------------------------------------ model directories (§8f-1)
+def test_reference_onnx_dir_decodes_like_safetensors(tiny, tmp_path):
+    """A reference-format model directory (encoder-/decoder-/joiner-*.onnx + tokens.txt, the
+    files create_recognizer opens, core/asr_engine.py:913-928) decodes bit-identically to the
+    same weights in this build's safetensors format, through the drop-in create_recognizer."""
+    from write_onnx import write_model_dir
+    from zasr.asr_engine import create_recognizer
+    from zasr.model import synth_tokens
+    cfg, w, path, rec = tiny
+    src = str(tmp_path / "onnx_model")
+    write_model_dir(src, w, synth_tokens(cfg.vocab_size), also_int8=True)
+    r2 = create_recognizer(src, max_active_paths=4, precision="fp32")
+    chunks = [_speech(s, 1700 + i) for i, s in enumerate((2.0, 5.5))]
+    a = rec.decode(chunks)
+    b = r2["handle"].decode(chunks)
+    for x, y in zip(a, b):
+        assert x.T == y.T
+        assert x.token_ids.tolist() == y.token_ids.tolist()
+        np.testing.assert_array_equal(x.log_probs, y.log_probs)
+        np.testing.assert_array_equal(x.stats, y.stats)
+
+
 # ------------------------------------------------------------------ ROVER (row L)
 def test_rover_shared_fbank_equals_separate_decodes(need_gpu):
     """decode_chunks_rover (one GPU fbank per chunk shared by both models) == each model
