@@ -132,6 +132,27 @@ const double* zasr_result_log_probs(const zasr_result* r, int32_t i);
 const float* zasr_result_token_stats(const zasr_result* r, int32_t i);
 void zasr_result_free(zasr_result* r);
 
+/* ---- CAM++ speaker embedding ----
+   Replaces the reference's onnxruntime CAM++ session and its numpy front end:
+   core/speaker_diarization_senko_campp_optimized.py:86-159 (_compute_fbank_vectorized),
+   :589-605 (batched emb_sess.run(['embs'], {'feats': batch})); the model is the reference's
+   convert_onnx/export_campplus_onnx.py CAMPPlus (192-dim).  model_dir holds
+   campp_config.json + campp.safetensors (state-dict names). */
+typedef struct zasr_campp zasr_campp;
+int zasr_campp_create(const char* model_dir, int32_t device_id, zasr_campp** out);
+void zasr_campp_destroy(zasr_campp* h);
+int32_t zasr_campp_embedding_dim(const zasr_campp* h);
+/* fbank + per-utterance CMVN of one waveform: *n_frames = 1 + (n - 400) / 160 (0 if n < 400) */
+int zasr_campp_fbank(zasr_campp* h, const float* wav, int64_t n, float* out, int64_t cap,
+                     int64_t* n_frames);
+/* embeddings of a feature batch [count][n_frames][80] (zero-padded like the reference's
+   batch tensor) -> out [count][embedding_dim] (not L2-normalised, as the ONNX output) */
+int zasr_campp_embed(zasr_campp* h, const float* feats, int32_t count, int32_t n_frames,
+                     float* out);
+/* same with device buffers on `stream` (NULL: the handle's stream); used by bench.py */
+int zasr_campp_embed_device(zasr_campp* h, const float* d_feats, int32_t count,
+                            int32_t n_frames, float* d_out, void* stream);
+
 /* model facts */
 int32_t zasr_vocab_size(const zasr_recognizer* h);
 int32_t zasr_joiner_dim(const zasr_recognizer* h);

@@ -41,6 +41,10 @@ void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t s
 // LDS images (no bit reversal, wave-local barriers only), then the even/odd split
 // X[k] = E[k] + W512^k O[k]; power spectrum f32, mel triangles (tables in LDS), log with
 // FLT_EPSILON floor.
+// CAMPP = true: the CAM++ front end instead (core/speaker_diarization_senko_campp_optimized.py:
+// 86-159): samples x 32768, snip_edges framing (frame f = samples 160 f .. 160 f + 399), the
+// first sample's pre-emphasis uses the previous SIGNAL sample (0 for frame 0), mel bank
+// 20 Hz .. Nyquist, floor 1.0 (CMVN follows in campp_cmvn_kernel).
 // =====================================================================================
 constexpr int kFbWaves = 4;
 constexpr int kMelWMax = 512;  // each FFT bin lies in at most two triangles
@@ -49,6 +53,7 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+template <bool CAMPP>
 __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
     const float* __restrict__ wav, const long* __restrict__ wav_off,
     const int* __restrict__ nsamp, const int* __restrict__ fr_off, int nseq, int total_frames,
@@ -74,17 +79,27 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
   const int frame = blockIdx.x * kFbWaves + w;
   const bool active = frame < total_frames;
   float xv[7];
+  float ctx0 = 0.f;  // CAMPP: the signal sample before the frame (scaled; 0 for frame 0)
   if (active) {
     const int b = find_seq(fr_off, nseq, frame);
     const int f = frame - fr_off[b];
     const long n = nsamp[b];
     const float* base = wav + wav_off[b];
+    if constexpr (CAMPP) {
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const int i = lane + 64 * k;
-      long s = (long)f * 160 - 120 + (i < 400 ? i : 399);
-      while (s < 0 || s >= n) s = (s < 0) ? (-s - 1) : (2L * n - 1 - s);
-      xv[k] = base[s];
+      for (int k = 0; k < 7; ++k) {
+        const int i = lane + 64 * k;
+        xv[k] = base[(long)f * 160 + (i < 400 ? i : 399)] * 32768.0f;
+      }
+      ctx0 = f > 0 ? base[(long)f * 160 - 1] * 32768.0f : 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int i = lane + 64 * k;
+        long s = (long)f * 160 - 120 + (i < 400 ? i : 399);
+        while (s < 0 || s >= n) s = (s < 0) ? (-s - 1) : (2L * n - 1 - s);
+        xv[k] = base[s];
+      }
     }
     double part = 0.0;
 #pragma unroll
@@ -106,7 +121,7 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       const float up = __shfl(xv[k], lane == 0 ? 0 : lane - 1, 64);
-      const float prev = lane != 0 ? up : (k == 0 ? xv[0] : carry);
+      const float prev = lane != 0 ? up : (k == 0 ? (CAMPP ? ctx0 : xv[0]) : carry);
       carry = __shfl(xv[k], 63, 64);
       const int i = lane + 64 * k;
       const float e = __fsub_rn(xv[k], __fmul_rn(0.97f, prev));
@@ -164,16 +179,20 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
     const int st = sMeta[m], ln = sMeta[80 + m], wo = sMeta[160 + m];
     float acc = 0.f;
     for (int k = 0; k < ln; ++k) acc = fmaf(sMelW[wo + k], pw[st + k], acc);
-    out[(long)frame * 80 + m] = logf(fmaxf(acc, 1.1920928955078125e-07f));
+    out[(long)frame * 80 + m] = logf(fmaxf(acc, CAMPP ? 1.0f : 1.1920928955078125e-07f));
   }
 }
 
 void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const int* fr_off,
                   int nseq, int total_frames, const FbankTables& tabs, float* out,
-                  hipStream_t st) {
+                  hipStream_t st, bool campp) {
   if (total_frames <= 0) return;
-  hipLaunchKernelGGL(fbank_kernel, dim3(cdiv(total_frames, kFbWaves)), dim3(64 * kFbWaves), 0,
-                     st, wav, wav_off, nsamp, fr_off, nseq, total_frames, tabs, out);
+  if (campp)
+    hipLaunchKernelGGL(fbank_kernel<true>, dim3(cdiv(total_frames, kFbWaves)), dim3(64 * kFbWaves),
+                       0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames, tabs, out);
+  else
+    hipLaunchKernelGGL(fbank_kernel<false>, dim3(cdiv(total_frames, kFbWaves)), dim3(64 * kFbWaves),
+                       0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames, tabs, out);
 }
 
 // =====================================================================================

@@ -21,6 +21,7 @@ enum GemmEpi : int {
   EPI_RESADD = 3,   // C += v          (residual: src = src + module(src))
   EPI_MULAUX = 4,   // C = v * aux[m, n]
   EPI_MULAUX16 = 5, // C = v * aux[m, n], aux bf16 (gemm_bf16 only)
+  EPI_RELU = 6,     // C = max(v, 0)  (gemm_f32 only: CAM++ TDNN layers, BN folded in)
 };
 
 enum GemmALoad : int {

@@ -205,6 +205,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
         float* dst = C + (long)row * p.ldc + col;
         if constexpr (EPI == EPI_SWOOSHL) v = swooshl(v);
         if constexpr (EPI == EPI_SWOOSHR) v = swooshr(v);
+        if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.f);
         if constexpr (EPI == EPI_MULAUX) v *= aux[(long)row * p.ldaux + col];
         if constexpr (EPI == EPI_RESADD) v += *dst;
         *dst = v;
@@ -864,6 +865,8 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
       case EPI_SWOOSHL: return launch_tile<ALOAD_DENSE, false, EPI_SWOOSHL>(p, st);
       case EPI_SWOOSHR: return launch_tile<ALOAD_DENSE, false, EPI_SWOOSHR>(p, st);
       case EPI_RESADD: return launch_tile<ALOAD_DENSE, false, EPI_RESADD>(p, st);
+      case EPI_RELU: return launch_tile<ALOAD_DENSE, false, EPI_RELU>(p, st);
+      case EPI_MULAUX: return launch_tile<ALOAD_DENSE, false, EPI_MULAUX>(p, st);
       default: break;
     }
   } else if (aload == ALOAD_DENSE && b_ncontig) {

@@ -19,9 +19,42 @@ struct FbankTables {
   const int* mel_woff;      // [80] offset into mel_w
   const float* mel_w;       // packed triangle weights
 };
+// campp: the CAM++ front end (x 32768, snip_edges, signal-context pre-emphasis, floor 1.0;
+// tables with the 20 Hz .. Nyquist mel bank) -- frames per sequence 1 + (n - 400) / 160
 void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const int* fr_off,
                   int nseq, int total_frames, const FbankTables& tabs, float* out,
-                  hipStream_t st);
+                  hipStream_t st, bool campp = false);
+
+// ---- CAM++ speaker embedding (campp_kernels.hip) ----
+struct CamppConv2d {
+  const float* x;      // [n][ci][fi][T]
+  const float* w;      // [32][ci][ks][ks]
+  const float* scale;  // [32] folded BN scale
+  const float* shift;  // [32] folded BN shift
+  const float* res;    // nullable residual [n][32][fo][T]
+  float* y;            // [n][32][fo][T], or [n][T][32 * fo] (tdnn_out)
+  int n, ci, fi, fo, T, sf;
+  int relu, tdnn_out;
+  int in_tf;           // x is the [n][T][fi] feature batch (ci = 1)
+};
+void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st);
+void launch_campp_bnrelu(const float* x, int ldx, long R, int C, const float* s, const float* b,
+                         float* y, hipStream_t st);
+void launch_campp_im2col1d(const float* x, int ldx, int N, int Tin, int Tout, int C, int K,
+                           int stride, int dil, int pad, float* out, hipStream_t st);
+struct CamppCamMask {
+  const float* h;      // [n * T][128] CAM input (nonlinear2 output)
+  const float* w1;     // [64][128] linear1
+  const float* b1;     // [64]
+  const float* w2;     // [32][64] linear2
+  const float* b2;     // [32]
+  float* mexp;         // [n * T][32] mask per frame
+  int n, T, seg_len;
+};
+void launch_campp_cam_mask(const CamppCamMask& a, hipStream_t st);
+void launch_campp_stats(const float* x, int N, int T, int C, const float* s, const float* b,
+                        float* out, hipStream_t st);
+void launch_campp_cmvn(float* x, const int* fr_off, int nseq, hipStream_t st);
 
 // ---- Conv2dSubsampling pieces (icefall subsampling.py, 3P) ----
 // conv.0 (1->8, 3x3, pad (0,1)) + SwooshR: fbank rows [T][80] -> [T-2][80][8]

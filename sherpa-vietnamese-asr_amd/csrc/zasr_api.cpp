@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "../../include/zasr.h"
+#include "campp.h"
 #include "common.h"
 #include "engine.h"
 #include "host_io.h"
@@ -19,6 +20,10 @@ struct zasr_recognizer {
 
 struct zasr_result {
   std::vector<TokenResult> items;
+};
+
+struct zasr_campp {
+  std::unique_ptr<zasr::CamppEngine> eng;
 };
 
 namespace {
@@ -86,6 +91,64 @@ int zasr_create(const zasr_config* cfg, zasr_recognizer** out) {
 }
 
 void zasr_destroy(zasr_recognizer* h) { delete h; }
+
+int zasr_campp_create(const char* model_dir, int32_t device_id, zasr_campp** out) {
+  if (!model_dir || !out) return fail(ZASR_ERR_INVALID, "null model_dir/out");
+  *out = nullptr;
+  return guarded([&]() {
+    auto* h = new zasr_campp;
+    try {
+      h->eng.reset(new zasr::CamppEngine(model_dir, device_id));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+    return (int)ZASR_OK;
+  });
+}
+
+void zasr_campp_destroy(zasr_campp* h) { delete h; }
+
+int32_t zasr_campp_embedding_dim(const zasr_campp* h) { return h ? h->eng->emb_dim() : 0; }
+
+int zasr_campp_fbank(zasr_campp* h, const float* wav, int64_t n, float* out, int64_t cap,
+                     int64_t* n_frames) {
+  if (!h || !n_frames || (n > 0 && !wav)) return fail(ZASR_ERR_INVALID, "null argument");
+  const int64_t frames = n >= 400 ? 1 + (n - 400) / 160 : 0;
+  *n_frames = frames;
+  if (frames * 80 > cap || (frames > 0 && !out)) return fail(ZASR_ERR_INVALID, "output buffer too small");
+  if (frames == 0) return ZASR_OK;
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    std::vector<float> f;
+    h->eng->fbank_host(wav, (long)n, f);
+    std::memcpy(out, f.data(), f.size() * sizeof(float));
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_campp_embed(zasr_campp* h, const float* feats, int32_t count, int32_t n_frames,
+                     float* out) {
+  if (!h || (count > 0 && (!feats || !out))) return fail(ZASR_ERR_INVALID, "null argument");
+  if (count < 0 || n_frames < 1) return fail(ZASR_ERR_INVALID, "count >= 0 and n_frames >= 1 required");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->embed_host(feats, count, n_frames, out);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_campp_embed_device(zasr_campp* h, const float* d_feats, int32_t count, int32_t n_frames,
+                            float* d_out, void* stream) {
+  if (!h || (count > 0 && (!d_feats || !d_out))) return fail(ZASR_ERR_INVALID, "null argument");
+  if (count < 0 || n_frames < 1) return fail(ZASR_ERR_INVALID, "count >= 0 and n_frames >= 1 required");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->embed_device(d_feats, count, n_frames, d_out, reinterpret_cast<hipStream_t>(stream));
+    return (int)ZASR_OK;
+  });
+}
 
 int zasr_convert_model(const char* model_dir, const char* out_dir) {
   if (!model_dir || !out_dir) return fail(ZASR_ERR_INVALID, "null model_dir/out_dir");

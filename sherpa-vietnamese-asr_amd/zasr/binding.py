@@ -23,7 +23,8 @@ EXPORTS = (
     "zasr_result_tokens", "zasr_result_frames", "zasr_result_log_probs",
     "zasr_result_token_stats", "zasr_result_free", "zasr_vocab_size", "zasr_joiner_dim",
     "zasr_profile_enable", "zasr_profile_reset", "zasr_profile_report", "zasr_last_error",
-    "zasr_version",
+    "zasr_version", "zasr_campp_create", "zasr_campp_destroy", "zasr_campp_embedding_dim",
+    "zasr_campp_fbank", "zasr_campp_embed", "zasr_campp_embed_device",
 )
 
 
@@ -119,6 +120,18 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_last_error.restype = C.c_char_p
     lib.zasr_version.argtypes = []
     lib.zasr_version.restype = C.c_char_p
+    lib.zasr_campp_create.argtypes = [C.c_char_p, I32, C.POINTER(P)]
+    lib.zasr_campp_create.restype = C.c_int
+    lib.zasr_campp_destroy.argtypes = [P]
+    lib.zasr_campp_destroy.restype = None
+    lib.zasr_campp_embedding_dim.argtypes = [P]
+    lib.zasr_campp_embedding_dim.restype = I32
+    lib.zasr_campp_fbank.argtypes = [P, fp, I64, fp, I64, C.POINTER(I64)]
+    lib.zasr_campp_fbank.restype = C.c_int
+    lib.zasr_campp_embed.argtypes = [P, fp, I32, I32, fp]
+    lib.zasr_campp_embed.restype = C.c_int
+    lib.zasr_campp_embed_device.argtypes = [P, P, I32, I32, P, P]
+    lib.zasr_campp_embed_device.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -315,3 +328,62 @@ class Recognizer:
             name, cnt, ms = line.split()
             out[name] = (int(cnt), float(ms))
         return out
+
+
+class CamppEmbedder:
+    """CAM++ speaker embeddings on the GPU (include/zasr.h zasr_campp_*): the reference's
+    numpy fbank (core/speaker_diarization_senko_campp_optimized.py:86-159) and its batched
+    ONNX CAM++ session (:589-605)."""
+
+    def __init__(self, model_dir: str, device_id: int = 0, lib_path: Optional[str] = None):
+        self.lib = load_library(lib_path)
+        h = C.c_void_p()
+        rc = self.lib.zasr_campp_create(model_dir.encode(), device_id, C.byref(h))
+        if rc != 0:
+            msg = self.lib.zasr_last_error().decode()
+            if rc == 2:
+                raise FileNotFoundError(msg)
+            raise ZasrError(msg)
+        self.handle = h
+        self.dim = self.lib.zasr_campp_embedding_dim(h)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.zasr_campp_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ZasrError(self.lib.zasr_last_error().decode())
+
+    def fbank(self, audio) -> np.ndarray:
+        a = _f32(audio)
+        n = a.shape[0]
+        frames = 1 + (n - 400) // 160 if n >= 400 else 0
+        out = np.empty((max(frames, 1), 80), dtype=np.float32)
+        nf = C.c_int64()
+        fp = C.POINTER(C.c_float)
+        self._check(self.lib.zasr_campp_fbank(self.handle, a.ctypes.data_as(fp), n,
+                                              out.ctypes.data_as(fp), out.size, C.byref(nf)))
+        return out[: nf.value]
+
+    def embed(self, feats) -> np.ndarray:
+        x = _f32(feats)
+        if x.ndim != 3 or x.shape[2] != 80:
+            raise ValueError("feats must be [N, T, 80]")
+        out = np.empty((x.shape[0], self.dim), dtype=np.float32)
+        fp = C.POINTER(C.c_float)
+        self._check(self.lib.zasr_campp_embed(self.handle, x.ctypes.data_as(fp), x.shape[0],
+                                              x.shape[1], out.ctypes.data_as(fp)))
+        return out
+
+    def embed_device(self, d_feats: int, count: int, n_frames: int, d_out: int, stream: int = 0):
+        self._check(self.lib.zasr_campp_embed_device(self.handle, C.c_void_p(d_feats), count,
+                                                     n_frames, C.c_void_p(d_out),
+                                                     C.c_void_p(stream)))

@@ -1,0 +1,68 @@
+"""CAM++ on the MI355X through the C ABI vs the oracle and the fixtures
+the reference's own CAMPPlus / _compute_fbank_vectorized produced.
+
+Tolerances: the reference's acceptance rule for a GPU CAM++ (core/calibration.py:71-78,
+1279-1286): max_abs <= 2e-3 OR rel_l2 <= 2e-4 -- held here as rel_l2 <= 2e-4 on every batch
+(random-init embeddings reach |x| ~ 50).  fbank: 2e-3 absolute on the log-mel (f32 power /
+mel sums on the GPU vs f64 in numpy)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "campp_golden.npz"))
+EMB_CASES = sorted(k[len("emb_in_"):] for k in GOLD.files if k.startswith("emb_in_"))
+
+
+@pytest.fixture(scope="module")
+def emb(tmp_path_factory):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from zasr.binding import CamppEmbedder
+    from zasr.campp import CamppConfig, save_model_dir, synth_weights
+    d = str(tmp_path_factory.mktemp("campp"))
+    cfg = CamppConfig()
+    w = synth_weights(cfg, int(GOLD["weight_seed"]))
+    save_model_dir(d, cfg, w)
+    e = CamppEmbedder(d)
+    yield cfg, w, e
+    e.close()
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.mark.parametrize("case", EMB_CASES)
+def test_campp_embedding_matches_reference(emb, case):
+    cfg, w, e = emb
+    got = e.embed(GOLD[f"emb_in_{case}"])
+    ref = GOLD[f"emb_out_{case}"]
+    assert got.shape == ref.shape
+    assert _rel(got, ref) <= 2e-4, (_rel(got, ref), float(np.abs(got - ref).max()))
+
+
+def test_campp_embedding_matches_oracle_large_batch(emb):
+    """A 32-window batch (the reference's batch size) of pipeline-shaped windows."""
+    from oracle.campplus import CamppOracle, campp_fbank
+    from zasr.campp import window_plan
+    from zasr.synth_audio import synth_speech
+    cfg, w, e = emb
+    fb = campp_fbank(synth_speech(22.0, 1800))
+    wins = [fb[s:s + n] for s, n in window_plan(fb.shape[0])][:32]
+    x = np.stack(wins)
+    got = e.embed(x)
+    ref = CamppOracle(cfg, w).embed(x)
+    assert _rel(got, ref) <= 2e-4
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_campp_fbank_matches_reference(emb, i):
+    got = emb[2].fbank(GOLD[f"fb_in_{i}"])
+    ref = GOLD[f"fb_out_{i}"]
+    assert got.shape == ref.shape
+    if ref.size:
+        np.testing.assert_allclose(got, ref, rtol=0, atol=2e-3)
