@@ -76,6 +76,11 @@ def parse_args(argv=None):
                     help="no GPU: exercise the launcher / rank / timing / JSON path with gloo "
                          "and a CPU stand-in step (tests/test_bench_launcher.py)")
     ap.add_argument("--profile-out", default="")
+    ap.add_argument("--stage", default="asr", choices=["asr", "campp"],
+                    help="asr: the Zipformer decode (default, BASELINE metric); campp: the CAM++ "
+                         "speaker-embedding stage of config 5 (1.5 s windows, 0.6 s step)")
+    ap.add_argument("--campp-batch", type=int, default=512,
+                    help="CAM++ windows per launch group (the reference batches 32 on CPU)")
     return ap.parse_args(argv)
 
 
@@ -294,11 +299,121 @@ def cpu_baseline(args, chunks, beam, hotwords, n_chunks=4):
                       f"{len(times)}"}
 
 
+# ------------------------------------------------------------------ CAM++ stage (config 5)
+def _campp_cpu(model_seed, feats, threads, repeats):
+    import torch
+    from oracle.campplus import CamppOracle
+    from zasr.campp import CamppConfig, synth_weights
+    torch.set_num_threads(threads)
+    cfg = CamppConfig()
+    orc = CamppOracle(cfg, synth_weights(cfg, model_seed))
+    orc.embed(feats[:2])
+    times = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        for b in range(0, feats.shape[0], 32):  # the reference's batch (:589-605)
+            orc.embed(feats[b:b + 32])
+        times.append(time.perf_counter() - t0)
+    return float(np.mean(times)), times
+
+
+def bench_campp(args):
+    """CAM++ embeddings of 1 h per GPU: speech regions (the planner's silence-split spans, no
+    overlap) -> CAM++ fbank per region -> 150-frame windows every 60 frames (core/speaker_
+    diarization_senko_campp_optimized.py:540-582) -> embeddings.  Timed: the embedding of all
+    windows (features resident in HBM), `--campp-batch` windows per launch."""
+    import torch
+    from zasr.binding import CamppEmbedder
+    from zasr.campp import CamppConfig, campp_flops, save_model_dir, synth_weights, window_plan
+    from zasr.plan import plan_chunks
+    from zasr.synth_audio import synth_speech
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    cfg = CamppConfig()
+    seed = 20261017
+    mdir = os.path.join(tempfile.gettempdir(), f"zasr_bench_campp_{os.getpid()}")
+    save_model_dir(mdir, cfg, synth_weights(cfg, seed))
+    emb = CamppEmbedder(mdir, device_id=local)
+    audio = synth_speech(args.audio_sec, AUDIO_SEED + rank)
+    wins = []
+    for a, e, _ in plan_chunks(audio, overlap_sec=0.0):
+        fb = emb.fbank(audio[a:e])
+        wins += [fb[s:s + n] for s, n in window_plan(fb.shape[0]) if n == 150]
+    feats = np.ascontiguousarray(np.stack(wins))
+    W = feats.shape[0]
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample = feats[:64]
+        mean, times = _campp_cpu(seed, sample, min(16, os.cpu_count() or 1), max(1, args.cpu_repeats))
+        cpu = {"value": round(64 / W * args.audio_sec / mean, 3), "unit": "audio-sec/sec",
+               "cores": min(16, os.cpu_count() or 1), "kind": "port",
+               "repeats": len(times), "sample": f"64 of the {W} windows, oracle CAMPPlus torch fp32, "
+                                                 f"batches of 32, 1 warm-up + mean of {len(times)}"}
+    d_in = torch.from_numpy(feats).cuda()
+    d_out = torch.empty((W, cfg.embedding_size), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    B = max(1, args.campp_batch)
+
+    def step():
+        for b in range(0, W, B):
+            n = min(B, W - b)
+            emb.embed_device(d_in.data_ptr() + b * 150 * 80 * 4, n, 150,
+                             d_out.data_ptr() + b * cfg.embedding_size * 4, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=f"cuda:{local}")
+    fl = W * campp_flops(cfg, 150)
+    t_step = el / args.steps
+    if rank == 0:
+        line = {"metric": "audio-sec/sec CAM++ speaker embedding (1.5 s windows, 0.6 s step)",
+                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(1000 * t_step, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (seeded speech-like audio, random-init CAM++ weights)",
+                "config": {"workload": "CAM++ 192-dim embeddings of 1 h per GPU (config 5 stage)",
+                           "windows_per_gpu": W, "launch_batch": B,
+                           "windows_per_sec": round(W * world / t_step, 1)},
+                "roofline": {"kernel": "campp (whole stage)", "bound": "mfma",
+                             "achieved": round(fl / t_step / 1e12, 2),
+                             "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                             "frac": round(fl / t_step / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+                             "flops_per_window": campp_flops(cfg, 150)},
+                "cpu_baseline": cpu}
+        print(json.dumps(line))
+        if args.profile_out:
+            with open(args.profile_out, "w") as f:
+                json.dump(line, f, indent=1)
+    emb.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse_args()
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(launch_ranks(args))
+    if args.stage == "campp":
+        return bench_campp(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
