@@ -153,6 +153,22 @@ int zasr_campp_embed(zasr_campp* h, const float* feats, int32_t count, int32_t n
 int zasr_campp_embed_device(zasr_campp* h, const float* d_feats, int32_t count,
                             int32_t n_frames, float* d_out, void* stream);
 
+/* ---- ViBERT-capu punctuation / capitalization ----
+   Replaces the reference's onnxruntime session of vibert-capu.onnx (core/gec_model.py:
+   366-412: session.run(None, {input_ids, attention_mask, token_type_ids, input_offsets}) ->
+   (logits, detect_logits)); graph: convert_onnx/export_vibert_onnx.py Seq2LabelsModel.
+   model_dir holds vibert_config.json + vibert.safetensors (Hugging Face names). */
+typedef struct zasr_vibert zasr_vibert;
+int zasr_vibert_create(const char* model_dir, int32_t device_id, zasr_vibert** out);
+void zasr_vibert_destroy(zasr_vibert* h);
+int32_t zasr_vibert_num_labels(const zasr_vibert* h);
+int32_t zasr_vibert_num_detect(const zasr_vibert* h);
+/* inputs int64 [batch][n_tokens] (ids, mask, token types) and [batch][n_words] offsets;
+   outputs logits [batch][n_words][num_labels], detect_logits [batch][n_words][num_detect] */
+int zasr_vibert_run(zasr_vibert* h, const int64_t* input_ids, const int64_t* attention_mask,
+                    const int64_t* token_type_ids, const int64_t* input_offsets, int32_t batch,
+                    int32_t n_tokens, int32_t n_words, float* logits, float* detect_logits);
+
 /* model facts */
 int32_t zasr_vocab_size(const zasr_recognizer* h);
 int32_t zasr_joiner_dim(const zasr_recognizer* h);

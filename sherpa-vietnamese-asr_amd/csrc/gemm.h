@@ -22,6 +22,7 @@ enum GemmEpi : int {
   EPI_MULAUX = 4,   // C = v * aux[m, n]
   EPI_MULAUX16 = 5, // C = v * aux[m, n], aux bf16 (gemm_bf16 only)
   EPI_RELU = 6,     // C = max(v, 0)  (gemm_f32 only: CAM++ TDNN layers, BN folded in)
+  EPI_GELU = 7,     // C = v * Phi(v) = 0.5 v (1 + erf(v / sqrt 2))  (gemm_f32 only: ViBERT FFN)
 };
 
 enum GemmALoad : int {

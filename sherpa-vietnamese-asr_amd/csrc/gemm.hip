@@ -206,6 +206,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
         if constexpr (EPI == EPI_SWOOSHL) v = swooshl(v);
         if constexpr (EPI == EPI_SWOOSHR) v = swooshr(v);
         if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.f);
+        if constexpr (EPI == EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
         if constexpr (EPI == EPI_MULAUX) v *= aux[(long)row * p.ldaux + col];
         if constexpr (EPI == EPI_RESADD) v += *dst;
         *dst = v;
@@ -866,6 +867,7 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
       case EPI_SWOOSHR: return launch_tile<ALOAD_DENSE, false, EPI_SWOOSHR>(p, st);
       case EPI_RESADD: return launch_tile<ALOAD_DENSE, false, EPI_RESADD>(p, st);
       case EPI_RELU: return launch_tile<ALOAD_DENSE, false, EPI_RELU>(p, st);
+      case EPI_GELU: return launch_tile<ALOAD_DENSE, false, EPI_GELU>(p, st);
       case EPI_MULAUX: return launch_tile<ALOAD_DENSE, false, EPI_MULAUX>(p, st);
       default: break;
     }

@@ -56,6 +56,33 @@ void launch_campp_stats(const float* x, int N, int T, int C, const float* s, con
                         float* out, hipStream_t st);
 void launch_campp_cmvn(float* x, const int* fr_off, int nseq, hipStream_t st);
 
+// ---- ViBERT-capu encoder pieces (vibert_kernels.hip) ----
+struct VibertEmbedArgs {
+  const long* ids;    // [B * L]
+  const long* tt;     // [B * L] token types
+  const float* word;  // [V][H]
+  const float* pos;   // [max_pos][H]
+  const float* type;  // [types][H]
+  const float* ln_g;
+  const float* ln_b;
+  float* x;           // [B * L][H]
+  int L, H;
+  float eps;
+};
+void launch_vibert_embed(const VibertEmbedArgs& a, long rows, hipStream_t st);
+void launch_vibert_layernorm(float* x, long rows, int H, const float* g, const float* b, float eps,
+                             hipStream_t st);
+struct VibertAttnArgs {
+  const float* qkv;   // [B * L][3 H]
+  const long* mask;   // [B * L] attention_mask (0 = padding)
+  float* ctx;         // [B * L][H]
+  int L, H;
+  float scale;        // 1 / sqrt(head dim)
+};
+void launch_vibert_attention(const VibertAttnArgs& a, int B, int heads, hipStream_t st);
+void launch_vibert_gather(const float* x, const long* offsets, int B, int L, int W, int H, float* g,
+                          hipStream_t st);
+
 // ---- Conv2dSubsampling pieces (icefall subsampling.py, 3P) ----
 // conv.0 (1->8, 3x3, pad (0,1)) + SwooshR: fbank rows [T][80] -> [T-2][80][8]
 // (out_bf16: bf16 output, native-exp/log SwooshR -- the bf16 mode)

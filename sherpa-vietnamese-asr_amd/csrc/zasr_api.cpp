@@ -7,6 +7,7 @@
 #include "../../include/zasr.h"
 #include "campp.h"
 #include "common.h"
+#include "vibert.h"
 #include "engine.h"
 #include "host_io.h"
 #include "onnx_io.h"
@@ -24,6 +25,10 @@ struct zasr_result {
 
 struct zasr_campp {
   std::unique_ptr<zasr::CamppEngine> eng;
+};
+
+struct zasr_vibert {
+  std::unique_ptr<zasr::VibertEngine> eng;
 };
 
 namespace {
@@ -111,6 +116,44 @@ int zasr_campp_create(const char* model_dir, int32_t device_id, zasr_campp** out
 void zasr_campp_destroy(zasr_campp* h) { delete h; }
 
 int32_t zasr_campp_embedding_dim(const zasr_campp* h) { return h ? h->eng->emb_dim() : 0; }
+
+int zasr_vibert_create(const char* model_dir, int32_t device_id, zasr_vibert** out) {
+  if (!model_dir || !out) return fail(ZASR_ERR_INVALID, "null model_dir/out");
+  *out = nullptr;
+  return guarded([&]() {
+    auto* h = new zasr_vibert;
+    try {
+      h->eng.reset(new zasr::VibertEngine(model_dir, device_id));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+    return (int)ZASR_OK;
+  });
+}
+
+void zasr_vibert_destroy(zasr_vibert* h) { delete h; }
+
+int32_t zasr_vibert_num_labels(const zasr_vibert* h) { return h ? h->eng->num_labels() : 0; }
+int32_t zasr_vibert_num_detect(const zasr_vibert* h) { return h ? h->eng->num_detect() : 0; }
+
+int zasr_vibert_run(zasr_vibert* h, const int64_t* input_ids, const int64_t* attention_mask,
+                    const int64_t* token_type_ids, const int64_t* input_offsets, int32_t batch,
+                    int32_t n_tokens, int32_t n_words, float* logits, float* detect_logits) {
+  if (!h || (batch > 0 && (!input_ids || !attention_mask || !token_type_ids || !input_offsets ||
+                           !logits || !detect_logits)))
+    return fail(ZASR_ERR_INVALID, "null argument");
+  if (batch < 0 || n_tokens < 1 || n_words < 1) return fail(ZASR_ERR_INVALID, "bad batch shape");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->run_host(reinterpret_cast<const long*>(input_ids), reinterpret_cast<const long*>(attention_mask),
+                     reinterpret_cast<const long*>(token_type_ids),
+                     reinterpret_cast<const long*>(input_offsets), batch, n_tokens, n_words, logits,
+                     detect_logits);
+    return (int)ZASR_OK;
+  });
+}
 
 int zasr_campp_fbank(zasr_campp* h, const float* wav, int64_t n, float* out, int64_t cap,
                      int64_t* n_frames) {

@@ -25,6 +25,8 @@ EXPORTS = (
     "zasr_profile_enable", "zasr_profile_reset", "zasr_profile_report", "zasr_last_error",
     "zasr_version", "zasr_campp_create", "zasr_campp_destroy", "zasr_campp_embedding_dim",
     "zasr_campp_fbank", "zasr_campp_embed", "zasr_campp_embed_device",
+    "zasr_vibert_create", "zasr_vibert_destroy", "zasr_vibert_num_labels",
+    "zasr_vibert_num_detect", "zasr_vibert_run",
 )
 
 
@@ -132,6 +134,16 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_campp_embed.restype = C.c_int
     lib.zasr_campp_embed_device.argtypes = [P, P, I32, I32, P, P]
     lib.zasr_campp_embed_device.restype = C.c_int
+    lib.zasr_vibert_create.argtypes = [C.c_char_p, I32, C.POINTER(P)]
+    lib.zasr_vibert_create.restype = C.c_int
+    lib.zasr_vibert_destroy.argtypes = [P]
+    lib.zasr_vibert_destroy.restype = None
+    for n in ("zasr_vibert_num_labels", "zasr_vibert_num_detect"):
+        getattr(lib, n).argtypes = [P]
+        getattr(lib, n).restype = I32
+    i64p = C.POINTER(I64)
+    lib.zasr_vibert_run.argtypes = [P, i64p, i64p, i64p, i64p, I32, I32, I32, fp, fp]
+    lib.zasr_vibert_run.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -387,3 +399,50 @@ class CamppEmbedder:
         self._check(self.lib.zasr_campp_embed_device(self.handle, C.c_void_p(d_feats), count,
                                                      n_frames, C.c_void_p(d_out),
                                                      C.c_void_p(stream)))
+
+
+class VibertSession:
+    """ViBERT-capu on the GPU with the onnxruntime InferenceSession surface the reference's
+    GecBERTModel uses (core/gec_model.py:366-412): run(None, feeds) -> [logits,
+    detect_logits] for feeds {input_ids, attention_mask, token_type_ids, input_offsets}."""
+
+    def __init__(self, model_dir: str, device_id: int = 0, lib_path: Optional[str] = None):
+        self.lib = load_library(lib_path)
+        h = C.c_void_p()
+        rc = self.lib.zasr_vibert_create(model_dir.encode(), device_id, C.byref(h))
+        if rc != 0:
+            msg = self.lib.zasr_last_error().decode()
+            if rc == 2:
+                raise FileNotFoundError(msg)
+            raise ZasrError(msg)
+        self.handle = h
+        self.num_labels = self.lib.zasr_vibert_num_labels(h)
+        self.num_detect = self.lib.zasr_vibert_num_detect(h)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.zasr_vibert_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, output_names, feeds):
+        i64 = lambda k: np.ascontiguousarray(np.asarray(feeds[k]), dtype=np.int64)  # noqa: E731
+        ids, am, tt, off = (i64(k) for k in ("input_ids", "attention_mask", "token_type_ids",
+                                              "input_offsets"))
+        B, L = ids.shape
+        W = off.shape[1]
+        lg = np.empty((B, W, self.num_labels), np.float32)
+        dl = np.empty((B, W, self.num_detect), np.float32)
+        p = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+        fp = C.POINTER(C.c_float)
+        rc = self.lib.zasr_vibert_run(self.handle, p(ids), p(am), p(tt), p(off), B, L, W,
+                                      lg.ctypes.data_as(fp), dl.ctypes.data_as(fp))
+        if rc != 0:
+            raise ZasrError(self.lib.zasr_last_error().decode())
+        outs = {"logits": lg, "detect_logits": dl}
+        return [lg, dl] if output_names is None else [outs[n] for n in output_names]
