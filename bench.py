@@ -76,9 +76,14 @@ def parse_args(argv=None):
                     help="no GPU: exercise the launcher / rank / timing / JSON path with gloo "
                          "and a CPU stand-in step (tests/test_bench_launcher.py)")
     ap.add_argument("--profile-out", default="")
-    ap.add_argument("--stage", default="asr", choices=["asr", "campp"],
+    ap.add_argument("--stage", default="asr", choices=["asr", "campp", "vad"],
                     help="asr: the Zipformer decode (default, BASELINE metric); campp: the CAM++ "
-                         "speaker-embedding stage of config 5 (1.5 s windows, 0.6 s step)")
+                         "speaker-embedding stage of config 5 (1.5 s windows, 0.6 s step); vad: "
+                         "Silero VAD probabilities + segments of the hour (core/asr_engine.py:2090)")
+    ap.add_argument("--vad-files", type=int, default=1,
+                    help="VAD stage: the hour split into this many files decoded in one call "
+                         "(1 = the reference's single-file case; the recurrence is one "
+                         "workgroup per file)")
     ap.add_argument("--campp-batch", type=int, default=512,
                     help="CAM++ windows per launch group (the reference batches 32 on CPU)")
     return ap.parse_args(argv)
@@ -407,6 +412,133 @@ def bench_campp(args):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------ Silero VAD stage
+def _vad_cpu(seed, audio, threads, repeats):
+    import torch
+    from oracle.silero import SileroOracle, run_windows
+    from zasr.silero import SileroConfig, synth_weights
+    torch.set_num_threads(threads)
+    cfg = SileroConfig()
+    sess = SileroOracle(cfg, synth_weights(cfg, seed)).session()
+    run_windows(sess, audio[:512 * 50])
+    times = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        run_windows(sess, audio)
+        times.append(time.perf_counter() - t0)
+    return float(np.mean(times)), times
+
+
+def bench_vad(args):
+    """Silero VAD of 1 h per GPU: speech probability of every 512-sample window (64-sample
+    context, LSTM state carried; core/vad_utils.py:80-111) with the low-amplitude boost, then
+    the host segmentation (get_vad_segments' defaults).  Audio resident in HBM; one step =
+    probabilities of the whole hour (`--vad-files` files in one call) + segments."""
+    import torch
+    from zasr.binding import VadSession
+    from zasr.silero import SileroConfig, save_model_dir, synth_weights, window_flops
+    from zasr.synth_audio import synth_speech
+    from zasr.vad_utils import _segments_from_probs
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    cfg = SileroConfig()
+    seed = 20261019
+    mdir = os.path.join(tempfile.gettempdir(), f"zasr_bench_vad_{os.getpid()}")
+    save_model_dir(mdir, cfg, synth_weights(cfg, seed))
+    sess = VadSession(mdir, device_id=local)
+    audio = synth_speech(args.audio_sec, AUDIO_SEED + rank)
+    F = max(1, args.vad_files)
+    bounds = np.linspace(0, len(audio), F + 1).astype(np.int64)
+    offs, lens = bounds[:-1], bounds[1:] - bounds[:-1]
+    nw = lens // 512
+    NW = int(nw.sum())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        n_s = 512 * 3000
+        mean, times = _vad_cpu(seed, audio[:n_s], 1, max(1, args.cpu_repeats))
+        cpu = {"value": round(n_s / SR / mean, 2), "unit": "audio-sec/sec", "cores": 1,
+               "kind": "port", "repeats": len(times),
+               "sample": f"first 3000 windows (96 s) of the hour, the reference's per-window loop "
+                         f"(core/vad_utils.py:97-111) over the oracle network, torch fp32 1 thread "
+                         f"(the reference's ORT session uses 1 intra-op thread, :30-33); "
+                         f"1 warm-up + mean of {len(times)}"}
+    d_audio = torch.from_numpy(audio).cuda()
+    d_probs = torch.empty(max(1, NW), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    wb = np.concatenate([[0], np.cumsum(nw)])
+    segs = []
+
+    def step():
+        sess.probs_device(d_audio.data_ptr(), offs, lens, d_probs.data_ptr(), auto_boost=True,
+                          stream=stream)
+        p = d_probs.cpu().numpy()
+        segs.clear()
+        for i in range(F):
+            segs.append(_segments_from_probs(p[wb[i]:wb[i + 1]], int(lens[i]), SR, 0.2, 100, 250,
+                                             1000, 250, True))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=f"cuda:{local}")
+    # the recurrence alone, HIP events on the engine's ordering stream
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    sess.probs_device(d_audio.data_ptr(), offs, lens, d_probs.data_ptr(), auto_boost=True,
+                      stream=stream)
+    ev1.record()
+    torch.cuda.synchronize()
+    t_gpu = ev0.elapsed_time(ev1) / 1e3
+    t_step = el / args.steps
+    if rank == 0:
+        byts = NW * (512 * 4 + 4)  # audio in + probabilities out (the stage's algorithmic bytes)
+        line = {"metric": "audio-sec/sec Silero VAD (512-sample windows, segments)",
+                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(1000 * t_step, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (seeded speech-like audio, random-init Silero v5 weights)",
+                "config": {"workload": f"Silero VAD of {args.audio_sec:.0f} s per GPU as {F} file(s) "
+                                       f"(get_vad_segments defaults)",
+                           "windows_per_gpu": NW, "files": F,
+                           "gpu_ms_probs": round(1000 * t_gpu, 3),
+                           "recurrence_passes": sess.last_passes,
+                           "n_segments": int(sum(len(x) for x in segs))},
+                "roofline": {"kernel": "vad (whole stage: STFT/encoder GEMMs + segmented LSTM)",
+                             "bound": "hbm", "achieved": round(byts / t_gpu / 1e9, 2),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(byts / t_gpu / 1e9 / HBM_PEAK_GBS, 5),
+                             "traffic": None,
+                             "mfma_tflops": round(NW * window_flops(cfg) / t_gpu / 1e12, 3),
+                             "note": "the recurrence is latency-bound per step; a file is decoded "
+                                     "as ~one segment per CU, parallel in time with verified state "
+                                     "continuity (vad.cpp VadEngine::recurrence)"},
+                "cpu_baseline": cpu}
+        print(json.dumps(line))
+        if args.profile_out:
+            with open(args.profile_out, "w") as f:
+                json.dump(line, f, indent=1)
+    sess.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse_args()
@@ -414,6 +546,8 @@ def main():
         sys.exit(launch_ranks(args))
     if args.stage == "campp":
         return bench_campp(args)
+    if args.stage == "vad":
+        return bench_vad(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

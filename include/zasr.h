@@ -169,6 +169,36 @@ int zasr_vibert_run(zasr_vibert* h, const int64_t* input_ids, const int64_t* att
                     const int64_t* token_type_ids, const int64_t* input_offsets, int32_t batch,
                     int32_t n_tokens, int32_t n_words, float* logits, float* detect_logits);
 
+/* ---- Silero VAD ----
+   Replaces the reference's per-window onnxruntime loop over silero_vad_16k_op15.onnx
+   (core/vad_utils.py:62-111: 64-sample context + 512-sample window, (2, 1, 128) LSTM state
+   carried across calls).  model_dir holds silero_config.json + silero_vad.safetensors
+   (torch state-dict names of the 16 kHz model). */
+typedef struct zasr_vad zasr_vad;
+int zasr_vad_create(const char* model_dir, int32_t device_id, zasr_vad** out);
+void zasr_vad_destroy(zasr_vad* h);
+/* speech probability of every full 512-sample window of n_files files (file i = audio
+   [offsets[i], offsets[i] + lengths[i])), state reset per file as in _run_vad_inference;
+   probs of file i start at sum_{k<i} lengths[k] / 512.  auto_boost != 0 scales a file whose
+   peak is in (1e-6, 0.071) to a 0.071 peak first (get_vad_segments, vad_utils.py:203-208).
+   Host buffers. */
+int zasr_vad_probs(zasr_vad* h, const float* audio, const int64_t* offsets,
+                   const int64_t* lengths, int32_t n_files, int32_t auto_boost, float* probs);
+/* the same with device-resident audio and probs; ordered after / before `stream`
+   (a hipStream_t, 0 = synchronous) */
+int zasr_vad_probs_device(zasr_vad* h, const float* d_audio, const int64_t* offsets,
+                          const int64_t* lengths, int32_t n_files, int32_t auto_boost,
+                          float* d_probs, void* stream);
+/* recurrence passes of the last probs call: a long file is decoded as parallel segments whose
+   chained start states are verified bit-exactly against the sequential recurrence (1 = the
+   warm-up guesses were all exact; set ZASR_VAD_PIT=0 before create for one workgroup per
+   file) */
+int32_t zasr_vad_last_passes(const zasr_vad* h);
+/* one session.run step for n independent streams: input [n][576], state [2][n][128] ->
+   prob [n], state_out [2][n][128] (the ORT session surface, vad_utils.py:100-102) */
+int zasr_vad_window(zasr_vad* h, const float* input, const float* state, int32_t n, float* prob,
+                    float* state_out);
+
 /* model facts */
 int32_t zasr_vocab_size(const zasr_recognizer* h);
 int32_t zasr_joiner_dim(const zasr_recognizer* h);

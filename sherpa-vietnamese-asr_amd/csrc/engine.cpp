@@ -215,7 +215,9 @@ T* Engine::ws(const std::string& name, size_t count) {
   Buf& b = ws_tag_.empty() ? ws_[name] : ws_[ws_tag_ + name];
   if (b.bytes < bytes) {
     if (b.p) {
-      ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+      // the buffer may be in use on any of the engine's streams (encoder sets, search, copy):
+      // drain the whole device before freeing it. Growth is rare (1.125x slack per buffer).
+      ZASR_HIP_CHECK(hipDeviceSynchronize());
       ZASR_HIP_CHECK(hipFree(b.p));
     }
     size_t alloc = bytes + bytes / 8;

@@ -83,6 +83,39 @@ void launch_vibert_attention(const VibertAttnArgs& a, int B, int heads, hipStrea
 void launch_vibert_gather(const float* x, const long* offsets, int B, int L, int W, int H, float* g,
                           hipStream_t st);
 
+// ---- Silero VAD pieces (vad_kernels.hip) ----
+struct VadFramesArgs {
+  const float* audio;      // file mode: concatenated audio
+  const long* off;         // [files] first sample of each file
+  const long* win_start;   // [files] first window of each file in the job
+  const unsigned* maxabs;  // [files] max |x| bits (auto boost) or nullptr
+  const float* rows576;    // row mode: [windows][576] explicit inputs (else nullptr)
+  float* frames;           // [windows * 4][256]
+  int n_files;
+};
+void launch_vad_maxabs(const float* audio, const long* off, const long* len, int n_files,
+                       unsigned* mx, hipStream_t st);
+void launch_vad_frames(const VadFramesArgs& a, long n_windows, hipStream_t st);
+void launch_vad_mag_im2col(const float* S, int ldS, int bins, int Kp, long n_windows, float* A,
+                           hipStream_t st);
+void launch_vad_im2col(const float* Y, long N, int T, int C, int stride, int Tout, float* A,
+                       hipStream_t st);
+struct VadLstmArgs {
+  const float* gx;         // [windows][512] x W_ih^T + b_ih
+  const float* whh;        // [512][128]
+  const float* bhh;        // [512]
+  const float* wd;         // [128] decoder conv weight
+  float bd;
+  const long* seg_start;   // [segments] first window whose probability the segment writes
+  const int* seg_count;    // [segments] windows written
+  const int* seg_warm;     // [segments] warm-up windows before seg_start, or nullptr
+  const float* init;       // [segments][2][128] (h, c) at the first (warm-up) window, or nullptr
+  float* s_out;            // [segments][2][128] state reached at seg_start, or nullptr
+  float* e_out;            // [segments][2][128] final state, or nullptr
+  float* probs;            // [windows]
+};
+void launch_vad_lstm(const VadLstmArgs& a, int n_segments, hipStream_t st);
+
 // ---- Conv2dSubsampling pieces (icefall subsampling.py, 3P) ----
 // conv.0 (1->8, 3x3, pad (0,1)) + SwooshR: fbank rows [T][80] -> [T-2][80][8]
 // (out_bf16: bf16 output, native-exp/log SwooshR -- the bf16 mode)

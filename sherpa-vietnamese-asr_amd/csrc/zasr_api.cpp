@@ -7,6 +7,7 @@
 #include "../../include/zasr.h"
 #include "campp.h"
 #include "common.h"
+#include "vad.h"
 #include "vibert.h"
 #include "engine.h"
 #include "host_io.h"
@@ -29,6 +30,10 @@ struct zasr_campp {
 
 struct zasr_vibert {
   std::unique_ptr<zasr::VibertEngine> eng;
+};
+
+struct zasr_vad {
+  std::unique_ptr<zasr::VadEngine> eng;
 };
 
 namespace {
@@ -151,6 +156,63 @@ int zasr_vibert_run(zasr_vibert* h, const int64_t* input_ids, const int64_t* att
                      reinterpret_cast<const long*>(token_type_ids),
                      reinterpret_cast<const long*>(input_offsets), batch, n_tokens, n_words, logits,
                      detect_logits);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_vad_create(const char* model_dir, int32_t device_id, zasr_vad** out) {
+  if (!model_dir || !out) return fail(ZASR_ERR_INVALID, "null model_dir/out");
+  *out = nullptr;
+  return guarded([&]() {
+    auto* h = new zasr_vad;
+    try {
+      h->eng.reset(new zasr::VadEngine(model_dir, device_id));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+    return (int)ZASR_OK;
+  });
+}
+
+void zasr_vad_destroy(zasr_vad* h) { delete h; }
+
+int32_t zasr_vad_last_passes(const zasr_vad* h) { return h ? h->eng->last_passes() : 0; }
+
+int zasr_vad_probs(zasr_vad* h, const float* audio, const int64_t* offsets,
+                   const int64_t* lengths, int32_t n_files, int32_t auto_boost, float* probs) {
+  if (!h || n_files < 0 || (n_files > 0 && (!audio || !offsets || !lengths || !probs)))
+    return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->probs_host(audio, reinterpret_cast<const long*>(offsets),
+                       reinterpret_cast<const long*>(lengths), n_files, auto_boost != 0, probs);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_vad_probs_device(zasr_vad* h, const float* d_audio, const int64_t* offsets,
+                          const int64_t* lengths, int32_t n_files, int32_t auto_boost,
+                          float* d_probs, void* stream) {
+  if (!h || n_files < 0 || (n_files > 0 && (!d_audio || !offsets || !lengths || !d_probs)))
+    return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->probs_device(d_audio, reinterpret_cast<const long*>(offsets),
+                         reinterpret_cast<const long*>(lengths), n_files, auto_boost != 0, d_probs,
+                         reinterpret_cast<hipStream_t>(stream));
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_vad_window(zasr_vad* h, const float* input, const float* state, int32_t n, float* prob,
+                    float* state_out) {
+  if (!h || n < 0 || (n > 0 && (!input || !state || !prob || !state_out)))
+    return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->window_host(input, state, n, prob, state_out);
     return (int)ZASR_OK;
   });
 }

@@ -27,6 +27,8 @@ EXPORTS = (
     "zasr_campp_fbank", "zasr_campp_embed", "zasr_campp_embed_device",
     "zasr_vibert_create", "zasr_vibert_destroy", "zasr_vibert_num_labels",
     "zasr_vibert_num_detect", "zasr_vibert_run",
+    "zasr_vad_create", "zasr_vad_destroy", "zasr_vad_probs", "zasr_vad_probs_device",
+    "zasr_vad_window", "zasr_vad_last_passes",
 )
 
 
@@ -144,6 +146,18 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     i64p = C.POINTER(I64)
     lib.zasr_vibert_run.argtypes = [P, i64p, i64p, i64p, i64p, I32, I32, I32, fp, fp]
     lib.zasr_vibert_run.restype = C.c_int
+    lib.zasr_vad_create.argtypes = [C.c_char_p, I32, C.POINTER(P)]
+    lib.zasr_vad_create.restype = C.c_int
+    lib.zasr_vad_destroy.argtypes = [P]
+    lib.zasr_vad_destroy.restype = None
+    lib.zasr_vad_probs.argtypes = [P, fp, i64p, i64p, I32, I32, fp]
+    lib.zasr_vad_probs.restype = C.c_int
+    lib.zasr_vad_probs_device.argtypes = [P, P, i64p, i64p, I32, I32, P, P]
+    lib.zasr_vad_probs_device.restype = C.c_int
+    lib.zasr_vad_window.argtypes = [P, fp, fp, I32, fp, fp]
+    lib.zasr_vad_window.restype = C.c_int
+    lib.zasr_vad_last_passes.argtypes = [P]
+    lib.zasr_vad_last_passes.restype = I32
     if path is None:
         _lib = lib
     return lib
@@ -446,3 +460,81 @@ class VibertSession:
             raise ZasrError(self.lib.zasr_last_error().decode())
         outs = {"logits": lg, "detect_logits": dl}
         return [lg, dl] if output_names is None else [outs[n] for n in output_names]
+
+
+class VadSession:
+    """Silero VAD on the GPU.  probs() runs whole files (the reference's
+    per-window loop at core/vad_utils.py:80-111, batched); run(None, feeds) is the
+    onnxruntime session surface ({input [n, 576], state [2, n, 128], sr} -> [prob [n, 1],
+    state]) for the reference's per-window callers."""
+
+    def __init__(self, model_dir: str, device_id: int = 0, lib_path: Optional[str] = None):
+        self.lib = load_library(lib_path)
+        h = C.c_void_p()
+        rc = self.lib.zasr_vad_create(model_dir.encode(), device_id, C.byref(h))
+        if rc != 0:
+            msg = self.lib.zasr_last_error().decode()
+            if rc == 2:
+                raise FileNotFoundError(msg)
+            raise ZasrError(msg)
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.zasr_vad_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ZasrError(self.lib.zasr_last_error().decode())
+
+    def probs(self, audios: Sequence[np.ndarray], auto_boost: bool = False) -> List[np.ndarray]:
+        audios = [np.ascontiguousarray(a, np.float32) for a in audios]
+        lens = np.array([a.shape[0] for a in audios], np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        flat = np.concatenate(audios) if audios else np.zeros(0, np.float32)
+        nw = lens // 512
+        out = np.empty(int(nw.sum()), np.float32)
+        fp = C.POINTER(C.c_float)
+        i64 = C.POINTER(C.c_int64)
+        if out.size:
+            self._check(self.lib.zasr_vad_probs(self.handle, flat.ctypes.data_as(fp),
+                                                offs.ctypes.data_as(i64), lens.ctypes.data_as(i64),
+                                                len(audios), int(auto_boost),
+                                                out.ctypes.data_as(fp)))
+        bounds = np.concatenate([[0], np.cumsum(nw)])
+        return [out[bounds[i]:bounds[i + 1]] for i in range(len(audios))]
+
+    @property
+    def last_passes(self) -> int:
+        return int(self.lib.zasr_vad_last_passes(self.handle))
+
+    def probs_device(self, d_audio: int, offsets: Sequence[int], lengths: Sequence[int],
+                     d_probs: int, auto_boost: bool = False, stream: int = 0) -> None:
+        offs = np.ascontiguousarray(offsets, np.int64)
+        lens = np.ascontiguousarray(lengths, np.int64)
+        i64 = C.POINTER(C.c_int64)
+        self._check(self.lib.zasr_vad_probs_device(
+            self.handle, C.c_void_p(d_audio), offs.ctypes.data_as(i64), lens.ctypes.data_as(i64),
+            len(offs), int(auto_boost), C.c_void_p(d_probs), C.c_void_p(stream)))
+
+    def run(self, output_names, feeds):
+        x = np.ascontiguousarray(feeds["input"], np.float32)
+        st = np.ascontiguousarray(feeds["state"], np.float32)
+        sr = int(np.asarray(feeds.get("sr", 16000)))
+        if sr != 16000 or x.ndim != 2 or x.shape[1] != 576 or st.shape != (2, x.shape[0], 128):
+            raise ZasrError("Silero VAD session: input [n, 576] at 16 kHz, state [2, n, 128]")
+        n = x.shape[0]
+        p = np.empty(n, np.float32)
+        so = np.empty_like(st)
+        fp = C.POINTER(C.c_float)
+        self._check(self.lib.zasr_vad_window(self.handle, x.ctypes.data_as(fp),
+                                             st.ctypes.data_as(fp), n, p.ctypes.data_as(fp),
+                                             so.ctypes.data_as(fp)))
+        return [p[:, None], so]

@@ -5,6 +5,9 @@
     import core.asr_engine, core.hardware_accel, core.calibration  # the reference's modules
     from zasr.dropin import install
     install(core.asr_engine, core.hardware_accel, core.calibration)  # before the pipeline runs
+    # optional: Silero VAD on the GPU too (needs models/silero-vad/silero_config.json +
+    # silero_vad.safetensors, zasr/silero.py)
+    import core.vad_utils; install(core.asr_engine, vad_module=core.vad_utils)
 
 This build's modules live in the `zasr` package, so importing them never shadows the
 reference's `core` package (both trees can be on sys.path in any order).
@@ -20,8 +23,12 @@ What is rebound (the ASR hot path, core/asr_engine.py:698-1326):
                   punctuation, DNSMOS) keep running on onnxruntime as before
   calibration     detect_calibration_status / run_device_calibration (the provider picker is
                   removed per the north star; ASR always runs on MI355X)
+  vad_utils       (only when vad_module is given) _get_vad_session, unload_vad_model,
+                  get_cached_vad_probs, _run_vad_inference, get_vad_segments; and the
+                  get_vad_segments / unload_vad_model names asr_engine imported from it
+                  (core/asr_engine.py:580)
 
-get_ort, TranscriberPipeline, the overlap merge, ROVER vote, VAD and UI glue stay the
+get_ort, TranscriberPipeline, the overlap merge, ROVER vote and UI glue stay the
 reference's.  create_recognizer reads the hotword file and score through the reference
 module's own get_hotwords_config (core/config.py:385-408), as the reference does (:993-1003).
 Returns the list of names rebound.
@@ -35,10 +42,14 @@ ENGINE_NAMES = ("compute_fbank_ort", "_log_add", "create_recognizer", "_ort_beam
                 "_compute_token_entropy", "_finalize_word_entropy", "decode_chunk")
 ACCEL_NAMES = ("configure_gpu_addon_paths",)
 CALIBRATION_NAMES = ("detect_calibration_status", "run_device_calibration")
+VAD_NAMES = ("_get_vad_session", "unload_vad_model", "get_cached_vad_probs",
+             "_run_vad_inference", "get_vad_segments")
+VAD_ENGINE_NAMES = ("get_vad_segments", "unload_vad_model")
 
 
 def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None,
-            calibration_module: Optional[ModuleType] = None) -> List[str]:
+            calibration_module: Optional[ModuleType] = None,
+            vad_module: Optional[ModuleType] = None) -> List[str]:
     from zasr import asr_engine as ours
     from zasr import calibration as ours_cal
     from zasr import hardware_accel as ours_hw
@@ -66,4 +77,16 @@ def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None
         for n in CALIBRATION_NAMES:
             setattr(calibration_module, n, getattr(ours_cal, n))
             done.append("calibration." + n)
+    if vad_module is not None:
+        from zasr import vad_utils as ours_vad
+        if vad_module is ours_vad:
+            raise ValueError("install() needs the reference's core.vad_utils module")
+        ours_vad.set_base_dir(getattr(vad_module, "BASE_DIR", None))
+        for n in VAD_NAMES:
+            setattr(vad_module, n, getattr(ours_vad, n))
+            done.append("vad_utils." + n)
+        for n in VAD_ENGINE_NAMES:
+            if hasattr(engine_module, n):
+                setattr(engine_module, n, getattr(ours_vad, n))
+                done.append("asr_engine." + n)
     return done

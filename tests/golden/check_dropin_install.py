@@ -90,6 +90,21 @@ def check(ref_root: str, ours_first: bool) -> None:
     phrases = parse_hotwords_file(hw_file)
     assert len(phrases) > 200, len(phrases)
     os.remove(hw_file)  # prepare_hotwords_file writes a temp copy
+
+    # VAD (opt-in): the reference's core.vad_utils names and the two asr_engine imported
+    # from it (core/asr_engine.py:580) become this build's; BASE_DIR decides the model dir
+    with contextlib.redirect_stdout(io.StringIO()):
+        import core.vad_utils as ref_vad
+    import zasr.vad_utils as ours_vad
+    from zasr.dropin import VAD_ENGINE_NAMES, VAD_NAMES
+    done_vad = install(ref, vad_module=ref_vad)
+    for n in VAD_NAMES:
+        assert getattr(ref_vad, n) is getattr(ours_vad, n), n
+    for n in VAD_ENGINE_NAMES:
+        assert getattr(ref, n) is getattr(ours_vad, n), n
+    os.environ.pop("ZASR_VAD_MODEL_DIR", None)
+    assert ours_vad.model_dir() == os.path.join(ref_vad.BASE_DIR, "models", "silero-vad")
+    done += [d for d in done_vad if d.startswith("vad_utils.")]
     print("dropin install ok (%s first): %d names rebound, %d hotword phrases via "
           "get_hotwords_config" % ("zasr" if ours_first else "reference", len(done), len(phrases)))
 

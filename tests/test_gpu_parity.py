@@ -432,3 +432,35 @@ def test_pipelined_batches_equal_per_batch_decode(need_gpu, method, beam):
         i += len(b)
     assert sum(r.token_ids.size for r in piped) > 20
     rec.close()
+
+
+def test_pipelined_workspace_growth_mid_pipeline(need_gpu):
+    """Batches of strictly growing size on a fresh engine: every workspace buffer is
+    reallocated while the previous batch's search and the next batch's encoder are in flight
+    on other streams (Engine::ws drains the device before freeing). Results must equal
+    per-batch decoding."""
+    import torch
+    from model_fixtures import m_model
+    from zasr.binding import Recognizer
+    cfg, w, path = m_model()
+    secs = [[0.5], [3.0, 1.0], [12.0, 9.0, 2.0], [30.0, 33.0, 28.0, 31.0, 25.0]]
+    batches = [[_speech(s, 1700 + 10 * i + j) for j, s in enumerate(b)] for i, b in enumerate(secs)]
+    flat = [c for b in batches for c in b]
+    lens = [c.shape[0] for c in flat]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    d = torch.from_numpy(np.concatenate(flat)).cuda()
+    torch.cuda.synchronize()
+    rec = Recognizer(path, "modified_beam_search", 4, precision="bf16")
+    piped = rec.decode_device_batches(d.data_ptr(), offs, lens, [len(b) for b in batches])
+    rec.close()
+    ref = Recognizer(path, "modified_beam_search", 4, precision="bf16")
+    alone = []
+    i = 0
+    for b in batches:
+        alone += ref.decode_device(d.data_ptr(), offs[i:i + len(b)], lens[i:i + len(b)])
+        i += len(b)
+    ref.close()
+    for a, p in zip(alone, piped):
+        assert a.token_ids.tolist() == p.token_ids.tolist()
+        assert a.frames.tolist() == p.frames.tolist()
+        np.testing.assert_array_equal(a.log_probs, p.log_probs)

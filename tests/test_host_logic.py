@@ -70,3 +70,27 @@ def test_dropin_install_rebinds_hot_path_names():
     with pytest.raises(ValueError):
         install(ours)
     ours.set_host_module(None)
+
+
+def test_dropin_install_vad_is_opt_in():
+    import types
+    import zasr.asr_engine as ours
+    import zasr.vad_utils as ours_vad
+    from zasr.dropin import VAD_NAMES, install
+    ref = types.ModuleType("core_asr_engine_standin")
+    ref.get_vad_segments = ref.unload_vad_model = None
+    install(ref)
+    assert ref.get_vad_segments is None  # no vad_module: the reference's VAD stays
+    vad = types.ModuleType("core_vad_utils_standin")
+    vad.BASE_DIR = "/opt/app"
+    for n in VAD_NAMES:
+        setattr(vad, n, None)
+    done = install(ref, vad_module=vad)
+    assert ref.get_vad_segments is ours_vad.get_vad_segments
+    assert vad._get_vad_session is ours_vad._get_vad_session
+    assert "vad_utils.get_vad_segments" in done
+    assert ours_vad.model_dir() == "/opt/app/models/silero-vad" or "ZASR_VAD_MODEL_DIR" in os.environ
+    with pytest.raises(ValueError):
+        install(ref, vad_module=ours_vad)
+    ours_vad.set_base_dir(None)
+    ours.set_host_module(None)
