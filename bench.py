@@ -127,7 +127,13 @@ def load_hotwords(path: str, V: int):
     return hash_tokenize_phrases(parse_hotwords_file(path, 1.5), V)
 
 
-FFN_FUSED_DIMS = (64, 96, 128, 192)  # ffn_kernels.hip ffn_fused_supported
+FFN_FUSED_DIMS = (64, 96, 128, 192, 256, 384, 512)  # ffn_kernels.hip ffn_fused_supported
+
+
+def ffn_fused(d: int, f: int) -> bool:
+    """Engine::layer_forward's choice: the fused FFN (ffn_fused_kernel up to 192,
+    ffn_wide_kernel from 256 with F a multiple of 32 up to 2048)."""
+    return d in FFN_FUSED_DIMS and (d < 256 or (f % 32 == 0 and f <= 2048))
 
 
 def gemm_class_work(cfg, L_list, bf16: bool):
@@ -166,7 +172,7 @@ def gemm_class_work(cfg, L_list, bf16: bool):
         for _ in range(cfg.num_layers[i]):
             lin(R, d, (2 * cfg.query_head_dim + cfg.pos_head_dim) * h, c=h16)
             for f in ((F * 3) // 4, F, (F * 5) // 4):
-                if bf16 and d in FFN_FUSED_DIMS:
+                if bf16 and ffn_fused(d, f):
                     acc["ffn_fused"][0] += 4.0 * R * d * f
                     acc["ffn_fused"][1] += 8.0 * R * d + 2 * 2.0 * f * d
                 else:

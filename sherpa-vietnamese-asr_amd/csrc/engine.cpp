@@ -501,6 +501,23 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
           for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mk(*l);
       }
     ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+    // the wide fused FFN (model dims 256..512) reads W1 / W2 in MFMA-fragment order
+    for (auto& s : model_.stacks)
+      for (auto& L : s.layers)
+        for (int a = 0; a < 3; ++a) {
+          const int F = L.ff_in[a].N, d = L.ff_in[a].K;
+          if (d < 256 || !ffn_fused_supported(d) || F % 32 != 0 || F > 2048) continue;
+          for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) {
+            std::vector<__bf16> h((size_t)l->N * l->K), pk(h.size());
+            ZASR_HIP_CHECK(hipMemcpy(h.data(), l->wh, h.size() * 2, hipMemcpyDeviceToHost));
+            ffn_pack_host(h.data(), l->N, l->K, pk.data());
+            void* p = nullptr;
+            ZASR_HIP_CHECK(hipMalloc(&p, pk.size() * 2));
+            model_.allocations.push_back(p);
+            ZASR_HIP_CHECK(hipMemcpy(p, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+            l->wp = p;
+          }
+        }
   }
   // ---- decoder-context table (kernels.h, DecTable): V^2 x D f32, built once ----
   {
@@ -885,10 +902,12 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     const DLin& fi = Ly.ff_in[k];
     const float* bo = (bf16 && k == 1) ? O : nullptr;
     const float* bs = (bf16 && k == 1) ? Ly.bypass_mid : nullptr;
-    if (fi.wh && !ffn_unfused && ffn_fused_supported(d)) {
+    if (fi.wh && !ffn_unfused && ffn_fused_supported(d) && (d < 256 || fi.wp)) {
       // bf16 mode: in_proj -> SwooshL -> out_proj + residual in one kernel, hidden on chip
+      // (d >= 256: the fragment-packed weights of ffn_wide_kernel)
       prof_begin("ffn_fused");
-      launch_ffn_fused(X, R, d, fi.N, fi.wh, fi.b, Ly.ff_out[k].wh, Ly.ff_out[k].b, st_, bo, bs);
+      launch_ffn_fused(X, R, d, fi.N, d < 256 ? fi.wh : fi.wp, fi.b,
+                       d < 256 ? Ly.ff_out[k].wh : Ly.ff_out[k].wp, Ly.ff_out[k].b, st_, bo, bs);
       prof_end();
       return;
     }

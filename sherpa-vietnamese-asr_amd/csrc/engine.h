@@ -31,6 +31,7 @@ struct DLin {
   int N = 0, K = 0;
   void* wh = nullptr;  // bf16 copy of w (precision mode bf16)
   float* bh = nullptr; // bias of the bf16 path when it differs from b (folded row scales)
+  void* wp = nullptr;  // bf16 in MFMA-fragment order (ffn_pack_host), the wide fused FFN's operand
 };
 
 struct DLayer {

@@ -20,13 +20,29 @@
 
 namespace zasr {
 
+#ifdef ZASR_FFN_STAMPS  // development: per-phase wall clock of block 0 (tools/ffnw_lab.hip)
+__device__ long long g_ffn_stamps[4096];
+#define FFN_STAMP(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (i) < 4096) g_ffn_stamps[(i)] = clock64();
+#else
+#define FFN_STAMP(i)
+#endif
+
 namespace {
+
+// LDS-only barrier: __syncthreads() also waits for every global load in flight (vmcnt(0)),
+// which would drain the weight prefetches at each of the two barriers per chunk
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTok = 128;  // tokens per block (4 waves x 32)
+constexpr int kMaxF = 2048; // ffn_wide_kernel: b1 staged in LDS
 constexpr int kW2Ld = 40;  // W2 chunk row stride (bf16): 80 B
 
 // slot of hidden index k (0..31) in a permuted W2 chunk row: swap bits 2 and 3
@@ -190,9 +206,197 @@ __global__ __launch_bounds__(256, (D <= 192 ? 2 : 1)) void ffn_fused_kernel(floa
     }
 }
 
-// D = 256 compiles to one wave per SIMD (384 registers) and measured slower than the two
-// GEMMs (tools/ffn_lab.hip): fused only up to 192
-bool ffn_fused_supported(int D) { return D == 64 || D == 96 || D == 128 || D == 192; }
+// Wide model dims (256, 384, 512), where the one-wave-per-32-tokens design above runs out of
+// registers: a block of 8 waves (two per SIMD, so one wave's loads hide behind the other's
+// MFMAs) owns a 64-token tile held once in LDS as bf16, and per 128-unit hidden chunk
+//   phase A  H^T = W1_c X^T     wave w computes hidden units 16 w .. 16 w + 15 for the four
+//                               16-token tiles (v_mfma_f32_16x16x32_bf16; A = W1 rows from
+//                               global/L2, B = X^T from LDS): each W1 fragment feeds 4 MFMAs
+//   (+ b1, SwooshL, bf16 -> the chunk's H in LDS, [token][hidden])
+//   phase B  O^T += W2_c H^T    wave w owns output channels [w D/8, (w + 1) D/8) for all 64
+//                               tokens (A = W2 rows from global/L2, B = H^T from LDS)
+// so the hidden activation never leaves the CU and each weight element is read once per
+// block (256 B per hidden unit per 64 tokens).  Weight fragments are register-prefetched a
+// phase ahead: the chunk's W2 fragments are issued before its phase A, the next chunk's W1
+// fragments right after this chunk's phase A.  Two barriers per chunk around the H write.
+// Epilogue as above: X += O^T + b2 (+ bypass_mid).
+template <int D>
+__global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X, int R, int F,
+                                                          const __bf16* __restrict__ W1,
+                                                          const float* __restrict__ b1,
+                                                          const __bf16* __restrict__ W2,
+                                                          const float* __restrict__ b2,
+                                                          const float* __restrict__ byp_orig,
+                                                          const float* __restrict__ byp_scale) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int TT = 64, HC = 128, NW = 8;
+  constexpr int XLD = D + 8, HLD = HC + 8;  // bf16 row strides (odd multiples of 16 B)
+  constexpr int KS = D / 32;                // phase-A k-steps (K = 32 per MFMA)
+  constexpr int OW = D / NW, OT = OW / 16;  // output channels / 16-row tiles per wave
+  __shared__ __attribute__((aligned(16))) __bf16 sX[TT * XLD];
+  constexpr int NB = D >= 384 ? 2 : 1;  // H buffers (double-buffering measured slower at 256)
+  __shared__ __attribute__((aligned(16))) __bf16 sH[NB][TT * HLD];
+  __shared__ __attribute__((aligned(16))) float sB1[kMaxF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const long t0 = (long)blockIdx.x * TT;
+
+  FFN_STAMP(0)
+  // ---- X tile -> bf16 LDS (rows past R: a clamped duplicate, never written back) ----
+  {
+    constexpr int NE = TT * D / 4 / (64 * NW);
+    float4 v[NE];
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
+      const long r = t0 + row < R ? t0 + row : R - 1;
+      v[i] = *reinterpret_cast<const float4*>(X + r * D + 4 * c4);
+    }
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
+      bf16x4 b;
+      b[0] = (__bf16)v[i].x; b[1] = (__bf16)v[i].y; b[2] = (__bf16)v[i].z; b[3] = (__bf16)v[i].w;
+      *reinterpret_cast<bf16x4*>(&sX[row * XLD + 4 * c4]) = b;
+    }
+  }
+
+  f32x4 o[OT][4];
+#pragma unroll
+  for (int t = 0; t < OT; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = (F + HC - 1) / HC;
+  // unconditional loads (a guarded load becomes a branch whose waits drain every load in
+  // flight): W1 rows past F clamp to row F - 1, W2 columns past F clamp into the row; both
+  // meet zero H (see below)
+  // W1 / W2 in MFMA-fragment order (ffn_pack_weights): every fragment load is one
+  // contiguous 1 KB wave read
+  const int S2 = F / 32;  // k-steps of a W2 row group
+  bf16x8 w1f[KS];
+  auto load_w1 = [&](int c) {
+    const int rg = min((c * HC) / 16 + wid, F / 16 - 1);
+    const __bf16* p = W1 + ((long)rg * KS * 64 + lane) * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(p + s * 512);
+  };
+  bf16x8 w2f[4][OT];
+  auto load_w2 = [&](int c) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ks = min(c * (HC / 32) + s, S2 - 1);
+#pragma unroll
+      for (int t = 0; t < OT; ++t)
+        w2f[s][t] = *reinterpret_cast<const bf16x8*>(W2 + (((long)(wid * OW / 16 + t) * S2 + ks) * 64 + lane) * 8);
+    }
+  };
+  load_w1(0);
+  load_w2(0);
+  for (int e = tid; e < F; e += 64 * NW) sB1[e] = b1[e];
+  lds_barrier();
+  FFN_STAMP(1)
+  for (int c = 0; c < nch; ++c) {
+    const int hid0 = c * HC + wid * 16;
+    const bool hvalid = hid0 < F;  // F % 16 == 0: a wave's 16 units are all valid or none
+    FFN_STAMP(2 + 4 * c)
+    f32x4 ha[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ha[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&sX[(16 * u + r16) * XLD + 32 * s + 8 * g4]);
+        ha[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[s], xb, ha[u], 0, 0, 0);
+      }
+    }
+    FFN_STAMP(3 + 4 * c)
+    // two buffers: H goes to buffer c & 1; every wave finished reading it (chunk c - 2's
+    // phase B) before it passed chunk c - 1's barrier, which precedes this write.  One
+    // buffer: a barrier first, so the previous chunk's phase B is done everywhere
+    if constexpr (NB == 1) lds_barrier();
+    FFN_STAMP(4 + 4 * c)
+    __bf16* sHc = sH[NB == 2 ? (c & 1) : 0];
+    if (hvalid) {
+      const float4 bb = *reinterpret_cast<const float4*>(&sB1[hid0 + 4 * g4]);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        bf16x4 p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = (__bf16)swooshl_fast(ha[u][q] + bv[q]);
+        *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = p;
+      }
+    } else {  // hidden units past F (tail chunk): zero H columns
+      const bf16x4 z = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = z;
+    }
+    lds_barrier();
+    FFN_STAMP(5 + 4 * c)
+    // in-order vmcnt: the next chunk's W1 (needed first) is issued before its W2
+    load_w1(min(c + 1, nch - 1));  // unconditional: a branch here costs exact vmcnt tracking
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 hf[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) hf[u] = *reinterpret_cast<const bf16x8*>(&sHc[(16 * u + r16) * HLD + 32 * s + 8 * g4]);
+#pragma unroll
+      for (int t = 0; t < OT; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[s][t], hf[u], o[t][u], 0, 0, 0);
+    }
+    load_w2(min(c + 1, nch - 1));
+  }
+
+  // ---- X[tok][ch] += O^T + b2 (+ bypass_mid): lane's token, 4 consecutive channels ----
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long tok = t0 + 16 * u + r16;
+    if (tok >= R) continue;
+    float* xr = X + tok * D;
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      const int ch = wid * OW + 16 * t + 4 * g4;
+      const float4 bv = *reinterpret_cast<const float4*>(b2 + ch);
+      float4 v = *reinterpret_cast<const float4*>(xr + ch);
+      v.x += o[t][u][0] + bv.x;
+      v.y += o[t][u][1] + bv.y;
+      v.z += o[t][u][2] + bv.z;
+      v.w += o[t][u][3] + bv.w;
+      if (byp_orig != nullptr) {
+        const float4 b0 = *reinterpret_cast<const float4*>(byp_orig + tok * D + ch);
+        const float4 k = *reinterpret_cast<const float4*>(byp_scale + ch);
+        v.x = b0.x + (v.x - b0.x) * k.x;
+        v.y = b0.y + (v.y - b0.y) * k.y;
+        v.z = b0.z + (v.z - b0.z) * k.z;
+        v.w = b0.w + (v.w - b0.w) * k.w;
+      }
+      *reinterpret_cast<float4*>(xr + ch) = v;
+    }
+  }
+}
+
+// D = 256 in the one-wave-per-32-tokens design compiles to one wave per SIMD (384
+// registers) and measured slower than the two GEMMs (tools/ffn_lab.hip); 256..512 use
+// ffn_wide_kernel
+// W1 [F][D] -> fragments [F/16][D/32][64 lanes][8] and W2 [D][F] -> [D/16][F/32][64][8]:
+// element j of lane l of fragment (g, s) is W[16 g + (l & 15)][32 s + 8 (l >> 4) + j]
+void ffn_pack_host(const __bf16* w, int rows, int cols, __bf16* out) {
+  for (int g = 0; g < rows / 16; ++g)
+    for (int s = 0; s < cols / 32; ++s)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j)
+          out[(((size_t)g * (cols / 32) + s) * 64 + l) * 8 + j] =
+              w[(size_t)(16 * g + (l & 15)) * cols + 32 * s + 8 * (l >> 4) + j];
+}
+
+bool ffn_fused_supported(int D) {
+  return D == 64 || D == 96 || D == 128 || D == 192 || D == 256 || D == 384 || D == 512;
+}
 
 void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float* b1,
                       const void* W2, const float* b2, hipStream_t st, const float* byp_orig,
@@ -200,16 +404,28 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
   if (R <= 0) return;
   ZASR_REQUIRE(ffn_fused_supported(D), "ffn_fused: unsupported model dim");
   ZASR_REQUIRE(F % 8 == 0, "ffn_fused: feed-forward dim must be a multiple of 8");
-  const dim3 grid(cdiv(R, kTok));
   const __bf16* w1 = reinterpret_cast<const __bf16*>(W1);
   const __bf16* w2 = reinterpret_cast<const __bf16*>(W2);
+  if (D >= 256) {
+    ZASR_REQUIRE(F % 32 == 0 && F >= 32 && F <= kMaxF,
+                 "ffn_fused: feed-forward dim must be a multiple of 32 in [32, 2048] for D >= 256");
+    const dim3 grid(cdiv(R, 64));
+#define ZASR_FFNW(DV) hipLaunchKernelGGL(ffn_wide_kernel<DV>, grid, dim3(512), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
+    switch (D) {
+      case 256: ZASR_FFNW(256); break;
+      case 384: ZASR_FFNW(384); break;
+      default: ZASR_FFNW(512); break;
+    }
+#undef ZASR_FFNW
+    return;
+  }
+  const dim3 grid(cdiv(R, kTok));
 #define ZASR_FFN(DV) hipLaunchKernelGGL(ffn_fused_kernel<DV>, grid, dim3(256), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
   switch (D) {
     case 64: ZASR_FFN(64); break;
     case 96: ZASR_FFN(96); break;
     case 128: ZASR_FFN(128); break;
-    case 192: ZASR_FFN(192); break;
-    default: ZASR_FFN(256); break;
+    default: ZASR_FFN(192); break;
   }
 #undef ZASR_FFN
 }

@@ -237,6 +237,7 @@ void launch_attn_sa(const AttnSAArgs& a, bool online, bool bf16, hipStream_t st)
 // ---- fused FeedforwardModule, bf16 mode (ffn_kernels.hip) ----
 // X[R][D] += W2 SwooshL(W1 X + b1) + b2; W1 [F][D], W2 [D][F] bf16; D in {64, 96, 128, 192, 256}
 bool ffn_fused_supported(int D);
+void ffn_pack_host(const __bf16* w, int rows, int cols, __bf16* out);
 void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float* b1,
                       const void* W2, const float* b2, hipStream_t st,
                       const float* byp_orig = nullptr, const float* byp_scale = nullptr);
