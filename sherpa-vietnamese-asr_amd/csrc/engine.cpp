@@ -283,6 +283,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     std::vector<uint32_t> ms((ncu + 31) / 32, 0u), me((ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; ++c) (c < search_cus_ ? ms : me)[c / 32] |= 1u << (c % 32);
     ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2_, (uint32_t)ms.size(), ms.data()));
+    ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream3_, (uint32_t)ms.size(), ms.data()));
     ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)me.size(), me.data()));
     for (auto& x : enc_extra_)
       ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&x, (uint32_t)me.size(), me.data()));
@@ -292,6 +293,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     int least = 0, greatest = 0;
     ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
+    ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream3_, hipStreamNonBlocking, greatest));
     for (auto& x : enc_extra_) ZASR_HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   }
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -622,11 +624,13 @@ Engine::~Engine() {
     (void)hipEventDestroy(pe.b);
   }
   (void)hipStreamSynchronize(stream2_);
+  (void)hipStreamSynchronize(stream3_);
   if (h_pinned_) (void)hipHostFree(h_pinned_);
   for (auto& a : pin_)
     if (a.p) (void)hipHostFree(a.p);
   for (auto e : part_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(stream2_);
+  (void)hipStreamDestroy(stream3_);
   for (auto x : enc_extra_) {
     (void)hipStreamSynchronize(x);
     (void)hipStreamDestroy(x);
@@ -1390,38 +1394,114 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     }
     for (auto e : live_ev) (void)hipEventDestroy(e);
   } else {
-  prof_begin("search");
-  launch_search_init(st, S, H, st_);
-  if (model_.dec_table) launch_table_init(dt, S, H, st_);
-  prof_end();
-  // per frame: [decoder + J when there is no table] -> joiner -> search step (which writes
-  // the next frame's J from the table)
-  int active = S;
+  // beam search: the streams are split into G groups whose frame chains run concurrently on
+  // the two search streams (each group's chain is latency-bound: joiner -> search step per
+  // frame; two chains interleave their launch and scheduling waits).  Group g holds the
+  // streams order[g], order[g + G], ... (each group sorted by T' descending, active streams
+  // a prefix), laid out contiguously; the search final runs over all of them.
+  static const int env_groups = getenv("ZASR_SEARCH_GROUPS") ? atoi(getenv("ZASR_SEARCH_GROUPS")) : 2;
+  const int G = std::max(1, std::min({env_groups, 2, S}));
+  if (G > 1) {
+    std::vector<int> reord;
+    for (int g = 0; g < G; ++g)
+      for (int i = g; i < S; i += G) reord.push_back(order[i]);
+    order = reord;
+    for (int i = 0; i < S; ++i) {
+      eo[i] = enc_off_all[order[i]];
+      el[i] = t_out[order[i]];
+    }
+    upload(d_eo, eo.data(), S * sizeof(int));
+    upload(d_el, el.data(), S * sizeof(int));
+  }
+  struct Group {
+    int s0, n;
+    SearchState st;
+    DecTable dt;
+    void* J;
+    float* logits;
+    hipStream_t stream;
+    int active;
+  };
+  std::vector<Group> grp(G);
+  for (int g = 0, s0 = 0; g < G; ++g) {
+    Group& q = grp[g];
+    q.s0 = s0;
+    q.n = (S - g + G - 1) / G;
+    s0 += q.n;
+    q.st = st;
+    const size_t so = (size_t)q.s0 * H, no = (size_t)q.s0 * st.node_cap;
+    q.st.lp += so; q.st.lpf += so; q.st.hash += so; q.st.len += so; q.st.y1 += so; q.st.y2 += so;
+    q.st.hw += so; q.st.node += so; q.st.nh += q.s0;
+    q.st.node_tok += no; q.st.node_frame += no; q.st.node_parent += no; q.st.node_lp += no;
+    q.st.node_stats += no; q.st.node_count += q.s0;
+    if (g > 0) q.st.stamps = nullptr;
+    q.stream = g == 0 ? st_ : stream3_;
+    if (g == 0) {
+      q.J = J;
+      q.logits = logits;
+    } else {
+      const size_t jr = (size_t)joiner_packed_rows((long)q.n * H);
+      q.J = bf16 ? (void*)ws<__bf16>("se_joinin_h1", jr * D) : (void*)ws<float>("se_joinin1", (size_t)q.n * H * D);
+      q.logits = ws<float>("se_logits1", (size_t)q.n * H * V);
+    }
+    q.dt = dt;
+    q.dt.enc_off = d_eo + q.s0;
+    q.dt.enc_len = d_el + q.s0;
+    q.dt.J = q.J;
+    q.active = q.n;
+  }
+  if (G > 1) {  // group 1 starts after the uploads / memsets / encoder-output wait on st_
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 3], st_));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(stream3_, part_ev_[kMaxEnc + 3], 0));
+    const size_t jr = (size_t)joiner_packed_rows((long)grp[1].n * H);
+    ZASR_HIP_CHECK(hipMemsetAsync(grp[1].J, 0, (bf16 ? jr * 2 : (size_t)grp[1].n * H * 4) * D, stream3_));
+  }
+  hipStream_t home = st_;
+  for (Group& q : grp) {
+    st_ = q.stream;
+    prof_begin("search");
+    launch_search_init(q.st, q.n, H, st_);
+    if (model_.dec_table) launch_table_init(q.dt, q.n, H, st_);
+    prof_end();
+  }
+  // per frame and group: [decoder + J when there is no table] -> joiner -> search step (which
+  // writes the next frame's J from the table)
   for (int t = 0; t < Tmax; ++t) {
-    while (active > 0 && el[active - 1] <= t) --active;
-    const int rows = active * H;
-    if (!model_.dec_table) {
-      DecJoinArgs da{dw, model_.dec_proj.w, st.y1, st.y2, d_enc, d_eo, J, rows, H, t, bf16 ? 1 : 0};
-      prof_begin("decoder");
-      launch_decjoin(da, st_);
+    for (Group& q : grp) {
+      const int* qel = el.data() + q.s0;
+      while (q.active > 0 && qel[q.active - 1] <= t) --q.active;
+      if (q.active == 0) continue;
+      st_ = q.stream;
+      const int rows = q.active * H;
+      if (!model_.dec_table) {
+        DecJoinArgs da{dw, model_.dec_proj.w, q.st.y1, q.st.y2, d_enc, d_eo + q.s0, q.J, rows, H, t, bf16 ? 1 : 0};
+        prof_begin("decoder");
+        launch_decjoin(da, st_);
+        prof_end();
+      }
+      prof_begin("joiner");
+      if (packed) {
+        JoinerPackedArgs ja{q.J, model_.joiner_packed, model_.joiner.b, q.logits, rows, V, D};
+        launch_joiner_packed(ja, st_);
+      } else if (bf16) {
+        JoinerBf16Args ja{reinterpret_cast<const __bf16*>(q.J), reinterpret_cast<const __bf16*>(model_.joiner.wh),
+                          model_.joiner.b, q.logits, rows, V, D};
+        launch_joiner_bf16(ja, st_);
+      } else {
+        JoinerArgs ja{reinterpret_cast<const float*>(q.J), model_.joiner.w, model_.joiner.b, q.logits, rows, V, D};
+        launch_joiner(ja, st_);
+      }
+      prof_end();
+      prof_begin("search");
+      launch_search_step(q.st, q.logits, V, q.active, H, beam, t, d_el + q.s0, hw_,
+                         model_.dec_table ? &q.dt : nullptr, st_);
       prof_end();
     }
-    prof_begin("joiner");
-    if (packed) {
-      JoinerPackedArgs ja{J, model_.joiner_packed, model_.joiner.b, logits, rows, V, D};
-      launch_joiner_packed(ja, st_);
-    } else if (bf16) {
-      JoinerBf16Args ja{reinterpret_cast<const __bf16*>(J), reinterpret_cast<const __bf16*>(model_.joiner.wh),
-                        model_.joiner.b, logits, rows, V, D};
-      launch_joiner_bf16(ja, st_);
-    } else {
-      JoinerArgs ja{reinterpret_cast<const float*>(J), model_.joiner.w, model_.joiner.b, logits, rows, V, D};
-      launch_joiner(ja, st_);
-    }
-    prof_end();
-    prof_begin("search");
-    launch_search_step(st, logits, V, active, H, beam, t, d_el, hw_, model_.dec_table ? &dt : nullptr, st_);
-    prof_end();
+  }
+  st_ = home;
+  if (G > 1) {  // the final pick on st_ reads every group's nodes
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 3], stream3_));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(st_, part_ev_[kMaxEnc + 3], 0));
   }
   }
   const int cap = Tmax;

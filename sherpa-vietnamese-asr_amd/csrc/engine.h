@@ -208,10 +208,11 @@ class Engine {
   int precision_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
+  hipStream_t stream3_ = nullptr;  // the second group of a beam search (high priority)
   int search_cus_ = 0;             // > 0: search / encoder streams on disjoint CU sets
   hipStream_t enc_extra_[kMaxEnc - 1] = {};  // encoder streams 1.. of the batch pipeline
   // [0, kMaxEnc]: encoder output slots; kMaxEnc + 1: search done; kMaxEnc + 2: start
-  hipEvent_t part_ev_[kMaxEnc + 3] = {};
+  hipEvent_t part_ev_[kMaxEnc + 4] = {};
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;
   // fbank tables
