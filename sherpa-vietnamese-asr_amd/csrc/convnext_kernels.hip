@@ -166,7 +166,27 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
 // pointwise MLP + residual.  Y / H tiles in LDS: [128 positions][136] bf16 (272-byte rows:
 // conflict-free 16-byte fragment reads).  Wave w owns hidden (pw1) / output (pw2) columns
 // 32 w .. 32 w + 31 of each 128-wide slice, for all 128 positions (4 MFMA tiles).
+// W1 / W2 arrive in MFMA-fragment order (pack_frag32_host: one contiguous 1 KB wave read per
+// fragment), b1 is staged in LDS, and the slice barriers are LDS-only, so the weight
+// prefetches stay in flight across them.
 // =====================================================================================
+namespace {
+__device__ __forceinline__ void lds_barrier_cx() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+}  // namespace
+
+// W [rows][cols] bf16 -> [rows/32][cols/16][64 lanes][8]: element j of lane l of fragment
+// (g, s) is W[32 g + (l & 31)][16 s + 8 (l >> 5) + j] (v_mfma_f32_32x32x16_bf16 A operand)
+void pack_frag32_host(const __bf16* w, int rows, int cols, __bf16* out) {
+  for (int g = 0; g < rows / 32; ++g)
+    for (int s = 0; s < cols / 16; ++s)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j)
+          out[(((size_t)g * (cols / 16) + s) * 64 + l) * 8 + j] =
+              w[(size_t)(32 * g + (l & 31)) * cols + 16 * s + 8 * (l >> 5) + j];
+}
 namespace {
 constexpr int kMlpM = 128;
 constexpr int kMlpLd = 136;
@@ -178,6 +198,7 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
     const float* __restrict__ b2, __bf16* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) __bf16 Ys[kMlpM * kMlpLd];
   __shared__ __attribute__((aligned(16))) __bf16 Hs[kMlpM * kMlpLd];
+  __shared__ float sB1[384];
   const long p0 = (long)blockIdx.x * kMlpM;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int col = lane & 31, half = lane >> 5;
@@ -196,8 +217,9 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
       const int e = tid + 256 * k;
       *reinterpret_cast<bf16x8*>(Ys + (e >> 4) * kMlpLd + 8 * (e & 15)) = v[k];
     }
+    for (int e = tid; e < 384; e += 256) sB1[e] = b1[e];
   }
-  __syncthreads();
+  lds_barrier_cx();
 
   f32x16 acc2[4];
 #pragma unroll
@@ -209,18 +231,15 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
   // is fetched under slice n3's pw2 MFMAs and W2 of slice n3 under its pw1 MFMAs, so only the
   // first slice's W1 round trip is exposed
   bf16x8 wf1[8], wf2[8];
-  {
-    const int hn = wid * 32 + col;
+  // fragment (row group, k-step) of the packed images: W1 [384][128] -> [12][8], W2 [128][384] -> [4][24]
+  auto w1frag = [&](int g, int ks) { return *reinterpret_cast<const bf16x8*>(w1 + (((long)g * 8 + ks) * 64 + lane) * 8); };
+  auto w2frag = [&](int g, int ks) { return *reinterpret_cast<const bf16x8*>(w2 + (((long)g * 24 + ks) * 64 + lane) * 8); };
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      wf1[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
-  }
+  for (int ks = 0; ks < 8; ++ks) wf1[ks] = w1frag(wid, ks);
   for (int n3 = 0; n3 < 3; ++n3) {
     // ---- H^T slice: rows = hidden units n3*128 + 32 wid + (0..31), cols = positions ----
-    const int on = wid * 32 + col;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      wf2[ks] = *reinterpret_cast<const bf16x8*>(w2 + (long)on * 384 + n3 * 128 + ks * 16 + 8 * half);
+    for (int ks = 0; ks < 8; ++ks) wf2[ks] = w2frag(wid, n3 * 8 + ks);
     f32x16 acc1[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -235,17 +254,16 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
         acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf1[ks], yf, acc1[t], 0, 0, 0);
       }
     }
-    if (n3 < 2) {
-      const int hn = (n3 + 1) * 128 + wid * 32 + col;
+    {  // next slice's W1 (unconditional: a branch here costs exact vmcnt tracking)
+      const int nn = n3 < 2 ? n3 + 1 : 2;
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
-        wf1[ks] = *reinterpret_cast<const bf16x8*>(w1 + (long)hn * 128 + ks * 16 + 8 * half);
+      for (int ks = 0; ks < 8; ++ks) wf1[ks] = w1frag(nn * 4 + wid, ks);
     }
     // bias of the 16 hidden rows this lane holds: wid*32 + (r&3) + 8 (r>>2) + 4 half
     float bb[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) bb[r] = b1[n3 * 128 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
-    if (n3 > 0) __syncthreads();  // the previous slice's pw2 is done reading Hs
+    for (int r = 0; r < 16; ++r) bb[r] = sB1[n3 * 128 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+    if (n3 > 0) lds_barrier_cx();  // the previous slice's pw2 is done reading Hs
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -255,7 +273,7 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
         for (int e = 0; e < 4; ++e) hv[e] = (__bf16)swooshl_fast(acc1[t][4 * g + e] + bb[4 * g + e]);
         *reinterpret_cast<bf16x4*>(Hs + (t * 32 + col) * kMlpLd + wid * 32 + 8 * g + 4 * half) = hv;
       }
-    __syncthreads();
+    lds_barrier_cx();
     // ---- O^T += W2[:, slice] H^T: rows = output channels 32 wid + (0..31) ----
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {

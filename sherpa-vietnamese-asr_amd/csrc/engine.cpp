@@ -503,6 +503,17 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
           for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mk(*l);
       }
     ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+    // the ConvNeXt MLP reads pw1 / pw2 in MFMA-fragment order
+    for (DLin* l : {&model_.pw1, &model_.pw2}) {
+      std::vector<__bf16> h((size_t)l->N * l->K), pk(h.size());
+      ZASR_HIP_CHECK(hipMemcpy(h.data(), l->wh, h.size() * 2, hipMemcpyDeviceToHost));
+      pack_frag32_host(h.data(), l->N, l->K, pk.data());
+      void* p = nullptr;
+      ZASR_HIP_CHECK(hipMalloc(&p, pk.size() * 2));
+      model_.allocations.push_back(p);
+      ZASR_HIP_CHECK(hipMemcpy(p, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+      l->wp = p;
+    }
     // the wide fused FFN (model dims 256..512) reads W1 / W2 in MFMA-fragment order
     for (auto& s : model_.stacks)
       for (auto& L : s.layers)
@@ -1196,8 +1207,8 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       gemm_bf16(p, model_.conv7.wh, EPI_SWOOSHR, ALOAD_CONV3, st_, fe16, true);
       prof_end();
       prof_begin("frontend_conv");
-      launch_convnext_bf16(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, model_.pw1.wh,
-                           model_.pw1.b, model_.pw2.wh, model_.pw2.b, y3, x4, st_);
+      launch_convnext_bf16(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, model_.pw1.wp,
+                           model_.pw1.b, model_.pw2.wp, model_.pw2.b, y3, x4, st_);
       prof_end();
       linear_h(model_.out, x4, true, 2432, mL.total, e0, false, d0, EPI_NONE);
     } else {

@@ -125,6 +125,8 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const i
 // ConvNeXt depthwise 7x7, zero padding per sequence: [L][19][128] -> [L][19][128]
 // bf16 mode: out = x + pw2(SwooshL(pw1(dwconv7x7(x)))) (convnext_kernels.hip), x / out /
 // ytmp (the depthwise output) bf16 [rows][19][128]; w1 / w2 the bf16 pw weights
+void pack_frag32_host(const __bf16* w, int rows, int cols, __bf16* out);
+// w1 / w2: pw1 [384][128] and pw2 [128][384] packed by pack_frag32_host
 void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int total_rows,
                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
                           const void* w2, const float* b2, void* ytmp, void* out,
