@@ -308,7 +308,7 @@ __device__ __forceinline__ float epi_act(float v) {
 }
 
 template <int BM, int BN, int BK, int WAVES_M, int WAVES_N, int ALOAD, int EPI, typename TA,
-          typename TC>
+          typename TC, bool DEEP>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmParams p,
                                                                           const __bf16* Bw,
                                                                           int tiles_n,
@@ -455,6 +455,81 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nkt = (K + BK - 1) / BK;
+  auto mma_slab = [&](int cur) {
+    const __bf16* As = sbase + cur * STAGE;
+    const __bf16* Bs = As + BM * LDH;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(
+            &As[(wm * WTM + i * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(
+            &Bs[(wn * WTN + j * 32 + (lane & 31)) * LDH + ks * 16 + 8 * (lane >> 5)]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if constexpr (DEEP) {
+    // dense A, K a multiple of 2 BK (host-checked): two register sets, so each K slab's loads
+    // have two slabs of MFMAs to land; the barriers are LDS-only (__syncthreads would drain
+    // the slab in flight with vmcnt(0)); every load is unconditional (slab index clamped), so
+    // the in-order vmcnt waits stay exact
+    bf16x8 xa[2][A_LD], xb[2][B_LD];
+    auto gl = [&](bf16x8 (&ra_)[A_LD], bf16x8 (&rb_)[B_LD], int kt) {
+      const int k0 = kt * BK;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        if constexpr (std::is_same<TA, __bf16>::value) {
+          ra_[i] = *reinterpret_cast<const bf16x8*>(arow[i] + k0);
+        } else {
+          const float* a = reinterpret_cast<const float*>(arow[i]) + k0;
+          ra_[i] = to_bf16x8(*reinterpret_cast<const float4*>(a), *reinterpret_cast<const float4*>(a + 4));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) rb_[i] = *reinterpret_cast<const bf16x8*>(brow[i] + k0);
+    };
+    auto ss = [&](const bf16x8 (&ra_)[A_LD], const bf16x8 (&rb_)[B_LD], int buf) {
+      __bf16* As = sbase + buf * STAGE;
+      __bf16* Bs = As + BM * LDH;
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        const int idx = tid + NT * i;
+        if (idx < A_G) *reinterpret_cast<bf16x8*>(&As[(idx / GPR) * LDH + 8 * (idx % GPR)]) = ra_[i];
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        const int idx = tid + NT * i;
+        if (idx < B_G) *reinterpret_cast<bf16x8*>(&Bs[(idx / GPR) * LDH + 8 * (idx % GPR)]) = rb_[i];
+      }
+    };
+    auto bar = []() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    gl(xa[0], xb[0], 0);
+    gl(xa[1], xb[1], 1);
+    ss(xa[0], xb[0], 0);
+    bar();
+    for (int kt = 0; kt < nkt; kt += 2) {
+      gl(xa[0], xb[0], min(kt + 2, nkt - 1));
+      mma_slab(0);
+      ss(xa[1], xb[1], 1);
+      bar();
+      gl(xa[1], xb[1], min(kt + 3, nkt - 1));
+      mma_slab(1);
+      ss(xa[0], xb[0], 0);
+      bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail loads
+  } else {
   gload(0);
   sstore(0);
   __syncthreads();
@@ -482,6 +557,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
     }
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
+  }
   }
 
   // epilogue: fragment -> LDS (lane: column lane&31, rows (r&3)+8(r>>2)+4(lane>>5)) ->
@@ -557,11 +633,21 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
   }
 }
 
+// ZASR_GEMM_DEEP=0 turns the two-slab register prefetch off (gemm_set_deep for the labs)
+static int g_gemm_deep = -1;
+void gemm_set_deep(int on) { g_gemm_deep = on; }
+
 template <int BM, int BN, int BK, int WM, int WN, int ALOAD, int EPI, typename TA, typename TC>
 void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC>), grid,
+  if (g_gemm_deep < 0) g_gemm_deep = getenv("ZASR_GEMM_DEEP") ? atoi(getenv("ZASR_GEMM_DEEP")) : 1;
+  if (g_gemm_deep && ALOAD == ALOAD_DENSE && !p.slices && p.K % (2 * BK) == 0 && p.lda % 8 == 0) {
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, true>), grid,
+                       dim3(64 * WM * WN), 0, st, p, Bw, tn, tm);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, false>), grid,
                      dim3(64 * WM * WN), 0, st, p, Bw, tn, tm);
 }
 

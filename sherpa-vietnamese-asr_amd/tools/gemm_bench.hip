@@ -80,10 +80,10 @@ static void run_variant(const char* tag, const Shape& s, float* dA, __bf16* dA16
 
 int main() {
   std::vector<Shape> shapes = {
-      {"pw1", 3750030, 128, 384, EPI_SWOOSHL}, {"pw2", 3750030, 384, 128, EPI_RESADD},
-      {"ffin0", 197370, 192, 768, EPI_SWOOSHL}, {"ffout0", 197370, 768, 192, EPI_RESADD},
-      {"ffout2", 49342, 1152, 384, EPI_RESADD}, {"inproj1", 98685, 256, 272, EPI_NONE},
-      {"ffin3", 24671, 512, 1280, EPI_SWOOSHL},
+      {"qkp384", 49442, 384, 768, EPI_NONE},   {"in864", 49442, 384, 864, EPI_NONE},
+      {"in512", 98813, 256, 512, EPI_NONE},    {"in1024", 24753, 512, 1024, EPI_NONE},
+      {"in192", 197561, 192, 384, EPI_NONE},   {"out1024", 49442, 1024, 384, EPI_RESADD},
+      {"out384", 49442, 384, 384, EPI_RESADD}, {"out256", 98813, 256, 256, EPI_RESADD},
   };
   size_t maxA = 0, maxC = 0, maxB = 0;
   for (auto& s : shapes) {
@@ -112,24 +112,13 @@ int main() {
   hipMemcpy(dA16, hA16.data(), maxA * 2, hipMemcpyHostToDevice);
   hipMemcpy(dB, hB16.data(), maxB * 2, hipMemcpyHostToDevice);
   hipMemcpy(dbias, hbias.data(), 4096 * 4, hipMemcpyHostToDevice);
-  for (auto& s : shapes) {
-    // A/B host copies must match the shape's (K) layout: reuse the prefix
-    switch (s.epi) {
-      case EPI_SWOOSHL:
-        run_variant<32, float, float, EPI_SWOOSHL>("bk32 f32A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        run_variant<64, float, float, EPI_SWOOSHL>("bk64 f32A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        run_variant<64, float, __bf16, EPI_SWOOSHL>("bk64 f32A bf16C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        break;
-      case EPI_RESADD:
-        run_variant<32, float, float, EPI_RESADD>("bk32 f32A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        run_variant<64, float, float, EPI_RESADD>("bk64 f32A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        run_variant<64, __bf16, float, EPI_RESADD>("bk64 bf16A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        break;
-      default:
-        run_variant<32, float, float, EPI_NONE>("bk32 f32A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        run_variant<64, float, float, EPI_NONE>("bk64 f32A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        run_variant<64, __bf16, float, EPI_NONE>("bk64 bf16A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-        break;
+  for (int deep = 0; deep < 2; ++deep) {
+    gemm_set_deep(deep);
+    for (auto& s : shapes) {
+      if (s.epi == EPI_RESADD)
+        run_variant<32, __bf16, float, EPI_RESADD>(deep ? "deep bf16A f32C" : "base bf16A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
+      else
+        run_variant<32, float, __bf16, EPI_NONE>(deep ? "deep f32A bf16C" : "base f32A bf16C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
     }
   }
   return 0;
