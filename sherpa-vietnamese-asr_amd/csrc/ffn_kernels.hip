@@ -230,7 +230,10 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
                                                           const float* __restrict__ byp_scale) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   constexpr int TT = 64, HC = 128, NW = 8;
-  constexpr int XLD = D + 8, HLD = HC + 8;  // bf16 row strides (odd multiples of 16 B)
+  // bf16 row strides of 16 (8 k + 2) bytes: the 16x16x32 operand reads (row = lane & 15,
+  // 16-byte column chunk lane >> 4) then hit 16 distinct 16-byte bank slots in each of
+  // ds_read_b128's four 16-lane groups (an odd multiple of 16 B suits 32x32 reads, not these)
+  constexpr int XLD = D + 16, HLD = HC + 16;
   constexpr int KS = D / 32;                // phase-A k-steps (K = 32 per MFMA)
   constexpr int OW = D / NW, OT = OW / 16;  // output channels / 16-row tiles per wave
   __shared__ __attribute__((aligned(16))) __bf16 sX[TT * XLD];
