@@ -88,6 +88,11 @@ CamppEngine::CamppEngine(const std::string& dir, int device) : device_(device) {
     const HostTensor& t = W.get(w);
     ZASR_REQUIRE(t.numel == (size_t)32 * ci * ks * ks, "CAM++: bad shape of " + w);
     c.w = dev(t.data, t.numel);
+    if (ci == 32) {
+      std::vector<float> pk(t.numel);
+      campp_conv2d_permute_weights(t.data, ks, pk.data());
+      c.wk = devv(pk);
+    }
     std::vector<float> s, b;
     bn_fold(W, bn, 32, true, s, b);
     c.s = devv(s);
@@ -289,6 +294,7 @@ void CamppEngine::embed_device(const float* d_feats, int N, int T, float* d_out,
     CamppConv2d a{};
     a.x = x;
     a.w = c.w;
+    a.wk = c.wk;
     a.scale = c.s;
     a.shift = c.b;
     a.res = res;

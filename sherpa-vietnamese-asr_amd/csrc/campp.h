@@ -41,6 +41,7 @@ class CamppEngine {
  private:
   struct Conv2 {
     float* w = nullptr;
+    float* wk = nullptr;  // ci = 32: the MFMA kernel's weight image
     float *s = nullptr, *b = nullptr;
   };
   struct Lin {  // GEMM weight [N][K] (+ bias)

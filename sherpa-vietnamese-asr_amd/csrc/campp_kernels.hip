@@ -69,8 +69,232 @@ __global__ __launch_bounds__(256) void campp_conv2d_kernel(CamppConv2d a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The same convolution for Ci = 32 as an implicit GEMM on the exact-f32 MFMA
+// (v_mfma_f32_16x16x4f32): O^T[co][pos] = sum_k W[co][k] X^T[k][pos], k = (r KS + q) Ci + ci.
+// A block owns `rb` consecutive output frequency rows of one window and slides down them two
+// rows at a time: 4 waves = 2 rows x 2 halves of T (<= 160, 5 tiles of 16 positions each),
+// 2 co tiles of 16.  All weights are staged in LDS once per block (pre-permuted on the host);
+// the input lives in a ring of ROWS = sf + KS rows (slot = (f + pad) mod ROWS) and the 2 sf
+// rows the next step needs are loaded into registers before the MFMA loop and written into the
+// slots just retired after it, so HBM traffic overlaps the matrix work.  Channel planes are TW
+// floats apart with ROWS * TW = 16 mod 32 and the weight rows XOR-swizzled by k parity, so
+// both halves of each ds_read_b32 are bank-conflict-free.  Epilogue as campp_conv2d_kernel.
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int cx_tw(int rows) {  // smallest TW >= 162 with rows * TW = 16 (mod 32)
+  int tw = 162;
+  while ((rows * tw) % 32 != 16) ++tw;
+  return tw;
+}
+constexpr int kCxCols = 162;  // staged columns: positions < 160 read columns < 162
+
+__device__ inline void cx_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// Input staging is per wave and per plane-row (channel ci of input row g, kCxCols columns
+// from t = -pad): wave w takes plane-rows p = w + 4 i (rr = p / 32, ci = p % 32), so the row
+// and LDS addresses are scalar and a lane only adds its columns lane + 64 c (c < 3).  Loads go
+// through a buffer descriptor over this window's [32][fi][T] planes: padding and rows outside
+// [0, fi) get an out-of-range offset and load 0, so the loads are unconditional.
+struct CxLane {
+  int lt[3];  // t of column lane + 64 c, or -1 when it is padding
+};
+__device__ inline CxLane cx_lane(int lane, int pad, int T) {
+  CxLane l;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = lane + 64 * c, t = col - pad;
+    l.lt[c] = (col < kCxCols && t >= 0 && t < T) ? t : -1;
+  }
+  return l;
+}
+__device__ inline void cx_load_prow(__amdgpu_buffer_rsrc_t rs, const CamppConv2d& a, int g, int ci,
+                                    const CxLane& l, float (&v)[3]) {
+  const bool rowok = g >= 0 && g < a.fi;
+  const int base = (ci * a.fi + g) * a.T;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int off = (rowok && l.lt[c] >= 0) ? (base + l.lt[c]) * 4 : (int)0x80000000;
+    v[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+  }
+}
+template <int ROWS, int TW, int PAD>
+__device__ inline void cx_store_prow(float* sX, int g, int ci, int lane, const float (&v)[3]) {
+  float* d = sX + (ci * ROWS + (g + PAD) % ROWS) * TW + lane;
+  d[0] = v[0];
+  d[64] = v[1];
+  if (lane + 128 < kCxCols) d[128] = v[2];
+}
+}  // namespace
+
+template <int KS, int SF>
+__global__ __launch_bounds__(256, 1) void campp_conv2d_mfma_kernel(CamppConv2d a, int rb) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int CI = 32, PAD = KS / 2, ROWS = SF + KS, NEW = 2 * SF, TW = cx_tw(ROWS);
+  constexpr int K = KS * KS * CI, NT = 5;  // NT position tiles of 16 per wave
+  __shared__ float sX[CI * ROWS * TW];
+  __shared__ float sW[K * 32];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = blockIdx.y, fo_begin = blockIdx.x * rb, fo_end = min(a.fo, fo_begin + rb);
+  const int T = a.T;
+  // weights arrive pre-permuted (a.wk: the sW image, k-major, XOR-swizzled): a float4 copy
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.wk);
+    float4* dst = reinterpret_cast<float4*>(sW);
+    constexpr int NW4 = K * 32 / 4, NI = (NW4 + 255) / 256;
+    float4 v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int e = tid + 256 * i;
+      v[i] = src[e < NW4 ? e : NW4 - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int e = tid + 256 * i;
+      if (e < NW4) dst[e] = v[i];
+    }
+  }
+  // buffer descriptor over this window's input planes
+  const float* xw = a.x + (long)n * CI * a.fi * T;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)xw);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long)xw >> 32));
+  const int nbytes = __builtin_amdgcn_readfirstlane(CI * a.fi * T * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((unsigned long)hi << 32) | lo), 0, nbytes, 0x00020000);
+  const CxLane cl = cx_lane(lane, PAD, T);
+  // the first ROWS input rows, 4 plane-rows (12 loads) in flight per wave
+  {
+    const int g0 = fo_begin * SF - PAD;
+#pragma unroll 1
+    for (int i0 = 0; i0 < ROWS * 8; i0 += 4) {
+      float v[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = w + 4 * (i0 + u);
+        cx_load_prow(rs, a, g0 + (p >> 5), p & 31, cl, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = w + 4 * (i0 + u);
+        cx_store_prow<ROWS, TW, PAD>(sX, g0 + (p >> 5), p & 31, lane, v[u]);
+      }
+    }
+  }
+  __syncthreads();
+  const int orow = w >> 1, tile0 = 5 * (w & 1);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int wsw = 16 * (g4 & 1);  // k parity of this lane
+  for (int fo = fo_begin; fo < fo_end; fo += 2) {
+    // prefetch the rows the next step adds (rows past fi load as 0)
+    const int gn = fo * SF - PAD + ROWS;
+    float pv[NEW * 8][3];
+#pragma unroll
+    for (int i = 0; i < NEW * 8; ++i) {
+      const int p = w + 4 * i;
+      cx_load_prow(rs, a, gn + (p >> 5), p & 31, cl, pv[i]);
+    }
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int u = 0; u < NT; ++u) acc[m][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K loop flattened to NS = KS KS CI / 4 steps, operands double-buffered in registers so
+    // step s + 1's LDS reads are in flight under step s's 10 MFMAs
+    const int fw = fo + orow;
+    const float* xrow[KS];
+#pragma unroll
+    for (int r = 0; r < KS; ++r)
+      xrow[r] = sX + ((fw * SF + r) % ROWS) * TW + tile0 * 16 + r16;  // input row fw sf - pad + r
+    constexpr int NS = KS * KS * CI / 4;
+    float opA[2][2], opB[2][NT];
+    auto ld = [&](int st, float (&A)[2], float (&B)[NT]) {
+      const int rq = st / (CI / 4), j = st % (CI / 4), r = rq / KS, q = rq % KS;
+      const int ci = 4 * j + g4, k = rq * CI + ci;
+      A[0] = sW[k * 32 + (r16 ^ wsw)];
+      A[1] = sW[k * 32 + ((16 + r16) ^ wsw)];
+      const float* xc = xrow[r] + q + ci * ROWS * TW;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) B[u] = xc[16 * u];
+    };
+    ld(0, opA[0], opB[0]);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const int cb = st & 1;
+      if (st + 1 < NS) ld(st + 1, opA[cb ^ 1], opB[cb ^ 1]);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        acc[0][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(opA[cb][0], opB[cb][u], acc[0][u], 0, 0, 0);
+        acc[1][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(opA[cb][1], opB[cb][u], acc[1][u], 0, 0, 0);
+      }
+    }
+    // every wave is done with the retiring slots: fill them with the prefetched rows
+    cx_lds_barrier();
+#pragma unroll
+    for (int i = 0; i < NEW * 8; ++i) {
+      const int p = w + 4 * i;
+      cx_store_prow<ROWS, TW, PAD>(sX, gn + (p >> 5), p & 31, lane, pv[i]);
+    }
+    // epilogue: lane holds positions t = 16 (tile0 + u) + r16, channels 16 m + 4 g4 + e
+    if (fw < fo_end) {
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int t = 16 * (tile0 + u) + r16;
+        if (t >= T) continue;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int co = 16 * m + 4 * g4 + e;
+            float y = fmaf(acc[m][u][e], a.scale[co], a.shift[co]);
+            const long o = (((long)n * 32 + co) * a.fo + fw) * T + t;
+            if (a.res) y += a.res[o];
+            if (a.relu) y = fmaxf(y, 0.f);
+            if (a.tdnn_out)
+              a.y[((long)n * T + t) * (32 * a.fo) + co * a.fo + fw] = y;
+            else
+              a.y[o] = y;
+          }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// the MFMA kernel's weight image: w [32][32][ks][ks] -> [k = (r ks + q) 32 + ci][co ^ 16 (k & 1)]
+void campp_conv2d_permute_weights(const float* w, int ks, float* out) {
+  const int K = ks * ks * 32;
+  for (int co = 0; co < 32; ++co)
+    for (int ci = 0; ci < 32; ++ci)
+      for (int rq = 0; rq < ks * ks; ++rq) {
+        const int k = rq * 32 + ci;
+        out[k * 32 + (co ^ (16 * (k & 1)))] = w[(co * 32 + ci) * ks * ks + rq];
+      }
+  (void)K;
+}
+
 void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st) {
   ZASR_REQUIRE(a.ci <= 32 && (ks == 1 || ks == 3), "campp conv2d: Ci <= 32, kernel 1 or 3");
+  static const bool direct = getenv("ZASR_CAMPP_DIRECT_CONV") != nullptr;
+  // the 3 x 3 convolutions take the MFMA kernel; the 1 x 1 shortcut (a quarter of the
+  // rows' work, no reuse across taps) stays on the direct kernel, which measured faster
+  if (!direct && ks == 3 && a.wk && a.ci == 32 && !a.in_tf && a.T <= 160 &&
+      (a.sf == 1 || a.sf == 2)) {
+    // rows per block: about 2048 blocks per launch, an even row count, at least 2
+    const int pairs = cdiv(a.fo, 2);
+    const int chunks = std::max(1, std::min(pairs, cdiv(2048, a.n)));
+    const int rb = 2 * cdiv(pairs, chunks);
+    const dim3 grid(cdiv(a.fo, rb), a.n);
+#define ZASR_CX(KSV, SFV) \
+  hipLaunchKernelGGL((campp_conv2d_mfma_kernel<KSV, SFV>), grid, dim3(256), 0, st, a, rb)
+    if (a.sf == 1) ZASR_CX(3, 1);
+    else ZASR_CX(3, 2);
+#undef ZASR_CX
+    return;
+  }
   dim3 grid(cdiv(a.T, 64), a.fo, a.n);
   if (ks == 3) hipLaunchKernelGGL(campp_conv2d_kernel<3>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(campp_conv2d_kernel<1>, grid, dim3(256), 0, st, a);
@@ -204,19 +428,41 @@ void launch_campp_stats(const float* x, int N, int T, int C, const float* s, con
 
 // per-utterance CMVN of fbank features: x[f][m] -= mean_f x[f][m] (one block per sequence,
 // one thread per mel bin)
-__global__ void campp_cmvn_kernel(float* __restrict__ x, const int* __restrict__ fr_off) {
-  const int s = blockIdx.x, m = threadIdx.x;
+// per-sequence mean removal over frames: 12 frame groups x 80 bins per block, f64 partial
+// sums (8 loads in flight per thread) combined in LDS
+__global__ __launch_bounds__(960) void campp_cmvn_kernel(float* __restrict__ x,
+                                                         const int* __restrict__ fr_off) {
+  constexpr int G = 12;
+  __shared__ double part[G][80];
+  __shared__ float mean_s[80];
+  const int s = blockIdx.x, m = threadIdx.x % 80, g = threadIdx.x / 80;
   const int a = fr_off[s], e = fr_off[s + 1];
-  if (m >= 80 || e <= a) return;
+  if (e <= a) return;
   double sum = 0.0;
-  for (int f = a; f < e; ++f) sum += x[(long)f * 80 + m];
-  const float mean = (float)(sum / (e - a));
-  for (int f = a; f < e; ++f) x[(long)f * 80 + m] -= mean;
+  int f = a + g;
+  for (; f + 7 * G < e; f += 8 * G) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = x[(long)(f + u * G) * 80 + m];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += v[u];
+  }
+  for (; f < e; f += G) sum += x[(long)f * 80 + m];
+  part[g][m] = sum;
+  __syncthreads();
+  if (g == 0) {
+    double t = 0.0;
+    for (int i = 0; i < G; ++i) t += part[i][m];
+    mean_s[m] = (float)(t / (e - a));
+  }
+  __syncthreads();
+  const float mean = mean_s[m];
+  for (f = a + g; f < e; f += G) x[(long)f * 80 + m] -= mean;
 }
 
 void launch_campp_cmvn(float* x, const int* fr_off, int nseq, hipStream_t st) {
   if (nseq <= 0) return;
-  hipLaunchKernelGGL(campp_cmvn_kernel, dim3(nseq), dim3(128), 0, st, x, fr_off);
+  hipLaunchKernelGGL(campp_cmvn_kernel, dim3(nseq), dim3(960), 0, st, x, fr_off);
 }
 
 }  // namespace zasr

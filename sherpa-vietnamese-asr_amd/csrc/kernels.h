@@ -36,7 +36,9 @@ struct CamppConv2d {
   int n, ci, fi, fo, T, sf;
   int relu, tdnn_out;
   int in_tf;           // x is the [n][T][fi] feature batch (ci = 1)
+  const float* wk = nullptr;  // ci = 32: weights permuted by campp_conv2d_permute_weights
 };
+void campp_conv2d_permute_weights(const float* w, int ks, float* out);
 void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st);
 void launch_campp_bnrelu(const float* x, int ldx, long R, int C, const float* s, const float* b,
                          float* y, hipStream_t st);
