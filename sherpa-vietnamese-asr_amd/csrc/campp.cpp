@@ -241,7 +241,8 @@ CamppEngine::~CamppEngine() {
 }
 
 void CamppEngine::gemm(const Lin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
-                       const float* aux, int ldaux) {
+                       const float* aux, int ldaux, int aload, const float* a_scale,
+                       const float* a_shift, const GemmIm2col1d* i2c) {
   GemmParams p{};
   p.A = A;
   p.lda = lda;
@@ -258,7 +259,10 @@ void CamppEngine::gemm(const Lin& l, const float* A, int lda, int M, float* C, i
   p.K = l.K;
   p.alpha = 1.f;
   p.max_M = M;
-  gemm_f32(p, epi, ALOAD_DENSE, false, st_);
+  p.a_scale = a_scale;
+  p.a_shift = a_shift;
+  if (i2c) p.i2c = *i2c;
+  gemm_f32(p, epi, aload, false, st_);
 }
 
 void CamppEngine::fbank_host(const float* wav, long n, std::vector<float>& out) {
@@ -336,30 +340,30 @@ void CamppEngine::embed_device(const float* d_feats, int N, int T, float* d_out,
   // ---- TDNN (k 5, stride 2, pad 2) ----
   const int T2 = (T - 1) / 2 + 1;
   const int R = N * T2;
-  float* col = ws<float>("col", (size_t)R * std::max(5 * head_out, 3 * cfg_.bn_size * cfg_.growth));
-  launch_campp_im2col1d(h, head_out, N, T, T2, head_out, 5, 2, 1, 2, col, st_);
+  // the im2col of both 1-D convolutions and the BN-ReLU in front of the dense layers' 1 x 1
+  // and transit projections happen in the GEMM's A loader (ALOAD_IM2COL1D / ALOAD_BNRELU)
   float* X = ws<float>("blk0", (size_t)R * blocks_[0].cmax);
-  gemm(tdnn_, col, 5 * head_out, R, X, blocks_[0].cmax, EPI_RELU);
+  const GemmIm2col1d tdnn_i2c{T, T2, head_out, 2, 1, 2};
+  gemm(tdnn_, h, head_out, R, X, blocks_[0].cmax, EPI_RELU, nullptr, 0, ALOAD_IM2COL1D, nullptr,
+       nullptr, &tdnn_i2c);
   // ---- dense blocks ----
   const int bnc = cfg_.bn_size * cfg_.growth;
-  float* H1 = ws<float>("h1", (size_t)R * 1024 * 2);
   float* H2 = ws<float>("h2", (size_t)R * bnc);
   float* mexp = ws<float>("mexp", (size_t)R * cfg_.growth);
   for (size_t bi = 0; bi < blocks_.size(); ++bi) {
     const Block& B = blocks_[bi];
     for (const DenseLayer& L : B.layers) {
-      launch_campp_bnrelu(X, B.cmax, R, L.cin, L.bn1_s, L.bn1_b, H1, st_);
-      gemm(L.l1, H1, L.cin, R, H2, bnc, EPI_RELU);
+      gemm(L.l1, X, B.cmax, R, H2, bnc, EPI_RELU, nullptr, 0, ALOAD_BNRELU, L.bn1_s, L.bn1_b);
       CamppCamMask m{H2, L.m1w, L.m1b, L.m2w, L.m2b, mexp, N, T2, cfg_.seg_len};
       launch_campp_cam_mask(m, st_);
       const int pad = (B.k - 1) / 2 * B.dil;
-      launch_campp_im2col1d(H2, bnc, N, T2, T2, bnc, B.k, 1, B.dil, pad, col, st_);
-      gemm(L.local, col, B.k * bnc, R, X + L.cin, B.cmax, EPI_MULAUX, mexp, cfg_.growth);
+      const GemmIm2col1d i2c{T2, T2, bnc, 1, B.dil, pad};
+      gemm(L.local, H2, bnc, R, X + L.cin, B.cmax, EPI_MULAUX, mexp, cfg_.growth, ALOAD_IM2COL1D,
+           nullptr, nullptr, &i2c);
     }
-    launch_campp_bnrelu(X, B.cmax, R, B.cmax, B.tr_s, B.tr_b, H1, st_);
     const int next_ld = bi + 1 < blocks_.size() ? blocks_[bi + 1].cmax : B.cmax / 2;
     float* Xn = ws<float>("blk" + std::to_string(bi + 1), (size_t)R * next_ld);
-    gemm(B.transit, H1, B.cmax, R, Xn, next_ld, EPI_NONE);
+    gemm(B.transit, X, B.cmax, R, Xn, next_ld, EPI_NONE, nullptr, 0, ALOAD_BNRELU, B.tr_s, B.tr_b);
     X = Xn;
   }
   // ---- BN-ReLU + statistics pooling + dense (affine-free BN folded) ----

@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "gemm.h"
 #include "kernels.h"
 
 namespace zasr {
@@ -65,7 +66,9 @@ class CamppEngine {
   template <class T>
   T* ws(const std::string& name, size_t count);
   void gemm(const Lin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
-            const float* aux = nullptr, int ldaux = 0);
+            const float* aux = nullptr, int ldaux = 0, int aload = 0,
+            const float* a_scale = nullptr, const float* a_shift = nullptr,
+            const GemmIm2col1d* i2c = nullptr);
 
   CamppConfig cfg_;
   int device_ = 0;

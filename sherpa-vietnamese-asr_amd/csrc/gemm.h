@@ -30,6 +30,13 @@ enum GemmALoad : int {
   ALOAD_JOINER = 1,  // retired (the joiner has its own split-K kernels)
   ALOAD_CONV2 = 2,   // im2col of conv1 output [T1][80][8]   -> conv.4 (3x3, stride 2)
   ALOAD_CONV3 = 3,   // im2col of conv2 output [L2][39][32]  -> conv.7 (3x3, stride (1,2))
+  ALOAD_BNRELU = 4,  // max(A[m * lda + k] * a_scale[k] + a_shift[k], 0)  (gemm_f32 only)
+  ALOAD_IM2COL1D = 5,  // 1-D conv im2col over sequences, see GemmIm2col1d  (gemm_f32 only)
+};
+// ALOAD_IM2COL1D: row m = n * Tout + t, column k = q * C + c reads
+// A[(n * Tin + t * stride + q * dil - pad) * lda + c], 0 outside [0, Tin).  C % 4 == 0.
+struct GemmIm2col1d {
+  int Tin = 0, Tout = 0, C = 0, stride = 1, dil = 1, pad = 0;
 };
 
 // Per z-slice descriptor (device array).  Offsets are in elements.
@@ -73,6 +80,9 @@ struct GemmParams {
   const float* byp_orig = nullptr;
   const float* byp_scale = nullptr;
   JoinerALoad joiner;
+  const float* a_scale = nullptr;  // ALOAD_BNRELU
+  const float* a_shift = nullptr;
+  GemmIm2col1d i2c;                // ALOAD_IM2COL1D
 };
 
 // Launch; picks a tile shape from (max_M, N).  B_ncontig selects the [K][N] B layout.

@@ -38,17 +38,31 @@ __device__ __forceinline__ float4 load_a4(const GemmParams& p, const float* A, i
     const int kk = k >> 3, c = k & 7;
     const int kt = kk / 3, kf = kk - kt * 3;
     v = *reinterpret_cast<const float4*>(A + ((long)(2 * t + kt) * 80 + 2 * f + kf) * 8 + c);
-  } else {  // ALOAD_CONV3
+  } else if constexpr (ALOAD == ALOAD_CONV3) {
     // out (t, f) of conv.7; k = (kt*3 + kf)*32 + c over conv2 output [L2][39][32]
     const int t = m / 19, f = m - t * 19;
     const int kk = k >> 5, c = k & 31;
     const int kt = kk / 3, kf = kk - kt * 3;
     v = *reinterpret_cast<const float4*>(A + ((long)(t + kt) * 39 + 2 * f + kf) * 32 + c);
+  } else if constexpr (ALOAD == ALOAD_BNRELU) {
+    v = *reinterpret_cast<const float4*>(A + (long)m * lda + k);
+    const float4 s = *reinterpret_cast<const float4*>(p.a_scale + k);
+    const float4 b = *reinterpret_cast<const float4*>(p.a_shift + k);
+    v = make_float4(fmaxf(fmaf(v.x, s.x, b.x), 0.f), fmaxf(fmaf(v.y, s.y, b.y), 0.f),
+                    fmaxf(fmaf(v.z, s.z, b.z), 0.f), fmaxf(fmaf(v.w, s.w, b.w), 0.f));
+  } else {  // ALOAD_IM2COL1D
+    const GemmIm2col1d& g = p.i2c;
+    const int n = m / g.Tout, t = m - n * g.Tout;
+    const int q = k / g.C, c = k - q * g.C;
+    const int ts = t * g.stride + q * g.dil - g.pad;
+    const bool in = ts >= 0 && ts < g.Tin;
+    v = *reinterpret_cast<const float4*>(A + ((long)n * g.Tin + (in ? ts : 0)) * lda + c);
+    return (ok && in) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, bool BNC, int EPI>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, bool BNC, int EPI, bool DEEP>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmParams p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int LDA_S = BM + 4;
@@ -91,10 +105,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
   const int wm = wid / WAVES_N;
   const int wn = wid - wm * WAVES_N;
 
-  float4 ra[A_LD];
-  float4 rb[B_LD];
-
-  auto gload = [&](int kt) {
+  auto gload_to = [&](float4 (&ra)[A_LD], float4 (&rb)[B_LD], int kt) {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       int idx = tid + NT * i;
@@ -124,7 +135,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
       rb[i] = v;
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore_from = [&](const float4 (&ra)[A_LD], const float4 (&rb)[B_LD], int buf) {
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       int idx = tid + NT * i;
@@ -165,12 +176,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nkt = (K + BK - 1) / BK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) gload(kt + 1);
+  auto mma_slab = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const int kr = kk + (lane >> 5);
@@ -185,8 +191,43 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nkt) sstore(cur ^ 1);
+  };
+  if constexpr (DEEP) {
+    // K a multiple of 2 BK (host-checked): two register sets, so each K slab's loads have two
+    // slabs of MFMAs to land; LDS-only barriers (__syncthreads would drain the slab in flight
+    // with vmcnt(0)); slab indices clamped so every load is unconditional
+    float4 xa[2][A_LD], xb[2][B_LD];
+    auto bar = []() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    gload_to(xa[0], xb[0], 0);
+    gload_to(xa[1], xb[1], 1);
+    sstore_from(xa[0], xb[0], 0);
+    bar();
+    for (int kt = 0; kt < nkt; kt += 2) {
+      gload_to(xa[0], xb[0], min(kt + 2, nkt - 1));
+      mma_slab(0);
+      sstore_from(xa[1], xb[1], 1);
+      bar();
+      gload_to(xa[1], xb[1], min(kt + 3, nkt - 1));
+      mma_slab(1);
+      sstore_from(xa[0], xb[0], 0);
+      bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail loads
+  } else {
+    float4 ra[A_LD], rb[B_LD];
+    gload_to(ra, rb, 0);
+    sstore_from(ra, rb, 0);
     __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nkt) gload_to(ra, rb, kt + 1);
+      mma_slab(cur);
+      if (kt + 1 < nkt) sstore_from(ra, rb, cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // epilogue: lane holds column (lane & 31), rows (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -215,10 +256,19 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
   }
 }
 
+int g_gemm_f32_deep = -1;  // ZASR_GEMM_DEEP (shared with the bf16 kernel's switch)
+
 template <int BM, int BN, int WM, int WN, int ALOAD, bool BNC, int EPI>
 void launch_t(const GemmParams& p, hipStream_t st) {
   dim3 grid(cdiv(p.N, BN), cdiv(p.max_M, BM), p.slices ? p.num_slices : 1);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI>), grid,
+  if (g_gemm_f32_deep < 0)
+    g_gemm_f32_deep = getenv("ZASR_GEMM_DEEP") ? atoi(getenv("ZASR_GEMM_DEEP")) : 1;
+  if (g_gemm_f32_deep && !p.slices && p.K % (2 * BK) == 0) {
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, true>), grid,
+                       dim3(64 * WM * WN), 0, st, p);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, false>), grid,
                      dim3(64 * WM * WN), 0, st, p);
 }
 
@@ -635,7 +685,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
 
 // ZASR_GEMM_DEEP=0 turns the two-slab register prefetch off (gemm_set_deep for the labs)
 static int g_gemm_deep = -1;
-void gemm_set_deep(int on) { g_gemm_deep = on; }
+void gemm_set_deep(int on) { g_gemm_deep = g_gemm_f32_deep = on; }
 
 template <int BM, int BN, int BK, int WM, int WN, int ALOAD, int EPI, typename TA, typename TC>
 void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
@@ -967,6 +1017,16 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
     return launch_tile<ALOAD_CONV2, false, EPI_SWOOSHR>(p, st);
   } else if (aload == ALOAD_CONV3 && !b_ncontig && epi == EPI_SWOOSHR) {
     return launch_tile<ALOAD_CONV3, false, EPI_SWOOSHR>(p, st);
+  } else if (aload == ALOAD_BNRELU && !b_ncontig && !p.slices) {
+    ZASR_REQUIRE(p.a_scale && p.a_shift, "gemm_f32: ALOAD_BNRELU needs a_scale / a_shift");
+    if (epi == EPI_NONE) return launch_tile<ALOAD_BNRELU, false, EPI_NONE>(p, st);
+    if (epi == EPI_RELU) return launch_tile<ALOAD_BNRELU, false, EPI_RELU>(p, st);
+  } else if (aload == ALOAD_IM2COL1D && !b_ncontig && !p.slices) {
+    ZASR_REQUIRE(p.i2c.C > 0 && p.i2c.C % 4 == 0 && p.i2c.Tout > 0 && p.K % p.i2c.C == 0 &&
+                     (long)p.M % p.i2c.Tout == 0,
+                 "gemm_f32: bad ALOAD_IM2COL1D geometry");
+    if (epi == EPI_RELU) return launch_tile<ALOAD_IM2COL1D, false, EPI_RELU>(p, st);
+    if (epi == EPI_MULAUX) return launch_tile<ALOAD_IM2COL1D, false, EPI_MULAUX>(p, st);
   }
   throw std::runtime_error("gemm_f32: unsupported (aload, epi, layout) combination");
 }
