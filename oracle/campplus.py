@@ -87,11 +87,13 @@ def campp_fbank(audio: np.ndarray) -> np.ndarray:
 
 
 class CamppOracle:
-    """Eval-mode CAMPPlus forward from a state dict (zasr/campp.py names), torch fp32."""
+    """Eval-mode CAMPPlus forward from a state dict (zasr/campp.py names), torch fp32 (the
+    reference's precision) or, with dtype=np.float64, in double as an exact yardstick."""
 
-    def __init__(self, cfg, weights: Dict[str, np.ndarray]):
+    def __init__(self, cfg, weights: Dict[str, np.ndarray], dtype=np.float32):
         self.cfg = cfg
-        self.w = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in weights.items()}
+        self.dtype = dtype
+        self.w = {k: torch.from_numpy(np.asarray(v, dtype)) for k, v in weights.items()}
 
     def _bn(self, x, name, affine=True):
         w = self.w
@@ -125,7 +127,7 @@ class CamppOracle:
     def embed(self, feats: np.ndarray) -> np.ndarray:
         cfg, w = self.cfg, self.w
         with torch.no_grad():
-            x = torch.from_numpy(np.asarray(feats, np.float32)).permute(0, 2, 1).unsqueeze(1)
+            x = torch.from_numpy(np.asarray(feats, self.dtype)).permute(0, 2, 1).unsqueeze(1)
             x = F.relu(self._bn(F.conv2d(x, w["head.conv1.weight"], padding=1), "head.bn1"))
             for li, nb in enumerate(cfg.head_blocks):
                 for b in range(nb):

@@ -359,43 +359,93 @@ void launch_campp_im2col1d(const float* x, int ldx, int N, int Tin, int Tout, in
 // (one per thread), the per-segment mask expanded to every frame of the segment:
 // mexp[n * T + t][o] for t in segment g.  avg_pool1d(ceil_mode) divides a clipped last
 // segment by its true length.
-__global__ __launch_bounds__(128) void campp_cam_mask_kernel(CamppCamMask a) {
+__global__ __launch_bounds__(256) void campp_cam_mask_kernel(CamppCamMask a) {
+  __shared__ double sPart[2][2][128];
   __shared__ float sCtx[128];
   __shared__ float sZ[64];
   __shared__ float sM[32];
   const int tid = threadIdx.x, n = blockIdx.y, g = blockIdx.x;
   const int T = a.T, L = a.seg_len;
   const int s0 = g * L, s1 = min(T, s0 + L);
-  const float* x = a.h + (long)n * T * 128 + tid;
-  double tot = 0.0, seg = 0.0;
-  for (int t = 0; t < T; ++t) {
-    const float v = x[(long)t * 128];
-    tot += v;
-    if (t >= s0 && t < s1) seg += v;
+  // frame sums: channel c = tid % 128, frames of parity h = tid / 128, 8 loads in flight
+  {
+    const int c = tid & 127, h = tid >> 7;
+    const float* x = a.h + (long)n * T * 128 + c;
+    double tot = 0.0, seg = 0.0;
+    int t = h;
+    for (; t + 14 < T; t += 16) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x[(long)(t + 2 * u) * 128];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int tu = t + 2 * u;
+        tot += v[u];
+        if (tu >= s0 && tu < s1) seg += v[u];
+      }
+    }
+    for (; t < T; t += 2) {
+      const float v = x[(long)t * 128];
+      tot += v;
+      if (t >= s0 && t < s1) seg += v;
+    }
+    sPart[h][0][c] = tot;
+    sPart[h][1][c] = seg;
   }
-  sCtx[tid] = (float)(tot / T) + (float)(seg / (s1 - s0));
   __syncthreads();
-  if (tid < 64) {
-    float z = a.b1[tid];
-    for (int c = 0; c < 128; ++c) z = fmaf(a.w1[tid * 128 + c], sCtx[c], z);
-    sZ[tid] = fmaxf(z, 0.f);
+  if (tid < 128)
+    sCtx[tid] = (float)((sPart[0][0][tid] + sPart[1][0][tid]) / T) +
+                (float)((sPart[0][1][tid] + sPart[1][1][tid]) / (s1 - s0));
+  __syncthreads();
+  // linear1 + ReLU: 4 lanes per output, 32 channels each
+  {
+    const int j = tid >> 2, q = tid & 3;
+    const float4* w = reinterpret_cast<const float4*>(a.w1 + j * 128 + q * 32);
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 v = w[i];
+      const float* cx = sCtx + q * 32 + 4 * i;
+      z = fmaf(v.x, cx[0], z);
+      z = fmaf(v.y, cx[1], z);
+      z = fmaf(v.z, cx[2], z);
+      z = fmaf(v.w, cx[3], z);
+    }
+    z += __shfl_xor(z, 1);
+    z += __shfl_xor(z, 2);
+    if (q == 0) sZ[j] = fmaxf(z + a.b1[j], 0.f);
   }
   __syncthreads();
-  if (tid < 32) {
-    float m = a.b2[tid];
-    for (int c = 0; c < 64; ++c) m = fmaf(a.w2[tid * 64 + c], sZ[c], m);
-    sM[tid] = 1.f / (1.f + expf(-m));
+  // linear2 + sigmoid: 8 lanes per output, 8 inputs each
+  {
+    const int o = tid >> 3, q = tid & 7;
+    const float4* w = reinterpret_cast<const float4*>(a.w2 + o * 64 + q * 8);
+    const float4 v0 = w[0], v1 = w[1];
+    const float* zz = sZ + q * 8;
+    float m = v0.x * zz[0];
+    m = fmaf(v0.y, zz[1], m);
+    m = fmaf(v0.z, zz[2], m);
+    m = fmaf(v0.w, zz[3], m);
+    m = fmaf(v1.x, zz[4], m);
+    m = fmaf(v1.y, zz[5], m);
+    m = fmaf(v1.z, zz[6], m);
+    m = fmaf(v1.w, zz[7], m);
+    m += __shfl_xor(m, 1);
+    m += __shfl_xor(m, 2);
+    m += __shfl_xor(m, 4);
+    if (q == 0) sM[o] = 1.f / (1.f + expf(-(m + a.b2[o])));
   }
   __syncthreads();
-  for (int i = tid; i < (s1 - s0) * 32; i += 128) {
-    const int t = s0 + i / 32, o = i % 32;
-    a.mexp[((long)n * T + t) * 32 + o] = sM[o];
+  for (int i = tid; i < (s1 - s0) * 8; i += 256) {
+    const int t = s0 + i / 8, o4 = i % 8;
+    *reinterpret_cast<float4*>(a.mexp + ((long)n * T + t) * 32 + 4 * o4) =
+        *reinterpret_cast<const float4*>(sM + 4 * o4);
   }
 }
 
 void launch_campp_cam_mask(const CamppCamMask& a, hipStream_t st) {
   const int nseg = cdiv(a.T, a.seg_len);
-  hipLaunchKernelGGL(campp_cam_mask_kernel, dim3(nseg, a.n), dim3(128), 0, st, a);
+  hipLaunchKernelGGL(campp_cam_mask_kernel, dim3(nseg, a.n), dim3(256), 0, st, a);
 }
 
 // statistics pooling over T frames of relu(bn(x)) (the out_nonlinear BN-ReLU folded in):
