@@ -130,7 +130,7 @@ __device__ inline void cx_store_prow(float* sX, int g, int ci, int lane, const f
 }
 }  // namespace
 
-template <int KS, int SF>
+template <int KS, int SF, bool RES>
 __global__ __launch_bounds__(256, 1) void campp_conv2d_mfma_kernel(CamppConv2d a, int rb) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   constexpr int CI = 32, PAD = KS / 2, ROWS = SF + KS, NEW = 2 * SF, TW = cx_tw(ROWS);
@@ -188,7 +188,31 @@ __global__ __launch_bounds__(256, 1) void campp_conv2d_mfma_kernel(CamppConv2d a
   const int orow = w >> 1, tile0 = 5 * (w & 1);
   const int r16 = lane & 15, g4 = lane >> 4;
   const int wsw = 16 * (g4 & 1);  // k parity of this lane
+  // epilogue constants of this lane's channels 16 m + 4 g4 + e
+  float esc[2][4], esh[2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      esc[m][e] = a.scale[16 * m + 4 * g4 + e];
+      esh[m][e] = a.shift[16 * m + 4 * g4 + e];
+    }
   for (int fo = fo_begin; fo < fo_end; fo += 2) {
+    const int fw = fo + orow;
+    // the residual this step's outputs add, loaded with the rows (clamped, unconditional)
+    float rv[RES ? 2 : 1][RES ? NT : 1][4];
+    if constexpr (RES) {
+      const int fr = min(fw, a.fo - 1);
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int t = min(16 * (tile0 + u) + r16, T - 1);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            rv[m][u][e] = a.res[(((long)n * 32 + 16 * m + 4 * g4 + e) * a.fo + fr) * T + t];
+      }
+    }
     // prefetch the rows the next step adds (rows past fi load as 0)
     const int gn = fo * SF - PAD + ROWS;
     float pv[NEW * 8][3];
@@ -204,7 +228,6 @@ __global__ __launch_bounds__(256, 1) void campp_conv2d_mfma_kernel(CamppConv2d a
       for (int u = 0; u < NT; ++u) acc[m][u] = f32x4{0.f, 0.f, 0.f, 0.f};
     // K loop flattened to NS = KS KS CI / 4 steps, operands double-buffered in registers so
     // step s + 1's LDS reads are in flight under step s's 10 MFMAs
-    const int fw = fo + orow;
     const float* xrow[KS];
 #pragma unroll
     for (int r = 0; r < KS; ++r)
@@ -249,9 +272,9 @@ __global__ __launch_bounds__(256, 1) void campp_conv2d_mfma_kernel(CamppConv2d a
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int co = 16 * m + 4 * g4 + e;
-            float y = fmaf(acc[m][u][e], a.scale[co], a.shift[co]);
+            float y = fmaf(acc[m][u][e], esc[m][e], esh[m][e]);
             const long o = (((long)n * 32 + co) * a.fo + fw) * T + t;
-            if (a.res) y += a.res[o];
+            if constexpr (RES) y += rv[m][u][e];
             if (a.relu) y = fmaxf(y, 0.f);
             if (a.tdnn_out)
               a.y[((long)n * T + t) * (32 * a.fo) + co * a.fo + fw] = y;
@@ -260,7 +283,9 @@ __global__ __launch_bounds__(256, 1) void campp_conv2d_mfma_kernel(CamppConv2d a
           }
       }
     }
-    __syncthreads();
+    // the ring slots written above must be complete before the next step reads them; the
+    // output stores need not (an LDS-only barrier leaves them in flight)
+    cx_lds_barrier();
   }
 }
 
@@ -288,10 +313,12 @@ void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st) {
     const int chunks = std::max(1, std::min(pairs, cdiv(2048, a.n)));
     const int rb = 2 * cdiv(pairs, chunks);
     const dim3 grid(cdiv(a.fo, rb), a.n);
-#define ZASR_CX(KSV, SFV) \
-  hipLaunchKernelGGL((campp_conv2d_mfma_kernel<KSV, SFV>), grid, dim3(256), 0, st, a, rb)
-    if (a.sf == 1) ZASR_CX(3, 1);
-    else ZASR_CX(3, 2);
+#define ZASR_CX(KSV, SFV, RESV) \
+  hipLaunchKernelGGL((campp_conv2d_mfma_kernel<KSV, SFV, RESV>), grid, dim3(256), 0, st, a, rb)
+    if (a.sf == 1 && a.res) ZASR_CX(3, 1, true);
+    else if (a.sf == 1) ZASR_CX(3, 1, false);
+    else if (a.res) ZASR_CX(3, 2, true);
+    else ZASR_CX(3, 2, false);
 #undef ZASR_CX
     return;
   }
