@@ -76,10 +76,12 @@ def parse_args(argv=None):
                     help="no GPU: exercise the launcher / rank / timing / JSON path with gloo "
                          "and a CPU stand-in step (tests/test_bench_launcher.py)")
     ap.add_argument("--profile-out", default="")
-    ap.add_argument("--stage", default="asr", choices=["asr", "campp", "vad"],
+    ap.add_argument("--stage", default="asr", choices=["asr", "campp", "vad", "pipe"],
                     help="asr: the Zipformer decode (default, BASELINE metric); campp: the CAM++ "
                          "speaker-embedding stage of config 5 (1.5 s windows, 0.6 s step); vad: "
-                         "Silero VAD probabilities + segments of the hour (core/asr_engine.py:2090)")
+                         "Silero VAD probabilities + segments of the hour (core/asr_engine.py:2090); "
+                         "pipe: BASELINE config 5, decode + merge + CAM++ embeddings + ViBERT "
+                         "punctuation of the hour (zasr/pipeline.py)")
     ap.add_argument("--vad-files", type=int, default=1,
                     help="VAD stage: the hour split into this many files decoded in one call "
                          "(1 = the reference's single-file case; the recurrence is one "
@@ -545,6 +547,147 @@ def bench_vad(args):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------ full pipe (config 5)
+def bench_pipe(args):
+    """BASELINE config 5 per GPU: one step = one hour through decode (68M, --method,
+    --precision) -> word post-processing -> chunk-overlap merge -> ViBERT-capu punctuation of
+    the transcript (56-word chunks / 16 overlap, 3 iterations, mini-batches of 32), with the
+    CAM++ front end + embeddings of the hour's speech regions (1.5 s windows every 0.6 s) on a
+    second stream under the decode, their L2-normalised copy on the host at the end.  The
+    audio is resident in HBM; the chunk / region plans are made once (zasr/plan.py)."""
+    import torch
+    from zasr.binding import CamppEmbedder, Recognizer, VibertSession
+    from zasr.campp import CamppConfig, campp_flops
+    from zasr.campp import save_model_dir as campp_save
+    from zasr.campp import synth_weights as campp_weights
+    from zasr.model import PRESETS, chunk_flops, save_model_dir, synth_tokens, synth_weights
+    from zasr.pipeline import FullPipe, punctuate, split_word_chunks, vibert_feeds
+    from zasr.synth_audio import synth_speech
+    from zasr.vibert import save_model_dir as vib_save
+    from zasr.vibert import synth_weights as vib_weights
+    from zasr.vibert import vibert_base, vibert_flops
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    tmp = tempfile.gettempdir()
+    cfg = PRESETS[args.model]()
+    beam = 1 if args.method == "greedy_search" else args.beam
+    hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
+    hotwords = load_hotwords(hw_path, cfg.vocab_size) if (hw_path and beam > 1) else None
+    mdir = os.path.join(tmp, f"zasr_pipe_asr_{os.getpid()}")
+    toks = synth_tokens(cfg.vocab_size)
+    save_model_dir(mdir, cfg, synth_weights(cfg, WEIGHT_SEED), toks)
+    rec = Recognizer(mdir, args.method, beam, hotwords=hotwords[0] if hotwords else None,
+                     hotword_scores=hotwords[1] if hotwords else None, device_id=local,
+                     precision=args.precision)
+    recd = {"id2token": dict(enumerate(toks)), "vocab_size": cfg.vocab_size}
+    ccfg = CamppConfig()
+    cdir = os.path.join(tmp, f"zasr_pipe_campp_{os.getpid()}")
+    campp_save(cdir, ccfg, campp_weights(ccfg, 20261017))
+    emb = CamppEmbedder(cdir, device_id=local)
+    vcfg = vibert_base()
+    vdir = os.path.join(tmp, f"zasr_pipe_vibert_{os.getpid()}")
+    vib_save(vdir, vcfg, vib_weights(vcfg, 20261018))
+    vib = VibertSession(vdir, device_id=local)
+
+    audio = synth_speech(args.audio_sec, AUDIO_SEED + rank)
+    pipe = FullPipe(rec, recd, emb, vib, vcfg.vocab_size, beam=beam, campp_batch=args.campp_batch)
+    pipe.prepare(audio)
+    out = {}
+
+    def step():
+        r = pipe.run()
+        out.update(windows=len(r["windows"]), words=len(r["words"]), chunks=len(r["labels"]),
+                   vibert_runs=r["vibert_runs"], tokens=r["tokens"])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=f"cuda:{local}")
+    t_step = el / args.steps
+    # stage times alone (one pass each, serialised): where the step goes
+    stage_ms = {}
+    main_st = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    words, _ = pipe.decode_words(main_st)
+    stage_ms["decode_words_merge"] = 1000 * (time.perf_counter() - t1)
+    t1 = time.perf_counter()
+    pipe.embed_windows(main_st)
+    torch.cuda.synchronize()
+    stage_ms["campp"] = 1000 * (time.perf_counter() - t1)
+    t1 = time.perf_counter()
+    punctuate(vib, [w["text"] for w in words], vcfg.vocab_size)
+    stage_ms["vibert"] = 1000 * (time.perf_counter() - t1)
+    c_len, plan, regions = pipe.c_len, pipe.c_off, pipe.r_off
+    # algorithmic flops of the step: decode + CAM++ windows + ViBERT passes
+    f_dec = sum(sum(chunk_flops(cfg, n, beam).values()) for n in c_len)
+    f_cam = out["windows"] * campp_flops(ccfg, 150)
+    vch = [c for c in split_word_chunks([w["text"] for w in words]) if len(c) >= 3]
+    f_vib = 0.0
+    if vch:
+        fd = vibert_feeds(vch, vcfg.vocab_size)
+        Lp, Wp = fd["input_ids"].shape[1], fd["input_offsets"].shape[1]
+        f_vib = 3 * vibert_flops(vcfg, len(vch), Lp, Wp)
+    fl = f_dec + f_cam + f_vib
+    p_dec = MFMA_BF16_PEAK_TFLOPS if args.precision != "fp32" else MFMA_F32_PEAK_TFLOPS
+    t_roof = f_dec / (p_dec * 1e12) + (f_cam + f_vib) / (MFMA_F32_PEAK_TFLOPS * 1e12)
+    if rank == 0:
+        line = {"metric": "audio-sec/sec full pipe (decode + CAM++ embeddings + ViBERT punctuation)",
+                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(1000 * t_step, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": f"{args.precision} decode, f32 CAM++ / ViBERT",
+                "data": "synthetic (seeded speech-like audio, random-init Zipformer / CAM++ / "
+                        "ViBERT weights)",
+                "config": {"workload": f"BASELINE config 5 per GPU: {args.model} {args.method}"
+                                       f"{'' if beam == 1 else ' beam %d' % beam} decode of 1 h "
+                                       f"+ merge + CAM++ windows + ViBERT-capu punctuation",
+                           "decode_chunks": len(plan), "campp_regions": len(regions),
+                           "campp_windows": out["windows"], "campp_launch_batch": args.campp_batch,
+                           "words": out["words"], "tokens": out["tokens"],
+                           "vibert_chunks": out["chunks"], "vibert_runs_per_step": out["vibert_runs"],
+                           "vibert_iterations": "3 passes over every chunk (the reference's "
+                                                "upper bound: it re-runs only changed chunks)",
+                           "stage_ms_alone": {k: round(v, 2) for k, v in stage_ms.items()}},
+                "roofline": {"kernel": "whole pipe (algorithmic flops / step time)",
+                             "bound": "mfma", "unit": "TFLOP/s",
+                             "achieved": round(fl / t_step / 1e12, 2),
+                             "peak": round(fl / t_roof / 1e12, 2),
+                             "frac": round(t_roof / t_step, 4),
+                             "flops_per_step": {"decode": f_dec, "campp": f_cam, "vibert": f_vib},
+                             "note": "peak = the mixed roof: decode flops at the bf16 MFMA peak "
+                                     "(f32 in fp32 mode) + CAM++ / ViBERT flops at the f32 MFMA "
+                                     "peak (exact f32, their reference tolerances); per-stage "
+                                     "roofs in the asr / campp stage lines"},
+                "cpu_baseline": None}
+        print(json.dumps(line))
+        if args.profile_out:
+            with open(args.profile_out, "w") as f:
+                json.dump(line, f, indent=1)
+    rec.close()
+    emb.close()
+    vib.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse_args()
@@ -554,6 +697,8 @@ def main():
         return bench_campp(args)
     if args.stage == "vad":
         return bench_vad(args)
+    if args.stage == "pipe":
+        return bench_pipe(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -152,6 +152,19 @@ int zasr_campp_embed(zasr_campp* h, const float* feats, int32_t count, int32_t n
 /* same with device buffers on `stream` (NULL: the handle's stream); used by bench.py */
 int zasr_campp_embed_device(zasr_campp* h, const float* d_feats, int32_t count,
                             int32_t n_frames, float* d_out, void* stream);
+/* the front end of a whole file in HBM: fbank + per-region CMVN of every speech region
+   [region_off[i], + region_len[i]) of d_wav, then the windows of window_frames frames every
+   step_frames (tail pulled back; a region shorter than a window gives one window of all its
+   frames, zero-padded; < 10 frames: none) gathered into d_feats [n][window_frames][80] on
+   `stream`.  Replaces _sliding_window_embeddings' fbank-once-slice-later loop and batch
+   tensor (core/speaker_diarization_senko_campp_optimized.py:540-600).  *n_windows = n;
+   window_region / window_first / window_nframes (host, capacity max_windows) describe each
+   window (its start time is region start + first * 10 ms, :567-577). */
+int zasr_campp_windows_device(zasr_campp* h, const float* d_wav, const int64_t* region_off,
+                              const int64_t* region_len, int32_t n_regions, int32_t window_frames,
+                              int32_t step_frames, float* d_feats, int64_t max_windows,
+                              int32_t* window_region, int32_t* window_first,
+                              int32_t* window_nframes, int64_t* n_windows, void* stream);
 
 /* ---- ViBERT-capu punctuation / capitalization ----
    Replaces the reference's onnxruntime session of vibert-capu.onnx (core/gec_model.py:

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 
 #include "common.h"
@@ -285,6 +286,67 @@ void CamppEngine::fbank_host(const float* wav, long n, std::vector<float>& out) 
   launch_campp_cmvn(df, dmeta + 1, 1, st_);
   ZASR_HIP_CHECK(hipMemcpyAsync(out.data(), df, out.size() * 4, hipMemcpyDeviceToHost, st_));
   ZASR_HIP_CHECK(hipStreamSynchronize(st_));
+}
+
+long CamppEngine::windows_device(const float* d_wav, const long* reg_off, const long* reg_len,
+                                 int nreg, int wf, int sf, float* d_feats, long max_windows,
+                                 int* win_region, int* win_first, int* win_frames,
+                                 hipStream_t st) {
+  ZASR_HIP_CHECK(hipSetDevice(device_));
+  st_ = st ? st : stream_;
+  ZASR_REQUIRE(wf >= 1 && sf >= 1, "CAM++ windows: window and step must be >= 1 frame");
+  // regions that yield windows (>= 10 fbank frames, :547-556), their packed fbank rows and
+  // the window plan (:558-582)
+  std::vector<long> woff;
+  std::vector<int> ns, fr_off{0}, wrow, wn;
+  long nwin = 0;
+  for (int r = 0; r < nreg; ++r) {
+    const long n = reg_len[r];
+    ZASR_REQUIRE(n >= 0 && n <= INT32_MAX, "CAM++ windows: region length out of range");
+    const long frames = n >= 400 ? 1 + (n - 400) / 160 : 0;
+    if (frames < 10) continue;
+    const int base = fr_off.back();
+    auto add = [&](long first, long cnt) {
+      ZASR_REQUIRE(nwin < max_windows, "CAM++ windows: more windows than max_windows");
+      win_region[nwin] = r;
+      win_first[nwin] = (int)first;
+      win_frames[nwin] = (int)cnt;
+      wrow.push_back(base + (int)first);
+      wn.push_back((int)cnt);
+      ++nwin;
+    };
+    if (frames < wf) {
+      add(0, frames);
+    } else {
+      long pos = 0;
+      for (; pos + wf < frames; pos += sf) add(pos, wf);  // strict < (:565)
+      add(std::max<long>(0, frames - wf), wf);            // tail pulled back (:572-577)
+    }
+    woff.push_back(reg_off[r]);
+    ns.push_back((int)n);
+    ZASR_REQUIRE((long)base + frames <= INT32_MAX, "CAM++ windows: too many fbank frames");
+    fr_off.push_back(base + (int)frames);
+  }
+  const int nv = (int)ns.size();
+  if (nwin == 0) return 0;
+  const int total = fr_off.back();
+  long* d_woff = ws<long>("wd_woff", nv);
+  int* d_ns = ws<int>("wd_ns", nv);
+  int* d_fo = ws<int>("wd_fo", nv + 1);
+  int* d_wrow = ws<int>("wd_wrow", nwin);
+  int* d_wn = ws<int>("wd_wn", nwin);
+  float* rows = ws<float>("wd_rows", (size_t)total * 80);
+  // pageable sources: HIP stages each copy before returning
+  ZASR_HIP_CHECK(hipMemcpyAsync(d_woff, woff.data(), nv * sizeof(long), hipMemcpyHostToDevice, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(d_ns, ns.data(), nv * sizeof(int), hipMemcpyHostToDevice, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(d_fo, fr_off.data(), (nv + 1) * sizeof(int), hipMemcpyHostToDevice, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(d_wrow, wrow.data(), nwin * sizeof(int), hipMemcpyHostToDevice, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(d_wn, wn.data(), nwin * sizeof(int), hipMemcpyHostToDevice, st_));
+  FbankTables t{d_twiddle_, d_window_, d_mel_meta_, d_mel_meta_ + 80, d_mel_meta_ + 160, d_mel_w_};
+  launch_fbank(d_wav, d_woff, d_ns, d_fo, nv, total, t, rows, st_, true);
+  launch_campp_cmvn(rows, d_fo, nv, st_);
+  launch_campp_gather(rows, d_wrow, d_wn, (int)nwin, wf, d_feats, st_);
+  return nwin;
 }
 
 void CamppEngine::embed_device(const float* d_feats, int N, int T, float* d_out, hipStream_t st) {

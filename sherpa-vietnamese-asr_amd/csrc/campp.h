@@ -36,6 +36,16 @@ class CamppEngine {
   // embeddings of a (zero-padded) feature batch [N][T][80] -> [N][emb]
   void embed_host(const float* feats, int N, int T, float* out);
   void embed_device(const float* d_feats, int N, int T, float* d_out, hipStream_t st);
+  // the front end of a whole file on the device (core/speaker_diarization_senko_campp_
+  // optimized.py:540-600): fbank + per-region CMVN of every speech region [reg_off, +reg_len)
+  // of d_wav in one launch, then the windows of `wf` frames every `sf` frames (tail pulled
+  // back; a region shorter than a window is one window of all its frames, zero-padded to wf
+  // like the reference's batch tensor; < 10 frames: none) gathered into d_feats [n][wf][80].
+  // Returns n; win_* (host, capacity max_windows) get each window's region, first frame and
+  // frame count.
+  long windows_device(const float* d_wav, const long* reg_off, const long* reg_len, int nreg,
+                      int wf, int sf, float* d_feats, long max_windows, int* win_region,
+                      int* win_first, int* win_frames, hipStream_t st);
 
   std::mutex mu;
 

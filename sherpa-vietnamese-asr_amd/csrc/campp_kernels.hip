@@ -542,4 +542,28 @@ void launch_campp_cmvn(float* x, const int* fr_off, int nseq, hipStream_t st) {
   hipLaunchKernelGGL(campp_cmvn_kernel, dim3(nseq), dim3(960), 0, st, x, fr_off);
 }
 
+// one block per window: 20 float4 per frame, consecutive threads on consecutive float4 of
+// the window (coalesced reads of the packed rows and writes of the window tensor)
+__global__ __launch_bounds__(256) void campp_gather_kernel(const float4* __restrict__ rows,
+                                                           const int* __restrict__ win_row,
+                                                           const int* __restrict__ win_n, int wf,
+                                                           float4* __restrict__ out) {
+  const int w = blockIdx.x;
+  const long r0 = win_row[w];
+  const int n = win_n[w];
+  float4* o = out + (long)w * wf * 20;
+  for (int i = threadIdx.x; i < wf * 20; i += 256) {
+    const int t = i / 20;
+    o[i] = t < n ? rows[r0 * 20 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+void launch_campp_gather(const float* rows, const int* win_row, const int* win_n, int nwin,
+                         int wf, float* out, hipStream_t st) {
+  if (nwin <= 0) return;
+  hipLaunchKernelGGL(campp_gather_kernel, dim3(nwin), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(rows), win_row, win_n, wf,
+                     reinterpret_cast<float4*>(out));
+}
+
 }  // namespace zasr

@@ -57,6 +57,9 @@ void launch_campp_cam_mask(const CamppCamMask& a, hipStream_t st);
 void launch_campp_stats(const float* x, int N, int T, int C, const float* s, const float* b,
                         float* out, hipStream_t st);
 void launch_campp_cmvn(float* x, const int* fr_off, int nseq, hipStream_t st);
+// window w = rows [win_row[w], + win_n[w]) of the packed fbank rows, zero-padded to wf frames
+void launch_campp_gather(const float* rows, const int* win_row, const int* win_n, int nwin,
+                         int wf, float* out, hipStream_t st);
 
 // ---- ViBERT-capu encoder pieces (vibert_kernels.hip) ----
 struct VibertEmbedArgs {

@@ -255,6 +255,27 @@ int zasr_campp_embed_device(zasr_campp* h, const float* d_feats, int32_t count, 
   });
 }
 
+int zasr_campp_windows_device(zasr_campp* h, const float* d_wav, const int64_t* region_off,
+                              const int64_t* region_len, int32_t n_regions, int32_t window_frames,
+                              int32_t step_frames, float* d_feats, int64_t max_windows,
+                              int32_t* window_region, int32_t* window_first,
+                              int32_t* window_nframes, int64_t* n_windows, void* stream) {
+  if (!h || !n_windows || n_regions < 0 || (n_regions > 0 && (!d_wav || !region_off || !region_len)) ||
+      max_windows < 0 || (max_windows > 0 && (!d_feats || !window_region || !window_first || !window_nframes)))
+    return fail(ZASR_ERR_INVALID, "null argument");
+  if (window_frames < 1 || step_frames < 1)
+    return fail(ZASR_ERR_INVALID, "window_frames and step_frames must be >= 1");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    *n_windows = h->eng->windows_device(d_wav, reinterpret_cast<const long*>(region_off),
+                                        reinterpret_cast<const long*>(region_len), n_regions,
+                                        window_frames, step_frames, d_feats, max_windows,
+                                        window_region, window_first, window_nframes,
+                                        reinterpret_cast<hipStream_t>(stream));
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_convert_model(const char* model_dir, const char* out_dir) {
   if (!model_dir || !out_dir) return fail(ZASR_ERR_INVALID, "null model_dir/out_dir");
   return guarded([&]() {

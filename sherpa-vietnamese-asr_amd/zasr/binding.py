@@ -24,7 +24,7 @@ EXPORTS = (
     "zasr_result_token_stats", "zasr_result_free", "zasr_vocab_size", "zasr_joiner_dim",
     "zasr_profile_enable", "zasr_profile_reset", "zasr_profile_report", "zasr_last_error",
     "zasr_version", "zasr_campp_create", "zasr_campp_destroy", "zasr_campp_embedding_dim",
-    "zasr_campp_fbank", "zasr_campp_embed", "zasr_campp_embed_device",
+    "zasr_campp_fbank", "zasr_campp_embed", "zasr_campp_embed_device", "zasr_campp_windows_device",
     "zasr_vibert_create", "zasr_vibert_destroy", "zasr_vibert_num_labels",
     "zasr_vibert_num_detect", "zasr_vibert_run",
     "zasr_vad_create", "zasr_vad_destroy", "zasr_vad_probs", "zasr_vad_probs_device",
@@ -136,6 +136,10 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_campp_embed.restype = C.c_int
     lib.zasr_campp_embed_device.argtypes = [P, P, I32, I32, P, P]
     lib.zasr_campp_embed_device.restype = C.c_int
+    i32p = C.POINTER(I32)
+    lib.zasr_campp_windows_device.argtypes = [P, P, C.POINTER(I64), C.POINTER(I64), I32, I32, I32,
+                                              P, I64, i32p, i32p, i32p, C.POINTER(I64), P]
+    lib.zasr_campp_windows_device.restype = C.c_int
     lib.zasr_vibert_create.argtypes = [C.c_char_p, I32, C.POINTER(P)]
     lib.zasr_vibert_create.restype = C.c_int
     lib.zasr_vibert_destroy.argtypes = [P]
@@ -413,6 +417,33 @@ class CamppEmbedder:
         self._check(self.lib.zasr_campp_embed_device(self.handle, C.c_void_p(d_feats), count,
                                                      n_frames, C.c_void_p(d_out),
                                                      C.c_void_p(stream)))
+
+
+    def windows_device(self, d_wav: int, region_off: Sequence[int], region_len: Sequence[int],
+                       d_feats: int, max_windows: int, window_frames: int = 150,
+                       step_frames: int = 60, stream: int = 0):
+        """fbank + CMVN of every speech region of a waveform in HBM and its 1.5 s windows
+        gathered into d_feats [n][window_frames][80] (zasr_campp_windows_device; the reference's
+        _sliding_window_embeddings front end, core/speaker_diarization_senko_campp_optimized.py:
+        540-600).  Returns (region, first frame, frame count) int32 arrays of the n windows."""
+        off = np.ascontiguousarray(region_off, dtype=np.int64)
+        ln = np.ascontiguousarray(region_len, dtype=np.int64)
+        if off.shape != ln.shape:
+            raise ValueError("region_off and region_len differ in length")
+        cap = max(0, int(max_windows))
+        reg = np.empty(max(cap, 1), np.int32)
+        first = np.empty(max(cap, 1), np.int32)
+        nfr = np.empty(max(cap, 1), np.int32)
+        n = C.c_int64()
+        i64p = C.POINTER(C.c_int64)
+        i32p = C.POINTER(C.c_int32)
+        self._check(self.lib.zasr_campp_windows_device(
+            self.handle, C.c_void_p(d_wav), off.ctypes.data_as(i64p), ln.ctypes.data_as(i64p),
+            off.size, window_frames, step_frames, C.c_void_p(d_feats), cap,
+            reg.ctypes.data_as(i32p), first.ctypes.data_as(i32p), nfr.ctypes.data_as(i32p),
+            C.byref(n), C.c_void_p(stream)))
+        k = n.value
+        return reg[:k], first[:k], nfr[:k]
 
 
 class VibertSession:

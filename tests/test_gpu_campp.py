@@ -79,3 +79,51 @@ def test_campp_fbank_matches_reference(emb, i):
     assert got.shape == ref.shape
     if ref.size:
         np.testing.assert_allclose(got, ref, rtol=0, atol=2e-3)
+
+
+def test_campp_windows_device_equals_per_region_fbank(emb):
+    """zasr_campp_windows_device (fbank + CMVN of every region of a file in HBM, windows
+    gathered on the device) == the per-region fbank + window_plan slicing of the reference's
+    _sliding_window_embeddings (core/speaker_diarization_senko_campp_optimized.py:540-600),
+    bit for bit: same kernels, same per-region reduction order.  Regions cover the window
+    plan's cases: long (strided + pulled-back tail), shorter than a window (one zero-padded
+    window), < 10 frames and < 400 samples (none)."""
+    import torch
+    from zasr.campp import window_plan
+    from zasr.synth_audio import synth_speech
+    cfg, w, e = emb
+    audio = synth_speech(40.0, 77)
+    regions = [(0, 16000 * 7 + 123), (16000 * 8, 16000 * 9), (16000 * 10, 16000 * 10 + 1700),
+               (16000 * 11, 16000 * 11 + 300), (16000 * 12, 16000 * 31 + 77)]
+    exp_feats, exp_meta = [], []
+    for r, (a, b) in enumerate(regions):
+        fb = e.fbank(audio[a:b])
+        for s, n in window_plan(fb.shape[0]):
+            x = np.zeros((150, 80), np.float32)
+            x[:n] = fb[s:s + n]
+            exp_feats.append(x)
+            exp_meta.append((r, s, n))
+    d_wav = torch.from_numpy(audio).cuda()
+    cap = len(exp_feats) + 4
+    d_feats = torch.full((cap, 150, 80), 7.0, dtype=torch.float32, device="cuda")
+    reg, first, nfr = e.windows_device(d_wav.data_ptr(), [a for a, _ in regions],
+                                       [b - a for a, b in regions], d_feats.data_ptr(), cap)
+    torch.cuda.synchronize()
+    assert list(zip(reg.tolist(), first.tolist(), nfr.tolist())) == exp_meta
+    got = d_feats[:len(exp_feats)].cpu().numpy()
+    assert np.array_equal(got, np.stack(exp_feats))
+    # embeddings of the gathered windows == embeddings of the host-sliced batch
+    d_out = torch.empty((len(exp_feats), cfg.embedding_size), dtype=torch.float32, device="cuda")
+    e.embed_device(d_feats.data_ptr(), len(exp_feats), 150, d_out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), e.embed(np.stack(exp_feats)))
+
+
+def test_campp_windows_device_rejects_overflow(emb):
+    import torch
+    from zasr.binding import ZasrError
+    cfg, w, e = emb
+    d_wav = torch.zeros(16000 * 20, dtype=torch.float32, device="cuda")
+    d_feats = torch.empty((2, 150, 80), dtype=torch.float32, device="cuda")
+    with pytest.raises(ZasrError):
+        e.windows_device(d_wav.data_ptr(), [0], [16000 * 20], d_feats.data_ptr(), 2)

@@ -1,0 +1,93 @@
+"""The config-5 pipe (zasr.pipeline.FullPipe) on the MI355X: decode + merge + CAM++ windows
++ ViBERT punctuation of one file, each output checked against the same stage run on its own
+through the already-pinned paths (host-sliced CAM++ windows, batch decode of the host chunks,
+the ViBERT session on the reference's preprocess feeds)."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pipe(tmp_path_factory):
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from zasr.binding import CamppEmbedder, Recognizer, VibertSession
+    from zasr.campp import CamppConfig
+    from zasr.campp import save_model_dir as campp_save
+    from zasr.campp import synth_weights as campp_weights
+    from zasr.model import save_model_dir, synth_tokens, synth_weights, zipformer_tiny
+    from zasr.pipeline import FullPipe
+    from zasr.synth_audio import synth_speech
+    from zasr.vibert import save_model_dir as vib_save
+    from zasr.vibert import synth_weights as vib_weights
+    from zasr.vibert import vibert_tiny
+    d = tmp_path_factory.mktemp("pipe")
+    cfg = zipformer_tiny(64)
+    toks = synth_tokens(cfg.vocab_size)
+    save_model_dir(str(d / "asr"), cfg, synth_weights(cfg, 5), toks)
+    rec = Recognizer(str(d / "asr"), "greedy_search", 1, precision="fp32")
+    ccfg = CamppConfig()
+    campp_save(str(d / "campp"), ccfg, campp_weights(ccfg, 3))
+    emb = CamppEmbedder(str(d / "campp"))
+    vcfg = vibert_tiny()
+    vib_save(str(d / "vib"), vcfg, vib_weights(vcfg, 4))
+    vib = VibertSession(str(d / "vib"))
+    recd = {"id2token": dict(enumerate(toks)), "vocab_size": cfg.vocab_size}
+    p = FullPipe(rec, recd, emb, vib, vcfg.vocab_size, beam=1, campp_batch=16)
+    audio = synth_speech(75.0, 31)
+    p.prepare(audio)
+    out = p.run()
+    yield p, audio, out, vcfg
+    rec.close()
+    emb.close()
+    vib.close()
+
+
+def test_pipe_words_equal_host_decode_and_merge(pipe):
+    from zasr.asr_engine import result_words
+    from zasr.merge import merge_chunks_with_overlap
+    p, audio, out, _ = pipe
+    assert len(p.c_off) >= 3  # 75 s: three planner chunks with 3 s overlaps
+    chunks = [audio[a:a + n] for a, n in zip(p.c_off, p.c_len)]
+    res = p.rec.decode(chunks, beam=1)
+    per = [{"words": result_words(p.recd, r, n, a / 16000.0), "audio_start_abs": a / 16000.0,
+            "audio_end_abs": (a + n) / 16000.0} for r, a, n in zip(res, p.c_off, p.c_len)]
+    words, _ = merge_chunks_with_overlap(per)
+    assert [w["text"] for w in out["words"]] == [w["text"] for w in words]
+    assert [w["start"] for w in out["words"]] == [w["start"] for w in words]
+    assert out["tokens"] == sum(int(r.token_ids.size) for r in res) > 0
+
+
+def test_pipe_embeddings_equal_host_windows(pipe):
+    from zasr.campp import window_plan
+    from zasr.pipeline import l2_normalise
+    p, audio, out, _ = pipe
+    feats, meta = [], []
+    for r, (a, n) in enumerate(zip(p.r_off, p.r_len)):
+        fb = p.emb.fbank(audio[a:a + n])
+        for s, k in window_plan(fb.shape[0]):
+            x = np.zeros((150, 80), np.float32)
+            x[:k] = fb[s:s + k]
+            feats.append(x)
+            meta.append((r, s, k))
+    assert out["windows"].tolist() == [list(m) for m in meta]
+    ref = l2_normalise(p.emb.embed(np.stack(feats)))
+    assert out["embeddings"].shape == ref.shape
+    assert np.array_equal(out["embeddings"], ref)
+    assert np.allclose(np.linalg.norm(out["embeddings"], axis=1), 1.0, atol=1e-5)
+
+
+def test_pipe_punctuation_labels(pipe):
+    from zasr.pipeline import split_word_chunks, vibert_feeds
+    p, audio, out, vcfg = pipe
+    texts = [w["text"] for w in out["words"]]
+    chunks = [c for c in split_word_chunks(texts) if len(c) >= 3]
+    assert len(chunks) == len(out["labels"]) >= 1
+    assert out["vibert_runs"] == 3 * ((len(chunks) + 31) // 32)
+    lg, dl = p.vib.run(None, vibert_feeds(chunks, vcfg.vocab_size))
+    assert lg.shape[2] == vcfg.num_labels and dl.shape[2] == vcfg.num_detect_classes
+    for i, c in enumerate(chunks):
+        assert out["labels"][i].tolist() == lg[i, 1:1 + len(c)].argmax(-1).tolist()
