@@ -279,25 +279,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
   if (const char* e = getenv("ZASR_SEARCH_CUS")) search_cus_ = atoi(e);
   int ncu = 0;
   ZASR_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_));
-  // ZASR_ENC_EXCL_CUS = N > 0: the encoder streams leave N evenly spaced CUs free and the
-  // search streams run unmasked (high priority), so a search launch always finds free CUs
-  int excl = 0;
-  if (const char* e = getenv("ZASR_ENC_EXCL_CUS")) excl = atoi(e);
-  if (excl > 0 && excl < ncu && search_cus_ <= 0) {
-    std::vector<uint32_t> me((ncu + 31) / 32, 0u);
-    std::vector<char> drop(ncu, 0);
-    for (int i = 0; i < excl; ++i) drop[(int)((long)i * ncu / excl)] = 1;
-    for (int c = 0; c < ncu; ++c)
-      if (!drop[c]) me[c / 32] |= 1u << (c % 32);
-    ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)me.size(), me.data()));
-    for (auto& x : enc_extra_)
-      ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&x, (uint32_t)me.size(), me.data()));
-    int least = 0, greatest = 0;
-    ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
-    ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream3_, hipStreamNonBlocking, greatest));
-    search_cus_ = -excl;  // encoder stream 0 is the engine's masked stream
-  } else if (search_cus_ > 0 && search_cus_ < ncu) {
+  if (search_cus_ > 0 && search_cus_ < ncu) {
     std::vector<uint32_t> ms((ncu + 31) / 32, 0u), me((ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; ++c) (c < search_cus_ ? ms : me)[c / 32] |= 1u << (c % 32);
     ZASR_HIP_CHECK(hipExtStreamCreateWithCUMask(&stream2_, (uint32_t)ms.size(), ms.data()));
@@ -1688,7 +1670,7 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
   const int L = E;
   // encoder stream 0 is the caller's stream, or (CU-partitioned) the engine's masked stream
-  hipStream_t enc_st[kMaxEnc] = {search_cus_ != 0 ? stream_ : main_st};
+  hipStream_t enc_st[kMaxEnc] = {search_cus_ > 0 ? stream_ : main_st};
   for (int e = 1; e < kMaxEnc; ++e) enc_st[e] = enc_extra_[e - 1];
   if (E > 1 || enc_st[0] != main_st) {  // the encoder streams start after the caller's prior work
     ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 2], main_st));

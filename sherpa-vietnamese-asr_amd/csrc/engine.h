@@ -209,7 +209,7 @@ class Engine {
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
   hipStream_t stream3_ = nullptr;  // the second group of a beam search (high priority)
-  int search_cus_ = 0;             // > 0: search / encoder streams on disjoint CU sets; < 0: encoder streams leave -search_cus_ CUs free
+  int search_cus_ = 0;             // > 0: search / encoder streams on disjoint CU sets
   hipStream_t enc_extra_[kMaxEnc - 1] = {};  // encoder streams 1.. of the batch pipeline
   // [0, kMaxEnc]: encoder output slots; kMaxEnc + 1: search done; kMaxEnc + 2: start
   hipEvent_t part_ev_[kMaxEnc + 4] = {};

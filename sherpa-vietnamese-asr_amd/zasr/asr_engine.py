@@ -261,6 +261,31 @@ def _compute_token_entropy(raw_logits, V):
 _ENTROPY_FALLBACK = {"tsallis_norm": 0, "margin": 1, "entropy_norm": 0, "top1_prob": 1.0}
 
 
+def _np_mean(xs):
+    """np.mean of a list of Python floats, bit for bit: numpy's float64 pairwise sum
+    (sequential below 8 elements; eight interleaved partial sums combined as
+    ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail, up to its 128-element block; larger
+    lists go to numpy) divided by the count -- without the array round trip per word."""
+    n = len(xs)
+    if n < 8:
+        s = 0.0
+        for x in xs:
+            s += x
+        return s / n
+    if n > 128:
+        return float(np.mean(xs))
+    r = list(xs[:8])
+    i = 8
+    while i + 8 <= n:
+        for k in range(8):
+            r[k] += xs[i + k]
+        i += 8
+    s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+    for x in xs[i:]:
+        s += x
+    return s / n
+
+
 def _finalize_word_entropy(w):
     """BPE-level -> word-level aggregation (reference :1187-1206)."""
     probs = w.pop("probs")
@@ -269,7 +294,7 @@ def _finalize_word_entropy(w):
     if ents:
         w["tsallis_max"] = round(float(max(e["tsallis_norm"] for e in ents)), 4)
         w["margin_min"] = round(float(min(e["margin"] for e in ents)), 4)
-        w["entropy_norm"] = round(float(np.mean([e["entropy_norm"] for e in ents])), 4)
+        w["entropy_norm"] = round(_np_mean([e["entropy_norm"] for e in ents]), 4)
         confs = [e["margin"] * (1.0 - e["tsallis_norm"]) for e in ents]
         w["_conf"] = round(float(sum(confs) / len(confs)), 4)
     else:

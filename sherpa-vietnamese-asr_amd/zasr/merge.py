@@ -15,6 +15,7 @@ from __future__ import annotations
 import re
 import unicodedata
 from difflib import SequenceMatcher
+from functools import lru_cache
 from typing import Dict, List, Sequence, Tuple
 
 OVERLAP_SEC = 3.0           # core/asr_engine.py:33
@@ -30,16 +31,19 @@ def overlap_key(text: str) -> str:
     return _NON_WORD.sub("", unicodedata.normalize("NFC", text.lower().strip()))
 
 
+@lru_cache(maxsize=1 << 16)
 def fuzzy_equal(a: str, b: str, threshold: float = FUZZY_MATCH_THRESHOLD) -> bool:
     """:52-67: identical, one containing the other (both longer than 2), or a difflib ratio
-    of at least `threshold`."""
+    of at least `threshold` (quick_ratio bounds ratio from above: below the threshold it
+    decides without the matching-block search)."""
     if a == b:
         return True
     if not a or not b:
         return False
     if len(a) > 2 and len(b) > 2 and (a in b or b in a):
         return True
-    return SequenceMatcher(None, a, b).ratio() >= threshold
+    sm = SequenceMatcher(None, a, b)
+    return sm.quick_ratio() >= threshold and sm.ratio() >= threshold
 
 
 def _mean_prob(ws: Sequence[Dict]) -> float:

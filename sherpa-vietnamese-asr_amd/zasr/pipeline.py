@@ -19,6 +19,7 @@ ids by a stable hash, the START token is the last id as after special_tokens_fix
 from __future__ import annotations
 
 import hashlib
+from functools import lru_cache
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -45,16 +46,20 @@ def split_word_chunks(words: Sequence[str], chunk_size: int = CHUNK_WORDS,
     return [list(words[i:i + chunk_size]) for i in range(0, n - overlap_size, stride)]
 
 
-def word_pieces(word: str, vocab_size: int) -> List[int]:
-    """Synthetic word-piece ids of one word (stable hash; ids 5 .. vocab_size - 2, ~1 in 8
-    words split in two)."""
+@lru_cache(maxsize=1 << 18)
+def _pieces(word: str, vocab_size: int) -> Tuple[int, ...]:
     h = hashlib.blake2b(word.encode("utf-8"), digest_size=8).digest()
     v = int.from_bytes(h, "little")
     span = vocab_size - 2 - 5
-    ids = [5 + v % span]
     if (v >> 40) % 8 == 0:
-        ids.append(5 + (v >> 20) % span)
-    return ids
+        return (5 + v % span, 5 + (v >> 20) % span)
+    return (5 + v % span,)
+
+
+def word_pieces(word: str, vocab_size: int) -> List[int]:
+    """Synthetic word-piece ids of one word (stable hash; ids 5 .. vocab_size - 2, ~1 in 8
+    words split in two; memoised per word like a tokenizer's vocabulary lookup)."""
+    return list(_pieces(word, vocab_size))
 
 
 def vibert_feeds(batch: Sequence[Sequence[str]], vocab_size: int, max_len: int = MAX_LEN
@@ -70,7 +75,7 @@ def vibert_feeds(batch: Sequence[Sequence[str]], vocab_size: int, max_len: int =
         ids, off = [start_id], [0]
         for w in list(seq)[:L]:
             off.append(len(ids))
-            ids += word_pieces(w, vocab_size)
+            ids += _pieces(w, vocab_size)
         rows.append(ids)
         offs.append(off)
     T = max(len(r) for r in rows)
@@ -94,7 +99,9 @@ def punctuate(session, words: Sequence[str], vocab_size: int, iterations: int = 
               mini_batch: int = MINI_BATCH) -> Tuple[List[np.ndarray], int]:
     """ViBERT passes over the transcript's word chunks: `iterations` passes of every chunk of
     at least 3 words (core/gec_model.py:623-654; the reference re-runs only chunks whose text
-    changed, so this is its upper bound), mini-batches of 32.  Returns the per-chunk label
+    changed, so this is its upper bound), mini-batches of `mini_batch` rows (32 in the
+    reference; <= 0: the whole pass in one run -- rows are independent and the padding is the
+    whole pass's either way, so the logits are the same bits).  Returns the per-chunk label
     argmax of the last pass (softmax is monotone: argmax of the logits, :579-581) and the
     number of session runs."""
     chunks = [c for c in split_word_chunks(list(words)) if len(c) >= 3]
@@ -105,8 +112,9 @@ def punctuate(session, words: Sequence[str], vocab_size: int, iterations: int = 
     for _ in range(iterations):
         # the whole batch is preprocessed (padded) at once, then sliced (:636-640, :380-392)
         feeds = vibert_feeds(chunks, vocab_size)
-        for b in range(0, len(chunks), mini_batch):
-            lg, _ = session.run(None, {k: v[b:b + mini_batch] for k, v in feeds.items()})
+        mb = mini_batch if mini_batch > 0 else len(chunks)
+        for b in range(0, len(chunks), mb):
+            lg, _ = session.run(None, {k: v[b:b + mb] for k, v in feeds.items()})
             runs += 1
             am = lg.argmax(-1)
             for i in range(am.shape[0]):
@@ -131,9 +139,10 @@ class FullPipe:
     size incl. START."""
 
     def __init__(self, rec, recd, emb, vib, vib_vocab: int, beam: int = 1,
-                 campp_batch: int = 512, iterations: int = ITERATIONS):
+                 campp_batch: int = 512, iterations: int = ITERATIONS, vib_batch: int = 0):
         self.rec, self.recd, self.emb, self.vib = rec, recd, emb, vib
         self.vib_vocab, self.beam, self.B, self.iterations = vib_vocab, beam, campp_batch, iterations
+        self.vib_batch = vib_batch  # <= 0: one ViBERT run per pass (punctuate)
 
     def prepare(self, audio: np.ndarray) -> None:
         import torch
@@ -153,16 +162,21 @@ class FullPipe:
         self.d_emb = torch.empty((self.cap, self.emb.dim), dtype=torch.float32, device="cuda")
         self.s_campp = torch.cuda.Stream()
 
-    def decode_words(self, stream: int) -> Tuple[List[Dict], int]:
+    def decode(self, stream: int):
+        return self.rec.decode_device(self.d_audio.data_ptr(), self.c_off, self.c_len,
+                                      beam=self.beam, stream=stream)
+
+    def words(self, res) -> Tuple[List[Dict], int]:
         from zasr.asr_engine import result_words
         from zasr.merge import merge_chunks_with_overlap
-        res = self.rec.decode_device(self.d_audio.data_ptr(), self.c_off, self.c_len,
-                                     beam=self.beam, stream=stream)
         chunks = [{"words": result_words(self.recd, r, n, s / 16000.0),
                    "audio_start_abs": s / 16000.0, "audio_end_abs": (s + n) / 16000.0}
                   for r, s, n in zip(res, self.c_off, self.c_len)]
         words, _ = merge_chunks_with_overlap(chunks)
         return words, sum(int(r.token_ids.size) for r in res)
+
+    def decode_words(self, stream: int) -> Tuple[List[Dict], int]:
+        return self.words(self.decode(stream))
 
     def embed_windows(self, stream: int):
         reg, first, nfr = self.emb.windows_device(self.d_audio.data_ptr(), self.r_off, self.r_len,
@@ -174,15 +188,32 @@ class FullPipe:
         return reg, first, nfr
 
     def run(self) -> Dict:
+        return self.run_many(1)[0]
+
+    def run_many(self, k: int) -> List[Dict]:
+        """k passes of the file through the pipe (k files of a job, here the same audio),
+        pipelined: the decode of pass i + 1 (a ctypes call on a worker thread: the GIL is
+        released while the GPU decodes) runs while this thread post-processes pass i's words,
+        merges them and runs its punctuation; CAM++ runs on its own stream beside both."""
         import torch
+        from concurrent.futures import ThreadPoolExecutor
         main = torch.cuda.current_stream()
-        self.s_campp.wait_stream(main)
-        # CAM++ on its own stream: it reads only the audio, so it runs under the decode
-        reg, first, nfr = self.embed_windows(self.s_campp.cuda_stream)
-        words, tokens = self.decode_words(main.cuda_stream)
-        labels, runs = punctuate(self.vib, [w["text"] for w in words], self.vib_vocab,
-                                 self.iterations)
-        self.s_campp.synchronize()
-        embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
-        return {"words": words, "tokens": tokens, "labels": labels, "vibert_runs": runs,
-                "embeddings": embs, "windows": np.stack([reg, first, nfr], 1)}
+        outs: List[Dict] = []
+        with ThreadPoolExecutor(1) as ex:
+            fut = ex.submit(self.decode, main.cuda_stream)
+            for i in range(k):
+                self.s_campp.wait_stream(main)
+                # CAM++ on its own stream: it reads only the audio
+                reg, first, nfr = self.embed_windows(self.s_campp.cuda_stream)
+                res = fut.result()
+                if i + 1 < k:
+                    fut = ex.submit(self.decode, main.cuda_stream)
+                words, tokens = self.words(res)
+                labels, runs = punctuate(self.vib, [w["text"] for w in words], self.vib_vocab,
+                                         self.iterations, self.vib_batch)
+                self.s_campp.synchronize()
+                embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
+                outs.append({"words": words, "tokens": tokens, "labels": labels,
+                             "vibert_runs": runs, "embeddings": embs,
+                             "windows": np.stack([reg, first, nfr], 1)})
+        return outs

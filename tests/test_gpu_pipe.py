@@ -27,7 +27,7 @@ def pipe(tmp_path_factory):
     d = tmp_path_factory.mktemp("pipe")
     cfg = zipformer_tiny(64)
     toks = synth_tokens(cfg.vocab_size)
-    save_model_dir(str(d / "asr"), cfg, synth_weights(cfg, 5), toks)
+    save_model_dir(str(d / "asr"), cfg, synth_weights(cfg, 5, blank_bias=-1.5), toks)
     rec = Recognizer(str(d / "asr"), "greedy_search", 1, precision="fp32")
     ccfg = CamppConfig()
     campp_save(str(d / "campp"), ccfg, campp_weights(ccfg, 3))
@@ -86,8 +86,35 @@ def test_pipe_punctuation_labels(pipe):
     texts = [w["text"] for w in out["words"]]
     chunks = [c for c in split_word_chunks(texts) if len(c) >= 3]
     assert len(chunks) == len(out["labels"]) >= 1
-    assert out["vibert_runs"] == 3 * ((len(chunks) + 31) // 32)
-    lg, dl = p.vib.run(None, vibert_feeds(chunks, vcfg.vocab_size))
+    assert out["vibert_runs"] == 3  # one run per pass (vib_batch 0)
+    feeds = vibert_feeds(chunks, vcfg.vocab_size)
+    lg, dl = p.vib.run(None, feeds)
     assert lg.shape[2] == vcfg.num_labels and dl.shape[2] == vcfg.num_detect_classes
     for i, c in enumerate(chunks):
         assert out["labels"][i].tolist() == lg[i, 1:1 + len(c)].argmax(-1).tolist()
+
+
+def test_vibert_whole_pass_equals_reference_mini_batches(pipe):
+    """One run over a whole padded pass == the reference's 32-row mini-batches of the same
+    feeds (core/gec_model.py:380-392), bit for bit."""
+    from zasr.pipeline import split_word_chunks, vibert_feeds
+    p, audio, out, vcfg = pipe
+    rng = np.random.default_rng(9)
+    words = [f"t{int(x)}" for x in rng.integers(0, 500, 3000)]
+    chunks = split_word_chunks(words)
+    assert len(chunks) > 64
+    feeds = vibert_feeds(chunks, vcfg.vocab_size)
+    lg, dl = p.vib.run(None, feeds)
+    parts = [p.vib.run(None, {k: v[b:b + 32] for k, v in feeds.items()})
+             for b in range(0, len(chunks), 32)]
+    assert np.array_equal(np.concatenate([x[0] for x in parts]), lg)
+    assert np.array_equal(np.concatenate([x[1] for x in parts]), dl)
+
+
+def test_pipelined_passes_equal_single_pass(pipe):
+    p, audio, out, _ = pipe
+    outs = p.run_many(3)
+    for o in outs:
+        assert [w["text"] for w in o["words"]] == [w["text"] for w in out["words"]]
+        assert np.array_equal(o["embeddings"], out["embeddings"])
+        assert all(np.array_equal(a, b) for a, b in zip(o["labels"], out["labels"]))
