@@ -86,8 +86,9 @@ def parse_args(argv=None):
                     help="VAD stage: the hour split into this many files decoded in one call "
                          "(1 = the reference's single-file case; the recurrence is one "
                          "workgroup per file)")
-    ap.add_argument("--campp-batch", type=int, default=512,
-                    help="CAM++ windows per launch group (the reference batches 32 on CPU)")
+    ap.add_argument("--campp-batch", type=int, default=4096,
+                    help="CAM++ windows per launch group (the reference batches 32 on CPU; "
+                         "measured 512 -> 6000: 167 -> 123 ms per hour, profiles/r02/campp_batch)")
     return ap.parse_args(argv)
 
 

@@ -80,56 +80,81 @@ void launch_vibert_layernorm(float* x, long rows, int H, const float* g, const f
   hipLaunchKernelGGL(vibert_ln_kernel, dim3((unsigned)rows), dim3(256), 0, st, x, H, g, b, eps);
 }
 
-// self-attention of one (sequence, head): K and V of the head in LDS, one query per thread at
-// a time; scores / sqrt(d) + the additive padding mask (finfo(f32).min for masked keys, as
-// transformers' extended attention mask), softmax (max-subtracted, two passes), context.
+// self-attention of one (sequence, head): K (row stride D + 1: conflict-free per-lane rows)
+// and V of the head in LDS, sized to L; each of the 4 waves takes queries qi = wave, wave + 4,
+// ...: lanes own keys j = lane + 64 c for the scores (q broadcast from LDS; the same fmaf
+// chain over d as a per-query loop), a wave max, p_j = exp(s_j * scale + mask_j - max) to a
+// per-wave LDS row, then lane d accumulates the context over j in ascending order together
+// with the sum of p (sequential, as a per-query loop would).  Scores / sqrt(d) + the additive
+// padding mask (finfo(f32).min for masked keys, as transformers' extended attention mask).
 // qkv: [B * L][3 H] (q | k | v), ctx: [B * L][H].  L <= 256, head dim D in {16, 32, 64}.
 template <int D>
 __global__ __launch_bounds__(256) void vibert_attn_kernel(VibertAttnArgs a) {
-  __shared__ float sK[256 * D];
-  __shared__ float sV[256 * D];
-  __shared__ float sM[256];
-  const int b = blockIdx.y, h = blockIdx.x, L = a.L, H = a.H;
+  constexpr int KS = D + 1;
+  extern __shared__ float smem[];
+  const int L = a.L, H = a.H;
+  float* sK = smem;             // [L][D + 1]
+  float* sV = sK + L * KS;      // [L][D]
+  float* sM = sV + L * D;       // [L]
+  float* sP = sM + L;           // [4][L]
+  float* sQ = sP + 4 * L;       // [4][D]
+  const int b = blockIdx.y, h = blockIdx.x;
   const long base = (long)b * L;
   for (int i = threadIdx.x; i < L * D; i += 256) {
-    const int j = i / D, d = i % D;
+    const int j = i / D, d = i - j * D;
     const float* row = a.qkv + (base + j) * 3 * H;
-    sK[i] = row[H + h * D + d];
+    sK[j * KS + d] = row[H + h * D + d];
     sV[i] = row[2 * H + h * D + d];
   }
   for (int j = threadIdx.x; j < L; j += 256)
     sM[j] = a.mask[base + j] ? 0.f : -3.4028234663852886e38f;
   __syncthreads();
   const float scale = a.scale;
-  for (int qi = threadIdx.x; qi < L; qi += 256) {
-    float q[D];
-    const float* qr = a.qkv + (base + qi) * 3 * H + h * D;
-#pragma unroll
-    for (int d = 0; d < D; ++d) q[d] = qr[d];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* q = sQ + wid * D;
+  float* pw = sP + wid * L;
+  for (int qi = wid; qi < L; qi += 4) {
+    if (lane < D) q[lane] = a.qkv[(base + qi) * 3 * H + h * D + lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // q visible to the whole wave
+    __builtin_amdgcn_wave_barrier();
+    float sc[4];
     float mx = -INFINITY;
-    for (int j = 0; j < L; ++j) {
-      float s = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) s = fmaf(q[d], sK[j * D + d], s);
-      mx = fmaxf(mx, s * scale + sM[j]);
+    for (int c = 0; c < 4; ++c) {
+      const int j = lane + 64 * c;
+      sc[c] = -INFINITY;
+      if (j < L) {
+        float s = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) s = fmaf(q[d], sK[j * KS + d], s);
+        sc[c] = s * scale + sM[j];
+        mx = fmaxf(mx, sc[c]);
+      }
     }
-    float sum = 0.f, o[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) o[d] = 0.f;
-    for (int j = 0; j < L; ++j) {
-      float s = 0.f;
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
 #pragma unroll
-      for (int d = 0; d < D; ++d) s = fmaf(q[d], sK[j * D + d], s);
-      const float p = __expf(s * scale + sM[j] - mx);
-      sum += p;
-#pragma unroll
-      for (int d = 0; d < D; ++d) o[d] = fmaf(p, sV[j * D + d], o[d]);
+    for (int c = 0; c < 4; ++c) {
+      const int j = lane + 64 * c;
+      if (j < L) pw[j] = __expf(sc[c] - mx);
     }
-    const float inv = 1.f / sum;
-    float* out = a.ctx + (base + qi) * H + h * D;
-#pragma unroll
-    for (int d = 0; d < D; ++d) out[d] = o[d] * inv;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < D) {
+      float sum = 0.f, o = 0.f;
+      for (int j = 0; j < L; ++j) {
+        const float p = pw[j];
+        sum += p;
+        o = fmaf(p, sV[j * D + lane], o);
+      }
+      a.ctx[(base + qi) * H + h * D + lane] = o * (1.f / sum);
+    }
+    __builtin_amdgcn_wave_barrier();  // the next query rewrites q and pw
   }
+}
+
+static size_t vibert_attn_lds(int L, int D) {
+  return sizeof(float) * ((size_t)L * (2 * D + 1) + L + 4 * (size_t)L + 4 * (size_t)D);
 }
 
 void launch_vibert_attention(const VibertAttnArgs& a, int B, int heads, hipStream_t st) {
@@ -137,12 +162,24 @@ void launch_vibert_attention(const VibertAttnArgs& a, int B, int heads, hipStrea
   ZASR_REQUIRE(a.L <= 256 && a.H == heads * D && (D == 16 || D == 32 || D == 64),
                "ViBERT attention: L <= 256, head dim 16, 32 or 64");
   if (B <= 0) return;
+  const size_t lds = vibert_attn_lds(a.L, D);
+  static bool attr = false;
+  if (!attr) {  // up to 138 KB of LDS at L = 256, D = 64
+    const int mx = (int)vibert_attn_lds(256, 64);
+    ZASR_HIP_CHECK(hipFuncSetAttribute((const void*)vibert_attn_kernel<64>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    ZASR_HIP_CHECK(hipFuncSetAttribute((const void*)vibert_attn_kernel<32>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    ZASR_HIP_CHECK(hipFuncSetAttribute((const void*)vibert_attn_kernel<16>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    attr = true;
+  }
   if (D == 64)
-    hipLaunchKernelGGL(vibert_attn_kernel<64>, dim3(heads, B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(vibert_attn_kernel<64>, dim3(heads, B), dim3(256), lds, st, a);
   else if (D == 32)
-    hipLaunchKernelGGL(vibert_attn_kernel<32>, dim3(heads, B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(vibert_attn_kernel<32>, dim3(heads, B), dim3(256), lds, st, a);
   else
-    hipLaunchKernelGGL(vibert_attn_kernel<16>, dim3(heads, B), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(vibert_attn_kernel<16>, dim3(heads, B), dim3(256), lds, st, a);
 }
 
 // g[b * W + w] = x[b * L + offsets[b][w]]

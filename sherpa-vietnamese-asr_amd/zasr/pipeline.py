@@ -139,7 +139,7 @@ class FullPipe:
     size incl. START."""
 
     def __init__(self, rec, recd, emb, vib, vib_vocab: int, beam: int = 1,
-                 campp_batch: int = 512, iterations: int = ITERATIONS, vib_batch: int = 0):
+                 campp_batch: int = 4096, iterations: int = ITERATIONS, vib_batch: int = 0):
         self.rec, self.recd, self.emb, self.vib = rec, recd, emb, vib
         self.vib_vocab, self.beam, self.B, self.iterations = vib_vocab, beam, campp_batch, iterations
         self.vib_batch = vib_batch  # <= 0: one ViBERT run per pass (punctuate)
