@@ -47,7 +47,9 @@ void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t s
 // 20 Hz .. Nyquist, floor 1.0 (CMVN follows in campp_cmvn_kernel).
 // =====================================================================================
 constexpr int kFbWaves = 4;
-constexpr int kMelWMax = 512;  // each FFT bin lies in at most two triangles
+constexpr int kMelWMax = 512;   // each FFT bin lies in at most two triangles
+constexpr int kFbSeqLds = 1024; // sequence offsets staged in LDS up to this many sequences
+constexpr int kFbBlocks = 2048; // grid-stride: 8 blocks per CU, each wave ~50 frames per hour
 
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -63,7 +65,13 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
   __shared__ int sMeta[240];
   __shared__ float sMelW[kMelWMax];
   __shared__ double2 sA[kFbWaves][256], sB[kFbWaves][256];
+  __shared__ int sOff[kFbSeqLds + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // sequence frame offsets in LDS when they fit (the per-frame sequence search then costs
+  // LDS round trips, not L2 ones)
+  const bool off_lds = nseq <= kFbSeqLds;
+  if (off_lds)
+    for (int i = tid; i <= nseq; i += 64 * kFbWaves) sOff[i] = fr_off[i];
   for (int i = tid; i < 256; i += 64 * kFbWaves)
     sTw[i] = make_double2(tabs.twiddle[2 * i], tabs.twiddle[2 * i + 1]);
   for (int i = tid; i < 400; i += 64 * kFbWaves) sWin[i] = tabs.window[i];
@@ -76,13 +84,17 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
     const int nw = tabs.mel_woff[79] + tabs.mel_len[79];
     for (int i = tid; i < nw && i < kMelWMax; i += 64 * kFbWaves) sMelW[i] = tabs.mel_w[i];
   }
-  const int frame = blockIdx.x * kFbWaves + w;
-  const bool active = frame < total_frames;
+  __syncthreads();  // tables staged
+  const int* offs = off_lds ? sOff : fr_off;
+  // grid-stride over frames: each wave takes frames w + kFbWaves * blockIdx.x + k * stride, so
+  // the tables are staged once per block, not once per 4 frames
+  const int stride = gridDim.x * kFbWaves;
+  for (int frame = blockIdx.x * kFbWaves + w; frame < total_frames; frame += stride) {
   float xv[7];
   float ctx0 = 0.f;  // CAMPP: the signal sample before the frame (scaled; 0 for frame 0)
-  if (active) {
-    const int b = find_seq(fr_off, nseq, frame);
-    const int f = frame - fr_off[b];
+  {
+    const int b = find_seq(offs, nseq, frame);
+    const int f = frame - offs[b];
     const long n = nsamp[b];
     const float* base = wav + wav_off[b];
     if constexpr (CAMPP) {
@@ -109,8 +121,6 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
 #pragma unroll
     for (int k = 0; k < 7; ++k) xv[k] = xv[k] - mean;
   }
-  __syncthreads();  // tables staged
-  if (!active) return;
   double2* A = sA[w];
   double2* B = sB[w];
   {
@@ -181,6 +191,8 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
     for (int k = 0; k < ln; ++k) acc = fmaf(sMelW[wo + k], pw[st + k], acc);
     out[(long)frame * 80 + m] = logf(fmaxf(acc, CAMPP ? 1.0f : 1.1920928955078125e-07f));
   }
+  __builtin_amdgcn_wave_barrier();  // the next frame rewrites this wave's A / B images
+  }
 }
 
 void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const int* fr_off,
@@ -188,11 +200,13 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
                   hipStream_t st, bool campp) {
   if (total_frames <= 0) return;
   if (campp)
-    hipLaunchKernelGGL(fbank_kernel<true>, dim3(cdiv(total_frames, kFbWaves)), dim3(64 * kFbWaves),
-                       0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames, tabs, out);
+    hipLaunchKernelGGL(fbank_kernel<true>, dim3(std::min(cdiv(total_frames, kFbWaves), kFbBlocks)),
+                       dim3(64 * kFbWaves), 0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames,
+                       tabs, out);
   else
-    hipLaunchKernelGGL(fbank_kernel<false>, dim3(cdiv(total_frames, kFbWaves)), dim3(64 * kFbWaves),
-                       0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames, tabs, out);
+    hipLaunchKernelGGL(fbank_kernel<false>, dim3(std::min(cdiv(total_frames, kFbWaves), kFbBlocks)),
+                       dim3(64 * kFbWaves), 0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames,
+                       tabs, out);
 }
 
 // =====================================================================================
