@@ -294,6 +294,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     ZASR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, greatest));
     ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream3_, hipStreamNonBlocking, greatest));
+    ZASR_HIP_CHECK(hipStreamCreateWithPriority(&stream4_, hipStreamNonBlocking, greatest));
     for (auto& x : enc_extra_) ZASR_HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
   }
   for (auto& e : part_ev_) ZASR_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -636,12 +637,16 @@ Engine::~Engine() {
   }
   (void)hipStreamSynchronize(stream2_);
   (void)hipStreamSynchronize(stream3_);
+  if (stream4_) (void)hipStreamSynchronize(stream4_);
   if (h_pinned_) (void)hipHostFree(h_pinned_);
+  for (auto& r : res_pin_)
+    if (r.p) (void)hipHostFree(r.p);
   for (auto& a : pin_)
     if (a.p) (void)hipHostFree(a.p);
   for (auto e : part_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(stream2_);
   (void)hipStreamDestroy(stream3_);
+  if (stream4_) (void)hipStreamDestroy(stream4_);
   for (auto x : enc_extra_) {
     (void)hipStreamSynchronize(x);
     (void)hipStreamDestroy(x);
@@ -1284,10 +1289,34 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
 
 std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vector<int>& t_out,
                                             int beam) {
+  SearchJob job;
+  launch_search(d_enc, t_out, beam, 0, st_, true, job);
+  return collect_search(job);
+}
+
+void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, int beam, int set,
+                           hipStream_t stream, bool split_groups, SearchJob& job) {
   const ModelConfig& cfg = model_.cfg;
   const int S_all = (int)t_out.size();
-  std::vector<TokenResult> res(S_all);
-  for (int s = 0; s < S_all; ++s) res[s].t_out = t_out[s];
+  job = SearchJob{};
+  job.S_all = S_all;
+  job.t_out = t_out;
+  job.set = set;
+  job.stream = stream;
+  hipStream_t caller_st = st_;
+  const std::string caller_tag = ws_tag_;
+  st_ = stream;
+  ws_tag_ = set ? "q" + std::to_string(set) + "/" : "";  // set 0: the single-search names
+  pin_reset(kMaxEnc + 1 + set);
+  struct Restore {
+    Engine* e;
+    hipStream_t st;
+    std::string tag;
+    ~Restore() {
+      e->st_ = st;
+      e->ws_tag_ = tag;
+    }
+  } restore{this, caller_st, caller_tag};
   // streams with T' >= 1, sorted by T' descending so active streams form a prefix
   std::vector<int> order;
   std::vector<int> enc_off_all(S_all + 1, 0);
@@ -1296,7 +1325,8 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
     if (t_out[s] > 0) order.push_back(s);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t_out[a] > t_out[b]; });
   const int S = (int)order.size();
-  if (S == 0) return res;
+  job.S = S;
+  if (S == 0) return;
   const int H = beam;
   const int Tmax = t_out[order[0]];
   const int V = cfg.V, D = cfg.joiner_dim;
@@ -1411,7 +1441,7 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   // streams order[g], order[g + G], ... (each group sorted by T' descending, active streams
   // a prefix), laid out contiguously; the search final runs over all of them.
   static const int env_groups = getenv("ZASR_SEARCH_GROUPS") ? atoi(getenv("ZASR_SEARCH_GROUPS")) : 2;
-  const int G = std::max(1, std::min({env_groups, 2, S}));
+  const int G = split_groups ? std::max(1, std::min({env_groups, 2, S})) : 1;
   if (G > 1) {
     std::vector<int> reord;
     for (int g = 0; g < G; ++g)
@@ -1516,6 +1546,11 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   }
   }
   const int cap = Tmax;
+  job.cap = cap;
+  job.Tmax = Tmax;
+  job.order = order;
+  job.stamps = stamps;
+  job.d_stamps = st.stamps;
   int* o_tok = ws<int>("so_tok", (size_t)S * cap);
   int* o_fr = ws<int>("so_fr", (size_t)S * cap);
   double* o_lp = ws<double>("so_lp", (size_t)S * cap);
@@ -1524,43 +1559,68 @@ std::vector<TokenResult> Engine::run_search(const float* d_enc, const std::vecto
   prof_begin("search");
   launch_search_final(st, S, H, hw_, cap, o_tok, o_fr, o_lp, o_st, o_cnt, st_);
   prof_end();
-  std::vector<int> h_tok((size_t)S * cap), h_fr((size_t)S * cap), h_cnt(S);
-  std::vector<double> h_lp((size_t)S * cap);
-  std::vector<float> h_st((size_t)S * cap * 4);
-  ZASR_HIP_CHECK(hipMemcpyAsync(h_cnt.data(), o_cnt, S * sizeof(int), hipMemcpyDeviceToHost, st_));
-  ZASR_HIP_CHECK(hipMemcpyAsync(h_tok.data(), o_tok, h_tok.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
-  ZASR_HIP_CHECK(hipMemcpyAsync(h_fr.data(), o_fr, h_fr.size() * sizeof(int), hipMemcpyDeviceToHost, st_));
-  ZASR_HIP_CHECK(hipMemcpyAsync(h_lp.data(), o_lp, h_lp.size() * sizeof(double), hipMemcpyDeviceToHost, st_));
-  ZASR_HIP_CHECK(hipMemcpyAsync(h_st.data(), o_st, h_st.size() * sizeof(float), hipMemcpyDeviceToHost, st_));
-  ZASR_HIP_CHECK(hipStreamSynchronize(st_));
-  if (stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
-    std::vector<unsigned long long> h((size_t)Tmax * 16);
-    ZASR_HIP_CHECK(hipMemcpy(h.data(), st.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+  // results into this set's pinned buffers (a copy into pageable memory would block the host
+  // until the search is done): [cnt S][tok S cap][fr S cap][lp S cap][stats S cap]
+  const size_t n = (size_t)S * cap;
+  const size_t bytes = 16 * n + 8 * n + 4 * n + 4 * n + 4 * (size_t)S + 64;
+  ResPin& rp = res_pin_[set];
+  if (rp.cap < bytes) {  // the set's previous job was collected: its buffer is free
+    if (rp.p) ZASR_HIP_CHECK(hipHostFree(rp.p));
+    rp.cap = bytes + bytes / 4;
+    ZASR_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&rp.p), rp.cap, hipHostMallocDefault));
+  }
+  char* h = rp.p;
+  ZASR_HIP_CHECK(hipMemcpyAsync(h, o_st, n * 16, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h + 16 * n, o_lp, n * 8, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h + 24 * n, o_tok, n * 4, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h + 28 * n, o_fr, n * 4, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipMemcpyAsync(h + 32 * n, o_cnt, (size_t)S * 4, hipMemcpyDeviceToHost, st_));
+  ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 4 + set], st_));
+}
+
+std::vector<TokenResult> Engine::collect_search(SearchJob& job) {
+  std::vector<TokenResult> res(job.S_all);
+  for (int s = 0; s < job.S_all; ++s) res[s].t_out = job.t_out[s];
+  if (job.S == 0) return res;
+  ZASR_HIP_CHECK(hipEventSynchronize(part_ev_[kMaxEnc + 4 + job.set]));
+  const int S = job.S, cap = job.cap;
+  const size_t n = (size_t)S * cap;
+  const char* h = res_pin_[job.set].p;
+  const float* h_st = reinterpret_cast<const float*>(h);
+  const double* h_lp = reinterpret_cast<const double*>(h + 16 * n);
+  const int* h_tok = reinterpret_cast<const int*>(h + 24 * n);
+  const int* h_fr = reinterpret_cast<const int*>(h + 28 * n);
+  const int* h_cnt = reinterpret_cast<const int*>(h + 32 * n);
+  if (job.stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
+    const int Tmax = job.Tmax;
+    std::vector<unsigned long long> hs((size_t)Tmax * 16);
+    ZASR_HIP_CHECK(hipMemcpy(hs.data(), job.d_stamps, hs.size() * 8, hipMemcpyDeviceToHost));
     const int seq[] = {0, 6, 7, 8, 10, 1, 2, 3, 4, 5};
     const char* name[] = {"nh", "row0_max", "row0_stats", "row0_topk", "rows_decode", "barrier",
                           "rank", "tail", "J"};
     const int NS = 9;
     double acc[16] = {0};
-    int n = 0;
+    int cnt = 0;
     for (int t = 0; t < Tmax; ++t) {
-      const unsigned long long* p = &h[(size_t)t * 16];
+      const unsigned long long* p = &hs[(size_t)t * 16];
       bool ok = true;
       for (int k = 0; k <= NS; ++k) ok = ok && p[seq[k]] != 0;
       if (!ok) continue;
       for (int k = 0; k < NS; ++k) acc[k] += (double)(p[seq[k + 1]] - p[seq[k]]);
-      ++n;
+      ++cnt;
     }
-    fprintf(stderr, "[zasr stamps] frames=%d mean cycles:", n);
-    for (int k = 0; k < NS; ++k) fprintf(stderr, " %s %.0f", name[k], n ? acc[k] / n : 0.0);
+    fprintf(stderr, "[zasr stamps] frames=%d mean cycles:", cnt);
+    for (int k = 0; k < NS; ++k) fprintf(stderr, " %s %.0f", name[k], cnt ? acc[k] / cnt : 0.0);
     fprintf(stderr, "\n");
   }
   for (int i = 0; i < S; ++i) {
-    TokenResult& r = res[order[i]];
+    TokenResult& r = res[job.order[i]];
     const int c = h_cnt[i];
-    r.tok.assign(h_tok.begin() + (size_t)i * cap, h_tok.begin() + (size_t)i * cap + c);
-    r.frame.assign(h_fr.begin() + (size_t)i * cap, h_fr.begin() + (size_t)i * cap + c);
-    r.lp.assign(h_lp.begin() + (size_t)i * cap, h_lp.begin() + (size_t)i * cap + c);
-    r.stats.assign(h_st.begin() + (size_t)i * cap * 4, h_st.begin() + ((size_t)i * cap + c) * 4);
+    const size_t o = (size_t)i * cap;
+    r.tok.assign(h_tok + o, h_tok + o + c);
+    r.frame.assign(h_fr + o, h_fr + o + c);
+    r.lp.assign(h_lp + o, h_lp + o + c);
+    r.stats.assign(h_st + 4 * o, h_st + 4 * (o + c));
   }
   return res;
 }
@@ -1622,7 +1682,6 @@ std::vector<TokenResult> Engine::search_stage(Pending& pd, int beam) {
   if (pd.valid.empty()) return out;
   hipStream_t main_st = st_;
   st_ = stream2_;
-  pin_reset(kMaxEnc + 1);
   ZASR_HIP_CHECK(hipStreamWaitEvent(stream2_, pd.ready, 0));
   std::vector<TokenResult> r = run_search(pd.enc, pd.t_out, beam);
   for (size_t i = 0; i < pd.valid.size(); ++i) out[pd.valid[i]] = std::move(r[i]);
@@ -1666,6 +1725,13 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   // stream only adds contention for it (69.9k vs 68.3k xRT at beam 8 + 20 hotwords).
   static const int env_e = getenv("ZASR_ENC_STREAMS") ? atoi(getenv("ZASR_ENC_STREAMS")) : 0;
   const int nb = (int)batch_sizes.size();
+  // Beam search: several batches' searches in flight (ZASR_SEARCH_JOBS, default 2).  Each
+  // batch's frame chain is latency-bound (joiner -> search step per frame, a few hundred
+  // blocks), so further chains on the other search streams run beside it at nearly the same
+  // per-frame latency.
+  static const int env_jobs = getenv("ZASR_SEARCH_JOBS") ? atoi(getenv("ZASR_SEARCH_JOBS")) : 2;
+  if (beam > 1 && env_jobs >= 2 && nb >= 2 && search_cus_ == 0 && stream4_ != nullptr)
+    return decode_batches_two_searches(d_wav, wav_off, n, batch_sizes, beam, main_st);
   const int want_e = env_e ? env_e : (beam > 1 ? 1 : 2);
   const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
   const int L = E;
@@ -1691,6 +1757,88 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
     if (k + L < nb) enqueue(k + L);
     std::vector<TokenResult> r = search_stage(pd[k % (L + 1)], beam);
     for (auto& x : r) out.push_back(std::move(x));
+  }
+  st_ = stream_;
+  return out;
+}
+
+std::vector<TokenResult> Engine::decode_batches_two_searches(const float* d_wav,
+                                                             const std::vector<long>& wav_off,
+                                                             const std::vector<long>& n,
+                                                             const std::vector<int>& batch_sizes,
+                                                             int beam, hipStream_t main_st) {
+  // J searches in flight (ZASR_SEARCH_JOBS, 2 or 3), L encoders enqueued ahead on E encoder
+  // streams (ZASR_ENC_STREAMS, 1 or 2; default 1), J + L encoder output slots.  Batch k:
+  // output slot / pinned arena k % (J + L), encoder stream and workspace set k % E, search job
+  // set k % J on its own high-priority stream.  Per iteration k: start batch k's search,
+  // collect batch k - J + 1's, enqueue batch k + L's encoder -- its slot was last used by
+  // batch k - J (collected in iteration k - 1), its stream's previous batch k + L - E is
+  // ordered before it on that stream, and job set k % J was last used by batch k - J.
+  static const int env_jobs = getenv("ZASR_SEARCH_JOBS") ? atoi(getenv("ZASR_SEARCH_JOBS")) : 2;
+  static const int env_e = getenv("ZASR_ENC_STREAMS") ? atoi(getenv("ZASR_ENC_STREAMS")) : 1;
+  const int nb = (int)batch_sizes.size();
+  const int J = std::max(2, std::min(env_jobs, (int)kMaxJobs));
+  const int L = std::max(1, kMaxEnc + 1 - J);
+  const int E = std::max(1, std::min(env_e, 2));
+  const int NS = J + L;
+  ZASR_REQUIRE(NS <= kMaxEnc + 1, "pipeline slots");
+  hipStream_t enc_st[2] = {main_st, enc_extra_[0]};
+  if (E > 1) {  // the second encoder stream starts after the caller's prior work
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 2], main_st));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(enc_st[1], part_ev_[kMaxEnc + 2], 0));
+  }
+  std::vector<long> first(nb + 1, 0);
+  for (int k = 0; k < nb; ++k) first[k + 1] = first[k] + batch_sizes[k];
+  Pending pd[kMaxEnc + 1];
+  auto enqueue = [&](int k) {
+    std::vector<long> o(wav_off.begin() + first[k], wav_off.begin() + first[k + 1]);
+    std::vector<long> l(n.begin() + first[k], n.begin() + first[k + 1]);
+    encode_stage(d_wav, o, l, k % NS, k % E, enc_st[k % E], pd[k % NS]);
+    st_ = main_st;
+  };
+  struct Job {
+    int B = 0;
+    std::vector<int> valid;
+    SearchJob sj;
+    bool launched = false;
+  } jobs[kMaxJobs];
+  const hipStream_t sst[kMaxJobs] = {stream2_, stream3_, stream4_};
+  auto start = [&](int k) {
+    Pending& p = pd[k % NS];
+    Job& j = jobs[k % J];
+    j.B = p.B;
+    j.valid = p.valid;
+    j.launched = !p.valid.empty();
+    if (!j.launched) return;
+    ZASR_HIP_CHECK(hipStreamWaitEvent(sst[k % J], p.ready, 0));
+    launch_search(p.enc, p.t_out, beam, k % J, sst[k % J], false, j.sj);
+  };
+  std::vector<TokenResult> out;
+  out.reserve(n.size());
+  auto finish = [&](int k) {
+    Job& j = jobs[k % J];
+    std::vector<TokenResult> o(j.B);
+    if (j.launched) {
+      std::vector<TokenResult> r = collect_search(j.sj);
+      for (size_t i = 0; i < j.valid.size(); ++i) o[j.valid[i]] = std::move(r[i]);
+    }
+    for (auto& x : o) out.push_back(std::move(x));
+  };
+  for (int k = 0; k < std::min(L, nb); ++k) enqueue(k);
+  for (int k = 0; k < nb; ++k) {
+    start(k);
+    if (k - J + 1 >= 0) finish(k - J + 1);
+    if (k + L < nb) enqueue(k + L);
+  }
+  for (int k = std::max(0, nb - J + 1); k < nb; ++k) finish(k);
+  // the call's stream sees every search and encoder complete (results are on the host)
+  for (int s = 0; s < J; ++s) {
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 1], sst[s]));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[kMaxEnc + 1], 0));
+  }
+  if (E > 1) {
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 1], enc_st[1]));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[kMaxEnc + 1], 0));
   }
   st_ = stream_;
   return out;

@@ -153,6 +153,12 @@ class Engine {
   void encode_stage(const float* d_wav, const std::vector<long>& wav_off, const std::vector<long>& n,
                     int out_slot, int ws_slot, hipStream_t stream, Pending& p);
   std::vector<TokenResult> search_stage(Pending& p, int beam);
+  // decode_device_batches for beam search: several batches' searches in flight
+  std::vector<TokenResult> decode_batches_two_searches(const float* d_wav,
+                                                       const std::vector<long>& wav_off,
+                                                       const std::vector<long>& n,
+                                                       const std::vector<int>& batch_sizes,
+                                                       int beam, hipStream_t main_st);
   // pinned staging for host->device metadata uploads: one arena per encoder output slot
   // plus one for the search, so an upload never waits for the stream to drain
   struct PinArena {
@@ -160,7 +166,9 @@ class Engine {
     size_t cap = 0, used = 0, want = 0;
   };
   static constexpr int kMaxEnc = 3;  // encoder streams of the batch pipeline
-  PinArena pin_[kMaxEnc + 2];       // kMaxEnc + 1 output slots, then the search's
+  // kMaxEnc + 1 output slots, then one per search job set (two beam searches in flight)
+  static constexpr int kMaxJobs = 3;  // beam searches in flight
+  PinArena pin_[kMaxEnc + 1 + kMaxJobs];
   std::string ws_tag_;  // workspace-name prefix of the encoder workspace set in use
   int pin_cur_ = 0;
   void pin_reset(int arena);
@@ -171,6 +179,24 @@ class Engine {
   void run_encoder(const float* d_feats, const std::vector<int>& T, float* d_enc,
                    std::vector<int>& t_out);
   std::vector<TokenResult> run_search(const float* d_enc, const std::vector<int>& t_out, int beam);
+  // a search whose launches and result copies are enqueued; collect_search waits for it.
+  // Job set `set` (0 .. kMaxJobs - 1) owns its search workspace, pinned arena, result buffers and
+  // completion event, so two jobs can be in flight on the two search streams.
+  struct SearchJob {
+    int S_all = 0, S = 0, cap = 0, set = 0, Tmax = 0;
+    std::vector<int> order, t_out;
+    bool stamps = false;
+    unsigned long long* d_stamps = nullptr;
+    hipStream_t stream = nullptr;
+  };
+  void launch_search(const float* d_enc, const std::vector<int>& t_out, int beam, int set,
+                     hipStream_t stream, bool split_groups, SearchJob& job);
+  std::vector<TokenResult> collect_search(SearchJob& job);
+  struct ResPin {  // pinned host result buffers of one job set
+    char* p = nullptr;
+    size_t cap = 0;
+  };
+  ResPin res_pin_[kMaxJobs];
   void layer_forward(const DStack& stk, const DLayer& ly, float* X, int R, const int* d_off,
                      const int* d_map, const std::vector<int>& lens, const long* d_aoff,
                      const void* d_slices_nl, int maxL, const int* d_o8, int R8, bool orig_ready = false,
@@ -209,10 +235,12 @@ class Engine {
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
   hipStream_t stream3_ = nullptr;  // the second group of a beam search (high priority)
+  hipStream_t stream4_ = nullptr;  // the third beam search in flight (high priority)
   int search_cus_ = 0;             // > 0: search / encoder streams on disjoint CU sets
   hipStream_t enc_extra_[kMaxEnc - 1] = {};  // encoder streams 1.. of the batch pipeline
-  // [0, kMaxEnc]: encoder output slots; kMaxEnc + 1: search done; kMaxEnc + 2: start
-  hipEvent_t part_ev_[kMaxEnc + 4] = {};
+  // [0, kMaxEnc]: encoder output slots; kMaxEnc + 1: search done; kMaxEnc + 2: start;
+  // kMaxEnc + 3: beam groups; kMaxEnc + 4 + set: search job `set` complete
+  hipEvent_t part_ev_[kMaxEnc + 4 + kMaxJobs] = {};
   hipStream_t st_ = nullptr;  // stream of the current call
   std::map<std::string, Buf> ws_;
   // fbank tables
