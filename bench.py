@@ -76,16 +76,21 @@ def parse_args(argv=None):
                     help="no GPU: exercise the launcher / rank / timing / JSON path with gloo "
                          "and a CPU stand-in step (tests/test_bench_launcher.py)")
     ap.add_argument("--profile-out", default="")
-    ap.add_argument("--stage", default="asr", choices=["asr", "campp", "vad", "pipe"],
+    ap.add_argument("--stage", default="asr", choices=["asr", "campp", "vad", "pipe", "rover"],
                     help="asr: the Zipformer decode (default, BASELINE metric); campp: the CAM++ "
                          "speaker-embedding stage of config 5 (1.5 s windows, 0.6 s step); vad: "
                          "Silero VAD probabilities + segments of the hour (core/asr_engine.py:2090); "
                          "pipe: BASELINE config 5, decode + merge + CAM++ embeddings + ViBERT "
-                         "punctuation of the hour (zasr/pipeline.py)")
+                         "punctuation of the hour (zasr/pipeline.py); rover: BASELINE config 4, "
+                         "30M + 68M decode of the hour + block vote + merge (zasr/rover.py)")
     ap.add_argument("--vad-files", type=int, default=1,
                     help="VAD stage: the hour split into this many files decoded in one call "
                          "(1 = the reference's single-file case; the recurrence is one "
                          "workgroup per file)")
+    ap.add_argument("--rover-sub-batches", type=int, default=2,
+                    help="ROVER stage: each model decodes the hour as this many pipelined batches "
+                         "(measured 1 / 2 / 4 / 8: 143 / 136 / 171 / 245 ms per hour: every batch "
+                         "adds a frame chain as long as its longest chunk)")
     ap.add_argument("--campp-batch", type=int, default=4096,
                     help="CAM++ windows per launch group (the reference batches 32 on CPU; "
                          "measured 512 -> 6000: 167 -> 123 ms per hour, profiles/r02/campp_batch)")
@@ -691,6 +696,115 @@ def bench_pipe(args):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------ ROVER pair (config 4)
+def bench_rover(args):
+    """BASELINE config 4 per GPU: one step = the hour's planner chunks through Zipformer-30M
+    (primary) and Zipformer-68M, both modified beam search with beam --beam (the reference's
+    decode_chunk always runs _ort_beam_search with max_active_paths = 8,
+    core/asr_engine.py:1224, :2041-2044), concurrently on the GPU, then the per-chunk block vote
+    and the chunk-overlap merge on the host, pipelined with the next step's decode
+    (zasr.rover.rover_device_many).  Audio resident in HBM."""
+    import torch
+    from zasr.binding import Recognizer
+    from zasr.model import PRESETS, chunk_flops, save_model_dir, synth_tokens, synth_weights
+    from zasr.rover import rover_device_many
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    beam = args.beam
+    recs, recds, cfgs = [], [], []
+    for name, seed in (("zipformer-30m", WEIGHT_SEED + 1), ("zipformer-68m", WEIGHT_SEED)):
+        cfg = PRESETS[name]()
+        hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
+        hotwords = load_hotwords(hw_path, cfg.vocab_size) if hw_path else None
+        mdir = os.path.join(tempfile.gettempdir(), f"zasr_rover_{name}_{os.getpid()}")
+        toks = synth_tokens(cfg.vocab_size)
+        save_model_dir(mdir, cfg, synth_weights(cfg, seed), toks)
+        recs.append(Recognizer(mdir, "modified_beam_search", beam,
+                               hotwords=hotwords[0] if hotwords else None,
+                               hotword_scores=hotwords[1] if hotwords else None,
+                               device_id=local, precision=args.precision))
+        recds.append({"id2token": dict(enumerate(toks)), "vocab_size": cfg.vocab_size})
+        cfgs.append(cfg)
+    chunks = make_chunks(args.audio_sec, AUDIO_SEED + rank)
+    lens = [c.shape[0] for c in chunks]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    d_wav = torch.from_numpy(np.concatenate(chunks)).cuda()
+    torch.cuda.synchronize()
+    phrases = []
+    if args.hotwords_file:
+        from zasr.hotword_context import parse_hotwords_file
+        hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
+        phrases = [p for p, _ in parse_hotwords_file(hw_path, 1.5)]
+    last = {}
+
+    def steps(k):
+        r = rover_device_many(recs[0], recs[1], recds[0], recds[1], d_wav.data_ptr(), offs, lens,
+                              k, beam, phrases, args.rover_sub_batches)[-1]
+        last.update(words=len(r[0]), disagree_blocks=sum(r[1]), tokens_a=r[2], tokens_b=r[3])
+
+    if args.warmup:
+        steps(args.warmup)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps(args.steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=f"cuda:{local}")
+    # each model alone (decode only, HIP work + result copies) for the breakdown
+    alone = {}
+    for name, rec in zip(("30m", "68m"), recs):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        rec.decode_device(d_wav.data_ptr(), offs, lens, beam=beam)
+        alone[name] = round(1000 * (time.perf_counter() - t1), 2)
+    t_step = el / args.steps
+    fl = sum(sum(chunk_flops(c, n, beam).values()) for c in cfgs for n in lens)
+    peak = MFMA_BF16_PEAK_TFLOPS if args.precision != "fp32" else MFMA_F32_PEAK_TFLOPS
+    if rank == 0:
+        line = {"metric": "audio-sec/sec (xRT) ROVER Zipformer-30M + 68M offline decode",
+                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(1000 * t_step, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": args.precision,
+                "data": "synthetic (seeded speech-like audio, random-init Zipformer-30M / 68M weights)",
+                "config": {"workload": f"BASELINE config 4 per GPU: zipformer-30m + zipformer-68m "
+                                       f"modified_beam_search beam {beam}"
+                                       f"{' + hotwords' if phrases else ''}, 1 h of planner "
+                                       f"chunks, block vote + overlap merge",
+                           "chunks_per_gpu": len(lens), "sub_batches": args.rover_sub_batches,
+                           "words": last["words"],
+                           "disagreeing_blocks": last["disagree_blocks"],
+                           "tokens_30m": last["tokens_a"], "tokens_68m": last["tokens_b"],
+                           "decode_alone_ms": alone,
+                           "parallelism": f"dp{world} (each rank its own hour; weak scaling)"},
+                "roofline": {"kernel": "both encoders + joiners (algorithmic flops / step time)",
+                             "bound": "mfma", "unit": "TFLOP/s",
+                             "achieved": round(fl / t_step / 1e12, 2), "peak": peak,
+                             "frac": round(fl / t_step / 1e12 / peak, 4),
+                             "flops_per_step": fl},
+                "cpu_baseline": None}
+        print(json.dumps(line))
+        if args.profile_out:
+            with open(args.profile_out, "w") as f:
+                json.dump(line, f, indent=1)
+    for r in recs:
+        r.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse_args()
@@ -702,6 +816,8 @@ def main():
         return bench_vad(args)
     if args.stage == "pipe":
         return bench_pipe(args)
+    if args.stage == "rover":
+        return bench_rover(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

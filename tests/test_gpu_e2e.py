@@ -267,3 +267,35 @@ def test_rover_30m_68m_matches_oracle(m_case, s_case):
         assert [w["text"] for w in g_merged] == [w["text"] for w in merged], ci
         assert [round(w["start"], 9) for w in g_merged] == [round(w["start"], 9) for w in merged]
         assert g_dis == dis
+
+
+def test_rover_device_passes_equal_host_route(m_case, s_case):
+    """zasr.rover.rover_device_many (both models decode the HBM-resident chunks concurrently,
+    each computing the fbank on the device, passes pipelined) == decode_chunks_rover (one
+    shared GPU fbank per chunk through host memory) + merge_chunks_with_overlap, for every
+    pass."""
+    import torch
+    from zasr.asr_engine import create_recognizer
+    from zasr.merge import merge_chunks_with_overlap
+    from zasr.rover import decode_chunks_rover, rover_device_many
+    ra = create_recognizer(s_case["path"], max_active_paths=8, precision="bf16")
+    rb = create_recognizer(m_case["path"], max_active_paths=8, precision="bf16")
+    chunks = [_speech(s, 1600 + i) for i, s in enumerate((14.0, 9.5, 11.0))]
+    lens = [c.shape[0] for c in chunks]
+    d = torch.from_numpy(np.concatenate(chunks)).cuda()
+    torch.cuda.synchronize()
+    # the chunks' positions in HBM are their time offsets (packed back to back)
+    poffs = np.cumsum([0] + lens[:-1]).tolist()
+    got2 = decode_chunks_rover(ra, rb, chunks, [o / 16000.0 for o in poffs])
+    ref2, _ = merge_chunks_with_overlap([{"words": m, "audio_start_abs": o / 16000.0,
+                                          "audio_end_abs": (o + n) / 16000.0}
+                                         for (m, _), o, n in zip(got2, poffs, lens)])
+    passes = rover_device_many(ra["handle"], rb["handle"], ra, rb, d.data_ptr(), poffs, lens, 2, 8)
+    passes += rover_device_many(ra["handle"], rb["handle"], ra, rb, d.data_ptr(), poffs, lens, 2,
+                                8, sub_batches=2)
+    for words, dis, ta, tb in passes:
+        assert [w["text"] for w in words] == [w["text"] for w in ref2]
+        assert [w["start"] for w in words] == [w["start"] for w in ref2]
+        assert dis == [len(x) for _, x in got2]
+        assert ta > 0 and tb > 0
+    assert len(ref2) > 0
