@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round measurement on the GPU box (development tool): the default bench line, a rocprofv3
-# kernel-trace/stats pass of the same bench command, and two PMC passes (FETCH_SIZE and
-# WRITE_SIZE in separate runs) for the HBM traffic of the dominant kernel class.
+# kernel-trace/stats pass of the same bench command, PMC passes (FETCH_SIZE and WRITE_SIZE in
+# separate runs, MFMA busy) for the dominant kernel class, kernel stats of the CAM++ / VAD
+# stages, and the bench lines of BASELINE configs 3, 4 and 5.
 # Usage (from the repo root, via gpurun): bash sherpa-vietnamese-asr_amd/tools/profile_round.sh TAG
 set -e
 TAG=${1:-r}
@@ -17,4 +18,9 @@ timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --out
 for st in campp vad; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_$st -o run -- python3 $R/bench.py --stage $st --no-cpu-baseline --steps 3 --warmup 1 > $OUT/stats_$st.json 2> $OUT/stats_$st.err
 done
+timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords.json 2> $OUT/bench_beam8.err
+timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwords-file default > $OUT/bench_rover.json 2> $OUT/bench_rover.err
+timeout -k 10 300 python3 $R/bench.py --stage pipe --steps 4 --warmup 1 > $OUT/bench_pipe.json 2> $OUT/bench_pipe.err
+timeout -k 10 300 python3 $R/bench.py --stage campp > $OUT/bench_campp.json 2> $OUT/bench_campp.err
+timeout -k 10 300 python3 $R/bench.py --stage vad > $OUT/bench_vad.json 2> $OUT/bench_vad.err
 echo done
