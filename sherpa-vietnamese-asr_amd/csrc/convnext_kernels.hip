@@ -82,6 +82,21 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
   const int c0 = blockIdx.y * kDwC;
   const int tid = threadIdx.x;
   if (tid == 0) sMasked = 0;
+  // every global load of the block is issued before the first wait: this thread's channel
+  // pair weights and bias, the sequence bounds of the tile frames (L_map -> L_off) and the
+  // staged input -- one memory round trip instead of three
+  const int p = tid & 31;  // channel pair c0 + 2p, c0 + 2p + 1 (fixed per thread)
+  float2 w[49];
+#pragma unroll
+  for (int k = 0; k < 49; ++k)
+    w[k] = make_float2(dw_w[(c0 + 2 * p) * 49 + k], dw_w[(c0 + 2 * p + 1) * 49 + k]);
+  const float2 bias = make_float2(dw_b[c0 + 2 * p], dw_b[c0 + 2 * p + 1]);
+  int seq_lo = 0, seq_hi = 0;
+  if (tid < kDwT && t0 + tid < total_rows) {
+    const int b = L_map[t0 + tid];
+    seq_lo = L_off[b];
+    seq_hi = L_off[b + 1];
+  }
   // ---- zero freq padding columns (3 + 3 per staged frame, 8 pieces of 16 B each) ----
   for (int e = tid; e < kDwH * 6 * 8; e += 256) {
     const int q = e & 7, cf = (e >> 3) % 6, rr = (e >> 3) / 6;
@@ -123,9 +138,8 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
     const int r = t0 + tid;
     int lo = -3, hi = 3;
     if (r < total_rows) {
-      const int b = L_map[r];
-      lo = max(L_off[b] - r, -3);
-      hi = min(L_off[b + 1] - 1 - r, 3);
+      lo = max(seq_lo - r, -3);
+      hi = min(seq_hi - 1 - r, 3);
     }
     sLo[tid] = lo;
     sHi[tid] = hi;
@@ -134,12 +148,6 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
   if (tid < kDwT && (sLo[tid] != -3 || sHi[tid] != 3)) atomicOr(&sMasked, 1);
   __syncthreads();
 
-  const int p = tid & 31;  // channel pair c0 + 2p, c0 + 2p + 1 (fixed per thread)
-  float2 w[49];
-#pragma unroll
-  for (int k = 0; k < 49; ++k)
-    w[k] = make_float2(dw_w[(c0 + 2 * p) * 49 + k], dw_w[(c0 + 2 * p + 1) * 49 + k]);
-  const float2 bias = make_float2(dw_b[c0 + 2 * p], dw_b[c0 + 2 * p + 1]);
   const bool masked = sMasked != 0;
   for (int it = tid; it < kDwItems; it += 256) {
     const int q = it >> 5;  // (segment, freq)

@@ -512,6 +512,28 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
   const int c0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
   if (tid == 0) sMasked = 0;
+  // every global load of the block is issued before the first wait: this lane's channel
+  // weights and bias, the sequence bounds of the tile rows (map -> off) and the staged
+  // input -- one memory round trip instead of three
+  const int c = tid & 63;
+  const int cw = c0 + c < d ? c0 + c : d - 1;  // clamped: lanes past d never store
+  float wr[K];
+  const int pad = (K - Kr) / 2;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int kk = k - pad;
+    const bool ok = kk >= 0 && kk < Kr;
+    const float wv = w[(long)cw * Kr + (ok ? kk : 0)];
+    wr[k] = ok ? wv : 0.f;
+  }
+  const float bc = bias[cw];
+  int seq_lo = 0, seq_hi = 0;
+  const int rb = r0 + (tid & (kDw1T - 1));
+  if (tid < kDw1T && rb < total_rows) {
+    const int b = map[rb];
+    seq_lo = off[b];
+    seq_hi = off[b + 1];
+  }
   {
     float4 a[kIt], g[kIt];
 #pragma unroll
@@ -541,28 +563,16 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
     const int r = r0 + tid;
     int lo = -half, hi = half;
     if (r < total_rows) {
-      const int b = map[r];
-      lo = max(off[b] - r, -half);
-      hi = min(off[b + 1] - 1 - r, half);
+      lo = max(seq_lo - r, -half);
+      hi = min(seq_hi - 1 - r, half);
     }
     sLo[tid] = lo;
     sHi[tid] = hi;
     if (lo != -half || hi != half) atomicOr(&sMasked, 1);
   }
   __syncthreads();
-  const int c = tid & 63;
   if (c0 + c >= d) return;
   const int tr0 = (tid >> 6) * 16;
-  float wr[K];
-  const int pad = (K - Kr) / 2;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int kk = k - pad;
-    const bool ok = kk >= 0 && kk < Kr;
-    const float wv = w[(long)(c0 + c) * Kr + (ok ? kk : 0)];
-    wr[k] = ok ? wv : 0.f;
-  }
-  const float bc = bias[c0 + c];
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = bc;
