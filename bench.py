@@ -31,6 +31,13 @@ import sys
 import tempfile
 import time
 
+# hardware queues per process (HIP's default is 4): the batch pipeline keeps up to five
+# streams busy (caller, two encoder streams, two beam searches), and streams beyond the queue
+# count share queues in creation order -- 8 measured +3.6 % on the beam 8 line, neutral on
+# greedy (profiles/r02/hw_queues).  Set before anything initialises HIP; <= 32 as the pool allows.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "sherpa-vietnamese-asr_amd")
 for _p in (REPO, PKG):
