@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import logging
 import math
+from functools import lru_cache
 import os
 import threading
 from typing import Dict, List, Optional, Sequence
@@ -68,6 +69,17 @@ class TokenStats:
 
     def __init__(self, row):
         self.entropy, self.s3, self.top1, self.top2 = (float(x) for x in row)
+
+    @staticmethod
+    def rows(stats) -> List["TokenStats"]:
+        """TokenStats of every row of an [n][4] float32 array (one tolist(): the same Python
+        floats as float() of each element, without the per-element numpy scalars)."""
+        out = []
+        for e, s3, t1, t2 in np.asarray(stats, np.float32).reshape(-1, 4).tolist():
+            t = TokenStats.__new__(TokenStats)
+            t.entropy, t.s3, t.top1, t.top2 = e, s3, t1, t2
+            out.append(t)
+        return out
 
 
 def _default_handle() -> Recognizer:
@@ -232,12 +244,20 @@ def _ort_beam_search(recognizer, features, beam_size=8):
             [TokenStats(s) for s in r.stats])
 
 
+@lru_cache(maxsize=64)
+def _entropy_norms(V):
+    """(max entropy, Tsallis-1/3 maximum) of a vocabulary (reference :1161-1165)."""
+    alpha = 1.0 / 3.0
+    max_entropy = math.log(V) if V > 1 else 1.0
+    ts_max = (1.0 / (alpha - 1.0)) * (1.0 - V ** (1.0 - alpha)) if V > 1 else 1.0
+    return max_entropy, ts_max
+
+
 def _compute_token_entropy(raw_logits, V):
     """Entropy metrics of one emitted token (reference :1159-1181).  Accepts the device
     TokenStats (normal path) or a raw logits row (computed as the reference does)."""
-    max_entropy = math.log(V) if V > 1 else 1.0
+    max_entropy, ts_max = _entropy_norms(V)
     alpha = 1.0 / 3.0
-    ts_max = (1.0 / (alpha - 1.0)) * (1.0 - V ** (1.0 - alpha)) if V > 1 else 1.0
     if isinstance(raw_logits, TokenStats):
         entropy, s3, top1, top2 = raw_logits.entropy, raw_logits.s3, raw_logits.top1, raw_logits.top2
     else:
@@ -359,7 +379,7 @@ def result_words(recognizer, r, n_samples: int, time_offset: float):
     decode_chunk, shared by decode_chunk / decode_chunks / the ROVER path."""
     return _words_from_search(recognizer["id2token"], recognizer["vocab_size"], n_samples,
                               time_offset, r.token_ids.tolist(), r.frames.tolist(),
-                              r.log_probs.tolist(), int(r.T), [TokenStats(s) for s in r.stats])
+                              r.log_probs.tolist(), int(r.T), TokenStats.rows(r.stats))
 
 
 def decode_chunk(recognizer, audio_chunk, time_offset=0.0, precomputed_features=None):

@@ -18,6 +18,7 @@ vote `rover_merge_words` (core/asr_engine.py:1446-1577), restated as `rover_merg
 from __future__ import annotations
 
 import re
+from functools import lru_cache
 import unicodedata
 from difflib import SequenceMatcher
 from typing import Dict, List, Optional, Sequence, Set, Tuple
@@ -30,10 +31,14 @@ DUP_WINDOW_SEC = 0.15
 Word = Dict
 
 
+_NON_WORD = re.compile(r"[^\w]", flags=re.UNICODE)
+
+
+@lru_cache(maxsize=1 << 16)
 def normalize_word(text: str) -> str:
-    """lowercase, NFC, word characters only (core/asr_engine.py:44-49)."""
-    t = unicodedata.normalize("NFC", text.lower().strip())
-    return re.sub(r"[^\w]", "", t, flags=re.UNICODE)
+    """lowercase, NFC, word characters only (core/asr_engine.py:44-49); memoised (a
+    transcript repeats its syllables)."""
+    return _NON_WORD.sub("", unicodedata.normalize("NFC", text.lower().strip()))
 
 
 def word_confidence(w: Word) -> float:
