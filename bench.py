@@ -35,7 +35,9 @@ import time
 # streams busy (caller, two encoder streams, two beam searches), and streams beyond the queue
 # count share queues in creation order -- 8 measured +3.6 % on the beam 8 line, neutral on
 # greedy (profiles/r02/hw_queues).  Set before anything initialises HIP; <= 32 as the pool allows.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+if os.environ.get("ZASR_HW_QUEUES"):  # explicit choice (A/B runs)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["ZASR_HW_QUEUES"]
+elif int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 REPO = os.path.dirname(os.path.abspath(__file__))
