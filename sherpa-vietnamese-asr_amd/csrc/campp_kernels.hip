@@ -20,11 +20,13 @@ namespace zasr {
 // Epilogue: y = acc * scale[co] + shift[co] (+ res) then ReLU (flags); output either NCHW or
 // (tdnn_out) the TDNN layout [N][T][Co * Fo] with channel co * Fo + fo.
 // ---------------------------------------------------------------------------------------
-template <int KS>
+template <int KS, int CIMAX>
 __global__ __launch_bounds__(256) void campp_conv2d_kernel(CamppConv2d a) {
   constexpr int CO = 32, TT = 64, PAD = KS / 2, TW = TT + KS - 1;
-  __shared__ float sW[CO * 32 * KS * KS];
-  __shared__ float sX[32 * KS * TW];
+  // LDS sized for CIMAX input channels: the FCM head's first convolution (Ci = 1) stages
+  // 2 KB instead of 61 KB, so 8 blocks (not 2) share a CU
+  __shared__ float sW[CO * CIMAX * KS * KS];
+  __shared__ float sX[CIMAX * KS * TW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int t0 = blockIdx.x * TT, fo = blockIdx.y, n = blockIdx.z;
   const int Ci = a.ci;
@@ -323,8 +325,9 @@ void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st) {
     return;
   }
   dim3 grid(cdiv(a.T, 64), a.fo, a.n);
-  if (ks == 3) hipLaunchKernelGGL(campp_conv2d_kernel<3>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(campp_conv2d_kernel<1>, grid, dim3(256), 0, st, a);
+  if (ks == 3 && a.ci == 1) hipLaunchKernelGGL((campp_conv2d_kernel<3, 1>), grid, dim3(256), 0, st, a);
+  else if (ks == 3) hipLaunchKernelGGL((campp_conv2d_kernel<3, 32>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((campp_conv2d_kernel<1, 32>), grid, dim3(256), 0, st, a);
 }
 
 // y[r][c] = relu(x[r][c] * s[c] + b[c]), c < C (x row stride ldx, y row stride C)
