@@ -563,6 +563,62 @@ def bench_vad(args):
 
 
 # ------------------------------------------------------------------ full pipe (config 5)
+def _pipe_cpu_job(job):
+    """The config-5 pipe on the CPU oracles for a bounded sample (spawned child: torch thread
+    count isolated, no GPU): decode (numpy fbank + torch fp32 encoder + the reference search,
+    greedy) of the sample's planner chunks, their words, the merge, CAM++ window embeddings of
+    the sample's speech regions (oracle fbank + CAMPPlus, batches of 32 as the reference) and
+    3 ViBERT passes over the sample's word chunks (mini-batches of 32)."""
+    import torch
+    from oracle.campplus import CamppOracle, campp_fbank
+    from oracle.fbank import fbank
+    from oracle.search import beam_search
+    from oracle.vibert import VibertOracle
+    from oracle.zipformer import ZipformerOracle
+    from zasr.asr_engine import TokenStats, _words_from_search
+    from zasr.campp import CamppConfig, window_plan
+    from zasr.campp import synth_weights as campp_weights
+    from zasr.merge import merge_chunks_with_overlap
+    from zasr.model import PRESETS, synth_tokens, synth_weights
+    from zasr.pipeline import punctuate, split_word_chunks, vibert_feeds
+    from zasr.vibert import synth_weights as vib_weights
+    from zasr.vibert import vibert_base
+    model, threads, chunks, offs, regions = job
+    torch.set_num_threads(threads)
+    cfg = PRESETS[model]()
+    orc = ZipformerOracle(cfg, synth_weights(cfg, WEIGHT_SEED))
+    toks = synth_tokens(cfg.vocab_size)
+    id2 = dict(enumerate(toks))
+    ccfg = CamppConfig()
+    corc = CamppOracle(ccfg, campp_weights(ccfg, 20261017))
+    vcfg = vibert_base()
+    vorc = VibertOracle(vcfg, vib_weights(vcfg, 20261018))
+
+    class Sess:
+        def run(self, names, feeds):
+            return list(vorc.run(feeds["input_ids"], feeds["attention_mask"],
+                                 feeds["token_type_ids"], feeds["input_offsets"]))
+
+    orc.encoder(fbank(chunks[0][:SR * 2]))  # warm-up
+    t0 = time.perf_counter()
+    per = []
+    for c, off in zip(chunks, offs):
+        enc = orc.encoder(fbank(c))
+        tk, fr, lp, T, emit = beam_search(enc, orc.decoder, orc.joiner, 1)
+        per.append({"words": _words_from_search(id2, cfg.vocab_size, len(c), off / SR, tk, fr, lp,
+                                                T, emit),
+                    "audio_start_abs": off / SR, "audio_end_abs": (off + len(c)) / SR})
+    words, _ = merge_chunks_with_overlap(per)
+    wins = []
+    for r in regions:
+        fb = campp_fbank(r)
+        wins += [fb[a:a + n] for a, n in window_plan(fb.shape[0]) if n == 150]
+    for b in range(0, len(wins), 32):
+        corc.embed(np.stack(wins[b:b + 32]))
+    punctuate(Sess(), [w["text"] for w in words], vcfg.vocab_size)
+    return time.perf_counter() - t0, len(words), len(wins)
+
+
 def bench_pipe(args):
     """BASELINE config 5 per GPU: one step = one hour through decode (68M, --method,
     --precision) -> word post-processing -> chunk-overlap merge -> ViBERT-capu punctuation of
@@ -584,6 +640,27 @@ def bench_pipe(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    audio = synth_speech(args.audio_sec, AUDIO_SEED + rank)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before this process touches the GPU (spawned child); bounded sample: the first two
+        # planner chunks and the speech regions they span
+        import multiprocessing as mp
+        from zasr.plan import plan_chunks
+        plan = plan_chunks(audio)[:2]
+        end = plan[-1][1]
+        regs = [audio[a:e] for a, e, _ in plan_chunks(audio, overlap_sec=0.0) if e <= end]
+        threads = min(16, os.cpu_count() or 1)
+        with mp.get_context("spawn").Pool(1) as pool:
+            el_cpu, nw, nwin = pool.map(_pipe_cpu_job, [(args.model, threads,
+                                                         [audio[a:e] for a, e, _ in plan],
+                                                         [a for a, _, _ in plan], regs)])[0]
+        cpu = {"value": round(end / SR / el_cpu, 3), "unit": "audio-sec/sec", "cores": threads,
+               "kind": "port", "repeats": 1,
+               "sample": f"the first {end / SR:.1f} s (2 planner chunks): oracle decode (greedy) "
+                         f"+ words + merge, CAM++ oracle on {nwin} windows (batches of 32), 3 "
+                         f"ViBERT oracle passes over {nw} words (mini-batches of 32); torch fp32, "
+                         f"{threads} threads, one timed pass after a warm-up"}
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -610,7 +687,6 @@ def bench_pipe(args):
     vib_save(vdir, vcfg, vib_weights(vcfg, 20261018))
     vib = VibertSession(vdir, device_id=local)
 
-    audio = synth_speech(args.audio_sec, AUDIO_SEED + rank)
     pipe = FullPipe(rec, recd, emb, vib, vcfg.vocab_size, beam=beam, campp_batch=args.campp_batch)
     pipe.prepare(audio)
     out = {}
@@ -693,7 +769,7 @@ def bench_pipe(args):
                                      "(f32 in fp32 mode) + CAM++ / ViBERT flops at the f32 MFMA "
                                      "peak (exact f32, their reference tolerances); per-stage "
                                      "roofs in the asr / campp stage lines"},
-                "cpu_baseline": None}
+                "cpu_baseline": cpu}
         print(json.dumps(line))
         if args.profile_out:
             with open(args.profile_out, "w") as f:
@@ -706,6 +782,40 @@ def bench_pipe(args):
 
 
 # ------------------------------------------------------------------ ROVER pair (config 4)
+def _rover_cpu_job(job):
+    """Config 4 on the CPU oracles for a bounded sample (spawned child, no GPU): both models'
+    oracle decode (numpy fbank once per chunk, shared as the reference does; torch fp32
+    encoders; the reference search, beam + hotword graph), their words and the block vote."""
+    import torch
+    from oracle.fbank import fbank
+    from oracle.search import HotwordGraph, beam_search
+    from oracle.zipformer import ZipformerOracle
+    from zasr.asr_engine import _words_from_search
+    from zasr.model import PRESETS, synth_tokens, synth_weights
+    from zasr.rover import rover_merge
+    threads, chunks, offs, beam, hw_path, phrases = job
+    torch.set_num_threads(threads)
+    models = []
+    for name, seed in (("zipformer-30m", WEIGHT_SEED + 1), ("zipformer-68m", WEIGHT_SEED)):
+        cfg = PRESETS[name]()
+        hw = load_hotwords(hw_path, cfg.vocab_size) if hw_path else None
+        models.append((cfg, ZipformerOracle(cfg, synth_weights(cfg, seed)),
+                       dict(enumerate(synth_tokens(cfg.vocab_size))),
+                       HotwordGraph(*hw) if hw and hw[0] else None))
+    models[0][1].encoder(fbank(chunks[0][:SR * 2]))  # warm-up
+    t0 = time.perf_counter()
+    n_words = 0
+    for c, off in zip(chunks, offs):
+        f = fbank(c)
+        per = []
+        for cfg, orc, id2, graph in models:
+            tk, fr, lp, T, emit = beam_search(orc.encoder(f), orc.decoder, orc.joiner, beam, graph)
+            per.append(_words_from_search(id2, cfg.vocab_size, len(c), off / SR, tk, fr, lp, T,
+                                          emit))
+        n_words += len(rover_merge(per[0], per[1], phrases)[0])
+    return time.perf_counter() - t0, n_words
+
+
 def bench_rover(args):
     """BASELINE config 4 per GPU: one step = the hour's planner chunks through Zipformer-30M
     (primary) and Zipformer-68M, both modified beam search with beam --beam (the reference's
@@ -720,16 +830,37 @@ def bench_rover(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    beam = args.beam
+    chunks = make_chunks(args.audio_sec, AUDIO_SEED + rank)
+    lens = [c.shape[0] for c in chunks]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    hw_path = (DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file) or ""
+    phrases = []
+    if hw_path:
+        from zasr.hotword_context import parse_hotwords_file
+        phrases = [p for p, _ in parse_hotwords_file(hw_path, 1.5)]
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before this process touches the GPU (spawned child); bounded sample: the first chunk
+        import multiprocessing as mp
+        threads = min(16, os.cpu_count() or 1)
+        with mp.get_context("spawn").Pool(1) as pool:
+            el_cpu, nw = pool.map(_rover_cpu_job, [(threads, chunks[:1], offs[:1], beam, hw_path,
+                                                    phrases)])[0]
+        cpu = {"value": round(lens[0] / SR / el_cpu, 3), "unit": "audio-sec/sec",
+               "cores": threads, "kind": "port", "repeats": 1,
+               "sample": f"the first planner chunk ({lens[0] / SR:.1f} s): oracle fbank once, "
+                         f"30M and 68M torch fp32 encoders + the reference search (beam {beam}"
+                         f"{' + hotwords' if phrases else ''}), words, block vote ({nw} words); "
+                         f"{threads} threads, one timed pass after a warm-up"}
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
-    beam = args.beam
     recs, recds, cfgs = [], [], []
     for name, seed in (("zipformer-30m", WEIGHT_SEED + 1), ("zipformer-68m", WEIGHT_SEED)):
         cfg = PRESETS[name]()
-        hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
         hotwords = load_hotwords(hw_path, cfg.vocab_size) if hw_path else None
         mdir = os.path.join(tempfile.gettempdir(), f"zasr_rover_{name}_{os.getpid()}")
         toks = synth_tokens(cfg.vocab_size)
@@ -740,16 +871,8 @@ def bench_rover(args):
                                device_id=local, precision=args.precision))
         recds.append({"id2token": dict(enumerate(toks)), "vocab_size": cfg.vocab_size})
         cfgs.append(cfg)
-    chunks = make_chunks(args.audio_sec, AUDIO_SEED + rank)
-    lens = [c.shape[0] for c in chunks]
-    offs = np.cumsum([0] + lens[:-1]).tolist()
     d_wav = torch.from_numpy(np.concatenate(chunks)).cuda()
     torch.cuda.synchronize()
-    phrases = []
-    if args.hotwords_file:
-        from zasr.hotword_context import parse_hotwords_file
-        hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
-        phrases = [p for p, _ in parse_hotwords_file(hw_path, 1.5)]
     last = {}
 
     def steps(k):
@@ -803,7 +926,7 @@ def bench_rover(args):
                              "achieved": round(fl / t_step / 1e12, 2), "peak": peak,
                              "frac": round(fl / t_step / 1e12 / peak, 4),
                              "flops_per_step": fl},
-                "cpu_baseline": None}
+                "cpu_baseline": cpu}
         print(json.dumps(line))
         if args.profile_out:
             with open(args.profile_out, "w") as f:
