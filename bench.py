@@ -96,10 +96,16 @@ def parse_args(argv=None):
                     help="VAD stage: the hour split into this many files decoded in one call "
                          "(1 = the reference's single-file case; the recurrence is one "
                          "workgroup per file)")
-    ap.add_argument("--rover-sub-batches", type=int, default=2,
+    ap.add_argument("--rover-sub-batches", type=int, default=1,
                     help="ROVER stage: each model decodes the hour as this many pipelined batches "
                          "(measured 1 / 2 / 4 / 8: 143 / 136 / 171 / 245 ms per hour: every batch "
                          "adds a frame chain as long as its longest chunk)")
+    ap.add_argument("--rover-passes-per-call", type=int, default=4,
+                    help="ROVER stage: hours per decode call (consecutive batches of one call "
+                         "share the batch pipeline, beam search with two searches in flight; the "
+                         "vote of a call's hours overlaps the next call's decode).  Measured "
+                         "(sub-batches, hours per call) = (2, 1) / (1, 2) / (1, 4) / (2, 2): "
+                         "25.7k / 27.0k / 29.1k / 23.5k xRT (profiles/r02/rover)")
     ap.add_argument("--campp-batch", type=int, default=4096,
                     help="CAM++ windows per launch group (the reference batches 32 on CPU; "
                          "measured 512 -> 6000: 167 -> 123 ms per hour, profiles/r02/campp_batch)")
@@ -877,7 +883,8 @@ def bench_rover(args):
 
     def steps(k):
         r = rover_device_many(recs[0], recs[1], recds[0], recds[1], d_wav.data_ptr(), offs, lens,
-                              k, beam, phrases, args.rover_sub_batches)[-1]
+                              k, beam, phrases, args.rover_sub_batches,
+                              args.rover_passes_per_call)[-1]
         last.update(words=len(r[0]), disagree_blocks=sum(r[1]), tokens_a=r[2], tokens_b=r[3])
 
     if args.warmup:
@@ -916,6 +923,7 @@ def bench_rover(args):
                                        f"{' + hotwords' if phrases else ''}, 1 h of planner "
                                        f"chunks, block vote + overlap merge",
                            "chunks_per_gpu": len(lens), "sub_batches": args.rover_sub_batches,
+                           "passes_per_call": args.rover_passes_per_call,
                            "words": last["words"],
                            "disagreeing_blocks": last["disagree_blocks"],
                            "tokens_30m": last["tokens_a"], "tokens_68m": last["tokens_b"],

@@ -155,49 +155,56 @@ def decode_chunks_rover(rec_a, rec_b, chunks, time_offsets, hotword_phrases: Seq
 
 
 def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths, k: int,
-                      beam: int, hotword_phrases: Sequence[str] = (), sub_batches: int = 1):
+                      beam: int, hotword_phrases: Sequence[str] = (), sub_batches: int = 1,
+                      passes_per_call: int = 1):
     """k passes of one file's chunk plan (waveforms in HBM) through the ROVER pair on one GPU
     (BASELINE config 4): model A (primary, 30M) and model B (68M) decode every chunk
     (`zasr_decode_device`, each on its own engine streams, concurrently: two worker threads,
     the GIL is released inside the ctypes calls), then the per-chunk block vote and the
-    chunk-overlap merge on the host -- while the GPU already decodes the next pass.
+    chunk-overlap merge on the host -- while the GPU already decodes the next passes.
     Reference: core/asr_engine.py:2018-2047 (the pair), :2346-2350 (both models per chunk),
     :1446-1577 (vote), :182-237 (merge).  The reference shares one fbank per chunk to save CPU
     time; here each engine computes it on the device from the same audio (bit-identical
-    features, ~1 ms per hour).  sub_batches > 1: each model decodes the pass as that many
-    consecutive batches through its batch pipeline (zasr_decode_device_batches: the next
-    batch's encoder under this batch's search), results identical.  Returns [(merged words,
-    disagreements per chunk, tokens of A, tokens of B)] per pass."""
+    features, ~1 ms per hour).  Each decode call takes `passes_per_call` passes, each pass
+    `sub_batches` consecutive batches, through the engine's batch pipeline
+    (zasr_decode_device_batches: the next batch's encoder under this batch's search; beam
+    search keeps two batches' searches in flight), results identical.  Returns [(merged
+    words, disagreements per chunk, tokens of A, tokens of B)] per pass."""
     from concurrent.futures import ThreadPoolExecutor
 
     from zasr.asr_engine import result_words
     from zasr.merge import merge_chunks_with_overlap
     offsets, lengths = list(offsets), list(lengths)
+    n = len(lengths)
+    nb = max(1, min(int(sub_batches), n))
+    sizes = [n * (i + 1) // nb - n * i // nb for i in range(nb)]
+    g = max(1, int(passes_per_call))
 
-    nb = max(1, min(int(sub_batches), len(lengths)))
-    sizes = [len(lengths) * (i + 1) // nb - len(lengths) * i // nb for i in range(nb)]
-
-    def dec(h):
-        if nb == 1:
+    def dec(h, passes):
+        if nb == 1 and passes == 1:
             return h.decode_device(d_wav, offsets, lengths, beam=beam)
-        return h.decode_device_batches(d_wav, offsets, lengths, sizes, beam=beam)
+        return h.decode_device_batches(d_wav, offsets * passes, lengths * passes, sizes * passes,
+                                       beam=beam)
 
+    calls = [min(g, k - i) for i in range(0, k, g)]
     out = []
     with ThreadPoolExecutor(2) as ex:
-        fa, fb = ex.submit(dec, rec_a), ex.submit(dec, rec_b)
-        for i in range(k):
-            ra, rb = fa.result(), fb.result()
-            if i + 1 < k:
-                fa, fb = ex.submit(dec, rec_a), ex.submit(dec, rec_b)
-            chunks, dis = [], []
-            for a, b, off, n in zip(ra, rb, offsets, lengths):
-                t0 = off / 16000.0
-                merged, d = rover_merge(result_words(recd_a, a, n, t0), result_words(recd_b, b, n, t0),
-                                        hotword_phrases)
-                chunks.append({"words": merged, "audio_start_abs": t0,
-                               "audio_end_abs": (off + n) / 16000.0})
-                dis.append(len(d))
-            words, _ = merge_chunks_with_overlap(chunks)
-            out.append((words, dis, sum(int(x.token_ids.size) for x in ra),
-                        sum(int(x.token_ids.size) for x in rb)))
+        fa, fb = ex.submit(dec, rec_a, calls[0]), ex.submit(dec, rec_b, calls[0])
+        for ci, passes in enumerate(calls):
+            ra_all, rb_all = fa.result(), fb.result()
+            if ci + 1 < len(calls):
+                fa, fb = ex.submit(dec, rec_a, calls[ci + 1]), ex.submit(dec, rec_b, calls[ci + 1])
+            for p in range(passes):
+                ra, rb = ra_all[p * n:(p + 1) * n], rb_all[p * n:(p + 1) * n]
+                chunks, dis = [], []
+                for a, b, off, ln in zip(ra, rb, offsets, lengths):
+                    t0 = off / 16000.0
+                    merged, d = rover_merge(result_words(recd_a, a, ln, t0),
+                                            result_words(recd_b, b, ln, t0), hotword_phrases)
+                    chunks.append({"words": merged, "audio_start_abs": t0,
+                                   "audio_end_abs": (off + ln) / 16000.0})
+                    dis.append(len(d))
+                words, _ = merge_chunks_with_overlap(chunks)
+                out.append((words, dis, sum(int(x.token_ids.size) for x in ra),
+                            sum(int(x.token_ids.size) for x in rb)))
     return out

@@ -293,6 +293,8 @@ def test_rover_device_passes_equal_host_route(m_case, s_case):
     passes = rover_device_many(ra["handle"], rb["handle"], ra, rb, d.data_ptr(), poffs, lens, 2, 8)
     passes += rover_device_many(ra["handle"], rb["handle"], ra, rb, d.data_ptr(), poffs, lens, 2,
                                 8, sub_batches=2)
+    passes += rover_device_many(ra["handle"], rb["handle"], ra, rb, d.data_ptr(), poffs, lens, 3,
+                                8, passes_per_call=2)
     for words, dis, ta, tb in passes:
         assert [w["text"] for w in words] == [w["text"] for w in ref2]
         assert [w["start"] for w in words] == [w["start"] for w in ref2]
