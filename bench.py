@@ -101,7 +101,7 @@ def parse_args(argv=None):
                          "(measured 1 / 2 / 4 / 8: 143 / 136 / 171 / 245 ms per hour: every batch "
                          "adds a frame chain as long as its longest chunk)")
     ap.add_argument("--rover-passes-per-call", type=int, default=4,
-                    help="ROVER stage: hours per decode call (consecutive batches of one call "
+                    help="ROVER and pipe stages: hours per decode call (consecutive batches of one call "
                          "share the batch pipeline, beam search with two searches in flight; the "
                          "vote of a call's hours overlaps the next call's decode).  Measured "
                          "(sub-batches, hours per call) = (2, 1) / (1, 2) / (1, 4) / (2, 2): "
@@ -699,7 +699,7 @@ def bench_pipe(args):
 
     def steps(k):
         # k steps = k passes of the hour through the pipe, pipelined (FullPipe.run_many)
-        r = pipe.run_many(k)[-1]
+        r = pipe.run_many(k, args.rover_passes_per_call)[-1]
         out.update(windows=len(r["windows"]), words=len(r["words"]), chunks=len(r["labels"]),
                    vibert_runs=r["vibert_runs"], tokens=r["tokens"])
 

@@ -162,9 +162,16 @@ class FullPipe:
         self.d_emb = torch.empty((self.cap, self.emb.dim), dtype=torch.float32, device="cuda")
         self.s_campp = torch.cuda.Stream()
 
-    def decode(self, stream: int):
-        return self.rec.decode_device(self.d_audio.data_ptr(), self.c_off, self.c_len,
-                                      beam=self.beam, stream=stream)
+    def decode(self, stream: int, passes: int = 1):
+        """Results of `passes` decodes of the file's chunks (one call: consecutive batches
+        through the engine's batch pipeline when passes > 1), chunk order, pass after pass."""
+        if passes == 1:
+            return self.rec.decode_device(self.d_audio.data_ptr(), self.c_off, self.c_len,
+                                          beam=self.beam, stream=stream)
+        n = len(self.c_len)
+        return self.rec.decode_device_batches(self.d_audio.data_ptr(), self.c_off * passes,
+                                              self.c_len * passes, [n] * passes,
+                                              beam=self.beam, stream=stream)
 
     def words(self, res) -> Tuple[List[Dict], int]:
         from zasr.asr_engine import result_words
@@ -190,30 +197,35 @@ class FullPipe:
     def run(self) -> Dict:
         return self.run_many(1)[0]
 
-    def run_many(self, k: int) -> List[Dict]:
+    def run_many(self, k: int, passes_per_call: int = 1) -> List[Dict]:
         """k passes of the file through the pipe (k files of a job, here the same audio),
-        pipelined: the decode of pass i + 1 (a ctypes call on a worker thread: the GIL is
-        released while the GPU decodes) runs while this thread post-processes pass i's words,
-        merges them and runs its punctuation; CAM++ runs on its own stream beside both."""
+        pipelined: the decode of the next passes (a ctypes call on a worker thread: the GIL is
+        released while the GPU decodes; `passes_per_call` passes per call share the engine's
+        batch pipeline) runs while this thread post-processes a pass's words, merges them and
+        runs its punctuation; CAM++ runs on its own stream beside both."""
         import torch
         from concurrent.futures import ThreadPoolExecutor
         main = torch.cuda.current_stream()
+        n = len(self.c_len)
+        g = max(1, int(passes_per_call))
+        calls = [min(g, k - i) for i in range(0, k, g)]
         outs: List[Dict] = []
         with ThreadPoolExecutor(1) as ex:
-            fut = ex.submit(self.decode, main.cuda_stream)
-            for i in range(k):
-                self.s_campp.wait_stream(main)
-                # CAM++ on its own stream: it reads only the audio
-                reg, first, nfr = self.embed_windows(self.s_campp.cuda_stream)
-                res = fut.result()
-                if i + 1 < k:
-                    fut = ex.submit(self.decode, main.cuda_stream)
-                words, tokens = self.words(res)
-                labels, runs = punctuate(self.vib, [w["text"] for w in words], self.vib_vocab,
-                                         self.iterations, self.vib_batch)
-                self.s_campp.synchronize()
-                embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
-                outs.append({"words": words, "tokens": tokens, "labels": labels,
-                             "vibert_runs": runs, "embeddings": embs,
-                             "windows": np.stack([reg, first, nfr], 1)})
+            fut = ex.submit(self.decode, main.cuda_stream, calls[0])
+            for ci, passes in enumerate(calls):
+                res_all = fut.result()
+                if ci + 1 < len(calls):
+                    fut = ex.submit(self.decode, main.cuda_stream, calls[ci + 1])
+                for p in range(passes):
+                    self.s_campp.wait_stream(main)
+                    # CAM++ on its own stream: it reads only the audio
+                    reg, first, nfr = self.embed_windows(self.s_campp.cuda_stream)
+                    words, tokens = self.words(res_all[p * n:(p + 1) * n])
+                    labels, runs = punctuate(self.vib, [w["text"] for w in words],
+                                             self.vib_vocab, self.iterations, self.vib_batch)
+                    self.s_campp.synchronize()
+                    embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
+                    outs.append({"words": words, "tokens": tokens, "labels": labels,
+                                 "vibert_runs": runs, "embeddings": embs,
+                                 "windows": np.stack([reg, first, nfr], 1)})
         return outs

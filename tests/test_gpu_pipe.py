@@ -113,7 +113,7 @@ def test_vibert_whole_pass_equals_reference_mini_batches(pipe):
 
 def test_pipelined_passes_equal_single_pass(pipe):
     p, audio, out, _ = pipe
-    outs = p.run_many(3)
+    outs = p.run_many(3) + p.run_many(3, passes_per_call=2)
     for o in outs:
         assert [w["text"] for w in o["words"]] == [w["text"] for w in out["words"]]
         assert np.array_equal(o["embeddings"], out["embeddings"])
