@@ -117,8 +117,13 @@ int main() {
     for (auto& s : shapes) {
       if (s.epi == EPI_RESADD)
         run_variant<32, __bf16, float, EPI_RESADD>(deep ? "deep bf16A f32C" : "base bf16A f32C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
-      else
+      else {
         run_variant<32, float, __bf16, EPI_NONE>(deep ? "deep f32A bf16C" : "base f32A bf16C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
+        // the same projection from a bf16 copy of A (what a bf16 shadow of the residual
+        // stream, written by its producer, would feed)
+        if (deep)
+          run_variant<32, __bf16, __bf16, EPI_NONE>("deep bf16A bf16C", s, dA, dA16, dB, dC, dC16, dbias, hA, hB, hbias);
+      }
     }
   }
   return 0;
