@@ -359,7 +359,10 @@ __device__ __forceinline__ float epi_act(float v) {
 
 template <int BM, int BN, int BK, int WAVES_M, int WAVES_N, int ALOAD, int EPI, typename TA,
           typename TC, bool DEEP>
-__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmParams p,
+// 8-wave tiles: hold 4 waves per SIMD (<= 128 VGPRs, two blocks per CU); at 130 VGPRs the
+// f32-A variants drop to one block per CU (tools/gemm_bench: 53 -> 64 us)
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N)
+__attribute__((amdgpu_waves_per_eu(WAVES_M * WAVES_N >= 8 ? 4 : 1))) void gemm_bf16_kernel(GemmParams p,
                                                                           const __bf16* Bw,
                                                                           int tiles_n,
                                                                           int tiles_m) {
@@ -377,8 +380,14 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
   constexpr int B_LD = (B_G + NT - 1) / NT;
   constexpr int STAGE = (BM + BN) * LDH;  // bf16 elements
   constexpr int LDE = 40;                 // epilogue fragment row stride (floats)
+  // bf16 C without side inputs: two adjacent 32x32 fragments go through LDS together so that
+  // every row segment is one 128-byte line written by 8 lanes x 16 bytes (one fragment alone
+  // gives 64-byte half lines of 8-byte stores)
+  constexpr bool PAIR = std::is_same<TC, __bf16>::value && FN % 2 == 0 && EPI != EPI_MULAUX &&
+                        EPI != EPI_MULAUX16 && EPI != EPI_RESADD && BM <= 128;
+  constexpr int LDE2 = 72;                // paired epilogue row stride (floats)
   constexpr int OPER_BYTES = 2 * STAGE * 2;
-  constexpr int EPI_BYTES = (NT / 64) * 32 * LDE * 4;
+  constexpr int EPI_BYTES = (NT / 64) * 32 * (PAIR ? LDE2 : LDE) * 4;
   constexpr int LDS_BYTES = OPER_BYTES > EPI_BYTES ? OPER_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   __bf16* const sbase = reinterpret_cast<__bf16*>(smem);
@@ -610,6 +619,52 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_bf16_kernel(GemmPa
   }
   }
 
+  if constexpr (PAIR) {
+    if (N % 8 == 0 && p.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0) {
+      float* sP = reinterpret_cast<float*>(smem) + wid * (32 * LDE2);
+      const int c8 = lane & 7;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; j += 2) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              sP[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE2 + 32 * h + (lane & 31)] =
+                  acc[i][j + h][r];
+          __builtin_amdgcn_wave_barrier();
+          const int col = n0 + wn * WTN + j * 32 + 8 * c8;
+          float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+          if (p.bias && col < N) {
+            b0 = *reinterpret_cast<const float4*>(p.bias + col);
+            b1 = *reinterpret_cast<const float4*>(p.bias + col + 4);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rl = (lane >> 3) + 8 * q;
+            const int row = m0 + wm * WTM + i * 32 + rl;
+            const float4 v0 = *reinterpret_cast<const float4*>(&sP[rl * LDE2 + 8 * c8]);
+            const float4 v1 = *reinterpret_cast<const float4*>(&sP[rl * LDE2 + 8 * c8 + 4]);
+            if (row < M && col < N) {
+              bf16x8 hv;
+              hv[0] = (__bf16)epi_act<EPI>(fmaf(v0.x, p.alpha, b0.x));
+              hv[1] = (__bf16)epi_act<EPI>(fmaf(v0.y, p.alpha, b0.y));
+              hv[2] = (__bf16)epi_act<EPI>(fmaf(v0.z, p.alpha, b0.z));
+              hv[3] = (__bf16)epi_act<EPI>(fmaf(v0.w, p.alpha, b0.w));
+              hv[4] = (__bf16)epi_act<EPI>(fmaf(v1.x, p.alpha, b1.x));
+              hv[5] = (__bf16)epi_act<EPI>(fmaf(v1.y, p.alpha, b1.y));
+              hv[6] = (__bf16)epi_act<EPI>(fmaf(v1.z, p.alpha, b1.z));
+              hv[7] = (__bf16)epi_act<EPI>(fmaf(v1.w, p.alpha, b1.w));
+              *reinterpret_cast<bf16x8*>(C + (long)row * p.ldc + col) = hv;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      return;
+    }
+  }
   // epilogue: fragment -> LDS (lane: column lane&31, rows (r&3)+8(r>>2)+4(lane>>5)) ->
   // float4 rows (8 lanes per 32-column row)
   float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
