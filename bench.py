@@ -66,7 +66,7 @@ def parse_args(argv=None):
     ap.add_argument("--method", default="greedy_search")
     ap.add_argument("--beam", type=int, default=8)
     ap.add_argument("--audio-sec", type=float, default=3600.0)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32", "bf16x3"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5,
                     help="CPU baseline: 1 warm-up then the mean of this many repeats "

@@ -263,8 +263,9 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
                const std::vector<std::vector<int>>& hotwords, const std::vector<float>& hotword_scores,
                int precision)
     : device_(device), beam_(beam), greedy_(greedy), precision_(precision) {
-  ZASR_REQUIRE(precision >= 0 && precision <= 2,
-               "precision must be 0 (fp32), 1 (bf16) or 2 (bf16 encoder, f32 joiner + search)");
+  ZASR_REQUIRE(precision >= 0 && precision <= 3,
+               "precision must be 0 (fp32), 1 (bf16), 2 (bf16 encoder, f32 joiner + search) or 3 "
+               "(bf16x3: split-bf16 products, f32 storage)");
   // host side first (no GPU state to unwind when the files are bad): config.json +
   // model.safetensors, or the reference's encoder-/decoder-/joiner-*.onnx (onnx_io.h;
   // core/asr_engine.py:913-928)
@@ -459,7 +460,29 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
   model_.dec_proj = lin("decoder_proj", cfg.joiner_dim, D);
   model_.joiner = lin("joiner.output_linear", cfg.V, cfg.joiner_dim);
   ensure_pos_tables(2048);
-  if (precision_ != 0) {  // bf16 copies of every dense projection weight
+  if (precision_ == 3) {  // split-bf16 (hi, lo) copies of every encoder projection weight
+    auto mkx = [&](DLin& l) {
+      void* p = nullptr;
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 4));
+      model_.allocations.push_back(p);
+      split_to_bf16(l.w, p, reinterpret_cast<__bf16*>(p) + (size_t)l.N * l.K, (long)l.N * l.K,
+                    stream_);
+      l.wx = p;
+    };
+    for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
+                    &model_.enc_proj})
+      mkx(*l);
+    for (auto& s : model_.stacks)
+      for (auto& L : s.layers) {
+        for (DLin* l : {&L.attn_in, &L.na_in, &L.na_out}) mkx(*l);
+        for (int a = 0; a < 2; ++a)
+          for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mkx(*l);
+        for (int a = 0; a < 3; ++a)
+          for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mkx(*l);
+      }
+    ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  if (precision_ == 1 || precision_ == 2) {  // bf16 copies of every dense projection weight
     auto mk = [&](DLin& l) {
       void* p = nullptr;
       ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2));
@@ -791,7 +814,9 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
     prof_begin(shape_key(cls, M, l.K, l.N, l.wh != nullptr, false, false, epi));
   else
     prof_begin(cls);
-  if (l.wh)
+  if (l.wx)
+    gemm_x3(p, l.wx, (long)l.N * l.K, epi, ALOAD_DENSE, st_);
+  else if (l.wh)
     gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_);
   else
     gemm_f32(p, epi, ALOAD_DENSE, false, st_);
@@ -888,7 +913,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   if (!orig_ready)  // else the previous layer's BiasNorm already wrote src here
     ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
   // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
-  const bool bf16 = precision_ != 0;
+  const bool bf16 = precision_ == 1 || precision_ == 2;
   float* qkp = nullptr;
   float* A = nullptr;
   __bf16* A16 = nullptr;
@@ -1086,7 +1111,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   std::vector<std::vector<GemmSlice>> sl_nl(ns);
   std::vector<std::vector<int>> o8(ns);
   std::vector<int> R8(ns, 0);
-  const bool bf16 = precision_ != 0;
+  const bool bf16 = precision_ == 1 || precision_ == 2;
   size_t attn_floats = 0;
   int maxL_all = 0;
   for (int i = 0; i < ns; ++i) {
@@ -1184,6 +1209,8 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     prof_begin("frontend_conv");
     if (fe16)
       gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_, true, true);
+    else if (model_.conv4.wx)
+      gemm_x3(p, model_.conv4.wx, 32L * 72, EPI_SWOOSHR, ALOAD_CONV2, st_);
     else if (model_.conv4.wh)
       gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_);
     else
@@ -1223,7 +1250,10 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       float* x3 = ws<float>("fe_x3", (size_t)mL.total * 19 * 128);
       p.C = x3;
       prof_begin("frontend_conv");
-      gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
+      if (model_.conv7.wx)
+        gemm_x3(p, model_.conv7.wx, 128L * 288, EPI_SWOOSHR, ALOAD_CONV3, st_);
+      else
+        gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
       prof_end();
       float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
       prof_begin("frontend_conv");

@@ -32,6 +32,7 @@ struct DLin {
   void* wh = nullptr;  // bf16 copy of w (precision mode bf16)
   float* bh = nullptr; // bias of the bf16 path when it differs from b (folded row scales)
   void* wp = nullptr;  // bf16 in MFMA-fragment order (ffn_pack_host), the wide fused FFN's operand
+  void* wx = nullptr;  // split bf16 of w (precision mode bf16x3): hi [N][K], then lo [N][K]
 };
 
 struct DLayer {

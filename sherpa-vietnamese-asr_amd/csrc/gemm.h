@@ -105,6 +105,14 @@ void gemm_rp_pack_weights(const void* W_bf16, int N, int K, void* out, hipStream
 bool gemm_rp(const void* A, bool a_bf16, int lda, const void* Bp, const float* bias, void* C,
              bool c_bf16, int ldc, int M, int N, int K, int epi, hipStream_t stream);
 
+// Split-bf16 variant (gemm_x3.hip, the "bf16x3" precision mode): A f32 (dense, or the
+// implicit-im2col loaders ALOAD_CONV2 / ALOAD_CONV3), W = hi [N][K] bf16 at Bw and lo at
+// Bw + b_lo elements (split_to_bf16); C f32.  Epilogues NONE, SWOOSHL, SWOOSHR, RESADD,
+// MULAUX (f32 aux).  N, ldc (and ldaux) multiples of 4; K a multiple of 8 for dense A.
+void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t stream);
+// hi[i] = bf16(src[i]), lo[i] = bf16(src[i] - hi[i])
+void split_to_bf16(const float* src, void* hi, void* lo, long n, hipStream_t stream);
+
 // device f32 -> bf16 (round to nearest even) copy
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t stream);
 // dst[r][k] = bf16(src[r][k] * row_scale[r]) (one rounding), src / dst [N][K]

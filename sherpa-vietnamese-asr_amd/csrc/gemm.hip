@@ -11,56 +11,13 @@
 
 #include "common.h"
 #include "gemm.h"
+#include "gemm_dev.h"
 
 namespace zasr {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
 constexpr int BK = 16;
-
-// A operand, 4 consecutive k of row gm.  Loads are unconditional (clamped into the valid
-// range, zero selected afterwards): a guarded load compiles to a branch with a vmcnt(0) wait,
-// which serialises the tile's memory round trips.  Requires M >= 1 and K % 4 == 0.
-template <int ALOAD>
-__device__ __forceinline__ float4 load_a4(const GemmParams& p, const float* A, int M, int K,
-                                          int lda, int gm, int gk) {
-  const bool ok = gm < M && gk < K;
-  const int m = gm < M ? gm : M - 1;
-  const int k = gk < K ? gk : K - 4;
-  float4 v;
-  if constexpr (ALOAD == ALOAD_DENSE) {
-    v = *reinterpret_cast<const float4*>(A + (long)m * lda + k);
-  } else if constexpr (ALOAD == ALOAD_CONV2) {
-    // out (t, f) of conv.4; k = (kt*3 + kf)*8 + c over conv1 output [T1][80][8]
-    const int t = m / 39, f = m - t * 39;
-    const int kk = k >> 3, c = k & 7;
-    const int kt = kk / 3, kf = kk - kt * 3;
-    v = *reinterpret_cast<const float4*>(A + ((long)(2 * t + kt) * 80 + 2 * f + kf) * 8 + c);
-  } else if constexpr (ALOAD == ALOAD_CONV3) {
-    // out (t, f) of conv.7; k = (kt*3 + kf)*32 + c over conv2 output [L2][39][32]
-    const int t = m / 19, f = m - t * 19;
-    const int kk = k >> 5, c = k & 31;
-    const int kt = kk / 3, kf = kk - kt * 3;
-    v = *reinterpret_cast<const float4*>(A + ((long)(t + kt) * 39 + 2 * f + kf) * 32 + c);
-  } else if constexpr (ALOAD == ALOAD_BNRELU) {
-    v = *reinterpret_cast<const float4*>(A + (long)m * lda + k);
-    const float4 s = *reinterpret_cast<const float4*>(p.a_scale + k);
-    const float4 b = *reinterpret_cast<const float4*>(p.a_shift + k);
-    v = make_float4(fmaxf(fmaf(v.x, s.x, b.x), 0.f), fmaxf(fmaf(v.y, s.y, b.y), 0.f),
-                    fmaxf(fmaf(v.z, s.z, b.z), 0.f), fmaxf(fmaf(v.w, s.w, b.w), 0.f));
-  } else {  // ALOAD_IM2COL1D
-    const GemmIm2col1d& g = p.i2c;
-    const int n = m / g.Tout, t = m - n * g.Tout;
-    const int q = k / g.C, c = k - q * g.C;
-    const int ts = t * g.stride + q * g.dil - g.pad;
-    const bool in = ts >= 0 && ts < g.Tin;
-    v = *reinterpret_cast<const float4*>(A + ((long)n * g.Tin + (in ? ts : 0)) * lda + c);
-    return (ok && in) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-}
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, bool BNC, int EPI, bool DEEP>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmParams p) {
@@ -304,8 +261,6 @@ void launch_tile(const GemmParams& p, hipStream_t st) {
 // land on the same XCD (blocks are dealt round-robin over the 8 XCDs, each with its own L2):
 // A is fetched from HBM once, not once per N tile.
 // ---------------------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 template <int ALOAD, typename TA>
 __device__ __forceinline__ bf16x8 load_a8(const GemmParams& p, const TA* A, int M, int K, int lda,
@@ -341,13 +296,6 @@ __device__ __forceinline__ bf16x8 load_a8(const GemmParams& p, const TA* A, int 
     v[4] = (__bf16)x1.x; v[5] = (__bf16)x1.y; v[6] = (__bf16)x1.z; v[7] = (__bf16)x1.w;
   }
   return v;
-}
-
-// logical tile of this block (see header comment): XCD x owns tiles [x*per + min(x, rem) ...)
-__device__ __forceinline__ int xcd_tile(int b, int nb) {
-  const int per = nb >> 3, rem = nb & 7;
-  const int xcd = b & 7, slot = b >> 3;
-  return xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
 }
 
 template <int EPI>

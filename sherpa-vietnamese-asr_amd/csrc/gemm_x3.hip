@@ -1,0 +1,400 @@
+// Split-bf16 ("bf16x3") MFMA GEMM: near-f32 products at bf16 MFMA rates.
+//
+//   C[m, n] = epi( sum_k A[m, k] * W[n, k] + bias[n] )
+//
+// Each f32 operand x is carried as two bf16 numbers, hi = bf16(x) and lo = bf16(x - hi)
+// (x - hi - lo is below 2^-17 |x|).  The product is accumulated as
+//   a_lo * w_hi + a_hi * w_lo + a_hi * w_hi
+// in f32 on v_mfma_f32_32x32x16_bf16 -- three MFMAs where the bf16 mode issues one; the
+// dropped a_lo * w_lo term and the two residuals leave a relative product error of ~2^-16
+// (bf16 alone: 2^-8).  The weights are split once at load (hi [N][K] then lo [N][K]); the
+// f32 activations are split while staging into LDS.  The encoder's projections are
+// HBM-bound with the MFMA pipes ~0.13 busy in the bf16 mode (profiles/r02/prof_r02e), so the
+// extra MFMAs mostly fill idle issue slots.  tests/precision_sim.py: the 68M model in this
+// mode decodes token-for-token like the fp32 oracle on test_gpu_e2e's chunks (bf16: TER 0.12).
+//
+// Structure follows gemm_bf16_kernel (gemm.hip): BM x BN block tile on 4 waves, BK = 32
+// slabs staged through LDS as row-major [row][BK + 8] bf16 images (hi and lo of A and of W),
+// two LDS stages, next slab's global loads in registers under the MFMAs (two register sets
+// when K is a multiple of 64), tiles numbered so that blocks sharing an A row panel land on
+// one XCD, epilogue through LDS as float4 rows.
+#include <type_traits>
+
+#include "common.h"
+#include "gemm.h"
+#include "gemm_dev.h"
+
+namespace zasr {
+namespace {
+
+__device__ __forceinline__ void split8(const float4 x0, const float4 x1, bf16x8& hi, bf16x8& lo) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const __bf16 h = (__bf16)v[q];
+    hi[q] = h;
+    lo[q] = (__bf16)(v[q] - (float)h);
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ float x3_act(float v) {
+  if constexpr (EPI == EPI_SWOOSHL) return swooshl(v);
+  if constexpr (EPI == EPI_SWOOSHR) return swooshr(v);
+  return v;
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP>
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmParams p,
+                                                                       const __bf16* Bw, long blo,
+                                                                       int tiles_n, int tiles_m) {
+  constexpr int BK = 32;
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WTM = BM / WAVES_M;
+  constexpr int WTN = BN / WAVES_N;
+  constexpr int FM = WTM / 32;
+  constexpr int FN = WTN / 32;
+  static_assert(FM >= 1 && FN >= 1, "wave tile must be a multiple of 32x32");
+  constexpr int LDH = BK + 8;
+  constexpr int GPR = BK / 8;
+  constexpr int A_G = BM * GPR;
+  constexpr int B_G = BN * GPR;
+  constexpr int A_LD = (A_G + NT - 1) / NT;
+  constexpr int B_LD = (B_G + NT - 1) / NT;
+  // stage: A hi [BM][LDH], A lo, W hi [BN][LDH], W lo
+  constexpr int STAGE = 2 * (BM + BN) * LDH;
+  constexpr int LDE = 40;
+  constexpr int OPER_BYTES = 2 * STAGE * 2;
+  constexpr int EPI_BYTES = (NT / 64) * 32 * LDE * 4;
+  constexpr int LDS_BYTES = OPER_BYTES > EPI_BYTES ? OPER_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  __bf16* const sbase = reinterpret_cast<__bf16*>(smem);
+
+  const float* A = p.A;
+  float* C = p.C;
+  const float* aux = p.aux;
+  int M = p.M, K = p.K, lda = p.lda;
+  long b_off = 0;
+  const int tiles = tiles_n * tiles_m;
+  const int lin = xcd_tile(blockIdx.x, gridDim.x);
+  const int zs = lin / tiles;
+  if (p.slices) {
+    const GemmSlice s = p.slices[zs];
+    A += s.a_off;
+    b_off = s.b_off;
+    C += s.c_off;
+    if (aux) aux += s.aux_off;
+    M = s.M;
+    K = s.K;
+    lda = s.lda;
+  }
+  const __bf16* B = Bw + b_off;
+  const int tile = lin - zs * tiles;
+  const int m_tile = tile / tiles_n;
+  const int m0 = m_tile * BM;
+  if (m0 >= M) return;
+  const int n0 = (tile - m_tile * tiles_n) * BN;
+  const int N = p.N;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WAVES_N;
+  const int wn = wid - wm * WAVES_N;
+
+  // k-invariant per-thread row pointers of the dense fast path (rows past M / N clamped)
+  const float* arow[A_LD];
+  const __bf16* brow[B_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int idx = tid + NT * i;
+    const int row = (idx < A_G ? idx : 0) / GPR, k8 = idx % GPR;
+    const int gm = m0 + row < M ? m0 + row : M - 1;
+    arow[i] = A + (long)gm * lda + 8 * k8;
+  }
+#pragma unroll
+  for (int i = 0; i < B_LD; ++i) {
+    const int idx = tid + NT * i;
+    const int n = (idx < B_G ? idx : 0) / GPR, k8 = idx % GPR;
+    const int gn = n0 + n < N ? n0 + n : N - 1;
+    brow[i] = B + (long)gn * p.sbn + 8 * k8;
+  }
+
+  struct Regs {
+    float4 a0[A_LD], a1[A_LD];
+    bf16x8 bh[B_LD], bl[B_LD];
+  };
+  auto gload = [&](Regs& r, int kt) {
+    const int k0 = kt * BK;
+    if (ALOAD == ALOAD_DENSE && (DEEP || k0 + BK <= K)) {
+#pragma unroll
+      for (int i = 0; i < A_LD; ++i) {
+        r.a0[i] = *reinterpret_cast<const float4*>(arow[i] + k0);
+        r.a1[i] = *reinterpret_cast<const float4*>(arow[i] + k0 + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < B_LD; ++i) {
+        r.bh[i] = *reinterpret_cast<const bf16x8*>(brow[i] + k0);
+        r.bl[i] = *reinterpret_cast<const bf16x8*>(brow[i] + blo + k0);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx / GPR, k8 = idx % GPR;
+      const int gm = m0 + (idx < A_G ? row : 0), gk = k0 + 8 * k8;
+      r.a0[i] = load_a4<ALOAD>(p, A, M, K, lda, gm, gk);
+      r.a1[i] = load_a4<ALOAD>(p, A, M, K, lda, gm, gk + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int idx = tid + NT * i;
+      const int n = idx / GPR, k8 = idx % GPR;
+      const int gn = n0 + n, gk = k0 + 8 * k8;
+      const bool ok = idx < B_G && gn < N && gk < K;
+      const int nc = gn < N ? gn : N - 1, kc = gk < K ? gk : K - 8;
+      bf16x8 h = *reinterpret_cast<const bf16x8*>(B + (long)nc * p.sbn + kc);
+      bf16x8 l = *reinterpret_cast<const bf16x8*>(B + blo + (long)nc * p.sbn + kc);
+      if (!ok) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) h[q] = l[q] = (__bf16)0.f;
+      }
+      r.bh[i] = h;
+      r.bl[i] = l;
+    }
+  };
+  auto sstore = [&](const Regs& r, int buf) {
+    __bf16* Ah = sbase + buf * STAGE;
+    __bf16* Al = Ah + BM * LDH;
+    __bf16* Bh = Al + BM * LDH;
+    __bf16* Bl = Bh + BN * LDH;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int idx = tid + NT * i;
+      if (idx < A_G) {
+        bf16x8 h, l;
+        split8(r.a0[i], r.a1[i], h, l);
+        const int o = (idx / GPR) * LDH + 8 * (idx % GPR);
+        *reinterpret_cast<bf16x8*>(&Ah[o]) = h;
+        *reinterpret_cast<bf16x8*>(&Al[o]) = l;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int idx = tid + NT * i;
+      if (idx < B_G) {
+        const int o = (idx / GPR) * LDH + 8 * (idx % GPR);
+        *reinterpret_cast<bf16x8*>(&Bh[o]) = r.bh[i];
+        *reinterpret_cast<bf16x8*>(&Bl[o]) = r.bl[i];
+      }
+    }
+  };
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto mma_slab = [&](int cur) {
+    const __bf16* Ah = sbase + cur * STAGE;
+    const __bf16* Al = Ah + BM * LDH;
+    const __bf16* Bh = Al + BM * LDH;
+    const __bf16* Bl = Bh + BN * LDH;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+      const int kc = ks * 16 + 8 * (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int o = (wm * WTM + i * 32 + (lane & 31)) * LDH + kc;
+        ah[i] = *reinterpret_cast<const bf16x8*>(&Ah[o]);
+        al[i] = *reinterpret_cast<const bf16x8*>(&Al[o]);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int o = (wn * WTN + j * 32 + (lane & 31)) * LDH + kc;
+        bh[j] = *reinterpret_cast<const bf16x8*>(&Bh[o]);
+        bl[j] = *reinterpret_cast<const bf16x8*>(&Bl[o]);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  const int nkt = (K + BK - 1) / BK;
+  if constexpr (DEEP) {
+    // dense A, K a multiple of 2 BK (host-checked): two register sets, LDS-only barriers
+    // (__syncthreads would drain the slab in flight with vmcnt(0)), slab indices clamped so
+    // every load is unconditional and the in-order vmcnt waits stay exact
+    Regs x0, x1;
+    auto bar = []() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    gload(x0, 0);
+    gload(x1, 1);
+    sstore(x0, 0);
+    bar();
+    for (int kt = 0; kt < nkt; kt += 2) {
+      gload(x0, min(kt + 2, nkt - 1));
+      mma_slab(0);
+      sstore(x1, 1);
+      bar();
+      gload(x1, min(kt + 3, nkt - 1));
+      mma_slab(1);
+      sstore(x0, 0);
+      bar();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    Regs r;
+    gload(r, 0);
+    sstore(r, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nkt) gload(r, kt + 1);
+      mma_slab(cur);
+      if (kt + 1 < nkt) sstore(r, cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: fragment -> LDS (lane: column lane&31, rows (r&3)+8(r>>2)+4(lane>>5)) ->
+  // float4 rows (8 lanes per 32-column row); side inputs loaded unconditionally (clamped)
+  float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
+  const int c4 = lane & 7;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sE[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE + (lane & 31)] = acc[i][j][r];
+      __builtin_amdgcn_wave_barrier();
+      const int col = n0 + wn * WTN + j * 32 + 4 * c4;
+      const int cc = col < N ? col : N - 4;
+      float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias) bias = *reinterpret_cast<const float4*>(p.bias + cc);
+      float4 side[4];
+      if constexpr (EPI == EPI_RESADD || EPI == EPI_MULAUX) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + wm * WTM + i * 32 + (lane >> 3) + 8 * q;
+          const int rc = row < M ? row : M - 1;
+          side[q] = EPI == EPI_RESADD
+                        ? *reinterpret_cast<const float4*>(C + (long)rc * p.ldc + cc)
+                        : *reinterpret_cast<const float4*>(aux + (long)rc * p.ldaux + cc);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = (lane >> 3) + 8 * q;
+        const int row = m0 + wm * WTM + i * 32 + rl;
+        float4 v = *reinterpret_cast<const float4*>(&sE[rl * LDE + 4 * c4]);
+        if (row < M && col < N) {
+          v.x = x3_act<EPI>(v.x + bias.x);
+          v.y = x3_act<EPI>(v.y + bias.y);
+          v.z = x3_act<EPI>(v.z + bias.z);
+          v.w = x3_act<EPI>(v.w + bias.w);
+          if constexpr (EPI == EPI_RESADD) {
+            v.x += side[q].x; v.y += side[q].y; v.z += side[q].z; v.w += side[q].w;
+          }
+          if constexpr (EPI == EPI_MULAUX) {
+            v.x *= side[q].x; v.y *= side[q].y; v.z *= side[q].z; v.w *= side[q].w;
+          }
+          *reinterpret_cast<float4*>(C + (long)row * p.ldc + col) = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int ALOAD, int EPI>
+void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
+  const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
+  dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
+  if (ALOAD == ALOAD_DENSE && !p.slices && p.K % 64 == 0 && p.lda % 4 == 0) {
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true>), grid,
+                       dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false>), grid,
+                     dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
+}
+
+template <int ALOAD, int EPI>
+void launch_x3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
+  // BN: the largest of {128, 64, 32} whose padded width is within 15 % of the tightest
+  const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
+  const int BN = (pad128 * 100 <= pad32 * 115) ? 128 : (pad64 * 100 <= pad32 * 115 ? 64 : 32);
+  const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
+  const bool big = blocks128 >= 512;
+  if (BN == 128) {
+    if (big) launch_x3_t<128, 128, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
+    else launch_x3_t<64, 128, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
+  } else if (BN == 64) {
+    if (big) launch_x3_t<128, 64, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
+    else launch_x3_t<64, 64, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
+  } else {
+    if (big) launch_x3_t<128, 32, 4, 1, ALOAD, EPI>(p, Bw, blo, st);
+    else launch_x3_t<64, 32, 2, 1, ALOAD, EPI>(p, Bw, blo, st);
+  }
+}
+
+__global__ void split_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ hi,
+                                  __bf16* __restrict__ lo, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const float x = src[i];
+    const __bf16 h = (__bf16)x;
+    hi[i] = h;
+    lo[i] = (__bf16)(x - (float)h);
+  }
+}
+
+}  // namespace
+
+void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t st) {
+  ZASR_REQUIRE(p.N > 0, "gemm_x3: N must be positive");
+  if (p.max_M <= 0) return;
+  ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (epi != EPI_MULAUX || p.ldaux % 4 == 0),
+               "gemm_x3: N and the C / aux row strides must be multiples of 4");
+  ZASR_REQUIRE(p.slices != nullptr || (p.K % 8 == 0 && p.lda % 4 == 0),
+               "gemm_x3: K must be a multiple of 8 and lda of 4");
+  const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
+  if (aload == ALOAD_DENSE) {
+    switch (epi) {
+      case EPI_NONE: return launch_x3<ALOAD_DENSE, EPI_NONE>(p, B, b_lo, st);
+      case EPI_SWOOSHL: return launch_x3<ALOAD_DENSE, EPI_SWOOSHL>(p, B, b_lo, st);
+      case EPI_SWOOSHR: return launch_x3<ALOAD_DENSE, EPI_SWOOSHR>(p, B, b_lo, st);
+      case EPI_RESADD: return launch_x3<ALOAD_DENSE, EPI_RESADD>(p, B, b_lo, st);
+      case EPI_MULAUX: return launch_x3<ALOAD_DENSE, EPI_MULAUX>(p, B, b_lo, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
+    return launch_x3<ALOAD_CONV2, EPI_SWOOSHR>(p, B, b_lo, st);
+  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR) {
+    return launch_x3<ALOAD_CONV3, EPI_SWOOSHR>(p, B, b_lo, st);
+  }
+  throw std::runtime_error("gemm_x3: unsupported (aload, epi) combination");
+}
+
+void split_to_bf16(const float* src, void* hi, void* lo, long n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(split_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
+                     reinterpret_cast<__bf16*>(hi), reinterpret_cast<__bf16*>(lo), n);
+}
+
+}  // namespace zasr

@@ -32,8 +32,9 @@ EXPORTS = (
 )
 
 
-# include/zasr.h ZASR_PRECISION_*: "bf16_enc" = the bf16 encoder with the f32 joiner + search
-PRECISIONS = {"fp32": 0, "bf16": 1, "bf16_enc": 2}
+# include/zasr.h ZASR_PRECISION_*: "bf16_enc" = the bf16 encoder with the f32 joiner + search;
+# "bf16x3" = f32 storage, split-bf16 (hi + lo) products on the bf16 MFMA
+PRECISIONS = {"fp32": 0, "bf16": 1, "bf16_enc": 2, "bf16x3": 3}
 
 
 class ZasrError(RuntimeError):

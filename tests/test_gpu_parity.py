@@ -83,13 +83,16 @@ def test_encoder_tiny_batched_matches_oracle(tiny):
         _enc_close(g, ref)
 
 
-def test_encoder_m_matches_oracle(need_gpu):
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3"])
+def test_encoder_m_matches_oracle(need_gpu, prec):
+    """68M encoder_out vs the oracle within 2e-3 * max(1, |ref|): exact-f32 MFMA (fp32) and
+    split-bf16 products (bf16x3, ~2^-16 relative per product)."""
     from model_fixtures import m_model
     from oracle.fbank import fbank
     from oracle.zipformer import ZipformerOracle
     from zasr.binding import Recognizer
     cfg, w, path = m_model()
-    rec = Recognizer(path, "greedy_search", 1)
+    rec = Recognizer(path, "greedy_search", 1, precision=prec)
     feats = [fbank(_speech(12.3, 5)), fbank(_speech(3.1, 6))]
     got = rec.encode_features(feats)
     orc = ZipformerOracle(cfg, w)
