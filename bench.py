@@ -66,7 +66,7 @@ def parse_args(argv=None):
     ap.add_argument("--method", default="greedy_search")
     ap.add_argument("--beam", type=int, default=8)
     ap.add_argument("--audio-sec", type=float, default=3600.0)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32", "bf16x3"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5,
                     help="CPU baseline: 1 warm-up then the mean of this many repeats "
@@ -85,13 +85,16 @@ def parse_args(argv=None):
                     help="no GPU: exercise the launcher / rank / timing / JSON path with gloo "
                          "and a CPU stand-in step (tests/test_bench_launcher.py)")
     ap.add_argument("--profile-out", default="")
-    ap.add_argument("--stage", default="asr", choices=["asr", "campp", "vad", "pipe", "rover"],
+    ap.add_argument("--stage", default="asr",
+                    choices=["asr", "campp", "vad", "pipe", "rover", "dropin"],
                     help="asr: the Zipformer decode (default, BASELINE metric); campp: the CAM++ "
                          "speaker-embedding stage of config 5 (1.5 s windows, 0.6 s step); vad: "
                          "Silero VAD probabilities + segments of the hour (core/asr_engine.py:2090); "
                          "pipe: BASELINE config 5, decode + merge + CAM++ embeddings + ViBERT "
                          "punctuation of the hour (zasr/pipeline.py); rover: BASELINE config 4, "
-                         "30M + 68M decode of the hour + block vote + merge (zasr/rover.py)")
+                         "30M + 68M decode of the hour + block vote + merge (zasr/rover.py); "
+                         "dropin: the reference's two-worker decode_chunk loop over the hour "
+                         "through the drop-in surface (plan-ahead batching, zasr/asr_engine.py)")
     ap.add_argument("--vad-files", type=int, default=1,
                     help="VAD stage: the hour split into this many files decoded in one call "
                          "(1 = the reference's single-file case; the recurrence is one "
@@ -945,6 +948,112 @@ def bench_rover(args):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------ drop-in loop
+def bench_dropin(args):
+    """The reference's transcription phase restated over the drop-in surface: the planner
+    (find_silent_regions -> ~30 s chunks with 3 s overlap, core/asr_engine.py:2137-2161; the
+    zasr.dropin hook registers the plan), TWO worker threads calling decode_chunk per chunk on
+    even / odd indices (:2326-2397; the recognizer of the reference's decode_chunk is always
+    modified beam search with max_active_paths, :1224), the timestamp map and the chunk-overlap
+    merge (:2488-2494).  One step = the whole phase for 1 h of host-resident audio (the
+    reference's waveform is a numpy array), hotwords per --hotwords-file.  The plan-ahead route
+    makes the two workers' 121 calls ONE batched GPU decode; --no-pipeline sets
+    ZASR_PLAN_AHEAD=0 (every call its own decode, the round-2 behaviour)."""
+    if args.no_pipeline:
+        os.environ["ZASR_PLAN_AHEAD"] = "0"
+    import threading
+
+    import torch
+    from zasr import asr_engine as ae
+    from zasr.merge import merge_chunks_with_overlap
+    from zasr.model import PRESETS, save_model_dir, synth_tokens, synth_weights
+    from zasr.plan import best_split, concat_to_original, silent_regions
+    from zasr.synth_audio import synth_speech
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    cfg = PRESETS[args.model]()
+    beam = args.beam
+    hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
+    hotwords = load_hotwords(hw_path, cfg.vocab_size) if hw_path else ([], [])
+    mdir = os.path.join(tempfile.gettempdir(), f"zasr_dropin_{args.model}_{os.getpid()}")
+    save_model_dir(mdir, cfg, synth_weights(cfg, WEIGHT_SEED), synth_tokens(cfg.vocab_size))
+    rec = ae.create_recognizer(mdir, 4, max_active_paths=beam, hotwords=hotwords,
+                               device_id=local, precision=args.precision)
+    concat = synth_speech(args.audio_sec, AUDIO_SEED + rank)
+    omap = [(0, 0, len(concat))]  # no VAD cut: the identity offset map (:2181)
+    info = {}
+
+    def phase():
+        # the planner (:2137-2161) through the hook the drop-in installs on find_silent_regions
+        regions = silent_regions(concat)
+        ae.register_plan_from_regions(concat, regions, best_split)
+        from zasr.plan import plan_from_regions
+        plan = plan_from_regions(len(concat), regions, best_split)
+        results = [None] * len(plan)
+
+        def worker(idx):
+            for i in idx:
+                s, e, ov = plan[i]
+                words = ae.decode_chunk(rec, concat[s:e], s / SR)
+                for w in words:
+                    w["start"] = concat_to_original(w["start"], omap)
+                    w["end"] = concat_to_original(w["end"], omap)
+                results[i] = {"words": words, "audio_start_abs": s / SR, "audio_end_abs": e / SR,
+                              "overlap_sec": ov / SR}
+
+        ts = [threading.Thread(target=worker, args=(list(range(k, len(plan), 2)),))
+              for k in (0, 1)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        merged, _ = merge_chunks_with_overlap(results)
+        info.update(chunks=len(plan), words=len(merged))
+
+    for _ in range(args.warmup):
+        phase()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        phase()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=f"cuda:{local}")
+    if rank == 0:
+        line = {"metric": "audio-sec/sec (xRT) drop-in decode_chunk loop (reference two-worker "
+                          "dispatch), Zipformer-68M",
+                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": args.precision,
+                "data": "synthetic (seeded speech-like audio, random-init Zipformer weights)",
+                "config": {"workload": f"{args.model} modified_beam_search beam {beam}"
+                                       f"{' + hotwords' if hotwords[0] else ''} through "
+                                       f"zasr.asr_engine.decode_chunk from two worker threads, "
+                                       f"1 h of host audio per GPU, timestamps mapped, overlap merge",
+                           "plan_ahead": os.environ.get("ZASR_PLAN_AHEAD", "1") != "0",
+                           **info},
+                "roofline": None, "cpu_baseline": None}
+        print(json.dumps(line))
+        if args.profile_out:
+            with open(args.profile_out, "w") as f:
+                json.dump(line, f, indent=1)
+    ae.clear_model_cache()
+    if dist:
+        dist.destroy_process_group()
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse_args()
@@ -958,6 +1067,8 @@ def main():
         return bench_pipe(args)
     if args.stage == "rover":
         return bench_rover(args)
+    if args.stage == "dropin":
+        return bench_dropin(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

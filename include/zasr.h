@@ -51,14 +51,16 @@ enum {
 /* FP32: exact-f32 MFMA everywhere (parity mode).  BF16: bf16 MFMA operands for the encoder
    projections / attention and the joiner, f32 accumulate, norms and search.  BF16_ENC: the
    BF16 encoder with the f32 joiner and search of FP32 (no bf16 rounding of the joiner input).
-   BF16X3: f32 storage as FP32, every projection product as three bf16 MFMAs over hi / lo
-   operand halves (relative product error ~2^-16; token-exact against the fp32 oracle on the
-   68M parity chunks). */
+   BF16X3: f32 storage as FP32, every encoder projection product as three bf16 MFMAs over
+   hi / lo operand halves (relative product error ~2^-16).  BF16X6: three bf16 pieces per
+   operand, six MFMAs per product (dropped terms below 2^-24: exact-f32 quality at bf16 MFMA
+   rates; token-exact against the fp32 oracle). */
 enum {
   ZASR_PRECISION_FP32 = 0,
   ZASR_PRECISION_BF16 = 1,
   ZASR_PRECISION_BF16_ENC = 2,
-  ZASR_PRECISION_BF16X3 = 3
+  ZASR_PRECISION_BF16X3 = 3,
+  ZASR_PRECISION_BF16X6 = 4
 };
 
 typedef struct zasr_config {

@@ -263,9 +263,9 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
                const std::vector<std::vector<int>>& hotwords, const std::vector<float>& hotword_scores,
                int precision)
     : device_(device), beam_(beam), greedy_(greedy), precision_(precision) {
-  ZASR_REQUIRE(precision >= 0 && precision <= 3,
-               "precision must be 0 (fp32), 1 (bf16), 2 (bf16 encoder, f32 joiner + search) or 3 "
-               "(bf16x3: split-bf16 products, f32 storage)");
+  ZASR_REQUIRE(precision >= 0 && precision <= 4,
+               "precision must be 0 (fp32), 1 (bf16), 2 (bf16 encoder, f32 joiner + search), 3 "
+               "(bf16x3: two-piece split-bf16 products) or 4 (bf16x6: three-piece, f32 quality)");
   // host side first (no GPU state to unwind when the files are bad): config.json +
   // model.safetensors, or the reference's encoder-/decoder-/joiner-*.onnx (onnx_io.h;
   // core/asr_engine.py:913-928)
@@ -460,13 +460,12 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
   model_.dec_proj = lin("decoder_proj", cfg.joiner_dim, D);
   model_.joiner = lin("joiner.output_linear", cfg.V, cfg.joiner_dim);
   ensure_pos_tables(2048);
-  if (precision_ == 3) {  // split-bf16 (hi, lo) copies of every encoder projection weight
+  if (split_pieces() > 0) {  // split-bf16 pieces of every encoder projection weight
     auto mkx = [&](DLin& l) {
       void* p = nullptr;
-      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 4));
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2 * split_pieces()));
       model_.allocations.push_back(p);
-      split_to_bf16(l.w, p, reinterpret_cast<__bf16*>(p) + (size_t)l.N * l.K, (long)l.N * l.K,
-                    stream_);
+      split_to_bf16(l.w, p, (long)l.N * l.K, split_pieces(), stream_);
       l.wx = p;
     };
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
@@ -815,7 +814,7 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
   else
     prof_begin(cls);
   if (l.wx)
-    gemm_x3(p, l.wx, (long)l.N * l.K, epi, ALOAD_DENSE, st_);
+    gemm_x3(p, l.wx, (long)l.N * l.K, epi, ALOAD_DENSE, st_, split_pieces());
   else if (l.wh)
     gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_);
   else
@@ -1210,7 +1209,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     if (fe16)
       gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_, true, true);
     else if (model_.conv4.wx)
-      gemm_x3(p, model_.conv4.wx, 32L * 72, EPI_SWOOSHR, ALOAD_CONV2, st_);
+      gemm_x3(p, model_.conv4.wx, 32L * 72, EPI_SWOOSHR, ALOAD_CONV2, st_, split_pieces());
     else if (model_.conv4.wh)
       gemm_bf16(p, model_.conv4.wh, EPI_SWOOSHR, ALOAD_CONV2, st_);
     else
@@ -1251,7 +1250,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       p.C = x3;
       prof_begin("frontend_conv");
       if (model_.conv7.wx)
-        gemm_x3(p, model_.conv7.wx, 128L * 288, EPI_SWOOSHR, ALOAD_CONV3, st_);
+        gemm_x3(p, model_.conv7.wx, 128L * 288, EPI_SWOOSHR, ALOAD_CONV3, st_, split_pieces());
       else
         gemm_f32(p, EPI_SWOOSHR, ALOAD_CONV3, false, st_);
       prof_end();

@@ -233,6 +233,8 @@ class Engine {
   int beam_ = 8;
   [[maybe_unused]] bool greedy_ = false;
   int precision_ = 0;
+  // bf16 pieces per operand of the split-bf16 modes (bf16x3: 2, bf16x6: 3), 0 otherwise
+  int split_pieces() const { return precision_ == 3 ? 2 : precision_ == 4 ? 3 : 0; }
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
   hipStream_t stream3_ = nullptr;  // the second group of a beam search (high priority)

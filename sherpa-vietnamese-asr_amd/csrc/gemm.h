@@ -105,13 +105,16 @@ void gemm_rp_pack_weights(const void* W_bf16, int N, int K, void* out, hipStream
 bool gemm_rp(const void* A, bool a_bf16, int lda, const void* Bp, const float* bias, void* C,
              bool c_bf16, int ldc, int M, int N, int K, int epi, hipStream_t stream);
 
-// Split-bf16 variant (gemm_x3.hip, the "bf16x3" precision mode): A f32 (dense, or the
-// implicit-im2col loaders ALOAD_CONV2 / ALOAD_CONV3), W = hi [N][K] bf16 at Bw and lo at
-// Bw + b_lo elements (split_to_bf16); C f32.  Epilogues NONE, SWOOSHL, SWOOSHR, RESADD,
-// MULAUX (f32 aux).  N, ldc (and ldaux) multiples of 4; K a multiple of 8 for dense A.
-void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t stream);
-// hi[i] = bf16(src[i]), lo[i] = bf16(src[i] - hi[i])
-void split_to_bf16(const float* src, void* hi, void* lo, long n, hipStream_t stream);
+// Split-bf16 variant (gemm_x3.hip; the "bf16x3" / "bf16x6" precision modes): A f32 (dense,
+// or the implicit-im2col loaders ALOAD_CONV2 / ALOAD_CONV3) split into `pieces` bf16 pieces
+// while staging; W pre-split by split_to_bf16, piece t at Bw + t * b_lo elements; C f32.
+// pieces = 2: 3 MFMAs per product (~2^-16 relative); pieces = 3: 6 MFMAs (exact-f32
+// quality).  Epilogues NONE, SWOOSHL, SWOOSHR, RESADD, MULAUX (f32 aux).  N, ldc (and ldaux)
+// multiples of 4; K a multiple of 8 for dense A.
+void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t stream,
+             int pieces);
+// dst[t * n + i] = piece t of src[i]: bf16(src[i] - sum of the previous pieces), t < pieces
+void split_to_bf16(const float* src, void* dst, long n, int pieces, hipStream_t stream);
 
 // device f32 -> bf16 (round to nearest even) copy
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t stream);

@@ -27,13 +27,19 @@
 namespace zasr {
 namespace {
 
-__device__ __forceinline__ void split8(const float4 x0, const float4 x1, bf16x8& hi, bf16x8& lo) {
+// x -> NP bf16 pieces p0 + p1 (+ p2), each the RNE bf16 of what the previous ones left
+template <int NP>
+__device__ __forceinline__ void split8(const float4 x0, const float4 x1, bf16x8 (&pc)[NP]) {
   const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const __bf16 h = (__bf16)v[q];
-    hi[q] = h;
-    lo[q] = (__bf16)(v[q] - (float)h);
+    float r = v[q];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const __bf16 h = (__bf16)r;
+      pc[t][q] = h;
+      if (t + 1 < NP) r -= (float)h;
+    }
   }
 }
 
@@ -44,11 +50,15 @@ __device__ __forceinline__ float x3_act(float v) {
   return v;
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP>
+// NP = 2 ("bf16x3"): pieces (hi, lo), products p0q0 + p0q1 + p1q0 (3 MFMAs), BK = 32.
+// NP = 3 ("bf16x6"): pieces (p0, p1, p2), the six products p_i q_j with i + j <= 2 (6 MFMAs,
+// dropped terms below 2^-24 relative: exact-f32 quality), BK = 16 (same MFMAs per slab and
+// the same LDS as NP = 2).  Weights: piece t at Bw + t * blo.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP, int NP>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmParams p,
                                                                        const __bf16* Bw, long blo,
                                                                        int tiles_n, int tiles_m) {
-  constexpr int BK = 32;
+  constexpr int BK = NP == 2 ? 32 : 16;
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WTM = BM / WAVES_M;
   constexpr int WTN = BN / WAVES_N;
@@ -61,8 +71,8 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
   constexpr int B_G = BN * GPR;
   constexpr int A_LD = (A_G + NT - 1) / NT;
   constexpr int B_LD = (B_G + NT - 1) / NT;
-  // stage: A hi [BM][LDH], A lo, W hi [BN][LDH], W lo
-  constexpr int STAGE = 2 * (BM + BN) * LDH;
+  // stage: A pieces [NP][BM][LDH], then W pieces [NP][BN][LDH]
+  constexpr int STAGE = NP * (BM + BN) * LDH;
   constexpr int LDE = 40;
   constexpr int OPER_BYTES = 2 * STAGE * 2;
   constexpr int EPI_BYTES = (NT / 64) * 32 * LDE * 4;
@@ -121,7 +131,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
 
   struct Regs {
     float4 a0[A_LD], a1[A_LD];
-    bf16x8 bh[B_LD], bl[B_LD];
+    bf16x8 b[NP][B_LD];
   };
   auto gload = [&](Regs& r, int kt) {
     const int k0 = kt * BK;
@@ -132,10 +142,9 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
         r.a1[i] = *reinterpret_cast<const float4*>(arow[i] + k0 + 4);
       }
 #pragma unroll
-      for (int i = 0; i < B_LD; ++i) {
-        r.bh[i] = *reinterpret_cast<const bf16x8*>(brow[i] + k0);
-        r.bl[i] = *reinterpret_cast<const bf16x8*>(brow[i] + blo + k0);
-      }
+      for (int t = 0; t < NP; ++t)
+#pragma unroll
+        for (int i = 0; i < B_LD; ++i) r.b[t][i] = *reinterpret_cast<const bf16x8*>(brow[i] + t * blo + k0);
       return;
     }
 #pragma unroll
@@ -153,30 +162,29 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
       const int gn = n0 + n, gk = k0 + 8 * k8;
       const bool ok = idx < B_G && gn < N && gk < K;
       const int nc = gn < N ? gn : N - 1, kc = gk < K ? gk : K - 8;
-      bf16x8 h = *reinterpret_cast<const bf16x8*>(B + (long)nc * p.sbn + kc);
-      bf16x8 l = *reinterpret_cast<const bf16x8*>(B + blo + (long)nc * p.sbn + kc);
-      if (!ok) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) h[q] = l[q] = (__bf16)0.f;
+      for (int t = 0; t < NP; ++t) {
+        bf16x8 h = *reinterpret_cast<const bf16x8*>(B + t * blo + (long)nc * p.sbn + kc);
+        if (!ok) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) h[q] = (__bf16)0.f;
+        }
+        r.b[t][i] = h;
       }
-      r.bh[i] = h;
-      r.bl[i] = l;
     }
   };
   auto sstore = [&](const Regs& r, int buf) {
-    __bf16* Ah = sbase + buf * STAGE;
-    __bf16* Al = Ah + BM * LDH;
-    __bf16* Bh = Al + BM * LDH;
-    __bf16* Bl = Bh + BN * LDH;
+    __bf16* As = sbase + buf * STAGE;
+    __bf16* Bs = As + NP * BM * LDH;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
       const int idx = tid + NT * i;
       if (idx < A_G) {
-        bf16x8 h, l;
-        split8(r.a0[i], r.a1[i], h, l);
+        bf16x8 pc[NP];
+        split8<NP>(r.a0[i], r.a1[i], pc);
         const int o = (idx / GPR) * LDH + 8 * (idx % GPR);
-        *reinterpret_cast<bf16x8*>(&Ah[o]) = h;
-        *reinterpret_cast<bf16x8*>(&Al[o]) = l;
+#pragma unroll
+        for (int t = 0; t < NP; ++t) *reinterpret_cast<bf16x8*>(&As[t * BM * LDH + o]) = pc[t];
       }
     }
 #pragma unroll
@@ -184,8 +192,8 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
       const int idx = tid + NT * i;
       if (idx < B_G) {
         const int o = (idx / GPR) * LDH + 8 * (idx % GPR);
-        *reinterpret_cast<bf16x8*>(&Bh[o]) = r.bh[i];
-        *reinterpret_cast<bf16x8*>(&Bl[o]) = r.bl[i];
+#pragma unroll
+        for (int t = 0; t < NP; ++t) *reinterpret_cast<bf16x8*>(&Bs[t * BN * LDH + o]) = r.b[t][i];
       }
     }
   };
@@ -199,40 +207,40 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto mma_slab = [&](int cur) {
-    const __bf16* Ah = sbase + cur * STAGE;
-    const __bf16* Al = Ah + BM * LDH;
-    const __bf16* Bh = Al + BM * LDH;
-    const __bf16* Bl = Bh + BN * LDH;
+    const __bf16* As = sbase + cur * STAGE;
+    const __bf16* Bs = As + NP * BM * LDH;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+      bf16x8 a[NP][FM], b[NP][FN];
       const int kc = ks * 16 + 8 * (lane >> 5);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int o = (wm * WTM + i * 32 + (lane & 31)) * LDH + kc;
-        ah[i] = *reinterpret_cast<const bf16x8*>(&Ah[o]);
-        al[i] = *reinterpret_cast<const bf16x8*>(&Al[o]);
-      }
+      for (int t = 0; t < NP; ++t) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int o = (wn * WTN + j * 32 + (lane & 31)) * LDH + kc;
-        bh[j] = *reinterpret_cast<const bf16x8*>(&Bh[o]);
-        bl[j] = *reinterpret_cast<const bf16x8*>(&Bl[o]);
+        for (int i = 0; i < FM; ++i)
+          a[t][i] = *reinterpret_cast<const bf16x8*>(
+              &As[t * BM * LDH + (wm * WTM + i * 32 + (lane & 31)) * LDH + kc]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          b[t][j] = *reinterpret_cast<const bf16x8*>(
+              &Bs[t * BN * LDH + (wn * WTN + j * 32 + (lane & 31)) * LDH + kc]);
       }
+      // smallest terms first: for NP = 3, (2,0) (1,1) (0,2) then (1,0) (0,1) then (0,0)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int sdeg = NP - 1; sdeg >= 0; --sdeg)
+#pragma unroll
+            for (int u = sdeg; u >= 0; --u)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u][i], b[sdeg - u][j],
+                                                                  acc[i][j], 0, 0, 0);
     }
   };
 
   const int nkt = (K + BK - 1) / BK;
   if constexpr (DEEP) {
-    // dense A, K a multiple of 2 BK (host-checked): two register sets, LDS-only barriers
+    // dense A, K a multiple of 64 (host-checked): two register sets, LDS-only barriers
     // (__syncthreads would drain the slab in flight with vmcnt(0)), slab indices clamped so
     // every load is unconditional and the in-order vmcnt waits stay exact
     Regs x0, x1;
@@ -321,20 +329,20 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ALOAD, int EPI>
+template <int BM, int BN, int WM, int WN, int ALOAD, int EPI, int NP>
 void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
   if (ALOAD == ALOAD_DENSE && !p.slices && p.K % 64 == 0 && p.lda % 4 == 0) {
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true>), grid,
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP>), grid,
                        dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
     return;
   }
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false>), grid,
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP>), grid,
                      dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
 }
 
-template <int ALOAD, int EPI>
+template <int ALOAD, int EPI, int NP>
 void launch_x3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   // BN: the largest of {128, 64, 32} whose padded width is within 15 % of the tightest
   const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
@@ -342,59 +350,72 @@ void launch_x3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
   const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
   const bool big = blocks128 >= 512;
   if (BN == 128) {
-    if (big) launch_x3_t<128, 128, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
-    else launch_x3_t<64, 128, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
+    if (big) launch_x3_t<128, 128, 2, 2, ALOAD, EPI, NP>(p, Bw, blo, st);
+    else launch_x3_t<64, 128, 2, 2, ALOAD, EPI, NP>(p, Bw, blo, st);
   } else if (BN == 64) {
-    if (big) launch_x3_t<128, 64, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
-    else launch_x3_t<64, 64, 2, 2, ALOAD, EPI>(p, Bw, blo, st);
+    if (big) launch_x3_t<128, 64, 2, 2, ALOAD, EPI, NP>(p, Bw, blo, st);
+    else launch_x3_t<64, 64, 2, 2, ALOAD, EPI, NP>(p, Bw, blo, st);
   } else {
-    if (big) launch_x3_t<128, 32, 4, 1, ALOAD, EPI>(p, Bw, blo, st);
-    else launch_x3_t<64, 32, 2, 1, ALOAD, EPI>(p, Bw, blo, st);
+    if (big) launch_x3_t<128, 32, 4, 1, ALOAD, EPI, NP>(p, Bw, blo, st);
+    else launch_x3_t<64, 32, 2, 1, ALOAD, EPI, NP>(p, Bw, blo, st);
   }
 }
 
-__global__ void split_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ hi,
-                                  __bf16* __restrict__ lo, long n) {
+template <int NP>
+void gemm_split_dispatch(const GemmParams& p, const __bf16* B, long b_lo, int epi, int aload,
+                         hipStream_t st) {
+  if (aload == ALOAD_DENSE) {
+    switch (epi) {
+      case EPI_NONE: return launch_x3<ALOAD_DENSE, EPI_NONE, NP>(p, B, b_lo, st);
+      case EPI_SWOOSHL: return launch_x3<ALOAD_DENSE, EPI_SWOOSHL, NP>(p, B, b_lo, st);
+      case EPI_SWOOSHR: return launch_x3<ALOAD_DENSE, EPI_SWOOSHR, NP>(p, B, b_lo, st);
+      case EPI_RESADD: return launch_x3<ALOAD_DENSE, EPI_RESADD, NP>(p, B, b_lo, st);
+      case EPI_MULAUX: return launch_x3<ALOAD_DENSE, EPI_MULAUX, NP>(p, B, b_lo, st);
+      default: break;
+    }
+  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
+    return launch_x3<ALOAD_CONV2, EPI_SWOOSHR, NP>(p, B, b_lo, st);
+  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR) {
+    return launch_x3<ALOAD_CONV3, EPI_SWOOSHR, NP>(p, B, b_lo, st);
+  }
+  throw std::runtime_error("gemm_x3: unsupported (aload, epi) combination");
+}
+
+__global__ void split_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ dst,
+                                  long n, int pieces) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const float x = src[i];
-    const __bf16 h = (__bf16)x;
-    hi[i] = h;
-    lo[i] = (__bf16)(x - (float)h);
+    float r = src[i];
+    for (int t = 0; t < pieces; ++t) {
+      const __bf16 h = (__bf16)r;
+      dst[t * n + i] = h;
+      r -= (float)h;
+    }
   }
 }
 
 }  // namespace
 
-void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t st) {
+void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t st,
+             int pieces) {
   ZASR_REQUIRE(p.N > 0, "gemm_x3: N must be positive");
   if (p.max_M <= 0) return;
   ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (epi != EPI_MULAUX || p.ldaux % 4 == 0),
                "gemm_x3: N and the C / aux row strides must be multiples of 4");
   ZASR_REQUIRE(p.slices != nullptr || (p.K % 8 == 0 && p.lda % 4 == 0),
                "gemm_x3: K must be a multiple of 8 and lda of 4");
+  ZASR_REQUIRE(pieces == 2 || pieces == 3, "gemm_x3: pieces must be 2 or 3");
   const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
-  if (aload == ALOAD_DENSE) {
-    switch (epi) {
-      case EPI_NONE: return launch_x3<ALOAD_DENSE, EPI_NONE>(p, B, b_lo, st);
-      case EPI_SWOOSHL: return launch_x3<ALOAD_DENSE, EPI_SWOOSHL>(p, B, b_lo, st);
-      case EPI_SWOOSHR: return launch_x3<ALOAD_DENSE, EPI_SWOOSHR>(p, B, b_lo, st);
-      case EPI_RESADD: return launch_x3<ALOAD_DENSE, EPI_RESADD>(p, B, b_lo, st);
-      case EPI_MULAUX: return launch_x3<ALOAD_DENSE, EPI_MULAUX>(p, B, b_lo, st);
-      default: break;
-    }
-  } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
-    return launch_x3<ALOAD_CONV2, EPI_SWOOSHR>(p, B, b_lo, st);
-  } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR) {
-    return launch_x3<ALOAD_CONV3, EPI_SWOOSHR>(p, B, b_lo, st);
-  }
-  throw std::runtime_error("gemm_x3: unsupported (aload, epi) combination");
+  if (pieces == 2)
+    gemm_split_dispatch<2>(p, B, b_lo, epi, aload, st);
+  else
+    gemm_split_dispatch<3>(p, B, b_lo, epi, aload, st);
 }
 
-void split_to_bf16(const float* src, void* hi, void* lo, long n, hipStream_t st) {
+void split_to_bf16(const float* src, void* dst, long n, int pieces, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(split_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
-                     reinterpret_cast<__bf16*>(hi), reinterpret_cast<__bf16*>(lo), n);
+                     reinterpret_cast<__bf16*>(dst), n, pieces);
 }
 
 }  // namespace zasr

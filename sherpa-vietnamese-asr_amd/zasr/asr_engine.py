@@ -19,6 +19,19 @@ with the same Python names, arguments and return shapes, so the reference's call
   decode_chunk(...)              :1209  same word dicts (BPE merge, timestamps, entropy)
   decode_chunks(...)             new    batched decode of many chunks in one GPU pass
 
+Plan-ahead batching (how the reference's UNCHANGED caller reaches the batch pipeline): the
+reference plans the whole file before decoding it (`TranscriberPipeline._run_pipeline`
+:2137-2161 -- find_silent_regions over the concatenated speech, then ~30 s boundaries) and
+then calls decode_chunk once per chunk from two worker threads (:2219-2237, :2326-2397).
+zasr.dropin.install() wraps the module-level find_silent_regions so the plan is registered
+(`register_plan`) the moment it is made; the first decode_chunk call that asks for a chunk
+of a registered plan (a view into the planned signal at one of the plan's spans) decodes the
+WHOLE plan in one batched GPU pass for that recognizer, and every later call -- from either
+worker -- is served from those results.  Batched results equal per-chunk results bit for bit
+(ragged batching, no padding), so the words are identical (tests/test_gpu_dropin.py).
+Chunks that are not views of a planned signal (WPE-processed copies, other callers) take
+the per-chunk path.  ZASR_PLAN_AHEAD=0 turns the routing off.
+
 The search and the word post-processing stay semantically identical to the reference;
 the arithmetic runs in libzasr (see DESIGN.md for precision modes and tolerances).
 """
@@ -29,6 +42,7 @@ import math
 from functools import lru_cache
 import os
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -92,7 +106,9 @@ def compute_fbank_ort(audio, sr=16000):
     """80-bin kaldi log-mel fbank (reference :698-721) computed by the HIP fbank kernel."""
     if sr != 16000:
         raise ValueError("only 16 kHz input is supported (reference resamples on load)")
-    return _default_handle().fbank(np.asarray(audio, dtype=np.float32))
+    feats = _default_handle().fbank(np.asarray(audio, dtype=np.float32))
+    _note_features(feats, audio)
+    return feats
 
 
 def _log_add(a, b):
@@ -202,7 +218,10 @@ def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_p
     provider_policy = str(execution_provider or "cpu").lower()
     dev = int(os.environ.get("ZASR_DEVICE", "0")) if device_id is None else int(device_id)
     prec = precision or os.environ.get("ZASR_PRECISION", "fp32")
-    key = (os.path.normpath(model_path), cpu_threads, max_active_paths, provider_policy, dev, prec,
+    # cpu_threads / execution_provider do not change the GPU engine, so they are not part of
+    # the key: the reference re-creates the recognizer with the worker thread count before its
+    # two workers start (:2290-2307), which must not load a second copy of the model
+    key = (os.path.normpath(model_path), max_active_paths, dev, prec,
            None if hotwords is None else repr(hotwords))
     global _last_handle
     with _cache_lock:
@@ -382,20 +401,144 @@ def result_words(recognizer, r, n_samples: int, time_offset: float):
                               r.log_probs.tolist(), int(r.T), TokenStats.rows(r.stats))
 
 
+# ------------------------------------------------------------------ plan-ahead batching
+PLAN_BATCH_CHUNKS = 256  # chunks per batched decode call (~2 h of audio)
+
+
+class _PlannedSignal:
+    """A signal the reference's planner cut into chunks.  Holds the signal weakly (the
+    pipeline owns it) and, per recognizer handle and beam, the search results of every chunk
+    of the plan once the first of them was asked for."""
+
+    def __init__(self, audio: np.ndarray, plan):
+        self.ref = weakref.ref(audio)
+        self.ptr = audio.__array_interface__["data"][0]
+        self.n = int(audio.shape[0])
+        self.plan = [(int(s), int(e)) for s, e, _ in plan if int(e) > int(s)]
+        self.spans = set(self.plan)
+        self.lock = threading.Lock()
+        self.results = weakref.WeakKeyDictionary()  # handle -> {beam: {(s, e): SearchResult}}
+
+    def alive(self) -> bool:
+        return self.ref() is not None
+
+    def result(self, handle, beam: int, span):
+        with self.lock:  # a second worker asking meanwhile waits for the same batch
+            per = self.results.get(handle)
+            res = per.get(beam) if per is not None else None
+            if res is None:
+                audio = self.ref()
+                if audio is None:
+                    return None
+                res = {}
+                for i in range(0, len(self.plan), PLAN_BATCH_CHUNKS):
+                    part = self.plan[i:i + PLAN_BATCH_CHUNKS]
+                    out = handle.decode([audio[s:e] for s, e in part], beam=beam)
+                    res.update(zip(part, out))
+                self.results.setdefault(handle, {})[beam] = res
+        return res.get(span)
+
+
+_plan_lock = threading.Lock()
+_planned: List[_PlannedSignal] = []
+_feat_src: Dict[int, tuple] = {}  # id(features) -> (weakref(features), chunk data ptr, samples)
+
+
+def _plan_ahead_on() -> bool:
+    return os.environ.get("ZASR_PLAN_AHEAD", "1") != "0"
+
+
+def _is_f32_vector(a) -> bool:
+    return (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.ndim == 1
+            and a.strides == (4,))
+
+
+def register_plan(audio, plan) -> bool:
+    """Remember that `audio` (the signal the planner worked on) is cut into `plan`
+    [(start, end, overlap)]; chunks decode_chunk later receives as views of it at those spans
+    are decoded together.  Keeps the last few signals (weakly)."""
+    if not _plan_ahead_on() or not _is_f32_vector(audio) or not plan:
+        return False
+    sig = _PlannedSignal(audio, plan)
+    with _plan_lock:
+        _planned[:] = [p for p in _planned if p.alive()][-3:] + [sig]
+    return True
+
+
+def register_plan_from_regions(audio, regions, best_split_fn=None) -> bool:
+    """The find_silent_regions hook: the plan the reference builds from these regions
+    (:2141-2161, zasr.plan.plan_from_regions with the reference's own find_best_split_point)."""
+    from zasr.plan import plan_from_regions
+    if not _is_f32_vector(audio):
+        return False
+    return register_plan(audio, plan_from_regions(int(audio.shape[0]), regions, best_split_fn))
+
+
+def _planned_span(chunk):
+    """(planned signal, (start, end)) when `chunk` is a view of a registered signal at one of
+    its plan's spans, else None."""
+    if not _is_f32_vector(chunk) or chunk.shape[0] == 0:
+        return None
+    p = chunk.__array_interface__["data"][0]
+    with _plan_lock:
+        sigs = list(_planned)
+    for sig in reversed(sigs):
+        if sig.ref() is None:
+            continue
+        off = p - sig.ptr
+        if off >= 0 and off % 4 == 0:
+            span = (off // 4, off // 4 + int(chunk.shape[0]))
+            if span in sig.spans:
+                return sig, span
+    return None
+
+
+def _note_features(feats, audio) -> None:
+    """compute_fbank_ort output: remember which chunk it came from, so decode_chunk with these
+    precomputed features (the ROVER path, :2346-2350) can still use the plan's batch results
+    (the batch computes the same fbank kernel on the same samples)."""
+    if not _plan_ahead_on() or not _is_f32_vector(audio):
+        return
+    key = id(feats)
+
+    def drop(_, k=key):
+        _feat_src.pop(k, None)
+    _feat_src[key] = (weakref.ref(feats, drop), audio.__array_interface__["data"][0],
+                      int(audio.shape[0]))
+
+
+def _planned_result(handle, beam, audio_chunk, precomputed_features):
+    if not _plan_ahead_on():
+        return None
+    if precomputed_features is not None:
+        src = _feat_src.get(id(precomputed_features))
+        if (src is None or src[0]() is not precomputed_features or not _is_f32_vector(audio_chunk)
+                or src[1] != audio_chunk.__array_interface__["data"][0]
+                or src[2] != audio_chunk.shape[0]):
+            return None
+    hit = _planned_span(audio_chunk)
+    if hit is None:
+        return None
+    return hit[0].result(handle, beam, hit[1])
+
+
 def decode_chunk(recognizer, audio_chunk, time_offset=0.0, precomputed_features=None):
-    """Decode one chunk into merged word dicts (reference :1209-1326)."""
+    """Decode one chunk into merged word dicts (reference :1209-1326).  A chunk of a
+    registered plan is served from the plan's batched decode (see the module docstring)."""
     beam = recognizer.get("max_active_paths", 8)
     h: Recognizer = recognizer["handle"]
-    if precomputed_features is not None:
-        feats = np.asarray(precomputed_features, np.float32)
-        if feats.shape[0] == 0:
-            return []
-        r = h.decode_features([feats], beam=beam)[0]
-    else:
-        a = np.asarray(audio_chunk, np.float32)
-        if a.shape[0] == 0:
-            return []
-        r = h.decode([a], beam=beam)[0]
+    r = _planned_result(h, beam, audio_chunk, precomputed_features)
+    if r is None:
+        if precomputed_features is not None:
+            feats = np.asarray(precomputed_features, np.float32)
+            if feats.shape[0] == 0:
+                return []
+            r = h.decode_features([feats], beam=beam)[0]
+        else:
+            a = np.asarray(audio_chunk, np.float32)
+            if a.shape[0] == 0:
+                return []
+            r = h.decode([a], beam=beam)[0]
     return result_words(recognizer, r, len(audio_chunk), time_offset)
 
 

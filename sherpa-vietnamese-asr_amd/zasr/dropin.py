@@ -16,7 +16,10 @@ What is rebound (the ASR hot path, core/asr_engine.py:698-1326):
   asr_engine      compute_fbank_ort, _log_add, create_recognizer, _ort_beam_search,
                   _compute_token_entropy, _finalize_word_entropy, decode_chunk, and
                   clear_model_cache wrapped so the reference's own version still unloads
-                  the punctuation restorer and the diarizer (:743-768)
+                  the punctuation restorer and the diarizer (:743-768); find_silent_regions
+                  wrapped (same result) so that the chunk plan built from it (:2137-2161) is
+                  registered and the per-chunk decode_chunk calls of the two workers are
+                  served from ONE batched decode of the plan (zasr.asr_engine, plan-ahead)
   hardware_accel  configure_gpu_addon_paths only (the DirectML / OpenVINO add-on dispatch is
                   removed per the north star); create_ort_session, is_gpu_provider and
                   auto_batch_size stay the reference's, so the stages outside ASR (diarization,
@@ -68,6 +71,22 @@ def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None
         clear_model_cache.__doc__ = orig_clear.__doc__
         engine_module.clear_model_cache = clear_model_cache
         done.append("asr_engine.clear_model_cache")
+    orig_fsr = getattr(engine_module, "find_silent_regions", None)
+    if orig_fsr is not None and not getattr(orig_fsr, "_zasr_wrapped", False):
+        split_fn = getattr(engine_module, "find_best_split_point", None)
+
+        def find_silent_regions(audio_data, *args, **kwargs):
+            regions = orig_fsr(audio_data, *args, **kwargs)
+            if not args and not kwargs:  # the planner's calls (:2139, :2183) use the defaults
+                try:
+                    ours.register_plan_from_regions(audio_data, regions, split_fn)
+                except Exception as e:  # routing is an optimisation: never break the caller
+                    ours.logger.warning(f"[zasr] plan registration skipped: {e}")
+            return regions
+        find_silent_regions._zasr_wrapped = True
+        find_silent_regions.__doc__ = orig_fsr.__doc__
+        engine_module.find_silent_regions = find_silent_regions
+        done.append("asr_engine.find_silent_regions")
     ours.set_host_module(engine_module)
     if accel_module is not None:
         for n in ACCEL_NAMES:

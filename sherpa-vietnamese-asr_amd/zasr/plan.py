@@ -6,7 +6,8 @@ planner so that the batched GPU decode receives the same independent units.
   concat_to_original    core/asr_engine.py:647-677    (timestamp map back)
   silent_regions        core/asr_engine.py:521-554    (10 ms RMS frames < 0.01 for >= 0.3 s)
   best_split            core/asr_engine.py:557-573    (silence midpoint nearest the target)
-  plan_chunks           core/asr_engine.py:2137-2157  (~30 s boundaries, 3 s overlap)
+  plan_from_regions     core/asr_engine.py:2141-2161  (the boundary loop given silent regions)
+  plan_chunks           core/asr_engine.py:2137-2161  (~30 s boundaries, 3 s overlap)
   split_long_segment    core/asr_engine.py:582-614    (even split of one long segment)
 
 All positions are sample indices at 16 kHz; returned plans are [(start, end, overlap)].
@@ -94,16 +95,17 @@ def best_split(target: int, total: int, regions: Sequence[Span], window: int = 2
     return best
 
 
-def plan_chunks(audio: np.ndarray, sr: int = SR, overlap_sec: float = OVERLAP_SEC) -> List[Chunk]:
-    """Silence-aligned ~30 s boundaries over (concatenated) speech; every chunk after the first
-    starts `overlap_sec` before its logical start: [(start, end, overlap_at_start)]."""
-    total = len(audio)
-    regions = silent_regions(audio, sr)
+def plan_from_regions(total: int, regions: Sequence[Span], best_split_fn=None,
+                      overlap_sec: float = OVERLAP_SEC, sr: int = SR) -> List[Chunk]:
+    """The reference's chunk loop over a signal of `total` samples given its silent regions
+    (core/asr_engine.py:2141-2161; `best_split_fn(target, total, regions)` is its
+    find_best_split_point, this module's best_split by default): [(start, end, overlap)]."""
+    split_at = best_split if best_split_fn is None else best_split_fn
     seg = SEGMENT_SEC * sr
     bounds = [0]
     cur = 0
     while cur + seg < total:
-        split = best_split(cur + seg, total, regions)
+        split = split_at(cur + seg, total, regions)
         if split <= cur + MIN_ADVANCE_SEC * sr:
             split = cur + seg
         bounds.append(split)
@@ -115,6 +117,12 @@ def plan_chunks(audio: np.ndarray, sr: int = SR, overlap_sec: float = OVERLAP_SE
         s = a if i == 0 else max(0, a - ov)
         plan.append((s, b, a - s))
     return plan
+
+
+def plan_chunks(audio: np.ndarray, sr: int = SR, overlap_sec: float = OVERLAP_SEC) -> List[Chunk]:
+    """Silence-aligned ~30 s boundaries over (concatenated) speech; every chunk after the first
+    starts `overlap_sec` before its logical start: [(start, end, overlap_at_start)]."""
+    return plan_from_regions(len(audio), silent_regions(audio, sr), None, overlap_sec, sr)
 
 
 def split_long_segment(start: int, end: int, max_sec: float = 30, overlap_sec: float = 3.0,

@@ -37,4 +37,4 @@ def main(modes):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["fp32", "bf16x3", "bf16"])
+    main(sys.argv[1:] or ["fp32", "bf16x6", "bf16x3", "bf16"])

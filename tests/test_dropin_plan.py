@@ -1,0 +1,132 @@
+"""Plan-ahead routing of the drop-in decode_chunk on CPU (no GPU): the reference's two-worker
+loop (core/asr_engine.py:2326-2397) calls decode_chunk once per chunk; after the planner's
+find_silent_regions call registered the plan (zasr.dropin wraps it), the whole plan must be
+decoded in ONE batched call per recognizer handle, and every chunk's words must equal what the
+per-chunk path returns.  The handle is a deterministic stand-in whose result depends only on a
+chunk's samples (the real engine's batched == per-chunk property is tested on the GPU,
+tests/test_gpu_dropin.py)."""
+import threading
+from types import SimpleNamespace
+
+import numpy as np
+
+from zasr import asr_engine as ae
+from zasr.plan import best_split, plan_chunks, silent_regions
+from zasr.synth_audio import synth_speech
+
+
+class FakeHandle:
+    """decode(chunks) -> one result per chunk computed from the chunk's own samples."""
+
+    def __init__(self):
+        self.calls = []
+        self.lock = threading.Lock()
+
+    def _one(self, a):
+        a = np.asarray(a, np.float32)
+        n = max(1, a.shape[0] // 4000)
+        toks = (np.abs(a[::4000][:n]) * 1e4).astype(np.int64) % 60 + 3
+        return SimpleNamespace(token_ids=toks, frames=np.arange(n, dtype=np.int64) * 3,
+                               log_probs=-np.abs(a[:n]).astype(np.float32),
+                               stats=np.tile(np.array([1.0, 5.0, 0.5, 0.2], np.float32), (n, 1)),
+                               T=3 * n + 1)
+
+    def decode(self, chunks, beam=0):
+        with self.lock:
+            self.calls.append(len(chunks))
+        return [self._one(c) for c in chunks]
+
+    def decode_features(self, feats, beam=0):
+        raise AssertionError("features path not expected")
+
+    def fbank(self, a):
+        return np.zeros((max(0, (len(a) + 80) // 160), 80), np.float32)
+
+
+def _rec(h):
+    toks = ["<blk>", "<sos/eos>", "<unk>"] + [f"▁w{i}" if i % 3 == 0 else f"p{i}" for i in range(3, 64)]
+    return {"handle": h, "id2token": dict(enumerate(toks)), "vocab_size": 64, "max_active_paths": 8}
+
+
+def _two_workers(rec, concat, plan):
+    out = [None] * len(plan)
+
+    def worker(idx):
+        for i in idx:
+            s, e, _ = plan[i]
+            out[i] = ae.decode_chunk(rec, concat[s:e], s / 16000.0)
+
+    ts = [threading.Thread(target=worker, args=(list(range(k, len(plan), 2)),)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return out
+
+
+def test_plan_registered_from_regions_equals_plan_chunks():
+    audio = synth_speech(150.0, 7)
+    assert ae.register_plan_from_regions(audio, silent_regions(audio), best_split)
+    hit = ae._planned_span(audio[plan_chunks(audio)[2][0]:plan_chunks(audio)[2][1]])
+    assert hit is not None
+    assert hit[0].plan == [(s, e) for s, e, _ in plan_chunks(audio)]
+
+
+def test_two_workers_served_by_one_batched_decode():
+    concat = synth_speech(200.0, 11)
+    plan = plan_chunks(concat)
+    assert len(plan) >= 6
+    direct = FakeHandle()
+    want = [ae.decode_chunk(_rec(direct), concat[s:e].copy(), s / 16000.0) for s, e, _ in plan]
+    assert direct.calls == [1] * len(plan)  # copies are not views of a planned signal
+    h = FakeHandle()
+    ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+    got = _two_workers(_rec(h), concat, plan)
+    assert h.calls == [len(plan)], h.calls  # ONE batched call for the whole plan
+    assert got == want
+    # a second pass (e.g. the reference's retry of failed chunks) reuses the results
+    again = [ae.decode_chunk(_rec(h), concat[s:e], s / 16000.0) for s, e, _ in plan]
+    assert h.calls == [len(plan)] and again == want
+
+
+def test_unplanned_spans_and_disabled_routing_take_the_per_chunk_path(monkeypatch):
+    concat = synth_speech(120.0, 12)
+    plan = plan_chunks(concat)
+    ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+    h = FakeHandle()
+    s, e, _ = plan[1]
+    ae.decode_chunk(_rec(h), concat[s + 1:e], 0.0)  # not a span of the plan
+    assert h.calls == [1]
+    monkeypatch.setenv("ZASR_PLAN_AHEAD", "0")
+    h2 = FakeHandle()
+    ae.decode_chunk(_rec(h2), concat[s:e], 0.0)
+    assert h2.calls == [1]
+
+
+def test_precomputed_features_route_only_for_our_fbank_of_that_chunk(monkeypatch):
+    concat = synth_speech(100.0, 13)
+    plan = plan_chunks(concat)
+    ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+    h = FakeHandle()
+    monkeypatch.setattr(ae, "_last_handle", h)
+    s, e, _ = plan[0]
+    feats = ae.compute_fbank_ort(concat[s:e])
+    ae.decode_chunk(_rec(h), concat[s:e], 0.0, precomputed_features=feats)
+    assert h.calls == [len(plan)]
+    other = np.zeros_like(feats)  # features of unknown origin: the per-chunk features path
+    h2 = FakeHandle()
+    try:
+        ae.decode_chunk(_rec(h2), concat[s:e], 0.0, precomputed_features=other)
+        raise RuntimeError("expected the features path")
+    except AssertionError as ex:
+        assert "features path" in str(ex)
+
+
+def test_dead_signal_is_not_matched():
+    a = synth_speech(70.0, 14)
+    ae.register_plan_from_regions(a, silent_regions(a), best_split)
+    ptr = a.__array_interface__["data"][0]
+    del a
+    b = np.zeros(70 * 16000, np.float32)
+    if b.__array_interface__["data"][0] == ptr:  # same address reused: still no match
+        assert ae._planned_span(b[: 30 * 16000]) is None

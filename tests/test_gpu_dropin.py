@@ -1,0 +1,89 @@
+"""The reference's unchanged two-worker loop through the drop-in decode_chunk on an MI355X
+(core/asr_engine.py:2219-2237, 2326-2397): with the plan registered (the find_silent_regions
+hook of zasr.dropin), every chunk's words come from ONE batched decode of the plan and equal
+the per-chunk path's words exactly (tokens, timestamps, probabilities, entropy fields); the
+ROVER route (compute_fbank_ort once per chunk, decode_chunk with precomputed_features,
+:2346-2350) likewise."""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dropin_rec():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    from model_fixtures import m_model
+    from zasr import asr_engine as ae
+    cfg, w, path = m_model()
+    rec = ae.create_recognizer(path, 4, max_active_paths=8, hotwords=([], []), precision="bf16x3")
+    yield ae, rec
+    ae.clear_model_cache()
+
+
+def _loop(ae, rec, concat, plan, feats=False):
+    out = [None] * len(plan)
+    errs = []
+
+    def worker(idx):
+        try:
+            for i in idx:
+                s, e, _ = plan[i]
+                c = concat[s:e]
+                f = ae.compute_fbank_ort(c, 16000) if feats else None
+                out[i] = ae.decode_chunk(rec, c, s / 16000.0, precomputed_features=f)
+        except Exception as ex:  # pragma: no cover - surfaced below
+            errs.append(ex)
+
+    ts = [threading.Thread(target=worker, args=(list(range(k, len(plan), 2)),)) for k in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    return out
+
+
+def _calls(h):
+    """Count the handle's decode / decode_features calls."""
+    n = {"decode": 0, "feat": 0, "chunks": 0}
+    d0, f0 = h.decode, h.decode_features
+
+    def dec(chunks, beam=0):
+        n["decode"] += 1
+        n["chunks"] += len(chunks)
+        return d0(chunks, beam=beam)
+
+    def decf(feats, beam=0):
+        n["feat"] += 1
+        return f0(feats, beam=beam)
+    h.decode, h.decode_features = dec, decf
+    return n
+
+
+@pytest.mark.parametrize("feats", [False, True], ids=["audio", "rover_features"])
+def test_two_worker_loop_routed_equals_per_chunk(dropin_rec, feats):
+    from zasr.plan import best_split, plan_chunks, silent_regions
+    from zasr.synth_audio import synth_speech
+    ae, rec = dropin_rec
+    concat = synth_speech(170.0, 31 + int(feats))
+    plan = plan_chunks(concat)
+    assert len(plan) >= 5
+    h = rec["handle"]
+    n = _calls(h)
+    try:
+        want = [ae.decode_chunk(rec, concat[s:e].copy(), s / 16000.0) for s, e, _ in plan]
+        assert n["decode"] == len(plan)
+        assert ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+        n["decode"] = n["feat"] = 0
+        got = _loop(ae, rec, concat, plan, feats)
+        assert n["decode"] == 1 and n["feat"] == 0, n  # one batched pass for the whole plan
+    finally:
+        del h.decode, h.decode_features
+    assert sum(len(w) for w in want) > 50
+    assert got == want

@@ -15,9 +15,12 @@ Tolerances (stated as the north star asks):
                  same encoder output: tokens / frames exact, log-probs within 5e-4 (a token
                  log-prob is the difference of two f32 hypothesis scores of magnitude ~2000
                  after 800 frames, core/asr_engine.py:1099-1100,1121: f32 ulp 1.2e-4)
-  bf16x3 mode    split-bf16 products (include/zasr.h ZASR_PRECISION_BF16X3): token ids and
-                 frames EXACT vs the fp32 oracle on the three 68M chunks (greedy and beam 8 +
-                 hotwords), encoder_out within 2e-3 * max(1, |ref|) like fp32
+  bf16x6 mode    three-piece split-bf16 products (include/zasr.h ZASR_PRECISION_BF16X6):
+                 token ids and frames EXACT vs the fp32 oracle on the three 68M chunks (greedy
+                 and beam 8 + hotwords), like fp32
+  bf16x3 mode    two-piece split (encoder_out ~3e-5 from the oracle vs ~4e-6 for fp32 /
+                 bf16x6): statistical like bf16, bounded by 0.05 (measured 0.0 greedy, 0.01
+                 beam 8 + hotwords; one near-tie of the 802-token chunk flips)
   bf16 modes     statistical: the token error rate (edit distance / reference tokens) vs the
                  fp32 oracle is measured, written to gpurun_out/bf16_token_error.json (kept
                  under profiles/) and bounded by 0.15 pooled over the chunks (measured
@@ -162,7 +165,7 @@ def test_m_bf16_token_error_rate(m_case):
     from zasr.binding import Recognizer
     ref = {"greedy": m_case["greedy"], "beam8_hotwords": m_case["beam8"]}
     report = {}
-    for prec in ("bf16", "bf16_enc", "fp32", "bf16x3"):
+    for prec in ("bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6"):
         for name, method, beam in (("greedy", "greedy_search", 1),
                                    ("beam8_hotwords", "modified_beam_search", 8)):
             kw = {"hotwords": m_case["phrases"], "hotword_scores": m_case["scores"]} if beam > 1 else {}
@@ -180,9 +183,11 @@ def test_m_bf16_token_error_rate(m_case):
         json.dump({"model": "zipformer-68m (random init)", "chunks_sec": M_SECS,
                    "reference": "fp32 oracle (fbank + torch encoder + reference search)",
                    "rates": report}, f, indent=1)
-    for prec in ("fp32", "bf16x3"):
+    for prec in ("fp32", "bf16x6"):
         assert report[f"{prec}/greedy"]["token_error_rate"] == 0.0, report
         assert report[f"{prec}/beam8_hotwords"]["token_error_rate"] == 0.0, report
+    for name in ("greedy", "beam8_hotwords"):
+        assert report[f"bf16x3/{name}"]["token_error_rate"] <= 0.05, report
     for k, v in report.items():
         assert v["token_error_rate"] <= 0.15, (k, v)
 
@@ -203,7 +208,7 @@ def test_s_encoder_matches_oracle(s_case):
     from zasr.binding import Recognizer
     feats = [fbank(_speech(s, 1300 + i)) for i, s in enumerate((17.0, 4.2, 29.0))]
     refs = [s_case["orc"].encoder(f) for f in feats]
-    for prec, tol in (("fp32", 2e-3), ("bf16x3", 2e-3), ("bf16", 0.05)):
+    for prec, tol in (("fp32", 2e-3), ("bf16x6", 2e-3), ("bf16x3", 2e-3), ("bf16", 0.05)):
         rec = Recognizer(s_case["path"], "greedy_search", 1, precision=prec)
         got = rec.encode_features(feats)
         rec.close()
