@@ -10,6 +10,8 @@
 //   B = t1 transposed in bf16, [hid][R8] (sequence b in columns [o8_b, o8_b + L8_b), zero
 //       padded), i.e. the [N][K] "weight" layout the GEMM streams with 16-byte loads,
 // and the `* y` factor in its epilogue.  The kernels here produce A0 and t1^T.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -53,11 +55,49 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 
 }  // namespace
 
-template <int MODE>
+// NP = 1: bf16 storage (the bf16 mode).  NP = 2 / 3: q / k / p / v / out / the head-0 weights
+// are f32 and every MFMA operand is split into NP bf16 pieces (x = p0 + p1 [+ p2]); a product
+// is the sum of the piece products p_u q_v with u + v < NP (3 / 6 MFMAs where the bf16 mode
+// issues one): near-f32 (NP = 2) / f32-quality (NP = 3) scores and outputs at bf16 MFMA rates
+// (the bf16x3 / bf16x6 modes).  In these modes q and p carry no log2(e) factor: the score is
+// scaled into the log2 domain after the positional term.
+template <int NP>
+__device__ __forceinline__ void split_f8(const float (&v)[8], bf16x8 (&pc)[NP]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float r = v[q];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const __bf16 h = (__bf16)r;
+      pc[t][q] = h;
+      if (t + 1 < NP) r -= (float)h;
+    }
+  }
+}
+
+// acc += sum over u + v < NP of x[u] * y[v], smallest terms first (written out: every index
+// a constant, so the piece arrays stay in registers)
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&x)[NP], const bf16x8 (&y)[NP], f32x16 acc) {
+#define ZASR_MF(u, v) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[u], y[v], acc, 0, 0, 0)
+  if constexpr (NP == 3) {
+    ZASR_MF(2, 0); ZASR_MF(1, 1); ZASR_MF(0, 2);
+  }
+  if constexpr (NP >= 2) {
+    ZASR_MF(NP - 1 == 1 ? 1 : 1, 0); ZASR_MF(0, 1);
+  }
+  ZASR_MF(0, 0);
+#undef ZASR_MF
+  return acc;
+}
+
+template <int MODE, int NP>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
+  constexpr bool SPLIT = NP > 1;
+  using T = typename std::conditional<SPLIT, float, __bf16>::type;
   extern __shared__ float4 sPos[];  // [L + kPosPad] positional rows of this head, x = xlo + t
-  __shared__ __attribute__((aligned(16))) __bf16 sK[2][32 * kKLd];
-  __shared__ __attribute__((aligned(16))) __bf16 sVt[2][12 * kKLd];
+  __shared__ __attribute__((aligned(16))) __bf16 sK[NP][2][32 * kKLd];
+  __shared__ __attribute__((aligned(16))) __bf16 sVt[NP][2][12 * kKLd];
   const int b = blockIdx.y;
   const int h = MODE == 0 ? 0 : blockIdx.z;
   const int r0 = a.row_off[b];
@@ -67,14 +107,16 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   const int H = a.H;
   const long ldq = 68L * H;
   const long ldv = 12L * H;
+  const T* qkp = reinterpret_cast<const T*>(a.qkp);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int c = lane & 31, h2 = lane >> 5;
   const int i0 = i0b + 32 * wid;
   const bool live = i0 < L;  // wave-uniform
   const int i = i0 + c;
   const int ic = i < L ? i : L - 1;
+  constexpr float kSc = SPLIT ? 1.4426950408889634f : 1.f;  // log2(e) applied in-kernel
 
-  // ---- positional rows: x in [xlo, xlo + L + kPosPad) (p_i carries the log2 e scale) ----
+  // ---- positional rows: x in [xlo, xlo + L + kPosPad) ----
   {
     const int xlo = -(i0b + 127);
     const int n = L + kPosPad;
@@ -85,30 +127,53 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       sPos[t] = *reinterpret_cast<const float4*>(a.pos_tab + (long)row * 4 * H + 4 * h);
     }
   }
-  // ---- this lane's query and positional query (log2 e already folded in) ----
-  const __bf16* qrow = a.qkp + (long)(r0 + ic) * ldq + 32 * h;
-  const bf16x8 qf0 = *reinterpret_cast<const bf16x8*>(qrow + 8 * h2);
-  const bf16x8 qf1 = *reinterpret_cast<const bf16x8*>(qrow + 16 + 8 * h2);
+  // ---- this lane's query (dims 8 h2 .. +8 and 16 + 8 h2 .. +8) and positional query ----
+  const T* qrow = qkp + (long)(r0 + ic) * ldq + 32 * h;
+  bf16x8 qf0[NP], qf1[NP];
   float4 pq;
-  {
-    const bf16x4 pv = *reinterpret_cast<const bf16x4*>(a.qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
+  if constexpr (SPLIT) {
+    float v0[8], v1[8];
+    *reinterpret_cast<float4*>(&v0[0]) = *reinterpret_cast<const float4*>(qrow + 8 * h2);
+    *reinterpret_cast<float4*>(&v0[4]) = *reinterpret_cast<const float4*>(qrow + 8 * h2 + 4);
+    *reinterpret_cast<float4*>(&v1[0]) = *reinterpret_cast<const float4*>(qrow + 16 + 8 * h2);
+    *reinterpret_cast<float4*>(&v1[4]) = *reinterpret_cast<const float4*>(qrow + 20 + 8 * h2);
+    split_f8<NP>(v0, qf0);
+    split_f8<NP>(v1, qf1);
+    pq = *reinterpret_cast<const float4*>(qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
+  } else {
+    qf0[0] = *reinterpret_cast<const bf16x8*>(qrow + 8 * h2);
+    qf1[0] = *reinterpret_cast<const bf16x8*>(qrow + 16 + 8 * h2);
+    const bf16x4 pv = *reinterpret_cast<const bf16x4*>(qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
     pq = make_float4((float)pv[0], (float)pv[1], (float)pv[2], (float)pv[3]);
   }
   // pos index of (this query, key j0 + jr): j0 + jr - 32 wid - c + 127
   const int pbase = 127 - 32 * wid - c;
 
   const int nkb = (L + 31) / 32;
-  // staging roles: threads 0..127 load K (key tid>>2, 16-byte chunk tid&3); threads
-  // 128..223 load V (key (tid-128)/3, 4 dims (tid-128)%3); MODE 0 needs no V
-  const __bf16* kbase = a.qkp + (long)r0 * ldq + 32 * H + 32 * h;
-  const __bf16* vbase = MODE == 0 ? nullptr : a.v + (long)r0 * ldv + 12 * h;
+  // staging roles: threads 0..127 load K (key tid>>2, 8 dims 8 (tid&3)); threads 128..223
+  // load V (key (tid-128)/3, 4 dims (tid-128)%3); MODE 0 needs no V
+  const T* kbase = qkp + (long)r0 * ldq + 32 * H + 32 * h;
+  const T* vbase = MODE == 0 ? nullptr : reinterpret_cast<const T*>(a.v) + (long)r0 * ldv + 12 * h;
   const int vt = tid - 128;
   const int vkey = vt / 3, vq = vt - 3 * (vt / 3);
   bf16x8 kreg;
   bf16x4 vreg;
+  // split modes: f32 staging registers; K rows (threads < 128) use both, V rows the first
+  float4 stg0 = make_float4(0.f, 0.f, 0.f, 0.f), stg1 = stg0;
   auto gload = [&](int kb) {
     const int j0 = kb * 32;
-    if (tid < 128) {
+    if constexpr (SPLIT) {
+      // one load site for both roles (V threads fetch their 4 dims twice): per-role
+      // assignments made the compiler keep the staging registers in scratch
+      const bool kt = tid < 128;
+      if (kt || (MODE != 0 && vt < 96)) {
+        int j = j0 + (kt ? (tid >> 2) : vkey);
+        j = j < L ? j : L - 1;
+        const T* src = kt ? kbase + (long)j * ldq + 8 * (tid & 3) : vbase + (long)j * ldv + 4 * vq;
+        stg0 = *reinterpret_cast<const float4*>(src);
+        stg1 = *reinterpret_cast<const float4*>(src + (kt ? 4 : 0));
+      }
+    } else if (tid < 128) {
       int j = j0 + (tid >> 2);
       j = j < L ? j : L - 1;
       kreg = *reinterpret_cast<const bf16x8*>(kbase + (long)j * ldq + 8 * (tid & 3));
@@ -120,26 +185,54 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   };
   auto sstore = [&](int buf) {
     if (tid < 128) {
-      *reinterpret_cast<bf16x8*>(&sK[buf][(tid >> 2) * kKLd + 8 * (tid & 3)]) = kreg;
+      __bf16* d = &sK[0][buf][(tid >> 2) * kKLd + 8 * (tid & 3)];
+      if constexpr (SPLIT) {
+        const float v[8] = {stg0.x, stg0.y, stg0.z, stg0.w, stg1.x, stg1.y, stg1.z, stg1.w};
+        bf16x8 pc[NP];
+        split_f8<NP>(v, pc);
+#pragma unroll
+        for (int t = 0; t < NP; ++t) *reinterpret_cast<bf16x8*>(d + t * 2 * 32 * kKLd) = pc[t];
+      } else {
+        *reinterpret_cast<bf16x8*>(d) = kreg;
+      }
     } else if (MODE != 0 && vt < 96) {
       // key jj sits in score register r = (jj&3) + 4 (jj>>3) of lane half (jj>>2)&1, which
       // the PV MFMA m = r >> 3 takes in k-slot 8 half + (r & 7)
       const int jj = vkey;
       const int r = (jj & 3) + 4 * (jj >> 3);
       const int slot = 16 * (r >> 3) + 8 * ((jj >> 2) & 1) + (r & 7);
+      if constexpr (SPLIT) {
+        auto put = [&](int e, float rr) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sVt[buf][(4 * vq + e) * kKLd + slot] = vreg[e];
+          for (int t = 0; t < NP; ++t) {
+            const __bf16 hh = (__bf16)rr;
+            sVt[t][buf][(4 * vq + e) * kKLd + slot] = hh;
+            if (t + 1 < NP) rr -= (float)hh;
+          }
+        };
+        put(0, stg0.x);
+        put(1, stg0.y);
+        put(2, stg0.z);
+        put(3, stg0.w);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sVt[0][buf][(4 * vq + e) * kKLd + slot] = vreg[e];
+      }
     }
   };
   // scores of key block kb (log2 domain), keys >= L masked to -inf
   auto scores = [&](int kb, int buf, f32x16& s) {
     const int j0 = kb * 32;
-    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(&sK[buf][c * kKLd + 8 * h2]);
-    const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(&sK[buf][c * kKLd + 16 + 8 * h2]);
+    bf16x8 k0[NP], k1[NP];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      k0[t] = *reinterpret_cast<const bf16x8*>(&sK[t][buf][c * kKLd + 8 * h2]);
+      k1[t] = *reinterpret_cast<const bf16x8*>(&sK[t][buf][c * kKLd + 16 + 8 * h2]);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
-    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, s, 0, 0, 0);
-    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf1, s, 0, 0, 0);
+    s = mfma_split<NP>(k0, qf0, s);
+    s = mfma_split<NP>(k1, qf1, s);
     const int pb = j0 + pbase;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -148,7 +241,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       float ps = fmaf(pq.x, pr.x, s[r]);
       ps = fmaf(pq.y, pr.y, ps);
       ps = fmaf(pq.z, pr.z, ps);
-      s[r] = fmaf(pq.w, pr.w, ps);
+      s[r] = fmaf(pq.w, pr.w, ps) * kSc;
     }
     if (j0 + 32 > L) {
 #pragma unroll
@@ -167,7 +260,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
 
   constexpr int NPASS = MODE == 0 ? 2 : 1;
-  __bf16* const a0 = MODE == 0 ? a.attn + a.a_off[b] : nullptr;
+  T* const a0 = MODE == 0 ? reinterpret_cast<T*>(a.attn) + a.a_off[b] : nullptr;
 #pragma unroll 1
   for (int pass = 0; pass < NPASS; ++pass) {
     if (MODE == 0 && pass == 1) {
@@ -204,14 +297,23 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           } else if (i < L) {
             const int L8 = (L + 7) & ~7;
             const int j0 = kb * 32;
-            __bf16* dst = a0 + (long)i * L8 + j0 + 4 * h2;
+            T* dst = a0 + (long)i * L8 + j0 + 4 * h2;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               if (j0 + 8 * g + 4 * h2 < L8) {
-                bf16x4 v;
+                if constexpr (SPLIT) {
+                  float4 v;
+                  v.x = fexp2(s[4 * g + 0] - cst);
+                  v.y = fexp2(s[4 * g + 1] - cst);
+                  v.z = fexp2(s[4 * g + 2] - cst);
+                  v.w = fexp2(s[4 * g + 3] - cst);
+                  *reinterpret_cast<float4*>(dst + 8 * g) = v;
+                } else {
+                  bf16x4 v;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = (__bf16)fexp2(s[4 * g + e] - cst);
-                *reinterpret_cast<bf16x4*>(dst + 8 * g) = v;
+                  for (int e = 0; e < 4; ++e) v[e] = (__bf16)fexp2(s[4 * g + e] - cst);
+                  *reinterpret_cast<bf16x4*>(dst + 8 * g) = v;
+                }
               }
             }
           }
@@ -240,16 +342,27 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           }
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
-            bf16x8 pf, vf;
+            bf16x8 pf[NP], vf[NP];
 #pragma unroll
-            for (int t = 0; t < 8; ++t) pf[t] = (__bf16)s[8 * mm + t];
-            if (c < 12) {
-              vf = *reinterpret_cast<const bf16x8*>(&sVt[cur][c * kKLd + 16 * mm + 8 * h2]);
-            } else {
+            for (int q = 0; q < 8; ++q) {
+              float r = s[8 * mm + q];
 #pragma unroll
-              for (int t = 0; t < 8; ++t) vf[t] = (__bf16)0.f;
+              for (int t = 0; t < NP; ++t) {
+                const __bf16 hh = (__bf16)r;
+                pf[t][q] = hh;
+                if (t + 1 < NP) r -= (float)hh;
+              }
             }
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NP; ++t) {
+              if (c < 12) {
+                vf[t] = *reinterpret_cast<const bf16x8*>(&sVt[t][cur][c * kKLd + 16 * mm + 8 * h2]);
+              } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) vf[t][e] = (__bf16)0.f;
+              }
+            }
+            o = mfma_split<NP>(vf, pf, o);
           }
         }
       }
@@ -266,30 +379,49 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       if (h2 == 0) a.stats_out[(long)(r0 + i) * H + h] = m + __log2f(lt);
     }
     // O^T rows = value dims d = (r&3) + 8 (r>>2) + 4 h2; d < 12 valid
-    __bf16* dst = a.out + (long)(r0 + i) * ldv + 12 * h;
-    bf16x4 v0, v1;
+    T* dst = reinterpret_cast<T*>(a.out) + (long)(r0 + i) * ldv + 12 * h;
+    if constexpr (SPLIT) {
+      const float4 v0 = make_float4(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+      const float4 v1 = make_float4(o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv);
+      *reinterpret_cast<float4*>(dst + 4 * h2) = v0;
+      if (h2 == 0) *reinterpret_cast<float4*>(dst + 8) = v1;
+    } else {
+      bf16x4 v0, v1;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v0[e] = (__bf16)(o[e] * inv);
-      v1[e] = (__bf16)(o[4 + e] * inv);
+      for (int e = 0; e < 4; ++e) {
+        v0[e] = (__bf16)(o[e] * inv);
+        v1[e] = (__bf16)(o[4 + e] * inv);
+      }
+      *reinterpret_cast<bf16x4*>(dst + 4 * h2) = v0;  // d 0..3 (h2 = 0) / 4..7 (h2 = 1)
+      if (h2 == 0) *reinterpret_cast<bf16x4*>(dst + 8) = v1;  // d 8..11
     }
-    *reinterpret_cast<bf16x4*>(dst + 4 * h2) = v0;  // d 0..3 (h2 = 0) / 4..7 (h2 = 1)
-    if (h2 == 0) *reinterpret_cast<bf16x4*>(dst + 8) = v1;  // d 8..11
   }
+}
+
+template <int NP>
+void launch_flash_np(const AttnFlashArgs& a, int mode, size_t lds, hipStream_t st) {
+  const dim3 grid(cdiv(a.max_len, 128), a.nseq, mode == 0 ? 1 : a.H);
+  if (mode == 0)
+    hipLaunchKernelGGL((attn_flash_kernel<0, NP>), grid, dim3(256), lds, st, a);
+  else if (mode == 1)
+    hipLaunchKernelGGL((attn_flash_kernel<1, NP>), grid, dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((attn_flash_kernel<2, NP>), grid, dim3(256), lds, st, a);
 }
 
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
   ZASR_REQUIRE(a.H % 2 == 0, "attention: the bf16 kernels need an even head count (16-byte q/k rows)");
   const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
-  ZASR_REQUIRE(lds <= 140 * 1024, "attention: sequence too long for the bf16 kernel's LDS");
-  const dim3 grid(cdiv(a.max_len, 128), a.nseq, mode == 0 ? 1 : a.H);
-  if (mode == 0)
-    hipLaunchKernelGGL(attn_flash_kernel<0>, grid, dim3(256), lds, st, a);
-  else if (mode == 1)
-    hipLaunchKernelGGL(attn_flash_kernel<1>, grid, dim3(256), lds, st, a);
+  ZASR_REQUIRE(lds <= 120 * 1024, "attention: sequence too long for the flash kernel's LDS");
+  if (a.pieces == 1)
+    launch_flash_np<1>(a, mode, lds, st);
+  else if (a.pieces == 2)
+    launch_flash_np<2>(a, mode, lds, st);
+  else if (a.pieces == 3)
+    launch_flash_np<3>(a, mode, lds, st);
   else
-    hipLaunchKernelGGL(attn_flash_kernel<2>, grid, dim3(256), lds, st, a);
+    throw std::runtime_error("attention: pieces must be 1, 2 or 3");
 }
 
 // =====================================================================================
@@ -304,7 +436,8 @@ __device__ __forceinline__ float4 h3_load4(const __bf16* p) {
   return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
 }
 
-template <typename TH>
+// NP > 1 (split modes): NP bf16 pieces of t1 per element, piece t at t1t + t * hid * R8
+template <typename TH, int NP>
 __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict__ h3,
                                                             const int* __restrict__ off,
                                                             const int* __restrict__ o8,
@@ -348,25 +481,40 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict
     const int ch = c0 + cl;
     if (ch >= hid) break;
     __bf16* dst = t1t + (long)ch * R8;
-    dst[col] = (__bf16)tile[cl][rl];
-    if (last)
-      for (int z = col + 1; z < pad_end; ++z) dst[z] = (__bf16)0.f;
+    float v = tile[cl][rl];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const __bf16 hh = (__bf16)v;
+      dst[(long)t * hid * R8 + col] = hh;
+      if (t + 1 < NP) v -= (float)hh;
+      if (last)
+        for (int z = col + 1; z < pad_end; ++z) dst[(long)t * hid * R8 + z] = (__bf16)0.f;
+    }
   }
 }
 
 void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const int* o8,
-                          const int* map, int R, int hid, int R8, void* t1t, hipStream_t st) {
+                          const int* map, int R, int hid, int R8, void* t1t, hipStream_t st,
+                          int pieces) {
   if (R <= 0) return;
   ZASR_REQUIRE(hid % 4 == 0, "nonlin_prep_t: hid must be a multiple of 4");
+  ZASR_REQUIRE(pieces == 1 || (!h3_bf16 && (pieces == 2 || pieces == 3)),
+               "nonlin_prep_t: pieces must be 1 (or 2 / 3 for an f32 h3)");
   const dim3 grid(cdiv(R, 64), cdiv(hid, 64));
+  __bf16* out = reinterpret_cast<__bf16*>(t1t);
+  const float* h3f = reinterpret_cast<const float*>(h3);
   if (h3_bf16)
-    hipLaunchKernelGGL(nonlin_prep_t_kernel<__bf16>, grid, dim3(256), 0, st,
-                       reinterpret_cast<const __bf16*>(h3), off, o8, map, R, hid, R8,
-                       reinterpret_cast<__bf16*>(t1t));
+    hipLaunchKernelGGL((nonlin_prep_t_kernel<__bf16, 1>), grid, dim3(256), 0, st,
+                       reinterpret_cast<const __bf16*>(h3), off, o8, map, R, hid, R8, out);
+  else if (pieces == 1)
+    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 1>), grid, dim3(256), 0, st, h3f, off, o8,
+                       map, R, hid, R8, out);
+  else if (pieces == 2)
+    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 2>), grid, dim3(256), 0, st, h3f, off, o8,
+                       map, R, hid, R8, out);
   else
-    hipLaunchKernelGGL(nonlin_prep_t_kernel<float>, grid, dim3(256), 0, st,
-                       reinterpret_cast<const float*>(h3), off, o8, map, R, hid, R8,
-                       reinterpret_cast<__bf16*>(t1t));
+    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 3>), grid, dim3(256), 0, st, h3f, off, o8,
+                       map, R, hid, R8, out);
 }
 
 }  // namespace zasr

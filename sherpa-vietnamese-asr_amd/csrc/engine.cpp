@@ -913,6 +913,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     ZASR_HIP_CHECK(hipMemcpyAsync(O, X, (size_t)R * d * sizeof(float), hipMemcpyDeviceToDevice, st_));
   // attention weights (shared by nonlin_attention, self_attn1, self_attn2)
   const bool bf16 = precision_ == 1 || precision_ == 2;
+  const int np = split_pieces();
   float* qkp = nullptr;
   float* A = nullptr;
   __bf16* A16 = nullptr;
@@ -927,6 +928,18 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
     fa = AttnFlashArgs{qkp16, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A16,
                        nullptr, nullptr, stats, stats};
+    prof_begin("attn_softmax");
+    launch_attn_flash(fa, 0, st_);
+    prof_end();
+  } else if (np) {
+    // split-bf16 modes: the same flash kernels on f32 q / k / v, every MFMA product split
+    // into np bf16 pieces per operand; head 0's weights in f32 (L8 row stride)
+    qkp = ws<float>("ly_qkp", (size_t)R * 68 * h);
+    linear(Ly.attn_in, X, d, R, qkp, 68 * h, EPI_NONE);
+    A = ws<float>("ly_attn", 1);  // sized by the caller
+    stats = ws<float>("ly_attn_stats", (size_t)R * h);
+    fa = AttnFlashArgs{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A,
+                       nullptr, nullptr, stats, stats, np};
     prof_begin("attn_softmax");
     launch_attn_flash(fa, 0, st_);
     prof_end();
@@ -985,6 +998,16 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     float* vv = ws<float>("ly_vv", (size_t)R * 12 * h);
     float* oa = ws<float>("ly_oa", (size_t)R * 12 * h);
     linear(Ly.sa_in[k], X, d, R, vv, 12 * h, EPI_NONE);
+    if (np) {
+      AttnFlashArgs a = fa;
+      a.v = vv;
+      a.out = oa;
+      prof_begin("attn_apply");
+      launch_attn_flash(a, k == 0 ? 1 : 2, st_);
+      prof_end();
+      linear(Ly.sa_out[k], oa, 12 * h, R, X, d, EPI_RESADD);
+      return;
+    }
     AttnSAArgs sa{qkp, h, Ly.pos_tab, model_.pmax, d_off, B, maxL, stats, vv, oa, stats};
     prof_begin("attn_apply");
     launch_attn_sa(sa, k == 0, false, st_);
@@ -1042,6 +1065,34 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     gemm_bf16(p, t1t, EPI_MULAUX16, ALOAD_DENSE, st_, true, true);
     prof_end();
     linear_h(Ly.na_out, z, true, hid, R, X, false, d, EPI_RESADD);
+  } else if (np) {
+    // z = (A0 @ t1) * y on the split-bf16 GEMM: A0 [L][L8] f32 (split while staging),
+    // t1^T as np bf16 pieces [np][hid][R8] (the weight layout), y f32 in the epilogue
+    float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
+    __bf16* t1t = ws<__bf16>("ly_t1t_x", (size_t)np * hid * R8);
+    float* z = ws<float>("ly_z", (size_t)R * hid);
+    linear(Ly.na_in, X, d, R, h3, 3 * hid, EPI_NONE);
+    prof_begin("elementwise");
+    launch_nonlin_prep_t(h3, false, d_off, d_o8, d_map, R, hid, R8, t1t, st_, np);
+    prof_end();
+    GemmParams p{};
+    p.A = A;
+    p.B = nullptr;
+    p.sbk = 1;
+    p.sbn = R8;
+    p.C = z;
+    p.ldc = hid;
+    p.N = hid;
+    p.alpha = 1.f;
+    p.aux = h3 + 2 * hid;
+    p.ldaux = 3 * hid;
+    p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
+    p.num_slices = B;
+    p.max_M = maxL;
+    prof_begin("attn_nonlin");
+    gemm_x3(p, t1t, (long)hid * R8, EPI_MULAUX, ALOAD_DENSE, st_, np);
+    prof_end();
+    linear(Ly.na_out, z, hid, R, X, d, EPI_RESADD);
   } else {
     float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
     float* t1 = ws<float>("ly_t1", (size_t)R * hid);
@@ -1111,6 +1162,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   std::vector<std::vector<int>> o8(ns);
   std::vector<int> R8(ns, 0);
   const bool bf16 = precision_ == 1 || precision_ == 2;
+  // the flash attention path (bf16 and the split-bf16 modes): head-0 weights with L8 rows,
+  // NonlinAttention's B operand as t1^T columns
+  const bool flash = bf16 || split_pieces() > 0;
   size_t attn_floats = 0;
   int maxL_all = 0;
   for (int i = 0; i < ns; ++i) {
@@ -1124,16 +1178,16 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     int c8 = 0;
     for (int b = 0; b < B; ++b) {
       const int Lb = len[b], L4 = (Lb + 3) & ~3, L8 = (Lb + 7) & ~7;
-      const int Lp = bf16 ? L8 : L4;  // weight row stride (bf16: the GEMM's K padding)
+      const int Lp = flash ? L8 : L4;  // weight row stride (flash: the GEMM's K padding)
       aoff[i].push_back(acc);
       o8[i].push_back(c8);
       GemmSlice g{};
       g.a_off = acc;  // head 0 block of this sequence
-      g.b_off = bf16 ? (long)c8 : (long)mst[i].off[b] * hid;  // bf16: column of t1^T
+      g.b_off = flash ? (long)c8 : (long)mst[i].off[b] * hid;  // flash: column of t1^T
       g.c_off = (long)mst[i].off[b] * hid;
       g.aux_off = (long)mst[i].off[b] * 3 * hid;
       g.M = Lb;
-      g.K = bf16 ? L8 : Lb;
+      g.K = flash ? L8 : Lb;
       g.lda = Lp;
       sl_nl[i].push_back(g);
       acc += (long)Lb * Lp;  // only head 0 is materialised (nonlin_attention)

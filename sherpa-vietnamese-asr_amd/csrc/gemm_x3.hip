@@ -1,17 +1,17 @@
-// Split-bf16 ("bf16x3") MFMA GEMM: near-f32 products at bf16 MFMA rates.
+// Split-bf16 MFMA GEMM ("bf16x3" / "bf16x6" precision modes): near-f32 or f32-quality
+// products at bf16 MFMA rates.
 //
 //   C[m, n] = epi( sum_k A[m, k] * W[n, k] + bias[n] )
 //
-// Each f32 operand x is carried as two bf16 numbers, hi = bf16(x) and lo = bf16(x - hi)
-// (x - hi - lo is below 2^-17 |x|).  The product is accumulated as
-//   a_lo * w_hi + a_hi * w_lo + a_hi * w_hi
-// in f32 on v_mfma_f32_32x32x16_bf16 -- three MFMAs where the bf16 mode issues one; the
-// dropped a_lo * w_lo term and the two residuals leave a relative product error of ~2^-16
-// (bf16 alone: 2^-8).  The weights are split once at load (hi [N][K] then lo [N][K]); the
-// f32 activations are split while staging into LDS.  The encoder's projections are
-// HBM-bound with the MFMA pipes ~0.13 busy in the bf16 mode (profiles/r02/prof_r02e), so the
-// extra MFMAs mostly fill idle issue slots.  tests/precision_sim.py: the 68M model in this
-// mode decodes token-for-token like the fp32 oracle on test_gpu_e2e's chunks (bf16: TER 0.12).
+// Each f32 operand x is carried as NP bf16 pieces, p0 = bf16(x), p1 = bf16(x - p0), ...
+// NP = 2: the product is a1 w0 + a0 w1 + a0 w0 in f32 on v_mfma_f32_32x32x16_bf16 (three
+// MFMAs where the bf16 mode issues one); the dropped a1 w1 and the two split residuals leave
+// ~2^-16 relative per product (bf16 alone: 2^-8): encoder_out ~3e-5 from the fp32 oracle.
+// NP = 3: six MFMAs (every a_i w_j with i + j <= 2); what is dropped is below 2^-24, so the
+// result is of exact-f32 quality (encoder_out within 4e-6 of the oracle like the exact-f32
+// MFMA mode, token-exact; profiles/r03/precision/).  The weights are split once at load;
+// the f32 activations are split while staging into LDS.  v_mfma_f32_32x32x2_f32 (the fp32
+// mode) runs at 1/16 of the bf16 rate, so six bf16 MFMAs are 2.7x cheaper per product.
 //
 // Structure follows gemm_bf16_kernel (gemm.hip): BM x BN block tile on 4 waves, BK = 32
 // slabs staged through LDS as row-major [row][BK + 8] bf16 images (hi and lo of A and of W),
@@ -43,10 +43,13 @@ __device__ __forceinline__ void split8(const float4 x0, const float4 x1, bf16x8 
   }
 }
 
+// native exp2 / log forms (common.h; ~1e-7 absolute from the libm forms, below the f32
+// rounding of the values they feed): the libm log1pf(expf()) pair made the SwooshL-epilogue
+// shapes 2-3x slower than the plain ones (profiles/r03/x3_shape_table.json)
 template <int EPI>
 __device__ __forceinline__ float x3_act(float v) {
-  if constexpr (EPI == EPI_SWOOSHL) return swooshl(v);
-  if constexpr (EPI == EPI_SWOOSHR) return swooshr(v);
+  if constexpr (EPI == EPI_SWOOSHL) return swooshl_fast(v);
+  if constexpr (EPI == EPI_SWOOSHR) return swooshr_fast(v);
   return v;
 }
 

@@ -204,7 +204,7 @@ void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
 //   mode 2: self-attention with the statistics of mode 1 (stats_in)
 // stats: [R][H] c = row max + log2(row sum), log2 domain
 struct AttnFlashArgs {
-  const __bf16* qkp;       // [R][68 H]
+  const void* qkp;         // [R][68 H]: bf16 (pieces == 1) or f32
   int H;
   const float* pos_tab;    // [(2 pmax - 1)][4 H]
   int pmax;
@@ -212,17 +212,23 @@ struct AttnFlashArgs {
   const long* a_off;       // [B] (mode 0)
   int nseq;
   int max_len;
-  __bf16* attn;            // mode 0
-  const __bf16* v;         // [R][12 H]
-  __bf16* out;             // [R][12 H]
+  void* attn;              // mode 0: head 0's weights [L][L8] per sequence, bf16 / f32
+  const void* v;           // [R][12 H], bf16 / f32
+  void* out;               // [R][12 H], bf16 / f32
   const float* stats_in;   // mode 2
   float* stats_out;        // mode 1
+  // 1: bf16 q / k / v / out / weights, log2(e) folded into q and p (the bf16 mode);
+  // 2 / 3: f32 storage, every MFMA product split into 2 / 3 bf16 pieces per operand (the
+  // bf16x3 / bf16x6 modes; q and p unscaled)
+  int pieces = 1;
 };
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st);
 // t1t[c][o8_b + j] = bf16(tanh(h3[r][c]) * h3[r][hid + c]) for packed row r = off_b + j;
 // columns [o8_b + L_b, o8_b + L8_b) zero; t1t row stride R8 = sum_b L8_b
+// pieces > 1 (an f32 h3, the split modes): piece t of every value at t1t + t * hid * R8
 void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const int* o8,
-                          const int* map, int R, int hid, int R8, void* t1t, hipStream_t st);
+                          const int* map, int R, int hid, int R8, void* t1t, hipStream_t st,
+                          int pieces = 1);
 // fused self-attention consumer: out[:, 12h:12h+12] = softmax(S_h) V_h, recomputing S
 struct AttnSAArgs {
   const float* qkp;

@@ -52,15 +52,21 @@ struct Pb {
     p += n;
     return s;
   }
+  // fixed-width field (wire types 1 and 5): checked before the pointer moves
+  const uint8_t* fixed(size_t n) {
+    if ((size_t)(end - p) < n) throw std::runtime_error("onnx: truncated field");
+    const uint8_t* q = p;
+    p += n;
+    return q;
+  }
   void skip(uint32_t wire) {
     switch (wire) {
       case 0: varint(); break;
-      case 1: p += 8; break;
+      case 1: fixed(8); break;
       case 2: bytes(); break;
-      case 5: p += 4; break;
+      case 5: fixed(4); break;
       default: throw std::runtime_error("onnx: unsupported wire type");
     }
-    if (p > end) throw std::runtime_error("onnx: truncated field");
   }
 };
 
@@ -138,8 +144,7 @@ RawTensor parse_tensor(Span s) {
         std::memcpy(t.f32.data(), b.p, k * 4);
       } else if (w == 5) {
         float v;
-        std::memcpy(&v, pb.p, 4);
-        pb.p += 4;
+        std::memcpy(&v, pb.fixed(4), 4);
         t.f32.push_back(v);
       } else {
         pb.skip(w);
@@ -165,9 +170,13 @@ RawTensor parse_tensor(Span s) {
         else if (f2 == 2 && w2 == 2) v = q.bytes().str();
         else q.skip(w2);
       }
-      if (k == "location") t.ext_location = v;
-      else if (k == "offset") t.ext_offset = std::stol(v);
-      else if (k == "length") t.ext_length = std::stol(v);
+      try {
+        if (k == "location") t.ext_location = v;
+        else if (k == "offset") t.ext_offset = std::stol(v);
+        else if (k == "length") t.ext_length = std::stol(v);
+      } catch (const std::logic_error&) {
+        throw std::runtime_error("onnx: bad external_data " + k + " '" + v + "'");
+      }
     } else {
       pb.skip(w);
     }
@@ -215,10 +224,31 @@ void parse_file(const std::string& path, OnnxFile& of) {
   if (!have_graph) throw std::runtime_error("onnx: no graph in " + path);
 }
 
+// element count; negative dims or a count beyond 2^40 (a corrupt header) are errors, not a
+// huge allocation
 size_t numel_of(const std::vector<int64_t>& d) {
   size_t n = 1;
-  for (int64_t x : d) n *= (size_t)x;
+  for (int64_t x : d) {
+    if (x < 0) throw std::runtime_error("onnx: negative tensor dimension");
+    if (x != 0 && n > ((size_t)1 << 40) / (size_t)x)
+      throw std::runtime_error("onnx: tensor too large");
+    n *= (size_t)x;
+  }
   return n;
+}
+
+// external data must stay inside the model directory: a relative path without '..'
+void check_ext_location(const std::string& loc) {
+  if (loc.empty() || loc[0] == '/' || loc[0] == '\\')
+    throw std::runtime_error("onnx: external data location must be relative: " + loc);
+  size_t a = 0;
+  while (a <= loc.size()) {
+    size_t b = loc.find_first_of("/\\", a);
+    if (b == std::string::npos) b = loc.size();
+    if (loc.compare(a, b - a, "..") == 0 && b - a == 2)
+      throw std::runtime_error("onnx: external data location leaves the model directory: " + loc);
+    a = b + 1;
+  }
 }
 
 // the tensor's values as f32 (float / double / half / bfloat16 / int8 / uint8 / int32 / int64)
@@ -228,6 +258,7 @@ std::vector<float> to_f32(const RawTensor& t, const std::string& dir) {
   std::string ext;
   Span raw = t.raw;
   if (!t.ext_location.empty()) {
+    check_ext_location(t.ext_location);
     ext = read_file(dir + "/" + t.ext_location);
     const long len = t.ext_length >= 0 ? t.ext_length : (long)ext.size() - t.ext_offset;
     if (t.ext_offset < 0 || t.ext_offset + len > (long)ext.size())

@@ -81,9 +81,12 @@ VibertEngine::VibertEngine(const std::string& dir, int device) : device_(device)
   const HostTensor& we = W.get("bert.embeddings.word_embeddings.weight");
   ZASR_REQUIRE(we.shape.size() == 2 && we.shape[1] == H_, "ViBERT: bad word embedding shape");
   word_ = dev(we.data, we.numel);
+  vocab_ = (long)we.shape[0];
   pos_ = dev(get("bert.embeddings.position_embeddings.weight", (size_t)max_pos_ * H_), (size_t)max_pos_ * H_);
   const HostTensor& te = W.get("bert.embeddings.token_type_embeddings.weight");
+  ZASR_REQUIRE(te.shape.size() == 2 && te.shape[1] == H_, "ViBERT: bad token type embedding shape");
   type_ = dev(te.data, te.numel);
+  type_vocab_ = (long)te.shape[0];
   eln_g_ = dev(get("bert.embeddings.LayerNorm.weight", H_), H_);
   eln_b_ = dev(get("bert.embeddings.LayerNorm.bias", H_), H_);
   for (int i = 0; i < nl; ++i) {
@@ -140,6 +143,12 @@ void VibertEngine::run_host(const long* ids, const long* am, const long* tt, con
   const long R = (long)B * L;
   for (long i = 0; i < (long)B * W; ++i)
     ZASR_REQUIRE(offs[i] >= 0 && offs[i] < L, "ViBERT: input_offsets out of range");
+  // the embedding kernel gathers rows by id: an id outside the tables would read out of
+  // bounds on the device (onnxruntime's Gather raises instead)
+  for (long i = 0; i < R; ++i) {
+    ZASR_REQUIRE(ids[i] >= 0 && ids[i] < vocab_, "ViBERT: input_ids out of range");
+    ZASR_REQUIRE(tt[i] >= 0 && tt[i] < type_vocab_, "ViBERT: token_type_ids out of range");
+  }
   long* d_in = ws<long>("in", (size_t)R * 3 + (size_t)B * W);
   ZASR_HIP_CHECK(hipMemcpyAsync(d_in, ids, R * 8, hipMemcpyHostToDevice, st_));
   ZASR_HIP_CHECK(hipMemcpyAsync(d_in + R, am, R * 8, hipMemcpyHostToDevice, st_));

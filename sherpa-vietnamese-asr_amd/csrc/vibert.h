@@ -40,6 +40,7 @@ class VibertEngine {
   void gemm(const Lin& l, const float* A, int M, float* C, int epi);
 
   int device_ = 0, H_ = 0, heads_ = 0, inter_ = 0, labels_ = 0, detect_ = 0, max_pos_ = 0;
+  long vocab_ = 0, type_vocab_ = 0;  // embedding rows (id range checks in run_host)
   float eps_ = 1e-12f;
   hipStream_t st_ = nullptr;
   float *word_ = nullptr, *pos_ = nullptr, *type_ = nullptr, *eln_g_ = nullptr, *eln_b_ = nullptr;

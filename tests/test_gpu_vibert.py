@@ -65,3 +65,20 @@ def test_vibert_base_full_minibatch_matches_oracle(sessions):
     rl, rd = VibertOracle(cfg, w).run(ids, am, tt, off)
     _check(lg, rl)
     _check(dl, rd)
+
+
+def test_vibert_rejects_out_of_range_ids(sessions):
+    """input_ids / token_type_ids outside the embedding tables are an error (onnxruntime's
+    Gather raises; the device gather would read out of bounds), checked before any copy."""
+    from zasr.binding import ZasrError
+    cfg, w, sess = next(iter(sessions.values()))
+    c = CASES[0]
+    feeds = {k: np.array(GOLD[c + "_" + k]) for k in ("input_ids", "attention_mask",
+                                                      "token_type_ids", "input_offsets")}
+    for key, bad in (("input_ids", cfg.vocab_size), ("input_ids", -1),
+                     ("token_type_ids", cfg.type_vocab_size)):
+        f = {k: v.copy() for k, v in feeds.items()}
+        f[key][0, 1] = bad
+        with pytest.raises(ZasrError, match="out of range"):
+            sess.run(None, f)
+    sess.run(None, feeds)  # the session stays usable

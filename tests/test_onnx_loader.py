@@ -123,3 +123,65 @@ def test_dropin_create_recognizer_accepts_onnx_dir_files(tmp_path):
     assert not ae.model_files_present(src)
     with pytest.raises(FileNotFoundError):
         ae.create_recognizer(src)
+
+
+# ------------------------------------------------------------------ hostile / corrupt files
+def _write_enc_with(src, extra_init: bytes):
+    """Replace the encoder file of a valid tiny model dir with one whose graph carries one more
+    initializer (raw protobuf bytes)."""
+    import glob
+    from write_onnx import _bytes
+    enc = glob.glob(os.path.join(src, "encoder-*.onnx"))[0]
+    data = open(enc, "rb").read()
+    # append to the graph: ModelProto field 7 is re-emitted with the extra GraphProto.initializer
+    from write_onnx import _key, _varint
+    graph = _bytes(5, extra_init)
+    with open(enc, "wb") as f:
+        f.write(data + _key(7, 2) + _varint(len(graph)) + graph)
+
+
+def _tiny_dir(tmp_path):
+    cfg = zipformer_tiny(64)
+    src = str(tmp_path / "model")
+    write_model_dir(src, synth_weights(cfg, 11), synth_tokens(64))
+    return src
+
+
+def test_truncated_onnx_raises_not_crashes(tmp_path):
+    """A truncated file is an error at every cut point class (inside a varint, a length-
+    delimited field, a fixed-width field), never a read past the buffer."""
+    import glob
+    from zasr.binding import ZasrError
+    src = _tiny_dir(tmp_path)
+    enc = glob.glob(os.path.join(src, "encoder-*.onnx"))[0]
+    data = open(enc, "rb").read()
+    for cut in (1, 2, 7, 100, len(data) // 3, len(data) - 5, len(data) - 1):
+        with open(enc, "wb") as f:
+            f.write(data[:cut])
+        with pytest.raises(ZasrError):
+            convert_model(src, str(tmp_path / f"out{cut}"))
+
+
+def test_external_data_outside_model_dir_rejected(tmp_path):
+    from write_onnx import _bytes, _key, _str, _varint
+    from zasr.binding import ZasrError
+    for loc in ("../secret.bin", "/etc/passwd", "a/../../b"):
+        src = _tiny_dir(tmp_path / loc.replace("/", "_").replace(".", "d"))
+        entry = lambda k, v: _bytes(13, _str(1, k) + _str(2, v))  # noqa: E731
+        t = (_key(1, 0) + _varint(4) + _key(2, 0) + _varint(1) + _str(8, "encoder.extra")
+             + entry("location", loc) + entry("offset", "0") + entry("length", "16")
+             + _key(14, 0) + _varint(1))
+        _write_enc_with(src, t)
+        with pytest.raises(ZasrError, match="external data"):
+            convert_model(src, str(tmp_path / "o" / loc.replace("/", "_")))
+
+
+def test_negative_dims_rejected(tmp_path):
+    from write_onnx import _bytes, _key, _str, _varint
+    from zasr.binding import ZasrError
+    src = _tiny_dir(tmp_path)
+    neg = _varint((1 << 64) - 3)  # int64 -3 as a protobuf varint
+    t = _key(1, 0) + neg + _key(2, 0) + _varint(1) + _str(8, "encoder.bad") + _bytes(9, b"")
+    _write_enc_with(src, t)
+    with pytest.raises(ZasrError, match="negative"):
+        convert_model(src, str(tmp_path / "out"))
