@@ -13,17 +13,11 @@
 #include <type_traits>
 
 #include "common.h"
+#include "gemm_dev.h"
 #include "kernels.h"
 
 namespace zasr {
 
-namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
-}  // namespace
 
 // =====================================================================================
 // bf16-mode attention (RelPositionMultiheadAttentionWeights + SelfAttention, icefall
@@ -61,36 +55,6 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 // issues one): near-f32 (NP = 2) / f32-quality (NP = 3) scores and outputs at bf16 MFMA rates
 // (the bf16x3 / bf16x6 modes).  In these modes q and p carry no log2(e) factor: the score is
 // scaled into the log2 domain after the positional term.
-template <int NP>
-__device__ __forceinline__ void split_f8(const float (&v)[8], bf16x8 (&pc)[NP]) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float r = v[q];
-#pragma unroll
-    for (int t = 0; t < NP; ++t) {
-      const __bf16 h = (__bf16)r;
-      pc[t][q] = h;
-      if (t + 1 < NP) r -= (float)h;
-    }
-  }
-}
-
-// acc += sum over u + v < NP of x[u] * y[v], smallest terms first (written out: every index
-// a constant, so the piece arrays stay in registers)
-template <int NP>
-__device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&x)[NP], const bf16x8 (&y)[NP], f32x16 acc) {
-#define ZASR_MF(u, v) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[u], y[v], acc, 0, 0, 0)
-  if constexpr (NP == 3) {
-    ZASR_MF(2, 0); ZASR_MF(1, 1); ZASR_MF(0, 2);
-  }
-  if constexpr (NP >= 2) {
-    ZASR_MF(NP - 1 == 1 ? 1 : 1, 0); ZASR_MF(0, 1);
-  }
-  ZASR_MF(0, 0);
-#undef ZASR_MF
-  return acc;
-}
-
 template <int MODE, int NP>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;

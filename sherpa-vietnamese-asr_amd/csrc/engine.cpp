@@ -469,7 +469,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
       l.wx = p;
     };
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
-                    &model_.enc_proj})
+                    &model_.enc_proj, &model_.joiner})
       mkx(*l);
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
@@ -1499,6 +1499,8 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
         } else {
           JoinerArgs ja{reinterpret_cast<const float*>(Js), model_.joiner.w, model_.joiner.b, lg,
                         S * F, V, D, d_t, d_el, F};
+          ja.Wx = reinterpret_cast<const __bf16*>(model_.joiner.wx);
+          ja.pieces = split_pieces();
           launch_joiner(ja, st_);
         }
         prof_end();
@@ -1616,6 +1618,8 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
         launch_joiner_bf16(ja, st_);
       } else {
         JoinerArgs ja{reinterpret_cast<const float*>(q.J), model_.joiner.w, model_.joiner.b, q.logits, rows, V, D};
+        ja.Wx = reinterpret_cast<const __bf16*>(model_.joiner.wx);
+        ja.pieces = split_pieces();
         launch_joiner(ja, st_);
       }
       prof_end();

@@ -58,4 +58,35 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
   return xcd < rem ? xcd * (per + 1) + slot : rem * (per + 1) + (xcd - rem) * per + slot;
 }
 
+// ---- split-bf16 helpers (the bf16x3 / bf16x6 modes) ----
+template <int NP>
+__device__ __forceinline__ void split_f8(const float (&v)[8], bf16x8 (&pc)[NP]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float r = v[q];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const __bf16 h = (__bf16)r;
+      pc[t][q] = h;
+      if (t + 1 < NP) r -= (float)h;
+    }
+  }
+}
+
+// acc += sum over u + v < NP of x[u] * y[v], smallest terms first (written out: every index
+// a constant, so the piece arrays stay in registers)
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_split(const bf16x8 (&x)[NP], const bf16x8 (&y)[NP], f32x16 acc) {
+#define ZASR_MF(u, v) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[u], y[v], acc, 0, 0, 0)
+  if constexpr (NP == 3) {
+    ZASR_MF(2, 0); ZASR_MF(1, 1); ZASR_MF(0, 2);
+  }
+  if constexpr (NP >= 2) {
+    ZASR_MF(NP - 1 == 1 ? 1 : 1, 0); ZASR_MF(0, 1);
+  }
+  ZASR_MF(0, 0);
+#undef ZASR_MF
+  return acc;
+}
+
 }  // namespace zasr

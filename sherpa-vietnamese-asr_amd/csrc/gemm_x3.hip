@@ -57,11 +57,11 @@ __device__ __forceinline__ float x3_act(float v) {
 // NP = 3 ("bf16x6"): pieces (p0, p1, p2), the six products p_i q_j with i + j <= 2 (6 MFMAs,
 // dropped terms below 2^-24 relative: exact-f32 quality), BK = 16 (same MFMAs per slab and
 // the same LDS as NP = 2).  Weights: piece t at Bw + t * blo.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP, int NP>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP, int NP,
+          int BK = (NP == 2 ? 32 : 16)>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmParams p,
                                                                        const __bf16* Bw, long blo,
                                                                        int tiles_n, int tiles_m) {
-  constexpr int BK = NP == 2 ? 32 : 16;
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WTM = BM / WAVES_M;
   constexpr int WTN = BN / WAVES_N;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
 
   const int nkt = (K + BK - 1) / BK;
   if constexpr (DEEP) {
-    // dense A, K a multiple of 64 (host-checked): two register sets, LDS-only barriers
+    // dense A, K a multiple of 2 BK (host-checked): two register sets, LDS-only barriers
     // (__syncthreads would drain the slab in flight with vmcnt(0)), slab indices clamped so
     // every load is unconditional and the in-order vmcnt waits stay exact
     Regs x0, x1;
@@ -332,16 +332,16 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ALOAD, int EPI, int NP>
+template <int BM, int BN, int WM, int WN, int ALOAD, int EPI, int NP, int BK = (NP == 2 ? 32 : 16)>
 void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
-  if (ALOAD == ALOAD_DENSE && !p.slices && p.K % 64 == 0 && p.lda % 4 == 0) {
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP>), grid,
+  if (ALOAD == ALOAD_DENSE && !p.slices && p.K % (2 * BK) == 0 && p.lda % 4 == 0) {
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP, BK>), grid,
                        dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
     return;
   }
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP>), grid,
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP, BK>), grid,
                      dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
 }
 

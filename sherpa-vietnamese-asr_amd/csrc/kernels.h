@@ -314,6 +314,9 @@ struct JoinerArgs {
   const int* live_t = nullptr;
   const int* live_len = nullptr;
   int live_f = 0;
+  // split-bf16 modes: W_out as `pieces` bf16 pieces (piece t at Wx + t V D); J stays f32
+  const __bf16* Wx = nullptr;
+  int pieces = 0;
 };
 struct JoinerBf16Args {
   const __bf16* J;       // [M][D]

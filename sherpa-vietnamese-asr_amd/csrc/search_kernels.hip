@@ -20,13 +20,12 @@
 // decoder_proj on MFMA) and writes J.
 // All hypothesis state lives in LDS during the step; global memory is written once.
 #include "common.h"
+#include "gemm_dev.h"
 #include "kernels.h"
 
 #include <cstdlib>
 
 namespace zasr {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -125,9 +124,6 @@ __device__ __forceinline__ void splitk_reduce(f32x16& acc, float* red) {
       acc[r] += red[r * 64 + lane] + red[(16 + r) * 64 + lane] + red[(32 + r) * 64 + lane];
   }
 }
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 // all streams of joiner rows m0 .. m0 + 31 finished (speculative greedy windows)
 __device__ __forceinline__ bool tile_done(const int* live_t, const int* live_len, int F, int m0,
@@ -437,8 +433,19 @@ __global__ __launch_bounds__(256) void joiner_kernel(JoinerArgs j) {
   }
 }
 
+template <int NP>
+void launch_joiner_split(const JoinerArgs& j, hipStream_t st);
+
 void launch_joiner(const JoinerArgs& j, hipStream_t st) {
   if (j.M <= 0) return;
+  if (j.Wx != nullptr) {  // split-bf16 modes (defined below)
+    ZASR_REQUIRE(j.pieces == 2 || j.pieces == 3, "joiner: pieces must be 2 or 3");
+    if (j.pieces == 2)
+      launch_joiner_split<2>(j, st);
+    else
+      launch_joiner_split<3>(j, st);
+    return;
+  }
   ZASR_REQUIRE(j.D % 32 == 0 && j.D <= 512, "joiner_dim must be a multiple of 32, <= 512");
   dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
   size_t lds = (32 * (j.D + 4) + 3 * 16 * 64) * sizeof(float);
@@ -500,6 +507,70 @@ void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
     case 128: hipLaunchKernelGGL(joiner_bf16_kernel<2>, grid, dim3(256), 0, st, j); break;
     case 256: hipLaunchKernelGGL(joiner_bf16_kernel<4>, grid, dim3(256), 0, st, j); break;
     case 512: hipLaunchKernelGGL(joiner_bf16_kernel<8>, grid, dim3(256), 0, st, j); break;
+    default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// split-bf16 joiner (the bf16x3 / bf16x6 modes): J f32 split into NP bf16 pieces as it is
+// loaded, W_out pre-split (piece t at Wx + t V D); the products of the pieces (3 / 6 MFMAs per
+// k16 step) accumulate in f32 -- near-f32 / f32-quality logits at bf16 MFMA rates.  Same
+// block / wave / split-K structure as joiner_bf16_kernel.
+// --------------------------------------------------------------------------------------
+template <int NK, int NP>
+__global__ __launch_bounds__(256) void joiner_split_kernel(JoinerArgs j) {
+  __shared__ float red[3 * 16 * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.y * 32;
+  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M)) return;
+  const int n = blockIdx.x * 32 + col;
+  const bool nv = n < j.V;
+  const int D = j.D;
+  const long blo = (long)j.V * D;
+  const int ar = m0 + col < j.M ? m0 + col : j.M - 1;
+  const int kb = wid * (D / 4) + 8 * h;
+  const float* arow = j.J + (long)ar * D + kb;
+  const __bf16* brow = j.Wx + (long)(nv ? n : 0) * D + kb;
+  float4 x0[NK], x1[NK];
+  bf16x8 b[NP][NK];
+#pragma unroll
+  for (int q = 0; q < NK; ++q) {
+    x0[q] = *reinterpret_cast<const float4*>(arow + 16 * q);
+    x1[q] = *reinterpret_cast<const float4*>(arow + 16 * q + 4);
+#pragma unroll
+    for (int t = 0; t < NP; ++t) b[t][q] = *reinterpret_cast<const bf16x8*>(brow + t * blo + 16 * q);
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int q = 0; q < NK; ++q) {
+    const float v[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w, x1[q].x, x1[q].y, x1[q].z, x1[q].w};
+    bf16x8 ap[NP], bp[NP];
+    split_f8<NP>(v, ap);
+#pragma unroll
+    for (int t = 0; t < NP; ++t) bp[t] = b[t][q];
+    acc = mfma_split<NP>(ap, bp, acc);
+  }
+  splitk_reduce(acc, red);
+  if (wid != 0 || !nv) return;
+  const float bias = j.bias[n];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < j.M) j.out[(long)row * j.V + n] = acc[r] + bias;
+  }
+}
+
+template <int NP>
+void launch_joiner_split(const JoinerArgs& j, hipStream_t st) {
+  dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
+  switch (j.D) {
+    case 64: hipLaunchKernelGGL((joiner_split_kernel<1, NP>), grid, dim3(256), 0, st, j); break;
+    case 128: hipLaunchKernelGGL((joiner_split_kernel<2, NP>), grid, dim3(256), 0, st, j); break;
+    case 256: hipLaunchKernelGGL((joiner_split_kernel<4, NP>), grid, dim3(256), 0, st, j); break;
+    case 512: hipLaunchKernelGGL((joiner_split_kernel<8, NP>), grid, dim3(256), 0, st, j); break;
     default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
   }
 }
