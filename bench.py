@@ -67,6 +67,14 @@ def parse_args(argv=None):
     ap.add_argument("--beam", type=int, default=8)
     ap.add_argument("--audio-sec", type=float, default=3600.0)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6"])
+    ap.add_argument("--parity-precision", default="bf16x6",
+                    choices=["none", "fp32", "bf16x6", "bf16x3"],
+                    help="asr stage: also time this token-exact precision mode on the same "
+                         "workload in the same run and report it as the line's `parity_mode` "
+                         "(bf16x6: split-bf16 products of exact-f32 quality, token-for-token "
+                         "equal to the fp32 oracle; tests/test_gpu_e2e.py "
+                         "test_m_bf16_token_error_rate)")
+    ap.add_argument("--parity-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5,
                     help="CPU baseline: 1 warm-up then the mean of this many repeats "
@@ -592,7 +600,7 @@ def _pipe_cpu_job(job):
     from zasr.pipeline import punctuate, split_word_chunks, vibert_feeds
     from zasr.vibert import synth_weights as vib_weights
     from zasr.vibert import vibert_base
-    model, threads, chunks, offs, regions = job
+    model, threads, chunks, offs, regions, repeats = job
     torch.set_num_threads(threads)
     cfg = PRESETS[model]()
     orc = ZipformerOracle(cfg, synth_weights(cfg, WEIGHT_SEED))
@@ -608,24 +616,31 @@ def _pipe_cpu_job(job):
             return list(vorc.run(feeds["input_ids"], feeds["attention_mask"],
                                  feeds["token_type_ids"], feeds["input_offsets"]))
 
-    orc.encoder(fbank(chunks[0][:SR * 2]))  # warm-up
-    t0 = time.perf_counter()
-    per = []
-    for c, off in zip(chunks, offs):
-        enc = orc.encoder(fbank(c))
-        tk, fr, lp, T, emit = beam_search(enc, orc.decoder, orc.joiner, 1)
-        per.append({"words": _words_from_search(id2, cfg.vocab_size, len(c), off / SR, tk, fr, lp,
-                                                T, emit),
-                    "audio_start_abs": off / SR, "audio_end_abs": (off + len(c)) / SR})
-    words, _ = merge_chunks_with_overlap(per)
-    wins = []
-    for r in regions:
-        fb = campp_fbank(r)
-        wins += [fb[a:a + n] for a, n in window_plan(fb.shape[0]) if n == 150]
-    for b in range(0, len(wins), 32):
-        corc.embed(np.stack(wins[b:b + 32]))
-    punctuate(Sess(), [w["text"] for w in words], vcfg.vocab_size)
-    return time.perf_counter() - t0, len(words), len(wins)
+    def one_pass():
+        per = []
+        for c, off in zip(chunks, offs):
+            enc = orc.encoder(fbank(c))
+            tk, fr, lp, T, emit = beam_search(enc, orc.decoder, orc.joiner, 1)
+            per.append({"words": _words_from_search(id2, cfg.vocab_size, len(c), off / SR, tk,
+                                                    fr, lp, T, emit),
+                        "audio_start_abs": off / SR, "audio_end_abs": (off + len(c)) / SR})
+        words, _ = merge_chunks_with_overlap(per)
+        wins = []
+        for r in regions:
+            fb = campp_fbank(r)
+            wins += [fb[a:a + n] for a, n in window_plan(fb.shape[0]) if n == 150]
+        for b in range(0, len(wins), 32):
+            corc.embed(np.stack(wins[b:b + 32]))
+        punctuate(Sess(), [w["text"] for w in words], vcfg.vocab_size)
+        return len(words), len(wins)
+
+    one_pass()  # warm-up (core/calibration.py:822-830: 1 warm-up, then the mean of repeats)
+    times = []
+    for _ in range(max(1, repeats)):
+        t0 = time.perf_counter()
+        nw, nwin = one_pass()
+        times.append(time.perf_counter() - t0)
+    return times, nw, nwin
 
 
 def bench_pipe(args):
@@ -661,15 +676,17 @@ def bench_pipe(args):
         regs = [audio[a:e] for a, e, _ in plan_chunks(audio, overlap_sec=0.0) if e <= end]
         threads = min(16, os.cpu_count() or 1)
         with mp.get_context("spawn").Pool(1) as pool:
-            el_cpu, nw, nwin = pool.map(_pipe_cpu_job, [(args.model, threads,
-                                                         [audio[a:e] for a, e, _ in plan],
-                                                         [a for a, _, _ in plan], regs)])[0]
+            times, nw, nwin = pool.map(_pipe_cpu_job, [(args.model, threads,
+                                                        [audio[a:e] for a, e, _ in plan],
+                                                        [a for a, _, _ in plan], regs,
+                                                        args.cpu_repeats)])[0]
+        el_cpu = float(np.mean(times))
         cpu = {"value": round(end / SR / el_cpu, 3), "unit": "audio-sec/sec", "cores": threads,
-               "kind": "port", "repeats": 1,
+               "kind": "port", "repeats": len(times), "repeat_s": [round(t, 3) for t in times],
                "sample": f"the first {end / SR:.1f} s (2 planner chunks): oracle decode (greedy) "
                          f"+ words + merge, CAM++ oracle on {nwin} windows (batches of 32), 3 "
                          f"ViBERT oracle passes over {nw} words (mini-batches of 32); torch fp32, "
-                         f"{threads} threads, one timed pass after a warm-up"}
+                         f"{threads} threads, 1 warm-up + mean of {len(times)}"}
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -802,7 +819,7 @@ def _rover_cpu_job(job):
     from zasr.asr_engine import _words_from_search
     from zasr.model import PRESETS, synth_tokens, synth_weights
     from zasr.rover import rover_merge
-    threads, chunks, offs, beam, hw_path, phrases = job
+    threads, chunks, offs, beam, hw_path, phrases, repeats = job
     torch.set_num_threads(threads)
     models = []
     for name, seed in (("zipformer-30m", WEIGHT_SEED + 1), ("zipformer-68m", WEIGHT_SEED)):
@@ -811,18 +828,26 @@ def _rover_cpu_job(job):
         models.append((cfg, ZipformerOracle(cfg, synth_weights(cfg, seed)),
                        dict(enumerate(synth_tokens(cfg.vocab_size))),
                        HotwordGraph(*hw) if hw and hw[0] else None))
-    models[0][1].encoder(fbank(chunks[0][:SR * 2]))  # warm-up
-    t0 = time.perf_counter()
-    n_words = 0
-    for c, off in zip(chunks, offs):
-        f = fbank(c)
-        per = []
-        for cfg, orc, id2, graph in models:
-            tk, fr, lp, T, emit = beam_search(orc.encoder(f), orc.decoder, orc.joiner, beam, graph)
-            per.append(_words_from_search(id2, cfg.vocab_size, len(c), off / SR, tk, fr, lp, T,
-                                          emit))
-        n_words += len(rover_merge(per[0], per[1], phrases)[0])
-    return time.perf_counter() - t0, n_words
+    def one_pass():
+        n_words = 0
+        for c, off in zip(chunks, offs):
+            f = fbank(c)
+            per = []
+            for cfg, orc, id2, graph in models:
+                tk, fr, lp, T, emit = beam_search(orc.encoder(f), orc.decoder, orc.joiner, beam,
+                                                  graph)
+                per.append(_words_from_search(id2, cfg.vocab_size, len(c), off / SR, tk, fr, lp,
+                                              T, emit))
+            n_words += len(rover_merge(per[0], per[1], phrases)[0])
+        return n_words
+
+    one_pass()  # warm-up (core/calibration.py:822-830: 1 warm-up, then the mean of repeats)
+    times = []
+    for _ in range(max(1, repeats)):
+        t0 = time.perf_counter()
+        n_words = one_pass()
+        times.append(time.perf_counter() - t0)
+    return times, n_words
 
 
 def bench_rover(args):
@@ -854,14 +879,16 @@ def bench_rover(args):
         import multiprocessing as mp
         threads = min(16, os.cpu_count() or 1)
         with mp.get_context("spawn").Pool(1) as pool:
-            el_cpu, nw = pool.map(_rover_cpu_job, [(threads, chunks[:1], offs[:1], beam, hw_path,
-                                                    phrases)])[0]
+            times, nw = pool.map(_rover_cpu_job, [(threads, chunks[:1], offs[:1], beam, hw_path,
+                                                   phrases, args.cpu_repeats)])[0]
+        el_cpu = float(np.mean(times))
         cpu = {"value": round(lens[0] / SR / el_cpu, 3), "unit": "audio-sec/sec",
-               "cores": threads, "kind": "port", "repeats": 1,
+               "cores": threads, "kind": "port", "repeats": len(times),
+               "repeat_s": [round(t, 3) for t in times],
                "sample": f"the first planner chunk ({lens[0] / SR:.1f} s): oracle fbank once, "
                          f"30M and 68M torch fp32 encoders + the reference search (beam {beam}"
                          f"{' + hotwords' if phrases else ''}), words, block vote ({nw} words); "
-                         f"{threads} threads, one timed pass after a warm-up"}
+                         f"{threads} threads, 1 warm-up + mean of {len(times)}"}
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -946,6 +973,84 @@ def bench_rover(args):
         r.close()
     if dist:
         dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ token-exact mode
+SPLIT_PRODUCTS = {"bf16x3": 3, "bf16x6": 6}
+
+
+def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream, fl_step,
+                     L_list, dist, dev):
+    """The same workload (same audio in HBM, same batched pipeline, same step count semantics)
+    in the token-exact precision mode: xRT, ms per step, the end-to-end roofline against the
+    f32 MFMA peak (the precision the mode reproduces) and, for the split-bf16 modes, the
+    fraction of the bf16 MFMA peak their split products occupy; the dominant kernel class's
+    roofline from the library's HIP-event class profile."""
+    import torch
+    from zasr.binding import Recognizer
+    prec = args.parity_precision
+    rec = Recognizer(mdir, args.method, beam, hotwords=hotwords[0] if hotwords else None,
+                     hotword_scores=hotwords[1] if hotwords else None,
+                     device_id=int(os.environ.get("LOCAL_RANK", "0")), precision=prec)
+    n = len(lens)
+    k = max(1, args.parity_steps)
+
+    def steps(m):
+        return rec.decode_device_batches(d_wav.data_ptr(), offs * m, lens * m, [n] * m,
+                                         beam=beam, stream=stream)
+
+    steps(1)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps(k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        from zasr.shard import max_over_ranks
+        el = max_over_ranks(el, device=dev)
+    rec.profile(1)
+    rec.profile_reset()
+    rec.decode_device(d_wav.data_ptr(), offs, lens, beam=beam, stream=stream)
+    torch.cuda.synchronize()
+    classes = rec.profile_report()
+    rec.profile(0)
+    rec.close()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    t_step = el / k
+    f32_tf = fl_step / t_step / 1e12
+    out = {"precision": prec, "value": round(args.audio_sec * world * k / el, 2),
+           "unit": "audio-sec/sec", "steps": k, "ms_per_step": round(1000 * t_step, 3),
+           "token_exact": prec in ("fp32", "bf16x6"),
+           "parity_evidence": "tests/test_gpu_e2e.py::test_m_bf16_token_error_rate (token error "
+                              "rate 0.0 vs the fp32 oracle, greedy and beam 8 + hotwords; "
+                              "profiles/r03/precision/)",
+           "roofline_e2e": {"flops_per_step": fl_step, "achieved": round(f32_tf, 2),
+                            "unit": "TFLOP/s", "peak_f32_mfma": MFMA_F32_PEAK_TFLOPS,
+                            "frac_of_f32_mfma_peak": round(f32_tf / MFMA_F32_PEAK_TFLOPS, 4)},
+           "kernel_classes_ms_per_step": {kk: round(v[1], 3) for kk, v in classes.items()}}
+    if prec in SPLIT_PRODUCTS:
+        mf = SPLIT_PRODUCTS[prec] * f32_tf
+        out["roofline_e2e"].update({"split_mfma_tflops": round(mf, 2),
+                                    "frac_of_bf16_mfma_peak": round(mf / MFMA_BF16_PEAK_TFLOPS, 4)})
+    if classes:
+        dom, (cnt, ms) = max(classes.items(), key=lambda kv: kv[1][1])
+        per = ms / cnt * 1e-3
+        if dom == "enc_gemm":
+            f_cls = gemm_class_work(cfg, L_list, False)["enc_gemm"][0]
+            tf = f_cls / cnt / per / 1e12
+            out["roofline"] = {"kernel": dom, "bound": "mfma", "avg_launch_ms": round(per * 1e3, 4),
+                               "launches_per_step": cnt, "f32_tflops": round(tf, 2),
+                               "frac_of_f32_mfma_peak": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
+            if prec in SPLIT_PRODUCTS:
+                out["roofline"]["frac_of_bf16_mfma_peak"] = round(
+                    SPLIT_PRODUCTS[prec] * tf / MFMA_BF16_PEAK_TFLOPS, 4)
+        else:
+            out["roofline"] = {"kernel": dom, "avg_launch_ms": round(per * 1e3, 4),
+                               "launches_per_step": cnt}
+    return out
 
 
 # ------------------------------------------------------------------ drop-in loop
@@ -1243,6 +1348,22 @@ def main():
             roof["traffic"] = tr["bytes_per_launch"]
             roof["traffic_source"] = tr["source"]
 
+    # fbank GB/s against HBM -- algorithmic bytes = the f32 samples read + the
+    # f32 [T][80] features written, per step, over the class's HIP-event time
+    fb_roof = None
+    if "fbank" in classes:
+        fb_bytes = sum(4 * n + 320 * ((n + 80) // 160) for n in lens)
+        fb_s = classes["fbank"][1] / nprof * 1e-3
+        fb_roof = {"bound": "hbm", "bytes_per_step": fb_bytes,
+                   "ms_per_step": round(fb_s * 1e3, 4),
+                   "achieved": round(fb_bytes / fb_s / 1e9, 1), "unit": "GB/s",
+                   "peak": HBM_PEAK_GBS, "frac": round(fb_bytes / fb_s / 1e9 / HBM_PEAK_GBS, 4)}
+    parity = None
+    if (rec is not None and args.parity_precision != "none"
+            and args.parity_precision != args.precision):
+        parity = parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
+                                  fl_step, L_list, dist, dev)
+
     if rank == 0:
         hw_tag = (f" + hotwords ({len(hotwords[0])} phrases of {os.path.basename(hw_path)})"
                   if hotwords else "")
@@ -1270,7 +1391,9 @@ def main():
             "roofline": roof,
             "roofline_e2e": e2e,
             "kernel_classes_ms_per_step": {k: round(v[1] / nprof, 3) for k, v in classes.items()},
+            "fbank_roofline": fb_roof,
             "cpu_baseline": cpu,
+            "parity_mode": parity,
         }
         if args.cpu_dry_run:
             line["dry_run"] = True

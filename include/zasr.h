@@ -213,9 +213,11 @@ int zasr_vad_probs_device(zasr_vad* h, const float* d_audio, const int64_t* offs
                           const int64_t* lengths, int32_t n_files, int32_t auto_boost,
                           float* d_probs, void* stream);
 /* recurrence passes of the last probs call: a long file is decoded as parallel segments whose
-   chained start states are verified bit-exactly against the sequential recurrence (1 = the
-   warm-up guesses were all exact; set ZASR_VAD_PIT=0 before create for one workgroup per
-   file) */
+   chained start states are checked against their predecessors' end states to a relative
+   1e-6 per element (the rounding-noise level of two summation orders; NOT bit-exact: the
+   probabilities stay within ~2.4e-7 of the sequential recurrence and give the same speech
+   segments, tests/test_gpu_vad.py).  1 = every warm-up guess passed; set ZASR_VAD_PIT=0
+   before create for one sequential workgroup per file */
 int32_t zasr_vad_last_passes(const zasr_vad* h);
 /* one session.run step for n independent streams: input [n][576], state [2][n][128] ->
    prob [n], state_out [2][n][128] (the ORT session surface, vad_utils.py:100-102) */

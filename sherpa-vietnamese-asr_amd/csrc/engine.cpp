@@ -1848,8 +1848,20 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
     std::vector<TokenResult> r = search_stage(pd[k % (L + 1)], beam);
     for (auto& x : r) out.push_back(std::move(x));
   }
+  order_after_encoders(enc_st, E, main_st);
   st_ = stream_;
   return out;
+}
+
+void Engine::order_after_encoders(const hipStream_t* enc_st, int E, hipStream_t main_st) {
+  // the caller's stream must not run ahead of an encoder stream that read its audio: a batch
+  // without valid chunks is never searched, so nothing else orders its fbank / encoder work
+  // (on a CU-masked stream_ or a second encoder stream) before the caller reuses the buffer
+  for (int e = 0; e < E; ++e) {
+    if (enc_st[e] == main_st) continue;
+    ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 2], enc_st[e]));
+    ZASR_HIP_CHECK(hipStreamWaitEvent(main_st, part_ev_[kMaxEnc + 2], 0));
+  }
 }
 
 std::vector<TokenResult> Engine::decode_batches_two_searches(const float* d_wav,

@@ -232,6 +232,8 @@ class Engine {
   int device_ = 0;
   int beam_ = 8;
   [[maybe_unused]] bool greedy_ = false;
+  // make main_st wait for every encoder stream of a batch pipeline that is not main_st
+  void order_after_encoders(const hipStream_t* enc_st, int E, hipStream_t main_st);
   int precision_ = 0;
   // bf16 pieces per operand of the split-bf16 modes (bf16x3: 2, bf16x6: 3), 0 otherwise
   int split_pieces() const { return precision_ == 3 ? 2 : precision_ == 4 ? 3 : 0; }

@@ -161,6 +161,9 @@ class FullPipe:
         self.d_feats = torch.empty((self.cap, 150, 80), dtype=torch.float32, device="cuda")
         self.d_emb = torch.empty((self.cap, self.emb.dim), dtype=torch.float32, device="cuda")
         self.s_campp = torch.cuda.Stream()
+        # the audio upload above ran on the current stream: complete it here, so the CAM++
+        # stream (which reads only the audio) never has to wait on the decode stream
+        torch.cuda.synchronize()
 
     def decode(self, stream: int, passes: int = 1):
         """Results of `passes` decodes of the file's chunks (one call: consecutive batches
@@ -217,14 +220,16 @@ class FullPipe:
                 if ci + 1 < len(calls):
                     fut = ex.submit(self.decode, main.cuda_stream, calls[ci + 1])
                 for p in range(passes):
-                    self.s_campp.wait_stream(main)
-                    # CAM++ on its own stream: it reads only the audio
+                    # CAM++ on its own stream: it reads only the (already uploaded) audio, so
+                    # it is not ordered behind the next passes' decode queued on `main`
                     reg, first, nfr = self.embed_windows(self.s_campp.cuda_stream)
                     words, tokens = self.words(res_all[p * n:(p + 1) * n])
                     labels, runs = punctuate(self.vib, [w["text"] for w in words],
                                              self.vib_vocab, self.iterations, self.vib_batch)
-                    self.s_campp.synchronize()
-                    embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
+                    # the copy runs on (and waits for) the CAM++ stream only, never on `main`
+                    # where the next decode is in flight
+                    with torch.cuda.stream(self.s_campp):
+                        embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
                     outs.append({"words": words, "tokens": tokens, "labels": labels,
                                  "vibert_runs": runs, "embeddings": embs,
                                  "windows": np.stack([reg, first, nfr], 1)})

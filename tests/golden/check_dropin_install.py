@@ -16,7 +16,15 @@ then ours, then the other order in a second process), imports the reference's ow
   * create_recognizer's hotword route goes through the reference's get_hotwords_config
     (core/config.py:385-408): the file it prepares from the reference's hotword.txt and its
     score 1.5 are what this build uses.
-Prints "dropin install ok" and exits 0 on success.
+  * the reference's own, unchanged TranscriberPipeline (core/asr_engine.py:1877-3459) run
+    over the installed build -- planner, two worker threads calling decode_chunk per chunk
+    (:2219-2237, :2326-2397), timestamp map, overlap merge -- reaches the engine as ONE
+    batched decode of the whole chunk plan (plan-ahead route), with segments identical to
+    the per-chunk route (ZASR_PLAN_AHEAD=0).  The engine is a deterministic CPU stand-in
+    (tests/test_dropin_plan.py FakeHandle; no GPU here); the audio loader is replaced by a
+    function returning synthetic speech (soundfile / ffmpeg are absent; audio I/O is outside
+    the path), and the pipeline's phase file is redirected to the temp dir.
+Prints "dropin install ok" and "pipeline dispatch ok" and exits 0 on success.
 """
 from __future__ import annotations
 
@@ -109,6 +117,70 @@ def check(ref_root: str, ours_first: bool) -> None:
           "get_hotwords_config" % ("zasr" if ours_first else "reference", len(done), len(phrases)))
 
 
+def check_pipeline(ref_root: str) -> None:
+    import tempfile
+
+    import numpy as np
+    sys.path[:0] = [ref_root, PKG, os.path.dirname(HERE)]
+    with contextlib.redirect_stdout(io.StringIO()):
+        import core.asr_engine as ref
+        import core.calibration as ref_cal
+        import core.hardware_accel as ref_hw
+    from test_dropin_plan import FakeHandle
+    from zasr import asr_engine as ours
+    from zasr.dropin import install
+    from zasr.synth_audio import synth_speech
+    install(ref, ref_hw, ref_cal)
+    ref.TranscriberPipeline._phase_file = os.path.join(tempfile.gettempdir(), "zasr_asr_phase")
+    audio = synth_speech(300.0, 5)
+    ref.load_audio = lambda *a, **k: audio.copy()
+    handle = {}
+
+    class StandIn:  # the Recognizer surface decode_chunk / compute_fbank_ort use
+        def __init__(self, *a, **k):
+            self.vocab_size = 64
+
+        def decode(self, chunks, beam=0):
+            return handle["h"].decode(chunks, beam)
+
+        def decode_features(self, feats, beam=0):
+            return handle["h"].decode_features(feats, beam)
+
+        def fbank(self, a):
+            return handle["h"].fbank(a)
+    ours.Recognizer = StandIn
+    md = tempfile.mkdtemp(prefix="zasr_dropin_model_")
+    for f in ("config.json", "model.safetensors"):
+        with open(os.path.join(md, f), "w") as fh:
+            fh.write("{}")
+    toks = ["<blk>", "<sos/eos>", "<unk>"] + [f"\u2581w{i}" if i % 3 == 0 else f"p{i}"
+                                             for i in range(3, 64)]
+    with open(os.path.join(md, "tokens.txt"), "w", encoding="utf-8") as fh:
+        fh.write("".join(f"{t} {i}\n" for i, t in enumerate(toks)))
+    cfg = {"cpu_threads": 4, "bypass_vad": True, "speaker_diarization": False,
+           "restore_punctuation": False, "skip_preprocessing": True}
+    runs = {}
+    for route in ("1", "0"):
+        os.environ["ZASR_PLAN_AHEAD"] = route
+        ours.clear_model_cache()
+        handle["h"] = FakeHandle()
+        with contextlib.redirect_stdout(io.StringIO()) as out:
+            res = ref.TranscriberPipeline("synthetic.wav", md, cfg).run()
+        runs[route] = (handle["h"].calls, res, out.getvalue())
+    calls, res, log = runs["1"]
+    per_calls, per_res, _ = runs["0"]
+    n_chunks = len(per_calls)
+    assert n_chunks >= 4 and per_calls == [1] * n_chunks, per_calls  # the 2-worker path ran
+    assert calls == [n_chunks], (calls, log[-2000:])
+    strip = lambda r: [{k: v for k, v in seg.items()} for seg in r["segments"]]  # noqa: E731
+    assert strip(res) == strip(per_res)
+    assert len(res["segments"]) > 10
+    os.environ.pop("ZASR_PLAN_AHEAD", None)
+    print("pipeline dispatch ok: the reference's TranscriberPipeline made %d decode_chunk calls "
+          "from 2 workers, served by %d batched decode call(s) of %d chunks; %d segments equal "
+          "to the per-chunk route" % (n_chunks, len(calls), calls[0], len(res["segments"])))
+
+
 def main():
     ref_root = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/root/reference"
     if "--ours-first" in sys.argv:
@@ -117,7 +189,10 @@ def main():
     if "--ref-first" in sys.argv:
         check(ref_root, False)
         return
-    for flag in ("--ref-first", "--ours-first"):  # fresh interpreter per sys.path order
+    if "--pipeline" in sys.argv:
+        check_pipeline(ref_root)
+        return
+    for flag in ("--ref-first", "--ours-first", "--pipeline"):  # fresh interpreter each
         r = subprocess.run([sys.executable, os.path.abspath(__file__), ref_root, flag],
                            capture_output=True, text=True)
         sys.stdout.write(r.stdout)

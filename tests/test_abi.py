@@ -53,10 +53,14 @@ def test_drop_in_modules_import():
     for name in ("create_recognizer", "compute_fbank_ort", "_ort_beam_search", "decode_chunk",
                  "get_ort", "_log_add", "_compute_token_entropy", "ROVER_MODEL_ID"):
         assert hasattr(ae, name)
-    for name in ("create_ort_session", "auto_batch_size", "is_gpu_provider",
-                 "configure_gpu_addon_paths"):
-        assert hasattr(ha, name)
-    assert cal.detect_calibration_status()["asr"] == "mi355x"
+    # only configure_gpu_addon_paths is replaced; create_ort_session & co. stay the reference's
+    assert ha.configure_gpu_addon_paths() == []
+    assert not hasattr(ha, "create_ort_session")
+    st = cal.detect_calibration_status()
+    assert st["asr"] == "mi355x" and st["preferred_provider"] == "MI355X:HIP"
+    calls = []
+    rep = cal.run_device_calibration("m", "s", 4, lambda m, p: calls.append(p))
+    assert rep["stages"] == {"asr": "mi355x"} and calls == [100]
     with pytest.raises(RuntimeError):
         ae.get_ort()
     assert hc.parse_hotwords_file(os.path.join(REPO, "tests", "golden", "hotword_sample.txt"))

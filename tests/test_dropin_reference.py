@@ -16,3 +16,5 @@ def test_install_rebinds_reference_modules():
     r = subprocess.run([sys.executable, SCRIPT, REF], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("dropin install ok") == 2, r.stdout
+    # the reference's unchanged TranscriberPipeline reaches ONE batched decode of its plan
+    assert "pipeline dispatch ok" in r.stdout, r.stdout

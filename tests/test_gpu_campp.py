@@ -64,12 +64,13 @@ def test_campp_embedding_matches_oracle_large_batch(emb):
     got = e.embed(x)
     ref = CamppOracle(cfg, w).embed(x)
     exact = CamppOracle(cfg, w, dtype=np.float64).embed(x)
-    # the random-init network is ill-conditioned: the f32 oracle itself sits ~1.5e-4 rel_l2 /
-    # 0.05 max_abs from the f64 result, so the GPU is held to the f64 result with the f32
-    # oracle's own error as the scale (x2), and to the reference rule where that is tighter
+    # the reference's CAM++ acceptance number (core/calibration.py:71-78: rel_l2 <= 2e-4),
+    # held against the exact (f64) embedding: the random-init network is ill-conditioned, so
+    # the f32 oracle itself sits ~1.5e-4 rel_l2 from the f64 result and two f32 runs can be
+    # further apart than that from each other
     f32_err = _rel(ref, exact)
     gpu_err = _rel(got, exact)
-    assert gpu_err <= max(2e-4, 2.0 * f32_err), (gpu_err, f32_err)
+    assert gpu_err <= 2e-4, (gpu_err, f32_err)
 
 
 @pytest.mark.parametrize("i", range(4))

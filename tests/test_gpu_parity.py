@@ -408,6 +408,10 @@ def test_pipelined_batches_equal_per_batch_decode(need_gpu, method, beam):
     streams; every chunk's result must be bit-identical to decoding its batch alone
     (batches of different sizes, an empty batch, short and empty chunks, a batch whose
     chunks are all too short)."""
+    check_pipelined_batches(method, beam)
+
+
+def check_pipelined_batches(method, beam):
     import torch
     from model_fixtures import m_model
     from zasr.binding import Recognizer
@@ -435,6 +439,26 @@ def test_pipelined_batches_equal_per_batch_decode(need_gpu, method, beam):
         i += len(b)
     assert sum(r.token_ids.size for r in piped) > 20
     rec.close()
+
+
+@pytest.mark.parametrize("env,method,beam", [
+    ({"ZASR_SEARCH_JOBS": "3", "ZASR_ENC_STREAMS": "2"}, "modified_beam_search", 4),
+    ({"ZASR_SEARCH_CUS": "32"}, "greedy_search", 1),
+], ids=["three_jobs_two_enc_streams", "cu_masked_search"])
+def test_pipelined_batches_env_variants(need_gpu, env, method, beam):
+    """The pipeline variants the engine reads from the environment at first use (three beam
+    searches in flight + two encoder streams; the CU-partitioned search stream, whose encoder
+    stream is not the caller's): a fresh process per variant, same bit-identity check."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_parity as t; "
+            "t.check_pipelined_batches(%r, %d); print('ok')"
+            % (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "sherpa-vietnamese-asr_amd"),
+               method, beam))
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env},
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
 
 
 def test_pipelined_workspace_growth_mid_pipeline(need_gpu):

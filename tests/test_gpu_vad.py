@@ -126,7 +126,8 @@ def test_long_file_and_ragged_batch_vs_oracle(sess):
 def test_parallel_in_time_matches_sequential(vad_dir, monkeypatch):
     """The segmented recurrence (warm-up guesses, state-continuity verification at 1e-6,
     reruns) matches the sequential one-workgroup-per-file probabilities to 1e-5 (two orders
-    below the parity tolerance) and needs at most 2 passes on speech."""
+    below the parity tolerance), needs at most 2 passes on speech, and yields the same
+    speech segments on the long files."""
     from zasr.binding import VadSession
     from zasr.synth_audio import synth_speech
     audios = [synth_speech(900.0, 51), synth_speech(40.0, 52), synth_speech(300.0, 53) * np.float32(0.02)]
@@ -143,6 +144,13 @@ def test_parallel_in_time_matches_sequential(vad_dir, monkeypatch):
     worst = max(float(np.max(np.abs(a - b))) for a, b in zip(got, ref))
     assert worst <= 1e-5, worst
     assert passes <= 2, passes
+    # the speech segments the reference's get_vad_segments cuts from them (its defaults,
+    # core/vad_utils.py:153-260, restated in zasr.vad_utils) are identical
+    from zasr.vad_utils import _segments_from_probs
+    for a, g, r in zip(audios, got, ref):
+        sg = _segments_from_probs(g, len(a), 16000, 0.2, 100, 250, 1000, 250, True)
+        sr = _segments_from_probs(r, len(a), 16000, 0.2, 100, 250, 1000, 250, True)
+        assert sg == sr
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/vad_pit_passes.json", "w") as f:
         json.dump({"passes": passes, "max_abs_vs_sequential": worst,
