@@ -84,6 +84,12 @@ def parse_args(argv=None):
                          "core/config.py:405-408); tokenized by the syllable hash (bpe.model is "
                          "absent).  'default' = tests/golden/hotword_sample.txt (the "
                          "reference's hotword.txt).  Beam search only.")
+    ap.add_argument("--shard-plan", action="store_true",
+                    help="strong scaling (BASELINE config 4's 'segments sharded across 8 GPUs'): "
+                         "every rank plans the SAME hour, decodes its longest-processing-time "
+                         "share of the chunks (zasr.shard.lpt_partition) and the results are "
+                         "gathered to every rank in chunk order (host object gather) inside the "
+                         "timed region; value = that hour x steps / max-over-ranks time")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="steps as separate decode_device calls (no cross-batch overlap)")
     ap.add_argument("--shape-table", action="store_true",
@@ -975,6 +981,35 @@ def bench_rover(args):
         dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------ strong scaling
+def gather_shards(res, mine, n_all, k, dist):
+    """--shard-plan: every rank's results of its LPT share over k pipelined steps -> the last
+    step's results of ALL chunks, in chunk order, on every rank (host object gather, the
+    decode_sharded protocol of zasr.shard; no collective on the GPU data path).  The payload
+    is what a caller needs per chunk: token ids, frames, log-probs, stats, T'."""
+    n = len(mine)
+    part = []
+    for s in range(k):
+        for j, i in enumerate(mine):
+            r = res[s * n + j]
+            part.append((s, i, {a: getattr(r, a) for a in ("token_ids", "frames", "log_probs",
+                                                              "stats", "T") if hasattr(r, a)}))
+    parts = [part]
+    if dist:
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, part)
+    from types import SimpleNamespace
+    out = [None] * n_all
+    for p in parts:
+        for s, i, d in p:
+            if s == k - 1:
+                out[i] = SimpleNamespace(**d)
+    missing = [i for i, r in enumerate(out) if r is None]
+    if missing:
+        raise RuntimeError(f"shard gather lost chunks {missing[:5]}")
+    return out
+
+
 # ------------------------------------------------------------------ token-exact mode
 SPLIT_PRODUCTS = {"bf16x3": 3, "bf16x6": 6}
 
@@ -1187,8 +1222,15 @@ def main():
     hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
     hotwords = load_hotwords(hw_path, cfg.vocab_size) if (hw_path and beam > 1) else None
 
-    # each rank: its own hour of audio (weak scaling), planned like the reference
-    chunks = make_chunks(args.audio_sec, AUDIO_SEED + rank)
+    # each rank: its own hour of audio (weak scaling), planned like the reference; with
+    # --shard-plan one hour for the whole job, each rank its LPT share of the chunks
+    all_chunks = make_chunks(args.audio_sec, AUDIO_SEED + (0 if args.shard_plan else rank))
+    if args.shard_plan:
+        from zasr.shard import lpt_partition
+        mine = lpt_partition([c.shape[0] for c in all_chunks], world)[rank]
+    else:
+        mine = list(range(len(all_chunks)))
+    chunks = [all_chunks[i] for i in mine]
     lens = [c.shape[0] for c in chunks]
 
     cpu = None
@@ -1203,11 +1245,16 @@ def main():
 
     rec, dev = None, None
     if args.cpu_dry_run:
-        # launcher / rank / timing path only: a CPU stand-in for the decode
+        # launcher / rank / timing path only: a CPU stand-in for the decode (one small result
+        # per chunk, so the --shard-plan gather moves real objects)
+        from types import SimpleNamespace
+
         def steps(k):
+            out = []
             for _ in range(k):
-                sum(float(np.abs(c[::97]).sum()) for c in chunks)
-            return []
+                out += [SimpleNamespace(token_ids=np.arange(int(np.abs(c[::97]).sum()) % 7 + 1),
+                                        T=c.shape[0] // 640) for c in chunks]
+            return out if args.shard_plan else out[len(out) - len(chunks):]
     else:
         torch.cuda.set_device(local)
         dev = f"cuda:{local}"
@@ -1221,7 +1268,7 @@ def main():
                          hotword_scores=hotwords[1] if hotwords else None, device_id=local,
                          precision=args.precision)
         offs = np.cumsum([0] + lens[:-1]).tolist()
-        d_wav = torch.from_numpy(np.concatenate(chunks)).to(dev)
+        d_wav = torch.from_numpy(np.concatenate(chunks) if chunks else np.zeros(1, np.float32)).to(dev)
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream().cuda_stream
 
@@ -1237,9 +1284,11 @@ def main():
                     r = step()
                 return r
             n = len(lens)
+            if n == 0:  # --shard-plan with more ranks than chunks
+                return []
             r = rec.decode_device_batches(d_wav.data_ptr(), offs * k, lens * k, [n] * k,
                                           beam=beam, stream=stream)
-            return r[-n:]
+            return r if args.shard_plan else r[-n:]
 
     def sync():
         if dev is not None:
@@ -1262,6 +1311,8 @@ def main():
     t0 = time.perf_counter()
     res = steps(args.steps)
     sync()
+    if args.shard_plan:
+        res = gather_shards(res, mine, len(all_chunks), args.steps, dist)
     el = time.perf_counter() - t0
     if dist:
         from zasr.shard import max_over_ranks
@@ -1287,7 +1338,8 @@ def main():
                                  MFMA_F32_PEAK_TFLOPS)
         rec.profile(0)
 
-    value = args.audio_sec * world * args.steps / el
+    # weak: every rank its own hour; strong (--shard-plan): one hour for the whole job
+    value = args.audio_sec * (1 if args.shard_plan else world) * args.steps / el
     emitted = sum(int(r.token_ids.size) for r in res)
     tprime = sum(int(r.T) for r in res)
 
@@ -1372,7 +1424,8 @@ def main():
             "value": round(value, 2), "unit": "audio-sec/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "scaling": "strong" if args.shard_plan else "weak", "vs_baseline": None,
+            "dtype": args.precision,
             "data": "synthetic (seeded 16 kHz speech-like audio, random-init Zipformer weights)",
             "config": {"workload": f"{args.model} {args.method}"
                                    f"{'' if beam == 1 else ' beam %d' % beam}{hw_tag}"
@@ -1381,8 +1434,13 @@ def main():
                        "chunk_sec_min_max": [round(min(lens) / SR, 2), round(max(lens) / SR, 2)],
                        "audio_sec_per_gpu": args.audio_sec,
                        "decoded_sec_per_gpu_incl_overlap": round(sum(lens) / SR, 1),
-                       "parallelism": f"dp{world} (each rank its own hour, seed + rank; weak "
-                                      f"scaling, no collective on the data path)",
+                       "parallelism": (f"dp{world} (one hour for the job: each rank decodes its "
+                                       f"LPT share of the chunk plan, results gathered to every "
+                                       f"rank in chunk order by a host object gather; strong "
+                                       f"scaling)" if args.shard_plan else
+                                       f"dp{world} (each rank its own hour, seed + rank; weak "
+                                       f"scaling, no collective on the data path)"),
+                       "shard_chunks_this_rank": len(chunks) if args.shard_plan else None,
                        "batch_pipeline": not args.no_pipeline,
                        "single_batch_latency_ms": (round(batch_latency_ms, 3)
                                                    if batch_latency_ms is not None else None),

@@ -38,12 +38,12 @@ def _dist():
 
 def decode_sharded(decode_fn: Callable[[List], List[R]], chunks: Sequence, lengths=None) -> List[R]:
     """Run `decode_fn` on this rank's LPT share of `chunks` and gather every rank's results
-    in chunk order.  Without an initialised process group this is `decode_fn(chunks)`."""
+    in chunk order (through the group's object gather, also at world size 1).  Without an
+    initialised process group this is `decode_fn(chunks)`."""
     dist = _dist()
-    world = dist.get_world_size() if dist else 1
-    if world == 1:
+    if dist is None:
         return list(decode_fn(list(chunks)))
-    rank = dist.get_rank()
+    world, rank = dist.get_world_size(), dist.get_rank()
     lens = [len(c) for c in chunks] if lengths is None else list(lengths)
     mine = lpt_partition(lens, world)[rank]
     res = list(decode_fn([chunks[i] for i in mine])) if mine else []

@@ -38,3 +38,19 @@ def test_bench_single_rank_default():
     assert line["n_gpus"] == 1
     assert line["config"]["chunks_per_gpu"] >= 1
     assert 20.0 <= line["config"]["chunk_sec_min_max"][1] <= 36.0
+
+
+def test_bench_shard_plan_two_ranks_strong_scaling():
+    """--shard-plan: both ranks plan the same audio, decode their LPT shares, gather every
+    chunk's result in chunk order (gloo object gather here) inside the timed region; the line
+    reports strong scaling and the job's audio once (not x ranks)."""
+    one = _run("--shard-plan")
+    two = _run("--gpus", "2", "--shard-plan")
+    assert two["n_gpus"] == 2 and two["scaling"] == "strong"
+    assert "LPT share" in two["config"]["parallelism"]
+    # the gathered hour: every chunk's result, the same token count as the single-rank run
+    assert two["config"]["tokens_emitted_per_gpu"] == one["config"]["tokens_emitted_per_gpu"]
+    assert two["config"]["shard_chunks_this_rank"] < one["config"]["shard_chunks_this_rank"]
+    # value = audio of the job / time (x1, not x world)
+    assert abs(two["value"] - 40.0 * two["steps"] / (two["ms_per_step"] * two["steps"] / 1e3)) \
+        <= 0.02 * two["value"]

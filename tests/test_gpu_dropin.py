@@ -87,3 +87,34 @@ def test_two_worker_loop_routed_equals_per_chunk(dropin_rec, feats):
         del h.decode, h.decode_features
     assert sum(len(w) for w in want) > 50
     assert got == want
+
+
+def test_decode_sharded_real_recognizer_nccl_world1(dropin_rec):
+    """zasr.shard.decode_sharded with a real Recognizer under an initialised RCCL ("nccl")
+    process group of size 1: the LPT split, the decode and the all_gather_object of the word
+    lists (pickled through device tensors) run once on the GPU; the words equal decode_chunk's
+    per chunk."""
+    import socket
+
+    import torch.distributed as dist
+    from zasr.plan import plan_chunks
+    from zasr.synth_audio import synth_speech
+    ae, rec = dropin_rec
+    audio = synth_speech(95.0, 77)
+    plan = plan_chunks(audio)
+    chunks = [audio[s:e].copy() for s, e, _ in plan]
+    offs = [s / 16000.0 for s, _, _ in plan]
+    want = [ae.decode_chunk(rec, c, o) for c, o in zip(chunks, offs)]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    import torch
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        got = ae.decode_chunks(rec, chunks, offs)
+    finally:
+        dist.destroy_process_group()
+    assert got == want
+    assert sum(len(w) for w in got) > 20
