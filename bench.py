@@ -591,7 +591,8 @@ def _pipe_cpu_job(job):
     count isolated, no GPU): decode (numpy fbank + torch fp32 encoder + the reference search,
     greedy) of the sample's planner chunks, their words, the merge, CAM++ window embeddings of
     the sample's speech regions (oracle fbank + CAMPPlus, batches of 32 as the reference) and
-    3 ViBERT passes over the sample's word chunks (mini-batches of 32)."""
+    the restorer over the sample's transcript (zasr.punct: up to 3 iterations, changed chunks
+    re-run, mini-batches of 32) on the ViBERT oracle."""
     import torch
     from oracle.campplus import CamppOracle, campp_fbank
     from oracle.fbank import fbank
@@ -603,7 +604,7 @@ def _pipe_cpu_job(job):
     from zasr.campp import synth_weights as campp_weights
     from zasr.merge import merge_chunks_with_overlap
     from zasr.model import PRESETS, synth_tokens, synth_weights
-    from zasr.pipeline import punctuate, split_word_chunks, vibert_feeds
+    from zasr.pipeline import make_punctuator, transcript_for_punctuation
     from zasr.vibert import synth_weights as vib_weights
     from zasr.vibert import vibert_base
     model, threads, chunks, offs, regions, repeats = job
@@ -637,7 +638,8 @@ def _pipe_cpu_job(job):
             wins += [fb[a:a + n] for a, n in window_plan(fb.shape[0]) if n == 150]
         for b in range(0, len(wins), 32):
             corc.embed(np.stack(wins[b:b + 32]))
-        punctuate(Sess(), [w["text"] for w in words], vcfg.vocab_size)
+        text, hints = transcript_for_punctuation(words)
+        make_punctuator(Sess(), vcfg.vocab_size, mini_batch=32).restore(text, pause_hints=hints)
         return len(words), len(wins)
 
     one_pass()  # warm-up (core/calibration.py:822-830: 1 warm-up, then the mean of repeats)
@@ -662,7 +664,7 @@ def bench_pipe(args):
     from zasr.campp import save_model_dir as campp_save
     from zasr.campp import synth_weights as campp_weights
     from zasr.model import PRESETS, chunk_flops, save_model_dir, synth_tokens, synth_weights
-    from zasr.pipeline import FullPipe, punctuate, split_word_chunks, vibert_feeds
+    from zasr.pipeline import FullPipe
     from zasr.synth_audio import synth_speech
     from zasr.vibert import save_model_dir as vib_save
     from zasr.vibert import synth_weights as vib_weights
@@ -690,8 +692,8 @@ def bench_pipe(args):
         cpu = {"value": round(end / SR / el_cpu, 3), "unit": "audio-sec/sec", "cores": threads,
                "kind": "port", "repeats": len(times), "repeat_s": [round(t, 3) for t in times],
                "sample": f"the first {end / SR:.1f} s (2 planner chunks): oracle decode (greedy) "
-                         f"+ words + merge, CAM++ oracle on {nwin} windows (batches of 32), 3 "
-                         f"ViBERT oracle passes over {nw} words (mini-batches of 32); torch fp32, "
+                         f"+ words + merge, CAM++ oracle on {nwin} windows (batches of 32), the "
+                         f"restorer (ViBERT oracle, mini-batches of 32) over {nw} words; torch fp32, "
                          f"{threads} threads, 1 warm-up + mean of {len(times)}"}
     dist = None
     if world > 1:
@@ -726,7 +728,7 @@ def bench_pipe(args):
     def steps(k):
         # k steps = k passes of the hour through the pipe, pipelined (FullPipe.run_many)
         r = pipe.run_many(k, args.rover_passes_per_call)[-1]
-        out.update(windows=len(r["windows"]), words=len(r["words"]), chunks=len(r["labels"]),
+        out.update(windows=len(r["windows"]), words=len(r["words"]), rows=r["vibert_rows"],
                    vibert_runs=r["vibert_runs"], tokens=r["tokens"])
 
     if args.warmup:
@@ -755,18 +757,15 @@ def bench_pipe(args):
     torch.cuda.synchronize()
     stage_ms["campp"] = 1000 * (time.perf_counter() - t1)
     t1 = time.perf_counter()
-    punctuate(vib, [w["text"] for w in words], vcfg.vocab_size, mini_batch=0)
+    s0 = len(pipe.punct.run_shapes)
+    pipe.punctuate(words)
     stage_ms["vibert"] = 1000 * (time.perf_counter() - t1)
+    vib_shapes = pipe.punct.run_shapes[s0:]
     c_len, plan, regions = pipe.c_len, pipe.c_off, pipe.r_off
     # algorithmic flops of the step: decode + CAM++ windows + ViBERT passes
     f_dec = sum(sum(chunk_flops(cfg, n, beam).values()) for n in c_len)
     f_cam = out["windows"] * campp_flops(ccfg, 150)
-    vch = [c for c in split_word_chunks([w["text"] for w in words]) if len(c) >= 3]
-    f_vib = 0.0
-    if vch:
-        fd = vibert_feeds(vch, vcfg.vocab_size)
-        Lp, Wp = fd["input_ids"].shape[1], fd["input_offsets"].shape[1]
-        f_vib = 3 * vibert_flops(vcfg, len(vch), Lp, Wp)
+    f_vib = sum(vibert_flops(vcfg, B, Lp, Wp) for B, Lp, Wp in vib_shapes)
     fl = f_dec + f_cam + f_vib
     p_dec = MFMA_BF16_PEAK_TFLOPS if args.precision != "fp32" else MFMA_F32_PEAK_TFLOPS
     t_roof = f_dec / (p_dec * 1e12) + (f_cam + f_vib) / (MFMA_F32_PEAK_TFLOPS * 1e12)
@@ -785,10 +784,12 @@ def bench_pipe(args):
                            "decode_chunks": len(plan), "campp_regions": len(regions),
                            "campp_windows": out["windows"], "campp_launch_batch": args.campp_batch,
                            "words": out["words"], "tokens": out["tokens"],
-                           "vibert_chunks": out["chunks"], "vibert_runs_per_step": out["vibert_runs"],
-                           "vibert_iterations": "3 passes over every chunk (the reference's "
-                                                "upper bound: it re-runs only changed chunks), "
-                                                "one run per pass (bit-identical to its 32-row "
+                           "vibert_rows_per_iteration": out["rows"],
+                           "vibert_runs_per_step": out["vibert_runs"],
+                           "vibert_iterations": "the reference's restorer (zasr.punct): edits "
+                                                "applied, later iterations re-run only the "
+                                                "chunks whose text changed; one run per "
+                                                "iteration (bit-identical to its 32-row "
                                                 "mini-batches, tests/test_gpu_pipe.py)",
                            "stage_ms_alone": {k: round(v, 2) for k, v in stage_ms.items()}},
                 "roofline": {"kernel": "whole pipe (algorithmic flops / step time)",

@@ -352,6 +352,9 @@ void launch_x3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
   const int BN = (pad128 * 100 <= pad32 * 115) ? 128 : (pad64 * 100 <= pad32 * 115 ? 64 : 32);
   const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
   const bool big = blocks128 >= 512;
+  // 8-wave 128 x 256 / 256 x 128 tiles were 10-20 % faster alone (tools/x6_bench,
+  // profiles/r03/split_gemm/x6_tile_lab_v1.txt) but slower under the batch pipeline, where
+  // two encoder streams share the CUs (enc_gemm 55.7 -> 58.4 ms per step): 4-wave tiles
   if (BN == 128) {
     if (big) launch_x3_t<128, 128, 2, 2, ALOAD, EPI, NP>(p, Bw, blo, st);
     else launch_x3_t<64, 128, 2, 2, ALOAD, EPI, NP>(p, Bw, blo, st);

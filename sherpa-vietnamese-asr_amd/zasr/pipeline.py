@@ -12,9 +12,12 @@ chunk_size 56, overlap 16, max_len 80, 3 iterations; core/gec_model.py:279-305 s
 
 On the GPU: the CAM++ front end and embeddings run on their own stream while the decode runs
 (they only read the audio); the punctuation model runs after the merge, on the ViBERT
-engine's stream.  Host work: word post-processing, the merge, the word chunking and the
-synthetic word-piece ids (the ViBERT vocab.txt tokenizer is absent: every word maps to 1-2
-ids by a stable hash, the START token is the last id as after special_tokens_fix).
+engine's stream.  Host work: word post-processing, the merge, and the reference's
+punctuation host logic (zasr.punct: chunking, softmax + confidence + pause nudges, edits,
+re-running only the changed chunks, chunk merge, the restorer's post-processing).  Word
+pieces come from the model dir's vocab.txt (zasr.punct.load_word_pieces) when it has one;
+the synthetic benchmark model has none, so every word maps to 1-2 ids by a stable hash, the
+START token being the last id as after special_tokens_fix.
 """
 from __future__ import annotations
 
@@ -35,15 +38,10 @@ def split_word_chunks(words: Sequence[str], chunk_size: int = CHUNK_WORDS,
                       overlap_size: int = OVERLAP_WORDS) -> List[List[str]]:
     """core/gec_model.py:279-305 for one sequence: whole when it fits, two halves sharing
     `overlap_size` words below 2 * chunk - overlap, else chunks every chunk - overlap words
-    while the start is before n - overlap."""
-    n = len(words)
-    if n <= chunk_size:
-        return [list(words)]
-    if n < chunk_size * 2 - overlap_size:
-        cut = (n + overlap_size + 1) // 2
-        return [list(words[:cut]), list(words[cut - overlap_size:])]
-    stride = chunk_size - overlap_size
-    return [list(words[i:i + chunk_size]) for i in range(0, n - overlap_size, stride)]
+    while the start is before n - overlap (zasr.punct.GecPunctuator.split_chunks)."""
+    from zasr.punct import GecPunctuator
+    g = GecPunctuator(None, None, 0, chunk_size=chunk_size, overlap_size=overlap_size)
+    return [list(c) for c in g.split_chunks([list(words)])[0]]
 
 
 @lru_cache(maxsize=1 << 18)
@@ -62,64 +60,48 @@ def word_pieces(word: str, vocab_size: int) -> List[int]:
     return list(_pieces(word, vocab_size))
 
 
-def vibert_feeds(batch: Sequence[Sequence[str]], vocab_size: int, max_len: int = MAX_LEN
-                 ) -> Dict[str, np.ndarray]:
-    """GecBERTModel.preprocess (core/gec_model.py:475-517): [START] + words[:max_len], word
-    pieces padded to the batch's longest, input_offsets = every position whose word id
-    differs from the previous one's -- the first piece of every word, plus the first padding
-    position of a padded row (its word id is None), zero-padded to the longest list."""
-    start_id = vocab_size - 1
-    L = min(max(len(s) for s in batch), max_len)
-    rows, offs = [], []
-    for seq in batch:
-        ids, off = [start_id], [0]
-        for w in list(seq)[:L]:
-            off.append(len(ids))
-            ids += _pieces(w, vocab_size)
-        rows.append(ids)
-        offs.append(off)
-    T = max(len(r) for r in rows)
-    for r, o in zip(rows, offs):
-        if len(r) < T:
-            o.append(len(r))
-    W = max(len(o) for o in offs)
-    B = len(rows)
-    input_ids = np.zeros((B, T), np.int64)
-    mask = np.zeros((B, T), np.int64)
-    offsets = np.zeros((B, W), np.int64)
-    for i, (r, o) in enumerate(zip(rows, offs)):
-        input_ids[i, :len(r)] = r
-        mask[i, :len(r)] = 1
-        offsets[i, :len(o)] = o
-    return {"input_ids": input_ids, "attention_mask": mask,
-            "token_type_ids": np.zeros((B, T), np.int64), "input_offsets": offsets}
+def make_punctuator(session, vocab_size: int, tokenizer=None, mini_batch: int = 0,
+                    **kw):
+    """zasr.punct.GecPunctuator (the reference's GecBERTModel host logic) over `session`.
+    tokenizer: (tokenize, start_id, pad_id) from zasr.punct.load_word_pieces for a model dir
+    with its vocab.txt; None -> the synthetic hashed word pieces (START = the last id).
+    mini_batch <= 0: one session run per iteration (rows are independent and the padding is
+    the iteration's either way, so the logits are the reference's 32-row mini-batches' bits,
+    tests/test_gpu_pipe.py)."""
+    from zasr.punct import GecPunctuator
+    if tokenizer is None:
+        tokenizer = (lambda w: _pieces(w, vocab_size), vocab_size - 1, 0)
+    tok, start_id, pad_id = tokenizer
+    return GecPunctuator(session, tok, start_id, pad_id=pad_id,
+                         mini_batch_size=mini_batch if mini_batch > 0 else 1 << 30, **kw)
 
 
-def punctuate(session, words: Sequence[str], vocab_size: int, iterations: int = ITERATIONS,
-              mini_batch: int = MINI_BATCH) -> Tuple[List[np.ndarray], int]:
-    """ViBERT passes over the transcript's word chunks: `iterations` passes of every chunk of
-    at least 3 words (core/gec_model.py:623-654; the reference re-runs only chunks whose text
-    changed, so this is its upper bound), mini-batches of `mini_batch` rows (32 in the
-    reference; <= 0: the whole pass in one run -- rows are independent and the padding is the
-    whole pass's either way, so the logits are the same bits).  Returns the per-chunk label
-    argmax of the last pass (softmax is monotone: argmax of the logits, :579-581) and the
-    number of session runs."""
-    chunks = [c for c in split_word_chunks(list(words)) if len(c) >= 3]
-    labels: List[np.ndarray] = [np.zeros(0, np.int64)] * len(chunks)
-    runs = 0
-    if not chunks:
-        return labels, runs
-    for _ in range(iterations):
-        # the whole batch is preprocessed (padded) at once, then sliced (:636-640, :380-392)
-        feeds = vibert_feeds(chunks, vocab_size)
-        mb = mini_batch if mini_batch > 0 else len(chunks)
-        for b in range(0, len(chunks), mb):
-            lg, _ = session.run(None, {k: v[b:b + mb] for k, v in feeds.items()})
-            runs += 1
-            am = lg.argmax(-1)
-            for i in range(am.shape[0]):
-                labels[b + i] = am[i, 1:1 + min(len(chunks[b + i]), MAX_LEN)]
-    return labels, runs
+def vibert_feeds(batch: Sequence[Sequence[str]], vocab_size: int) -> Dict[str, np.ndarray]:
+    """GecBERTModel.preprocess (core/gec_model.py:445-481) of `batch` with the synthetic word
+    pieces (zasr.punct.GecPunctuator.preprocess)."""
+    return make_punctuator(None, vocab_size).preprocess(batch)
+
+
+FILLER_WORDS = {"à", "ờ", "ừ", "ơ", "uh", "um"}   # core/asr_engine.py:1584
+
+
+def transcript_for_punctuation(words: Sequence[Dict]) -> Tuple[str, List[float]]:
+    """The text and pause hints the reference hands to restorer.restore after the merge
+    (core/asr_engine.py): filler words dropped (remove_filler_words :1587-1608), full_text =
+    the words joined by spaces, str.capitalize()d (:2577-2580), pause_hints[i] = the gap
+    after word i clipped at 0, 1.0 after the last word, None with fewer than 2 words or when
+    the count differs from the text's word count (:3118-3132)."""
+    ws = [w for w in words if w["text"].lower() not in FILLER_WORDS]
+    text = " ".join(w["text"] for w in ws)
+    if text:
+        text = text.capitalize()
+    hints = None
+    if len(ws) >= 2:
+        hints = [max(0.0, ws[i + 1].get("start", 0) - ws[i].get("end", 0)) for i in range(len(ws) - 1)]
+        hints.append(1.0)
+        if len(hints) != len(text.split()):
+            hints = None
+    return text, hints
 
 
 def l2_normalise(embs: np.ndarray) -> np.ndarray:
@@ -131,18 +113,31 @@ def l2_normalise(embs: np.ndarray) -> np.ndarray:
 
 class FullPipe:
     """One file through the config-5 pipe on one GPU (module docstring).  The audio goes to
-    HBM once; `run()` returns the merged word dicts, the punctuation label ids per word chunk,
-    the L2-normalised window embeddings and their (region, first frame, frames) plan.
+    HBM once; `run()` returns the merged word dicts, the punctuated transcript (the
+    reference's restorer output), the L2-normalised window embeddings and their (region,
+    first frame, frames) plan.
 
     rec: zasr.binding.Recognizer; recd: {"id2token", "vocab_size"} of its tokens; emb:
     CamppEmbedder; vib: VibertSession (ONNX session surface); vib_vocab: ViBERT vocabulary
     size incl. START."""
 
     def __init__(self, rec, recd, emb, vib, vib_vocab: int, beam: int = 1,
-                 campp_batch: int = 4096, iterations: int = ITERATIONS, vib_batch: int = 0):
+                 campp_batch: int = 4096, iterations: int = ITERATIONS, vib_batch: int = 0,
+                 tokenizer=None, confidence: float = 0.3, case_confidence: float = 0.0):
         self.rec, self.recd, self.emb, self.vib = rec, recd, emb, vib
         self.vib_vocab, self.beam, self.B, self.iterations = vib_vocab, beam, campp_batch, iterations
-        self.vib_batch = vib_batch  # <= 0: one ViBERT run per pass (punctuate)
+        # <= 0: one ViBERT run per iteration (make_punctuator)
+        self.punct = make_punctuator(vib, vib_vocab, tokenizer, vib_batch, iterations=iterations,
+                                     confidence=confidence, case_confidence=case_confidence)
+
+    def punctuate(self, words: Sequence[Dict]) -> Tuple[str, int, List[int]]:
+        """restorer.restore of the merged transcript (zasr.punct; the reference's
+        ImprovedPunctuationRestorer.restore): edits applied, later iterations re-run only the
+        chunks whose text changed.  Returns (text, session runs, rows per iteration)."""
+        text, hints = transcript_for_punctuation(words)
+        r0, n0 = self.punct.runs, len(self.punct.rows_run)
+        out = self.punct.restore(text, pause_hints=hints)
+        return out, self.punct.runs - r0, self.punct.rows_run[n0:]
 
     def prepare(self, audio: np.ndarray) -> None:
         import torch
@@ -224,13 +219,12 @@ class FullPipe:
                     # it is not ordered behind the next passes' decode queued on `main`
                     reg, first, nfr = self.embed_windows(self.s_campp.cuda_stream)
                     words, tokens = self.words(res_all[p * n:(p + 1) * n])
-                    labels, runs = punctuate(self.vib, [w["text"] for w in words],
-                                             self.vib_vocab, self.iterations, self.vib_batch)
+                    text, runs, rows = self.punctuate(words)
                     # the copy runs on (and waits for) the CAM++ stream only, never on `main`
                     # where the next decode is in flight
                     with torch.cuda.stream(self.s_campp):
                         embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
-                    outs.append({"words": words, "tokens": tokens, "labels": labels,
-                                 "vibert_runs": runs, "embeddings": embs,
+                    outs.append({"words": words, "tokens": tokens, "text": text,
+                                 "vibert_runs": runs, "vibert_rows": rows, "embeddings": embs,
                                  "windows": np.stack([reg, first, nfr], 1)})
         return outs

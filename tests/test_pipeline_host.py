@@ -1,10 +1,12 @@
 """Host logic of the full pipe (zasr.pipeline): the word chunking of the punctuation model
-(core/gec_model.py:279-305 split_chunks, restated; the module imports onnxruntime, absent
-here, so these expectations are derived by hand from its code -- parity unpinned by
-execution) and the ONNX feeds of GecBERTModel.preprocess (:475-517)."""
+(core/gec_model.py:279-305 split_chunks), the ONNX feeds of GecBERTModel.preprocess
+(:445-481) with the synthetic word pieces, the edit loop and the transcript handed to the
+restorer.  The reference's own handle_batch / restore pin the whole punctuation logic in
+tests/test_punct.py."""
 import numpy as np
 
-from zasr.pipeline import l2_normalise, punctuate, split_word_chunks, vibert_feeds, word_pieces
+from zasr.pipeline import (l2_normalise, make_punctuator, split_word_chunks,
+                           transcript_for_punctuation, vibert_feeds, word_pieces)
 
 
 def _w(n):
@@ -46,7 +48,11 @@ def test_vibert_feeds_offsets_and_padding():
     assert all(5 <= i <= V - 2 for w in "abcd" for i in word_pieces(w, V))
 
 
-def test_punctuate_runs_every_chunk_three_times():
+def test_punctuator_applies_edits_and_stops_when_stable():
+    """A session that always predicts $APPEND_. (label 3) at every slot: iteration 1 appends a
+    period after every word and one at the $START slot (before the first word, as the
+    reference does); iteration 2 predicts the same edits, which target_by_edits skips (a
+    period is already adjacent), so no chunk changes and the loop ends after 2 runs."""
     calls = []
 
     class Sess:
@@ -54,14 +60,22 @@ def test_punctuate_runs_every_chunk_three_times():
             B, W = feeds["input_offsets"].shape
             calls.append(B)
             lg = np.zeros((B, W, 15), np.float32)
-            lg[:, :, 3] = 1.0
+            lg[:, :, 3] = 10.0
             return [lg, np.zeros((B, W, 4), np.float32)]
 
-    labels, runs = punctuate(Sess(), _w(1000), 1000)
-    n = len([c for c in split_word_chunks(_w(1000)) if len(c) >= 3])
-    assert runs == 3 * ((n + 31) // 32) and sum(calls) == 3 * n
-    assert all((l == 3).all() and len(l) == len(c)
-               for l, c in zip(labels, split_word_chunks(_w(1000))))
+    g = make_punctuator(Sess(), 1000, mini_batch=32)
+    out = g.handle_batch([_w(20)])[0]
+    assert out == ". " + " ".join(w + "." for w in _w(20))
+    assert g.rows_run == [1, 1]
+
+
+def test_transcript_for_punctuation():
+    ws = [{"text": "xin", "start": 0.0, "end": 0.3}, {"text": "ờ", "start": 0.4, "end": 0.5},
+          {"text": "chào", "start": 0.9, "end": 1.2}, {"text": "BẠN", "start": 1.25, "end": 1.5}]
+    text, hints = transcript_for_punctuation(ws)
+    assert text == "Xin chào bạn"      # filler dropped, str.capitalize lowers the rest
+    assert hints == [0.6000000000000001, 0.050000000000000044, 1.0]
+    assert transcript_for_punctuation(ws[:1]) == ("Xin", None)
 
 
 def test_l2_normalise():
