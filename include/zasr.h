@@ -90,6 +90,18 @@ void zasr_destroy(zasr_recognizer* h);
    Replaces the ORT session load's file handling; ZASR_ERR_NOT_FOUND when files are missing. */
 int zasr_convert_model(const char* model_dir, const char* out_dir);
 
+/* Host-only (no GPU): the same for the single-graph models of the other stages, kind
+   "silero" | "campp" | "vibert": read the file the reference opens in model_dir
+   (silero_vad_16k_op15.onnx or silero_vad.onnx, core/vad_utils.py:22-24;
+   campplus_cn_en_common_200k.onnx, core/speaker_diarization_senko_campp_optimized.py:324-325;
+   vibert-capu.onnx or vibert-capu.int8.onnx, core/gec_model.py:133-140) -- or the engine's
+   own <kind>_config.json + safetensors when present -- and write out_dir/<kind>_config.json +
+   out_dir/{silero_vad,campp,vibert}.safetensors (torch state-dict names; the LSTM gates of
+   the ONNX LSTM node reordered to torch's; a BatchNorm the exporter fused into its Conv kept
+   as "<bn>.fused_shift").  zasr_vad_create / zasr_campp_create / zasr_vibert_create accept
+   the reference's directories directly through the same reader. */
+int zasr_convert_stage_model(const char* kind, const char* model_dir, const char* out_dir);
+
 /* log-mel fbank of one waveform (f32 in [-1,1], 16 kHz).  out holds cap floats;
    *n_frames = (n + 80) / 160, output row-major [n_frames][80].  h may be NULL
    (uses device 0). */
@@ -146,8 +158,9 @@ void zasr_result_free(zasr_result* r);
    Replaces the reference's onnxruntime CAM++ session and its numpy front end:
    core/speaker_diarization_senko_campp_optimized.py:86-159 (_compute_fbank_vectorized),
    :589-605 (batched emb_sess.run(['embs'], {'feats': batch})); the model is the reference's
-   convert_onnx/export_campplus_onnx.py CAMPPlus (192-dim).  model_dir holds
-   campp_config.json + campp.safetensors (state-dict names). */
+   convert_onnx/export_campplus_onnx.py CAMPPlus (192-dim).  model_dir holds the reference's
+   campplus_cn_en_common_200k.onnx (Conv+BN fused by the exporter or not) or
+   campp_config.json + campp.safetensors (state-dict names); see zasr_convert_stage_model. */
 typedef struct zasr_campp zasr_campp;
 int zasr_campp_create(const char* model_dir, int32_t device_id, zasr_campp** out);
 void zasr_campp_destroy(zasr_campp* h);
@@ -180,7 +193,9 @@ int zasr_campp_windows_device(zasr_campp* h, const float* d_wav, const int64_t* 
    Replaces the reference's onnxruntime session of vibert-capu.onnx (core/gec_model.py:
    366-412: session.run(None, {input_ids, attention_mask, token_type_ids, input_offsets}) ->
    (logits, detect_logits)); graph: convert_onnx/export_vibert_onnx.py Seq2LabelsModel.
-   model_dir holds vibert_config.json + vibert.safetensors (Hugging Face names). */
+   model_dir holds the reference's vibert-capu.onnx (or .int8.onnx, dequantized; config.json
+   beside it gives the head count, else head dim 64) or vibert_config.json +
+   vibert.safetensors (Hugging Face names); see zasr_convert_stage_model. */
 typedef struct zasr_vibert zasr_vibert;
 int zasr_vibert_create(const char* model_dir, int32_t device_id, zasr_vibert** out);
 void zasr_vibert_destroy(zasr_vibert* h);
@@ -195,8 +210,10 @@ int zasr_vibert_run(zasr_vibert* h, const int64_t* input_ids, const int64_t* att
 /* ---- Silero VAD ----
    Replaces the reference's per-window onnxruntime loop over silero_vad_16k_op15.onnx
    (core/vad_utils.py:62-111: 64-sample context + 512-sample window, (2, 1, 128) LSTM state
-   carried across calls).  model_dir holds silero_config.json + silero_vad.safetensors
-   (torch state-dict names of the 16 kHz model). */
+   carried across calls).  model_dir holds the reference's silero_vad_16k_op15.onnx (or
+   silero_vad.onnx; the 16 kHz branch is found by walking the graph, If branches included) or
+   silero_config.json + silero_vad.safetensors (torch state-dict names of the 16 kHz model);
+   see zasr_convert_stage_model. */
 typedef struct zasr_vad zasr_vad;
 int zasr_vad_create(const char* model_dir, int32_t device_id, zasr_vad** out);
 void zasr_vad_destroy(zasr_vad* h);

@@ -9,15 +9,24 @@
 #include "common.h"
 #include "gemm.h"
 #include "host_io.h"
+#include "onnx_io.h"
 
 namespace zasr {
 
 namespace {
 constexpr double kBnEps = 1e-5;
 
-// eval BatchNorm as y = x * s + b
+// eval BatchNorm as y = x * s + b; a BatchNorm the ONNX exporter already fused into the Conv
+// before it (onnx_io.cpp load_campp_graph: "<bn>.fused_shift") is s = 1, b = the fused bias
 void bn_fold(const SafeTensors& W, const std::string& p, int C, bool affine, std::vector<float>& s,
              std::vector<float>& b) {
+  if (W.has(p + ".fused_shift")) {
+    const HostTensor& f = W.get(p + ".fused_shift");
+    ZASR_REQUIRE((int)f.numel == C, "CAM++: fused BN size mismatch for " + p);
+    s.assign(C, 1.f);
+    b.assign(f.data, f.data + C);
+    return;
+  }
   const HostTensor& m = W.get(p + ".running_mean");
   const HostTensor& v = W.get(p + ".running_var");
   ZASR_REQUIRE((int)m.numel == C && (int)v.numel == C, "CAM++: BN size mismatch for " + p);
@@ -53,10 +62,9 @@ T* CamppEngine::ws(const std::string& name, size_t count) {
 }
 
 CamppEngine::CamppEngine(const std::string& dir, int device) : device_(device) {
-  const std::string cfg_path = dir + "/campp_config.json", st_path = dir + "/campp.safetensors";
-  if (!file_exists(cfg_path) || !file_exists(st_path))
-    throw std::invalid_argument("missing CAM++ model files (campp_config.json, campp.safetensors) in " + dir);
-  const Json j = Json::parse(read_file(cfg_path));
+  // campp_config.json + campp.safetensors, or the reference's campplus_cn_en_common_200k.onnx
+  SafeTensors W;
+  const Json j = Json::parse(load_stage_dir(dir, "campp", W));
   if (j.has("feat_dim")) cfg_.feat_dim = (int)j.at("feat_dim").num;
   if (j.has("embedding_size")) cfg_.emb = (int)j.at("embedding_size").num;
   if (j.has("growth_rate")) cfg_.growth = (int)j.at("growth_rate").num;
@@ -70,9 +78,6 @@ CamppEngine::CamppEngine(const std::string& dir, int device) : device_(device) {
   cfg_.block_dil = ints(j, "block_dilations", cfg_.block_dil);
   ZASR_REQUIRE(cfg_.feat_dim == 80 && cfg_.m_ch == 32 && cfg_.growth == 32 && cfg_.bn_size == 4,
                "CAM++ kernels are specialised for feat_dim 80, m_channels 32, growth 32, bn_size 4");
-  SafeTensors W;
-  W.load(st_path);
-
   ZASR_HIP_CHECK(hipSetDevice(device_));
   ZASR_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   st_ = stream_;

@@ -88,12 +88,13 @@ struct RawTensor {
 struct Node {
   std::string name, op;
   std::vector<std::string> in, out;
+  std::map<std::string, std::vector<int64_t>> ints;  // int / ints attributes (strides, ...)
 };
 
 struct OnnxFile {
   std::string bytes;  // the whole file
   std::vector<RawTensor> inits;
-  std::vector<Node> nodes;
+  std::vector<Node> nodes;  // the main graph's, then each subgraph's (If branches) after its node
 };
 
 float half_to_float(uint16_t h) {
@@ -184,19 +185,80 @@ RawTensor parse_tensor(Span s) {
   return t;
 }
 
-Node parse_node(Span s) {
+// GraphProto: nodes (1) and initializers (5); subgraphs of node attributes (If / Loop
+// branches: AttributeProto.g 6, .graphs 11) are flattened after their node, and Constant nodes'
+// tensors (AttributeProto.t 5 of "value") count as initializers named by the node's output
+void parse_graph(Span s, OnnxFile& of, int depth);
+
+void parse_node(Span s, OnnxFile& of, int depth) {
   Node n;
+  std::vector<Span> subgraphs;
+  std::vector<RawTensor> consts;
   Pb pb(s);
   while (pb.more()) {
     uint32_t f, w;
     pb.key(f, w);
-    if (w == 2 && f == 1) n.in.push_back(pb.bytes().str());
-    else if (w == 2 && f == 2) n.out.push_back(pb.bytes().str());
-    else if (w == 2 && f == 3) n.name = pb.bytes().str();
-    else if (w == 2 && f == 4) n.op = pb.bytes().str();
-    else pb.skip(w);
+    if (w == 2 && f == 1) {
+      n.in.push_back(pb.bytes().str());
+    } else if (w == 2 && f == 2) {
+      n.out.push_back(pb.bytes().str());
+    } else if (w == 2 && f == 3) {
+      n.name = pb.bytes().str();
+    } else if (w == 2 && f == 4) {
+      n.op = pb.bytes().str();
+    } else if (w == 2 && f == 5) {  // AttributeProto
+      Pb a(pb.bytes());
+      std::string an;
+      std::vector<int64_t> iv;
+      bool has_int = false;
+      while (a.more()) {
+        uint32_t af, aw;
+        a.key(af, aw);
+        if (af == 1 && aw == 2) {
+          an = a.bytes().str();
+        } else if (af == 3 && aw == 0) {
+          iv.push_back((int64_t)a.varint());
+          has_int = true;
+        } else if (af == 8) {
+          has_int = true;
+          if (aw == 2) {
+            Pb q(a.bytes());
+            while (q.more()) iv.push_back((int64_t)q.varint());
+          } else {
+            iv.push_back((int64_t)a.varint());
+          }
+        } else if (af == 5 && aw == 2) {
+          consts.push_back(parse_tensor(a.bytes()));
+        } else if ((af == 6 || af == 11) && aw == 2) {
+          subgraphs.push_back(a.bytes());
+        } else {
+          a.skip(aw);
+        }
+      }
+      if (has_int && !an.empty()) n.ints[an] = iv;
+    } else {
+      pb.skip(w);
+    }
   }
-  return n;
+  if (n.op == "Constant" && !n.out.empty())
+    for (auto& t : consts) {
+      t.name = n.out[0];
+      of.inits.push_back(std::move(t));
+    }
+  of.nodes.push_back(std::move(n));
+  for (const Span& g : subgraphs) parse_graph(g, of, depth + 1);
+}
+
+void parse_graph(Span s, OnnxFile& of, int depth) {
+  if (depth > 8) throw std::runtime_error("onnx: subgraphs nested too deeply");
+  Pb g(s);
+  while (g.more()) {
+    uint32_t gf, gw;
+    g.key(gf, gw);
+    if (gf == 1 && gw == 2) parse_node(g.bytes(), of, depth);
+    else if (gf == 5 && gw == 2) of.inits.push_back(parse_tensor(g.bytes()));
+    else g.skip(gw);
+  }
 }
 
 void parse_file(const std::string& path, OnnxFile& of) {
@@ -209,14 +271,7 @@ void parse_file(const std::string& path, OnnxFile& of) {
     model.key(f, w);
     if (f == 7 && w == 2) {  // ModelProto.graph
       have_graph = true;
-      Pb g(model.bytes());
-      while (g.more()) {
-        uint32_t gf, gw;
-        g.key(gf, gw);
-        if (gf == 1 && gw == 2) of.nodes.push_back(parse_node(g.bytes()));
-        else if (gf == 5 && gw == 2) of.inits.push_back(parse_tensor(g.bytes()));
-        else g.skip(gw);
-      }
+      parse_graph(model.bytes(), of, 0);
     } else {
       model.skip(w);
     }
@@ -351,14 +406,12 @@ struct Loaded {
   std::vector<float> data;
 };
 
-// one file's initializers under the names the engine uses; MatMul weights that neither a scope
-// name nor a following bias names are appended to `unnamed` in graph (execution) order
-void map_file(const OnnxFile& of, const std::string& dir, const std::string& prefix,
-              std::map<std::string, Loaded>& out, std::vector<Loaded>* unnamed) {
+// every initializer of a file as f32 under its own name, "<w>_quantized" int8 / uint8 tensors
+// dequantized with "<w>_scale" and "<w>_zero_point" into "<w>" (onnxruntime quantize_dynamic:
+// per-tensor scale; per-channel along the last axis)
+std::map<std::string, Loaded> all_values(const OnnxFile& of, const std::string& dir) {
   std::map<std::string, const RawTensor*> byname;
   for (const auto& t : of.inits) byname[t.name] = &t;
-  // 1. dequantize "<w>_quantized" (int8 / uint8) with "<w>_scale" and "<w>_zero_point"
-  //    (onnxruntime quantize_dynamic: per-tensor scale; per-channel along the last axis)
   std::map<std::string, Loaded> vals;
   std::set<std::string> consumed;
   for (const auto& t : of.inits) {
@@ -383,6 +436,15 @@ void map_file(const OnnxFile& of, const std::string& dir, const std::string& pre
   }
   for (const auto& t : of.inits)
     if (!consumed.count(t.name) && !vals.count(t.name)) vals[t.name] = Loaded{t.dims, to_f32(t, dir)};
+  return vals;
+}
+
+// one file's initializers under the names the engine uses; MatMul weights that neither a scope
+// name nor a following bias names are appended to `unnamed` in graph (execution) order
+void map_file(const OnnxFile& of, const std::string& dir, const std::string& prefix,
+              std::map<std::string, Loaded>& out, std::vector<Loaded>* unnamed) {
+  // 1. every initializer, int8 weights dequantized
+  std::map<std::string, Loaded> vals = all_values(of, dir);
   // 2. MatMul / MatMulInteger weight operands: the exporter stores nn.Linear weights
   //    transposed ([in][out]) under generated names; name them from the node's scope path, or
   //    from the bias of the Add that follows (through Cast / Mul for MatMulInteger)
@@ -493,6 +555,239 @@ std::string infer_config(const std::map<std::string, Loaded>& w) {
   return os.str();
 }
 
+
+// ------------------------------------------------------------ single-graph stage models
+const Loaded* input_value(const std::map<std::string, Loaded>& v, const Node& n, size_t i) {
+  if (i >= n.in.size()) return nullptr;
+  auto it = v.find(n.in[i]);
+  return it == v.end() ? nullptr : &it->second;
+}
+
+int64_t attr0(const Node& n, const std::string& k, int64_t dflt) {
+  auto it = n.ints.find(k);
+  return it == n.ints.end() || it->second.empty() ? dflt : it->second[0];
+}
+
+// ONNX LSTM gate blocks (i, o, f, c) -> torch LSTMCell (i, f, g, o) rows of [4H][K]
+std::vector<float> lstm_gates_to_torch(const float* src, int64_t H, int64_t K) {
+  static const int from[4] = {0, 2, 3, 1};
+  std::vector<float> out((size_t)(4 * H * K));
+  for (int g = 0; g < 4; ++g)
+    std::memcpy(out.data() + (size_t)g * H * K, src + (size_t)from[g] * H * K, (size_t)(H * K) * 4);
+  return out;
+}
+
+// Silero VAD v5, 16 kHz branch (silero_vad_16k_op15.onnx / silero_vad.onnx, core/vad_utils.py:
+// 22-24).  The graph is walked, not its names: the STFT Conv (basis [258][1][256]; an 8 kHz
+// branch's [130][1][128] is passed over), the kernel-3 Convs chained from 129 channels up to
+// the LSTM (strides from their attributes), the LSTM node (W / R / B, ONNX gate order iofc,
+// reordered to torch's ifgo) or named decoder.rnn.* tensors, then the [1][H][1] output Conv.
+// Every subgraph is flattened (an If on the sample rate keeps its branches there).
+std::string load_silero_graph(const OnnxFile& of, const std::string& dir, SafeTensors& out) {
+  const auto v = all_values(of, dir);
+  const size_t N = of.nodes.size();
+  size_t at = N;
+  for (size_t k = 0; k < N && at == N; ++k) {
+    const Node& n = of.nodes[k];
+    const Loaded* w = n.op == "Conv" ? input_value(v, n, 1) : nullptr;
+    if (w && w->dims.size() == 3 && w->dims[0] == 258 && w->dims[1] == 1 && w->dims[2] == 256) at = k;
+  }
+  if (at == N) throw std::runtime_error("silero onnx: no 16 kHz STFT Conv (basis [258][1][256])");
+  const std::string P = "_model.";
+  out.put(P + "stft.forward_basis_buffer", {258, 1, 256}, std::vector<float>(input_value(v, of.nodes[at], 1)->data));
+  std::vector<int> ch, sd;
+  int64_t cin = 129;
+  size_t k = at + 1;
+  for (; k < N && of.nodes[k].op != "LSTM"; ++k) {
+    const Node& n = of.nodes[k];
+    const Loaded* w = n.op == "Conv" ? input_value(v, n, 1) : nullptr;
+    if (!w || w->dims.size() != 3 || w->dims[2] != 3 || w->dims[1] != cin) continue;
+    const int64_t co = w->dims[0];
+    const std::string L = P + "encoder." + std::to_string(ch.size()) + ".reparam_conv.";
+    out.put(L + "weight", w->dims, std::vector<float>(w->data));
+    const Loaded* b = input_value(v, n, 2);
+    if (b && (int64_t)b->data.size() != co) throw std::runtime_error("silero onnx: bad encoder bias");
+    out.put(L + "bias", {co}, b ? std::vector<float>(b->data) : std::vector<float>((size_t)co, 0.f));
+    ch.push_back((int)co);
+    sd.push_back((int)attr0(n, "strides", 1));
+    cin = co;
+  }
+  if (ch.empty()) throw std::runtime_error("silero onnx: no encoder Convs after the STFT");
+  int64_t H = 0;
+  if (k < N) {  // the LSTM node: X, W [1][4H][in], R [1][4H][H], B [1][8H]
+    const Node& n = of.nodes[k];
+    const Loaded *W = input_value(v, n, 1), *R = input_value(v, n, 2), *B = input_value(v, n, 3);
+    if (!W || !R || W->dims.size() != 3 || R->dims.size() != 3 || W->dims[0] != 1 || W->dims[2] != cin)
+      throw std::runtime_error("silero onnx: unsupported LSTM weights");
+    H = R->dims[2];
+    if (W->dims[1] != 4 * H || R->dims[1] != 4 * H) throw std::runtime_error("silero onnx: bad LSTM shapes");
+    out.put(P + "decoder.rnn.weight_ih", {4 * H, cin}, lstm_gates_to_torch(W->data.data(), H, cin));
+    out.put(P + "decoder.rnn.weight_hh", {4 * H, H}, lstm_gates_to_torch(R->data.data(), H, H));
+    std::vector<float> bi((size_t)(4 * H), 0.f), bh((size_t)(4 * H), 0.f);
+    if (B) {
+      if ((int64_t)B->data.size() != 8 * H) throw std::runtime_error("silero onnx: bad LSTM bias");
+      bi = lstm_gates_to_torch(B->data.data(), H, 1);
+      bh = lstm_gates_to_torch(B->data.data() + 4 * H, H, 1);
+    }
+    out.put(P + "decoder.rnn.bias_ih", {4 * H}, std::move(bi));
+    out.put(P + "decoder.rnn.bias_hh", {4 * H}, std::move(bh));
+  } else {  // an export that keeps the LSTMCell parameters by name
+    for (const char* nm : {"weight_ih", "weight_hh", "bias_ih", "bias_hh"}) {
+      const Loaded* f = nullptr;
+      for (const auto& kv : v)
+        if (ends_with(kv.first, std::string("decoder.rnn.") + nm) && kv.first.find("8k") == std::string::npos) f = &kv.second;
+      if (!f) throw std::runtime_error(std::string("silero onnx: no LSTM node and no decoder.rnn.") + nm);
+      if (H == 0) H = f->dims[0] / 4;
+      out.put(P + "decoder.rnn." + nm, f->dims, std::vector<float>(f->data));
+    }
+    k = at;
+  }
+  bool dec = false;
+  for (size_t q = k + 1; q < N && !dec; ++q) {
+    const Node& n = of.nodes[q];
+    const Loaded* w = n.op == "Conv" ? input_value(v, n, 1) : nullptr;
+    if (!w || w->dims.size() != 3 || w->dims[0] != 1 || w->dims[1] != H || w->dims[2] != 1) continue;
+    const Loaded* b = input_value(v, n, 2);
+    out.put(P + "decoder.decoder.2.weight", {1, H, 1}, std::vector<float>(w->data));
+    out.put(P + "decoder.decoder.2.bias", {1}, b ? std::vector<float>(b->data) : std::vector<float>(1, 0.f));
+    dec = true;
+  }
+  if (!dec) throw std::runtime_error("silero onnx: no output Conv [1][H][1] after the LSTM");
+  std::ostringstream os;
+  os << "{\"sample_rate\": 16000, \"window\": 512, \"context\": 64, \"filter_length\": 256, "
+     << "\"hop\": " << attr0(of.nodes[at], "strides", 128) << ", \"enc_channels\": " << ivec(ch)
+     << ", \"enc_strides\": " << ivec(sd) << ", \"hidden\": " << H << "}";
+  return os.str();
+}
+
+// CAM++ (campplus_cn_en_common_200k.onnx, convert_onnx/export_campplus_onnx.py: torch.onnx,
+// opset 17, constant folding, eval mode).  Tensors that keep their state-dict names are taken
+// as they are; Conv and BatchNormalization nodes are named from their scope path
+// ("/xvector/block1/tdnnd1/linear1/Conv").  A Conv that carries a bias where the state dict has
+// a BatchNorm after it was fused by the exporter (W*s, beta - mean*s): its bias becomes
+// "<bn>.fused_shift" and the engine applies the identity scale (campp.cpp bn_fold).
+std::string bn_after_conv(const std::string& mod) {
+  auto rep = [&](const std::string& a, const std::string& b) { return mod.substr(0, mod.size() - a.size()) + b; };
+  if (mod.rfind("head.", 0) == 0) {
+    if (ends_with(mod, "conv1")) return rep("conv1", "bn1");
+    if (ends_with(mod, "conv2")) return rep("conv2", "bn2");
+    if (ends_with(mod, "shortcut.0")) return rep("shortcut.0", "shortcut.1");
+    return "";
+  }
+  if (mod == "xvector.tdnn.linear") return "xvector.tdnn.nonlinear.batchnorm";
+  if (mod == "xvector.dense.linear") return "xvector.dense.nonlinear.batchnorm";
+  if (mod.find(".tdnnd") != std::string::npos && mod.find("cam_layer") == std::string::npos &&
+      ends_with(mod, ".linear1"))
+    return rep("linear1", "nonlinear2.batchnorm");
+  return "";
+}
+
+std::string load_campp_graph(const OnnxFile& of, const std::string& dir, SafeTensors& out) {
+  const auto v = all_values(of, dir);
+  std::map<std::string, Loaded> w;
+  for (const auto& kv : v)
+    if (kv.first.rfind("head.", 0) == 0 || kv.first.rfind("xvector.", 0) == 0) w[kv.first] = kv.second;
+  std::set<std::string> bn_nodes;
+  for (const Node& n : of.nodes) {
+    const std::string mod = scope_module(n.name);
+    if (n.op != "BatchNormalization" || mod.empty()) continue;
+    bn_nodes.insert(mod);
+    static const char* parts[] = {"weight", "bias", "running_mean", "running_var"};
+    for (size_t i = 0; i < 4; ++i) {
+      const Loaded* x = input_value(v, n, i + 1);
+      if (x && !w.count(mod + "." + parts[i])) w[mod + "." + parts[i]] = *x;
+    }
+  }
+  std::map<std::string, std::vector<int>> dil;  // Conv dilations by module (block kernels)
+  for (const Node& n : of.nodes) {
+    const std::string mod = scope_module(n.name);
+    if (n.op != "Conv" || mod.empty()) continue;
+    const Loaded* x = input_value(v, n, 1);
+    if (x && !w.count(mod + ".weight")) w[mod + ".weight"] = *x;
+    dil[mod] = {(int)attr0(n, "dilations", 1)};
+    const Loaded* b = input_value(v, n, 2);
+    if (!b) continue;
+    const std::string bn = bn_after_conv(mod);
+    if (!bn.empty() && !bn_nodes.count(bn) && !w.count(bn + ".running_mean")) {
+      w[bn + ".fused_shift"] = *b;
+    } else if (!w.count(mod + ".bias")) {
+      w[mod + ".bias"] = *b;
+    }
+  }
+  if (!w.count("xvector.tdnn.linear.weight") || !w.count("xvector.dense.linear.weight"))
+    throw std::runtime_error("campp onnx: xvector.tdnn / xvector.dense Conv weights not found (scope names "
+                             "or state-dict names needed)");
+  std::vector<int> head, layers, kernels, dils;
+  for (int l = 1; w.count("head.layer" + std::to_string(l) + ".0.conv1.weight"); ++l) {
+    int nb = 0;
+    while (w.count("head.layer" + std::to_string(l) + "." + std::to_string(nb) + ".conv1.weight")) ++nb;
+    head.push_back(nb);
+  }
+  for (int b = 1; w.count("xvector.block" + std::to_string(b) + ".tdnnd1.linear1.weight"); ++b) {
+    const std::string B = "xvector.block" + std::to_string(b) + ".tdnnd";
+    int nl = 0;
+    while (w.count(B + std::to_string(nl + 1) + ".linear1.weight")) ++nl;
+    layers.push_back(nl);
+    const std::string loc = B + "1.cam_layer.linear_local";
+    kernels.push_back((int)w.at(loc + ".weight").dims.back());
+    dils.push_back(dil.count(loc) ? dil[loc][0] : 1);
+  }
+  const Loaded& tdnn = w.at("xvector.tdnn.linear.weight");
+  const Loaded& dense = w.at("xvector.dense.linear.weight");
+  const Loaded& l1 = w.at("xvector.block1.tdnnd1.linear1.weight");
+  const Loaded& loc1 = w.at("xvector.block1.tdnnd1.cam_layer.linear_local.weight");
+  std::ostringstream os;
+  os << "{\"feat_dim\": " << tdnn.dims[1] / 32 * 8 << ", \"embedding_size\": " << dense.dims[0]
+     << ", \"growth_rate\": " << loc1.dims[0] << ", \"bn_size\": " << l1.dims[0] / loc1.dims[0]
+     << ", \"init_channels\": " << tdnn.dims[0] << ", \"m_channels\": " << w.at("head.conv1.weight").dims[0]
+     << ", \"head_blocks\": " << ivec(head) << ", \"block_layers\": " << ivec(layers)
+     << ", \"block_kernels\": " << ivec(kernels) << ", \"block_dilations\": " << ivec(dils) << "}";
+  for (auto& kv : w) out.put(kv.first, kv.second.dims, std::move(kv.second.data));
+  return os.str();
+}
+
+// ViBERT-capu (vibert-capu.onnx / .int8.onnx, convert_onnx/export_vibert_onnx.py: the
+// Seq2LabelsModel inside the _ViBERTForExport wrapper, so every name carries "model.").  Linear
+// weights are named by map_file (scope path or bias Add) and transposed back; the head count
+// and LayerNorm eps are not in the tensors: config.json's num_attention_heads /
+// layer_norm_eps when the directory has them, else BERT's head dim 64 and 1e-12.
+std::string load_vibert_graph(const OnnxFile& of, const std::string& dir, SafeTensors& out) {
+  std::map<std::string, Loaded> m, w;
+  map_file(of, dir, "", m, nullptr);
+  for (auto& kv : m) {
+    std::string n = kv.first;
+    if (n.rfind("model.", 0) == 0) n = n.substr(6);
+    const bool param = ends_with(n, ".weight") || ends_with(n, ".bias");  // not the id buffers
+    if (param && (n.rfind("bert.", 0) == 0 || n.rfind("classifier.", 0) == 0 || n.rfind("detector.", 0) == 0))
+      w[n] = std::move(kv.second);
+  }
+  const std::string E = "bert.embeddings.";
+  const int H = dim(w, E + "word_embeddings.weight", 1);
+  int layers = 0;
+  while (w.count("bert.encoder.layer." + std::to_string(layers) + ".attention.self.query.weight")) ++layers;
+  if (layers == 0) throw std::runtime_error("vibert onnx: no encoder layers found");
+  int heads = H / 64;
+  double eps = 1e-12;
+  const std::string cj = dir + "/config.json";
+  if (file_exists(cj)) {
+    const Json j = Json::parse(read_file(cj));
+    if (j.has("num_attention_heads")) heads = (int)j.at("num_attention_heads").num;
+    if (j.has("layer_norm_eps")) eps = j.at("layer_norm_eps").num;
+  }
+  std::ostringstream os;
+  os.precision(17);
+  os << "{\"hidden_size\": " << H << ", \"num_hidden_layers\": " << layers
+     << ", \"num_attention_heads\": " << heads
+     << ", \"intermediate_size\": " << dim(w, "bert.encoder.layer.0.intermediate.dense.weight", 0)
+     << ", \"max_position_embeddings\": " << dim(w, E + "position_embeddings.weight", 0)
+     << ", \"type_vocab_size\": " << dim(w, E + "token_type_embeddings.weight", 0)
+     << ", \"vocab_size\": " << dim(w, E + "word_embeddings.weight", 0)
+     << ", \"num_labels\": " << dim(w, "classifier.weight", 0)
+     << ", \"num_detect_classes\": " << dim(w, "detector.weight", 0) << ", \"layer_norm_eps\": " << eps << "}";
+  for (auto& kv : w) out.put(kv.first, kv.second.dims, std::move(kv.second.data));
+  return os.str();
+}
+
 }  // namespace
 
 OnnxFiles find_onnx_files(const std::string& dir) {
@@ -600,6 +895,53 @@ void write_safetensors(const std::string& path, const SafeTensors& t) {
   for (const auto& kv : t.all())
     f.write(reinterpret_cast<const char*>(kv.second.data), (std::streamsize)(kv.second.numel * 4));
   if (!f) throw std::runtime_error("write failed: " + path);
+}
+
+std::string find_stage_onnx(const std::string& dir, const std::string& kind) {
+  // the file names the reference opens (core/vad_utils.py:22-24, core/speaker_diarization_
+  // senko_campp_optimized.py:324-325, core/gec_model.py:133-140: fp32 preferred)
+  std::vector<std::string> cands;
+  if (kind == "silero") cands = {"silero_vad_16k_op15.onnx", "silero_vad.onnx"};
+  else if (kind == "campp") cands = {"campplus_cn_en_common_200k.onnx"};
+  else if (kind == "vibert") cands = {"vibert-capu.onnx", "vibert-capu.int8.onnx"};
+  else throw std::invalid_argument("unknown model kind " + kind);
+  for (const auto& c : cands)
+    if (file_exists(dir + "/" + c)) return dir + "/" + c;
+  return "";
+}
+
+std::string load_stage_onnx(const std::string& path, const std::string& kind, SafeTensors& out) {
+  OnnxFile of;
+  parse_file(path, of);
+  const std::string dir = path.substr(0, path.rfind('/') == std::string::npos ? 0 : path.rfind('/'));
+  if (kind == "silero") return load_silero_graph(of, dir.empty() ? "." : dir, out);
+  if (kind == "campp") return load_campp_graph(of, dir.empty() ? "." : dir, out);
+  if (kind == "vibert") return load_vibert_graph(of, dir.empty() ? "." : dir, out);
+  throw std::invalid_argument("unknown model kind " + kind);
+}
+
+std::string load_stage_dir(const std::string& dir, const std::string& kind, SafeTensors& out) {
+  std::string cfg, st;
+  if (kind == "silero") cfg = "silero_config.json", st = "silero_vad.safetensors";
+  else if (kind == "campp") cfg = "campp_config.json", st = "campp.safetensors";
+  else if (kind == "vibert") cfg = "vibert_config.json", st = "vibert.safetensors";
+  else throw std::invalid_argument("unknown model kind " + kind);
+  if (file_exists(dir + "/" + cfg) && file_exists(dir + "/" + st)) {
+    out.load(dir + "/" + st);
+    return read_file(dir + "/" + cfg);
+  }
+  const std::string f = find_stage_onnx(dir, kind);
+  if (f.empty())
+    throw std::invalid_argument("missing " + kind + " model files in " + dir + " (" + cfg + " + " + st +
+                                ", or the reference's .onnx)");
+  return load_stage_onnx(f, kind, out);
+}
+
+std::string stage_safetensors_name(const std::string& kind) {
+  if (kind == "silero") return "silero_vad.safetensors";
+  if (kind == "campp") return "campp.safetensors";
+  if (kind == "vibert") return "vibert.safetensors";
+  throw std::invalid_argument("unknown model kind " + kind);
 }
 
 }  // namespace zasr

@@ -30,6 +30,20 @@ std::string load_onnx_model(const OnnxFiles& files, SafeTensors& out);
 // neither form is present.
 std::string load_model_dir(const std::string& dir, SafeTensors& out);
 
+// The single-graph models of the other stages, kind "silero" | "campp" | "vibert":
+// silero_vad_16k_op15.onnx (or silero_vad.onnx), campplus_cn_en_common_200k.onnx,
+// vibert-capu.onnx (or vibert-capu.int8.onnx) -- the files the reference opens.  Returns the
+// path in `dir` the reference would open, "" when none is there.
+std::string find_stage_onnx(const std::string& dir, const std::string& kind);
+// Loads one such file into the engine's tensor names (torch state-dict names) and returns the
+// engine's <kind>_config.json text inferred from the graph (shapes, Conv attributes).
+std::string load_stage_onnx(const std::string& path, const std::string& kind, SafeTensors& out);
+// <kind>_config.json + the engine's safetensors file when present, else the reference .onnx.
+// Throws std::invalid_argument when neither is in dir.
+std::string load_stage_dir(const std::string& dir, const std::string& kind, SafeTensors& out);
+// "silero_vad.safetensors" | "campp.safetensors" | "vibert.safetensors"
+std::string stage_safetensors_name(const std::string& kind);
+
 // Writes tensors as a float32 safetensors file (sorted names).
 void write_safetensors(const std::string& path, const SafeTensors& t);
 

@@ -9,6 +9,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "host_io.h"
+#include "onnx_io.h"
 #include "kernels.h"
 
 namespace zasr {
@@ -33,18 +34,15 @@ T* VadEngine::ws(const std::string& name, size_t count) {
 }
 
 VadEngine::VadEngine(const std::string& dir, int device) : device_(device) {
-  const std::string cfg_path = dir + "/silero_config.json", st_path = dir + "/silero_vad.safetensors";
-  if (!file_exists(cfg_path) || !file_exists(st_path))
-    throw std::invalid_argument("missing Silero VAD model files (silero_config.json, silero_vad.safetensors) in " + dir);
-  const Json j = Json::parse(read_file(cfg_path));
+  // silero_config.json + silero_vad.safetensors, or the reference's silero_vad_16k_op15.onnx
+  SafeTensors W;
+  const Json j = Json::parse(load_stage_dir(dir, "silero", W));
   ZASR_REQUIRE(j.at("window").as_int() == VW && j.at("context").as_int() == VIN - VW &&
                    j.at("filter_length").as_int() == VFL && j.at("hop").as_int() == 128 &&
                    j.at("hidden").as_int() == VH,
                "Silero VAD: only the 16 kHz v5 shape (window 512, context 64, STFT 256/128, LSTM 128)");
   const std::vector<int> ch = j.at("enc_channels").as_int_vec(), sd = j.at("enc_strides").as_int_vec();
   ZASR_REQUIRE(ch.size() == sd.size() && !ch.empty() && ch.back() == VH, "Silero VAD: bad encoder config");
-  SafeTensors W;
-  W.load(st_path);
   ZASR_HIP_CHECK(hipSetDevice(device_));
   ZASR_HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
   {

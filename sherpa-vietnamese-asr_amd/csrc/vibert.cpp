@@ -8,6 +8,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "host_io.h"
+#include "onnx_io.h"
 #include "kernels.h"
 
 namespace zasr {
@@ -28,10 +29,9 @@ T* VibertEngine::ws(const std::string& name, size_t count) {
 }
 
 VibertEngine::VibertEngine(const std::string& dir, int device) : device_(device) {
-  const std::string cfg_path = dir + "/vibert_config.json", st_path = dir + "/vibert.safetensors";
-  if (!file_exists(cfg_path) || !file_exists(st_path))
-    throw std::invalid_argument("missing ViBERT model files (vibert_config.json, vibert.safetensors) in " + dir);
-  const Json j = Json::parse(read_file(cfg_path));
+  // vibert_config.json + vibert.safetensors, or the reference's vibert-capu.onnx (onnx_io.h)
+  SafeTensors W;
+  const Json j = Json::parse(load_stage_dir(dir, "vibert", W));
   H_ = (int)j.at("hidden_size").num;
   heads_ = (int)j.at("num_attention_heads").num;
   inter_ = (int)j.at("intermediate_size").num;
@@ -44,8 +44,6 @@ VibertEngine::VibertEngine(const std::string& dir, int device) : device_(device)
                "ViBERT: hidden <= 1024, divisible by the head count");
   const int hd = H_ / heads_;
   ZASR_REQUIRE(hd == 16 || hd == 32 || hd == 64, "ViBERT: head dim 16, 32 or 64");
-  SafeTensors W;
-  W.load(st_path);
   ZASR_HIP_CHECK(hipSetDevice(device_));
   ZASR_HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
   auto dev = [&](const float* src, size_t n) {

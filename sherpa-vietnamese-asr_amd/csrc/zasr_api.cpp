@@ -291,6 +291,25 @@ int zasr_convert_model(const char* model_dir, const char* out_dir) {
   });
 }
 
+int zasr_convert_stage_model(const char* kind, const char* model_dir, const char* out_dir) {
+  if (!kind || !model_dir || !out_dir) return fail(ZASR_ERR_INVALID, "null kind/model_dir/out_dir");
+  const std::string k(kind);
+  if (k != "silero" && k != "campp" && k != "vibert")
+    return fail(ZASR_ERR_INVALID, "kind must be silero, campp or vibert");
+  return guarded([&]() {
+    zasr::SafeTensors w;
+    const std::string cfg = zasr::load_stage_dir(model_dir, k, w);
+    zasr::write_safetensors(std::string(out_dir) + "/" + zasr::stage_safetensors_name(k), w);
+    const std::string cp = std::string(out_dir) + "/" + k + "_config.json";
+    FILE* f = fopen(cp.c_str(), "wb");
+    if (!f) return fail(ZASR_ERR_RUNTIME, "cannot write " + cp);
+    const size_t wr = fwrite(cfg.data(), 1, cfg.size(), f);
+    fclose(f);
+    if (wr != cfg.size()) return fail(ZASR_ERR_RUNTIME, "short write of " + cp);
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_fbank(zasr_recognizer* h, const float* wav, int64_t n, int32_t sr, float* out,
                int64_t cap, int64_t* n_frames) {
   if (!n_frames || (n > 0 && !wav)) return fail(ZASR_ERR_INVALID, "null argument");

@@ -17,7 +17,7 @@ DEFAULT_LIB = os.path.join(_PKG, "lib", "libzasr.so")
 
 # every symbol declared in include/zasr.h (the CPU test checks the .so exports them all)
 EXPORTS = (
-    "zasr_create", "zasr_destroy", "zasr_convert_model", "zasr_fbank", "zasr_decode_batch", "zasr_decode_features",
+    "zasr_create", "zasr_destroy", "zasr_convert_model", "zasr_convert_stage_model", "zasr_fbank", "zasr_decode_batch", "zasr_decode_features",
     "zasr_decode_device", "zasr_decode_device_batches", "zasr_encode_features", "zasr_search_encoder_out",
     "zasr_result_count", "zasr_result_num_tokens", "zasr_result_num_frames",
     "zasr_result_tokens", "zasr_result_frames", "zasr_result_log_probs",
@@ -78,6 +78,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_destroy.restype = None
     lib.zasr_convert_model.argtypes = [C.c_char_p, C.c_char_p]
     lib.zasr_convert_model.restype = C.c_int
+    lib.zasr_convert_stage_model.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p]
+    lib.zasr_convert_stage_model.restype = C.c_int
     lib.zasr_fbank.argtypes = [P, fp, I64, I32, fp, I64, C.POINTER(I64)]
     lib.zasr_fbank.restype = C.c_int
     lib.zasr_decode_batch.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, I32, C.POINTER(P)]
@@ -176,6 +178,21 @@ def convert_model(model_dir: str, out_dir: str, lib_path: Optional[str] = None) 
     lib = load_library(lib_path)
     os.makedirs(out_dir, exist_ok=True)
     rc = lib.zasr_convert_model(model_dir.encode(), out_dir.encode())
+    if rc != 0:
+        msg = lib.zasr_last_error().decode()
+        if rc == 2:
+            raise FileNotFoundError(msg)
+        raise ZasrError(msg)
+
+
+def convert_stage_model(kind: str, model_dir: str, out_dir: str,
+                        lib_path: Optional[str] = None) -> None:
+    """Host-only load of a Silero VAD / CAM++ / ViBERT model directory (the reference's .onnx
+    or the engine's own files) through libzasr's reader, written as out_dir/<kind>_config.json
+    + the engine's safetensors file (include/zasr.h zasr_convert_stage_model)."""
+    lib = load_library(lib_path)
+    os.makedirs(out_dir, exist_ok=True)
+    rc = lib.zasr_convert_stage_model(kind.encode(), model_dir.encode(), out_dir.encode())
     if rc != 0:
         msg = lib.zasr_last_error().decode()
         if rc == 2:

@@ -5,8 +5,8 @@
     import core.asr_engine, core.hardware_accel, core.calibration  # the reference's modules
     from zasr.dropin import install
     install(core.asr_engine, core.hardware_accel, core.calibration)  # before the pipeline runs
-    # optional: Silero VAD on the GPU too (needs models/silero-vad/silero_config.json +
-    # silero_vad.safetensors, zasr/silero.py)
+    # optional: Silero VAD on the GPU too (reads the reference's
+    # models/silero-vad/silero_vad_16k_op15.onnx, or silero_config.json + silero_vad.safetensors)
     import core.vad_utils; install(core.asr_engine, vad_module=core.vad_utils)
 
 This build's modules live in the `zasr` package, so importing them never shadows the

@@ -12,11 +12,13 @@
   get_vad_segments_batch          MI355X-native: many files' VAD in one call (one LSTM
                                   workgroup per file), same per-file results
 
-Model files: silero_config.json + silero_vad.safetensors (zasr/silero.py) in
-$ZASR_VAD_MODEL_DIR, else <BASE_DIR>/models/silero-vad of the installed reference.  The
-reference's silero_vad_16k_op15.onnx itself is not read (the converter for its graph is not
-built); a directory holding only the .onnx raises FileNotFoundError, which the reference's
-pipeline already handles by falling back to silence chunking (core/asr_engine.py:2171-2204).
+Model files: the reference's own models/silero-vad/silero_vad_16k_op15.onnx (or
+silero_vad.onnx; read by libzasr's ONNX reader, onnx_io.cpp load_stage_onnx: the 16 kHz
+branch's tensors found by walking the graph, LSTM gates reordered) or silero_config.json +
+silero_vad.safetensors (zasr/silero.py), in $ZASR_VAD_MODEL_DIR, else <BASE_DIR>/models/
+silero-vad of the installed reference.  A directory with neither raises FileNotFoundError,
+which the reference's pipeline handles by falling back to silence chunking
+(core/asr_engine.py:2171-2204).
 """
 from __future__ import annotations
 
