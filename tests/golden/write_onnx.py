@@ -8,7 +8,9 @@ under a generated "onnx::MatMul_<n>" name and consumed by a MatMul node whose na
 module scope ("/encoder/encoders.0/layers.0/feed_forward1/in_proj/MatMul"), followed by an Add
 with the named bias.  `scope_names=False` drops the node names (the loader then names a weight
 from the Add's bias), and `int8=True` writes onnxruntime quantize_dynamic-style weights
-("<w>_quantized" int8 + "<w>_scale" + "<w>_zero_point", MatMulInteger).
+("<w>_quantized" int8 + "<w>_scale" + "<w>_zero_point", MatMulInteger).  The encoder also
+carries one positional-encoding constant per stack ("onnx::Slice_<n>", 1999 x 48 f32), as the
+traced icefall graph does (tests/test_encoder_bytes.py), which the loader must pass over.
 
 Only the initializers (and the nodes that name them) matter to this build: it does not run the
 graphs.  Protobuf wire format is written by hand (the onnx package is not installed).
@@ -117,11 +119,34 @@ def graph_for(names: List[str], w: Dict[str, np.ndarray], strip: str, scope_name
     return nodes, inits
 
 
+def pe_constants(w: Dict[str, np.ndarray], counter: List[int]):
+    """The traced CompactRelPositionalEncoding tables the real encoder graph carries (one per
+    encoder stack, (2 * 1000 - 1) x pos_dim f32, computed at construction and held as a plain
+    tensor attribute, so the trace bakes each into a generated-name constant sliced by the
+    sequence length; tests/test_encoder_bytes.py): the loader must pass over them."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from oracle.zipformer import compact_rel_pos_emb
+    stacks = sorted({int(n.split(".")[2]) for n in w if n.startswith("encoder.encoders.")})
+    pos_dim = next(a.shape[1] for n, a in w.items() if n.endswith("linear_pos.weight"))
+    table = compact_rel_pos_emb(1000, pos_dim).numpy()
+    nodes, inits = [], []
+    for i in stacks:
+        counter[0] += 1
+        name = f"onnx::Slice_{counter[0]}"
+        inits.append(tensor_proto(name, table, FLOAT))
+        nodes.append(node_proto("Slice", [name, "pe_start", "pe_end"], [name + "_out"],
+                                f"/encoder/encoders.{i}/encoder_pos/Slice"))
+    return nodes, inits
+
+
 def write_model_dir(path: str, w: Dict[str, np.ndarray], tokens: List[str], tag: str = "epoch-99-avg-1",
-                    scope_names: bool = True, int8: bool = False, also_int8: bool = False) -> Dict[str, str]:
+                    scope_names: bool = True, int8: bool = False, also_int8: bool = False,
+                    pe_tables: bool = True) -> Dict[str, str]:
     """Writes encoder-<tag>.onnx, decoder-<tag>.onnx, joiner-<tag>.onnx (or *.int8.onnx) and
     tokens.txt.  also_int8 additionally writes the int8 variants next to the float files (the
-    loader must prefer the float ones).  Returns {part: file path}."""
+    loader must prefer the float ones); pe_tables adds the encoder's positional-encoding
+    constants (pe_constants).  Returns {part: file path}."""
     os.makedirs(path, exist_ok=True)
     parts = {
         "encoder": sorted(n for n in w if n.startswith(("encoder.", "encoder_embed.", "encoder_proj."))),
@@ -135,6 +160,9 @@ def write_model_dir(path: str, w: Dict[str, np.ndarray], tokens: List[str], tag:
         for part, names in parts.items():
             strip = "joiner." if part == "joiner" else ""
             nodes, inits = graph_for(names, w, strip, scope_names, q, counter)
+            if part == "encoder" and pe_tables:
+                n_, i_ = pe_constants(w, counter)
+                nodes, inits = nodes + n_, inits + i_
             fn = os.path.join(path, f"{part}-{tag}{'.int8' if q else ''}.onnx")
             with open(fn, "wb") as f:
                 f.write(model_proto(nodes, inits))
