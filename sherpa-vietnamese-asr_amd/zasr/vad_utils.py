@@ -60,9 +60,10 @@ def _get_vad_session():
         if _vad_session is None:
             from zasr.binding import VadSession
             d = model_dir()
-            if not os.path.isfile(os.path.join(d, "silero_config.json")):
-                raise FileNotFoundError(f"Silero VAD model (silero_config.json + "
-                                        f"silero_vad.safetensors) not found in {d}")
+            names = ("silero_config.json", "silero_vad_16k_op15.onnx", "silero_vad.onnx")
+            if not any(os.path.isfile(os.path.join(d, n)) for n in names):
+                raise FileNotFoundError(f"Silero VAD model (silero_vad_16k_op15.onnx, silero_vad.onnx "
+                                        f"or silero_config.json + silero_vad.safetensors) not found in {d}")
             _vad_session = VadSession(d)
         return _vad_session
 

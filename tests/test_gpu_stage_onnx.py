@@ -66,7 +66,7 @@ def test_silero_onnx_dir_equals_safetensors_and_install_route(gpu, tmp_path, mon
         vu.unload_vad_model()
         vu.set_base_dir(None)
     assert got == want
-    assert sum(len(s) for s in got) >= 3
+    assert all(len(s) >= 1 for s in got)
 
 
 def test_vibert_onnx_dir_equals_safetensors(gpu, tmp_path):
