@@ -6,8 +6,8 @@
 //
 // The product A0 @ t1 is a per-sequence GEMM with K = L (up to ~1700 keys): it runs on the
 // bf16 MFMA GEMM (gemm.hip, one z-slice per sequence) with
-//   A = A0 in bf16, [L][L8] per sequence (L8 = L rounded up to 8, columns >= L zero),
-//   B = t1 transposed in bf16, [hid][R8] (sequence b in columns [o8_b, o8_b + L8_b), zero
+//   A = A0 in bf16, [L][L32] per sequence (L32 = L rounded up to 32, columns >= L zero),
+//   B = t1 transposed in bf16, [hid][R32] (sequence b in columns [o32_b, o32_b + L32_b), zero
 //       padded), i.e. the [N][K] "weight" layout the GEMM streams with 16-byte loads,
 // and the `* y` factor in its epilogue.  The kernels here produce A0 and t1^T.
 #include <type_traits>
@@ -47,6 +47,13 @@ constexpr int kPosPad = 160;  // staged positional rows beyond L (the last key b
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// packed f32 pair: one v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32 does two lanes' worth of
+// f32 work per issue (the kernels below are VALU-bound: SQ_ACTIVE_INST_VALU ~0.75 of SIMD
+// cycles, profiles/r03/attn_pmc/)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 }  // namespace
 
 // NP = 1: bf16 storage (the bf16 mode).  NP = 2 / 3: q / k / p / v / out / the head-0 weights
@@ -59,7 +66,10 @@ template <int MODE, int NP>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;
   using T = typename std::conditional<SPLIT, float, __bf16>::type;
-  extern __shared__ float4 sPos[];  // [L + kPosPad] positional rows of this head, x = xlo + t
+  // positional rows of this head, x = xlo + t for t < L + kPosPad, one plane per pos dim
+  // (structure of arrays: the rows of two adjacent keys are adjacent floats in each plane,
+  // so a ds_read2_b32 puts them into the register pair a packed FMA takes)
+  extern __shared__ float sPos[];
   __shared__ __attribute__((aligned(16))) __bf16 sK[NP][2][32 * kKLd];
   __shared__ __attribute__((aligned(16))) __bf16 sVt[NP][2][12 * kKLd];
   const int b = blockIdx.y;
@@ -88,13 +98,24 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     for (int t = tid; t < n; t += 256) {
       int row = xlo + t + a.pmax - 1;
       row = row < 0 ? 0 : (row > rmax ? rmax : row);
-      sPos[t] = *reinterpret_cast<const float4*>(a.pos_tab + (long)row * 4 * H + 4 * h);
+      const float4 v = *reinterpret_cast<const float4*>(a.pos_tab + (long)row * 4 * H + 4 * h);
+      if constexpr (SPLIT) {
+        sPos[t] = v.x;
+        sPos[n + t] = v.y;
+        sPos[2 * n + t] = v.z;
+        sPos[3 * n + t] = v.w;
+      } else {
+        // bf16 mode: the rows in bf16 (8 B), consumed by v_dot2_f32_bf16 against the bf16 p_i
+        const bf16x4 w = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+        reinterpret_cast<bf16x4*>(sPos)[t] = w;
+      }
     }
   }
   // ---- this lane's query (dims 8 h2 .. +8 and 16 + 8 h2 .. +8) and positional query ----
   const T* qrow = qkp + (long)(r0 + ic) * ldq + 32 * h;
   bf16x8 qf0[NP], qf1[NP];
-  float4 pq;
+  float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
+  bf16x2 pq01, pq23;  // bf16 mode: p_i as two bf16 pairs for v_dot2_f32_bf16
   if constexpr (SPLIT) {
     float v0[8], v1[8];
     *reinterpret_cast<float4*>(&v0[0]) = *reinterpret_cast<const float4*>(qrow + 8 * h2);
@@ -108,7 +129,8 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     qf0[0] = *reinterpret_cast<const bf16x8*>(qrow + 8 * h2);
     qf1[0] = *reinterpret_cast<const bf16x8*>(qrow + 16 + 8 * h2);
     const bf16x4 pv = *reinterpret_cast<const bf16x4*>(qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
-    pq = make_float4((float)pv[0], (float)pv[1], (float)pv[2], (float)pv[3]);
+    pq01 = (bf16x2){pv[0], pv[1]};
+    pq23 = (bf16x2){pv[2], pv[3]};
   }
   // pos index of (this query, key j0 + jr): j0 + jr - 32 wid - c + 127
   const int pbase = 127 - 32 * wid - c;
@@ -120,44 +142,45 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   const T* vbase = MODE == 0 ? nullptr : reinterpret_cast<const T*>(a.v) + (long)r0 * ldv + 12 * h;
   const int vt = tid - 128;
   const int vkey = vt / 3, vq = vt - 3 * (vt / 3);
-  bf16x8 kreg;
-  bf16x4 vreg;
+  // two register sets: key block kb + 2's global loads are in flight while block kb is
+  // computed and block kb + 1 (loaded one block earlier) goes to LDS, so the loads have two
+  // blocks of compute to land in (one block was not enough to cover their latency)
+  bf16x8 kv[2];  // bf16 mode: K threads' 8 dims, or V threads' 4 dims in elements 0..3
   // split modes: f32 staging registers; K rows (threads < 128) use both, V rows the first
-  float4 stg0 = make_float4(0.f, 0.f, 0.f, 0.f), stg1 = stg0;
-  auto gload = [&](int kb) {
+  float4 stg0[2], stg1[2];
+  // every thread issues the same loads whatever its role (threads without one re-read a K
+  // row), so the wait before storing a set can count the newer set's loads still in flight
+  // (divergent load sites made the compiler wait for everything)
+  const bool kt = tid < 128;
+  const bool vrole = MODE != 0 && vt >= 0 && vt < 96;
+  auto gload = [&](int kb, auto set) {
+    constexpr int S = decltype(set)::value;
     const int j0 = kb * 32;
+    int j = j0 + (vrole ? vkey : ((tid >> 2) & 31));
+    j = j < L ? j : L - 1;
+    const T* src = vrole ? vbase + (long)j * ldv + 4 * vq : kbase + (long)j * ldq + 8 * (tid & 3);
     if constexpr (SPLIT) {
-      // one load site for both roles (V threads fetch their 4 dims twice): per-role
-      // assignments made the compiler keep the staging registers in scratch
-      const bool kt = tid < 128;
-      if (kt || (MODE != 0 && vt < 96)) {
-        int j = j0 + (kt ? (tid >> 2) : vkey);
-        j = j < L ? j : L - 1;
-        const T* src = kt ? kbase + (long)j * ldq + 8 * (tid & 3) : vbase + (long)j * ldv + 4 * vq;
-        stg0 = *reinterpret_cast<const float4*>(src);
-        stg1 = *reinterpret_cast<const float4*>(src + (kt ? 4 : 0));
-      }
-    } else if (tid < 128) {
-      int j = j0 + (tid >> 2);
-      j = j < L ? j : L - 1;
-      kreg = *reinterpret_cast<const bf16x8*>(kbase + (long)j * ldq + 8 * (tid & 3));
-    } else if (MODE != 0 && vt < 96) {
-      int j = j0 + vkey;
-      j = j < L ? j : L - 1;
-      vreg = *reinterpret_cast<const bf16x4*>(vbase + (long)j * ldv + 4 * vq);
+      stg0[S] = *reinterpret_cast<const float4*>(src);
+      stg1[S] = *reinterpret_cast<const float4*>(src + (vrole ? 0 : 4));
+    } else {
+      // a V thread reads 8 dims of which it keeps 4 (the row tail past the head is in bounds:
+      // the next head's or, for the very last row, the workspace's slack)
+      kv[S] = *reinterpret_cast<const bf16x8*>(src);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, auto set) {
+    constexpr int S = decltype(set)::value;
     if (tid < 128) {
       __bf16* d = &sK[0][buf][(tid >> 2) * kKLd + 8 * (tid & 3)];
       if constexpr (SPLIT) {
-        const float v[8] = {stg0.x, stg0.y, stg0.z, stg0.w, stg1.x, stg1.y, stg1.z, stg1.w};
+        const float v[8] = {stg0[S].x, stg0[S].y, stg0[S].z, stg0[S].w,
+                            stg1[S].x, stg1[S].y, stg1[S].z, stg1[S].w};
         bf16x8 pc[NP];
         split_f8<NP>(v, pc);
 #pragma unroll
         for (int t = 0; t < NP; ++t) *reinterpret_cast<bf16x8*>(d + t * 2 * 32 * kKLd) = pc[t];
       } else {
-        *reinterpret_cast<bf16x8*>(d) = kreg;
+        *reinterpret_cast<bf16x8*>(d) = kv[S];
       }
     } else if (MODE != 0 && vt < 96) {
       // key jj sits in score register r = (jj&3) + 4 (jj>>3) of lane half (jj>>2)&1, which
@@ -174,13 +197,13 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
             if (t + 1 < NP) rr -= (float)hh;
           }
         };
-        put(0, stg0.x);
-        put(1, stg0.y);
-        put(2, stg0.z);
-        put(3, stg0.w);
+        put(0, stg0[S].x);
+        put(1, stg0[S].y);
+        put(2, stg0[S].z);
+        put(3, stg0[S].w);
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sVt[0][buf][(4 * vq + e) * kKLd + slot] = vreg[e];
+        for (int e = 0; e < 4; ++e) sVt[0][buf][(4 * vq + e) * kKLd + slot] = kv[S][e];
       }
     }
   };
@@ -198,14 +221,36 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     s = mfma_split<NP>(k0, qf0, s);
     s = mfma_split<NP>(k1, qf1, s);
     const int pb = j0 + pbase;
+    // positional term p_i . R[j - i] for the key pair (r, r + 1) = keys (jr, jr + 1) as packed
+    // FMAs: the same fma chain per score as scalar fmaf, half the VALU issues
+    if constexpr (!SPLIT) {
+      // bf16 mode: p_i . R[j - i] as two bf16 dot products per score (8 LDS bytes a score
+      // instead of 16: the kernels are bound by LDS bandwidth, profiles/r03/attn_pmc/)
+      const bf16x4* pr = reinterpret_cast<const bf16x4*>(sPos) + pb;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < 16; ++r) {
+        const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
+        const bf16x4 w = pr[jr];
+        s[r] = __builtin_amdgcn_fdot2_f32_bf16(pq23, (bf16x2){w[2], w[3]},
+                                               __builtin_amdgcn_fdot2_f32_bf16(pq01, (bf16x2){w[0], w[1]}, s[r], false),
+                                               false);
+      }
+    } else {
+    const f32x2 qx = {pq.x, pq.x}, qy = {pq.y, pq.y}, qz = {pq.z, pq.z}, qw = {pq.w, pq.w};
+    const int np = L + kPosPad;
+    const float* px = sPos + pb;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
       const int jr = (r & 3) + 8 * (r >> 2) + 4 * h2;
-      const float4 pr = sPos[pb + jr];
-      float ps = fmaf(pq.x, pr.x, s[r]);
-      ps = fmaf(pq.y, pr.y, ps);
-      ps = fmaf(pq.z, pr.z, ps);
-      s[r] = fmaf(pq.w, pr.w, ps) * kSc;
+      f32x2 ps = {s[r], s[r + 1]};
+      ps = pk_fma(qx, (f32x2){px[jr], px[jr + 1]}, ps);
+      ps = pk_fma(qy, (f32x2){px[np + jr], px[np + jr + 1]}, ps);
+      ps = pk_fma(qz, (f32x2){px[2 * np + jr], px[2 * np + jr + 1]}, ps);
+      ps = pk_fma(qw, (f32x2){px[3 * np + jr], px[3 * np + jr + 1]}, ps);
+      ps *= (f32x2){kSc, kSc};
+      s[r] = ps.x;
+      s[r + 1] = ps.y;
+    }
     }
     if (j0 + 32 > L) {
 #pragma unroll
@@ -222,6 +267,14 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   f32x16 o;
 #pragma unroll
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  // V^T fragments of the PV MFMAs; value dims d >= 12 (lanes c >= 12) stay zero
+  bf16x8 vf[2][NP];
+#pragma unroll
+  for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+    for (int t = 0; t < NP; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vf[mm][t][e] = (__bf16)0.f;
 
   constexpr int NPASS = MODE == 0 ? 2 : 1;
   T* const a0 = MODE == 0 ? reinterpret_cast<T*>(a.attn) + a.a_off[b] : nullptr;
@@ -234,14 +287,19 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       const float Ls = l * fexp2(m - M) + lo * fexp2(mo - M);
       cst = M + __log2f(Ls);
     }
-    gload(0);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    gload(0, I0{});
+    if (nkb > 1) gload(1, I1{});
     __syncthreads();  // previous pass's readers are done with buffer 0 (and sPos is staged)
-    sstore(0);
+    sstore(0, I0{});
     __syncthreads();
-#pragma unroll 1
-    for (int kb = 0; kb < nkb; ++kb) {
+    // one key block: its loads went out two blocks ago (set S), block kb + 2's go out now
+    // into the same set, block kb + 1 (set 1 - S) is stored for the next step
+    auto block = [&](int kb, auto set) {
+      constexpr int S = decltype(set)::value;
       const int cur = kb & 1;
-      if (kb + 1 < nkb) gload(kb + 1);
+      gload(kb + 2, set);  // unconditional (clamped rows past the end): see gload
       if (live) {
         f32x16 s;
         scores(kb, cur, s);
@@ -252,32 +310,35 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
             for (int r = 1; r < 16; ++r) bm = fmaxf(bm, s[r]);
             const float mn = fmaxf(m, bm);
             if (mn != -INFINITY) {  // a lane half can see only masked keys (L <= 4)
-              float acc = 0.f;
+              const f32x2 nm = {-mn, -mn};
+              f32x2 acc = {0.f, 0.f};
 #pragma unroll
-              for (int r = 0; r < 16; ++r) acc += fexp2(s[r] - mn);
-              l = l * fexp2(m - mn) + acc;
+              for (int r = 0; r < 16; r += 2) {
+                const f32x2 d = (f32x2){s[r], s[r + 1]} + nm;
+                acc += (f32x2){fexp2(d.x), fexp2(d.y)};
+              }
+              l = l * fexp2(m - mn) + (acc.x + acc.y);
               m = mn;
             }
           } else if (i < L) {
-            const int L8 = (L + 7) & ~7;
+            // row stride L32: the key blocks cover [0, L32) exactly, keys >= L write zeros
+            const int L32 = (L + 31) & ~31;
             const int j0 = kb * 32;
-            T* dst = a0 + (long)i * L8 + j0 + 4 * h2;
+            T* dst = a0 + (long)i * L32 + j0 + 4 * h2;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              if (j0 + 8 * g + 4 * h2 < L8) {
-                if constexpr (SPLIT) {
-                  float4 v;
-                  v.x = fexp2(s[4 * g + 0] - cst);
-                  v.y = fexp2(s[4 * g + 1] - cst);
-                  v.z = fexp2(s[4 * g + 2] - cst);
-                  v.w = fexp2(s[4 * g + 3] - cst);
-                  *reinterpret_cast<float4*>(dst + 8 * g) = v;
-                } else {
-                  bf16x4 v;
+              if constexpr (SPLIT) {
+                float4 v;
+                v.x = fexp2(s[4 * g + 0] - cst);
+                v.y = fexp2(s[4 * g + 1] - cst);
+                v.z = fexp2(s[4 * g + 2] - cst);
+                v.w = fexp2(s[4 * g + 3] - cst);
+                *reinterpret_cast<float4*>(dst + 8 * g) = v;
+              } else {
+                bf16x4 v;
 #pragma unroll
-                  for (int e = 0; e < 4; ++e) v[e] = (__bf16)fexp2(s[4 * g + e] - cst);
-                  *reinterpret_cast<bf16x4*>(dst + 8 * g) = v;
-                }
+                for (int e = 0; e < 4; ++e) v[e] = (__bf16)fexp2(s[4 * g + e] - cst);
+                *reinterpret_cast<bf16x4*>(dst + 8 * g) = v;
               }
             }
           }
@@ -290,23 +351,38 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
             const float mn = fmaxf(m, bm);
             if (__any(mn > m)) {
               const float sc = fexp2(m - mn);  // m = -inf -> 0
+              // o[8..15] are rows 16..31 of O^T: no value dims there (d < 12), never read
 #pragma unroll
-              for (int r = 0; r < 16; ++r) o[r] *= sc;
+              for (int r = 0; r < 8; r += 2) {
+                const f32x2 v = (f32x2){o[r], o[r + 1]} * (f32x2){sc, sc};
+                o[r] = v.x;
+                o[r + 1] = v.y;
+              }
               l *= sc;
               m = mn;
             }
+            const f32x2 nm = {-m, -m};
+            f32x2 acc = {0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              s[r] = fexp2(s[r] - m);
-              l += s[r];
+            for (int r = 0; r < 16; r += 2) {
+              const f32x2 d = (f32x2){s[r], s[r + 1]} + nm;
+              s[r] = fexp2(d.x);
+              s[r + 1] = fexp2(d.y);
+              acc += (f32x2){s[r], s[r + 1]};
             }
+            l += acc.x + acc.y;
           } else {
+            const f32x2 nc = {-cst, -cst};
 #pragma unroll
-            for (int r = 0; r < 16; ++r) s[r] = fexp2(s[r] - cst);
+            for (int r = 0; r < 16; r += 2) {
+              const f32x2 d = (f32x2){s[r], s[r + 1]} + nc;
+              s[r] = fexp2(d.x);
+              s[r + 1] = fexp2(d.y);
+            }
           }
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
-            bf16x8 pf[NP], vf[NP];
+            bf16x8 pf[NP];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
               float r = s[8 * mm + q];
@@ -317,21 +393,22 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
                 if (t + 1 < NP) r -= (float)hh;
               }
             }
+            if (c < 12) {  // lanes 12..31 keep the zeros set before the loop
 #pragma unroll
-            for (int t = 0; t < NP; ++t) {
-              if (c < 12) {
-                vf[t] = *reinterpret_cast<const bf16x8*>(&sVt[t][cur][c * kKLd + 16 * mm + 8 * h2]);
-              } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) vf[t][e] = (__bf16)0.f;
-              }
+              for (int t = 0; t < NP; ++t)
+                vf[mm][t] = *reinterpret_cast<const bf16x8*>(&sVt[t][cur][c * kKLd + 16 * mm + 8 * h2]);
             }
-            o = mfma_split<NP>(vf, pf, o);
+            o = mfma_split<NP>(vf[mm], pf, o);
           }
         }
       }
-      if (kb + 1 < nkb) sstore(cur ^ 1);
+      if (kb + 1 < nkb) sstore(cur ^ 1, std::integral_constant<int, 1 - S>{});
       __syncthreads();
+    };
+#pragma unroll 1
+    for (int kb = 0; kb < nkb; kb += 2) {
+      block(kb, I0{});
+      if (kb + 1 < nkb) block(kb + 1, I1{});
     }
   }
   if constexpr (MODE != 0) {
@@ -391,8 +468,8 @@ void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
 // =====================================================================================
 // t1^T = (tanh(s) * x)^T in bf16: h3 [R][3 hid] f32 -> t1t [hid][R8].  Tile 64 rows x 64
 // channels transposed through LDS; packed row r of sequence b goes to column
-// r + (o8_b - off_b); the last row of a sequence also writes the zero padding up to
-// o8_b + L8_b.
+// r + (o32_b - off_b); the last row of a sequence also writes the zero padding up to
+// o32_b + L32_b (the K padding of gemm_nonlin_bf16 / gemm_x3).
 // =====================================================================================
 __device__ __forceinline__ float4 h3_load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 h3_load4(const __bf16* p) {
@@ -440,7 +517,7 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict
   const int shift = o8[b] - off[b];
   const int col = r + shift;
   const bool last = r == off[b + 1] - 1;
-  const int pad_end = o8[b] + ((off[b + 1] - off[b] + 7) & ~7);
+  const int pad_end = o8[b] + ((off[b + 1] - off[b] + 31) & ~31);
   for (int cl = tid >> 6; cl < 64; cl += 4) {
     const int ch = c0 + cl;
     if (ch >= hid) break;

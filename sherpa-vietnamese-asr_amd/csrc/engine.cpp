@@ -1037,7 +1037,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   ff(0);
   // 2. nonlin_attention (attention head 0 only)
   if (bf16) {
-    // z = (A0 @ t1) * y on bf16 MFMA: A0 [L][L8] bf16, t1^T [hid][R8] bf16, z bf16
+    // z = (A0 @ t1) * y on bf16 MFMA: A0 [L][L32] bf16, t1^T [hid][R32] bf16, z bf16
     // (s, x, y) = chunk(in_proj(src), 3) in bf16: read by the transpose kernel (s, x) and
     // by the GEMM epilogue (y)
     __bf16* h3 = ws<__bf16>("ly_h3_h", (size_t)R * 3 * hid);
@@ -1061,8 +1061,9 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
     p.num_slices = B;
     p.max_M = maxL;
+    p.ldaux = 3 * hid;
     prof_begin("attn_nonlin");
-    gemm_bf16(p, t1t, EPI_MULAUX16, ALOAD_DENSE, st_, true, true);
+    gemm_nonlin_bf16(p, t1t, st_);
     prof_end();
     linear_h(Ly.na_out, z, true, hid, R, X, false, d, EPI_RESADD);
   } else if (np) {
@@ -1162,7 +1163,8 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   std::vector<std::vector<int>> o8(ns);
   std::vector<int> R8(ns, 0);
   const bool bf16 = precision_ == 1 || precision_ == 2;
-  // the flash attention path (bf16 and the split-bf16 modes): head-0 weights with L8 rows,
+  // the flash attention path (bf16 and the split-bf16 modes): head-0 weights with L32 rows
+  // ("L8" / "o8" / "R8" below: 32-padded),
   // NonlinAttention's B operand as t1^T columns
   const bool flash = bf16 || split_pieces() > 0;
   size_t attn_floats = 0;
@@ -1177,8 +1179,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
     const int hid = 3 * s.d / 4;
     int c8 = 0;
     for (int b = 0; b < B; ++b) {
-      const int Lb = len[b], L4 = (Lb + 3) & ~3, L8 = (Lb + 7) & ~7;
-      const int Lp = flash ? L8 : L4;  // weight row stride (flash: the GEMM's K padding)
+      const int Lb = len[b], L4 = (Lb + 3) & ~3, L8 = (Lb + 31) & ~31;
+      // weight row stride (flash: the GEMM's K padding, 32 for the LDS-DMA nonlin GEMM)
+      const int Lp = flash ? L8 : L4;
       aoff[i].push_back(acc);
       o8[i].push_back(c8);
       GemmSlice g{};

@@ -775,10 +775,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int NS, int EPI, typename TA, typename TC>
+// BN = 64 / 128 (the four waves split it in two halves); SL: z-slices (one linear grid over
+// (slice, tile); every slice's K a multiple of 32) -- the NonlinAttention product A0 @ t1 per
+// sequence, whose K = L-deep panels the register-staged kernel streams one slab at a time
+template <int NS, int EPI, typename TA, typename TC, int BN = 128, bool SL = false>
 __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf16* Bw,
-                                                        int tiles_n) {
-  constexpr int BM = 128, BN = 128, BK = 32;
+                                                        int tiles_n, int tiles_m = 0) {
+  constexpr int BM = 128, BK = 32;
+  constexpr int FN = BN / 64;  // 32-wide fragments per wave along N
   constexpr bool AF32 = std::is_same<TA, float>::value;
   constexpr int A_BYTES = BM * BK * (AF32 ? 4 : 2);
   constexpr int B_BYTES = BN * BK * 2;
@@ -794,10 +798,25 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
 
   const TA* A = reinterpret_cast<const TA*>(p.A);
   TC* C = reinterpret_cast<TC*>(p.C);
-  const int M = p.M, K = p.K, lda = p.lda;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const __bf16* aux16 = EPI == EPI_MULAUX16 ? reinterpret_cast<const __bf16*>(p.aux) : nullptr;
+  int M = p.M, K = p.K, lda = p.lda;
+  int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const __bf16* B = Bw;
+  if constexpr (SL) {
+    const int zs = tile / (tiles_n * tiles_m);
+    tile -= zs * tiles_n * tiles_m;
+    const GemmSlice sl = p.slices[zs];
+    A += sl.a_off;
+    B += sl.b_off;
+    C += sl.c_off;
+    if (aux16) aux16 += sl.aux_off;
+    M = sl.M;
+    K = sl.K;
+    lda = sl.lda;
+  }
   const int m_tile = tile / tiles_n;
   const int m0 = m_tile * BM;
+  if (SL && m0 >= M) return;
   const int n0 = (tile - m_tile * tiles_n) * BN;
   const int N = p.N;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -828,7 +847,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
     const int row = ins * 16 + (lane >> 2);
     const int lc = (lane & 3) ^ ((row >> 2) & 3);
     const int gn = n0 + row < N ? n0 + row : N - 1;
-    bsrc[g] = Bw + (long)gn * p.sbn + 8 * lc;
+    bsrc[g] = B + (long)gn * p.sbn + 8 * lc;
   }
   auto issue = [&](int kt) {
     unsigned char* st = smem + (kt % NS) * STAGE;
@@ -839,11 +858,11 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
     for (int g = 0; g < GB; ++g) glds16(bsrc[g] + k0, st + A_BYTES + (wid * GB + g) * 1024);
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][FN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -863,7 +882,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = 2 * ks + h;  // 16-byte bf16 chunk of the fragment's k range
-      bf16x8 a[2], b[2];
+      bf16x8 a[2], b[FN];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = wm * 64 + i * 32 + r32;
@@ -878,14 +897,14 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
         }
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wn * 64 + j * 32 + r32;
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + r32;
         b[j] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + row * 64 + ((ch ^ ((row >> 2) & 3)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
@@ -897,12 +916,12 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < FN; ++j) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         sE[((r & 3) + 8 * (r >> 2) + 4 * h) * LDE + r32] = acc[i][j][r];
       __builtin_amdgcn_wave_barrier();
-      const int col = n0 + wn * 64 + j * 32 + 4 * c4;
+      const int col = n0 + wn * (BN / 2) + j * 32 + 4 * c4;
       float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
       if (p.bias && col < N) bias = *reinterpret_cast<const float4*>(p.bias + col);
       // residual-epilogue side inputs: unconditional (clamped) loads, all in flight before
@@ -929,6 +948,10 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
           v.y = epi_act<EPI>(fmaf(v.y, p.alpha, bias.y));
           v.z = epi_act<EPI>(fmaf(v.z, p.alpha, bias.z));
           v.w = epi_act<EPI>(fmaf(v.w, p.alpha, bias.w));
+          if constexpr (EPI == EPI_MULAUX16) {
+            const bf16x4 x = *reinterpret_cast<const bf16x4*>(aux16 + (long)row * p.ldaux + col);
+            v.x *= (float)x[0]; v.y *= (float)x[1]; v.z *= (float)x[2]; v.w *= (float)x[3];
+          }
           TC* dst = C + (long)row * p.ldc + col;
           if constexpr (std::is_same<TC, float>::value) {
             if constexpr (EPI == EPI_RESADD) {
@@ -993,6 +1016,26 @@ void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
 }
 
 }  // namespace
+
+void gemm_nonlin_bf16(const GemmParams& p, const void* Bw, hipStream_t st) {
+  ZASR_REQUIRE(p.slices != nullptr && p.num_slices > 0, "gemm_nonlin_bf16: needs z-slices");
+  ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && p.ldaux % 4 == 0 && p.sbn % 8 == 0,
+               "gemm_nonlin_bf16: N, ldc, ldaux multiples of 4 and sbn of 8");
+  if (p.max_M <= 0) return;
+  // BN 64 when it wastes fewer padded columns (hid 144 / 192 / 288 -> 192 / 192 / 320)
+  const int pad64 = cdiv(p.N, 64) * 64, pad128 = cdiv(p.N, 128) * 128;
+  const int tm = cdiv(p.max_M, 128);
+  const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
+  if (pad64 < pad128) {
+    const int tn = cdiv(p.N, 64);
+    hipLaunchKernelGGL((gemm_glds_kernel<4, EPI_MULAUX16, __bf16, __bf16, 64, true>),
+                       dim3(tn * tm * p.num_slices), dim3(256), 0, st, p, B, tn, tm);
+  } else {
+    const int tn = cdiv(p.N, 128);
+    hipLaunchKernelGGL((gemm_glds_kernel<4, EPI_MULAUX16, __bf16, __bf16, 128, true>),
+                       dim3(tn * tm * p.num_slices), dim3(256), 0, st, p, B, tn, tm);
+  }
+}
 
 void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream_t st) {
   ZASR_REQUIRE(p.N > 0, "gemm: N must be positive");
