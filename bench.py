@@ -1131,9 +1131,13 @@ def bench_dropin(args):
     info = {}
 
     def phase():
-        # the planner (:2137-2161) through the hook the drop-in installs on find_silent_regions
-        regions = silent_regions(concat)
-        ae.register_plan_from_regions(concat, regions, best_split)
+        # the planner (:2137-2161) through the hook the drop-in installs on find_silent_regions:
+        # the GPU silence detector (the signal stays in HBM, the plan's decode starts at once),
+        # or with --no-pipeline / ZASR_GPU_PLANNER=0 the reference's numpy function
+        regions = ae.plan_ahead_regions(concat, best_split)
+        if regions is None:
+            regions = silent_regions(concat)
+            ae.register_plan_from_regions(concat, regions, best_split)
         from zasr.plan import plan_from_regions
         plan = plan_from_regions(len(concat), regions, best_split)
         results = [None] * len(plan)
@@ -1184,6 +1188,7 @@ def bench_dropin(args):
                                        f"zasr.asr_engine.decode_chunk from two worker threads, "
                                        f"1 h of host audio per GPU, timestamps mapped, overlap merge",
                            "plan_ahead": os.environ.get("ZASR_PLAN_AHEAD", "1") != "0",
+                           "gpu_planner": ae._gpu_planner_on(),
                            **info},
                 "roofline": None, "cpu_baseline": None}
         print(json.dumps(line))

@@ -24,6 +24,8 @@
  *   zasr_decode_features   core/asr_engine.py:1224 _ort_beam_search with precomputed
  *                          features (ROVER shares one fbank, core/asr_engine.py:2346-2350)
  *   zasr_encode_features   the encoder session run, core/asr_engine.py:1045-1049
+ *   zasr_silence_flags     core/asr_engine.py:521-554 find_silent_regions (the planner's
+ *                          frame energies, numpy float32 bit for bit; regions on the host)
  *   zasr_search_encoder_out  the search loop alone, core/asr_engine.py:1051-1153
  *   zasr_result_*          the (token_ids, frames, ys_log_probs, T, emit_logits) tuple of
  *                          core/asr_engine.py:1153 (entropy statistics instead of raw
@@ -107,6 +109,15 @@ int zasr_convert_stage_model(const char* kind, const char* model_dir, const char
    (uses device 0). */
 int zasr_fbank(zasr_recognizer* h, const float* wav, int64_t n, int32_t sample_rate, float* out,
                int64_t cap, int64_t* n_frames);
+
+/* The chunk planner's silence detector (core/asr_engine.py:521-554 find_silent_regions):
+   for each of the n / frame_len frames of the HBM-resident signal d_wav (16-byte aligned),
+   d_flags[f] = 1 when sqrt(mean(frame ** 2)) < threshold, evaluated exactly as numpy does
+   in float32 (pairwise row sum, f32 divide, correctly rounded sqrt, f32 compare), else 0.
+   frame_len: a multiple of 4, at most 256 (160 at 16 kHz).  Runs on `stream` (a hipStream_t,
+   NULL = the default stream); needs no recognizer handle. */
+int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float threshold,
+                       uint8_t* d_flags, void* stream);
 
 /* Decode `count` independent chunks (host buffers).  beam <= 0 uses the handle's
    configured decoding method / max_active_paths. */

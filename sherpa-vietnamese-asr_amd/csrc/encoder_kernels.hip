@@ -210,6 +210,86 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
 }
 
 // =====================================================================================
+// The planner's silence detector (core/asr_engine.py:521-554 find_silent_regions):
+//   energies = sqrt(mean(frames ** 2, axis=1)) < threshold
+// in numpy's float32 arithmetic, bit for bit.  numpy reduces each row with its pairwise sum
+// (numpy/_core/src/umath/loops_utils.h.src pairwise_sum): n <= 128 -> eight running partial
+// sums over blocks of 8, combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail in
+// order; n > 128 -> the halves [0, n2) and [n2, n) with n2 = n/2 rounded down to a multiple
+// of 8, summed separately and added.  Then / n (f32 true divide), sqrt (correctly rounded),
+// and the comparison in f32 (a Python float threshold is cast to the array's f32).  Every
+// square and add is an explicit _rn op, so nothing contracts into an FMA.
+// One thread per frame; the frame's row is read as float4s (rows are 16-byte aligned when
+// frame_len % 4 == 0, host-checked).  HBM-bound: 4 B per sample.
+// =====================================================================================
+__device__ __forceinline__ float np_pairwise_sq(const float* x, int n) {
+  // n <= 128: numpy's unrolled block sum of x[i]^2
+  if (n < 8) {
+    float s = -0.0f;
+    for (int i = 0; i < n; ++i) s = __fadd_rn(s, __fmul_rn(x[i], x[i]));
+    return s;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = __fmul_rn(x[j], x[j]);
+  int i = 8;
+  const int nb = n - (n % 8);
+  for (; i < nb; i += 8) {
+    const float4 a = *reinterpret_cast<const float4*>(x + i);
+    const float4 b = *reinterpret_cast<const float4*>(x + i + 4);
+    r[0] = __fadd_rn(r[0], __fmul_rn(a.x, a.x));
+    r[1] = __fadd_rn(r[1], __fmul_rn(a.y, a.y));
+    r[2] = __fadd_rn(r[2], __fmul_rn(a.z, a.z));
+    r[3] = __fadd_rn(r[3], __fmul_rn(a.w, a.w));
+    r[4] = __fadd_rn(r[4], __fmul_rn(b.x, b.x));
+    r[5] = __fadd_rn(r[5], __fmul_rn(b.y, b.y));
+    r[6] = __fadd_rn(r[6], __fmul_rn(b.z, b.z));
+    r[7] = __fadd_rn(r[7], __fmul_rn(b.w, b.w));
+  }
+  float s = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                      __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+  for (; i < n; ++i) s = __fadd_rn(s, __fmul_rn(x[i], x[i]));
+  return s;
+}
+
+__global__ __launch_bounds__(256) void silence_flags_kernel(const float* __restrict__ wav,
+                                                            long nframes, int flen, int n2,
+                                                            float threshold,
+                                                            unsigned char* __restrict__ flags) {
+  const long f = (long)blockIdx.x * 256 + threadIdx.x;
+  if (f >= nframes) return;
+  const float* x = wav + f * flen;
+  float s;
+  if (n2 == 0) {
+    s = np_pairwise_sq(x, flen);
+  } else {
+    s = __fadd_rn(np_pairwise_sq(x, n2), np_pairwise_sq(x + n2, flen - n2));
+  }
+  const float e = __fsqrt_rn(__fdiv_rn(s, (float)flen));
+  flags[f] = e < threshold ? 1 : 0;
+}
+
+void launch_silence_flags(const float* wav, long n, int frame_len, float threshold,
+                          unsigned char* flags, hipStream_t st) {
+  ZASR_REQUIRE(frame_len > 0 && frame_len % 4 == 0,
+               "silence flags: frame length must be a positive multiple of 4 samples");
+  ZASR_REQUIRE((reinterpret_cast<uintptr_t>(wav) & 15) == 0,
+               "silence flags: the signal must be 16-byte aligned");
+  // numpy's split (n > 128): halves of n2 = (n / 2) rounded down to 8 and n - n2, each <= 128
+  int n2 = 0;
+  if (frame_len > 128) {
+    n2 = frame_len / 2;
+    n2 -= n2 % 8;
+    ZASR_REQUIRE(n2 <= 128 && frame_len - n2 <= 128,
+                 "silence flags: frame length above 256 samples (numpy's deeper split) unsupported");
+  }
+  const long nframes = n / frame_len;
+  if (nframes <= 0) return;
+  hipLaunchKernelGGL(silence_flags_kernel, dim3((unsigned)cdivl(nframes, 256)), dim3(256), 0, st,
+                     wav, nframes, frame_len, n2, threshold, flags);
+}
+
+// =====================================================================================
 // conv.0: Conv2d(1 -> 8, 3x3, padding (0, 1)) + SwooshR.  One thread per (t, f).
 // =====================================================================================
 // BF16: bf16 output and the native-exp/log SwooshR (the bf16 mode; conv.4 reads it through

@@ -25,6 +25,12 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
                   int nseq, int total_frames, const FbankTables& tabs, float* out,
                   hipStream_t st, bool campp = false);
 
+// the planner's silence detector (core/asr_engine.py:521-554): flags[f] = RMS of samples
+// [f * frame_len, (f + 1) * frame_len) < threshold in numpy's float32 arithmetic, bit for bit;
+// n / frame_len frames
+void launch_silence_flags(const float* wav, long n, int frame_len, float threshold,
+                          unsigned char* flags, hipStream_t st);
+
 // ---- CAM++ speaker embedding (campp_kernels.hip) ----
 struct CamppConv2d {
   const float* x;      // [n][ci][fi][T]

@@ -511,6 +511,17 @@ int zasr_profile_report(zasr_recognizer* h, char* buf, int64_t cap) {
   });
 }
 
+int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float threshold,
+                       uint8_t* d_flags, void* stream) {
+  if (n < 0 || (n > 0 && (!d_wav || !d_flags))) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    zasr::launch_silence_flags(d_wav, (long)n, (int)frame_len, threshold, d_flags,
+                               reinterpret_cast<hipStream_t>(stream));
+    ZASR_HIP_CHECK(hipGetLastError());
+    return (int)ZASR_OK;
+  });
+}
+
 const char* zasr_last_error(void) { return g_last_error.c_str(); }
 const char* zasr_version(void) { return "zasr 0.1 (gfx950)"; }
 

@@ -393,50 +393,129 @@ def _words_from_search(id2token, V, n_samples, time_offset, token_ids, frames, l
     return words
 
 
+try:  # the same post-processing in C (csrc/words_ext.c); Python >= 3.12 sums floats with
+    # compensation (sum()), which the C twin does not restate: the Python version runs there
+    import sys as _sys
+    from zasr import _zasr_words
+    if _sys.version_info >= (3, 12):
+        _zasr_words = None
+except ImportError:  # pragma: no cover - built by __graft_entry__.build() / make
+    _zasr_words = None
+
+_tok_tables: Dict[int, tuple] = {}
+
+
+def _token_tables(id2token):
+    """(pieces, lowered) lists indexed by token id for the C word builder: id2token.get(t, "")
+    and its .lower(), built once per vocabulary."""
+    ent = _tok_tables.get(id(id2token))
+    if ent is None or ent[0] is not id2token or ent[1] != len(id2token):
+        hi = max((k for k in id2token if isinstance(k, int)), default=-1)
+        pieces = [id2token.get(i, "") for i in range(hi + 1)]
+        ent = (id2token, len(id2token), pieces, [p.lower() for p in pieces])
+        _tok_tables[id(id2token)] = ent
+    return ent[2], ent[3]
+
+
 def result_words(recognizer, r, n_samples: int, time_offset: float):
     """Word dicts of one device search result (reference :1227-1326): the tail of
-    decode_chunk, shared by decode_chunk / decode_chunks / the ROVER path."""
+    decode_chunk, shared by decode_chunk / decode_chunks / the ROVER path.  Runs in the C
+    extension when it is built (identical dicts, tests/test_words_ext.py), else in Python."""
+    if _zasr_words is not None:
+        pieces, lowered = _token_tables(recognizer["id2token"])
+        return _zasr_words.words_from_search(
+            pieces, lowered, int(recognizer["vocab_size"]), int(n_samples), float(time_offset),
+            np.ascontiguousarray(r.token_ids, np.int32), np.ascontiguousarray(r.frames, np.int32),
+            np.ascontiguousarray(r.log_probs, np.float64), int(r.T),
+            np.ascontiguousarray(r.stats, np.float32))
     return _words_from_search(recognizer["id2token"], recognizer["vocab_size"], n_samples,
                               time_offset, r.token_ids.tolist(), r.frames.tolist(),
                               r.log_probs.tolist(), int(r.T), TokenStats.rows(r.stats))
 
 
 # ------------------------------------------------------------------ plan-ahead batching
-PLAN_BATCH_CHUNKS = 256  # chunks per batched decode call (~2 h of audio)
+PLAN_BATCH_CHUNKS = 256  # chunks per batch of the plan's decode (~2 h of audio)
+FRAME_LEN = 160          # find_silent_regions' 10 ms frame at 16 kHz (:526)
+SILENCE_THRESHOLD = 0.01  # its defaults (:521)
+MIN_SILENCE_SEC = 0.3
 
 
 class _PlannedSignal:
     """A signal the reference's planner cut into chunks.  Holds the signal weakly (the
-    pipeline owns it) and, per recognizer handle and beam, the search results of every chunk
-    of the plan once the first of them was asked for."""
+    pipeline owns it), the signal's HBM copy when the GPU silence detector uploaded it, and
+    per recognizer handle and beam one decode of every chunk of the plan: started in the
+    background the moment the plan is registered (for the recognizers already loaded, which
+    the reference creates before it plans, :2041-2057), or on the first chunk asked for."""
 
-    def __init__(self, audio: np.ndarray, plan):
+    def __init__(self, audio: np.ndarray, plan, d_audio=None):
         self.ref = weakref.ref(audio)
         self.ptr = audio.__array_interface__["data"][0]
         self.n = int(audio.shape[0])
         self.plan = [(int(s), int(e)) for s, e, _ in plan if int(e) > int(s)]
         self.spans = set(self.plan)
+        self.d_audio = d_audio
         self.lock = threading.Lock()
-        self.results = weakref.WeakKeyDictionary()  # handle -> {beam: {(s, e): SearchResult}}
+        self.jobs = weakref.WeakKeyDictionary()  # handle -> {beam: _PlanDecode}
 
     def alive(self) -> bool:
         return self.ref() is not None
 
+    def _decode(self, handle, beam):
+        """Every chunk of the plan through the batch pipeline: from the HBM copy when there
+        is one (no second upload), else from the host signal."""
+        audio = self.ref()
+        if audio is None:
+            return None
+        res = {}
+        sizes = [min(PLAN_BATCH_CHUNKS, len(self.plan) - i)
+                 for i in range(0, len(self.plan), PLAN_BATCH_CHUNKS)]
+        if self.d_audio is not None and getattr(handle, "device_id", None) == self.d_audio.device.index:
+            out = handle.decode_device_batches(self.d_audio.data_ptr(), [s for s, _ in self.plan],
+                                               [e - s for s, e in self.plan], sizes, beam=beam)
+            res.update(zip(self.plan, out))
+        else:
+            for i in range(0, len(self.plan), PLAN_BATCH_CHUNKS):
+                part = self.plan[i:i + PLAN_BATCH_CHUNKS]
+                res.update(zip(part, handle.decode([audio[s:e] for s, e in part], beam=beam)))
+        return res
+
+    def start(self, handle, beam: int) -> "_PlanDecode":
+        with self.lock:
+            per = self.jobs.get(handle)
+            if per is None:
+                per = self.jobs[handle] = {}
+            job = per.get(beam)
+            if job is None:
+                job = per[beam] = _PlanDecode(self, handle, beam)
+        return job
+
     def result(self, handle, beam: int, span):
-        with self.lock:  # a second worker asking meanwhile waits for the same batch
-            per = self.results.get(handle)
-            res = per.get(beam) if per is not None else None
-            if res is None:
-                audio = self.ref()
-                if audio is None:
-                    return None
-                res = {}
-                for i in range(0, len(self.plan), PLAN_BATCH_CHUNKS):
-                    part = self.plan[i:i + PLAN_BATCH_CHUNKS]
-                    out = handle.decode([audio[s:e] for s, e in part], beam=beam)
-                    res.update(zip(part, out))
-                self.results.setdefault(handle, {})[beam] = res
-        return res.get(span)
+        res = self.start(handle, beam).wait()
+        return None if res is None else res.get(span)
+
+
+class _PlanDecode:
+    """One background decode of a plan for (handle, beam); wait() returns its results (the
+    ctypes call releases the GIL, so the caller's own work runs beside the GPU decode)."""
+
+    def __init__(self, sig: _PlannedSignal, handle, beam: int):
+        self.res, self.err = None, None
+        self.thread = threading.Thread(target=self._run, args=(weakref.ref(sig), handle, beam),
+                                       name="zasr-plan-decode", daemon=True)
+        self.thread.start()
+
+    def _run(self, sig_ref, handle, beam):
+        try:
+            sig = sig_ref()
+            self.res = sig._decode(handle, beam) if sig is not None else None
+        except BaseException as e:  # re-raised in the caller's decode_chunk
+            self.err = e
+
+    def wait(self):
+        self.thread.join()
+        if self.err is not None:
+            raise self.err
+        return self.res
 
 
 _plan_lock = threading.Lock()
@@ -453,25 +532,83 @@ def _is_f32_vector(a) -> bool:
             and a.strides == (4,))
 
 
-def register_plan(audio, plan) -> bool:
+def _loaded_handles():
+    """(handle, beam) of the recognizers the cache holds (the reference creates its one --
+    or, for ROVER, two -- recognizers before it plans); none when more are cached."""
+    with _cache_lock:
+        recs = list(_recognizer_cache.values())
+    out, seen = [], set()
+    for r in recs:
+        h = r["handle"]
+        if id(h) not in seen:
+            seen.add(id(h))
+            out.append((h, int(r.get("max_active_paths", 8))))
+    return out if len(out) <= 2 else []
+
+
+def register_plan(audio, plan, d_audio=None, start: bool = True) -> bool:
     """Remember that `audio` (the signal the planner worked on) is cut into `plan`
     [(start, end, overlap)]; chunks decode_chunk later receives as views of it at those spans
-    are decoded together.  Keeps the last few signals (weakly)."""
+    are served from one batched decode of the plan, started now for the loaded recognizers.
+    `d_audio`: the signal's HBM copy (a torch tensor), when the GPU planner made one.  Keeps
+    the last few signals (weakly)."""
     if not _plan_ahead_on() or not _is_f32_vector(audio) or not plan:
         return False
-    sig = _PlannedSignal(audio, plan)
+    sig = _PlannedSignal(audio, plan, d_audio)
     with _plan_lock:
         _planned[:] = [p for p in _planned if p.alive()][-3:] + [sig]
+    if start:
+        for h, beam in _loaded_handles():
+            sig.start(h, beam)
     return True
 
 
-def register_plan_from_regions(audio, regions, best_split_fn=None) -> bool:
+def register_plan_from_regions(audio, regions, best_split_fn=None, d_audio=None) -> bool:
     """The find_silent_regions hook: the plan the reference builds from these regions
     (:2141-2161, zasr.plan.plan_from_regions with the reference's own find_best_split_point)."""
     from zasr.plan import plan_from_regions
     if not _is_f32_vector(audio):
         return False
-    return register_plan(audio, plan_from_regions(int(audio.shape[0]), regions, best_split_fn))
+    return register_plan(audio, plan_from_regions(int(audio.shape[0]), regions, best_split_fn),
+                         d_audio)
+
+
+def _gpu_planner_on() -> bool:
+    return _plan_ahead_on() and os.environ.get("ZASR_GPU_PLANNER", "1") != "0"
+
+
+def silent_regions_device(audio: np.ndarray, device_id: int = 0):
+    """find_silent_regions (:521-554) with its defaults, on the GPU: the signal goes to HBM
+    once (it stays there for the plan's decode), zasr_silence_flags evaluates every 10 ms
+    frame's RMS < 0.01 exactly as numpy's float32 does, and the regions are built from the
+    flags on the host (zasr.plan.regions_from_flags).  Returns (regions, device tensor)."""
+    import torch
+    from zasr.binding import silence_flags
+    from zasr.plan import regions_from_flags
+    n = int(audio.shape[0])
+    nf = n // FRAME_LEN
+    dev = torch.device("cuda", int(device_id))
+    d = torch.from_numpy(audio).to(dev)
+    if nf == 0:
+        return [], d
+    flags = torch.empty(nf, dtype=torch.uint8, device=dev)
+    silence_flags(d.data_ptr(), n, FRAME_LEN, SILENCE_THRESHOLD, flags.data_ptr(),
+                  torch.cuda.current_stream(dev).cuda_stream)
+    return regions_from_flags(flags.cpu().numpy().astype(bool), FRAME_LEN, n, MIN_SILENCE_SEC), d
+
+
+def plan_ahead_regions(audio, best_split_fn=None):
+    """The drop-in's find_silent_regions for the planner's default-argument calls
+    (:2139, :2183): the regions from the GPU silence detector (bit-identical to the
+    reference's), with the plan built from them registered and its decode started.  None
+    when the route does not apply (then the reference's own function runs)."""
+    if not _gpu_planner_on() or not _is_f32_vector(audio) or not audio.flags.writeable:
+        return None
+    handles = _loaded_handles()
+    dev = handles[0][0].device_id if handles else int(os.environ.get("ZASR_DEVICE", "0"))
+    regions, d = silent_regions_device(audio, dev)
+    register_plan_from_regions(audio, regions, best_split_fn, d_audio=d)
+    return regions
 
 
 def _planned_span(chunk):

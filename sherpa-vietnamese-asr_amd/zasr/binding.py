@@ -28,7 +28,7 @@ EXPORTS = (
     "zasr_vibert_create", "zasr_vibert_destroy", "zasr_vibert_num_labels",
     "zasr_vibert_num_detect", "zasr_vibert_run",
     "zasr_vad_create", "zasr_vad_destroy", "zasr_vad_probs", "zasr_vad_probs_device",
-    "zasr_vad_window", "zasr_vad_last_passes",
+    "zasr_vad_window", "zasr_vad_last_passes", "zasr_silence_flags",
 )
 
 
@@ -166,6 +166,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_vad_window.restype = C.c_int
     lib.zasr_vad_last_passes.argtypes = [P]
     lib.zasr_vad_last_passes.restype = I32
+    lib.zasr_silence_flags.argtypes = [P, I64, I32, C.c_float, P, P]
+    lib.zasr_silence_flags.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -198,6 +200,17 @@ def convert_stage_model(kind: str, model_dir: str, out_dir: str,
         if rc == 2:
             raise FileNotFoundError(msg)
         raise ZasrError(msg)
+
+
+def silence_flags(d_wav_ptr: int, n: int, frame_len: int, threshold: float, d_flags_ptr: int,
+                  stream: int = 0, lib_path: Optional[str] = None) -> None:
+    """Per-frame silence flags of an HBM-resident signal (include/zasr.h zasr_silence_flags):
+    d_flags[f] = sqrt(mean(frame_f ** 2)) < threshold in numpy float32 arithmetic."""
+    lib = load_library(lib_path)
+    rc = lib.zasr_silence_flags(C.c_void_p(d_wav_ptr), int(n), int(frame_len),
+                                float(threshold), C.c_void_p(d_flags_ptr), C.c_void_p(stream))
+    if rc != 0:
+        raise ZasrError(lib.zasr_last_error().decode())
 
 
 @dataclasses.dataclass
@@ -245,6 +258,7 @@ class Recognizer:
                 raise FileNotFoundError(msg)
             raise ZasrError(msg)
         self.handle = h
+        self.device_id = int(device_id)
         self.vocab_size = self.lib.zasr_vocab_size(h)
         self.joiner_dim = self.lib.zasr_joiner_dim(h)
 

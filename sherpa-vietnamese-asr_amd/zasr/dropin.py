@@ -17,9 +17,11 @@ What is rebound (the ASR hot path, core/asr_engine.py:698-1326):
                   _compute_token_entropy, _finalize_word_entropy, decode_chunk, and
                   clear_model_cache wrapped so the reference's own version still unloads
                   the punctuation restorer and the diarizer (:743-768); find_silent_regions
-                  wrapped (same result) so that the chunk plan built from it (:2137-2161) is
-                  registered and the per-chunk decode_chunk calls of the two workers are
-                  served from ONE batched decode of the plan (zasr.asr_engine, plan-ahead)
+                  wrapped (same result: the frame energies run on the GPU, numpy-float32
+                  exact, and the signal stays in HBM) so that the chunk plan built from it
+                  (:2137-2161) is registered, its batched decode starts at once for the
+                  loaded recognizers, and the per-chunk decode_chunk calls of the two
+                  workers are served from that ONE decode (zasr.asr_engine, plan-ahead)
   hardware_accel  configure_gpu_addon_paths only (the DirectML / OpenVINO add-on dispatch is
                   removed per the north star); create_ort_session, is_gpu_provider and
                   auto_batch_size stay the reference's, so the stages outside ASR (diarization,
@@ -76,11 +78,18 @@ def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None
         split_fn = getattr(engine_module, "find_best_split_point", None)
 
         def find_silent_regions(audio_data, *args, **kwargs):
-            regions = orig_fsr(audio_data, *args, **kwargs)
             if not args and not kwargs:  # the planner's calls (:2139, :2183) use the defaults
+                try:  # the GPU silence detector: same regions, plan registered + decoding
+                    regions = ours.plan_ahead_regions(audio_data, split_fn)
+                    if regions is not None:
+                        return regions
+                except Exception as e:  # routing is an optimisation: never break the caller
+                    ours.logger.warning(f"[zasr] GPU planner skipped: {e}")
+            regions = orig_fsr(audio_data, *args, **kwargs)
+            if not args and not kwargs:
                 try:
                     ours.register_plan_from_regions(audio_data, regions, split_fn)
-                except Exception as e:  # routing is an optimisation: never break the caller
+                except Exception as e:
                     ours.logger.warning(f"[zasr] plan registration skipped: {e}")
             return regions
         find_silent_regions._zasr_wrapped = True

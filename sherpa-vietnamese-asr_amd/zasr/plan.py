@@ -73,12 +73,20 @@ def silent_regions(audio: np.ndarray, sr: int = SR, threshold: float = 0.01,
     if nf == 0:
         return []
     rms = np.sqrt(np.mean(audio[:nf * flen].reshape(nf, flen) ** 2, axis=1))
-    quiet = np.concatenate([[False], rms < threshold, [False]]).astype(np.int8)
-    edges = np.diff(quiet)
+    return regions_from_flags(rms < threshold, flen, len(audio), min_silence)
+
+
+def regions_from_flags(quiet: np.ndarray, flen: int, n: int, min_silence: float = 0.3) -> List[Span]:
+    """The region tail of find_silent_regions (core/asr_engine.py:536-554) given the per-frame
+    flags `energies < threshold` (host numpy, or zasr_silence_flags on the device)."""
+    if len(quiet) == 0:
+        return []
+    q = np.concatenate([[False], np.asarray(quiet, bool), [False]]).astype(np.int8)
+    edges = np.diff(q)
     starts = np.flatnonzero(edges == 1)          # first quiet frame
     ends = np.flatnonzero(edges == -1)           # one past the last quiet frame
     need = int(min_silence / 0.01)
-    return [(int(a) * flen, min(int(b) * flen, len(audio)))
+    return [(int(a) * flen, min(int(b) * flen, n))
             for a, b in zip(starts, ends) if b - a >= need]
 
 

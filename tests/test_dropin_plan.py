@@ -130,3 +130,44 @@ def test_dead_signal_is_not_matched():
     b = np.zeros(70 * 16000, np.float32)
     if b.__array_interface__["data"][0] == ptr:  # same address reused: still no match
         assert ae._planned_span(b[: 30 * 16000]) is None
+
+
+def test_registration_starts_the_plan_decode_for_loaded_recognizers(monkeypatch):
+    """The reference loads its recognizer(s) before it plans (:2041-2057): registering the plan
+    starts their batched decode at once (a background thread), so the GPU works while the
+    caller still builds its boundary list; the workers' calls then wait on that one decode."""
+    concat = synth_speech(150.0, 15)
+    plan = plan_chunks(concat)
+    h = FakeHandle()
+    rec = _rec(h)
+    monkeypatch.setattr(ae, "_recognizer_cache", {("m", 8): rec})
+    assert ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+    sig = ae._planned_span(concat[plan[0][0]:plan[0][1]])[0]
+    sig.jobs[h][8].thread.join(timeout=30)
+    assert h.calls == [len(plan)]  # decoded before any decode_chunk call
+    got = _two_workers(rec, concat, plan)
+    assert h.calls == [len(plan)]
+    want = [ae.decode_chunk(rec, concat[s:e].copy(), s / 16000.0) for s, e, _ in plan]
+    assert got == want
+
+
+def test_silent_regions_from_flags_equals_the_reference_restatement():
+    """regions_from_flags (the tail the GPU planner runs on zasr_silence_flags' output) gives
+    the restated find_silent_regions' regions; pinned by plan_cases.json through
+    test_host_plan_rover.  Edge cases: leading / trailing silence, runs of exactly 29 / 30
+    frames (int(0.3 / 0.01) = 29), a signal shorter than one frame."""
+    from zasr.plan import regions_from_flags
+    rng = np.random.default_rng(3)
+    for n_frames, pattern in [(400, "edges"), (1000, "random"), (0, "none")]:
+        a = (rng.standard_normal(n_frames * 160 + 37) * 0.05).astype(np.float32)
+        if pattern == "edges":
+            a[:50 * 160] *= 0.01
+            a[-45 * 160:] *= 0.01
+            a[100 * 160:129 * 160] *= 0.01  # 29 quiet frames: a region
+            a[200 * 160:228 * 160] *= 0.01  # 28: not
+        elif pattern == "random":
+            for s in rng.integers(0, n_frames - 40, 20):
+                a[s * 160:(s + int(rng.integers(10, 40))) * 160] *= 0.01
+        nf = len(a) // 160
+        rms = np.sqrt(np.mean(a[:nf * 160].reshape(nf, 160) ** 2, axis=1))
+        assert regions_from_flags(rms < 0.01, 160, len(a)) == silent_regions(a)

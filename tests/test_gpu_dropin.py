@@ -79,8 +79,8 @@ def test_two_worker_loop_routed_equals_per_chunk(dropin_rec, feats):
     try:
         want = [ae.decode_chunk(rec, concat[s:e].copy(), s / 16000.0) for s, e, _ in plan]
         assert n["decode"] == len(plan)
+        n["decode"] = n["feat"] = 0  # before registering: the plan's decode starts there
         assert ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
-        n["decode"] = n["feat"] = 0
         got = _loop(ae, rec, concat, plan, feats)
         assert n["decode"] == 1 and n["feat"] == 0, n  # one batched pass for the whole plan
     finally:
@@ -118,3 +118,66 @@ def test_decode_sharded_real_recognizer_nccl_world1(dropin_rec):
         dist.destroy_process_group()
     assert got == want
     assert sum(len(w) for w in got) > 20
+
+
+def _np_flags(a, flen, thr=0.01):
+    nf = len(a) // flen
+    return np.sqrt(np.mean(a[:nf * flen].reshape(nf, flen) ** 2, axis=1)) < thr
+
+
+@pytest.mark.parametrize("flen", [160, 80, 240, 128, 136])
+def test_silence_flags_bit_exact_vs_numpy(flen):
+    """zasr_silence_flags against numpy's own float32 evaluation of find_silent_regions'
+    energies < threshold (core/asr_engine.py:526-536), with frames placed within a few ulps
+    of the threshold (RMS = 0.01 * (1 + k * 2^-24)) where any other summation order, an FMA
+    contraction or a float64 comparison flips the flag."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    from zasr.binding import silence_flags
+    rng = np.random.default_rng(flen)
+    nf = 20000
+    a = (rng.standard_normal(nf * flen + 50) * 0.02).astype(np.float32)
+    for f in range(0, nf, 3):  # two thirds of the frames right at the threshold
+        row = rng.standard_normal(flen).astype(np.float64)
+        row *= 0.01 * (1.0 + rng.integers(-40, 41) * 2.0 ** -24) / np.sqrt(np.mean(row ** 2))
+        a[f * flen:(f + 1) * flen] = row.astype(np.float32)
+    d = torch.from_numpy(a).cuda()
+    flags = torch.zeros(nf, dtype=torch.uint8, device="cuda")
+    silence_flags(d.data_ptr(), len(a), flen, 0.01, flags.data_ptr())
+    got = flags.cpu().numpy().astype(bool)
+    want = _np_flags(a, flen)
+    assert 0.2 < want.mean() < 0.8
+    assert np.array_equal(got, want), int((got != want).sum())
+
+
+def test_gpu_planner_routes_the_two_worker_loop(dropin_rec):
+    """The drop-in's find_silent_regions route: the regions from the GPU silence detector
+    equal the reference's (restated, plan_cases-pinned) find_silent_regions; the plan's
+    decode starts at registration from the HBM copy of the signal (one
+    decode_device_batches call, no host upload, no per-chunk decode) and the two workers'
+    decode_chunk words equal the per-chunk path's."""
+    from zasr.plan import best_split, plan_chunks, silent_regions
+    from zasr.synth_audio import synth_speech
+    ae, rec = dropin_rec
+    concat = synth_speech(260.0, 41)
+    plan = plan_chunks(concat)
+    h = rec["handle"]
+    want = [ae.decode_chunk(rec, concat[s:e].copy(), s / 16000.0) for s, e, _ in plan]
+    n = _calls(h)
+    nb = {"batches": 0}
+    b0 = h.decode_device_batches
+
+    def dev_batches(*a, **k):
+        nb["batches"] += 1
+        return b0(*a, **k)
+    h.decode_device_batches = dev_batches
+    try:
+        regions = ae.plan_ahead_regions(concat, best_split)
+        assert regions == silent_regions(concat)
+        got = _loop(ae, rec, concat, plan)
+        assert nb["batches"] == 1 and n["decode"] == 0 and n["feat"] == 0, (nb, n)
+    finally:
+        del h.decode, h.decode_features, h.decode_device_batches
+    assert sum(len(w) for w in want) > 50
+    assert got == want
