@@ -217,38 +217,42 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
 // sums over blocks of 8, combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail in
 // order; n > 128 -> the halves [0, n2) and [n2, n) with n2 = n/2 rounded down to a multiple
 // of 8, summed separately and added.  Then / n (f32 true divide), sqrt (correctly rounded),
-// and the comparison in f32 (a Python float threshold is cast to the array's f32).  Every
-// square and add is an explicit _rn op, so nothing contracts into an FMA.
+// and the comparison in f32 (a Python float threshold is cast to the array's f32).  No
+// square and add may contract into an FMA (see np_pairwise_sq).
 // One thread per frame; the frame's row is read as float4s (rows are 16-byte aligned when
 // frame_len % 4 == 0, host-checked).  HBM-bound: 4 B per sample.
 // =====================================================================================
+// HIP's __fadd_rn / __fmul_rn are plain operators (contractible into FMAs) and __fsqrt_rn is
+// the native sqrt unless OCML_BASIC_ROUNDED_OPERATIONS is set (clang __clang_hip_math.h): the
+// code below turns contraction off and uses sqrtf / '/', which hipcc lowers correctly rounded
+// (-fhip-fp32-correctly-rounded-divide-sqrt is the default).
 __device__ __forceinline__ float np_pairwise_sq(const float* x, int n) {
+#pragma clang fp contract(off)
   // n <= 128: numpy's unrolled block sum of x[i]^2
   if (n < 8) {
     float s = -0.0f;
-    for (int i = 0; i < n; ++i) s = __fadd_rn(s, __fmul_rn(x[i], x[i]));
+    for (int i = 0; i < n; ++i) s = s + x[i] * x[i];
     return s;
   }
   float r[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = __fmul_rn(x[j], x[j]);
+  for (int j = 0; j < 8; ++j) r[j] = x[j] * x[j];
   int i = 8;
   const int nb = n - (n % 8);
   for (; i < nb; i += 8) {
     const float4 a = *reinterpret_cast<const float4*>(x + i);
     const float4 b = *reinterpret_cast<const float4*>(x + i + 4);
-    r[0] = __fadd_rn(r[0], __fmul_rn(a.x, a.x));
-    r[1] = __fadd_rn(r[1], __fmul_rn(a.y, a.y));
-    r[2] = __fadd_rn(r[2], __fmul_rn(a.z, a.z));
-    r[3] = __fadd_rn(r[3], __fmul_rn(a.w, a.w));
-    r[4] = __fadd_rn(r[4], __fmul_rn(b.x, b.x));
-    r[5] = __fadd_rn(r[5], __fmul_rn(b.y, b.y));
-    r[6] = __fadd_rn(r[6], __fmul_rn(b.z, b.z));
-    r[7] = __fadd_rn(r[7], __fmul_rn(b.w, b.w));
+    r[0] = r[0] + a.x * a.x;
+    r[1] = r[1] + a.y * a.y;
+    r[2] = r[2] + a.z * a.z;
+    r[3] = r[3] + a.w * a.w;
+    r[4] = r[4] + b.x * b.x;
+    r[5] = r[5] + b.y * b.y;
+    r[6] = r[6] + b.z * b.z;
+    r[7] = r[7] + b.w * b.w;
   }
-  float s = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
-                      __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
-  for (; i < n; ++i) s = __fadd_rn(s, __fmul_rn(x[i], x[i]));
+  float s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) s = s + x[i] * x[i];
   return s;
 }
 
@@ -256,6 +260,7 @@ __global__ __launch_bounds__(256) void silence_flags_kernel(const float* __restr
                                                             long nframes, int flen, int n2,
                                                             float threshold,
                                                             unsigned char* __restrict__ flags) {
+#pragma clang fp contract(off)
   const long f = (long)blockIdx.x * 256 + threadIdx.x;
   if (f >= nframes) return;
   const float* x = wav + f * flen;
@@ -263,9 +268,9 @@ __global__ __launch_bounds__(256) void silence_flags_kernel(const float* __restr
   if (n2 == 0) {
     s = np_pairwise_sq(x, flen);
   } else {
-    s = __fadd_rn(np_pairwise_sq(x, n2), np_pairwise_sq(x + n2, flen - n2));
+    s = np_pairwise_sq(x, n2) + np_pairwise_sq(x + n2, flen - n2);
   }
-  const float e = __fsqrt_rn(__fdiv_rn(s, (float)flen));
+  const float e = sqrtf(s / (float)flen);
   flags[f] = e < threshold ? 1 : 0;
 }
 

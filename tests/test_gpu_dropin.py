@@ -147,7 +147,7 @@ def test_silence_flags_bit_exact_vs_numpy(flen):
     silence_flags(d.data_ptr(), len(a), flen, 0.01, flags.data_ptr())
     got = flags.cpu().numpy().astype(bool)
     want = _np_flags(a, flen)
-    assert 0.2 < want.mean() < 0.8
+    assert 0.1 < want.mean() < 0.5  # a sixth of the frames below the threshold
     assert np.array_equal(got, want), int((got != want).sum())
 
 
