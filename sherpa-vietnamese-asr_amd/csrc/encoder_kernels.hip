@@ -87,32 +87,52 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
   __syncthreads();  // tables staged
   const int* offs = off_lds ? sOff : fr_off;
   // grid-stride over frames: each wave takes frames w + kFbWaves * blockIdx.x + k * stride, so
-  // the tables are staged once per block, not once per 4 frames
+  // the tables are staged once per block, not once per 4 frames.  The samples of the wave's
+  // NEXT frame are gathered before the current frame is computed (7 loads per lane in flight
+  // under the FFT and mel work; the index is clamped, so the loads are unconditional and the
+  // waits stay counted)
   const int stride = gridDim.x * kFbWaves;
-  for (int frame = blockIdx.x * kFbWaves + w; frame < total_frames; frame += stride) {
-  float xv[7];
-  float ctx0 = 0.f;  // CAMPP: the signal sample before the frame (scaled; 0 for frame 0)
-  {
+  auto gather = [&](int frame, float (&x)[7], float& ctx, int& f) {
     const int b = find_seq(offs, nseq, frame);
-    const int f = frame - offs[b];
+    f = frame - offs[b];
     const long n = nsamp[b];
     const float* base = wav + wav_off[b];
     if constexpr (CAMPP) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         const int i = lane + 64 * k;
-        xv[k] = base[(long)f * 160 + (i < 400 ? i : 399)] * 32768.0f;
+        x[k] = base[(long)f * 160 + (i < 400 ? i : 399)];
       }
-      ctx0 = f > 0 ? base[(long)f * 160 - 1] * 32768.0f : 0.f;
+      ctx = base[f > 0 ? (long)f * 160 - 1 : 0];
     } else {
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         const int i = lane + 64 * k;
         long s = (long)f * 160 - 120 + (i < 400 ? i : 399);
         while (s < 0 || s >= n) s = (s < 0) ? (-s - 1) : (2L * n - 1 - s);
-        xv[k] = base[s];
+        x[k] = base[s];
       }
+      ctx = 0.f;
     }
+  };
+  const int first = blockIdx.x * kFbWaves + w;
+  float xn[7], ctxn = 0.f;
+  int fn = 0;
+  if (first < total_frames) gather(first, xn, ctxn, fn);
+  for (int frame = first; frame < total_frames; frame += stride) {
+  float xv[7];
+  float ctx0 = 0.f;  // CAMPP: the signal sample before the frame (scaled; 0 for frame 0)
+  {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) xv[k] = xn[k];
+    const int f0 = fn;
+    if constexpr (CAMPP) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) xv[k] *= 32768.0f;
+      ctx0 = f0 > 0 ? ctxn * 32768.0f : 0.f;
+    }
+    const int nxt = frame + stride < total_frames ? frame + stride : total_frames - 1;
+    gather(nxt, xn, ctxn, fn);
     double part = 0.0;
 #pragma unroll
     for (int k = 0; k < 7; ++k)
@@ -187,8 +207,18 @@ __global__ __launch_bounds__(64 * kFbWaves) void fbank_kernel(
   __builtin_amdgcn_wave_barrier();
   for (int m = lane; m < 80; m += 64) {
     const int st = sMeta[m], ln = sMeta[80 + m], wo = sMeta[160 + m];
+    // the taps in order (the same fma chain), four LDS pairs read ahead of their fmas
     float acc = 0.f;
-    for (int k = 0; k < ln; ++k) acc = fmaf(sMelW[wo + k], pw[st + k], acc);
+    int k = 0;
+    for (; k + 4 <= ln; k += 4) {
+      const float w0 = sMelW[wo + k], w1 = sMelW[wo + k + 1], w2 = sMelW[wo + k + 2], w3 = sMelW[wo + k + 3];
+      const float p0 = pw[st + k], p1 = pw[st + k + 1], p2 = pw[st + k + 2], p3 = pw[st + k + 3];
+      acc = fmaf(w0, p0, acc);
+      acc = fmaf(w1, p1, acc);
+      acc = fmaf(w2, p2, acc);
+      acc = fmaf(w3, p3, acc);
+    }
+    for (; k < ln; ++k) acc = fmaf(sMelW[wo + k], pw[st + k], acc);
     out[(long)frame * 80 + m] = logf(fmaxf(acc, CAMPP ? 1.0f : 1.1920928955078125e-07f));
   }
   __builtin_amdgcn_wave_barrier();  // the next frame rewrites this wave's A / B images

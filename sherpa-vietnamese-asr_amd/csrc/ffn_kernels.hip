@@ -15,6 +15,8 @@
 // 4 waves (128 tokens), double-buffered: the next chunk's global loads are in flight while the
 // current chunk computes.  Epilogue: X[token][d] += O^T + b2 (f32 read-modify-write).
 // Bytes per token: D * 4 read + D * 4 written; the 2 F D bf16 weight bytes are L2-resident.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -286,25 +288,65 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
 #pragma unroll
     for (int s = 0; s < KS; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(p + s * 512);
   };
-  bf16x8 w2f[4][OT];
-  auto load_w2 = [&](int c) {
+#ifndef ZASR_FFN_W2SETS
+#define ZASR_FFN_W2SETS 2
+#endif
+#ifndef ZASR_FFN_AORDER
+#define ZASR_FFN_AORDER 0
+#endif
+  // W2SETS = 2: two W2 register sets; chunk c + 1's W2 goes out right after chunk c's H
+  // barrier (with its W1), so it has chunk c's phase B AND chunk c + 1's phase A to land
+  // instead of phase A alone.  W2SETS = 1: the single set reloaded after phase B.
+  constexpr int W2S = ZASR_FFN_W2SETS;
+  // AORDER: phase A token-sub-tile outer with the SwooshL / H write interleaved (two H
+  // buffers only: with one, the barrier before the H write would move in front of phase A)
+  constexpr bool AO = ZASR_FFN_AORDER && NB == 2;
+  bf16x8 w2f[W2S][4][OT];
+  auto load_w2 = [&](int c, auto set) {
+    constexpr int S = decltype(set)::value;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int ks = min(c * (HC / 32) + s, S2 - 1);
 #pragma unroll
       for (int t = 0; t < OT; ++t)
-        w2f[s][t] = *reinterpret_cast<const bf16x8*>(W2 + (((long)(wid * OW / 16 + t) * S2 + ks) * 64 + lane) * 8);
+        w2f[S][s][t] = *reinterpret_cast<const bf16x8*>(W2 + (((long)(wid * OW / 16 + t) * S2 + ks) * 64 + lane) * 8);
     }
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, W2S - 1>;
   load_w1(0);
-  load_w2(0);
+  load_w2(0, I0{});
   for (int e = tid; e < F; e += 64 * NW) sB1[e] = b1[e];
   lds_barrier();
   FFN_STAMP(1)
-  for (int c = 0; c < nch; ++c) {
+  auto chunk = [&](int c, auto set) {
+    constexpr int S = decltype(set)::value;
     const int hid0 = c * HC + wid * 16;
     const bool hvalid = hid0 < F;  // F % 16 == 0: a wave's 16 units are all valid or none
     FFN_STAMP(2 + 4 * c)
+    __bf16* sHc = sH[NB == 2 ? (c & 1) : 0];
+    if constexpr (AO) {
+      // token sub-tile outer: ha is complete after its KS MFMAs, so its bias + SwooshL + H
+      // write (VALU / LDS) issue beside the next sub-tile's MFMAs instead of after all of
+      // them (two H buffers: see below why no barrier precedes the write)
+      const float4 bb = *reinterpret_cast<const float4*>(&sB1[min(hid0, F - 16) + 4 * g4]);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        f32x4 ha = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&sX[(16 * u + r16) * XLD + 32 * s + 8 * g4]);
+          ha = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[s], xb, ha, 0, 0, 0);
+        }
+        bf16x4 p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = hvalid ? (__bf16)swooshl_fast(ha[q] + bv[q]) : (__bf16)0.f;
+        *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = p;
+      }
+      FFN_STAMP(3 + 4 * c)
+      FFN_STAMP(4 + 4 * c)
+    } else {
     f32x4 ha[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) ha[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -322,7 +364,6 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
     // buffer: a barrier first, so the previous chunk's phase B is done everywhere
     if constexpr (NB == 1) lds_barrier();
     FFN_STAMP(4 + 4 * c)
-    __bf16* sHc = sH[NB == 2 ? (c & 1) : 0];
     if (hvalid) {
       const float4 bb = *reinterpret_cast<const float4*>(&sB1[hid0 + 4 * g4]);
       const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
@@ -338,10 +379,12 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
 #pragma unroll
       for (int u = 0; u < 4; ++u) *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = z;
     }
+    }
     lds_barrier();
     FFN_STAMP(5 + 4 * c)
     // in-order vmcnt: the next chunk's W1 (needed first) is issued before its W2
     load_w1(min(c + 1, nch - 1));  // unconditional: a branch here costs exact vmcnt tracking
+    if constexpr (W2S == 2) load_w2(min(c + 1, nch - 1), std::integral_constant<int, 1 - S>{});
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8 hf[4];
@@ -350,9 +393,15 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
 #pragma unroll
       for (int t = 0; t < OT; ++t)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) o[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[s][t], hf[u], o[t][u], 0, 0, 0);
+        for (int u = 0; u < 4; ++u) o[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[S][s][t], hf[u], o[t][u], 0, 0, 0);
     }
-    load_w2(min(c + 1, nch - 1));
+    if constexpr (W2S == 1) load_w2(min(c + 1, nch - 1), I0{});
+  };
+  for (int c = 0; c < nch; c += W2S) {
+    chunk(c, I0{});
+    if constexpr (W2S == 2) {
+      if (c + 1 < nch) chunk(c + 1, I1{});
+    }
   }
 
   // ---- X[tok][ch] += O^T + b2 (+ bypass_mid): lane's token, 4 consecutive channels ----
