@@ -1401,6 +1401,10 @@ def main():
                     "unit": None, "frac": None, "traffic": None}
         roof["avg_launch_ms"] = round(per_launch_s * 1e3, 4)
         roof["launches_per_step"] = cnt // nprof
+        roof["timing"] = (f"HIP events around every launch of the class on its stream, over "
+                          f"{nprof} extra profiled steps after the timed region (profile mode "
+                          f"times each kernel alone; the timed steps above run the batch "
+                          f"pipeline, where kernels of two batches overlap)")
         tr = pmc_traffic(dom, args)
         if tr is not None:
             roof["traffic"] = tr["bytes_per_launch"]

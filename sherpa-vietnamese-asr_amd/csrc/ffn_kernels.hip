@@ -291,16 +291,14 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
 #ifndef ZASR_FFN_W2SETS
 #define ZASR_FFN_W2SETS 2
 #endif
-#ifndef ZASR_FFN_AORDER
-#define ZASR_FFN_AORDER 0
-#endif
+
   // W2SETS = 2: two W2 register sets; chunk c + 1's W2 goes out right after chunk c's H
   // barrier (with its W1), so it has chunk c's phase B AND chunk c + 1's phase A to land
   // instead of phase A alone.  W2SETS = 1: the single set reloaded after phase B.
   constexpr int W2S = ZASR_FFN_W2SETS;
-  // AORDER: phase A token-sub-tile outer with the SwooshL / H write interleaved (two H
-  // buffers only: with one, the barrier before the H write would move in front of phase A)
-  constexpr bool AO = ZASR_FFN_AORDER && NB == 2;
+  // (measured and dropped: phase A token-sub-tile outer with each sub-tile's SwooshL / H
+  // write interleaved -- phase A 2200 -> 3800 cycles, the kernel 10-16 % slower,
+  // profiles/r03/ffn_w2sets/aorder_*)
   bf16x8 w2f[W2S][4][OT];
   auto load_w2 = [&](int c, auto set) {
     constexpr int S = decltype(set)::value;
@@ -325,28 +323,6 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
     const bool hvalid = hid0 < F;  // F % 16 == 0: a wave's 16 units are all valid or none
     FFN_STAMP(2 + 4 * c)
     __bf16* sHc = sH[NB == 2 ? (c & 1) : 0];
-    if constexpr (AO) {
-      // token sub-tile outer: ha is complete after its KS MFMAs, so its bias + SwooshL + H
-      // write (VALU / LDS) issue beside the next sub-tile's MFMAs instead of after all of
-      // them (two H buffers: see below why no barrier precedes the write)
-      const float4 bb = *reinterpret_cast<const float4*>(&sB1[min(hid0, F - 16) + 4 * g4]);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        f32x4 ha = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&sX[(16 * u + r16) * XLD + 32 * s + 8 * g4]);
-          ha = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[s], xb, ha, 0, 0, 0);
-        }
-        bf16x4 p;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) p[q] = hvalid ? (__bf16)swooshl_fast(ha[q] + bv[q]) : (__bf16)0.f;
-        *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = p;
-      }
-      FFN_STAMP(3 + 4 * c)
-      FFN_STAMP(4 + 4 * c)
-    } else {
     f32x4 ha[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) ha[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -378,7 +354,6 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
       const bf16x4 z = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
 #pragma unroll
       for (int u = 0; u < 4; ++u) *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = z;
-    }
     }
     lds_barrier();
     FFN_STAMP(5 + 4 * c)
