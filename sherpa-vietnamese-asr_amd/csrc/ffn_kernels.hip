@@ -296,9 +296,11 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
   // barrier (with its W1), so it has chunk c's phase B AND chunk c + 1's phase A to land
   // instead of phase A alone.  W2SETS = 1: the single set reloaded after phase B.
   constexpr int W2S = ZASR_FFN_W2SETS;
-  // (measured and dropped: phase A token-sub-tile outer with each sub-tile's SwooshL / H
-  // write interleaved -- phase A 2200 -> 3800 cycles, the kernel 10-16 % slower,
-  // profiles/r03/ffn_w2sets/aorder_*)
+  // Measured and dropped (profiles/r03/ffn_w2sets/): phase A token-sub-tile outer with each
+  // sub-tile's SwooshL / H write interleaved (phase A 2200 -> 3800 cycles, 10-16 % slower);
+  // a software-pipelined loop running chunk c + 1's phase A in the instruction stream of
+  // chunk c's SwooshL / H write, with and without sched_group_barrier interleaving (the
+  // SwooshL VALU stayed a ~2000-cycle block after the MFMAs; +-2 %, no gain).
   bf16x8 w2f[W2S][4][OT];
   auto load_w2 = [&](int c, auto set) {
     constexpr int S = decltype(set)::value;
