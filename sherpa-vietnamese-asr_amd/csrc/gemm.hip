@@ -1006,12 +1006,63 @@ bool try_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   return true;
 }
 
+// Measured tile per projection shape of the Zipformer stacks (tools/gemm_tune.hip over the
+// bench's shape table, profiles/r03/gemm_tune/): every variant accumulates each output over
+// the same 32-deep K slabs in the same MFMA order, so the choice changes speed only (the lab
+// checks the outputs are bit-identical).  Used for large row counts (the batched encoder);
+// other shapes keep the generic heuristics below.  enc_gemm 7.87 -> 7.40 ms in the lab.
+enum TunedTile { TT_NONE, TT_GLDS3, TT_64x64, TT_64x128, TT_128x64, TT_128x128, TT_256x128 };
+struct TunedEntry {
+  short K, N;
+  signed char a16, c16, epi;
+  signed char tile;
+};
+constexpr TunedEntry kTuned[] = {
+    // residual projections: bf16 A -> f32 C += (EPI_RESADD)
+    {384, 384, 1, 0, EPI_RESADD, TT_GLDS3},   {288, 384, 1, 0, EPI_RESADD, TT_GLDS3},
+    {256, 256, 1, 0, EPI_RESADD, TT_128x64},  {192, 256, 1, 0, EPI_RESADD, TT_64x128},
+    {48, 384, 1, 0, EPI_RESADD, TT_64x64},    {48, 256, 1, 0, EPI_RESADD, TT_64x64},
+    {48, 192, 1, 0, EPI_RESADD, TT_64x64},    {96, 512, 1, 0, EPI_RESADD, TT_64x64},
+    {144, 192, 1, 0, EPI_RESADD, TT_64x64},
+    // in-projections from the f32 residual stream -> bf16
+    {384, 864, 0, 1, EPI_NONE, TT_128x128},   {192, 384, 0, 1, EPI_NONE, TT_128x128},
+    {192, 272, 0, 1, EPI_NONE, TT_128x128},   {384, 272, 0, 1, EPI_NONE, TT_128x128},
+    {256, 272, 0, 1, EPI_NONE, TT_256x128},   {256, 576, 0, 1, EPI_NONE, TT_256x128},
+    {512, 544, 0, 1, EPI_NONE, TT_256x128},   {512, 96, 0, 1, EPI_NONE, TT_64x128},
+    {384, 48, 0, 1, EPI_NONE, TT_128x64},     {256, 48, 0, 1, EPI_NONE, TT_64x64},
+    {192, 48, 0, 1, EPI_NONE, TT_64x64},
+    // Conv2dSubsampling output linear (K = 128 channels x 19 freq)
+    {2432, 192, 1, 0, EPI_NONE, TT_256x128},
+};
+
+template <int EPI, typename TA, typename TC>
+int tuned_tile(const GemmParams& p) {
+  static const bool off = getenv("ZASR_GEMM_TUNED") != nullptr && atoi(getenv("ZASR_GEMM_TUNED")) == 0;
+  if (off || p.slices != nullptr || p.M < 16384 || p.lda != p.K || p.sbn % 8 != 0) return TT_NONE;
+  const int a16 = std::is_same<TA, __bf16>::value, c16 = std::is_same<TC, __bf16>::value;
+  for (const TunedEntry& e : kTuned)
+    if (e.K == p.K && e.N == p.N && e.a16 == a16 && e.c16 == c16 && e.epi == EPI) return e.tile;
+  return TT_NONE;
+}
+
 // BK = 32: at these K (72..1920) the 2-stage 64-deep variant measured 20-60 % slower (LDS
 // occupancy), tools/gemm_bench.hip
 template <int ALOAD, int EPI, typename TA, typename TC>
 void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
-  if constexpr (ALOAD == ALOAD_DENSE && EPI != EPI_MULAUX && EPI != EPI_MULAUX16)
+  if constexpr (ALOAD == ALOAD_DENSE && EPI != EPI_MULAUX && EPI != EPI_MULAUX16) {
+    switch (tuned_tile<EPI, TA, TC>(p)) {
+      case TT_GLDS3:
+        if (p.K % 32 == 0 && p.K >= 128 && p.lda % 8 == 0) return launch_glds<3, EPI, TA, TC>(p, Bw, st);
+        break;
+      case TT_64x64: return launch_h<64, 64, 32, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+      case TT_64x128: return launch_h<64, 128, 32, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+      case TT_128x64: return launch_h<128, 64, 32, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+      case TT_128x128: return launch_h<128, 128, 32, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+      case TT_256x128: return launch_h<256, 128, 32, 4, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
+      default: break;
+    }
     if (try_glds<EPI, TA, TC>(p, Bw, st)) return;
+  }
   launch_tile_h<32, ALOAD, EPI, TA, TC>(p, Bw, st);
 }
 

@@ -1,0 +1,159 @@
+// Tile-shape sweep of the encoder projection GEMMs (development tool, not part of libzasr):
+// every bf16-mode enc_gemm shape of the 68M bench step (bench.py --shape-table) through every
+// register-staged tile (launch_h) and the LDS-DMA kernel (launch_glds), mean of 10 launches
+// after 2 warm-ups.  All variants accumulate each output over the same 32-deep K slabs in the
+// same MFMA order, so their results are bit-identical (checked here against the default
+// launch on 4096 sampled outputs): the choice is a pure speed decision.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -o gemm_tune gemm_tune.hip
+#include "../csrc/gemm.hip"
+
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <vector>
+
+using namespace zasr;
+
+struct Shape {
+  int M, K, N;
+  bool a16, c16;
+  int epi;
+};
+
+static float* dA;
+static __bf16 *dA16, *dB, *dC16, *dRef16;
+static float *dC, *dRef, *dbias;
+
+template <typename TA, typename TC, int EPI>
+static void sweep(const Shape& s) {
+  GemmParams p{};
+  p.A = std::is_same<TA, float>::value ? dA : reinterpret_cast<const float*>(dA16);
+  p.lda = s.K;
+  p.sbk = 1;
+  p.sbn = s.K;
+  p.C = std::is_same<TC, float>::value ? dC : reinterpret_cast<float*>(dC16);
+  p.ldc = s.N;
+  p.bias = dbias;
+  p.M = s.M;
+  p.N = s.N;
+  p.K = s.K;
+  p.alpha = 1.f;
+  p.max_M = s.M;
+  const size_t cbytes = (size_t)s.M * s.N * sizeof(TC);
+  void* ref = std::is_same<TC, float>::value ? (void*)dRef : (void*)dRef16;
+  // reference output of the default launch (RESADD: C starts at zero for the check)
+  hipMemset(p.C, 0, cbytes);
+  launch_bk_h<ALOAD_DENSE, EPI, TA, TC>(p, dB, 0);
+  hipMemcpy(ref, p.C, cbytes, hipMemcpyDeviceToDevice);
+  std::vector<std::pair<const char*, std::function<void()>>> vars = {
+      {"default", [&] { launch_bk_h<ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"64x64", [&] { launch_h<64, 64, 32, 2, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"64x128", [&] { launch_h<64, 128, 32, 2, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"128x64", [&] { launch_h<128, 64, 32, 2, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"128x128", [&] { launch_h<128, 128, 32, 2, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"128x256", [&] { launch_h<128, 256, 32, 2, 4, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"256x128", [&] { launch_h<256, 128, 32, 4, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"128x32", [&] { launch_h<128, 32, 32, 4, 1, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"glds3", [&] { launch_glds<3, EPI, TA, TC>(p, dB, 0); }},
+      {"glds4", [&] { launch_glds<4, EPI, TA, TC>(p, dB, 0); }},
+  };
+  printf("M=%6d K=%5d N=%5d a%s c%s epi%d:", s.M, s.K, s.N, s.a16 ? "16" : "32",
+         s.c16 ? "16" : "32", EPI);
+  std::mt19937 rng(7);
+  for (auto& v : vars) {
+    if (!strncmp(v.first, "glds", 4) && (s.K % 32 != 0 || s.K < 128)) continue;
+    hipMemset(p.C, 0, cbytes);
+    v.second();
+    hipDeviceSynchronize();
+    // bit-identical check on sampled outputs
+    std::vector<unsigned short> a(4096), b(4096);
+    std::vector<float> af(4096), bf(4096);
+    bool same = true;
+    for (int q = 0; q < 4096 && same; ++q) {
+      const size_t idx = ((size_t)rng() * 2654435761u) % ((size_t)s.M * s.N);
+      if (std::is_same<TC, float>::value) {
+        hipMemcpy(&af[q], dC + idx, 4, hipMemcpyDeviceToHost);
+        hipMemcpy(&bf[q], dRef + idx, 4, hipMemcpyDeviceToHost);
+        same = memcmp(&af[q], &bf[q], 4) == 0;
+      } else {
+        hipMemcpy(&a[q], dC16 + idx, 2, hipMemcpyDeviceToHost);
+        hipMemcpy(&b[q], dRef16 + idx, 2, hipMemcpyDeviceToHost);
+        same = a[q] == b[q];
+      }
+      if (q >= 256) break;  // 256 samples keep the sweep short
+    }
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    v.second();
+    v.second();
+    hipEventRecord(e0, 0);
+    for (int r = 0; r < 10; ++r) v.second();
+    hipEventRecord(e1, 0);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("  %s %.1f%s", v.first, ms * 100.f, same ? "" : "(DIFF)");
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  }
+  printf("\n");
+  fflush(stdout);
+}
+
+int main() {
+  // bench.py --shape-table, bf16 mode, 68M, 1 h per step (profiles/r03/ffn_w2sets/)
+  std::vector<Shape> shapes = {
+      {49442, 384, 768, false, true, EPI_NONE},   {49442, 384, 384, true, false, EPI_RESADD},
+      {98813, 256, 512, false, true, EPI_NONE},   {98813, 256, 256, true, false, EPI_RESADD},
+      {197561, 2432, 192, true, false, EPI_NONE}, {49442, 384, 864, false, true, EPI_NONE},
+      {49442, 48, 384, true, false, EPI_RESADD},  {197561, 192, 384, false, true, EPI_NONE},
+      {24753, 512, 1024, false, true, EPI_NONE},  {197561, 192, 192, true, false, EPI_RESADD},
+      {49442, 288, 384, true, false, EPI_RESADD}, {98813, 48, 256, true, false, EPI_RESADD},
+      {24753, 512, 512, true, false, EPI_RESADD}, {98813, 256, 576, false, true, EPI_NONE},
+      {197561, 192, 272, false, true, EPI_NONE},  {49442, 384, 272, false, true, EPI_NONE},
+      {197561, 48, 192, true, false, EPI_RESADD}, {49442, 384, 48, false, true, EPI_NONE},
+      {98813, 256, 272, false, true, EPI_NONE},   {98813, 192, 256, true, false, EPI_RESADD},
+      {197561, 192, 432, false, true, EPI_NONE},  {24753, 512, 1152, false, true, EPI_NONE},
+      {98813, 256, 48, false, true, EPI_NONE},    {24753, 96, 512, true, false, EPI_RESADD},
+      {24753, 512, 544, false, true, EPI_NONE},   {197561, 144, 192, true, false, EPI_RESADD},
+      {24753, 512, 96, false, true, EPI_NONE},    {98813, 512, 512, false, false, EPI_NONE},
+      {24753, 384, 512, true, false, EPI_RESADD}, {197561, 192, 48, false, true, EPI_NONE},
+  };
+  size_t maxA = 0, maxC = 0, maxB = 0;
+  for (auto& s : shapes) {
+    maxA = std::max(maxA, (size_t)s.M * s.K);
+    maxC = std::max(maxC, (size_t)s.M * s.N);
+    maxB = std::max(maxB, (size_t)s.N * s.K);
+  }
+  hipMalloc(&dA, maxA * 4);
+  hipMalloc(&dA16, maxA * 2);
+  hipMalloc(&dC, maxC * 4);
+  hipMalloc(&dC16, maxC * 2);
+  hipMalloc(&dRef, maxC * 4);
+  hipMalloc(&dRef16, maxC * 2);
+  hipMalloc(&dB, maxB * 2);
+  hipMalloc(&dbias, 4096 * 4);
+  std::mt19937 rng(1);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  std::vector<float> hA(maxA), hbias(4096);
+  std::vector<__bf16> hA16(maxA), hB16(maxB);
+  for (size_t i = 0; i < maxA; ++i) {
+    hA[i] = nd(rng);
+    hA16[i] = (__bf16)hA[i];
+  }
+  for (auto& x : hB16) x = (__bf16)(nd(rng) * 0.08f);
+  for (auto& x : hbias) x = nd(rng) * 0.1f;
+  hipMemcpy(dA, hA.data(), maxA * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dA16, hA16.data(), maxA * 2, hipMemcpyHostToDevice);
+  hipMemcpy(dB, hB16.data(), maxB * 2, hipMemcpyHostToDevice);
+  hipMemcpy(dbias, hbias.data(), 4096 * 4, hipMemcpyHostToDevice);
+  for (auto& s : shapes) {
+    if (!s.a16 && s.c16 && s.epi == EPI_NONE) sweep<float, __bf16, EPI_NONE>(s);
+    else if (s.a16 && !s.c16 && s.epi == EPI_RESADD) sweep<__bf16, float, EPI_RESADD>(s);
+    else if (s.a16 && !s.c16 && s.epi == EPI_NONE) sweep<__bf16, float, EPI_NONE>(s);
+    else if (!s.a16 && !s.c16 && s.epi == EPI_NONE) sweep<float, float, EPI_NONE>(s);
+  }
+  return 0;
+}
