@@ -23,4 +23,5 @@ timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwo
 timeout -k 10 300 python3 $R/bench.py --stage pipe --steps 4 --warmup 1 > $OUT/bench_pipe.json 2> $OUT/bench_pipe.err
 timeout -k 10 300 python3 $R/bench.py --stage campp > $OUT/bench_campp.json 2> $OUT/bench_campp.err
 timeout -k 10 300 python3 $R/bench.py --stage vad > $OUT/bench_vad.json 2> $OUT/bench_vad.err
+timeout -k 10 300 python3 $R/bench.py --stage dropin --steps 3 --warmup 1 --hotwords-file default > $OUT/bench_dropin.json 2> $OUT/bench_dropin.err
 echo done
