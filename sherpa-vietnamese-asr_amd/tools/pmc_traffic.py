@@ -34,8 +34,11 @@ def gemm_args(name: str):
 
 def in_class(name: str, cls: str) -> bool:
     if cls == "enc_gemm":
-        if "gemm_glds_kernel" in name:  # multi-stage LDS-DMA variant: dense projections only
-            return True
+        if "gemm_glds_kernel" in name:  # multi-stage LDS-DMA variant: its EPI_MULAUX(16)
+            # z-sliced instances are the NonlinAttention product (class attn_nonlin)
+            m = re.search(r"gemm_glds_kernel(?:<\s*\d+,\s*(\d+)|ILi\d+ELi(\d+)E)", name)
+            epi = (m.group(1) or m.group(2)) if m else "0"
+            return epi not in ("4", "5")
         kind, args = gemm_args(name)
         if kind is None:
             return False
