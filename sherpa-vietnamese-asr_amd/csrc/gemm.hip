@@ -1077,9 +1077,10 @@ void gemm_nonlin_bf16(const GemmParams& p, const void* Bw, hipStream_t st) {
   const int pad64 = cdiv(p.N, 64) * 64, pad128 = cdiv(p.N, 128) * 128;
   const int tm = cdiv(p.max_M, 128);
   const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
-  // BN 192 (ZASR_NONLIN_BN=192, A/B): one column tile for hid 144 / 192 (and two for 384),
-  // so each sequence's K = L-deep weight panel is streamed once per row tile instead of 2-3x
-  static const int nl_bn = getenv("ZASR_NONLIN_BN") ? atoi(getenv("ZASR_NONLIN_BN")) : 0;
+  // BN 192: one column tile for hid 144 / 192 (and two for 384), so each sequence's K = L-deep
+  // weight panel is streamed once per row tile instead of 2-3x: attn_nonlin 1.71 -> 1.58 ms
+  // per step (profiles/r03/nonlin_bn192/; ZASR_NONLIN_BN=0 restores the 64 / 128 tiles)
+  static const int nl_bn = getenv("ZASR_NONLIN_BN") ? atoi(getenv("ZASR_NONLIN_BN")) : 192;
   if (nl_bn == 192 && (p.N <= 192 || p.N % 192 == 0)) {
     const int tn = cdiv(p.N, 192);
     hipLaunchKernelGGL((gemm_glds_kernel<4, EPI_MULAUX16, __bf16, __bf16, 192, true>),
