@@ -1808,7 +1808,8 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   st_ = main_st;
   std::vector<TokenResult> out;
   out.reserve(n.size());
-  // E encoder streams; L = E batches' encoders are enqueued ahead of the search in flight.
+  // E encoder streams; L (= E + 1 by default, below) batches' encoders are enqueued ahead of
+  // the search in flight.
   // Batch k: encoder output / event / pinned arena slot k % (L + 1), stream + workspace set
   // k % E.  When batch k + L is enqueued, the previous user of its output slot (batch k - 1)
   // has been searched (the search returns on the host), and its stream's previous batch
@@ -1827,7 +1828,11 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
     return decode_batches_two_searches(d_wav, wav_off, n, batch_sizes, beam, main_st);
   const int want_e = env_e ? env_e : (beam > 1 ? 1 : 2);
   const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
-  const int L = E;
+  // L: batches whose encoders are queued ahead of the search in flight, one more than the
+  // encoder streams (at most kMaxEnc: L + 1 output slots): 111.8-113.1k -> 113.5-114.3k xRT
+  // on one box (profiles/r03/enc_ahead/); ZASR_ENC_AHEAD overrides
+  static const int env_ahead = getenv("ZASR_ENC_AHEAD") ? atoi(getenv("ZASR_ENC_AHEAD")) : 0;
+  const int L = std::max(E, std::min({env_ahead > 0 ? env_ahead : E + 1, (int)kMaxEnc, nb}));
   // encoder stream 0 is the caller's stream, or (CU-partitioned) the engine's masked stream
   hipStream_t enc_st[kMaxEnc] = {search_cus_ > 0 ? stream_ : main_st};
   for (int e = 1; e < kMaxEnc; ++e) enc_st[e] = enc_extra_[e - 1];
