@@ -1130,10 +1130,13 @@ def bench_dropin(args):
     omap = [(0, 0, len(concat))]  # no VAD cut: the identity offset map (:2181)
     info = {}
 
+    split = {"regions": 0.0, "decode_start": 0.0, "decode": 0.0, "after_decode": 0.0, "merge": 0.0}
+
     def phase():
         # the planner (:2137-2161) through the hook the drop-in installs on find_silent_regions:
         # the GPU silence detector (the signal stays in HBM, the plan's decode starts at once),
         # or with --no-pipeline / ZASR_GPU_PLANNER=0 the reference's numpy function
+        t0 = time.perf_counter()
         regions = ae.plan_ahead_regions(concat, best_split)
         if regions is None:
             regions = silent_regions(concat)
@@ -1154,18 +1157,32 @@ def bench_dropin(args):
 
         ts = [threading.Thread(target=worker, args=(list(range(k, len(plan), 2)),))
               for k in (0, 1)]
+        t1 = time.perf_counter()
         for t in ts:
             t.start()
         for t in ts:
             t.join()
+        t2 = time.perf_counter()
         merged, _ = merge_chunks_with_overlap(results)
+        t3 = time.perf_counter()
         info.update(chunks=len(plan), words=len(merged))
+        # phase split (ms per step, summed over the timed steps): the planner call, the plan's
+        # background decode, the workers' word building after it, the merge
+        jobs = [j for sig in ae._planned[-1:] for per in sig.jobs.values() for j in per.values()]
+        dec = jobs[0] if jobs and jobs[0].t_end is not None else None
+        split["regions"] += t1 - t0
+        split["decode_start"] += (dec.t_start - t0) if dec else 0.0
+        split["decode"] += (dec.t_end - dec.t_start) if dec else 0.0
+        split["after_decode"] += (t2 - max(dec.t_end, t1)) if dec else t2 - t1
+        split["merge"] += t3 - t2
 
     for _ in range(args.warmup):
         phase()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
+    for k in split:
+        split[k] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         phase()
@@ -1189,6 +1206,8 @@ def bench_dropin(args):
                                        f"1 h of host audio per GPU, timestamps mapped, overlap merge",
                            "plan_ahead": os.environ.get("ZASR_PLAN_AHEAD", "1") != "0",
                            "gpu_planner": ae._gpu_planner_on(),
+                           "phase_ms_per_step": {k: round(1000 * v / args.steps, 3)
+                                                 for k, v in split.items()},
                            **info},
                 "roofline": None, "cpu_baseline": None}
         print(json.dumps(line))

@@ -72,24 +72,31 @@ typedef struct {
   double tsallis_norm, margin, entropy_norm;
 } Ent;
 
-static int set_f(PyObject* d, const char* k, double v) {
+/* dict keys, interned once (PyDict_SetItemString would build and intern a str per call) */
+enum { K_TEXT, K_START, K_END, K_LSTART, K_LEND, K_PROB, K_TSMAX, K_MMIN, K_ENORM, K_CONF, K_TOKS,
+       K_TSL, K_N };
+static const char* const kKeyNames[K_N] = {
+    "text", "start", "end", "local_start", "local_end", "prob", "tsallis_max", "margin_min",
+    "entropy_norm", "_conf", "_chunk_bpe_tokens", "_chunk_bpe_timestamps_local"};
+static PyObject* kKeys[K_N];
+
+static int set_f(PyObject* d, int key, double v) {
   PyObject* o = PyFloat_FromDouble(v);
   if (!o) return -1;
-  int rc = PyDict_SetItemString(d, k, o);
+  int rc = PyDict_SetItem(d, kKeys[key], o);
   Py_DECREF(o);
   return rc;
 }
 
-/* _finalize_word_entropy (:1187-1206) of the current word: probs / ents of its pieces */
+/* _finalize_word_entropy (:1187-1206) of one word: probs / ents of its pieces */
 static int finalize(PyObject* w, const double* probs, Py_ssize_t np_, const Ent* ents,
                     Py_ssize_t ne, double* scratch) {
   double s = 0.0;
   for (Py_ssize_t i = 0; i < np_; ++i) s += probs[i];
-  if (set_f(w, "prob", s / (double)np_) < 0) return -1;
+  if (set_f(w, K_PROB, s / (double)np_) < 0) return -1;
   if (ne == 0) {
-    const char* keys[4] = {"tsallis_max", "margin_min", "entropy_norm", "_conf"};
-    for (int i = 0; i < 4; ++i)
-      if (PyDict_SetItemString(w, keys[i], Py_None) < 0) return -1;
+    for (int i = K_TSMAX; i <= K_CONF; ++i)
+      if (PyDict_SetItem(w, kKeys[i], Py_None) < 0) return -1;
     return 0;
   }
   double tmax = ents[0].tsallis_norm, mmin = ents[0].margin, conf = 0.0;
@@ -99,11 +106,27 @@ static int finalize(PyObject* w, const double* probs, Py_ssize_t np_, const Ent*
     scratch[i] = ents[i].entropy_norm;
     conf += ents[i].margin * (1.0 - ents[i].tsallis_norm);
   }
-  if (set_f(w, "tsallis_max", round4(tmax)) < 0) return -1;
-  if (set_f(w, "margin_min", round4(mmin)) < 0) return -1;
-  if (set_f(w, "entropy_norm", round4(pairwise(scratch, ne) / (double)ne)) < 0) return -1;
-  if (set_f(w, "_conf", round4(conf / (double)ne)) < 0) return -1;
+  if (set_f(w, K_TSMAX, round4(tmax)) < 0) return -1;
+  if (set_f(w, K_MMIN, round4(mmin)) < 0) return -1;
+  if (set_f(w, K_ENORM, round4(pairwise(scratch, ne) / (double)ne)) < 0) return -1;
+  if (set_f(w, K_CONF, round4(conf / (double)ne)) < 0) return -1;
   return 0;
+}
+
+/* text.startswith(" ") or text.startswith("▁") */
+static int starts_word(PyObject* text) {
+  if (PyUnicode_GET_LENGTH(text) == 0) return 0;
+  const Py_UCS4 c = PyUnicode_READ_CHAR(text, 0);
+  return c == 0x20 || c == 0x2581;
+}
+
+/* text.lstrip(" ").lstrip("▁") (a new reference) */
+static PyObject* strip_word_start(PyObject* text) {
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(text);
+  Py_ssize_t i = 0;
+  while (i < n && PyUnicode_READ_CHAR(text, i) == 0x20) ++i;
+  while (i < n && PyUnicode_READ_CHAR(text, i) == 0x2581) ++i;
+  return PyUnicode_Substring(text, i, n);
 }
 
 static int get_buf(PyObject* o, Py_buffer* b, Py_ssize_t itemsize, const char* what) {
@@ -147,15 +170,15 @@ static PyObject* words_from_search(PyObject* self, PyObject* args) {
   const double* lp = (const double*)bl.buf;
   const float* st = (const float*)bs.buf;
   PyObject* empty = PyUnicode_FromString("");
-  PyObject* sp = PyUnicode_FromString(" ");
-  PyObject* lower_bar = PyUnicode_FromString("\xe2\x96\x81"); /* U+2581 */
-  if (!words || !empty || !sp || !lower_bar) goto fail;
+  Py_ssize_t* wst = NULL;
+  if (!words || !empty) goto fail;
   if (k == 0 || T <= 0 || nfr < k) goto done;
   ts = (double*)malloc(sizeof(double) * k);
   probs = (double*)malloc(sizeof(double) * k);
   scratch = (double*)malloc(sizeof(double) * k);
   ents = (Ent*)malloc(sizeof(Ent) * k);
-  if (!ts || !probs || !scratch || !ents) { PyErr_NoMemory(); goto fail; }
+  wst = (Py_ssize_t*)malloc(sizeof(Py_ssize_t) * (k + 1));
+  if (!ts || !probs || !scratch || !ents || !wst) { PyErr_NoMemory(); goto fail; }
   {
     const double chunk_dur = (double)n_samples / 16000.0;
     for (Py_ssize_t j = 0; j < k; ++j) ts[j] = (double)fr[j] / (double)T * chunk_dur;
@@ -176,59 +199,47 @@ static PyObject* words_from_search(PyObject* self, PyObject* args) {
         ents[j].margin = 1.0;
         ents[j].entropy_norm = 0.0;
       }
-    }
-    Py_ssize_t w0 = 0;  /* first piece of the current word */
-    for (Py_ssize_t j = 0; j < k; ++j) {
-      const double t0 = ts[j];
-      const double t1 = j + 1 < k ? ts[j + 1] : t0 + avg;
       probs[j] = j < nlp ? exp(lp[j]) : 1.0;
+    }
+    /* word boundaries: a piece starting with " " or "▁" opens a word (:1227-1290) */
+    Py_ssize_t nw = 0;
+    for (Py_ssize_t j = 0; j < k; ++j) {
       const int id = tok[j];
       PyObject* text = (id >= 0 && id < ntab) ? PyList_GET_ITEM(lowered, id) : empty;
-      const int starts = PyUnicode_Tailmatch(text, sp, 0, PY_SSIZE_T_MAX, -1) == 1 ||
-                         PyUnicode_Tailmatch(text, lower_bar, 0, PY_SSIZE_T_MAX, -1) == 1;
-      if (starts || cur == NULL) {
-        if (cur != NULL) {
-          if (finalize(cur, probs + w0, j - w0, ents + w0, j - w0, scratch) < 0) goto fail;
-          if (PyList_Append(words, cur) < 0) goto fail;
-          Py_CLEAR(cur);
-        }
-        w0 = j;
-        cur = PyDict_New();
-        if (!cur) goto fail;
-        PyObject* t;
-        if (starts) {  /* text.lstrip(" ").lstrip("▁") */
-          PyObject* a = PyObject_CallMethod(text, "lstrip", "O", sp);
-          if (!a) goto fail;
-          t = PyObject_CallMethod(a, "lstrip", "O", lower_bar);
-          Py_DECREF(a);
-          if (!t) goto fail;
-        } else {
-          t = text;
-          Py_INCREF(t);
-        }
-        int rc = PyDict_SetItemString(cur, "text", t);
-        Py_DECREF(t);
-        if (rc < 0 || set_f(cur, "start", t0 + time_offset) < 0 ||
-            set_f(cur, "end", t1 + time_offset) < 0 || set_f(cur, "local_start", t0) < 0 ||
-            set_f(cur, "local_end", t1) < 0 || set_f(cur, "last_bpe_start", t0 + time_offset) < 0)
-          goto fail;
-      } else {
-        PyObject* old = PyDict_GetItemString(cur, "text"); /* borrowed */
-        PyObject* t = PyUnicode_Concat(old, text);
-        if (!t) goto fail;
-        int rc = PyDict_SetItemString(cur, "text", t);
-        Py_DECREF(t);
-        if (rc < 0 || set_f(cur, "end", t1 + time_offset) < 0 || set_f(cur, "local_end", t1) < 0 ||
-            set_f(cur, "last_bpe_start", t0 + time_offset) < 0)
-          goto fail;
-      }
+      if (j == 0 || starts_word(text)) wst[nw++] = j;
     }
-    if (cur != NULL) {
-      if (finalize(cur, probs + w0, k - w0, ents + w0, k - w0, scratch) < 0) goto fail;
+    wst[nw] = k;
+    /* one dict per word, keys in the order the reference's dicts end up with: text, start,
+     * end, local_start, local_end (end: the last piece's start + the mean piece spacing, capped
+     * at the next word's start, :1316-1322), then the entropy fields */
+    for (Py_ssize_t i = 0; i < nw; ++i) {
+      const Py_ssize_t a = wst[i], b = wst[i + 1];
+      PyObject* first = (tok[a] >= 0 && tok[a] < ntab) ? PyList_GET_ITEM(lowered, tok[a]) : empty;
+      PyObject* t = starts_word(first) ? strip_word_start(first) : (Py_INCREF(first), first);
+      if (!t) goto fail;
+      for (Py_ssize_t j = a + 1; j < b && t; ++j) {  /* cur["text"] += text */
+        PyObject* x = (tok[j] >= 0 && tok[j] < ntab) ? PyList_GET_ITEM(lowered, tok[j]) : empty;
+        PyObject* u = PyUnicode_Concat(t, x);
+        Py_DECREF(t);
+        t = u;
+      }
+      if (!t) goto fail;
+      cur = PyDict_New();
+      if (!cur) { Py_DECREF(t); goto fail; }
+      int rc = PyDict_SetItem(cur, kKeys[K_TEXT], t);
+      Py_DECREF(t);
+      double end = (ts[b - 1] + time_offset) + avg;
+      if (i + 1 < nw) {
+        const double nxt = ts[b] + time_offset;
+        if (nxt < end) end = nxt;  /* min(end, next start): the first argument on ties */
+      }
+      if (rc < 0 || set_f(cur, K_START, ts[a] + time_offset) < 0 || set_f(cur, K_END, end) < 0 ||
+          set_f(cur, K_LSTART, ts[a]) < 0 || set_f(cur, K_LEND, end - time_offset) < 0 ||
+          finalize(cur, probs + a, b - a, ents + a, b - a, scratch) < 0)
+        goto fail;
       if (PyList_Append(words, cur) < 0) goto fail;
       Py_CLEAR(cur);
     }
-    const Py_ssize_t nw = PyList_GET_SIZE(words);
     if (nw > 0) {
       PyObject* w = PyList_GET_ITEM(words, 0);
       PyObject* pl = PyList_New(k);
@@ -243,26 +254,16 @@ static PyObject* words_from_search(PyObject* self, PyObject* args) {
         if (!f) { Py_DECREF(pl); Py_DECREF(tl); goto fail; }
         PyList_SET_ITEM(tl, j, f);
       }
-      int rc = PyDict_SetItemString(w, "_chunk_bpe_tokens", pl);
+      int rc = PyDict_SetItem(w, kKeys[K_TOKS], pl);
       Py_DECREF(pl);
-      if (rc == 0) rc = PyDict_SetItemString(w, "_chunk_bpe_timestamps_local", tl);
+      if (rc == 0) rc = PyDict_SetItem(w, kKeys[K_TSL], tl);
       Py_DECREF(tl);
       if (rc < 0) goto fail;
     }
-    for (Py_ssize_t i = 0; i < nw; ++i) {
-      PyObject* w = PyList_GET_ITEM(words, i);
-      double end = PyFloat_AsDouble(PyDict_GetItemString(w, "last_bpe_start")) + avg;
-      if (i + 1 < nw) {
-        const double nxt = PyFloat_AsDouble(PyDict_GetItemString(PyList_GET_ITEM(words, i + 1), "start"));
-        if (nxt < end) end = nxt;  /* min(end, next start): the first argument on ties */
-      }
-      if (set_f(w, "end", end) < 0 || set_f(w, "local_end", end - time_offset) < 0) goto fail;
-      if (PyDict_DelItemString(w, "last_bpe_start") < 0) goto fail;
-    }
   }
 done:
-  free(ts); free(probs); free(scratch); free(ents);
-  Py_XDECREF(empty); Py_XDECREF(sp); Py_XDECREF(lower_bar);
+  free(ts); free(probs); free(scratch); free(ents); free(wst);
+  Py_XDECREF(empty);
   PyBuffer_Release(&bt); PyBuffer_Release(&bf); PyBuffer_Release(&bl); PyBuffer_Release(&bs);
   return words;
 fail:
@@ -286,4 +287,8 @@ static PyMethodDef methods[] = {
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_zasr_words", NULL, -1, methods};
 
-PyMODINIT_FUNC PyInit__zasr_words(void) { return PyModule_Create(&module); }
+PyMODINIT_FUNC PyInit__zasr_words(void) {
+  for (int i = 0; i < K_N; ++i)
+    if (!kKeys[i] && !(kKeys[i] = PyUnicode_InternFromString(kKeyNames[i]))) return NULL;
+  return PyModule_Create(&module);
+}

@@ -500,16 +500,20 @@ class _PlanDecode:
 
     def __init__(self, sig: _PlannedSignal, handle, beam: int):
         self.res, self.err = None, None
+        self.t_start = self.t_end = None  # perf_counter() around the decode (bench phase split)
         self.thread = threading.Thread(target=self._run, args=(weakref.ref(sig), handle, beam),
                                        name="zasr-plan-decode", daemon=True)
         self.thread.start()
 
     def _run(self, sig_ref, handle, beam):
+        import time
+        self.t_start = time.perf_counter()
         try:
             sig = sig_ref()
             self.res = sig._decode(handle, beam) if sig is not None else None
         except BaseException as e:  # re-raised in the caller's decode_chunk
             self.err = e
+        self.t_end = time.perf_counter()
 
     def wait(self):
         self.thread.join()

@@ -86,8 +86,8 @@ def regions_from_flags(quiet: np.ndarray, flen: int, n: int, min_silence: float 
     starts = np.flatnonzero(edges == 1)          # first quiet frame
     ends = np.flatnonzero(edges == -1)           # one past the last quiet frame
     need = int(min_silence / 0.01)
-    return [(int(a) * flen, min(int(b) * flen, n))
-            for a, b in zip(starts, ends) if b - a >= need]
+    keep = (ends - starts) >= need
+    return list(zip((starts[keep] * flen).tolist(), np.minimum(ends[keep] * flen, n).tolist()))
 
 
 def best_split(target: int, total: int, regions: Sequence[Span], window: int = 2 * SR) -> int:
