@@ -55,6 +55,10 @@ static void sweep(const Shape& s) {
       {"128x256", [&] { launch_h<128, 256, 32, 2, 4, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
       {"256x128", [&] { launch_h<256, 128, 32, 4, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
       {"128x32", [&] { launch_h<128, 32, 32, 4, 1, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"128x128k64", [&] { launch_h<128, 128, 64, 2, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"128x256k64", [&] { launch_h<128, 256, 64, 2, 4, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"256x128k64", [&] { launch_h<256, 128, 64, 4, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"64x128k64", [&] { launch_h<64, 128, 64, 2, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
       {"glds3", [&] { launch_glds<3, EPI, TA, TC>(p, dB, 0); }},
       {"glds4", [&] { launch_glds<4, EPI, TA, TC>(p, dB, 0); }},
   };
@@ -63,6 +67,7 @@ static void sweep(const Shape& s) {
   std::mt19937 rng(7);
   for (auto& v : vars) {
     if (!strncmp(v.first, "glds", 4) && (s.K % 32 != 0 || s.K < 128)) continue;
+    if (strstr(v.first, "k64") && (s.K % 64 != 0 || s.K < 128)) continue;
     hipMemset(p.C, 0, cbytes);
     v.second();
     hipDeviceSynchronize();
