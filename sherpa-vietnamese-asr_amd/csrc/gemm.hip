@@ -775,7 +775,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// BN = 64 / 128 (the four waves split it in two halves); SL: z-slices (one linear grid over
+// BN = 64 / 128 / 192 (the four waves split it in two halves); SL: z-slices (one linear grid over
 // (slice, tile); every slice's K a multiple of 32) -- the NonlinAttention product A0 @ t1 per
 // sequence, whose K = L-deep panels the register-staged kernel streams one slab at a time
 template <int NS, int EPI, typename TA, typename TC, int BN = 128, bool SL = false>
@@ -1011,7 +1011,7 @@ bool try_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
 // the same 32-deep K slabs in the same MFMA order, so the choice changes speed only (the lab
 // checks the outputs are bit-identical).  Used for large row counts (the batched encoder);
 // other shapes keep the generic heuristics below.  enc_gemm 7.87 -> 7.40 ms in the lab.
-enum TunedTile { TT_NONE, TT_GLDS3, TT_64x64, TT_64x128, TT_128x64, TT_128x128, TT_256x128 };
+enum TunedTile { TT_NONE, TT_GLDS3, TT_GLDS3_192, TT_64x64, TT_64x128, TT_128x64, TT_128x128, TT_256x128 };
 struct TunedEntry {
   short K, N;
   signed char a16, c16, epi;
@@ -1031,8 +1031,9 @@ constexpr TunedEntry kTuned[] = {
     {512, 544, 0, 1, EPI_NONE, TT_256x128},   {512, 96, 0, 1, EPI_NONE, TT_64x128},
     {384, 48, 0, 1, EPI_NONE, TT_128x64},     {256, 48, 0, 1, EPI_NONE, TT_64x64},
     {192, 48, 0, 1, EPI_NONE, TT_64x64},
-    // Conv2dSubsampling output linear (K = 128 channels x 19 freq)
-    {2432, 192, 1, 0, EPI_NONE, TT_256x128},
+    // Conv2dSubsampling output linear (K = 128 channels x 19 freq): one 192-wide column tile,
+    // so the 2432-deep A panel is streamed once (399 -> 333 us, profiles/r03/gemm_tune/bn192/)
+    {2432, 192, 1, 0, EPI_NONE, TT_GLDS3_192},
 };
 
 template <int EPI, typename TA, typename TC>
@@ -1053,6 +1054,14 @@ void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
     switch (tuned_tile<EPI, TA, TC>(p)) {
       case TT_GLDS3:
         if (p.K % 32 == 0 && p.K >= 128 && p.lda % 8 == 0) return launch_glds<3, EPI, TA, TC>(p, Bw, st);
+        break;
+      case TT_GLDS3_192:
+        if (p.K % 32 == 0 && p.K >= 128 && p.lda % 8 == 0 && p.N % 192 == 0) {
+          const int tn = p.N / 192, tm = cdiv(p.M, 128);
+          hipLaunchKernelGGL((gemm_glds_kernel<3, EPI, TA, TC, 192, false>), dim3(tn * tm), dim3(256),
+                             0, st, p, Bw, tn);
+          return;
+        }
         break;
       case TT_64x64: return launch_h<64, 64, 32, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
       case TT_64x128: return launch_h<64, 128, 32, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);

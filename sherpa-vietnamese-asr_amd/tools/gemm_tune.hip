@@ -55,6 +55,14 @@ static void sweep(const Shape& s) {
       {"128x256", [&] { launch_h<128, 256, 32, 2, 4, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
       {"256x128", [&] { launch_h<256, 128, 32, 4, 2, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
       {"128x32", [&] { launch_h<128, 32, 32, 4, 1, ALOAD_DENSE, EPI, TA, TC>(p, dB, 0); }},
+      {"glds3_192", [&] {
+         const int tn = cdiv(p.N, 192), tm = cdiv(p.M, 128);
+         hipLaunchKernelGGL((gemm_glds_kernel<3, EPI, TA, TC, 192, false>), dim3(tn * tm), dim3(256), 0, 0, p, dB, tn);
+       }},
+      {"glds4_192", [&] {
+         const int tn = cdiv(p.N, 192), tm = cdiv(p.M, 128);
+         hipLaunchKernelGGL((gemm_glds_kernel<4, EPI, TA, TC, 192, false>), dim3(tn * tm), dim3(256), 0, 0, p, dB, tn);
+       }},
       {"glds3", [&] { launch_glds<3, EPI, TA, TC>(p, dB, 0); }},
       {"glds4", [&] { launch_glds<4, EPI, TA, TC>(p, dB, 0); }},
   };
@@ -76,7 +84,7 @@ static void sweep(const Shape& s) {
   std::mt19937 rng(7);
   for (auto& v : vars) {
     if (!strncmp(v.first, "glds", 4) && (s.K % 32 != 0 || s.K < 128)) continue;
-    if (strstr(v.first, "k64") && (s.K % 64 != 0 || s.K < 128)) continue;
+    if (strstr(v.first, "_192") && s.N % 192 != 0) continue;
     hipMemset(p.C, 0, cbytes);
     v.second();
     hipDeviceSynchronize();
