@@ -491,3 +491,38 @@ def test_pipelined_workspace_growth_mid_pipeline(need_gpu):
         assert a.token_ids.tolist() == p.token_ids.tolist()
         assert a.frames.tolist() == p.frames.tolist()
         np.testing.assert_array_equal(a.log_probs, p.log_probs)
+
+
+def check_encoder_out(out_path):
+    """Encoder output of 12 x 33 s of speech (19.8k 50 Hz rows: stack 0 and the subsampling
+    output linear run at the row counts where gemm.hip's measured tile table applies) -> .npy"""
+    from model_fixtures import m_model
+    from oracle.fbank import fbank
+    from zasr.binding import Recognizer
+    cfg, w, path = m_model()
+    rec = Recognizer(path, "greedy_search", 1, precision="bf16")
+    feats = [fbank(_speech(33.0, 2000 + i)) for i in range(12)]
+    np.save(out_path, np.concatenate(rec.encode_features(feats)))
+    rec.close()
+
+
+def test_tuned_gemm_tiles_bit_identical(need_gpu, tmp_path):
+    """The per-shape tile table (gemm.hip kTuned, incl. the 192-wide LDS-DMA tile of the
+    subsampling output linear) changes speed only: the bf16 encoder output with the table equals
+    the one with ZASR_GEMM_TUNED=0 bit for bit (a fresh process each: the switch is read once)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for tuned in ("1", "0"):
+        out = str(tmp_path / f"enc_{tuned}.npy")
+        code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_parity as t; "
+                "t.check_encoder_out(%r); print('ok')"
+                % (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "sherpa-vietnamese-asr_amd"),
+                   out))
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "ZASR_GEMM_TUNED": tuned},
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
+        outs.append(np.load(out))
+    assert outs[0].shape == outs[1].shape and outs[0].shape[0] > 9000
+    np.testing.assert_array_equal(outs[0], outs[1])
