@@ -736,10 +736,17 @@ std::string load_campp_graph(const OnnxFile& of, const std::string& dir, SafeTen
   const Loaded& dense = w.at("xvector.dense.linear.weight");
   const Loaded& l1 = w.at("xvector.block1.tdnnd1.linear1.weight");
   const Loaded& loc1 = w.at("xvector.block1.tdnnd1.cam_layer.linear_local.weight");
+  // the FCM head's output is m_channels x (feat_dim / 8) features (head.conv1's output
+  // channels = m_channels): the TDNN input width divided by it, times 8
+  const long m_channels = w.at("head.conv1.weight").dims[0];
+  if (m_channels <= 0 || tdnn.dims[1] % m_channels != 0)
+    throw std::runtime_error("CAM++ graph: TDNN input width " + std::to_string(tdnn.dims[1]) +
+                             " is not a multiple of the head's m_channels " +
+                             std::to_string(m_channels));
   std::ostringstream os;
-  os << "{\"feat_dim\": " << tdnn.dims[1] / 32 * 8 << ", \"embedding_size\": " << dense.dims[0]
+  os << "{\"feat_dim\": " << tdnn.dims[1] / m_channels * 8 << ", \"embedding_size\": " << dense.dims[0]
      << ", \"growth_rate\": " << loc1.dims[0] << ", \"bn_size\": " << l1.dims[0] / loc1.dims[0]
-     << ", \"init_channels\": " << tdnn.dims[0] << ", \"m_channels\": " << w.at("head.conv1.weight").dims[0]
+     << ", \"init_channels\": " << tdnn.dims[0] << ", \"m_channels\": " << m_channels
      << ", \"head_blocks\": " << ivec(head) << ", \"block_layers\": " << ivec(layers)
      << ", \"block_kernels\": " << ivec(kernels) << ", \"block_dilations\": " << ivec(dils) << "}";
   for (auto& kv : w) out.put(kv.first, kv.second.dims, std::move(kv.second.data));

@@ -150,6 +150,17 @@ static PyObject* words_from_search(PyObject* self, PyObject* args) {
   if (!PyArg_ParseTuple(args, "O!O!lldOOOlO", &PyList_Type, &pieces, &PyList_Type, &lowered, &V,
                         &n_samples, &time_offset, &o_tok, &o_fr, &o_lp, &T, &o_st))
     return NULL;
+  /* the two tables are indexed with the same bounds check: equal lengths, str entries */
+  if (PyList_GET_SIZE(lowered) != PyList_GET_SIZE(pieces)) {
+    PyErr_SetString(PyExc_ValueError, "words_from_search: pieces and lowered differ in length");
+    return NULL;
+  }
+  for (Py_ssize_t i = 0; i < PyList_GET_SIZE(pieces); ++i) {
+    if (!PyUnicode_Check(PyList_GET_ITEM(pieces, i)) || !PyUnicode_Check(PyList_GET_ITEM(lowered, i))) {
+      PyErr_SetString(PyExc_TypeError, "words_from_search: vocabulary entries must be str");
+      return NULL;
+    }
+  }
   Py_buffer bt, bf, bl, bs;
   if (get_buf(o_tok, &bt, 4, "token_ids") < 0) return NULL;
   if (get_buf(o_fr, &bf, 4, "frames") < 0) { PyBuffer_Release(&bt); return NULL; }

@@ -448,7 +448,9 @@ class _PlannedSignal:
     the reference creates before it plans, :2041-2057), or on the first chunk asked for."""
 
     def __init__(self, audio: np.ndarray, plan, d_audio=None):
-        self.ref = weakref.ref(audio)
+        # when the pipeline drops the signal, the entry goes with it (its HBM copy and the
+        # plan's results): _prune_planned runs from the weakref callback
+        self.ref = weakref.ref(audio, lambda _r: _prune_planned())
         self.ptr = audio.__array_interface__["data"][0]
         self.n = int(audio.shape[0])
         self.plan = [(int(s), int(e)) for s, e, _ in plan if int(e) > int(s)]
@@ -456,6 +458,7 @@ class _PlannedSignal:
         self.d_audio = d_audio
         self.lock = threading.Lock()
         self.jobs = weakref.WeakKeyDictionary()  # handle -> {beam: _PlanDecode}
+        self.running = 0
 
     def alive(self) -> bool:
         return self.ref() is not None
@@ -469,8 +472,9 @@ class _PlannedSignal:
         res = {}
         sizes = [min(PLAN_BATCH_CHUNKS, len(self.plan) - i)
                  for i in range(0, len(self.plan), PLAN_BATCH_CHUNKS)]
-        if self.d_audio is not None and getattr(handle, "device_id", None) == self.d_audio.device.index:
-            out = handle.decode_device_batches(self.d_audio.data_ptr(), [s for s, _ in self.plan],
+        d_audio = self.d_audio
+        if d_audio is not None and getattr(handle, "device_id", None) == d_audio.device.index:
+            out = handle.decode_device_batches(d_audio.data_ptr(), [s for s, _ in self.plan],
                                                [e - s for s, e in self.plan], sizes, beam=beam)
             res.update(zip(self.plan, out))
         else:
@@ -487,9 +491,20 @@ class _PlannedSignal:
             job = per.get(beam)
             if job is None:
                 job = per[beam] = _PlanDecode(self, handle, beam)
+                self.running += 1
         return job
 
+    def job_done(self) -> None:
+        """A plan decode finished: once none is running, the signal's HBM copy is released
+        (a decode started later for another recognizer reads the host signal instead)."""
+        with self.lock:
+            self.running -= 1
+            if self.running == 0:
+                self.d_audio = None
+
     def result(self, handle, beam: int, span):
+        """The plan's result for `span`, or None when the plan's decode failed (logged once;
+        the caller then decodes the chunk on its own, as without plan-ahead)."""
         res = self.start(handle, beam).wait()
         return None if res is None else res.get(span)
 
@@ -500,6 +515,7 @@ class _PlanDecode:
 
     def __init__(self, sig: _PlannedSignal, handle, beam: int):
         self.res, self.err = None, None
+        self.lock, self.logged = threading.Lock(), False
         self.t_start = self.t_end = None  # perf_counter() around the decode (bench phase split)
         self.thread = threading.Thread(target=self._run, args=(weakref.ref(sig), handle, beam),
                                        name="zasr-plan-decode", daemon=True)
@@ -508,21 +524,34 @@ class _PlanDecode:
     def _run(self, sig_ref, handle, beam):
         import time
         self.t_start = time.perf_counter()
+        sig = sig_ref()
         try:
-            sig = sig_ref()
             self.res = sig._decode(handle, beam) if sig is not None else None
-        except BaseException as e:  # re-raised in the caller's decode_chunk
+        except BaseException as e:  # reported once by wait(); the chunks fall back
             self.err = e
-        self.t_end = time.perf_counter()
+        finally:
+            self.t_end = time.perf_counter()
+            if sig is not None:
+                sig.job_done()
+            del sig
 
     def wait(self):
+        """The plan's results, or None when its decode failed.  Plan-ahead is an optimisation
+        and must never break the caller (zasr.dropin): a failure (e.g. out of HBM on a long
+        file while other stages hold memory) is logged once and every chunk of the plan takes
+        the per-chunk path, which may still succeed."""
         self.thread.join()
         if self.err is not None:
-            raise self.err
+            with self.lock:
+                if not self.logged:
+                    self.logged = True
+                    logger.warning(f"[zasr] plan decode failed, chunks decode one by one: "
+                                   f"{self.err!r}")
+            return None
         return self.res
 
 
-_plan_lock = threading.Lock()
+_plan_lock = threading.RLock()  # re-entered by the signal weakref callback
 _planned: List[_PlannedSignal] = []
 _feat_src: Dict[int, tuple] = {}  # id(features) -> (weakref(features), chunk data ptr, samples)
 
@@ -546,8 +575,25 @@ def _loaded_handles():
         h = r["handle"]
         if id(h) not in seen:
             seen.add(id(h))
-            out.append((h, int(r.get("max_active_paths", 8))))
+            out.append((h, int(r.get("max_active_paths", 8)), r.get("model_path", "")))
     return out if len(out) <= 2 else []
+
+
+def _eager_handles():
+    """The recognizers whose plan decode starts at registration: the one used last (the
+    reference creates it right before planning, :2041-2057) and, when the two cached models
+    are the ROVER pair (ROVER_MODEL_IDS, :2018-2047), both.  Any other cached recognizer (an
+    earlier model still in the cache) starts its decode on its first planned chunk instead."""
+    loaded = _loaded_handles()
+    names = {os.path.basename(os.path.normpath(p)) for _, _, p in loaded}
+    if len(loaded) == 2 and names == set(ROVER_MODEL_IDS):
+        return [(h, b) for h, b, _ in loaded]
+    return [(h, b) for h, b, _ in loaded if h is _last_handle][:1]
+
+
+def _prune_planned() -> None:
+    with _plan_lock:
+        _planned[:] = [p for p in _planned if p.alive()]
 
 
 def register_plan(audio, plan, d_audio=None, start: bool = True) -> bool:
@@ -562,19 +608,20 @@ def register_plan(audio, plan, d_audio=None, start: bool = True) -> bool:
     with _plan_lock:
         _planned[:] = [p for p in _planned if p.alive()][-3:] + [sig]
     if start:
-        for h, beam in _loaded_handles():
+        for h, beam in _eager_handles():
             sig.start(h, beam)
     return True
 
 
-def register_plan_from_regions(audio, regions, best_split_fn=None, d_audio=None) -> bool:
+def register_plan_from_regions(audio, regions, best_split_fn=None, d_audio=None,
+                               start: bool = True) -> bool:
     """The find_silent_regions hook: the plan the reference builds from these regions
     (:2141-2161, zasr.plan.plan_from_regions with the reference's own find_best_split_point)."""
     from zasr.plan import plan_from_regions
     if not _is_f32_vector(audio):
         return False
     return register_plan(audio, plan_from_regions(int(audio.shape[0]), regions, best_split_fn),
-                         d_audio)
+                         d_audio, start)
 
 
 def _gpu_planner_on() -> bool:
@@ -601,17 +648,19 @@ def silent_regions_device(audio: np.ndarray, device_id: int = 0):
     return regions_from_flags(flags.cpu().numpy().astype(bool), FRAME_LEN, n, MIN_SILENCE_SEC), d
 
 
-def plan_ahead_regions(audio, best_split_fn=None):
+def plan_ahead_regions(audio, best_split_fn=None, start: bool = True):
     """The drop-in's find_silent_regions for the planner's default-argument calls
     (:2139, :2183): the regions from the GPU silence detector (bit-identical to the
-    reference's), with the plan built from them registered and its decode started.  None
+    reference's), with the plan built from them registered and its decode started (unless
+    `start` is False: the caller's chunks will not be views of this signal, e.g. WPE).  None
     when the route does not apply (then the reference's own function runs)."""
     if not _gpu_planner_on() or not _is_f32_vector(audio) or not audio.flags.writeable:
         return None
-    handles = _loaded_handles()
+    handles = _eager_handles() or [(h, b) for h, b, _ in _loaded_handles()]
     dev = handles[0][0].device_id if handles else int(os.environ.get("ZASR_DEVICE", "0"))
     regions, d = silent_regions_device(audio, dev)
-    register_plan_from_regions(audio, regions, best_split_fn, d_audio=d)
+    register_plan_from_regions(audio, regions, best_split_fn, d_audio=d if start else None,
+                               start=start)
     return regions
 
 

@@ -40,6 +40,7 @@ Returns the list of names rebound.
 """
 from __future__ import annotations
 
+import sys
 from types import ModuleType
 from typing import List, Optional
 
@@ -50,6 +51,16 @@ CALIBRATION_NAMES = ("detect_calibration_status", "run_device_calibration")
 VAD_NAMES = ("_get_vad_session", "unload_vad_model", "get_cached_vad_probs",
              "_run_vad_inference", "get_vad_segments")
 VAD_ENGINE_NAMES = ("get_vad_segments", "unload_vad_model")
+
+
+def _caller_uses_wpe(frame) -> bool:
+    """True when the planner's caller is a TranscriberPipeline whose config enables WPE
+    dereverberation (core/asr_engine.py:2248): its `self.config["preprocess_wpe"]`."""
+    try:
+        cfg = getattr(frame.f_locals.get("self"), "config", None)
+        return bool(cfg.get("preprocess_wpe", False)) if hasattr(cfg, "get") else False
+    except Exception:
+        return False
 
 
 def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None,
@@ -78,9 +89,12 @@ def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None
         split_fn = getattr(engine_module, "find_best_split_point", None)
 
         def find_silent_regions(audio_data, *args, **kwargs):
+            # with preprocess_wpe the workers decode WPE-processed copies, never views of the
+            # planned signal (:2248, :2338-2341): register the plan, start no decode for it
+            start = not _caller_uses_wpe(sys._getframe(1))
             if not args and not kwargs:  # the planner's calls (:2139, :2183) use the defaults
                 try:  # the GPU silence detector: same regions, plan registered + decoding
-                    regions = ours.plan_ahead_regions(audio_data, split_fn)
+                    regions = ours.plan_ahead_regions(audio_data, split_fn, start=start)
                     if regions is not None:
                         return regions
                 except Exception as e:  # routing is an optimisation: never break the caller
@@ -88,7 +102,7 @@ def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None
             regions = orig_fsr(audio_data, *args, **kwargs)
             if not args and not kwargs:
                 try:
-                    ours.register_plan_from_regions(audio_data, regions, split_fn)
+                    ours.register_plan_from_regions(audio_data, regions, split_fn, start=start)
                 except Exception as e:
                     ours.logger.warning(f"[zasr] plan registration skipped: {e}")
             return regions

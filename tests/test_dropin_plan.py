@@ -141,6 +141,7 @@ def test_registration_starts_the_plan_decode_for_loaded_recognizers(monkeypatch)
     h = FakeHandle()
     rec = _rec(h)
     monkeypatch.setattr(ae, "_recognizer_cache", {("m", 8): rec})
+    monkeypatch.setattr(ae, "_last_handle", h)
     assert ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
     sig = ae._planned_span(concat[plan[0][0]:plan[0][1]])[0]
     sig.jobs[h][8].thread.join(timeout=30)
@@ -171,3 +172,100 @@ def test_silent_regions_from_flags_equals_the_reference_restatement():
         nf = len(a) // 160
         rms = np.sqrt(np.mean(a[:nf * 160].reshape(nf, 160) ** 2, axis=1))
         assert regions_from_flags(rms < 0.01, 160, len(a)) == silent_regions(a)
+
+
+class FailingBatchHandle(FakeHandle):
+    """Batched decodes fail (e.g. out of HBM for a long plan), single chunks succeed."""
+
+    def decode(self, chunks, beam=0):
+        if len(chunks) > 1:
+            with self.lock:
+                self.calls.append(-len(chunks))
+            raise RuntimeError("hipErrorOutOfMemory (stand-in)")
+        return super().decode(chunks, beam)
+
+
+def test_failed_plan_decode_falls_back_to_the_per_chunk_path(caplog):
+    """a failed plan decode must not fail every chunk of the plan: it is logged
+    once and each chunk decodes on its own, with the per-chunk words."""
+    concat = synth_speech(160.0, 16)
+    plan = plan_chunks(concat)
+    want = [ae.decode_chunk(_rec(FakeHandle()), concat[s:e].copy(), s / 16000.0)
+            for s, e, _ in plan]
+    h = FailingBatchHandle()
+    ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+    with caplog.at_level("WARNING", logger="zasr.asr_engine"):
+        got = _two_workers(_rec(h), concat, plan)
+    assert got == want
+    assert h.calls[0] == -len(plan) and h.calls.count(1) == len(plan)
+    assert sum("plan decode failed" in r.getMessage() for r in caplog.records) == 1
+
+
+def test_eager_start_only_for_the_last_used_recognizer_or_the_rover_pair(monkeypatch):
+    """a second cached recognizer of an earlier model is not decoded eagerly; the
+    ROVER pair (both models used per chunk, :2346-2350) is."""
+    concat = synth_speech(90.0, 17)
+    plan = plan_chunks(concat)
+    old, cur = FakeHandle(), FakeHandle()
+    r_old, r_cur = _rec(old), _rec(cur)
+    r_old["model_path"], r_cur["model_path"] = "/m/other-model", "/m/current-model"
+    monkeypatch.setattr(ae, "_recognizer_cache", {("a", 8): r_old, ("b", 8): r_cur})
+    monkeypatch.setattr(ae, "_last_handle", cur)
+    assert [h for h, _ in ae._eager_handles()] == [cur]
+    ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+    sig = ae._planned_span(concat[plan[0][0]:plan[0][1]])[0]
+    sig.jobs[cur][8].thread.join(timeout=30)
+    assert cur.calls == [len(plan)] and old.calls == [] and old not in sig.jobs
+    # the earlier model still gets the plan's batch on its first planned chunk
+    s, e, _ = plan[0]
+    ae.decode_chunk(r_old, concat[s:e], 0.0)
+    assert old.calls == [len(plan)]
+    a, b = FakeHandle(), FakeHandle()
+    ra, rb = _rec(a), _rec(b)
+    ra["model_path"] = "/models/" + ae.ROVER_MODEL_IDS[0]
+    rb["model_path"] = "/models/" + ae.ROVER_MODEL_IDS[1] + "/"
+    monkeypatch.setattr(ae, "_recognizer_cache", {("a", 8): ra, ("b", 8): rb})
+    assert {id(h) for h, _ in ae._eager_handles()} == {id(a), id(b)}
+
+
+def test_wpe_caller_registers_without_decoding(monkeypatch):
+    """With preprocess_wpe the workers decode WPE copies (:2338-2341): the hook registers the
+    plan but starts no decode (zasr.dropin._caller_uses_wpe reads the caller's config)."""
+    from zasr.dropin import _caller_uses_wpe
+    concat = synth_speech(80.0, 18)
+    h = FakeHandle()
+    monkeypatch.setattr(ae, "_recognizer_cache", {("m", 8): _rec(h)})
+    monkeypatch.setattr(ae, "_last_handle", h)
+
+    class Pipe:
+        def __init__(self, wpe):
+            self.config = {"preprocess_wpe": wpe}
+
+        def plan(self):
+            import sys
+            return _caller_uses_wpe(sys._getframe(0))
+
+    assert Pipe(True).plan() and not Pipe(False).plan()
+    assert ae.register_plan_from_regions(concat, silent_regions(concat), best_split, start=False)
+    sig = ae._planned_span(concat[: plan_chunks(concat)[0][1]])[0]
+    assert h not in sig.jobs and h.calls == []
+
+
+def test_hbm_copy_released_after_the_decode_and_entry_pruned_with_the_signal(monkeypatch):
+    """the plan's HBM copy of the signal is dropped once its decode has finished,
+    and the registry entry goes when the pipeline drops the signal (weakref callback)."""
+    import gc
+    concat = synth_speech(75.0, 19)
+    plan = plan_chunks(concat)
+    h = FakeHandle()
+    monkeypatch.setattr(ae, "_recognizer_cache", {("m", 8): _rec(h)})
+    monkeypatch.setattr(ae, "_last_handle", h)
+    marker = SimpleNamespace(device=SimpleNamespace(index=-1))  # an HBM copy on another device
+    ae.register_plan_from_regions(concat, silent_regions(concat), best_split, d_audio=marker)
+    sig = ae._planned_span(concat[plan[0][0]:plan[0][1]])[0]
+    sig.jobs[h][8].thread.join(timeout=30)
+    assert sig.d_audio is None and h.calls == [len(plan)]
+    n_before = len(ae._planned)
+    del concat
+    gc.collect()
+    assert sig not in ae._planned and len(ae._planned) == n_before - 1

@@ -129,3 +129,16 @@ def test_round4_equals_python_round():
     for x in xs.tolist():
         a, b = words_ext.round4(x), round(x, 4)
         assert a == b and np.signbit(a) == np.signbit(b), (x, a, b)
+
+
+def test_table_checks():
+    """mismatched table lengths raise ValueError, non-str entries TypeError (the
+    Python path's behaviour), instead of reading past the lowered list or crashing."""
+    tok = np.array([1, 2], np.int32)
+    fr = np.array([0, 3], np.int32)
+    lp = np.zeros(2, np.float64)
+    st = np.zeros((2, 4), np.float32)
+    with pytest.raises(ValueError):
+        words_ext.words_from_search(["a", "b", "c"], ["a", "b"], 3, 16000, 0.0, tok, fr, lp, 10, st)
+    with pytest.raises(TypeError):
+        words_ext.words_from_search(["a", 5, "c"], ["a", "b", "c"], 3, 16000, 0.0, tok, fr, lp, 10, st)
