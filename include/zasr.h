@@ -165,6 +165,44 @@ const double* zasr_result_log_probs(const zasr_result* r, int32_t i);
 const float* zasr_result_token_stats(const zasr_result* r, int32_t i);
 void zasr_result_free(zasr_result* r);
 
+/* ---- offline streams: the sherpa-onnx OfflineRecognizer / OfflineStream surface ----
+   The stream-shaped calls the reference's other callers bind: sherpa-onnx's C API
+   (offline_pwa/static/vendor/sherpa-onnx-wasm/sherpa-onnx-asr.js:1782-1880) and its Python
+   OfflineRecognizer (streaming_asr.py:224-243, core/audio_analyzer.py:345-361:
+   create_stream -> accept_waveform -> decode_stream -> stream.result).  A stream holds host
+   samples until decoded; zasr_decode_streams decodes several in ONE batched GPU pass (the
+   zasr_decode_batch path), with the recognizer's configured method and beam.  A stream with
+   fewer than 1360 samples (under 9 fbank frames) decodes to an empty result.
+     zasr_create_stream            SherpaOnnxCreateOfflineStream (sherpa-onnx-asr.js:1862)
+     zasr_destroy_stream           SherpaOnnxDestroyOfflineStream (:1790)
+     zasr_stream_accept_waveform   SherpaOnnxAcceptWaveformOffline (:1799-1805); 16 kHz only
+                                   (the reference resamples on load); appends
+     zasr_decode_stream            SherpaOnnxDecodeOfflineStream (:1866-1868)
+     zasr_decode_streams           SherpaOnnxDecodeMultipleOfflineStreams (one batch)
+     zasr_stream_result_json       SherpaOnnxGetOfflineStreamResultAsJson (:1870-1878): keys
+                                   lang, emotion, event, text, timestamps (frame x 0.04 s),
+                                   tokens (tokens.txt strings, a leading U+2581 as a space, as
+                                   sherpa-onnx's SymbolTable), ys_log_probs, words; *needed =
+                                   bytes incl. the NUL (call with buf NULL to size it)
+     zasr_stream_tokens / _frames / _log_probs / _token_stats / _num_*: the result arrays, as
+                                   zasr_result_* for one chunk (valid until the stream is
+                                   destroyed) */
+typedef struct zasr_stream zasr_stream;
+int zasr_create_stream(zasr_recognizer* h, zasr_stream** out);
+void zasr_destroy_stream(zasr_stream* s);
+int zasr_stream_accept_waveform(zasr_stream* s, int32_t sample_rate, const float* samples,
+                                int64_t n);
+int zasr_decode_stream(zasr_recognizer* h, zasr_stream* s);
+int zasr_decode_streams(zasr_recognizer* h, zasr_stream* const* streams, int32_t n);
+int32_t zasr_stream_is_decoded(const zasr_stream* s);
+int32_t zasr_stream_num_tokens(const zasr_stream* s);
+int32_t zasr_stream_num_frames(const zasr_stream* s);
+const int32_t* zasr_stream_tokens(const zasr_stream* s);
+const int32_t* zasr_stream_frames(const zasr_stream* s);
+const double* zasr_stream_log_probs(const zasr_stream* s);
+const float* zasr_stream_token_stats(const zasr_stream* s);
+int zasr_stream_result_json(const zasr_stream* s, char* buf, int64_t cap, int64_t* needed);
+
 /* ---- CAM++ speaker embedding ----
    Replaces the reference's onnxruntime CAM++ session and its numpy front end:
    core/speaker_diarization_senko_campp_optimized.py:86-159 (_compute_fbank_vectorized),

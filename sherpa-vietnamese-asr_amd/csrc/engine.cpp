@@ -471,6 +471,19 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
                     &model_.enc_proj, &model_.joiner})
       mkx(*l);
+    if (cfg.joiner_dim == 256 || cfg.joiner_dim == 512) {
+      // the joiner's W pieces in MFMA-fragment order (one packed image per piece) for
+      // joiner_split_packed_kernel; J is written in the same order, already split, by store_j4
+      const long pe = gemm_rp_packed_elems(cfg.V, cfg.joiner_dim);
+      void* p = nullptr;
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)pe * 2 * split_pieces()));
+      model_.allocations.push_back(p);
+      for (int t = 0; t < split_pieces(); ++t)
+        gemm_rp_pack_weights(reinterpret_cast<const __bf16*>(model_.joiner.wx) + (long)t * cfg.V * cfg.joiner_dim,
+                             cfg.V, cfg.joiner_dim, reinterpret_cast<__bf16*>(p) + t * pe, stream_);
+      model_.joiner_packed = p;
+      model_.joiner_plane = pe;
+    }
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
         for (DLin* l : {&L.attn_in, &L.na_in, &L.na_out}) mkx(*l);
@@ -1454,28 +1467,47 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
     ZASR_HIP_CHECK(hipMemsetAsync(st.stamps, 0, (size_t)Tmax * 16 * 8, st_));
   }
   float* logits = ws<float>("se_logits", slots * V);
+  // split-bf16 modes: J written once as `np` packed bf16 pieces (store_j4), the joiner on the
+  // packed W pieces; bf16: one packed bf16 image
+  const int jnp = split_pieces();
   const bool bf16 = model_.joiner.wh != nullptr;
   // bf16 with the decoder-context table: J in fragment order for the packed joiner (every
   // J writer goes through store_j4); without the table decjoin writes row-major J
   static const bool no_pack = getenv("ZASR_JOINER_UNPACKED") != nullptr;
-  const bool packed = bf16 && model_.joiner_packed && model_.dec_table && !no_pack;
+  const bool packed = (bf16 || jnp > 0) && model_.joiner_packed && model_.dec_table && !no_pack;
+  const int jpc = packed && jnp > 0 ? jnp : 1;  // packed images of J
+  const bool j16 = bf16 || packed;              // J buffer in bf16 elements
   const size_t jrows = (size_t)joiner_packed_rows((long)slots);
-  void* J = bf16 ? (void*)ws<__bf16>("se_joinin_h", jrows * D) : (void*)ws<float>("se_joinin", slots * D);
-  ZASR_HIP_CHECK(hipMemsetAsync(J, 0, (bf16 ? jrows * 2 : slots * 4) * D, st_));
+  void* J = j16 ? (void*)ws<__bf16>("se_joinin_h", jrows * D * jpc) : (void*)ws<float>("se_joinin", slots * D);
+  ZASR_HIP_CHECK(hipMemsetAsync(J, 0, (j16 ? jrows * 2 * jpc : slots * 4) * D, st_));
   DecTable dt{model_.dec_table, V, d_enc, d_eo, d_el, J, D, bf16 ? 1 : 0};
   dt.j_packed = packed ? 1 : 0;
+  dt.j_pieces = packed ? jnp : 0;
+  dt.j_plane = (long)jrows * D;
+  auto packed_args = [&](const void* Jp, long jplane, float* out, int rows) {
+    JoinerPackedArgs ja{Jp, model_.joiner_packed, model_.joiner.b, out, rows, V, D};
+    if (jnp > 0) {
+      ja.pieces = jnp;
+      ja.j_plane = jplane;
+      ja.w_plane = model_.joiner_plane;
+    }
+    return ja;
+  };
   DecoderW dw{model_.dec_tap0, model_.dec_tap1, model_.dec_proj.b, D};
   // greedy with the decoder-context table: speculative windows (kernels.h, greedy_spec)
   const char* spec_env = getenv("ZASR_GREEDY_WINDOW");
   const int F = spec_env ? atoi(spec_env) : 4;
   if (H == 1 && model_.dec_table && (F == 4 || F == 8)) {
-    void* Js = bf16 ? (void*)ws<__bf16>("gs_joinin_h", (size_t)joiner_packed_rows((long)S * F) * D)
-                    : (void*)ws<float>("gs_joinin", (size_t)S * F * D);
+    const size_t jrs = (size_t)joiner_packed_rows((long)S * F);
+    void* Js = j16 ? (void*)ws<__bf16>("gs_joinin_h", jrs * D * jpc)
+                   : (void*)ws<float>("gs_joinin", (size_t)S * F * D);
     float* lg = ws<float>("gs_logits", (size_t)S * F * V);
     int* d_t = ws<int>("gs_t", S);
     int* d_active = ws<int>("gs_active", 2);
     DecTable ds{model_.dec_table, V, d_enc, d_eo, d_el, Js, D, bf16 ? 1 : 0};
     ds.j_packed = packed ? 1 : 0;
+    ds.j_pieces = packed ? jnp : 0;
+    ds.j_plane = (long)jrs * D;
     prof_begin("search");
     launch_search_init(st, S, 1, st_);
     launch_greedy_spec_init(ds, S, F, d_t, d_active, st_);
@@ -1492,7 +1524,10 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
       for (int b = 0; b < kSync && k < Tmax; ++b, ++k) {
         prof_begin("joiner");
         if (packed) {
-          JoinerPackedArgs ja{Js, model_.joiner_packed, model_.joiner.b, lg, S * F, V, D, d_t, d_el, F};
+          JoinerPackedArgs ja = packed_args(Js, ds.j_plane, lg, S * F);
+          ja.live_t = d_t;
+          ja.live_len = d_el;
+          ja.live_f = F;
           launch_joiner_packed(ja, st_);
         } else if (bf16) {
           JoinerBf16Args ja{reinterpret_cast<const __bf16*>(Js),
@@ -1573,20 +1608,21 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
       q.logits = logits;
     } else {
       const size_t jr = (size_t)joiner_packed_rows((long)q.n * H);
-      q.J = bf16 ? (void*)ws<__bf16>("se_joinin_h1", jr * D) : (void*)ws<float>("se_joinin1", (size_t)q.n * H * D);
+      q.J = j16 ? (void*)ws<__bf16>("se_joinin_h1", jr * D * jpc) : (void*)ws<float>("se_joinin1", (size_t)q.n * H * D);
       q.logits = ws<float>("se_logits1", (size_t)q.n * H * V);
     }
     q.dt = dt;
     q.dt.enc_off = d_eo + q.s0;
     q.dt.enc_len = d_el + q.s0;
     q.dt.J = q.J;
+    if (g > 0) q.dt.j_plane = (long)joiner_packed_rows((long)q.n * H) * D;
     q.active = q.n;
   }
   if (G > 1) {  // group 1 starts after the uploads / memsets / encoder-output wait on st_
     ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 3], st_));
     ZASR_HIP_CHECK(hipStreamWaitEvent(stream3_, part_ev_[kMaxEnc + 3], 0));
     const size_t jr = (size_t)joiner_packed_rows((long)grp[1].n * H);
-    ZASR_HIP_CHECK(hipMemsetAsync(grp[1].J, 0, (bf16 ? jr * 2 : (size_t)grp[1].n * H * 4) * D, stream3_));
+    ZASR_HIP_CHECK(hipMemsetAsync(grp[1].J, 0, (j16 ? jr * 2 * jpc : (size_t)grp[1].n * H * 4) * D, stream3_));
   }
   hipStream_t home = st_;
   for (Group& q : grp) {
@@ -1613,7 +1649,7 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
       }
       prof_begin("joiner");
       if (packed) {
-        JoinerPackedArgs ja{q.J, model_.joiner_packed, model_.joiner.b, q.logits, rows, V, D};
+        JoinerPackedArgs ja = packed_args(q.J, q.dt.j_plane, q.logits, rows);
         launch_joiner_packed(ja, st_);
       } else if (bf16) {
         JoinerBf16Args ja{reinterpret_cast<const __bf16*>(q.J), reinterpret_cast<const __bf16*>(model_.joiner.wh),

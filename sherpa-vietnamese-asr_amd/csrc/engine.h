@@ -65,7 +65,9 @@ struct DModel {
   float out_ds_w[2] = {0, 0};
   float* dec_emb = nullptr;   // [V][D]
   float* dec_conv = nullptr;  // [D][4][2]
-  void* joiner_packed = nullptr;  // bf16 joiner weights in MFMA-fragment order (bf16 mode)
+  void* joiner_packed = nullptr;  // bf16 joiner weights in MFMA-fragment order (bf16 mode),
+                                  // or their split pieces (bf16x3 / bf16x6), one image each
+  long joiner_plane = 0;          // bf16 elements per packed piece image
   float* dec_table = nullptr;  // [V*V][D] decoder output per context (null: too large)
   float* dec_tap0 = nullptr;  // [V][D] conv tap 0 of each embedding row
   float* dec_tap1 = nullptr;  // [V][D] conv tap 1

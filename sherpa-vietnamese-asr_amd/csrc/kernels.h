@@ -349,6 +349,10 @@ struct DecTable {
   int D;
   int j_bf16;
   int j_packed = 0;         // bf16 J in MFMA-fragment order (joiner_packed_kernel's A operand)
+  // split-bf16 modes with j_packed: J = tanh() in f32 written as j_pieces bf16 pieces
+  // (p0 = bf16(x), p1 = bf16(x - p0), ...), piece t at element offset t * j_plane
+  int j_pieces = 0;
+  long j_plane = 0;
 };
 // Speculative-greedy joiner on fragment-packed operands: J packed by the greedy search
 // kernels ([row/32][D/16][64 lanes][8] bf16, rows padded to a multiple of 64), W packed once
@@ -364,6 +368,11 @@ struct JoinerPackedArgs {
   const int* live_t = nullptr;
   const int* live_len = nullptr;
   int live_f = 0;
+  // split-bf16 modes: J and W as `pieces` packed images each (piece t of J at Jp + t j_plane,
+  // of W at Wp + t w_plane, in bf16 elements); the logits are the f32 sum of the piece
+  // products with u + v < pieces (joiner_split_packed_kernel)
+  int pieces = 0;
+  long j_plane = 0, w_plane = 0;
 };
 void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st);
 // rows the packed J buffer must hold for M joiner rows

@@ -680,9 +680,83 @@ __global__ __launch_bounds__(256) void joiner_reg_kernel(JoinerPackedArgs j) {
   }
 }
 
+// Split-bf16 modes on packed pieces: the joiner_reg_kernel structure (no LDS: co-resides with
+// the encoder blocks of the next batch), each k16 step loading the NP pieces of its J and W
+// fragments (written / packed once: store_j4, Engine load) and issuing the NP (NP + 1) / 2
+// piece products smallest first (mfma_split, the order of gemm_x3 / joiner_split_kernel).
+// CH k16 steps of fragments in flight per register set.
+template <int QK, int NP, int CH>
+__global__ __launch_bounds__(256) void joiner_split_packed_kernel(JoinerPackedArgs j) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.y * 64;
+  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M) &&
+      (m0 + 32 >= j.M || tile_done(j.live_t, j.live_len, j.live_f, m0 + 32, j.M)))
+    return;  // block-uniform: every stream of these 64 rows has finished
+  const int rt = wid >> 1, gc = wid & 1;
+  const int row0 = m0 + 32 * rt;
+  const int g = blockIdx.x * 2 + gc;
+  if (row0 >= j.M || g * 32 >= j.V) return;
+  const bf16x8* srcJ = reinterpret_cast<const bf16x8*>(j.Jp) + (long)(row0 >> 5) * QK * 64 + lane;
+  const bf16x8* srcW = reinterpret_cast<const bf16x8*>(j.Wp) + (long)g * QK * 64 + lane;
+  const long jp = j.j_plane / 8, wp = j.w_plane / 8;  // planes in bf16x8 units
+  constexpr int NCH = QK / CH;
+  bf16x8 a[2][CH][NP], b[2][CH][NP];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      a[0][c][t] = srcJ[t * jp + c * 64];
+      b[0][c][t] = srcW[t * wp + c * 64];
+    }
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  // the next set's loads go out as one group before this set's MFMAs (scheduling barriers:
+  // left alone, the compiler streams one load per MFMA with ~4 in flight, latency-bound)
+#pragma unroll
+  for (int h = 0; h < NCH; ++h) {
+    const int cur = h & 1;
+    if (h + 1 < NCH) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+          a[cur ^ 1][c][t] = srcJ[t * jp + ((h + 1) * CH + c) * 64];
+          b[cur ^ 1][c][t] = srcW[t * wp + ((h + 1) * CH + c) * 64];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) acc = mfma_split<NP>(a[cur][c], b[cur][c], acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int col = g * 32 + (lane & 31);
+  if (col >= j.V) return;
+  const float bb = j.bias[col];
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    if (row < j.M) j.out[(long)row * j.V + col] = acc[r] + bb;
+  }
+}
+
 void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st) {
   if (j.M <= 0) return;
   dim3 grid(cdiv(j.V, 64), cdiv(j.M, 64));
+  if (j.pieces > 0) {
+    ZASR_REQUIRE(j.pieces == 2 || j.pieces == 3, "packed split joiner: pieces must be 2 or 3");
+    ZASR_REQUIRE(j.D == 256 || j.D == 512, "packed split joiner: joiner dim must be 256 or 512");
+    const int qk = j.D / 16;
+    if (j.pieces == 2) {
+      if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 2, 4>), grid, dim3(256), 0, st, j);
+      else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 2, 4>), grid, dim3(256), 0, st, j);
+    } else {
+      if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 3, 4>), grid, dim3(256), 0, st, j);
+      else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 3, 4>), grid, dim3(256), 0, st, j);
+    }
+    return;
+  }
   // ZASR_JOINER_LDS=1: the LDS-shared kernel (lowest latency on an idle GPU)
   static const bool lds = getenv("ZASR_JOINER_LDS") != nullptr && atoi(getenv("ZASR_JOINER_LDS")) != 0;
   switch (j.D) {
@@ -706,7 +780,21 @@ __device__ __forceinline__ long packed_j_off(long row, int k, int D) {
 }
 
 __device__ __forceinline__ void store_j4(const DecTable& dt, long row, int k, float4 e, float4 d) {
-  if (dt.j_packed) {  // 4 consecutive k stay inside one 8-element fragment slot
+  if (dt.j_packed && dt.j_pieces > 0) {
+    // split-bf16 modes: the f32 J of the f32 path (tanhf), written once as bf16 pieces in
+    // fragment order, so the joiner reads ready MFMA operands (no per-launch split)
+    float r[4] = {tanhf(e.x + d.x), tanhf(e.y + d.y), tanhf(e.z + d.z), tanhf(e.w + d.w)};
+    __bf16* base = reinterpret_cast<__bf16*>(dt.J) + packed_j_off(row, k, dt.D);
+    for (int t = 0; t < dt.j_pieces; ++t) {
+      bf16x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = (__bf16)r[q];
+        r[q] -= (float)v[q];
+      }
+      *reinterpret_cast<bf16x4*>(base + t * dt.j_plane) = v;
+    }
+  } else if (dt.j_packed) {  // 4 consecutive k stay inside one 8-element fragment slot
     bf16x4 v;
     v[0] = (__bf16)fast_tanh(e.x + d.x);
     v[1] = (__bf16)fast_tanh(e.y + d.y);

@@ -1,6 +1,10 @@
 // C ABI of libzasr (include/zasr.h): argument checking, error capture, result objects.
+#include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <memory>
+#include <mutex>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -18,6 +22,21 @@ using zasr::TokenResult;
 
 struct zasr_recognizer {
   std::unique_ptr<Engine> eng;
+  std::string model_dir;
+  // tokens.txt of model_dir, loaded on the first JSON result (sherpa-onnx SymbolTable: a
+  // leading "\u2581" becomes a space)
+  std::mutex sym_mu;
+  std::vector<std::string> syms;
+  bool syms_loaded = false;
+};
+
+// an offline stream (sherpa-onnx OfflineStream): the samples accepted so far and, once
+// decoded, its result; bound to the recognizer that created it
+struct zasr_stream {
+  zasr_recognizer* rec = nullptr;
+  std::vector<float> samples;
+  bool decoded = false;
+  TokenResult res;
 };
 
 struct zasr_result {
@@ -61,6 +80,79 @@ int resolve_beam(zasr_recognizer* h, int32_t beam) {
   return beam > 0 ? beam : h->eng->default_beam();
 }
 
+// fewest samples the encoder accepts: 9 fbank frames ((n + 80) / 160 >= 9); shorter streams
+// decode to an empty result, as an encoder output of no frames does
+constexpr long kMinStreamSamples = 9 * 160 - 80;
+
+// Decode streams [s0, s1, ...] of one recognizer in ONE batched pass (host samples staged
+// into one device buffer, the zasr_decode_batch path); results stored in the streams.
+void decode_streams_impl(zasr_recognizer* h, zasr_stream* const* ss, int n) {
+  Engine* e = h->eng.get();
+  std::vector<int> idx;
+  std::vector<long> off, len;
+  long tot = 0;
+  for (int i = 0; i < n; ++i) {
+    const long m = (long)ss[i]->samples.size();
+    if (m < kMinStreamSamples) {
+      ss[i]->res = TokenResult{};
+      ss[i]->decoded = true;
+      continue;
+    }
+    idx.push_back(i);
+    off.push_back(tot);
+    len.push_back(m);
+    tot += m;
+  }
+  if (idx.empty()) return;
+  std::lock_guard<std::mutex> lk(e->mu);
+  float* d = nullptr;
+  ZASR_HIP_CHECK(hipMalloc(&d, tot * sizeof(float)));
+  std::unique_ptr<float, decltype(&hipFree)> guard(d, hipFree);
+  for (size_t j = 0; j < idx.size(); ++j)
+    ZASR_HIP_CHECK(hipMemcpyAsync(d + off[j], ss[idx[j]]->samples.data(), len[j] * 4,
+                                  hipMemcpyHostToDevice, e->stream()));
+  std::vector<TokenResult> r = e->decode_device(d, off, len, e->default_beam(), e->stream());
+  ZASR_HIP_CHECK(hipStreamSynchronize(e->stream()));
+  for (size_t j = 0; j < idx.size(); ++j) {
+    ss[idx[j]]->res = std::move(r[j]);
+    ss[idx[j]]->decoded = true;
+  }
+}
+
+const std::vector<std::string>& symbols(zasr_recognizer* h) {
+  std::lock_guard<std::mutex> lk(h->sym_mu);
+  if (!h->syms_loaded) {
+    std::ifstream f(h->model_dir + "/tokens.txt");
+    if (!f) throw std::invalid_argument("tokens.txt not found in " + h->model_dir);
+    std::string line;
+    while (std::getline(f, line)) {
+      std::istringstream ls(line);
+      std::string sym, id_s;
+      if (!(ls >> sym >> id_s)) continue;
+      const long id = std::stol(id_s);
+      if (id < 0) continue;
+      if (sym.compare(0, 3, "\xe2\x96\x81") == 0) sym.replace(0, 3, " ");
+      if ((long)h->syms.size() <= id) h->syms.resize(id + 1);
+      h->syms[id] = sym;
+    }
+    h->syms_loaded = true;
+  }
+  return h->syms;
+}
+
+void json_string(std::ostringstream& os, const std::string& s) {
+  os << '"';
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') os << '\\' << c;
+    else if (c < 0x20) {
+      char b[8];
+      std::snprintf(b, sizeof b, "\\u%04x", c);
+      os << b;
+    } else os << c;
+  }
+  os << '"';
+}
+
 }  // namespace
 
 extern "C" {
@@ -95,6 +187,7 @@ int zasr_create(const zasr_config* cfg, zasr_recognizer** out) {
       delete h;
       throw;
     }
+    h->model_dir = cfg->model_dir;
     *out = h;
     return (int)ZASR_OK;
   });
@@ -518,6 +611,101 @@ int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float t
     zasr::launch_silence_flags(d_wav, (long)n, (int)frame_len, threshold, d_flags,
                                reinterpret_cast<hipStream_t>(stream));
     ZASR_HIP_CHECK(hipGetLastError());
+    return (int)ZASR_OK;
+  });
+}
+
+// ---- offline streams (sherpa-onnx OfflineStream surface) ----
+int zasr_create_stream(zasr_recognizer* h, zasr_stream** out) {
+  if (!h || !out) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    auto* s = new zasr_stream;
+    s->rec = h;
+    *out = s;
+    return (int)ZASR_OK;
+  });
+}
+
+void zasr_destroy_stream(zasr_stream* s) { delete s; }
+
+int zasr_stream_accept_waveform(zasr_stream* s, int32_t sample_rate, const float* samples,
+                                int64_t n) {
+  if (!s || n < 0 || (n > 0 && !samples)) return fail(ZASR_ERR_INVALID, "null argument");
+  if (sample_rate != 16000) return fail(ZASR_ERR_INVALID, "sample rate must be 16000");
+  if (s->decoded) return fail(ZASR_ERR_INVALID, "stream already decoded");
+  return guarded([&]() {
+    s->samples.insert(s->samples.end(), samples, samples + n);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_decode_stream(zasr_recognizer* h, zasr_stream* s) {
+  return zasr_decode_streams(h, &s, 1);
+}
+
+int zasr_decode_streams(zasr_recognizer* h, zasr_stream* const* ss, int32_t n) {
+  if (!h || n < 0 || (n > 0 && !ss)) return fail(ZASR_ERR_INVALID, "null argument");
+  for (int32_t i = 0; i < n; ++i) {
+    if (!ss[i]) return fail(ZASR_ERR_INVALID, "null stream");
+    if (ss[i]->rec != h) return fail(ZASR_ERR_INVALID, "stream belongs to another recognizer");
+    for (int32_t j = 0; j < i; ++j)
+      if (ss[j] == ss[i]) return fail(ZASR_ERR_INVALID, "stream listed twice");
+  }
+  return guarded([&]() {
+    decode_streams_impl(h, ss, n);
+    return (int)ZASR_OK;
+  });
+}
+
+int32_t zasr_stream_is_decoded(const zasr_stream* s) { return s && s->decoded ? 1 : 0; }
+int32_t zasr_stream_num_tokens(const zasr_stream* s) {
+  return s ? (int32_t)s->res.tok.size() : 0;
+}
+int32_t zasr_stream_num_frames(const zasr_stream* s) { return s ? s->res.t_out : 0; }
+const int32_t* zasr_stream_tokens(const zasr_stream* s) { return s ? s->res.tok.data() : nullptr; }
+const int32_t* zasr_stream_frames(const zasr_stream* s) { return s ? s->res.frame.data() : nullptr; }
+const double* zasr_stream_log_probs(const zasr_stream* s) { return s ? s->res.lp.data() : nullptr; }
+const float* zasr_stream_token_stats(const zasr_stream* s) {
+  return s ? s->res.stats.data() : nullptr;
+}
+
+int zasr_stream_result_json(const zasr_stream* s, char* buf, int64_t cap, int64_t* needed) {
+  if (!s || !needed) return fail(ZASR_ERR_INVALID, "null argument");
+  if (!s->decoded) return fail(ZASR_ERR_INVALID, "stream not decoded");
+  return guarded([&]() {
+    const std::vector<std::string>& sym = symbols(s->rec);
+    const TokenResult& r = s->res;
+    std::ostringstream os;
+    std::string text;
+    std::vector<std::string> toks;
+    for (int t : r.tok) {
+      toks.push_back(t >= 0 && t < (int)sym.size() ? sym[t] : std::string());
+      text += toks.back();
+    }
+    os << "{\"lang\": \"\", \"emotion\": \"\", \"event\": \"\", \"text\": ";
+    json_string(os, text);
+    os << ", \"timestamps\": [";
+    char b[40];
+    for (size_t i = 0; i < r.frame.size(); ++i) {
+      // frame shift 10 ms x subsampling 4 (sherpa-onnx OfflineRecognitionResult timestamps)
+      std::snprintf(b, sizeof b, "%s%.2f", i ? ", " : "", (float)(0.04f * (float)r.frame[i]));
+      os << b;
+    }
+    os << "], \"tokens\": [";
+    for (size_t i = 0; i < toks.size(); ++i) {
+      if (i) os << ", ";
+      json_string(os, toks[i]);
+    }
+    os << "], \"ys_log_probs\": [";
+    for (size_t i = 0; i < r.lp.size(); ++i) {
+      std::snprintf(b, sizeof b, "%s%.17g", i ? ", " : "", r.lp[i]);
+      os << b;
+    }
+    os << "], \"words\": []}";
+    const std::string js = os.str();
+    *needed = (int64_t)js.size() + 1;
+    if (!buf || cap < *needed) return fail(ZASR_ERR_INVALID, "result buffer too small");
+    std::memcpy(buf, js.c_str(), js.size() + 1);
     return (int)ZASR_OK;
   });
 }

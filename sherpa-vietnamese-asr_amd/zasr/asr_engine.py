@@ -57,6 +57,11 @@ BLANK_ID = 0
 UNK_ID = 2
 CONTEXT_SIZE = 2
 
+# the precision create_recognizer (and zasr.offline) use unless told otherwise: the
+# token-exact split-bf16 mode (exact-f32 quality products), the mode
+# bench.py reports as parity_mode and times the drop-in stage in; ZASR_PRECISION overrides
+DEFAULT_PRECISION = "bf16x6"
+
 _recognizer_cache: Dict[tuple, dict] = {}
 _cache_lock = threading.Lock()
 _last_handle: Optional[Recognizer] = None
@@ -217,7 +222,7 @@ def create_recognizer(model_path, cpu_threads=4, max_active_paths=8, execution_p
     """
     provider_policy = str(execution_provider or "cpu").lower()
     dev = int(os.environ.get("ZASR_DEVICE", "0")) if device_id is None else int(device_id)
-    prec = precision or os.environ.get("ZASR_PRECISION", "fp32")
+    prec = precision or os.environ.get("ZASR_PRECISION", DEFAULT_PRECISION)
     # cpu_threads / execution_provider do not change the GPU engine, so they are not part of
     # the key: the reference re-creates the recognizer with the worker thread count before its
     # two workers start (:2290-2307), which must not load a second copy of the model

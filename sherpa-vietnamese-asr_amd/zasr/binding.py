@@ -29,6 +29,11 @@ EXPORTS = (
     "zasr_vibert_num_detect", "zasr_vibert_run",
     "zasr_vad_create", "zasr_vad_destroy", "zasr_vad_probs", "zasr_vad_probs_device",
     "zasr_vad_window", "zasr_vad_last_passes", "zasr_silence_flags",
+    "zasr_create_stream", "zasr_destroy_stream", "zasr_stream_accept_waveform",
+    "zasr_decode_stream", "zasr_decode_streams", "zasr_stream_is_decoded",
+    "zasr_stream_num_tokens", "zasr_stream_num_frames", "zasr_stream_tokens",
+    "zasr_stream_frames", "zasr_stream_log_probs", "zasr_stream_token_stats",
+    "zasr_stream_result_json",
 )
 
 
@@ -168,6 +173,30 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_vad_last_passes.restype = I32
     lib.zasr_silence_flags.argtypes = [P, I64, I32, C.c_float, P, P]
     lib.zasr_silence_flags.restype = C.c_int
+    # offline streams (the sherpa-onnx OfflineStream surface, zasr/offline.py)
+    lib.zasr_create_stream.argtypes = [P, C.POINTER(P)]
+    lib.zasr_create_stream.restype = C.c_int
+    lib.zasr_destroy_stream.argtypes = [P]
+    lib.zasr_destroy_stream.restype = None
+    lib.zasr_stream_accept_waveform.argtypes = [P, I32, fp, I64]
+    lib.zasr_stream_accept_waveform.restype = C.c_int
+    lib.zasr_decode_stream.argtypes = [P, P]
+    lib.zasr_decode_stream.restype = C.c_int
+    lib.zasr_decode_streams.argtypes = [P, C.POINTER(P), I32]
+    lib.zasr_decode_streams.restype = C.c_int
+    for n in ("zasr_stream_is_decoded", "zasr_stream_num_tokens", "zasr_stream_num_frames"):
+        getattr(lib, n).argtypes = [P]
+        getattr(lib, n).restype = I32
+    lib.zasr_stream_tokens.argtypes = [P]
+    lib.zasr_stream_tokens.restype = C.POINTER(I32)
+    lib.zasr_stream_frames.argtypes = [P]
+    lib.zasr_stream_frames.restype = C.POINTER(I32)
+    lib.zasr_stream_log_probs.argtypes = [P]
+    lib.zasr_stream_log_probs.restype = C.POINTER(C.c_double)
+    lib.zasr_stream_token_stats.argtypes = [P]
+    lib.zasr_stream_token_stats.restype = fp
+    lib.zasr_stream_result_json.argtypes = [P, C.c_char_p, I64, C.POINTER(I64)]
+    lib.zasr_stream_result_json.restype = C.c_int
     if path is None:
         _lib = lib
     return lib

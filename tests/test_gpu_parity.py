@@ -237,7 +237,7 @@ def test_empty_and_short_chunks(tiny):
     assert res[2].T > 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x6", "bf16x3"])
 def test_speculative_greedy_equals_frame_by_frame(need_gpu, precision, monkeypatch):
     """Greedy with the decoder-context table runs speculative windows of F frames
     (kernels.h greedy_spec); results must be bit-identical to the frame-by-frame search step
