@@ -66,14 +66,18 @@ def parse_args(argv=None):
     ap.add_argument("--method", default="greedy_search")
     ap.add_argument("--beam", type=int, default=8)
     ap.add_argument("--audio-sec", type=float, default=3600.0)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6"])
-    ap.add_argument("--parity-precision", default="bf16x6",
-                    choices=["none", "fp32", "bf16x6", "bf16x3"],
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6", "f16x3"])
+    ap.add_argument("--parity-precision", default="f16x3",
+                    choices=["none", "fp32", "bf16x6", "bf16x3", "f16x3"],
                     help="asr stage: also time this token-exact precision mode on the same "
                          "workload in the same run and report it as the line's `parity_mode` "
-                         "(bf16x6: split-bf16 products of exact-f32 quality, token-for-token "
-                         "equal to the fp32 oracle; tests/test_gpu_e2e.py "
-                         "test_m_bf16_token_error_rate)")
+                         "(f16x3: fp16 hi + scaled lo pieces, three MFMAs per product, f32 "
+                         "quality; bf16x6: six bf16 piece products), with the count of the "
+                         "benched chunks whose tokens equal an exact-f32 (fp32 mode) decode of "
+                         "the same hour")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the fp32 decode of the hour that parity_mode's "
+                         "chunks_identical_to_fp32 is measured against")
     ap.add_argument("--parity-steps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5,
@@ -672,7 +676,9 @@ def bench_pipe(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    audio = synth_speech(args.audio_sec, AUDIO_SEED + rank)
+    # --shard-plan: one hour for the whole job (every rank the same audio, its share of the
+    # chunks / regions / ViBERT rows: FullPipe(shard=True)); else each rank its own hour
+    audio = synth_speech(args.audio_sec, AUDIO_SEED + (0 if args.shard_plan else rank))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before this process touches the GPU (spawned child); bounded sample: the first two
@@ -721,7 +727,8 @@ def bench_pipe(args):
     vib_save(vdir, vcfg, vib_weights(vcfg, 20261018))
     vib = VibertSession(vdir, device_id=local)
 
-    pipe = FullPipe(rec, recd, emb, vib, vcfg.vocab_size, beam=beam, campp_batch=args.campp_batch)
+    pipe = FullPipe(rec, recd, emb, vib, vcfg.vocab_size, beam=beam, campp_batch=args.campp_batch,
+                    shard=args.shard_plan and world > 1)
     pipe.prepare(audio)
     out = {}
 
@@ -761,7 +768,7 @@ def bench_pipe(args):
     pipe.punctuate(words)
     stage_ms["vibert"] = 1000 * (time.perf_counter() - t1)
     vib_shapes = pipe.punct.run_shapes[s0:]
-    c_len, plan, regions = pipe.c_len, pipe.c_off, pipe.r_off
+    c_len, plan, regions = pipe.c_len_all, pipe.c_off_all, pipe.r_off_all
     # algorithmic flops of the step: decode + CAM++ windows + ViBERT passes
     f_dec = sum(sum(chunk_flops(cfg, n, beam).values()) for n in c_len)
     f_cam = out["windows"] * campp_flops(ccfg, 150)
@@ -771,10 +778,11 @@ def bench_pipe(args):
     t_roof = f_dec / (p_dec * 1e12) + (f_cam + f_vib) / (MFMA_F32_PEAK_TFLOPS * 1e12)
     if rank == 0:
         line = {"metric": "audio-sec/sec full pipe (decode + CAM++ embeddings + ViBERT punctuation)",
-                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "value": round(args.audio_sec * (1 if args.shard_plan else world) * args.steps / el, 2),
                 "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(1000 * t_step, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "higher_is_better": True, "scaling": "strong" if args.shard_plan else "weak",
+                "vs_baseline": None,
                 "dtype": f"{args.precision} decode, f32 CAM++ / ViBERT",
                 "data": "synthetic (seeded speech-like audio, random-init Zipformer / CAM++ / "
                         "ViBERT weights)",
@@ -782,6 +790,13 @@ def bench_pipe(args):
                                        f"{'' if beam == 1 else ' beam %d' % beam} decode of 1 h "
                                        f"+ merge + CAM++ windows + ViBERT-capu punctuation",
                            "decode_chunks": len(plan), "campp_regions": len(regions),
+                           "parallelism": (f"dp{world} (one hour for the job: each rank its LPT "
+                                           f"share of the chunks and regions and of every ViBERT "
+                                           f"run's rows; words / embeddings / logits gathered to "
+                                           f"every rank by host object gathers; strong scaling)"
+                                           if args.shard_plan else
+                                           f"dp{world} (each rank its own hour; weak scaling)"),
+                           "shard_chunks_this_rank": len(pipe.c_len) if args.shard_plan else None,
                            "campp_windows": out["windows"], "campp_launch_batch": args.campp_batch,
                            "words": out["words"], "tokens": out["tokens"],
                            "vibert_rows_per_iteration": out["rows"],
@@ -872,9 +887,15 @@ def bench_rover(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     beam = args.beam
-    chunks = make_chunks(args.audio_sec, AUDIO_SEED + rank)
+    # --shard-plan: one hour for the whole job, each rank decodes + votes its LPT share of the
+    # chunks and the voted chunks are gathered in chunk order for the merge (zasr.rover)
+    chunks = make_chunks(args.audio_sec, AUDIO_SEED + (0 if args.shard_plan else rank))
     lens = [c.shape[0] for c in chunks]
     offs = np.cumsum([0] + lens[:-1]).tolist()
+    mine = None
+    if args.shard_plan:
+        from zasr.shard import lpt_partition
+        mine = lpt_partition(lens, world)[rank]
     hw_path = (DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file) or ""
     phrases = []
     if hw_path:
@@ -921,7 +942,7 @@ def bench_rover(args):
     def steps(k):
         r = rover_device_many(recs[0], recs[1], recds[0], recds[1], d_wav.data_ptr(), offs, lens,
                               k, beam, phrases, args.rover_sub_batches,
-                              args.rover_passes_per_call)[-1]
+                              args.rover_passes_per_call, mine=mine)[-1]
         last.update(words=len(r[0]), disagree_blocks=sum(r[1]), tokens_a=r[2], tokens_b=r[3])
 
     if args.warmup:
@@ -939,20 +960,24 @@ def bench_rover(args):
         el = max_over_ranks(el, device=f"cuda:{local}")
     # each model alone (decode only, HIP work + result copies) for the breakdown
     alone = {}
+    sel = list(range(len(lens))) if mine is None else mine
     for name, rec in zip(("30m", "68m"), recs):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        rec.decode_device(d_wav.data_ptr(), offs, lens, beam=beam)
+        if sel:
+            rec.decode_device(d_wav.data_ptr(), [offs[i] for i in sel], [lens[i] for i in sel],
+                              beam=beam)
         alone[name] = round(1000 * (time.perf_counter() - t1), 2)
     t_step = el / args.steps
     fl = sum(sum(chunk_flops(c, n, beam).values()) for c in cfgs for n in lens)
     peak = MFMA_BF16_PEAK_TFLOPS if args.precision != "fp32" else MFMA_F32_PEAK_TFLOPS
     if rank == 0:
         line = {"metric": "audio-sec/sec (xRT) ROVER Zipformer-30M + 68M offline decode",
-                "value": round(args.audio_sec * world * args.steps / el, 2),
+                "value": round(args.audio_sec * (1 if args.shard_plan else world) * args.steps / el, 2),
                 "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(1000 * t_step, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "higher_is_better": True, "scaling": "strong" if args.shard_plan else "weak",
+                "vs_baseline": None,
                 "dtype": args.precision,
                 "data": "synthetic (seeded speech-like audio, random-init Zipformer-30M / 68M weights)",
                 "config": {"workload": f"BASELINE config 4 per GPU: zipformer-30m + zipformer-68m "
@@ -965,7 +990,13 @@ def bench_rover(args):
                            "disagreeing_blocks": last["disagree_blocks"],
                            "tokens_30m": last["tokens_a"], "tokens_68m": last["tokens_b"],
                            "decode_alone_ms": alone,
-                           "parallelism": f"dp{world} (each rank its own hour; weak scaling)"},
+                           "shard_chunks_this_rank": len(mine) if mine is not None else None,
+                           "parallelism": (f"dp{world} (one hour for the job: each rank decodes "
+                                           f"and votes its LPT share of the chunks, the voted "
+                                           f"chunks gathered to every rank in chunk order by a "
+                                           f"host object gather, merged there; strong scaling)"
+                                           if args.shard_plan else
+                                           f"dp{world} (each rank its own hour; weak scaling)")},
                 "roofline": {"kernel": "both encoders + joiners (algorithmic flops / step time)",
                              "bound": "mfma", "unit": "TFLOP/s",
                              "achieved": round(fl / t_step / 1e12, 2), "peak": peak,
@@ -1012,7 +1043,7 @@ def gather_shards(res, mine, n_all, k, dist):
 
 
 # ------------------------------------------------------------------ token-exact mode
-SPLIT_PRODUCTS = {"bf16x3": 3, "bf16x6": 6}
+SPLIT_PRODUCTS = {"bf16x3": 3, "bf16x6": 6, "f16x3": 3}
 
 
 def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream, fl_step,
@@ -1035,15 +1066,42 @@ def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
         return rec.decode_device_batches(d_wav.data_ptr(), offs * m, lens * m, [n] * m,
                                          beam=beam, stream=stream)
 
-    steps(1)
+    first = steps(1)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    steps(k)
+    res = steps(k)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # the claim, measured: the timed batches' tokens against an exact-f32 decode of the same
+    # chunks (the fp32 mode: exact-f32 MFMA, f64 FFT; tests pin it token-exact to the oracle)
+    check = None
+    if not args.no_parity_check and prec != "fp32":
+        ref_rec = Recognizer(mdir, args.method, beam, hotwords=hotwords[0] if hotwords else None,
+                             hotword_scores=hotwords[1] if hotwords else None,
+                             device_id=int(os.environ.get("LOCAL_RANK", "0")), precision="fp32")
+        ref = ref_rec.decode_device(d_wav.data_ptr(), offs, lens, beam=beam, stream=stream)
+        torch.cuda.synchronize()
+        ref_rec.close()
+        ref_toks = [r.token_ids.tolist() for r in ref]
+        steps_same = []
+        for st in range(k):
+            got = [r.token_ids.tolist() for r in res[st * n:(st + 1) * n]]
+            steps_same.append(sum(a == b for a, b in zip(got, ref_toks)))
+        diff = [i for i, (a, b) in enumerate(zip([r.token_ids.tolist() for r in res[-n:]], ref_toks))
+                if a != b]
+        lp_max = max((float(np.max(np.abs(a.log_probs - b.log_probs)))
+                      for a, b in zip(res[-n:], ref) if a.token_ids.tolist() == b.token_ids.tolist()
+                      and a.log_probs.size), default=0.0)
+        check = {"chunks_identical_to_fp32": f"{min(steps_same)}/{n}",
+                 "per_timed_step": steps_same,
+                 "fp32_tokens": int(sum(len(t) for t in ref_toks)),
+                 "differing_chunks": diff[:20],
+                 "max_abs_log_prob_diff_identical_chunks": lp_max,
+                 "reference": "the same chunks decoded by the fp32 mode (exact-f32 MFMA), "
+                              "same search"}
     if dist:
         from zasr.shard import max_over_ranks
         el = max_over_ranks(el, device=dev)
@@ -1059,10 +1117,11 @@ def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
     f32_tf = fl_step / t_step / 1e12
     out = {"precision": prec, "value": round(args.audio_sec * world * k / el, 2),
            "unit": "audio-sec/sec", "steps": k, "ms_per_step": round(1000 * t_step, 3),
-           "token_exact": prec in ("fp32", "bf16x6"),
-           "parity_evidence": "tests/test_gpu_e2e.py::test_m_bf16_token_error_rate (token error "
-                              "rate 0.0 vs the fp32 oracle, greedy and beam 8 + hotwords; "
-                              "profiles/r03/precision/)",
+           "parity_check": check,
+           "token_exact": (check["chunks_identical_to_fp32"] == f"{n}/{n}") if check else None,
+           "parity_evidence": "parity_check (this run: every timed batch vs the fp32 decode) and "
+                              "tests/test_gpu_e2e.py::test_m_bf16_token_error_rate (token error "
+                              "rate 0.0 vs the fp32 oracle, greedy and beam 8 + hotwords)",
            "roofline_e2e": {"flops_per_step": fl_step, "achieved": round(f32_tf, 2),
                             "unit": "TFLOP/s", "peak_f32_mfma": MFMA_F32_PEAK_TFLOPS,
                             "frac_of_f32_mfma_peak": round(f32_tf / MFMA_F32_PEAK_TFLOPS, 4)},

@@ -56,13 +56,17 @@ enum {
    BF16X3: f32 storage as FP32, every encoder projection product as three bf16 MFMAs over
    hi / lo operand halves (relative product error ~2^-16).  BF16X6: three bf16 pieces per
    operand, six MFMAs per product (dropped terms below 2^-24: exact-f32 quality at bf16 MFMA
-   rates; token-exact against the fp32 oracle). */
+   rates; token-exact against the fp32 oracle).  F16X3: two fp16 pieces
+   per operand, hi = fp16(x) and lo = fp16((x - hi) * 2^11), three fp16 MFMAs per product
+   (hi*hi + (hi*lo + lo*hi) * 2^-11, ~2^-22 relative: f32 quality at half the MFMAs of
+   BF16X6); operands must stay below 65504 in magnitude (the 68M model's stay below 30). */
 enum {
   ZASR_PRECISION_FP32 = 0,
   ZASR_PRECISION_BF16 = 1,
   ZASR_PRECISION_BF16_ENC = 2,
   ZASR_PRECISION_BF16X3 = 3,
-  ZASR_PRECISION_BF16X6 = 4
+  ZASR_PRECISION_BF16X6 = 4,
+  ZASR_PRECISION_F16X3 = 5
 };
 
 typedef struct zasr_config {

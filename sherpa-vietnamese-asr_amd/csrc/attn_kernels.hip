@@ -13,6 +13,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "gemm.h"
 #include "gemm_dev.h"
 #include "kernels.h"
 
@@ -62,9 +63,13 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 // issues one): near-f32 (NP = 2) / f32-quality (NP = 3) scores and outputs at bf16 MFMA rates
 // (the bf16x3 / bf16x6 modes).  In these modes q and p carry no log2(e) factor: the score is
 // scaled into the log2 domain after the positional term.
-template <int MODE, int NP>
+// FMT 1 (the f16x3 mode, NP = 2): the pieces are fp16 hi + lo * 2^-11 (gemm_dev.h split_h8)
+// and every product is hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16 MFMAs, the lo products in a
+// second accumulator (scores: combined per key block; O: at the end, and rescaled with O).
+template <int MODE, int NP, int FMT = 0>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;
+  static_assert(FMT == 0 || NP == 2, "fp16 pieces: NP = 2");
   using T = typename std::conditional<SPLIT, float, __bf16>::type;
   // positional rows of this head, x = xlo + t for t < L + kPosPad, one plane per pos dim
   // (structure of arrays: the rows of two adjacent keys are adjacent floats in each plane,
@@ -122,8 +127,8 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     *reinterpret_cast<float4*>(&v0[4]) = *reinterpret_cast<const float4*>(qrow + 8 * h2 + 4);
     *reinterpret_cast<float4*>(&v1[0]) = *reinterpret_cast<const float4*>(qrow + 16 + 8 * h2);
     *reinterpret_cast<float4*>(&v1[4]) = *reinterpret_cast<const float4*>(qrow + 20 + 8 * h2);
-    split_f8<NP>(v0, qf0);
-    split_f8<NP>(v1, qf1);
+    split_fx<FMT, NP>(v0, qf0);
+    split_fx<FMT, NP>(v1, qf1);
     pq = *reinterpret_cast<const float4*>(qkp + (long)(r0 + ic) * ldq + 64 * H + 4 * h);
   } else {
     qf0[0] = *reinterpret_cast<const bf16x8*>(qrow + 8 * h2);
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
         const float v[8] = {stg0[S].x, stg0[S].y, stg0[S].z, stg0[S].w,
                             stg1[S].x, stg1[S].y, stg1[S].z, stg1[S].w};
         bf16x8 pc[NP];
-        split_f8<NP>(v, pc);
+        split_fx<FMT, NP>(v, pc);
 #pragma unroll
         for (int t = 0; t < NP; ++t) *reinterpret_cast<bf16x8*>(d + t * 2 * 32 * kKLd) = pc[t];
       } else {
@@ -190,11 +195,18 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       const int slot = 16 * (r >> 3) + 8 * ((jj >> 2) & 1) + (r & 7);
       if constexpr (SPLIT) {
         auto put = [&](int e, float rr) {
+          if constexpr (FMT == 1) {
+            const _Float16 hh = (_Float16)rr;
+            sVt[0][buf][(4 * vq + e) * kKLd + slot] = __builtin_bit_cast(__bf16, hh);
+            sVt[1][buf][(4 * vq + e) * kKLd + slot] =
+                __builtin_bit_cast(__bf16, (_Float16)((rr - (float)hh) * kF16Lo));
+          } else {
 #pragma unroll
-          for (int t = 0; t < NP; ++t) {
-            const __bf16 hh = (__bf16)rr;
-            sVt[t][buf][(4 * vq + e) * kKLd + slot] = hh;
-            if (t + 1 < NP) rr -= (float)hh;
+            for (int t = 0; t < NP; ++t) {
+              const __bf16 hh = (__bf16)rr;
+              sVt[t][buf][(4 * vq + e) * kKLd + slot] = hh;
+              if (t + 1 < NP) rr -= (float)hh;
+            }
           }
         };
         put(0, stg0[S].x);
@@ -218,8 +230,18 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
-    s = mfma_split<NP>(k0, qf0, s);
-    s = mfma_split<NP>(k1, qf1, s);
+    if constexpr (FMT == 1) {
+      f32x16 sl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sl[r] = 0.f;
+      mfma_h3(k0, qf0, s, sl);
+      mfma_h3(k1, qf1, s, sl);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] += sl[r] * kF16LoInv;
+    } else {
+      s = mfma_split<NP>(k0, qf0, s);
+      s = mfma_split<NP>(k1, qf1, s);
+    }
     const int pb = j0 + pbase;
     // positional term p_i . R[j - i] for the key pair (r, r + 1) = keys (jr, jr + 1) as packed
     // FMAs: the same fma chain per score as scalar fmaf, half the VALU issues
@@ -264,9 +286,9 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   // ---- key-block loop(s) ----
   float m = -INFINITY, l = 0.f, cst = 0.f;
   if constexpr (MODE == 2) cst = a.stats_in[(long)(r0 + ic) * H + h];
-  f32x16 o;
+  f32x16 o, ol;  // ol: the lo products of O (FMT 1)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  for (int r = 0; r < 16; ++r) o[r] = ol[r] = 0.f;
   // V^T fragments of the PV MFMAs; value dims d >= 12 (lanes c >= 12) stay zero
   bf16x8 vf[2][NP];
 #pragma unroll
@@ -357,6 +379,11 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
                 const f32x2 v = (f32x2){o[r], o[r + 1]} * (f32x2){sc, sc};
                 o[r] = v.x;
                 o[r + 1] = v.y;
+                if constexpr (FMT == 1) {
+                  const f32x2 w = (f32x2){ol[r], ol[r + 1]} * (f32x2){sc, sc};
+                  ol[r] = w.x;
+                  ol[r + 1] = w.y;
+                }
               }
               l *= sc;
               m = mn;
@@ -383,14 +410,21 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
             bf16x8 pf[NP];
+            if constexpr (FMT == 1) {
+              float pv[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              float r = s[8 * mm + q];
+              for (int q = 0; q < 8; ++q) pv[q] = s[8 * mm + q];
+              split_fx<FMT, NP>(pv, pf);
+            } else {
 #pragma unroll
-              for (int t = 0; t < NP; ++t) {
-                const __bf16 hh = (__bf16)r;
-                pf[t][q] = hh;
-                if (t + 1 < NP) r -= (float)hh;
+              for (int q = 0; q < 8; ++q) {
+                float r = s[8 * mm + q];
+#pragma unroll
+                for (int t = 0; t < NP; ++t) {
+                  const __bf16 hh = (__bf16)r;
+                  pf[t][q] = hh;
+                  if (t + 1 < NP) r -= (float)hh;
+                }
               }
             }
             if (c < 12) {  // lanes 12..31 keep the zeros set before the loop
@@ -398,7 +432,13 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
               for (int t = 0; t < NP; ++t)
                 vf[mm][t] = *reinterpret_cast<const bf16x8*>(&sVt[t][cur][c * kKLd + 16 * mm + 8 * h2]);
             }
-            o = mfma_split<NP>(vf[mm], pf, o);
+            if constexpr (FMT == 1) {
+              const bf16x8 x[2] = {vf[mm][0], vf[mm][1]};
+              const bf16x8 y[2] = {pf[0], pf[1]};
+              mfma_h3(x, y, o, ol);
+            } else {
+              o = mfma_split<NP>(vf[mm], pf, o);
+            }
           }
         }
       }
@@ -418,6 +458,10 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       const float lt = l + __shfl_xor(l, 32, 64);
       inv = 1.f / lt;
       if (h2 == 0) a.stats_out[(long)(r0 + i) * H + h] = m + __log2f(lt);
+    }
+    if constexpr (FMT == 1) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) o[r] += ol[r] * kF16LoInv;
     }
     // O^T rows = value dims d = (r&3) + 8 (r>>2) + 4 h2; d < 12 valid
     T* dst = reinterpret_cast<T*>(a.out) + (long)(r0 + i) * ldv + 12 * h;
@@ -439,15 +483,15 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   }
 }
 
-template <int NP>
+template <int NP, int FMT = 0>
 void launch_flash_np(const AttnFlashArgs& a, int mode, size_t lds, hipStream_t st) {
   const dim3 grid(cdiv(a.max_len, 128), a.nseq, mode == 0 ? 1 : a.H);
   if (mode == 0)
-    hipLaunchKernelGGL((attn_flash_kernel<0, NP>), grid, dim3(256), lds, st, a);
+    hipLaunchKernelGGL((attn_flash_kernel<0, NP, FMT>), grid, dim3(256), lds, st, a);
   else if (mode == 1)
-    hipLaunchKernelGGL((attn_flash_kernel<1, NP>), grid, dim3(256), lds, st, a);
+    hipLaunchKernelGGL((attn_flash_kernel<1, NP, FMT>), grid, dim3(256), lds, st, a);
   else
-    hipLaunchKernelGGL((attn_flash_kernel<2, NP>), grid, dim3(256), lds, st, a);
+    hipLaunchKernelGGL((attn_flash_kernel<2, NP, FMT>), grid, dim3(256), lds, st, a);
 }
 
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
@@ -461,8 +505,10 @@ void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
     launch_flash_np<2>(a, mode, lds, st);
   else if (a.pieces == 3)
     launch_flash_np<3>(a, mode, lds, st);
+  else if (a.pieces == kPiecesF16)
+    launch_flash_np<2, 1>(a, mode, lds, st);
   else
-    throw std::runtime_error("attention: pieces must be 1, 2 or 3");
+    throw std::runtime_error("attention: pieces must be 1, 2, 3 or kPiecesF16");
 }
 
 // =====================================================================================
@@ -477,7 +523,8 @@ __device__ __forceinline__ float4 h3_load4(const __bf16* p) {
   return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
 }
 
-// NP > 1 (split modes): NP bf16 pieces of t1 per element, piece t at t1t + t * hid * R8
+// NP > 1 (split modes): NP bf16 pieces of t1 per element, piece t at t1t + t * hid * R8;
+// NP = kPiecesF16: the two fp16 pieces hi, (t1 - hi) * 2^11 (gemm_dev.h split_h8)
 template <typename TH, int NP>
 __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict__ h3,
                                                             const int* __restrict__ off,
@@ -523,13 +570,21 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict
     if (ch >= hid) break;
     __bf16* dst = t1t + (long)ch * R8;
     float v = tile[cl][rl];
-#pragma unroll
-    for (int t = 0; t < NP; ++t) {
-      const __bf16 hh = (__bf16)v;
-      dst[(long)t * hid * R8 + col] = hh;
-      if (t + 1 < NP) v -= (float)hh;
+    if constexpr (NP == kPiecesF16) {
+      const _Float16 hh = (_Float16)v;
+      dst[col] = __builtin_bit_cast(__bf16, hh);
+      dst[(long)hid * R8 + col] = __builtin_bit_cast(__bf16, (_Float16)((v - (float)hh) * kF16Lo));
       if (last)
-        for (int z = col + 1; z < pad_end; ++z) dst[(long)t * hid * R8 + z] = (__bf16)0.f;
+        for (int z = col + 1; z < pad_end; ++z) dst[z] = dst[(long)hid * R8 + z] = (__bf16)0.f;
+    } else {
+#pragma unroll
+      for (int t = 0; t < NP; ++t) {
+        const __bf16 hh = (__bf16)v;
+        dst[(long)t * hid * R8 + col] = hh;
+        if (t + 1 < NP) v -= (float)hh;
+        if (last)
+          for (int z = col + 1; z < pad_end; ++z) dst[(long)t * hid * R8 + z] = (__bf16)0.f;
+      }
     }
   }
 }
@@ -539,8 +594,8 @@ void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const in
                           int pieces) {
   if (R <= 0) return;
   ZASR_REQUIRE(hid % 4 == 0, "nonlin_prep_t: hid must be a multiple of 4");
-  ZASR_REQUIRE(pieces == 1 || (!h3_bf16 && (pieces == 2 || pieces == 3)),
-               "nonlin_prep_t: pieces must be 1 (or 2 / 3 for an f32 h3)");
+  ZASR_REQUIRE(pieces == 1 || (!h3_bf16 && (pieces == 2 || pieces == 3 || pieces == kPiecesF16)),
+               "nonlin_prep_t: pieces must be 1 (or 2 / 3 / kPiecesF16 for an f32 h3)");
   const dim3 grid(cdiv(R, 64), cdiv(hid, 64));
   __bf16* out = reinterpret_cast<__bf16*>(t1t);
   const float* h3f = reinterpret_cast<const float*>(h3);
@@ -553,6 +608,9 @@ void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const in
   else if (pieces == 2)
     hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 2>), grid, dim3(256), 0, st, h3f, off, o8,
                        map, R, hid, R8, out);
+  else if (pieces == kPiecesF16)
+    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, kPiecesF16>), grid, dim3(256), 0, st, h3f,
+                       off, o8, map, R, hid, R8, out);
   else
     hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 3>), grid, dim3(256), 0, st, h3f, off, o8,
                        map, R, hid, R8, out);

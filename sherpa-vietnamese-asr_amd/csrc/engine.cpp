@@ -263,9 +263,10 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
                const std::vector<std::vector<int>>& hotwords, const std::vector<float>& hotword_scores,
                int precision)
     : device_(device), beam_(beam), greedy_(greedy), precision_(precision) {
-  ZASR_REQUIRE(precision >= 0 && precision <= 4,
+  ZASR_REQUIRE(precision >= 0 && precision <= 5,
                "precision must be 0 (fp32), 1 (bf16), 2 (bf16 encoder, f32 joiner + search), 3 "
-               "(bf16x3: two-piece split-bf16 products) or 4 (bf16x6: three-piece, f32 quality)");
+               "(bf16x3: two-piece split-bf16 products), 4 (bf16x6: three-piece, f32 quality) or "
+               "5 (f16x3: fp16 hi + scaled lo pieces, f32 quality)");
   // host side first (no GPU state to unwind when the files are bad): config.json +
   // model.safetensors, or the reference's encoder-/decoder-/joiner-*.onnx (onnx_io.h;
   // core/asr_engine.py:913-928)
@@ -463,7 +464,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
   if (split_pieces() > 0) {  // split-bf16 pieces of every encoder projection weight
     auto mkx = [&](DLin& l) {
       void* p = nullptr;
-      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2 * split_pieces()));
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2 * stored_pieces(split_pieces())));
       model_.allocations.push_back(p);
       split_to_bf16(l.w, p, (long)l.N * l.K, split_pieces(), stream_);
       l.wx = p;
@@ -476,9 +477,9 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
       // joiner_split_packed_kernel; J is written in the same order, already split, by store_j4
       const long pe = gemm_rp_packed_elems(cfg.V, cfg.joiner_dim);
       void* p = nullptr;
-      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)pe * 2 * split_pieces()));
+      ZASR_HIP_CHECK(hipMalloc(&p, (size_t)pe * 2 * stored_pieces(split_pieces())));
       model_.allocations.push_back(p);
-      for (int t = 0; t < split_pieces(); ++t)
+      for (int t = 0; t < stored_pieces(split_pieces()); ++t)
         gemm_rp_pack_weights(reinterpret_cast<const __bf16*>(model_.joiner.wx) + (long)t * cfg.V * cfg.joiner_dim,
                              cfg.V, cfg.joiner_dim, reinterpret_cast<__bf16*>(p) + t * pe, stream_);
       model_.joiner_packed = p;
@@ -1083,7 +1084,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     // z = (A0 @ t1) * y on the split-bf16 GEMM: A0 [L][L8] f32 (split while staging),
     // t1^T as np bf16 pieces [np][hid][R8] (the weight layout), y f32 in the epilogue
     float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
-    __bf16* t1t = ws<__bf16>("ly_t1t_x", (size_t)np * hid * R8);
+    __bf16* t1t = ws<__bf16>("ly_t1t_x", (size_t)stored_pieces(np) * hid * R8);
     float* z = ws<float>("ly_z", (size_t)R * hid);
     linear(Ly.na_in, X, d, R, h3, 3 * hid, EPI_NONE);
     prof_begin("elementwise");
@@ -1475,7 +1476,7 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   // J writer goes through store_j4); without the table decjoin writes row-major J
   static const bool no_pack = getenv("ZASR_JOINER_UNPACKED") != nullptr;
   const bool packed = (bf16 || jnp > 0) && model_.joiner_packed && model_.dec_table && !no_pack;
-  const int jpc = packed && jnp > 0 ? jnp : 1;  // packed images of J
+  const int jpc = packed && jnp > 0 ? stored_pieces(jnp) : 1;  // packed images of J
   const bool j16 = bf16 || packed;              // J buffer in bf16 elements
   const size_t jrows = (size_t)joiner_packed_rows((long)slots);
   void* J = j16 ? (void*)ws<__bf16>("se_joinin_h", jrows * D * jpc) : (void*)ws<float>("se_joinin", slots * D);

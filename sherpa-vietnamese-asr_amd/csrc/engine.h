@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "gemm.h"
 #include "kernels.h"
 
 namespace zasr {
@@ -238,7 +239,11 @@ class Engine {
   void order_after_encoders(const hipStream_t* enc_st, int E, hipStream_t main_st);
   int precision_ = 0;
   // bf16 pieces per operand of the split-bf16 modes (bf16x3: 2, bf16x6: 3), 0 otherwise
-  int split_pieces() const { return precision_ == 3 ? 2 : precision_ == 4 ? 3 : 0; }
+  // the `pieces` code of the split modes: 2 / 3 bf16 pieces (bf16x3 / bf16x6), kPiecesF16
+  // for the two fp16 pieces of f16x3 (gemm.h); 0 otherwise
+  int split_pieces() const {
+    return precision_ == 3 ? 2 : precision_ == 4 ? 3 : precision_ == 5 ? kPiecesF16 : 0;
+  }
   hipStream_t stream_ = nullptr;
   hipStream_t stream2_ = nullptr;  // searches (high priority: overlaps the next batch's encoder)
   hipStream_t stream3_ = nullptr;  // the second group of a beam search (high priority)

@@ -114,8 +114,14 @@ bool gemm_rp(const void* A, bool a_bf16, int lda, const void* Bp, const float* b
 // or the implicit-im2col loaders ALOAD_CONV2 / ALOAD_CONV3) split into `pieces` bf16 pieces
 // while staging; W pre-split by split_to_bf16, piece t at Bw + t * b_lo elements; C f32.
 // pieces = 2: 3 MFMAs per product (~2^-16 relative); pieces = 3: 6 MFMAs (exact-f32
-// quality).  Epilogues NONE, SWOOSHL, SWOOSHR, RESADD, MULAUX (f32 aux).  N, ldc (and ldaux)
+// quality); pieces = kPiecesF16: the f16x3 format, two fp16 pieces hi + lo * 2^-11 per
+// operand and 3 fp16 MFMAs per product (~2^-22 relative, two accumulators; operands below
+// 65504).  Epilogues NONE, SWOOSHL, SWOOSHR, RESADD, MULAUX (f32 aux).  N, ldc (and ldaux)
 // multiples of 4; K a multiple of 8 for dense A.
+// the `pieces` code of the f16x3 format (two fp16 pieces stored; see gemm_dev.h split_h8)
+constexpr int kPiecesF16 = 4;
+// pieces stored per operand for a `pieces` code
+inline int stored_pieces(int pieces) { return pieces == kPiecesF16 ? 2 : pieces; }
 void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t stream,
              int pieces);
 // dst[t * n + i] = piece t of src[i]: bf16(src[i] - sum of the previous pieces), t < pieces

@@ -73,6 +73,47 @@ __device__ __forceinline__ void split_f8(const float (&v)[8], bf16x8 (&pc)[NP]) 
   }
 }
 
+// ---- fp16 hi + scaled-lo pieces (the "f16x3" mode) ----
+// x = hi + lo * 2^-11 with hi = fp16(x), lo = fp16((x - hi) * 2^11): 11 + 11 significant bits
+// (~2^-22 relative; the residual is exact in f32 and its scaled value stays in the fp16 normal
+// range wherever hi does).  A product is hi*hi + (hi*lo + lo*hi) * 2^-11: three fp16 MFMAs at
+// the bf16 rate, two accumulators.  Operands must stay below 65504 in magnitude.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr float kF16Lo = 2048.f;
+constexpr float kF16LoInv = 1.f / 2048.f;
+
+__device__ __forceinline__ void split_h8(const float (&v)[8], bf16x8 (&pc)[2]) {
+  f16x8 h, l;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    h[q] = (_Float16)v[q];
+    l[q] = (_Float16)((v[q] - (float)h[q]) * kF16Lo);
+  }
+  pc[0] = __builtin_bit_cast(bf16x8, h);
+  pc[1] = __builtin_bit_cast(bf16x8, l);
+}
+
+// FMT 0: NP bf16 pieces (split_f8); FMT 1: the two fp16 pieces (split_h8, NP = 2)
+template <int FMT, int NP>
+__device__ __forceinline__ void split_fx(const float (&v)[8], bf16x8 (&pc)[NP]) {
+  if constexpr (FMT == 1) {
+    static_assert(NP == 2, "fp16 format: two pieces");
+    split_h8(v, pc);
+  } else {
+    split_f8<NP>(v, pc);
+  }
+}
+
+// hi += x0 y0; lo += x1 y0 + x0 y1 (fp16 MFMAs; pieces carried in bf16x8 containers)
+__device__ __forceinline__ void mfma_h3(const bf16x8 (&x)[2], const bf16x8 (&y)[2], f32x16& hi,
+                                        f32x16& lo) {
+  const f16x8 x0 = __builtin_bit_cast(f16x8, x[0]), x1 = __builtin_bit_cast(f16x8, x[1]);
+  const f16x8 y0 = __builtin_bit_cast(f16x8, y[0]), y1 = __builtin_bit_cast(f16x8, y[1]);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, y0, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, y1, lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, y0, hi, 0, 0, 0);
+}
+
 // acc += sum over u + v < NP of x[u] * y[v], smallest terms first (written out: every index
 // a constant, so the piece arrays stay in registers)
 template <int NP>

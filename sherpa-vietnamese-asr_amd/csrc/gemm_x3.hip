@@ -57,9 +57,11 @@ __device__ __forceinline__ float x3_act(float v) {
 // NP = 3 ("bf16x6"): pieces (p0, p1, p2), the six products p_i q_j with i + j <= 2 (6 MFMAs,
 // dropped terms below 2^-24 relative: exact-f32 quality), BK = 16 (same MFMAs per slab and
 // the same LDS as NP = 2).  Weights: piece t at Bw + t * blo.
+// FMT 1 ("f16x3"): NP = 2 fp16 pieces, hi + lo * 2^-11 (gemm_dev.h split_h8), the products
+// hi*hi into one accumulator and hi*lo + lo*hi into a second, combined in the epilogue.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP, int NP,
-          int BK = (NP == 2 ? 32 : 16)>
-__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmParams p,
+          int BK = (NP == 2 ? 32 : 16), int FMT = 0>
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N, FMT == 1 ? 2 : 1) void gemm_x3_kernel(GemmParams p,
                                                                        const __bf16* Bw, long blo,
                                                                        int tiles_n, int tiles_m) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -184,7 +186,9 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
       const int idx = tid + NT * i;
       if (idx < A_G) {
         bf16x8 pc[NP];
-        split8<NP>(r.a0[i], r.a1[i], pc);
+        const float v[8] = {r.a0[i].x, r.a0[i].y, r.a0[i].z, r.a0[i].w,
+                            r.a1[i].x, r.a1[i].y, r.a1[i].z, r.a1[i].w};
+        split_fx<FMT, NP>(v, pc);
         const int o = (idx / GPR) * LDH + 8 * (idx % GPR);
 #pragma unroll
         for (int t = 0; t < NP; ++t) *reinterpret_cast<bf16x8*>(&As[t * BM * LDH + o]) = pc[t];
@@ -202,12 +206,21 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
   };
 
   f32x16 acc[FM][FN];
+  constexpr int FL = FMT == 1 ? FM : 1;  // the lo-product accumulators (FMT 1 only)
+  constexpr int FLN = FMT == 1 ? FN : 1;
+  f32x16 accl[FL][FLN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < FL; ++i)
+#pragma unroll
+    for (int j = 0; j < FLN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accl[i][j][r] = 0.f;
 
   auto mma_slab = [&](int cur) {
     const __bf16* As = sbase + cur * STAGE;
@@ -231,13 +244,20 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (FMT == 1) {
+            const bf16x8 x[2] = {a[0][i], a[1][i]};
+            const bf16x8 y[2] = {b[0][j], b[1][j]};
+            mfma_h3(x, y, acc[i][j], accl[i % FL][j % FLN]);
+          } else {
 #pragma unroll
-          for (int sdeg = NP - 1; sdeg >= 0; --sdeg)
+            for (int sdeg = NP - 1; sdeg >= 0; --sdeg)
 #pragma unroll
-            for (int u = sdeg; u >= 0; --u)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u][i], b[sdeg - u][j],
-                                                                  acc[i][j], 0, 0, 0);
+              for (int u = sdeg; u >= 0; --u)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u][i], b[sdeg - u][j],
+                                                                    acc[i][j], 0, 0, 0);
+          }
+        }
     }
   };
 
@@ -291,7 +311,8 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
     for (int j = 0; j < FN; ++j) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        sE[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE + (lane & 31)] = acc[i][j][r];
+        sE[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * LDE + (lane & 31)] =
+            FMT == 1 ? acc[i][j][r] + accl[i % FL][j % FLN][r] * kF16LoInv : acc[i][j][r];
       __builtin_amdgcn_wave_barrier();
       const int col = n0 + wn * WTN + j * 32 + 4 * c4;
       const int cc = col < N ? col : N - 4;
@@ -332,17 +353,37 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_x3_kernel(GemmPara
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ALOAD, int EPI, int NP, int BK = (NP == 2 ? 32 : 16)>
+template <int BM, int BN, int WM, int WN, int ALOAD, int EPI, int NP, int BK = (NP == 2 ? 32 : 16),
+          int FMT = 0>
 void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
   if (ALOAD == ALOAD_DENSE && !p.slices && p.K % (2 * BK) == 0 && p.lda % 4 == 0) {
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP, BK>), grid,
+    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP, BK, FMT>), grid,
                        dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
     return;
   }
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP, BK>), grid,
+  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP, BK, FMT>), grid,
                      dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
+}
+
+// fp16 pieces (FMT 1): BK = 16 keeps two stages at 41 KB of LDS (3 blocks per CU)
+template <int ALOAD, int EPI>
+void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
+  const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
+  const int BN = (pad128 * 100 <= pad32 * 115) ? 128 : (pad64 * 100 <= pad32 * 115 ? 64 : 32);
+  const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
+  const bool big = blocks128 >= 512;
+  if (BN == 128) {
+    if (big) launch_x3_t<128, 128, 2, 2, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+    else launch_x3_t<64, 128, 2, 2, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+  } else if (BN == 64) {
+    if (big) launch_x3_t<128, 64, 2, 2, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+    else launch_x3_t<64, 64, 2, 2, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+  } else {
+    if (big) launch_x3_t<128, 32, 4, 1, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+    else launch_x3_t<64, 32, 2, 1, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+  }
 }
 
 template <int ALOAD, int EPI, int NP>
@@ -367,23 +408,32 @@ void launch_x3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
   }
 }
 
+// NP = 2 / 3: bf16 pieces; NP = kPiecesF16 (4): the two fp16 pieces of the f16x3 format
 template <int NP>
 void gemm_split_dispatch(const GemmParams& p, const __bf16* B, long b_lo, int epi, int aload,
                          hipStream_t st) {
+#define ZASR_X3(AL, EP)                                  \
+  do {                                                   \
+    if constexpr (NP == kPiecesF16)                      \
+      return launch_h3<AL, EP>(p, B, b_lo, st);          \
+    else                                                 \
+      return launch_x3<AL, EP, NP>(p, B, b_lo, st);      \
+  } while (0)
   if (aload == ALOAD_DENSE) {
     switch (epi) {
-      case EPI_NONE: return launch_x3<ALOAD_DENSE, EPI_NONE, NP>(p, B, b_lo, st);
-      case EPI_SWOOSHL: return launch_x3<ALOAD_DENSE, EPI_SWOOSHL, NP>(p, B, b_lo, st);
-      case EPI_SWOOSHR: return launch_x3<ALOAD_DENSE, EPI_SWOOSHR, NP>(p, B, b_lo, st);
-      case EPI_RESADD: return launch_x3<ALOAD_DENSE, EPI_RESADD, NP>(p, B, b_lo, st);
-      case EPI_MULAUX: return launch_x3<ALOAD_DENSE, EPI_MULAUX, NP>(p, B, b_lo, st);
+      case EPI_NONE: ZASR_X3(ALOAD_DENSE, EPI_NONE);
+      case EPI_SWOOSHL: ZASR_X3(ALOAD_DENSE, EPI_SWOOSHL);
+      case EPI_SWOOSHR: ZASR_X3(ALOAD_DENSE, EPI_SWOOSHR);
+      case EPI_RESADD: ZASR_X3(ALOAD_DENSE, EPI_RESADD);
+      case EPI_MULAUX: ZASR_X3(ALOAD_DENSE, EPI_MULAUX);
       default: break;
     }
   } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
-    return launch_x3<ALOAD_CONV2, EPI_SWOOSHR, NP>(p, B, b_lo, st);
+    ZASR_X3(ALOAD_CONV2, EPI_SWOOSHR);
   } else if (aload == ALOAD_CONV3 && epi == EPI_SWOOSHR) {
-    return launch_x3<ALOAD_CONV3, EPI_SWOOSHR, NP>(p, B, b_lo, st);
+    ZASR_X3(ALOAD_CONV3, EPI_SWOOSHR);
   }
+#undef ZASR_X3
   throw std::runtime_error("gemm_x3: unsupported (aload, epi) combination");
 }
 
@@ -392,6 +442,13 @@ __global__ void split_bf16_kernel(const float* __restrict__ src, __bf16* __restr
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     float r = src[i];
+    if (pieces == kPiecesF16) {  // fp16 hi, fp16 (x - hi) * 2^11 (gemm_dev.h split_h8)
+      const _Float16 h = (_Float16)r;
+      const _Float16 l = (_Float16)((r - (float)h) * kF16Lo);
+      reinterpret_cast<_Float16*>(dst)[i] = h;
+      reinterpret_cast<_Float16*>(dst)[n + i] = l;
+      return;
+    }
     for (int t = 0; t < pieces; ++t) {
       const __bf16 h = (__bf16)r;
       dst[t * n + i] = h;
@@ -410,12 +467,15 @@ void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload,
                "gemm_x3: N and the C / aux row strides must be multiples of 4");
   ZASR_REQUIRE(p.slices != nullptr || (p.K % 8 == 0 && p.lda % 4 == 0),
                "gemm_x3: K must be a multiple of 8 and lda of 4");
-  ZASR_REQUIRE(pieces == 2 || pieces == 3, "gemm_x3: pieces must be 2 or 3");
+  ZASR_REQUIRE(pieces == 2 || pieces == 3 || pieces == kPiecesF16,
+               "gemm_x3: pieces must be 2, 3 or kPiecesF16");
   const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
   if (pieces == 2)
     gemm_split_dispatch<2>(p, B, b_lo, epi, aload, st);
-  else
+  else if (pieces == 3)
     gemm_split_dispatch<3>(p, B, b_lo, epi, aload, st);
+  else
+    gemm_split_dispatch<kPiecesF16>(p, B, b_lo, epi, aload, st);
 }
 
 void split_to_bf16(const float* src, void* dst, long n, int pieces, hipStream_t st) {

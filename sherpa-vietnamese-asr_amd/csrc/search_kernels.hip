@@ -685,7 +685,7 @@ __global__ __launch_bounds__(256) void joiner_reg_kernel(JoinerPackedArgs j) {
 // fragments (written / packed once: store_j4, Engine load) and issuing the NP (NP + 1) / 2
 // piece products smallest first (mfma_split, the order of gemm_x3 / joiner_split_kernel).
 // CH k16 steps of fragments in flight per register set.
-template <int QK, int NP, int CH>
+template <int QK, int NP, int CH, int FMT = 0>
 __global__ __launch_bounds__(256) void joiner_split_packed_kernel(JoinerPackedArgs j) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m0 = blockIdx.y * 64;
@@ -708,9 +708,9 @@ __global__ __launch_bounds__(256) void joiner_split_packed_kernel(JoinerPackedAr
       a[0][c][t] = srcJ[t * jp + c * 64];
       b[0][c][t] = srcW[t * wp + c * 64];
     }
-  f32x16 acc;
+  f32x16 acc, accl;  // accl: the lo products (FMT 1, the f16x3 format)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = accl[r] = 0.f;
   // the next set's loads go out as one group before this set's MFMAs (scheduling barriers:
   // left alone, the compiler streams one load per MFMA with ~4 in flight, latency-bound)
 #pragma unroll
@@ -727,8 +727,20 @@ __global__ __launch_bounds__(256) void joiner_split_packed_kernel(JoinerPackedAr
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < CH; ++c) acc = mfma_split<NP>(a[cur][c], b[cur][c], acc);
+    for (int c = 0; c < CH; ++c) {
+      if constexpr (FMT == 1) {
+        const bf16x8 x[2] = {a[cur][c][0], a[cur][c][1]};
+        const bf16x8 y[2] = {b[cur][c][0], b[cur][c][1]};
+        mfma_h3(x, y, acc, accl);
+      } else {
+        acc = mfma_split<NP>(a[cur][c], b[cur][c], acc);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (FMT == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += accl[r] * kF16LoInv;
   }
   const int col = g * 32 + (lane & 31);
   if (col >= j.V) return;
@@ -745,10 +757,14 @@ void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st) {
   if (j.M <= 0) return;
   dim3 grid(cdiv(j.V, 64), cdiv(j.M, 64));
   if (j.pieces > 0) {
-    ZASR_REQUIRE(j.pieces == 2 || j.pieces == 3, "packed split joiner: pieces must be 2 or 3");
+    ZASR_REQUIRE(j.pieces == 2 || j.pieces == 3 || j.pieces == kPiecesF16,
+                 "packed split joiner: pieces must be 2, 3 or kPiecesF16");
     ZASR_REQUIRE(j.D == 256 || j.D == 512, "packed split joiner: joiner dim must be 256 or 512");
     const int qk = j.D / 16;
-    if (j.pieces == 2) {
+    if (j.pieces == kPiecesF16) {
+      if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 2, 4, 1>), grid, dim3(256), 0, st, j);
+      else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 2, 4, 1>), grid, dim3(256), 0, st, j);
+    } else if (j.pieces == 2) {
       if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 2, 4>), grid, dim3(256), 0, st, j);
       else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 2, 4>), grid, dim3(256), 0, st, j);
     } else {
@@ -785,6 +801,18 @@ __device__ __forceinline__ void store_j4(const DecTable& dt, long row, int k, fl
     // fragment order, so the joiner reads ready MFMA operands (no per-launch split)
     float r[4] = {tanhf(e.x + d.x), tanhf(e.y + d.y), tanhf(e.z + d.z), tanhf(e.w + d.w)};
     __bf16* base = reinterpret_cast<__bf16*>(dt.J) + packed_j_off(row, k, dt.D);
+    if (dt.j_pieces == kPiecesF16) {  // fp16 hi, (x - hi) * 2^11 (gemm_dev.h split_h8)
+      bf16x4 vh, vl;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const _Float16 hh = (_Float16)r[q];
+        vh[q] = __builtin_bit_cast(__bf16, hh);
+        vl[q] = __builtin_bit_cast(__bf16, (_Float16)((r[q] - (float)hh) * kF16Lo));
+      }
+      *reinterpret_cast<bf16x4*>(base) = vh;
+      *reinterpret_cast<bf16x4*>(base + dt.j_plane) = vl;
+      return;
+    }
     for (int t = 0; t < dt.j_pieces; ++t) {
       bf16x4 v;
 #pragma unroll

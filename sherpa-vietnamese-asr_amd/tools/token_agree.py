@@ -41,7 +41,7 @@ def edit_distance(a, b) -> int:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="bf16x6,bf16x3,bf16")
+    ap.add_argument("--modes", default="f16x3,bf16x6,bf16x3,bf16")
     ap.add_argument("--methods", default="greedy,beam8hw")
     ap.add_argument("--audio-sec", type=float, default=3600.0)
     ap.add_argument("--model", default="zipformer-68m")

@@ -40,7 +40,7 @@ EXPORTS = (
 # include/zasr.h ZASR_PRECISION_*: "bf16_enc" = the bf16 encoder with the f32 joiner + search;
 # "bf16x3" / "bf16x6" = f32 storage, split-bf16 products (2 / 3 pieces per operand) on the
 # bf16 MFMA
-PRECISIONS = {"fp32": 0, "bf16": 1, "bf16_enc": 2, "bf16x3": 3, "bf16x6": 4}
+PRECISIONS = {"fp32": 0, "bf16": 1, "bf16_enc": 2, "bf16x3": 3, "bf16x6": 4, "f16x3": 5}
 
 
 class ZasrError(RuntimeError):

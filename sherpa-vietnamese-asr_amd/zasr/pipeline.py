@@ -123,11 +123,22 @@ class FullPipe:
 
     def __init__(self, rec, recd, emb, vib, vib_vocab: int, beam: int = 1,
                  campp_batch: int = 4096, iterations: int = ITERATIONS, vib_batch: int = 0,
-                 tokenizer=None, confidence: float = 0.3, case_confidence: float = 0.0):
+                 tokenizer=None, confidence: float = 0.3, case_confidence: float = 0.0,
+                 shard: bool = False):
+        """shard: strong scaling over the ranks of an initialised torch.distributed group (one
+        process per GPU, every rank given the same file): each rank decodes its
+        zasr.shard.lpt_partition share of the chunk plan and embeds its share of the speech
+        regions; the per-chunk words are gathered to every rank in chunk order and merged
+        there, every rank runs the restorer's host logic on the same transcript with each
+        ViBERT run's rows split over the ranks (zasr.shard.RowShardedSession), and the window
+        embeddings are gathered in region order.  Without a group it is the one-GPU pipe."""
+        from zasr.shard import RowShardedSession
         self.rec, self.recd, self.emb, self.vib = rec, recd, emb, vib
         self.vib_vocab, self.beam, self.B, self.iterations = vib_vocab, beam, campp_batch, iterations
+        self.shard = bool(shard)
         # <= 0: one ViBERT run per iteration (make_punctuator)
-        self.punct = make_punctuator(vib, vib_vocab, tokenizer, vib_batch, iterations=iterations,
+        self.punct = make_punctuator(RowShardedSession(vib) if self.shard else vib, vib_vocab,
+                                     tokenizer, vib_batch, iterations=iterations,
                                      confidence=confidence, case_confidence=case_confidence)
 
     def punctuate(self, words: Sequence[Dict]) -> Tuple[str, int, List[int]]:
@@ -146,12 +157,26 @@ class FullPipe:
         self.n = a.shape[0]
         plan = plan_chunks(a)                      # decode chunks, 3 s overlap
         regions = plan_chunks(a, overlap_sec=0.0)  # diarization speech regions
-        self.c_off = [s for s, _, _ in plan]
-        self.c_len = [e - s for s, e, _ in plan]
-        self.r_off = [s for s, _, _ in regions]
-        self.r_len = [e - s for s, e, _ in regions]
+        self.c_off_all = [s for s, _, _ in plan]
+        self.c_len_all = [e - s for s, e, _ in plan]
+        self.r_off_all = [s for s, _, _ in regions]
+        self.r_len_all = [e - s for s, e, _ in regions]
+        n_c, n_r = len(plan), len(regions)
+        self.mine_c, self.mine_r = list(range(n_c)), list(range(n_r))
+        if self.shard:
+            from zasr.shard import _dist, lpt_partition
+            dist = _dist()
+            if dist is not None:
+                world, rank = dist.get_world_size(), dist.get_rank()
+                self.mine_c = lpt_partition(self.c_len_all, world)[rank]
+                self.mine_r = lpt_partition(self.r_len_all, world)[rank]
+        # this rank's chunks and regions (all of them on one GPU)
+        self.c_off = [self.c_off_all[i] for i in self.mine_c]
+        self.c_len = [self.c_len_all[i] for i in self.mine_c]
+        self.r_off = [self.r_off_all[i] for i in self.mine_r]
+        self.r_len = [self.r_len_all[i] for i in self.mine_r]
         # window count bound: (frames - 150) / 60 + 2 per region
-        self.cap = sum(max(1, (n // 160) // 60 + 2) for n in self.r_len)
+        self.cap = max(1, sum(max(1, (n // 160) // 60 + 2) for n in self.r_len))
         self.d_audio = torch.from_numpy(a).cuda()
         self.d_feats = torch.empty((self.cap, 150, 80), dtype=torch.float32, device="cuda")
         self.d_emb = torch.empty((self.cap, self.emb.dim), dtype=torch.float32, device="cuda")
@@ -167,6 +192,8 @@ class FullPipe:
             return self.rec.decode_device(self.d_audio.data_ptr(), self.c_off, self.c_len,
                                           beam=self.beam, stream=stream)
         n = len(self.c_len)
+        if n == 0:  # more ranks than chunks
+            return []
         return self.rec.decode_device_batches(self.d_audio.data_ptr(), self.c_off * passes,
                                               self.c_len * passes, [n] * passes,
                                               beam=self.beam, stream=stream)
@@ -177,6 +204,9 @@ class FullPipe:
         chunks = [{"words": result_words(self.recd, r, n, s / 16000.0),
                    "audio_start_abs": s / 16000.0, "audio_end_abs": (s + n) / 16000.0}
                   for r, s, n in zip(res, self.c_off, self.c_len)]
+        if self.shard:
+            from zasr.shard import gather_chunks
+            chunks = gather_chunks(list(zip(self.mine_c, chunks)), len(self.c_len_all))
         words, _ = merge_chunks_with_overlap(chunks)
         return words, sum(int(r.token_ids.size) for r in res)
 
@@ -184,6 +214,9 @@ class FullPipe:
         return self.words(self.decode(stream))
 
     def embed_windows(self, stream: int):
+        if not self.r_len:
+            z = np.zeros(0, np.int32)
+            return z, z, z
         reg, first, nfr = self.emb.windows_device(self.d_audio.data_ptr(), self.r_off, self.r_len,
                                                   self.d_feats.data_ptr(), self.cap, stream=stream)
         W, D = len(reg), self.emb.dim
@@ -224,7 +257,26 @@ class FullPipe:
                     # where the next decode is in flight
                     with torch.cuda.stream(self.s_campp):
                         embs = l2_normalise(self.d_emb[:len(reg)].cpu().numpy())
+                    win = np.stack([np.asarray(self.mine_r, np.int64)[np.asarray(reg, np.int64)]
+                                    if len(reg) else np.zeros(0, np.int64), first, nfr], 1)
+                    if self.shard:
+                        embs, win = self._gather_windows(embs, win)
                     outs.append({"words": words, "tokens": tokens, "text": text,
                                  "vibert_runs": runs, "vibert_rows": rows, "embeddings": embs,
-                                 "windows": np.stack([reg, first, nfr], 1)})
+                                 "windows": win})
         return outs
+
+    def _gather_windows(self, embs: np.ndarray, win: np.ndarray):
+        """Every rank's window embeddings and (region, first frame, frames) rows, in region
+        order (regions are whole per rank, windows in order within a region)."""
+        from zasr.shard import gather_chunks
+        part = []
+        for ri in self.mine_r:
+            sel = win[:, 0] == ri
+            part.append((ri, (embs[sel], win[sel])))
+        got = gather_chunks(part, len(self.r_len_all))
+        dim = embs.shape[1] if embs.ndim == 2 else self.emb.dim
+        e = [g[0] for g in got if len(g[0])]
+        w = [g[1] for g in got if len(g[1])]
+        return (np.concatenate(e) if e else np.zeros((0, dim), np.float32),
+                np.concatenate(w) if w else np.zeros((0, 3), np.int64))

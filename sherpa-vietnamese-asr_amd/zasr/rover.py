@@ -156,7 +156,7 @@ def decode_chunks_rover(rec_a, rec_b, chunks, time_offsets, hotword_phrases: Seq
 
 def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths, k: int,
                       beam: int, hotword_phrases: Sequence[str] = (), sub_batches: int = 1,
-                      passes_per_call: int = 1):
+                      passes_per_call: int = 1, mine: Optional[Sequence[int]] = None):
     """k passes of one file's chunk plan (waveforms in HBM) through the ROVER pair on one GPU
     (BASELINE config 4): model A (primary, 30M) and model B (68M) decode every chunk
     (`zasr_decode_device`, each on its own engine streams, concurrently: two worker threads,
@@ -169,13 +169,31 @@ def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths
     `sub_batches` consecutive batches, through the engine's batch pipeline
     (zasr_decode_device_batches: the next batch's encoder under this batch's search; beam
     search keeps two batches' searches in flight), results identical.  Returns [(merged
-    words, disagreements per chunk, tokens of A, tokens of B)] per pass."""
+    words, disagreements per chunk, tokens of A, tokens of B)] per pass.
+
+    mine: strong scaling over the ranks of an initialised torch.distributed group (one process
+    per GPU, BASELINE config 4's "sharded across 8 GPUs"): this rank decodes and votes only
+    the chunk indices `mine` (its zasr.shard.lpt_partition share of the SAME plan on every
+    rank), the voted chunks are gathered to every rank in chunk order (a host object gather,
+    zasr.shard.gather_chunks: the vote is per chunk, so the only exchange is its result) and
+    every rank merges the whole file; disagreements / tokens are this rank's."""
     from concurrent.futures import ThreadPoolExecutor
 
     from zasr.asr_engine import result_words
     from zasr.merge import merge_chunks_with_overlap
+    from zasr.shard import gather_chunks
+    n_all = len(lengths)
+    if mine is not None:
+        mine = list(mine)
+        offsets, lengths = [offsets[i] for i in mine], [lengths[i] for i in mine]
     offsets, lengths = list(offsets), list(lengths)
     n = len(lengths)
+    if n == 0:  # more ranks than chunks: nothing to decode, still part of every gather
+        out = []
+        for _ in range(k):
+            words, _ = merge_chunks_with_overlap(gather_chunks([], n_all))
+            out.append((words, [], 0, 0))
+        return out
     nb = max(1, min(int(sub_batches), n))
     sizes = [n * (i + 1) // nb - n * i // nb for i in range(nb)]
     g = max(1, int(passes_per_call))
@@ -204,6 +222,8 @@ def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths
                     chunks.append({"words": merged, "audio_start_abs": t0,
                                    "audio_end_abs": (off + ln) / 16000.0})
                     dis.append(len(d))
+                if mine is not None:
+                    chunks = gather_chunks(list(zip(mine, chunks)), n_all)
                 words, _ = merge_chunks_with_overlap(chunks)
                 out.append((words, dis, sum(int(x.token_ids.size) for x in ra),
                             sum(int(x.token_ids.size) for x in rb)))

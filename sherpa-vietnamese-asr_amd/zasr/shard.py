@@ -58,6 +58,57 @@ def decode_sharded(decode_fn: Callable[[List], List[R]], chunks: Sequence, lengt
     return out
 
 
+def gather_chunks(part: Sequence, n_all: int) -> List:
+    """This rank's [(chunk index, item)] -> every rank's items of all n_all chunks, in chunk
+    order (host object gather; the identity ordering without a process group).  Raises when a
+    chunk is missing or delivered twice."""
+    dist = _dist()
+    parts = [list(part)]
+    if dist is not None:
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, list(part))
+    out: List = [None] * n_all
+    seen = [False] * n_all
+    for p in parts:
+        for i, item in p:
+            if seen[i]:
+                raise RuntimeError(f"chunk {i} delivered twice")
+            seen[i] = True
+            out[i] = item
+    missing = [i for i, s in enumerate(seen) if not s]
+    if missing:
+        raise RuntimeError(f"chunk gather lost chunks {missing[:5]}")
+    return out
+
+
+class RowShardedSession:
+    """An ONNX-session-shaped wrapper (`run(output_names, feeds)`) that splits every call's
+    batch rows over the ranks of the process group: each rank runs its contiguous share on its
+    own GPU and the outputs are gathered to every rank in row order (host object gather).  All
+    ranks must make the same calls with the same feeds -- true when each rank runs the same
+    deterministic host logic on the same input (the config-5 restorer on the gathered
+    transcript).  Rows are independent (per-sequence attention, row-wise projections), so the
+    gathered outputs equal one whole-batch run (tests/test_multiproc.py, tests/test_gpu_pipe.py)."""
+
+    def __init__(self, session):
+        self.session = session
+
+    def run(self, output_names, feeds):
+        import numpy as np
+        dist = _dist()
+        if dist is None or dist.get_world_size() == 1:
+            return self.session.run(output_names, feeds)
+        world, rank = dist.get_world_size(), dist.get_rank()
+        B = int(next(iter(feeds.values())).shape[0])
+        lo, hi = B * rank // world, B * (rank + 1) // world
+        mine = list(self.session.run(output_names, {k: v[lo:hi] for k, v in feeds.items()})) \
+            if hi > lo else None
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        got = [p for p in parts if p is not None]
+        return [np.concatenate([p[j] for p in got], axis=0) for j in range(len(got[0]))]
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Max of a per-rank scalar (bench.py's elapsed time); identity without a group."""
     dist = _dist()

@@ -9,6 +9,8 @@ Operand modes (f32 accumulate throughout):
   bf16   each operand rounded to bf16 (one MFMA)
   x3     hi + lo split of both operands, hi*hi + hi*lo + lo*hi (three bf16 MFMAs)
   x6     hi + mid + lo split, the six products down to 2^-24 (six bf16 MFMAs)
+  h3     fp16 hi + lo with the lo piece scaled by 2^11, hi*hi + (hi*lo + lo*hi) * 2^-11
+         (three fp16 MFMAs, ~2^-22 relative; operands must stay below 65504)
 
     python tests/precision_sim.py [modes...] [--joiner-f32]
 """
@@ -42,10 +44,29 @@ def split(x, n):
     return parts
 
 
+_RANGE = {"max": 0.0}
+
+
+def _h(x):
+    return x.to(torch.float16).to(torch.float32)
+
+
+def hsplit(x):
+    """fp16 hi + lo split with the lo piece pre-scaled by 2^11 (kept in the fp16 normal
+    range): x = hi + lo * 2^-11 to ~2^-22 relative (the "fp16x3" operand format)."""
+    _RANGE["max"] = max(_RANGE["max"], float(x.abs().max()) if x.numel() else 0.0)
+    h = _h(x)
+    return h, _h((x - h) * 2048.0)
+
+
 def emu_mm(a, b):
     m = _MODE["m"]
     if m is None:
         return torch.matmul(a, b)
+    if m == "h3":
+        ah, al = hsplit(a)
+        bh, bl = hsplit(b)
+        return torch.matmul(ah, bh) + (torch.matmul(ah, bl) + torch.matmul(al, bh)) * (1.0 / 2048.0)
     if m == "bf16":
         return torch.matmul(_bf(a), _bf(b))
     if m == "x3":
@@ -108,6 +129,8 @@ def run(modes, joiner_f32=False):
             rep[name] = {"ter": round(sum(errs) / max(1, sum(n)), 5), "errs": errs, "ref_tokens": n}
         d = max(float(np.abs(a - b).max()) for a, b in zip(se, encs))
         out[m] = {"enc_max_abs_diff": d, **rep}
+        if m == "h3":
+            out[m]["max_abs_operand"] = _RANGE["max"]
         print(m, json.dumps(out[m]), flush=True)
     return out
 
@@ -137,6 +160,10 @@ def _conv(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
         return c(x, w, b)
     if m == "bf16":
         return c(_bf(x), _bf(w), b)
+    if m == "h3":
+        xh, xl = hsplit(x)
+        wh, wl = hsplit(w)
+        return c(xh, wh, b) + (c(xh, wl) + c(xl, wh)) * (1.0 / 2048.0)
     if m == "x3":
         xh, xl = split(x, 2)
         wh, wl = split(w, 2)

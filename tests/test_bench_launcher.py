@@ -54,3 +54,12 @@ def test_bench_shard_plan_two_ranks_strong_scaling():
     # value = audio of the job / time (x1, not x world)
     assert abs(two["value"] - 40.0 * two["steps"] / (two["ms_per_step"] * two["steps"] / 1e3)) \
         <= 0.02 * two["value"]
+
+
+def test_bench_gpus8_shard_plan():
+    """The 8-rank launch the driver runs at round end (SCALE), on CPU: 8 gloo ranks, the hour's
+    chunks LPT-split 8 ways and gathered in chunk order."""
+    one = _run("--shard-plan")
+    eight = _run("--gpus", "8", "--shard-plan")
+    assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+    assert eight["config"]["tokens_emitted_per_gpu"] == one["config"]["tokens_emitted_per_gpu"]

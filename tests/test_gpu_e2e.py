@@ -165,7 +165,7 @@ def test_m_bf16_token_error_rate(m_case):
     from zasr.binding import Recognizer
     ref = {"greedy": m_case["greedy"], "beam8_hotwords": m_case["beam8"]}
     report = {}
-    for prec in ("bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6"):
+    for prec in ("bf16", "bf16_enc", "fp32", "bf16x3", "bf16x6", "f16x3"):
         for name, method, beam in (("greedy", "greedy_search", 1),
                                    ("beam8_hotwords", "modified_beam_search", 8)):
             kw = {"hotwords": m_case["phrases"], "hotword_scores": m_case["scores"]} if beam > 1 else {}
@@ -183,7 +183,7 @@ def test_m_bf16_token_error_rate(m_case):
         json.dump({"model": "zipformer-68m (random init)", "chunks_sec": M_SECS,
                    "reference": "fp32 oracle (fbank + torch encoder + reference search)",
                    "rates": report}, f, indent=1)
-    for prec in ("fp32", "bf16x6"):
+    for prec in ("fp32", "bf16x6", "f16x3"):
         assert report[f"{prec}/greedy"]["token_error_rate"] == 0.0, report
         assert report[f"{prec}/beam8_hotwords"]["token_error_rate"] == 0.0, report
     for name in ("greedy", "beam8_hotwords"):

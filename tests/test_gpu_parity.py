@@ -83,7 +83,7 @@ def test_encoder_tiny_batched_matches_oracle(tiny):
         _enc_close(g, ref)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16x6", "bf16x3", "f16x3"])
 def test_encoder_m_matches_oracle(need_gpu, prec):
     """68M encoder_out vs the oracle within 2e-3 * max(1, |ref|): exact-f32 MFMA (fp32) and
     split-bf16 products (bf16x6: f32 quality; bf16x3: ~2^-16 relative per product)."""
@@ -237,7 +237,7 @@ def test_empty_and_short_chunks(tiny):
     assert res[2].T > 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16x6", "bf16x3", "f16x3"])
 def test_speculative_greedy_equals_frame_by_frame(need_gpu, precision, monkeypatch):
     """Greedy with the decoder-context table runs speculative windows of F frames
     (kernels.h greedy_spec); results must be bit-identical to the frame-by-frame search step
