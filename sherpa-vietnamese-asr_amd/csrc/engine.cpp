@@ -322,7 +322,15 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     DLin l;
     l.N = N;
     l.K = K;
-    l.w = dev(tensor(pre + ".weight", {N, K}).data, (size_t)N * K);
+    const float* hw = tensor(pre + ".weight", {N, K}).data;
+    if (precision_ == 5) {
+      // f16x3 splits every weight into fp16 pieces: a magnitude at or beyond the fp16 range
+      // would become inf, so such a model is refused here (use bf16x6: same quality)
+      for (size_t i = 0; i < (size_t)N * K; ++i)
+        ZASR_REQUIRE(std::fabs(hw[i]) < 65504.f,
+                     "precision f16x3: weight " + pre + " exceeds the fp16 range; use bf16x6");
+    }
+    l.w = dev(hw, (size_t)N * K);
     if (bias) l.b = dev(tensor(pre + ".bias", {N}).data, N);
     return l;
   };
@@ -1429,6 +1437,7 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t_out[a] > t_out[b]; });
   const int S = (int)order.size();
   job.S = S;
+  job.check_finite = precision_ == 5;
   if (S == 0) return;
   const int H = beam;
   const int Tmax = t_out[order[0]];
@@ -1705,6 +1714,12 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   ZASR_HIP_CHECK(hipMemcpyAsync(h + 24 * n, o_tok, n * 4, hipMemcpyDeviceToHost, st_));
   ZASR_HIP_CHECK(hipMemcpyAsync(h + 28 * n, o_fr, n * 4, hipMemcpyDeviceToHost, st_));
   ZASR_HIP_CHECK(hipMemcpyAsync(h + 32 * n, o_cnt, (size_t)S * 4, hipMemcpyDeviceToHost, st_));
+  if (job.check_finite) {
+    // f16x3: the encoder output this search read must be finite (fp16 range guard)
+    int* d_bad = ws<int>("so_nonfinite", 1);
+    launch_nonfinite_check(d_enc, (long)enc_off_all[S_all] * D, d_bad, st_);
+    ZASR_HIP_CHECK(hipMemcpyAsync(h + 32 * n + 4 * (size_t)S, d_bad, 4, hipMemcpyDeviceToHost, st_));
+  }
   ZASR_HIP_CHECK(hipEventRecord(part_ev_[kMaxEnc + 4 + set], st_));
 }
 
@@ -1721,6 +1736,9 @@ std::vector<TokenResult> Engine::collect_search(SearchJob& job) {
   const int* h_tok = reinterpret_cast<const int*>(h + 24 * n);
   const int* h_fr = reinterpret_cast<const int*>(h + 28 * n);
   const int* h_cnt = reinterpret_cast<const int*>(h + 32 * n);
+  if (job.check_finite && h_cnt[S] != 0)
+    throw std::runtime_error("precision f16x3: non-finite encoder output (an activation exceeded "
+                             "the fp16 range of the split operands); decode with bf16x6 or fp32");
   if (job.stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
     const int Tmax = job.Tmax;
     std::vector<unsigned long long> hs((size_t)Tmax * 16);

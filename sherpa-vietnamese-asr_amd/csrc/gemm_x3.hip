@@ -61,7 +61,8 @@ __device__ __forceinline__ float x3_act(float v) {
 // hi*hi into one accumulator and hi*lo + lo*hi into a second, combined in the epilogue.
 template <int BM, int BN, int WAVES_M, int WAVES_N, int ALOAD, int EPI, bool DEEP, int NP,
           int BK = (NP == 2 ? 32 : 16), int FMT = 0>
-__global__ __launch_bounds__(64 * WAVES_M* WAVES_N, FMT == 1 ? 2 : 1) void gemm_x3_kernel(GemmParams p,
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N,
+                             FMT == 1 && WAVES_M * WAVES_N <= 4 ? 2 : 1) void gemm_x3_kernel(GemmParams p,
                                                                        const __bf16* Bw, long blo,
                                                                        int tiles_n, int tiles_m) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;

@@ -375,6 +375,8 @@ struct JoinerPackedArgs {
   long j_plane = 0, w_plane = 0;
 };
 void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st);
+// *flag (device int) = 1 if any of the n floats of x is not finite, else 0
+void launch_nonfinite_check(const float* x, long n, int* flag, hipStream_t st);
 // rows the packed J buffer must hold for M joiner rows
 inline long joiner_packed_rows(long M) { return (M + 63) / 64 * 64; }
 void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st);

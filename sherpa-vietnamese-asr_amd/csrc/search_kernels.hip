@@ -433,17 +433,20 @@ __global__ __launch_bounds__(256) void joiner_kernel(JoinerArgs j) {
   }
 }
 
-template <int NP>
+template <int NP, int FMT = 0>
 void launch_joiner_split(const JoinerArgs& j, hipStream_t st);
 
 void launch_joiner(const JoinerArgs& j, hipStream_t st) {
   if (j.M <= 0) return;
   if (j.Wx != nullptr) {  // split-bf16 modes (defined below)
-    ZASR_REQUIRE(j.pieces == 2 || j.pieces == 3, "joiner: pieces must be 2 or 3");
+    ZASR_REQUIRE(j.pieces == 2 || j.pieces == 3 || j.pieces == kPiecesF16,
+                 "joiner: pieces must be 2, 3 or kPiecesF16");
     if (j.pieces == 2)
       launch_joiner_split<2>(j, st);
-    else
+    else if (j.pieces == 3)
       launch_joiner_split<3>(j, st);
+    else
+      launch_joiner_split<2, 1>(j, st);
     return;
   }
   ZASR_REQUIRE(j.D % 32 == 0 && j.D <= 512, "joiner_dim must be a multiple of 32, <= 512");
@@ -517,7 +520,7 @@ void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
 // k16 step) accumulate in f32 -- near-f32 / f32-quality logits at bf16 MFMA rates.  Same
 // block / wave / split-K structure as joiner_bf16_kernel.
 // --------------------------------------------------------------------------------------
-template <int NK, int NP>
+template <int NK, int NP, int FMT = 0>
 __global__ __launch_bounds__(256) void joiner_split_kernel(JoinerArgs j) {
   __shared__ float red[3 * 16 * 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -541,17 +544,25 @@ __global__ __launch_bounds__(256) void joiner_split_kernel(JoinerArgs j) {
 #pragma unroll
     for (int t = 0; t < NP; ++t) b[t][q] = *reinterpret_cast<const bf16x8*>(brow + t * blo + 16 * q);
   }
-  f32x16 acc;
+  f32x16 acc, accl;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = accl[r] = 0.f;
 #pragma unroll
   for (int q = 0; q < NK; ++q) {
     const float v[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w, x1[q].x, x1[q].y, x1[q].z, x1[q].w};
     bf16x8 ap[NP], bp[NP];
-    split_f8<NP>(v, ap);
+    split_fx<FMT, NP>(v, ap);
 #pragma unroll
     for (int t = 0; t < NP; ++t) bp[t] = b[t][q];
-    acc = mfma_split<NP>(ap, bp, acc);
+    if constexpr (FMT == 1) {
+      mfma_h3(ap, bp, acc, accl);
+    } else {
+      acc = mfma_split<NP>(ap, bp, acc);
+    }
+  }
+  if constexpr (FMT == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += accl[r] * kF16LoInv;
   }
   splitk_reduce(acc, red);
   if (wid != 0 || !nv) return;
@@ -563,14 +574,14 @@ __global__ __launch_bounds__(256) void joiner_split_kernel(JoinerArgs j) {
   }
 }
 
-template <int NP>
+template <int NP, int FMT>
 void launch_joiner_split(const JoinerArgs& j, hipStream_t st) {
   dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
   switch (j.D) {
-    case 64: hipLaunchKernelGGL((joiner_split_kernel<1, NP>), grid, dim3(256), 0, st, j); break;
-    case 128: hipLaunchKernelGGL((joiner_split_kernel<2, NP>), grid, dim3(256), 0, st, j); break;
-    case 256: hipLaunchKernelGGL((joiner_split_kernel<4, NP>), grid, dim3(256), 0, st, j); break;
-    case 512: hipLaunchKernelGGL((joiner_split_kernel<8, NP>), grid, dim3(256), 0, st, j); break;
+    case 64: hipLaunchKernelGGL((joiner_split_kernel<1, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 128: hipLaunchKernelGGL((joiner_split_kernel<2, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 256: hipLaunchKernelGGL((joiner_split_kernel<4, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 512: hipLaunchKernelGGL((joiner_split_kernel<8, NP, FMT>), grid, dim3(256), 0, st, j); break;
     default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
   }
 }
@@ -840,6 +851,28 @@ __device__ __forceinline__ void store_j4(const DecTable& dt, long row, int k, fl
     *reinterpret_cast<float4*>(reinterpret_cast<float*>(dt.J) + row * dt.D + k) =
         make_float4(tanhf(e.x + d.x), tanhf(e.y + d.y), tanhf(e.z + d.z), tanhf(e.w + d.w));
   }
+}
+
+// f16x3 guard: *flag = 1 when any of the n floats is not finite (an activation beyond the
+// fp16 range became inf in a split and spread); read back with the search results
+__global__ void nonfinite_kernel(const float4* __restrict__ x, long n4, int* __restrict__ flag) {
+  bool bad = false;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = x[i];
+    bad |= !(__builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z) &&
+             __builtin_isfinite(v.w));
+  }
+  if (bad) *flag = 1;
+}
+
+void launch_nonfinite_check(const float* x, long n, int* flag, hipStream_t st) {
+  ZASR_REQUIRE(n % 4 == 0, "nonfinite check: n must be a multiple of 4");
+  ZASR_HIP_CHECK(hipMemsetAsync(flag, 0, sizeof(int), st));
+  if (n <= 0) return;
+  const long n4 = n / 4;
+  const int blocks = (int)std::min<long>(cdivl(n4, 256), 2048);
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(blocks), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(x), n4, flag);
 }
 
 // J of frame 0, slot 0 of stream s: context (0, 0) = table row 0

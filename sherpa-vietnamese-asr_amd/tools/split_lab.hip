@@ -73,6 +73,43 @@ int main(int argc, char** argv) {
     p.K = s.K;
     p.alpha = 1.f;
     p.max_M = s.M;
+    // f16x3 tile variants (all bit-identical: same 16-deep slabs in the same MFMA order
+    // per output; BK = 32 changes nothing in the per-output order either)
+    if (getenv("SPLIT_LAB_TILES")) {
+      split_to_bf16(dW, dWx, (long)nw, kPiecesF16, 0);
+      struct V {
+        const char* name;
+        void (*fn)(const GemmParams&, const __bf16*, long, hipStream_t);
+      };
+#define ZV(BM, BN, WM, WN, BK) \
+  {#BM "x" #BN " w" #WM "x" #WN " bk" #BK, [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
+     if (q.N % BN) return; \
+     launch_x3_t<BM, BN, WM, WN, ALOAD_DENSE, EPI_NONE, 2, BK, 1>(q, b, lo, st); }}
+      const V vars[] = {ZV(128, 128, 2, 2, 16), ZV(128, 128, 2, 2, 32), ZV(256, 128, 4, 2, 16),
+                        ZV(128, 256, 2, 4, 16), ZV(128, 64, 2, 2, 16), ZV(128, 64, 2, 2, 32),
+                        ZV(256, 64, 4, 2, 16), ZV(64, 128, 2, 2, 32), ZV(64, 128, 2, 2, 16),
+                        ZV(64, 64, 2, 2, 16), ZV(128, 32, 4, 1, 16)};
+#undef ZV
+      for (const V& v : vars) {
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        for (int w = 0; w < 2; ++w) v.fn(p, dWx, (long)nw, 0);
+        hipEventRecord(e0, 0);
+        for (int it = 0; it < 10; ++it) v.fn(p, dWx, (long)nw, 0);
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, e0, e1);
+        const double us = ms * 100.0;
+        const double f32flops = 2.0 * s.M * s.K * s.N;
+        printf("%-14s f16x3 %-20s %8.1f us  mfma %.3f of 2.5 PF\n", s.name, v.name, us,
+               3 * f32flops / us * 1e-6 / 2500.0);
+        fflush(stdout);
+      }
+      hipFree(dA); hipFree(dW); hipFree(dWx); hipFree(db); hipFree(dC); hipFree(dC0);
+      continue;
+    }
     for (int pieces : {3, kPiecesF16}) {
       split_to_bf16(dW, dWx, (long)nw, pieces, 0);
       auto run = [&]() {

@@ -60,7 +60,7 @@ CONTEXT_SIZE = 2
 # the precision create_recognizer (and zasr.offline) use unless told otherwise: the
 # token-exact split-bf16 mode (exact-f32 quality products), the mode
 # bench.py reports as parity_mode and times the drop-in stage in; ZASR_PRECISION overrides
-DEFAULT_PRECISION = "bf16x6"
+DEFAULT_PRECISION = "f16x3"
 
 _recognizer_cache: Dict[tuple, dict] = {}
 _cache_lock = threading.Lock()

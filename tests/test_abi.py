@@ -70,3 +70,20 @@ def test_create_recognizer_missing_files(tmp_path):
     import zasr.asr_engine as ae
     with pytest.raises(FileNotFoundError):
         ae.create_recognizer(str(tmp_path))
+
+
+def test_calibration_asks_the_kfd_topology(tmp_path):
+    """zasr.calibration names GPUs from the driver's KFD topology (no HIP call): only gfx950
+    nodes count as ready; CPU nodes (no SIMDs) are skipped (ADVICE/VERDICT r03: the status
+    must not label every render node an MI355X)."""
+    import zasr.calibration as cal
+    for node, props in {"0": "cpu_cores_count 64\nsimd_count 0\n",
+                        "1": "simd_count 1024\nsimd_per_cu 4\ngfx_target_version 90500\n",
+                        "2": "simd_count 1216\nsimd_per_cu 4\ngfx_target_version 90402\n"}.items():
+        d = tmp_path / node
+        d.mkdir()
+        (d / "properties").write_text(props)
+    gpus = cal.detect_gpus(str(tmp_path))
+    assert [(g["node"], g["gfx"], g["supported"], g["compute_units"]) for g in gpus] == \
+        [("1", "gfx950", True, 256), ("2", "gfx942", False, 304)]
+    assert cal.detect_gpus(str(tmp_path / "missing")) == []

@@ -208,7 +208,8 @@ def test_s_encoder_matches_oracle(s_case):
     from zasr.binding import Recognizer
     feats = [fbank(_speech(s, 1300 + i)) for i, s in enumerate((17.0, 4.2, 29.0))]
     refs = [s_case["orc"].encoder(f) for f in feats]
-    for prec, tol in (("fp32", 2e-3), ("bf16x6", 2e-3), ("bf16x3", 2e-3), ("bf16", 0.05)):
+    for prec, tol in (("fp32", 2e-3), ("bf16x6", 2e-3), ("f16x3", 2e-3), ("bf16x3", 2e-3),
+                      ("bf16", 0.05)):
         rec = Recognizer(s_case["path"], "greedy_search", 1, precision=prec)
         got = rec.encode_features(feats)
         rec.close()

@@ -179,8 +179,10 @@ def test_dropin_words_from_device_search_match_reference(need_gpu, path):
 
 
 # ------------------------------------------------------------------ end to end
-def test_end_to_end_tiny_matches_oracle(tiny):
-    """fbank -> encoder -> modified beam search (beam 4) + hotwords, GPU vs oracle pipeline."""
+@pytest.mark.parametrize("prec", ["fp32", "f16x3", "bf16x6"])
+def test_end_to_end_tiny_matches_oracle(tiny, prec):
+    """fbank -> encoder -> modified beam search (beam 4) + hotwords, GPU vs oracle pipeline
+    (the tiny model's joiner dim takes the unpacked split joiner in the split modes)."""
     from oracle.fbank import fbank
     from oracle.search import HotwordGraph, beam_search
     from oracle.zipformer import ZipformerOracle
@@ -188,7 +190,8 @@ def test_end_to_end_tiny_matches_oracle(tiny):
     cfg, w, path, _ = tiny
     phrases = [[5, 9, 11], [17, 3], [40]]
     scores = [2.0, 1.5, 1.0]
-    rec = Recognizer(path, "modified_beam_search", 4, hotwords=phrases, hotword_scores=scores)
+    rec = Recognizer(path, "modified_beam_search", 4, hotwords=phrases, hotword_scores=scores,
+                     precision=prec)
     orc = ZipformerOracle(cfg, w)
     chunks = [_speech(s, 40 + i) for i, s in enumerate((2.5, 6.0, 0.04, 3.3))]
     res = rec.decode(chunks)
@@ -526,3 +529,32 @@ def test_tuned_gemm_tiles_bit_identical(need_gpu, tmp_path):
         outs.append(np.load(out))
     assert outs[0].shape == outs[1].shape and outs[0].shape[0] > 9000
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+# ------------------------------------------------------------------ f16x3 range guards
+def test_f16x3_range_guards(need_gpu, tmp_path):
+    """f16x3 carries operands as fp16 pieces: a weight at or beyond 65504 is refused when the
+    model loads, and an activation that overflows the pieces (here: layer 0's feed_forward1
+    output scaled so the residual stream reaches ~1e5) makes the decode fail loudly with the
+    non-finite guard instead of returning tokens; fp32 decodes the same model."""
+    from model_fixtures import tiny_model
+    from zasr.binding import Recognizer, ZasrError
+    from zasr.model import save_model_dir, synth_tokens
+    cfg, w, _ = tiny_model()
+    big = dict(w)
+    name = next(k for k in w if k.endswith("layers.0.feed_forward1.out_proj.weight"))
+    big[name] = (w[name] * (2e5 / max(1e-9, float(np.abs(w[name]).max())))).astype(np.float32)
+    p1 = str(tmp_path / "big_weight")
+    save_model_dir(p1, cfg, big, synth_tokens(cfg.vocab_size))
+    with pytest.raises(ZasrError, match="fp16 range"):
+        Recognizer(p1, "greedy_search", 1, precision="f16x3")
+    hot = dict(w)
+    hot[name] = (w[name] * (3e4 / max(1e-9, float(np.abs(w[name]).max())))).astype(np.float32)
+    p2 = str(tmp_path / "hot_activations")
+    save_model_dir(p2, cfg, hot, synth_tokens(cfg.vocab_size))
+    chunks = [_speech(4.0, 3100)]
+    Recognizer(p2, "greedy_search", 1, precision="fp32").decode(chunks)
+    rec = Recognizer(p2, "greedy_search", 1, precision="f16x3")
+    with pytest.raises(ZasrError, match="non-finite"):
+        rec.decode(chunks)
+    rec.close()
