@@ -75,6 +75,7 @@ def parse_args(argv=None):
                          "quality; bf16x6: six bf16 piece products), with the count of the "
                          "benched chunks whose tokens equal an exact-f32 (fp32 mode) decode of "
                          "the same hour")
+    ap.add_argument("--parity-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-parity-check", action="store_true",
                     help="skip the fp32 decode of the hour that parity_mode's "
                          "chunks_identical_to_fp32 is measured against")
@@ -1183,8 +1184,12 @@ def bench_dropin(args):
     hotwords = load_hotwords(hw_path, cfg.vocab_size) if hw_path else ([], [])
     mdir = os.path.join(tempfile.gettempdir(), f"zasr_dropin_{args.model}_{os.getpid()}")
     save_model_dir(mdir, cfg, synth_weights(cfg, WEIGHT_SEED), synth_tokens(cfg.vocab_size))
+    # the drop-in's own default precision (zasr.asr_engine.DEFAULT_PRECISION: what install()
+    # users get) unless --precision is given explicitly
+    prec = args.precision if any(a.startswith("--precision") for a in sys.argv[1:]) \
+        else ae.DEFAULT_PRECISION
     rec = ae.create_recognizer(mdir, 4, max_active_paths=beam, hotwords=hotwords,
-                               device_id=local, precision=args.precision)
+                               device_id=local, precision=prec)
     concat = synth_speech(args.audio_sec, AUDIO_SEED + rank)
     omap = [(0, 0, len(concat))]  # no VAD cut: the identity offset map (:2181)
     info = {}
@@ -1257,7 +1262,7 @@ def bench_dropin(args):
                 "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": args.precision,
+                "dtype": prec,
                 "data": "synthetic (seeded speech-like audio, random-init Zipformer weights)",
                 "config": {"workload": f"{args.model} modified_beam_search beam {beam}"
                                        f"{' + hotwords' if hotwords[0] else ''} through "
@@ -1279,10 +1284,54 @@ def bench_dropin(args):
 
 
 # ------------------------------------------------------------------ main
+def run_parity_child():
+    """The parity-mode line measured in a CHILD process (this process has initialised the
+    GPU: the child is started, never exec'd into).  A second engine in this process would put
+    its streams on hardware queues the headline engine already holds (streams beyond
+    GPU_MAX_HW_QUEUES share queues in creation order and serialise): the mode
+    measured 26k xRT beside the headline engine vs its own pipeline's rate alone."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--parity-child"] + sys.argv[1:]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
+    for line in r.stdout.splitlines():
+        if line.startswith("PARITY_JSON "):
+            return json.loads(line[len("PARITY_JSON "):])
+    sys.stderr.write(r.stdout[-2000:] + r.stderr[-4000:])
+    raise RuntimeError(f"parity-mode child failed (rc {r.returncode})")
+
+
+def parity_child_main(args):
+    """--parity-child: the bench workload (same chunks, same weights) in the parity precision
+    only; prints one PARITY_JSON line for the parent (run_parity_child)."""
+    import torch
+    from zasr.model import PRESETS, chunk_flops, save_model_dir, synth_tokens, synth_weights
+    cfg = PRESETS[args.model]()
+    beam = 1 if args.method == "greedy_search" else args.beam
+    hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
+    hotwords = load_hotwords(hw_path, cfg.vocab_size) if (hw_path and beam > 1) else None
+    chunks = make_chunks(args.audio_sec, AUDIO_SEED)
+    lens = [c.shape[0] for c in chunks]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    torch.cuda.set_device(0)
+    dev = "cuda:0"
+    mdir = os.path.join(tempfile.gettempdir(), f"zasr_parity_{args.model}_{os.getpid()}")
+    save_model_dir(mdir, cfg, synth_weights(cfg, WEIGHT_SEED), synth_tokens(cfg.vocab_size))
+    d_wav = torch.from_numpy(np.concatenate(chunks)).to(dev)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    fl_step = sum(sum(chunk_flops(cfg, n, beam).values()) for n in lens)
+    L_list = [((n + 80) // 160 - 7) // 2 for n in lens]
+    out = parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream, fl_step,
+                           L_list, None, dev)
+    out["process"] = "child of the bench process (own HIP context and hardware queues)"
+    print("PARITY_JSON " + json.dumps(out), flush=True)
+
+
 def main():
     args = parse_args()
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(launch_ranks(args))
+    if args.parity_child:
+        return parity_child_main(args)
     if args.stage == "campp":
         return bench_campp(args)
     if args.stage == "vad":
@@ -1499,10 +1548,9 @@ def main():
                    "achieved": round(fb_bytes / fb_s / 1e9, 1), "unit": "GB/s",
                    "peak": HBM_PEAK_GBS, "frac": round(fb_bytes / fb_s / 1e9 / HBM_PEAK_GBS, 4)}
     parity = None
-    if (rec is not None and args.parity_precision != "none"
+    if (rec is not None and world == 1 and args.parity_precision != "none"
             and args.parity_precision != args.precision):
-        parity = parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
-                                  fl_step, L_list, dist, dev)
+        parity = run_parity_child()
 
     if rank == 0:
         hw_tag = (f" + hotwords ({len(hotwords[0])} phrases of {os.path.basename(hw_path)})"

@@ -16,6 +16,8 @@
 //    v_mfma_f32_32x32x16_bf16 (so one lane holds 4 consecutive hidden units of one position
 //    per register group: 8-byte LDS stores), SwooshL, then O^T += W2 H^T.  Epilogue adds b2
 //    and the residual x and writes bf16.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -38,20 +40,24 @@ constexpr int kDwItems = 2 * 19 * 32;   // (segment, freq, channel pair) work it
 // staged tile: [kDwH frames][25 = 3 + 19 + 3 freq, zero columns at the edges][kDwC] bf16
 constexpr int kDwF = 25;
 
-template <bool MASKED>
-__device__ __forceinline__ void dw_item(const __bf16* __restrict__ tile, int seg, int f, int p,
+template <bool MASKED, typename T = __bf16, int C = kDwC>
+__device__ __forceinline__ void dw_item(const T* __restrict__ tile, int seg, int f, int p,
                                         const float2 (&w)[49], float2 bias, const int* sLo,
                                         const int* sHi, float2 (&acc)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = bias;
-  const __bf16* base = tile + ((seg * 8) * kDwF + f) * kDwC + 2 * p;
+  const T* base = tile + ((seg * 8) * kDwF + f) * C + 2 * p;
 #pragma unroll
   for (int rr = 0; rr < 14; ++rr) {  // staged frame seg*8 + rr <-> tap row rr - i
     float2 v[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) {  // freq tap j <-> staged column f + j
-      const bf16x2 hv = *reinterpret_cast<const bf16x2*>(base + (rr * kDwF + j) * kDwC);
-      v[j] = make_float2((float)hv[0], (float)hv[1]);
+      if constexpr (std::is_same<T, float>::value) {
+        v[j] = *reinterpret_cast<const float2*>(base + (rr * kDwF + j) * C);
+      } else {
+        const bf16x2 hv = *reinterpret_cast<const bf16x2*>(base + (rr * kDwF + j) * C);
+        v[j] = make_float2((float)hv[0], (float)hv[1]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -72,20 +78,29 @@ __device__ __forceinline__ void dw_item(const __bf16* __restrict__ tile, int seg
   }
 }
 
+// T = __bf16 (the bf16 mode, C = 64 channels per block) or float (the f32 / split modes,
+// C = 32: the same 16-byte pieces per staged row, 70 KB of LDS); the f32 variant replaces a
+// one-output-per-thread kernel that re-read every staged value 49 times (7 ms per hour).
+template <typename T = __bf16, int C = kDwC>
 __global__ __launch_bounds__(256) void convnext_dw_kernel(
-    const __bf16* __restrict__ x, const int* __restrict__ L_off, const int* __restrict__ L_map,
+    const T* __restrict__ x, const int* __restrict__ L_off, const int* __restrict__ L_map,
     int total_rows, const float* __restrict__ dw_w, const float* __restrict__ dw_b,
-    __bf16* __restrict__ y) {
-  __shared__ __attribute__((aligned(16))) __bf16 tile[kDwH * kDwF * kDwC];
+    T* __restrict__ y) {
+  constexpr int PAIRS = C / 2;          // channel pairs per block
+  constexpr int EPP = 16 / sizeof(T);   // elements per 16-byte piece
+  constexpr int PPR = C / EPP;          // pieces per staged (frame, freq) row
+  static_assert(PPR == 8, "eight 16-byte pieces per row");
+  typedef T T8 __attribute__((ext_vector_type(EPP)));
+  __shared__ __attribute__((aligned(16))) T tile[kDwH * kDwF * C];
   __shared__ int sLo[kDwT], sHi[kDwT], sMasked;
   const int t0 = blockIdx.x * kDwT;
-  const int c0 = blockIdx.y * kDwC;
+  const int c0 = blockIdx.y * C;
   const int tid = threadIdx.x;
   if (tid == 0) sMasked = 0;
   // every global load of the block is issued before the first wait: this thread's channel
   // pair weights and bias, the sequence bounds of the tile frames (L_map -> L_off) and the
   // staged input -- one memory round trip instead of three
-  const int p = tid & 31;  // channel pair c0 + 2p, c0 + 2p + 1 (fixed per thread)
+  const int p = tid & (PAIRS - 1);  // channel pair c0 + 2p, c0 + 2p + 1 (fixed per thread)
   float2 w[49];
 #pragma unroll
   for (int k = 0; k < 49; ++k)
@@ -101,15 +116,15 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
   for (int e = tid; e < kDwH * 6 * 8; e += 256) {
     const int q = e & 7, cf = (e >> 3) % 6, rr = (e >> 3) / 6;
     const int fcol = cf < 3 ? cf : 19 + cf;
-    bf16x8 z;
+    T8 z;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) z[t] = (__bf16)0.f;
-    *reinterpret_cast<bf16x8*>(tile + (rr * kDwF + fcol) * kDwC + 8 * q) = z;
+    for (int t = 0; t < EPP; ++t) z[t] = (T)0.f;
+    *reinterpret_cast<T8*>(tile + (rr * kDwF + fcol) * C + EPP * q) = z;
   }
-  // ---- stage frames t0-3 .. t0+18, channels c0..c0+63: 22 x 19 x 8 16-byte pieces ----
+  // ---- stage frames t0-3 .. t0+18, channels c0..c0+C-1: 22 x 19 x 8 16-byte pieces ----
   constexpr int kPieces = kDwH * 19 * 8;  // 3344
   constexpr int kIt = (kPieces + 255) / 256;
-  bf16x8 v[kIt];
+  T8 v[kIt];
 #pragma unroll
   for (int k = 0; k < kIt; ++k) {
     const int e = tid + 256 * k;
@@ -119,10 +134,10 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
     int r = t0 - 3 + rr;
     const bool ok = e < kPieces && r >= 0 && r < total_rows;
     r = r < 0 ? 0 : (r >= total_rows ? total_rows - 1 : r);
-    v[k] = *reinterpret_cast<const bf16x8*>(x + ((long)r * 19 + f) * 128 + c0 + 8 * q);
+    v[k] = *reinterpret_cast<const T8*>(x + ((long)r * 19 + f) * 128 + c0 + EPP * q);
     if (!ok) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[k][t] = (__bf16)0.f;
+      for (int t = 0; t < EPP; ++t) v[k][t] = (T)0.f;
     }
   }
 #pragma unroll
@@ -131,7 +146,7 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
     if (e < kPieces) {
       const int rf = e >> 3, q = e & 7;
       const int rr = rf / 19, f = rf - rr * 19;
-      *reinterpret_cast<bf16x8*>(tile + (rr * kDwF + 3 + f) * kDwC + 8 * q) = v[k];
+      *reinterpret_cast<T8*>(tile + (rr * kDwF + 3 + f) * C + EPP * q) = v[k];
     }
   }
   if (tid < kDwT) {
@@ -149,25 +164,37 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
   __syncthreads();
 
   const bool masked = sMasked != 0;
-  for (int it = tid; it < kDwItems; it += 256) {
-    const int q = it >> 5;  // (segment, freq)
+  constexpr int kItems = 2 * 19 * PAIRS;  // (segment, freq, channel pair) work items
+  for (int it = tid; it < kItems; it += 256) {
+    const int q = it / PAIRS;  // (segment, freq)
     const int seg = q / 19, f = q - seg * 19;
     float2 acc[8];
     if (masked)
-      dw_item<true>(tile, seg, f, p, w, bias, sLo, sHi, acc);
+      dw_item<true, T, C>(tile, seg, f, p, w, bias, sLo, sHi, acc);
     else
-      dw_item<false>(tile, seg, f, p, w, bias, sLo, sHi, acc);
+      dw_item<false, T, C>(tile, seg, f, p, w, bias, sLo, sHi, acc);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = t0 + seg * 8 + i;
       if (r < total_rows) {
-        bf16x2 o;
-        o[0] = (__bf16)acc[i].x;
-        o[1] = (__bf16)acc[i].y;
-        *reinterpret_cast<bf16x2*>(y + ((long)r * 19 + f) * 128 + c0 + 2 * p) = o;
+        if constexpr (std::is_same<T, float>::value) {
+          *reinterpret_cast<float2*>(y + ((long)r * 19 + f) * 128 + c0 + 2 * p) = acc[i];
+        } else {
+          bf16x2 o;
+          o[0] = (__bf16)acc[i].x;
+          o[1] = (__bf16)acc[i].y;
+          *reinterpret_cast<bf16x2*>(y + ((long)r * 19 + f) * 128 + c0 + 2 * p) = o;
+        }
       }
     }
   }
+}
+
+void launch_dwconv2d_tiled(const float* x, const int* L_off, const int* L_map, int total_rows,
+                           const float* w, const float* b, float* out, hipStream_t st) {
+  if (total_rows <= 0) return;
+  hipLaunchKernelGGL((convnext_dw_kernel<float, 32>), dim3(cdiv(total_rows, kDwT), 128 / 32),
+                     dim3(256), 0, st, x, L_off, L_map, total_rows, w, b, out);
 }
 
 // =====================================================================================
@@ -322,6 +349,180 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
   }
 }
 
+// =====================================================================================
+// f16x3 ConvNeXt MLP: out = x + pw2(SwooshL(pw1(y) + b1)) + b2 in f32 with every product on
+// fp16 MFMAs as hi*hi + (hi*lo + lo*hi) * 2^-11 (gemm_dev.h split_h8: f32 quality), the
+// 384-wide hidden layer never leaving the CU (the unfused f16x3 path writes and re-reads it in
+// f32: 5.8 GB per hour of audio).  Structure of convnext_mlp_kernel: 128 positions per block,
+// the hidden layer in three 128-wide slices; Y and the H slice live in LDS as (hi, lo) fp16
+// piece images (139 KB: one block per CU, one wave per SIMD -- MFMA work per wave is long
+// enough: 576 MFMAs); W1 / W2 pieces come straight from L2 in MFMA-fragment order
+// (pack_frag32_host per piece: piece t of W at wp + t * N * K).
+// =====================================================================================
+namespace {
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void mfma_h3_cx(bf16x8 wh, bf16x8 wl, bf16x8 yh, bf16x8 yl, f32x16& hi,
+                                           f32x16& lo) {
+  const f16x8 a0 = __builtin_bit_cast(f16x8, wh), a1 = __builtin_bit_cast(f16x8, wl);
+  const f16x8 b0 = __builtin_bit_cast(f16x8, yh), b1 = __builtin_bit_cast(f16x8, yl);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, hi, 0, 0, 0);
+}
+}  // namespace
+
+__global__ __launch_bounds__(256, 1) void convnext_mlp_h3_kernel(
+    const float* __restrict__ yin, const float* __restrict__ x, long npos,
+    const __bf16* __restrict__ w1, const float* __restrict__ b1, const __bf16* __restrict__ w2,
+    const float* __restrict__ b2, float* __restrict__ out) {
+  // [piece][128 positions][kMlpLd] fp16 bits (bf16 containers)
+  __shared__ __attribute__((aligned(16))) __bf16 Ys[2][kMlpM * kMlpLd];
+  __shared__ __attribute__((aligned(16))) __bf16 Hs[2][kMlpM * kMlpLd];
+  __shared__ float sB1[384];
+  constexpr long W1P = 384L * 128, W2P = 128L * 384;  // elements per packed piece image
+  const long p0 = (long)blockIdx.x * kMlpM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int col = lane & 31, half = lane >> 5;
+  // ---- Y tile: 128 positions x 128 channels f32 = 2048 groups of 8, 8 per thread ----
+  {
+    float4 v0[8], v1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = tid + 256 * k;
+      long pp = p0 + (e >> 4);
+      pp = pp < npos ? pp : npos - 1;
+      const float* src = yin + pp * 128 + 8 * (e & 15);
+      v0[k] = *reinterpret_cast<const float4*>(src);
+      v1[k] = *reinterpret_cast<const float4*>(src + 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = tid + 256 * k;
+      f16x8 hh, ll;
+      const float v[8] = {v0[k].x, v0[k].y, v0[k].z, v0[k].w, v1[k].x, v1[k].y, v1[k].z, v1[k].w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        hh[q] = (_Float16)v[q];
+        ll[q] = (_Float16)((v[q] - (float)hh[q]) * 2048.f);
+      }
+      const int o = (e >> 4) * kMlpLd + 8 * (e & 15);
+      *reinterpret_cast<f16x8*>(Ys[0] + o) = hh;
+      *reinterpret_cast<f16x8*>(Ys[1] + o) = ll;
+    }
+    for (int e = tid; e < 384; e += 256) sB1[e] = b1[e];
+  }
+  lds_barrier_cx();
+
+  f32x16 acc2[4], acc2l[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc2[t][r] = acc2l[t][r] = 0.f;
+  auto w1frag = [&](int pc, int g, int ks) {
+    return *reinterpret_cast<const bf16x8*>(w1 + pc * W1P + (((long)g * 8 + ks) * 64 + lane) * 8);
+  };
+  auto w2frag = [&](int pc, int g, int ks) {
+    return *reinterpret_cast<const bf16x8*>(w2 + pc * W2P + (((long)g * 24 + ks) * 64 + lane) * 8);
+  };
+  // one weight-fragment set live at a time (two sets + both accumulator pairs spill)
+  bf16x8 wf[8][2];
+  for (int n3 = 0; n3 < 3; ++n3) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      wf[ks][0] = w1frag(0, n3 * 4 + wid, ks);
+      wf[ks][1] = w1frag(1, n3 * 4 + wid, ks);
+    }
+    f32x16 acc1[4], acc1l[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[t][r] = acc1l[t][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int o = (t * 32 + col) * kMlpLd + ks * 16 + 8 * half;
+        mfma_h3_cx(wf[ks][0], wf[ks][1], *reinterpret_cast<const bf16x8*>(Ys[0] + o),
+                   *reinterpret_cast<const bf16x8*>(Ys[1] + o), acc1[t], acc1l[t]);
+      }
+    }
+    // this slice's W2 pieces, in flight under the SwooshL / H write
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      wf[ks][0] = w2frag(0, wid, n3 * 8 + ks);
+      wf[ks][1] = w2frag(1, wid, n3 * 8 + ks);
+    }
+    float bb[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bb[r] = sB1[n3 * 128 + wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
+    if (n3 > 0) lds_barrier_cx();  // the previous slice's pw2 is done reading Hs
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f16x4 hh, ll;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = swooshl_fast(acc1[t][4 * g + e] + acc1l[t][4 * g + e] * (1.f / 2048.f) +
+                                       bb[4 * g + e]);
+          hh[e] = (_Float16)v;
+          ll[e] = (_Float16)((v - (float)hh[e]) * 2048.f);
+        }
+        const int o = (t * 32 + col) * kMlpLd + wid * 32 + 8 * g + 4 * half;
+        *reinterpret_cast<f16x4*>(Hs[0] + o) = hh;
+        *reinterpret_cast<f16x4*>(Hs[1] + o) = ll;
+      }
+    lds_barrier_cx();
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int o = (t * 32 + col) * kMlpLd + ks * 16 + 8 * half;
+        mfma_h3_cx(wf[ks][0], wf[ks][1], *reinterpret_cast<const bf16x8*>(Hs[0] + o),
+                   *reinterpret_cast<const bf16x8*>(Hs[1] + o), acc2[t], acc2l[t]);
+      }
+    }
+  }
+
+  // ---- out = x + O + b2 (f32) ----
+  float4 xr[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      long pp = p0 + t * 32 + col;
+      pp = pp < npos ? pp : npos - 1;
+      xr[g][t] = *reinterpret_cast<const float4*>(x + pp * 128 + wid * 32 + 8 * g + 4 * half);
+    }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int ch = wid * 32 + 8 * g + 4 * half;
+    const float4 bo = *reinterpret_cast<const float4*>(b2 + ch);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const long pp = p0 + t * 32 + col;
+      const int r = 4 * g;
+      float4 o;
+      o.x = xr[g][t].x + ((acc2[t][r + 0] + acc2l[t][r + 0] * (1.f / 2048.f)) + bo.x);
+      o.y = xr[g][t].y + ((acc2[t][r + 1] + acc2l[t][r + 1] * (1.f / 2048.f)) + bo.y);
+      o.z = xr[g][t].z + ((acc2[t][r + 2] + acc2l[t][r + 2] * (1.f / 2048.f)) + bo.z);
+      o.w = xr[g][t].w + ((acc2[t][r + 3] + acc2l[t][r + 3] * (1.f / 2048.f)) + bo.w);
+      if (pp < npos) *reinterpret_cast<float4*>(out + pp * 128 + ch) = o;
+    }
+  }
+}
+
+void launch_convnext_mlp_h3(const float* y, const float* x, long npos, const void* w1p,
+                            const float* b1, const void* w2p, const float* b2, float* out,
+                            hipStream_t st) {
+  if (npos <= 0) return;
+  hipLaunchKernelGGL(convnext_mlp_h3_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
+                     y, x, npos, reinterpret_cast<const __bf16*>(w1p), b1,
+                     reinterpret_cast<const __bf16*>(w2p), b2, out);
+}
+
 void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int total_rows,
                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
                           const void* w2, const float* b2, void* ytmp, void* out,
@@ -329,8 +530,8 @@ void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int
   if (total_rows <= 0) return;
   const __bf16* xb = reinterpret_cast<const __bf16*>(x);
   __bf16* yb = reinterpret_cast<__bf16*>(ytmp);
-  hipLaunchKernelGGL(convnext_dw_kernel, dim3(cdiv(total_rows, kDwT), 128 / kDwC), dim3(256), 0,
-                     st, xb, L_off, L_map, total_rows, dw_w, dw_b, yb);
+  hipLaunchKernelGGL((convnext_dw_kernel<__bf16, kDwC>), dim3(cdiv(total_rows, kDwT), 128 / kDwC),
+                     dim3(256), 0, st, xb, L_off, L_map, total_rows, dw_w, dw_b, yb);
   const long npos = (long)total_rows * 19;
   hipLaunchKernelGGL(convnext_mlp_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
                      yb, xb, npos, reinterpret_cast<const __bf16*>(w1), b1,

@@ -480,6 +480,29 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     for (DLin* l : {&model_.conv4, &model_.conv7, &model_.pw1, &model_.pw2, &model_.out,
                     &model_.enc_proj, &model_.joiner})
       mkx(*l);
+    if (split_pieces() == kPiecesF16) {
+      // the fused f16x3 ConvNeXt MLP reads pw1 / pw2 as fp16 piece images in MFMA-fragment
+      // order (pack_frag32_host per piece, the same split as split_to_bf16)
+      for (DLin* l : {&model_.pw1, &model_.pw2}) {
+        const size_t n = (size_t)l->N * l->K;
+        std::vector<float> w(n);
+        ZASR_HIP_CHECK(hipMemcpy(w.data(), l->w, n * 4, hipMemcpyDeviceToHost));
+        std::vector<__bf16> piece(n), pk(2 * n);
+        for (int t = 0; t < 2; ++t) {
+          for (size_t i = 0; i < n; ++i) {
+            const _Float16 hi = (_Float16)w[i];
+            const _Float16 v = t == 0 ? hi : (_Float16)((w[i] - (float)hi) * 2048.f);
+            std::memcpy(&piece[i], &v, 2);
+          }
+          pack_frag32_host(piece.data(), l->N, l->K, pk.data() + t * n);
+        }
+        void* p = nullptr;
+        ZASR_HIP_CHECK(hipMalloc(&p, pk.size() * 2));
+        model_.allocations.push_back(p);
+        ZASR_HIP_CHECK(hipMemcpy(p, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+        l->wp = p;
+      }
+    }
     if (cfg.joiner_dim == 256 || cfg.joiner_dim == 512) {
       // the joiner's W pieces in MFMA-fragment order (one packed image per piece) for
       // joiner_split_packed_kernel; J is written in the same order, already split, by store_j4
@@ -1335,11 +1358,24 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       prof_end();
       float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
       prof_begin("frontend_conv");
-      launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+      static const bool dw_old = getenv("ZASR_DWCONV_OLD") != nullptr;
+      if (dw_old)
+        launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+      else
+        launch_dwconv2d_tiled(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
       prof_end();
-      float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
-      linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
-      linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
+      static const bool cx_unfused = getenv("ZASR_CONVNEXT_UNFUSED") != nullptr;
+      if (model_.pw1.wp && model_.pw2.wp && split_pieces() == kPiecesF16 && !cx_unfused) {
+        // f16x3: pw1 -> SwooshL -> pw2 + residual in one kernel, the hidden layer on chip
+        prof_begin("frontend_conv");
+        launch_convnext_mlp_h3(y3, x3, (long)mL.total * 19, model_.pw1.wp, model_.pw1.b,
+                               model_.pw2.wp, model_.pw2.b, x3, st_);
+        prof_end();
+      } else {
+        float* hcn = ws<float>("fe_h", (size_t)mL.total * 19 * 384);
+        linear(model_.pw1, y3, 128, mL.total * 19, hcn, 384, EPI_SWOOSHL);
+        linear(model_.pw2, hcn, 384, mL.total * 19, x3, 128, EPI_RESADD);
+      }
       linear(model_.out, x3, 2432, mL.total, e0, d0, EPI_NONE);
     }
   }

@@ -368,9 +368,211 @@ void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st
                      dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
 }
 
+// ---------------------------------------------------------------------------------------
+// f16x3 on the LDS-DMA pipeline (dense A, K % 32 == 0, no z-slices): every operand byte
+// reaches LDS by global_load_lds (16 B per lane, no VGPR staging, no ds_write): the f32 A
+// slab (128 rows x 32 k, rows swizzled as gemm.hip's gemm_glds_kernel: 16-byte chunk c of row
+// r at chunk c ^ ((r >> 1) & 7)) and the two fp16 piece images of W (BN rows x 32 k each,
+// chunk c of row r at c ^ ((r >> 2) & 3)); NS stages, NS - 2 slabs in flight across the raw
+// barrier.  Each wave splits its A fragments into (hi, lo) at the fragment read (VALU beside
+// the MFMAs) and issues hi*hi into one accumulator, hi*lo + lo*hi into the other.
+// 4 waves, wave tile 64 x BN/2.
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* h3_lds_t;
+
+template <int NS, int EPI, int BN>
+__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(GemmParams p,
+                                                                          const __bf16* Bw,
+                                                                          long blo, int tiles_n) {
+  constexpr int BM = 128, BK = 32;
+  constexpr int FN = BN / 64;
+  constexpr int A_BYTES = BM * BK * 4;
+  constexpr int B_BYTES = BN * BK * 2;  // one piece
+  constexpr int STAGE = A_BYTES + 2 * B_BYTES;
+  constexpr int GA = A_BYTES / 1024 / 4;
+  constexpr int GB = B_BYTES / 1024 / 4;
+  constexpr int G = GA + 2 * GB;
+  constexpr int LDE = 40;
+  constexpr int EPI_BYTES = 4 * 32 * LDE * 4;
+  constexpr int LDS_BYTES = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
+  static_assert(NS >= 2 && NS <= 3, "stages");
+  static_assert(B_BYTES % 4096 == 0, "BN must be a multiple of 64");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS_BYTES];
+
+  const float* A = p.A;
+  float* C = p.C;
+  const int M = p.M, K = p.K, lda = p.lda, N = p.N;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int m_tile = tile / tiles_n;
+  const int m0 = m_tile * BM;
+  const int n0 = (tile - m_tile * tiles_n) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nkt = K / BK;
+
+  const float* asrc[GA];
+  const __bf16* bsrc[GB];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int row = (wid * GA + g) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    const int gr = m0 + row < M ? m0 + row : M - 1;
+    asrc[g] = A + (long)gr * lda + 4 * lc;
+  }
+#pragma unroll
+  for (int g = 0; g < GB; ++g) {
+    const int row = (wid * GB + g) * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ ((row >> 2) & 3);
+    const int gn = n0 + row < N ? n0 + row : N - 1;
+    bsrc[g] = Bw + (long)gn * p.sbn + 8 * lc;
+  }
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NS) * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int g = 0; g < GA; ++g)
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[g] + k0),
+                                       (h3_lds_t)(st + (wid * GA + g) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int g = 0; g < GB; ++g)
+        __builtin_amdgcn_global_load_lds(const_cast<__bf16*>(bsrc[g] + t * blo + k0),
+                                         (h3_lds_t)(st + A_BYTES + t * B_BYTES + (wid * GB + g) * 1024),
+                                         16, 0, 0);
+  };
+
+  f32x16 acc[2][FN], accl[2][FN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = accl[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nkt) issue(s);
+  const int r32 = lane & 31, h = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    if constexpr (NS == 3) {
+      if (kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nkt) issue(kt + NS - 1);  // the stage every wave finished reading
+    const unsigned char* st = smem + (kt % NS) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 2 * ks + h;
+      bf16x8 a[2][2], b[FN][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + r32;
+        const int sw = (row >> 1) & 7;
+        const float4 x0 = *reinterpret_cast<const float4*>(st + row * 128 + (((2 * ch) ^ sw) << 4));
+        const float4 x1 = *reinterpret_cast<const float4*>(st + row * 128 + (((2 * ch + 1) ^ sw) << 4));
+        const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        split_h8(v, a[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + r32;
+        const int off = row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
+        b[j][0] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + off);
+        b[j][1] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + B_BYTES + off);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mfma_h3(a[i], b[j], acc[i][j], accl[i][j]);
+    }
+  }
+  __syncthreads();
+
+  // epilogue (gemm_x3_kernel's): fragment -> LDS -> float4 rows, side inputs clamped
+  float* sE = reinterpret_cast<float*>(smem) + wid * (32 * LDE);
+  const int c4 = lane & 7;
+  const float* aux = p.aux;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sE[((r & 3) + 8 * (r >> 2) + 4 * h) * LDE + r32] = acc[i][j][r] + accl[i][j][r] * kF16LoInv;
+      __builtin_amdgcn_wave_barrier();
+      const int col = n0 + wn * (BN / 2) + j * 32 + 4 * c4;
+      const int cc = col < N ? col : N - 4;
+      float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias) bias = *reinterpret_cast<const float4*>(p.bias + cc);
+      float4 side[4];
+      if constexpr (EPI == EPI_RESADD || EPI == EPI_MULAUX) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + wm * 64 + i * 32 + (lane >> 3) + 8 * q;
+          const int rc = row < M ? row : M - 1;
+          side[q] = EPI == EPI_RESADD
+                        ? *reinterpret_cast<const float4*>(C + (long)rc * p.ldc + cc)
+                        : *reinterpret_cast<const float4*>(aux + (long)rc * p.ldaux + cc);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = (lane >> 3) + 8 * q;
+        const int row = m0 + wm * 64 + i * 32 + rl;
+        float4 v = *reinterpret_cast<const float4*>(&sE[rl * LDE + 4 * c4]);
+        if (row < M && col < N) {
+          v.x = x3_act<EPI>(v.x + bias.x);
+          v.y = x3_act<EPI>(v.y + bias.y);
+          v.z = x3_act<EPI>(v.z + bias.z);
+          v.w = x3_act<EPI>(v.w + bias.w);
+          if constexpr (EPI == EPI_RESADD) {
+            v.x += side[q].x; v.y += side[q].y; v.z += side[q].z; v.w += side[q].w;
+          }
+          if constexpr (EPI == EPI_MULAUX) {
+            v.x *= side[q].x; v.y *= side[q].y; v.z *= side[q].z; v.w *= side[q].w;
+          }
+          *reinterpret_cast<float4*>(C + (long)row * p.ldc + col) = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+template <int NS, int EPI, int BN>
+void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
+  const int tn = cdiv(p.N, BN), tm = cdiv(p.M, 128);
+  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN>), dim3(tn * tm), dim3(256), 0, st, p, Bw,
+                     blo, tn);
+}
+
+// ZASR_H3_GLDS: 0 = the register-staged kernel only; 2 / 3 = LDS-DMA stages (A/B runs)
+int h3_glds_mode() {
+  const char* e = getenv("ZASR_H3_GLDS");
+  return e ? atoi(e) : 2;
+}
+
 // fp16 pieces (FMT 1): BK = 16 keeps two stages at 41 KB of LDS (3 blocks per CU)
 template <int ALOAD, int EPI>
 void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
+  if constexpr (ALOAD == ALOAD_DENSE) {
+    const int mode = h3_glds_mode();
+    if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
+        p.M >= 128 && p.N % 64 == 0) {
+      const bool w128 = p.N % 128 == 0;
+      if (mode == 3) {
+        if (w128) return launch_glds_h3<3, EPI, 128>(p, Bw, blo, st);
+        return launch_glds_h3<3, EPI, 64>(p, Bw, blo, st);
+      }
+      if (w128) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
+      return launch_glds_h3<2, EPI, 64>(p, Bw, blo, st);
+    }
+  }
   const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
   const int BN = (pad128 * 100 <= pad32 * 115) ? 128 : (pad64 * 100 <= pad32 * 115 ? 64 : 32);
   const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);

@@ -142,6 +142,16 @@ void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int
                           const float* dw_w, const float* dw_b, const void* w1, const float* b1,
                           const void* w2, const float* b2, void* ytmp, void* out,
                           hipStream_t st);
+// f16x3: out = x + pw2(SwooshL(pw1(y) + b1)) + b2 in f32 over npos positions ([npos][128]
+// each), the hidden layer on chip; w1p / w2p: the two fp16 pieces (hi, (w - hi) * 2^11) of
+// pw1 / pw2, each packed by pack_frag32_host, piece t at offset t * 384 * 128 elements
+void launch_convnext_mlp_h3(const float* y, const float* x, long npos, const void* w1p,
+                            const float* b1, const void* w2p, const float* b2, float* out,
+                            hipStream_t st);
+// the same depthwise 7x7 (f32) on the tiled ConvNeXt kernel (convnext_kernels.hip, 32
+// channels per block, staged values reused by up to 7 output frames); same FMA order per output
+void launch_dwconv2d_tiled(const float* x, const int* L_off, const int* L_map, int total_rows,
+                           const float* w, const float* b, float* out, hipStream_t st);
 void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
                      const float* w /*[128][49]*/, const float* b, float* out, hipStream_t st);
 

@@ -85,15 +85,30 @@ int main(int argc, char** argv) {
   {#BM "x" #BN " w" #WM "x" #WN " bk" #BK, [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
      if (q.N % BN) return; \
      launch_x3_t<BM, BN, WM, WN, ALOAD_DENSE, EPI_NONE, 2, BK, 1>(q, b, lo, st); }}
+#define ZG(NS, BN) \
+  {"glds ns" #NS " bn" #BN, [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
+     if (q.N % BN || q.K % 32) return; \
+     launch_glds_h3<NS, EPI_NONE, BN>(q, b, lo, st); }}
       const V vars[] = {ZV(128, 128, 2, 2, 16), ZV(128, 128, 2, 2, 32), ZV(256, 128, 4, 2, 16),
                         ZV(128, 256, 2, 4, 16), ZV(128, 64, 2, 2, 16), ZV(128, 64, 2, 2, 32),
                         ZV(256, 64, 4, 2, 16), ZV(64, 128, 2, 2, 32), ZV(64, 128, 2, 2, 16),
-                        ZV(64, 64, 2, 2, 16), ZV(128, 32, 4, 1, 16)};
+                        ZV(64, 64, 2, 2, 16), ZV(128, 32, 4, 1, 16), ZG(2, 128), ZG(2, 64),
+                        ZG(3, 128), ZG(3, 64)};
+#undef ZG
 #undef ZV
+      std::vector<float> ref0;
       for (const V& v : vars) {
         hipEvent_t e0, e1;
         hipEventCreate(&e0);
         hipEventCreate(&e1);
+        hipMemset(dC, 0, nc * 4);
+        v.fn(p, dWx, (long)nw, 0);
+        hipDeviceSynchronize();
+        std::vector<float> got(nc);
+        hipMemcpy(got.data(), dC, nc * 4, hipMemcpyDeviceToHost);
+        if (ref0.empty()) ref0 = got;
+        size_t ndiff = 0;
+        for (size_t i = 0; i < nc; i += 7) ndiff += got[i] != ref0[i];
         for (int w = 0; w < 2; ++w) v.fn(p, dWx, (long)nw, 0);
         hipEventRecord(e0, 0);
         for (int it = 0; it < 10; ++it) v.fn(p, dWx, (long)nw, 0);
@@ -103,8 +118,8 @@ int main(int argc, char** argv) {
         hipEventElapsedTime(&ms, e0, e1);
         const double us = ms * 100.0;
         const double f32flops = 2.0 * s.M * s.K * s.N;
-        printf("%-14s f16x3 %-20s %8.1f us  mfma %.3f of 2.5 PF\n", s.name, v.name, us,
-               3 * f32flops / us * 1e-6 / 2500.0);
+        printf("%-14s f16x3 %-20s %8.1f us  mfma %.3f of 2.5 PF  differs_from_first %zu\n", s.name,
+               v.name, us, 3 * f32flops / us * 1e-6 / 2500.0, ndiff);
         fflush(stdout);
       }
       hipFree(dA); hipFree(dW); hipFree(dWx); hipFree(db); hipFree(dC); hipFree(dC0);

@@ -192,6 +192,73 @@ def test_m_bf16_token_error_rate(m_case):
         assert v["token_error_rate"] <= 0.15, (k, v)
 
 
+# ------------------------------------------------------------------ token-exact, widened
+WIDE_CHUNKS = 12
+
+
+@pytest.fixture(scope="module")
+def m_wide(need_gpu):
+    """The first 12 planner chunks of the benched hour (bench.make_chunks: 27-35 s each), the
+    68M oracle's greedy and beam 8 + hotwords decodes of them (hotword.txt + n-grams the model
+    emits, as m_case)."""
+    import bench
+    from model_fixtures import m_model
+    from oracle.fbank import fbank
+    from oracle.search import HotwordGraph, beam_search
+    from oracle.zipformer import ZipformerOracle
+    cfg, w, path = m_model(bench.WEIGHT_SEED)
+    orc = ZipformerOracle(cfg, w)
+    chunks = bench.make_chunks(WIDE_CHUNKS * 32.0 + 40.0, bench.AUDIO_SEED)[:WIDE_CHUNKS]
+    encs = [orc.encoder(fbank(c)) for c in chunks]
+    greedy = [beam_search(e, orc.decoder, orc.joiner, 1) for e in encs]
+    phrases, scores = _hotword_phrases(cfg.vocab_size, greedy[0][0])
+    graph = HotwordGraph(phrases, scores)
+    beam8 = [beam_search(e, orc.decoder, orc.joiner, 8, graph) for e in encs]
+    return {"path": path, "chunks": chunks, "greedy": greedy, "beam8": beam8,
+            "phrases": phrases, "scores": scores}
+
+
+@pytest.mark.timeout(900)
+def test_m_token_exact_wide(m_wide):
+    """token-exactness measured on >= 12 planner chunks (>= 1.5k greedy and
+    >= 6k beam-8 tokens).  fp32, f16x3 and bf16x6 must equal the fp32 oracle token for token
+    (and f16x3 / bf16x6 the GPU fp32 mode); bf16x3 / bf16 are reported.  Writes
+    gpurun_out/token_exact_wide.json (kept under profiles/)."""
+    from zasr.binding import Recognizer
+    ref = {"greedy": m_wide["greedy"], "beam8_hotwords": m_wide["beam8"]}
+    n_tok = {k: sum(len(g[0]) for g in v) for k, v in ref.items()}
+    assert n_tok["greedy"] >= 1500 and n_tok["beam8_hotwords"] >= 6000, n_tok
+    report, toks = {}, {}
+    for prec in ("fp32", "f16x3", "bf16x6", "bf16x3", "bf16"):
+        for name, method, beam in (("greedy", "greedy_search", 1),
+                                   ("beam8_hotwords", "modified_beam_search", 8)):
+            kw = {"hotwords": m_wide["phrases"], "hotword_scores": m_wide["scores"]} if beam > 1 else {}
+            rec = Recognizer(m_wide["path"], method, beam, precision=prec, **kw)
+            res = rec.decode(m_wide["chunks"])
+            rec.close()
+            got = [r.token_ids.tolist() for r in res]
+            toks[(prec, name)] = got
+            errs = [edit_distance(g, r[0]) for g, r in zip(got, ref[name])]
+            report[f"{prec}/{name}"] = {
+                "token_error_rate": round(sum(errs) / max(1, n_tok[name]), 6),
+                "exact_chunks": f"{sum(int(e == 0) for e in errs)}/{len(errs)}",
+                "oracle_tokens": n_tok[name],
+                "identical_to_gpu_fp32": None if prec == "fp32" else
+                f"{sum(a == b for a, b in zip(got, toks[('fp32', name)]))}/{len(got)}"}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/token_exact_wide.json", "w") as f:
+        json.dump({"model": "zipformer-68m (random init, bench weights)",
+                   "chunks": [round(len(c) / 16000.0, 2) for c in m_wide["chunks"]],
+                   "reference": "fp32 oracle (numpy fbank + torch fp32 encoder + reference search)",
+                   "rates": report}, f, indent=1)
+    for prec in ("fp32", "f16x3", "bf16x6"):
+        for name in ("greedy", "beam8_hotwords"):
+            assert report[f"{prec}/{name}"]["token_error_rate"] == 0.0, report
+            if prec != "fp32":
+                assert report[f"{prec}/{name}"]["identical_to_gpu_fp32"] == \
+                    f"{WIDE_CHUNKS}/{WIDE_CHUNKS}", report
+
+
 # ------------------------------------------------------------------ Zipformer-30M
 @pytest.fixture(scope="module")
 def s_case(need_gpu):
