@@ -380,12 +380,16 @@ void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st
 // ---------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void* h3_lds_t;
 
-template <int NS, int EPI, int BN>
+template <int NS, int EPI, int BN, int WM = 2>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(GemmParams p,
                                                                           const __bf16* Bw,
                                                                           long blo, int tiles_n) {
   constexpr int BM = 128, BK = 32;
-  constexpr int FN = BN / 64;
+  // WM x WN waves: WM = 4 gives each wave all BN columns of 32 rows, so every A element is
+  // split by one wave (WM = 2: by two)
+  constexpr int WN = 4 / WM;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 32, FN = WTN / 32;
   constexpr int A_BYTES = BM * BK * 4;
   constexpr int B_BYTES = BN * BK * 2;  // one piece
   constexpr int STAGE = A_BYTES + 2 * B_BYTES;
@@ -407,7 +411,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
   const int m0 = m_tile * BM;
   const int n0 = (tile - m_tile * tiles_n) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int nkt = K / BK;
 
   const float* asrc[GA];
@@ -442,9 +446,9 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
                                          16, 0, 0);
   };
 
-  f32x16 acc[2][FN], accl[2][FN];
+  f32x16 acc[FM][FN], accl[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -468,10 +472,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = 2 * ks + h;
-      bf16x8 a[2][2], b[FN][2];
+      bf16x8 a[FM][2], b[FN][2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wm * 64 + i * 32 + r32;
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * WTM + i * 32 + r32;
         const int sw = (row >> 1) & 7;
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * 128 + (((2 * ch) ^ sw) << 4));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * 128 + (((2 * ch + 1) ^ sw) << 4));
@@ -480,13 +484,13 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int row = wn * (BN / 2) + j * 32 + r32;
+        const int row = wn * WTN + j * 32 + r32;
         const int off = row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
         b[j][0] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + off);
         b[j][1] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + B_BYTES + off);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) mfma_h3(a[i], b[j], acc[i][j], accl[i][j]);
     }
@@ -498,14 +502,14 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
   const int c4 = lane & 7;
   const float* aux = p.aux;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < FM; ++i) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         sE[((r & 3) + 8 * (r >> 2) + 4 * h) * LDE + r32] = acc[i][j][r] + accl[i][j][r] * kF16LoInv;
       __builtin_amdgcn_wave_barrier();
-      const int col = n0 + wn * (BN / 2) + j * 32 + 4 * c4;
+      const int col = n0 + wn * WTN + j * 32 + 4 * c4;
       const int cc = col < N ? col : N - 4;
       float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
       if (p.bias) bias = *reinterpret_cast<const float4*>(p.bias + cc);
@@ -513,7 +517,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
       if constexpr (EPI == EPI_RESADD || EPI == EPI_MULAUX) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int row = m0 + wm * 64 + i * 32 + (lane >> 3) + 8 * q;
+          const int row = m0 + wm * WTM + i * 32 + (lane >> 3) + 8 * q;
           const int rc = row < M ? row : M - 1;
           side[q] = EPI == EPI_RESADD
                         ? *reinterpret_cast<const float4*>(C + (long)rc * p.ldc + cc)
@@ -523,7 +527,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int rl = (lane >> 3) + 8 * q;
-        const int row = m0 + wm * 64 + i * 32 + rl;
+        const int row = m0 + wm * WTM + i * 32 + rl;
         float4 v = *reinterpret_cast<const float4*>(&sE[rl * LDE + 4 * c4]);
         if (row < M && col < N) {
           v.x = x3_act<EPI>(v.x + bias.x);
@@ -544,14 +548,15 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
   }
 }
 
-template <int NS, int EPI, int BN>
+template <int NS, int EPI, int BN, int WM = 2>
 void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.M, 128);
-  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN>), dim3(tn * tm), dim3(256), 0, st, p, Bw,
-                     blo, tn);
+  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN, WM>), dim3(tn * tm), dim3(256), 0, st, p,
+                     Bw, blo, tn);
 }
 
-// ZASR_H3_GLDS: 0 = the register-staged kernel only; 2 / 3 = LDS-DMA stages (A/B runs)
+// ZASR_H3_GLDS: 0 = the register-staged kernel only; 2 / 3 = LDS-DMA stages, 2x2 waves;
+// 4 = two stages, 4x1 waves (A/B runs)
 int h3_glds_mode() {
   const char* e = getenv("ZASR_H3_GLDS");
   return e ? atoi(e) : 2;
@@ -565,6 +570,10 @@ void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
     if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
         p.M >= 128 && p.N % 64 == 0) {
       const bool w128 = p.N % 128 == 0;
+      if (mode == 4) {  // 4x1 waves: each A fragment split by one wave
+        if (w128) return launch_glds_h3<2, EPI, 128, 4>(p, Bw, blo, st);
+        return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
+      }
       if (mode == 3) {
         if (w128) return launch_glds_h3<3, EPI, 128>(p, Bw, blo, st);
         return launch_glds_h3<3, EPI, 64>(p, Bw, blo, st);

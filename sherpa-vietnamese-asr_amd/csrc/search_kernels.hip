@@ -1538,7 +1538,11 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
                   : (((v.w - m1) - ls) + lf == vmax) ? i + 3 : 0x7fffffff;
       bq = c < bq ? c : bq;
     }
-    const int best = wave_min_i_dpp(bq);  // smallest index reaching the top value
+    // smallest index reaching the top value; a row with no match (non-finite logits, which
+    // the encoder-output guard reports after the decode) reads as blank so that no index
+    // derived from it leaves the vocabulary
+    const int bm = wave_min_i_dpp(bq);
+    const int best = bm < V ? bm : 0;
     if (lane == 0) sTok[f] = best;
     // a non-blank top-1 may be the window's emission: fetch the decoder-table row of the
     // context it would create now, under the block-wide decision below

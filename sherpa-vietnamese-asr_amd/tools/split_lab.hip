@@ -89,12 +89,15 @@ int main(int argc, char** argv) {
   {"glds ns" #NS " bn" #BN, [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
      if (q.N % BN || q.K % 32) return; \
      launch_glds_h3<NS, EPI_NONE, BN>(q, b, lo, st); }}
-      const V vars[] = {ZV(128, 128, 2, 2, 16), ZV(128, 128, 2, 2, 32), ZV(256, 128, 4, 2, 16),
-                        ZV(128, 256, 2, 4, 16), ZV(128, 64, 2, 2, 16), ZV(128, 64, 2, 2, 32),
-                        ZV(256, 64, 4, 2, 16), ZV(64, 128, 2, 2, 32), ZV(64, 128, 2, 2, 16),
-                        ZV(64, 64, 2, 2, 16), ZV(128, 32, 4, 1, 16), ZG(2, 128), ZG(2, 64),
-                        ZG(3, 128), ZG(3, 64)};
+#define ZG4(NS, BN) \
+  {"glds ns" #NS " bn" #BN " w4x1", [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
+     if (q.N % BN || q.K % 32) return; \
+     launch_glds_h3<NS, EPI_NONE, BN, 4>(q, b, lo, st); }}
+      const V vars[] = {ZV(128, 128, 2, 2, 32), ZV(128, 128, 4, 1, 32), ZV(128, 64, 2, 2, 32),
+                        ZV(128, 64, 4, 1, 32), ZG(2, 128), ZG(2, 64), ZG4(2, 128), ZG4(2, 64),
+                        ZG4(3, 64)};
 #undef ZG
+#undef ZG4
 #undef ZV
       std::vector<float> ref0;
       for (const V& v : vars) {
