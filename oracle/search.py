@@ -163,8 +163,11 @@ def log_add(a, b):
 
 def beam_search(enc_out: np.ndarray, decoder: Callable[[np.ndarray], np.ndarray],
                 joiner: Callable[[np.ndarray, np.ndarray], np.ndarray], beam: int,
-                graph: Optional[HotwordGraph] = None):
-    """enc_out float32 (T', D).  Returns (token_ids, frames, tok_logps, T', emit_logits)."""
+                graph: Optional[HotwordGraph] = None, ties: Optional[list] = None):
+    """enc_out float32 (T', D).  Returns (token_ids, frames, tok_logps, T', emit_logits).
+    `ties` (checker use): a list that receives every frame whose beam-th and (beam+1)-th
+    candidate scores are exactly equal -- there the kept set is whatever np.argpartition's
+    introselect leaves (not a stable order), i.e. the reference's result depends on it."""
     Tn = enc_out.shape[0]
     cache: Dict[Tuple[int, int], np.ndarray] = {}
 
@@ -201,6 +204,10 @@ def beam_search(enc_out: np.ndarray, decoder: Callable[[np.ndarray], np.ndarray]
         k = min(beam, flat.shape[0])
         top = np.argpartition(flat, -k)[-k:]
         top = top[np.argsort(flat[top])[::-1]]
+        if ties is not None and flat.shape[0] > k:
+            kth = flat[top[-1]]
+            if np.count_nonzero(flat == kth) > np.count_nonzero(flat[top] == kth):
+                ties.append(t)
         nxt: Dict[tuple, list] = {}
         for idx in top:
             hi, tok = int(idx // V), int(idx % V)
