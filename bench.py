@@ -79,7 +79,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-parity-check", action="store_true",
                     help="skip the fp32 decode of the hour that parity_mode's "
                          "chunks_identical_to_fp32 is measured against")
-    ap.add_argument("--parity-steps", type=int, default=5)
+    ap.add_argument("--parity-steps", type=int, default=0,
+                    help="timed steps of the parity-mode line (default: --steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5,
                     help="CPU baseline: 1 warm-up then the mean of this many repeats "
@@ -1061,7 +1062,7 @@ def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
                      hotword_scores=hotwords[1] if hotwords else None,
                      device_id=int(os.environ.get("LOCAL_RANK", "0")), precision=prec)
     n = len(lens)
-    k = max(1, args.parity_steps)
+    k = max(1, args.parity_steps or args.steps)
 
     def steps(m):
         return rec.decode_device_batches(d_wav.data_ptr(), offs * m, lens * m, [n] * m,

@@ -578,145 +578,9 @@ void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t
                      p, Bw, blo, tn);
 }
 
-// ---------------------------------------------------------------------------------------
-// f16x3 with A in registers: each of the 4 waves owns 32 rows x BN columns of a 128 x BN
-// tile, so no A element is shared between waves and A never goes through LDS: every lane
-// loads its MFMA A operand rows straight from global memory (two float4 per 16-deep step,
-// one k-tile ahead, double-buffered in registers) and splits them once into (hi, lo) for all
-// BN / 32 column fragments.  Only the two fp16 W piece images go through LDS (layout of
-// gemm_glds_h3_kernel: chunk c of row r at c ^ ((r >> 2) & 3)), two stages, staged through
-// registers: B(kt + 1) is loaded at the top of k-tile kt and written to the other stage after
-// kt's MFMAs.  Plain global loads only (no LDS-DMA): the compiler's vmcnt bookkeeping stays
-// exact (it drains to vmcnt(0) when a register load is consumed while LDS-DMA is in flight).
-// Per 16-deep step a wave splits 8 A elements per lane for 3 * BN / 32 MFMAs (the LDS-A
-// kernels: 16 per 12 MFMAs, after reading A from LDS).
-// ---------------------------------------------------------------------------------------
-template <int EPI, int BN>
-__global__ __launch_bounds__(256, 2) void gemm_ra_h3_kernel(GemmParams p, const __bf16* Bw,
-                                                            long blo, int tiles_n) {
-  constexpr int BM = 128, BK = 32;
-  constexpr int FN = BN / 32;
-  constexpr int B_BYTES = BN * BK * 2;  // one piece
-  constexpr int STAGE = 2 * B_BYTES;
-  constexpr int NB = 2 * BN * 4 / 256;  // 16-byte W chunks per thread per k-tile
-  constexpr int LDE = 40;
-  constexpr int EPI_BYTES = 4 * 32 * LDE * 4;
-  constexpr int LDS_BYTES = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
-  static_assert(NB == 2 || NB == 4, "BN: 64 or 128");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS_BYTES];
-
-  const int M = p.M, K = p.K, N = p.N;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int m_tile = tile / tiles_n;
-  const int m0 = m_tile * BM;
-  const int n0 = (tile - m_tile * tiles_n) * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int nkt = K / BK;
-
-  // this lane's A row (clamped: rows >= M are computed and never stored) and k offset
-  const int arow = m0 + wid * 32 + r32;
-  const float* ap = p.A + (long)(arow < M ? arow : M - 1) * p.lda + 8 * h;
-  // this thread's W chunks: piece t, tile row, 16-byte chunk c (8 k values)
-  const __bf16* bsrc[NB];
-  int bdst[NB];
-#pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const int q = tid + 256 * u;
-    const int t = q / (BN * 4), rem = q - t * (BN * 4);
-    const int row = rem >> 2, c = rem & 3;
-    const int gn = n0 + row < N ? n0 + row : N - 1;
-    bsrc[u] = Bw + t * blo + (long)gn * p.sbn + 8 * c;
-    bdst[u] = t * B_BYTES + row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
-  }
-  auto load_a = [&](int kt, float4 (&x)[4]) __attribute__((always_inline)) {
-    const float* q = ap + kt * BK;
-    x[0] = *reinterpret_cast<const float4*>(q);
-    x[1] = *reinterpret_cast<const float4*>(q + 4);
-    x[2] = *reinterpret_cast<const float4*>(q + 16);
-    x[3] = *reinterpret_cast<const float4*>(q + 20);
-  };
-
-  f32x16 acc[1][FN], accl[1][FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][j][r] = accl[0][j][r] = 0.f;
-
-  float4 xa[4], xb[4];
-  {
-    uint4 y[NB];
-#pragma unroll
-    for (int u = 0; u < NB; ++u) y[u] = *reinterpret_cast<const uint4*>(bsrc[u]);
-    load_a(0, xa);
-#pragma unroll
-    for (int u = 0; u < NB; ++u) *reinterpret_cast<uint4*>(smem + bdst[u]) = y[u];
-  }
-
-  // k-tile kt: B(kt) in stage kt & 1 (written before the barrier), A(kt) in `cur`
-  auto step = [&](int kt, float4 (&cur)[4], float4 (&nxt)[4]) __attribute__((always_inline)) {
-    __syncthreads();
-    const int kn = kt + 1 < nkt ? kt + 1 : nkt - 1;  // past the end: a harmless re-read
-    // pinned at the top: the scheduler would otherwise sink the loads next to their uses
-    // (the ds_write below, the next step's split) and expose their latency
-    __builtin_amdgcn_sched_barrier(0);
-    // (named registers, not an array: the array stayed a stack object here)
-    const uint4 y0 = *reinterpret_cast<const uint4*>(bsrc[0] + kn * BK);
-    const uint4 y1 = *reinterpret_cast<const uint4*>(bsrc[1] + kn * BK);
-    uint4 y2, y3;
-    if constexpr (NB == 4) {
-      y2 = *reinterpret_cast<const uint4*>(bsrc[2] + kn * BK);
-      y3 = *reinterpret_cast<const uint4*>(bsrc[3] + kn * BK);
-    }
-    load_a(kn, nxt);
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned char* st = smem + (kt & 1) * STAGE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const float4 x0 = cur[2 * ks], x1 = cur[2 * ks + 1];
-      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      bf16x8 a[2];
-      split_h8(v, a);
-      const int ch = 2 * ks + h;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int row = j * 32 + r32;
-        const int off = row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
-        bf16x8 b[2];
-        b[0] = *reinterpret_cast<const bf16x8*>(st + off);
-        b[1] = *reinterpret_cast<const bf16x8*>(st + B_BYTES + off);
-        mfma_h3(a, b, acc[0][j], accl[0][j]);
-      }
-    }
-    // the other stage was last read in kt - 1, before this step's barrier
-    __builtin_amdgcn_sched_barrier(0);
-    unsigned char* sn = smem + ((kt + 1) & 1) * STAGE;
-    *reinterpret_cast<uint4*>(sn + bdst[0]) = y0;
-    *reinterpret_cast<uint4*>(sn + bdst[1]) = y1;
-    if constexpr (NB == 4) {
-      *reinterpret_cast<uint4*>(sn + bdst[2]) = y2;
-      *reinterpret_cast<uint4*>(sn + bdst[3]) = y3;
-    }
-  };
-  // K % 64 == 0 (launch_h3 checks): an even k-tile count, both halves of the pair always run
-  for (int kt = 0; kt < nkt; kt += 2) {
-    step(kt, xa, xb);
-    step(kt + 1, xb, xa);
-  }
-  __syncthreads();
-  h3_epilogue<EPI, 1, FN>(p, reinterpret_cast<float*>(smem) + wid * (32 * LDE), acc, accl,
-                          m0 + wid * 32, n0, lane);
-}
-
-template <int EPI, int BN>
-void launch_ra_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
-  const int tn = cdiv(p.N, BN), tm = cdiv(p.M, 128);
-  hipLaunchKernelGGL((gemm_ra_h3_kernel<EPI, BN>), dim3(tn * tm), dim3(256), 0, st, p, Bw, blo,
-                     tn);
-}
-
 // ZASR_H3_GLDS: 0 = the register-staged kernel only; 2 / 3 = LDS-DMA stages, 2x2 waves;
-// 4 = two stages, 4x1 waves; 5 = A in registers (gemm_ra_h3_kernel) (A/B runs)
+// 4 = two stages, 4x1 waves (A/B runs; the register-A and deep-ring variants measured in
+// round 4 are gone)
 int h3_glds_mode() {
   const char* e = getenv("ZASR_H3_GLDS");
   return e ? atoi(e) : 2;
@@ -730,20 +594,15 @@ void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
     if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
         p.M >= 128 && p.N % 64 == 0) {
       const bool w128 = p.N % 128 == 0;
-      if (mode == 5 && p.K % 64 == 0) {
-        if (w128) return launch_ra_h3<EPI, 128>(p, Bw, blo, st);
-        return launch_ra_h3<EPI, 64>(p, Bw, blo, st);
-      }
-      if (mode == 4) {  // 4x1 waves: each A fragment split by one wave
-        if (w128) return launch_glds_h3<2, EPI, 128, 4>(p, Bw, blo, st);
-        return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
-      }
+      if (mode == 4 && w128) return launch_glds_h3<2, EPI, 128, 4>(p, Bw, blo, st);
       if (mode == 3) {
         if (w128) return launch_glds_h3<3, EPI, 128>(p, Bw, blo, st);
         return launch_glds_h3<3, EPI, 64>(p, Bw, blo, st);
       }
+      // N % 128 != 0: the 64-wide tile with 4 x 1 waves (split_lab_tiles_v4: 0.22-0.26 vs
+      // 0.21-0.24 of the 2 x 2 layout on the same shapes)
       if (w128) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
-      return launch_glds_h3<2, EPI, 64>(p, Bw, blo, st);
+      return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
     }
   }
   const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
