@@ -96,6 +96,11 @@ def parse_args(argv=None):
                          "share of the chunks (zasr.shard.lpt_partition) and the results are "
                          "gathered to every rank in chunk order (host object gather) inside the "
                          "timed region; value = that hour x steps / max-over-ranks time")
+    ap.add_argument("--proxy-ranks", type=int, default=0,
+                    help="single-GPU proxy of --shard-plan at N ranks (implies --shard-plan, "
+                         "world 1 only): decode the largest of the N LPT shares; value = the "
+                         "hour x steps / that share's time, the strong-scaling ceiling of N "
+                         "ranks before the gather (DESIGN.md §9)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="steps as separate decode_device calls (no cross-batch overlap)")
     ap.add_argument("--shape-table", action="store_true",
@@ -132,7 +137,10 @@ def parse_args(argv=None):
     ap.add_argument("--campp-batch", type=int, default=4096,
                     help="CAM++ windows per launch group (the reference batches 32 on CPU; "
                          "measured 512 -> 6000: 167 -> 123 ms per hour, profiles/r02/campp_batch)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.proxy_ranks > 1:
+        args.shard_plan = True
+    return args
 
 
 # ------------------------------------------------------------------ launcher
@@ -156,6 +164,16 @@ def launch_ranks(args) -> int:
 
 
 # ------------------------------------------------------------------ workload
+def shard_share(lens, world, rank, proxy_ranks=0):
+    """This rank's chunk indices under --shard-plan (zasr.shard.lpt_partition); with
+    --proxy-ranks N on one GPU, the largest (critical) of the N shares."""
+    from zasr.shard import lpt_partition
+    if proxy_ranks > 1 and world == 1:
+        parts = lpt_partition(lens, proxy_ranks)
+        return max(parts, key=lambda ix: sum(lens[i] for i in ix))
+    return lpt_partition(lens, world)[rank]
+
+
 def make_chunks(audio_sec: float, seed: int):
     """`audio_sec` of seeded synthetic speech cut by the reference planner (silence-aligned
     ~30 s boundaries, 3 s overlap; zasr/plan.py restates core/asr_engine.py:2137-2161).  The
@@ -896,8 +914,7 @@ def bench_rover(args):
     offs = np.cumsum([0] + lens[:-1]).tolist()
     mine = None
     if args.shard_plan:
-        from zasr.shard import lpt_partition
-        mine = lpt_partition(lens, world)[rank]
+        mine = shard_share(lens, world, rank, args.proxy_ranks)
     hw_path = (DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file) or ""
     phrases = []
     if hw_path:
@@ -944,7 +961,8 @@ def bench_rover(args):
     def steps(k):
         r = rover_device_many(recs[0], recs[1], recds[0], recds[1], d_wav.data_ptr(), offs, lens,
                               k, beam, phrases, args.rover_sub_batches,
-                              args.rover_passes_per_call, mine=mine)[-1]
+                              args.rover_passes_per_call, mine=mine,
+                              gather=not (args.proxy_ranks > 1 and world == 1))[-1]
         last.update(words=len(r[0]), disagree_blocks=sum(r[1]), tokens_a=r[2], tokens_b=r[3])
 
     if args.warmup:
@@ -993,6 +1011,7 @@ def bench_rover(args):
                            "tokens_30m": last["tokens_a"], "tokens_68m": last["tokens_b"],
                            "decode_alone_ms": alone,
                            "shard_chunks_this_rank": len(mine) if mine is not None else None,
+                           "proxy_ranks": args.proxy_ranks or None,
                            "parallelism": (f"dp{world} (one hour for the job: each rank decodes "
                                            f"and votes its LPT share of the chunks, the voted "
                                            f"chunks gathered to every rank in chunk order by a "
@@ -1016,7 +1035,7 @@ def bench_rover(args):
 
 
 # ------------------------------------------------------------------ strong scaling
-def gather_shards(res, mine, n_all, k, dist):
+def gather_shards(res, mine, n_all, k, dist, partial=False):
     """--shard-plan: every rank's results of its LPT share over k pipelined steps -> the last
     step's results of ALL chunks, in chunk order, on every rank (host object gather, the
     decode_sharded protocol of zasr.shard; no collective on the GPU data path).  The payload
@@ -1038,6 +1057,8 @@ def gather_shards(res, mine, n_all, k, dist):
         for s, i, d in p:
             if s == k - 1:
                 out[i] = SimpleNamespace(**d)
+    if partial:  # --proxy-ranks: only this share was decoded
+        return [r for r in out if r is not None]
     missing = [i for i, r in enumerate(out) if r is None]
     if missing:
         raise RuntimeError(f"shard gather lost chunks {missing[:5]}")
@@ -1360,8 +1381,7 @@ def main():
     # --shard-plan one hour for the whole job, each rank its LPT share of the chunks
     all_chunks = make_chunks(args.audio_sec, AUDIO_SEED + (0 if args.shard_plan else rank))
     if args.shard_plan:
-        from zasr.shard import lpt_partition
-        mine = lpt_partition([c.shape[0] for c in all_chunks], world)[rank]
+        mine = shard_share([c.shape[0] for c in all_chunks], world, rank, args.proxy_ranks)
     else:
         mine = list(range(len(all_chunks)))
     chunks = [all_chunks[i] for i in mine]
@@ -1446,7 +1466,8 @@ def main():
     res = steps(args.steps)
     sync()
     if args.shard_plan:
-        res = gather_shards(res, mine, len(all_chunks), args.steps, dist)
+        res = gather_shards(res, mine, len(all_chunks), args.steps, dist,
+                            partial=args.proxy_ranks > 1 and not dist)
     el = time.perf_counter() - t0
     if dist:
         from zasr.shard import max_over_ranks
@@ -1578,6 +1599,7 @@ def main():
                                        f"dp{world} (each rank its own hour, seed + rank; weak "
                                        f"scaling, no collective on the data path)"),
                        "shard_chunks_this_rank": len(chunks) if args.shard_plan else None,
+                       "proxy_ranks": args.proxy_ranks or None,
                        "batch_pipeline": not args.no_pipeline,
                        "single_batch_latency_ms": (round(batch_latency_ms, 3)
                                                    if batch_latency_ms is not None else None),

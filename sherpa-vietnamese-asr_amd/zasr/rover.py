@@ -156,7 +156,8 @@ def decode_chunks_rover(rec_a, rec_b, chunks, time_offsets, hotword_phrases: Seq
 
 def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths, k: int,
                       beam: int, hotword_phrases: Sequence[str] = (), sub_batches: int = 1,
-                      passes_per_call: int = 1, mine: Optional[Sequence[int]] = None):
+                      passes_per_call: int = 1, mine: Optional[Sequence[int]] = None,
+                      gather: bool = True):
     """k passes of one file's chunk plan (waveforms in HBM) through the ROVER pair on one GPU
     (BASELINE config 4): model A (primary, 30M) and model B (68M) decode every chunk
     (`zasr_decode_device`, each on its own engine streams, concurrently: two worker threads,
@@ -176,7 +177,8 @@ def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths
     the chunk indices `mine` (its zasr.shard.lpt_partition share of the SAME plan on every
     rank), the voted chunks are gathered to every rank in chunk order (a host object gather,
     zasr.shard.gather_chunks: the vote is per chunk, so the only exchange is its result) and
-    every rank merges the whole file; disagreements / tokens are this rank's."""
+    every rank merges the whole file; disagreements / tokens are this rank's.  gather=False
+    (bench.py --proxy-ranks, one process standing in for one rank): merge this share alone."""
     from concurrent.futures import ThreadPoolExecutor
 
     from zasr.asr_engine import result_words
@@ -222,7 +224,7 @@ def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths
                     chunks.append({"words": merged, "audio_start_abs": t0,
                                    "audio_end_abs": (off + ln) / 16000.0})
                     dis.append(len(d))
-                if mine is not None:
+                if mine is not None and gather:
                     chunks = gather_chunks(list(zip(mine, chunks)), n_all)
                 words, _ = merge_chunks_with_overlap(chunks)
                 out.append((words, dis, sum(int(x.token_ids.size) for x in ra),

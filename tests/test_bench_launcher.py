@@ -63,3 +63,13 @@ def test_bench_gpus8_shard_plan():
     eight = _run("--gpus", "8", "--shard-plan")
     assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
     assert eight["config"]["tokens_emitted_per_gpu"] == one["config"]["tokens_emitted_per_gpu"]
+
+
+def test_bench_proxy_ranks_single_gpu():
+    """--proxy-ranks 8 (DESIGN §9's single-GPU proxy): one process decodes the largest of the
+    8 LPT shares of the hour; strong-scaling line, the job's audio over that share's time."""
+    one = _run("--shard-plan")
+    proxy = _run("--proxy-ranks", "8")
+    assert proxy["n_gpus"] == 1 and proxy["scaling"] == "strong"
+    assert proxy["config"]["proxy_ranks"] == 8
+    assert 1 <= proxy["config"]["shard_chunks_this_rank"] < one["config"]["shard_chunks_this_rank"]
