@@ -29,4 +29,7 @@ timeout -k 10 300 python3 $R/bench.py --stage campp > $OUT/bench_campp.json 2> $
 timeout -k 10 300 python3 $R/bench.py --stage vad > $OUT/bench_vad.json 2> $OUT/bench_vad.err
 timeout -k 10 300 python3 $R/bench.py --stage dropin --steps 3 --warmup 1 --hotwords-file default > $OUT/bench_dropin.json 2> $OUT/bench_dropin.err
 timeout -k 10 300 python3 $R/bench.py --stage dropin --precision bf16 --steps 3 --warmup 1 --hotwords-file default > $OUT/bench_dropin_bf16.json 2> $OUT/bench_dropin_bf16.err
+# DESIGN §9's single-GPU proxies of the 8-rank shard plan (largest LPT share of the hour)
+timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --parity-precision none --proxy-ranks 8 > $OUT/bench_proxy8.json 2> $OUT/bench_proxy8.err
+timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwords-file default --no-cpu-baseline --proxy-ranks 8 > $OUT/bench_rover_proxy8.json 2> $OUT/bench_rover_proxy8.err
 echo done
