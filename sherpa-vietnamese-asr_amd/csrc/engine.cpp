@@ -839,7 +839,7 @@ std::string Engine::shape_key(const char* cls, int M, int K, int N, bool w16, bo
 // building blocks
 // ------------------------------------------------------------------------------------
 void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
-                    const char* cls) {
+                    const char* cls, const float* byp_orig, const float* byp_scale) {
   GemmParams p{};
   p.A = A;
   p.lda = lda;
@@ -854,6 +854,9 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
   p.K = l.K;
   p.alpha = 1.f;
   p.max_M = M;
+  ZASR_REQUIRE(byp_orig == nullptr || l.wx, "bypass epilogue: split-mode weights only");
+  p.byp_orig = byp_orig;
+  p.byp_scale = byp_scale;
   if (prof_shapes_ && prof_on_)
     prof_begin(shape_key(cls, M, l.K, l.N, l.wh != nullptr, false, false, epi));
   else
@@ -1021,9 +1024,12 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
       linear_h(fi, X, false, d, R, H, true, fi.N, EPI_SWOOSHL);
       linear_h(Ly.ff_out[k], H, true, fi.N, R, X, false, d, EPI_RESADD, bo, bs);
     } else {
+      // split modes: feed_forward2's epilogue applies bypass_mid too (fp32: launch_bypass)
+      const bool byp = k == 1 && Ly.ff_out[k].wx != nullptr;
       float* H = ws<float>("ly_hid", (size_t)R * fi.N);
       linear(fi, X, d, R, H, fi.N, EPI_SWOOSHL);
-      linear(Ly.ff_out[k], H, fi.N, R, X, d, EPI_RESADD);
+      linear(Ly.ff_out[k], H, fi.N, R, X, d, EPI_RESADD, "enc_gemm", byp ? O : nullptr,
+             byp ? Ly.bypass_mid : nullptr);
     }
   };
   auto self_attn = [&](int k) {
@@ -1170,8 +1176,8 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   self_attn(0);
   conv(0);
   ff(1);
-  // 4. bypass_mid (bf16 mode: folded into feed_forward2's epilogue)
-  if (!bf16) {
+  // 4. bypass_mid (bf16 and split modes: folded into feed_forward2's epilogue)
+  if (!bf16 && Ly.ff_out[1].wx == nullptr) {
     prof_begin("elementwise");
     launch_bypass(X, O, Ly.bypass_mid, R, d, st_);
     prof_end();

@@ -206,8 +206,10 @@ class Engine {
                      const int* d_map, const std::vector<int>& lens, const long* d_aoff,
                      const void* d_slices_nl, int maxL, const int* d_o8, int R8, bool orig_ready = false,
                      bool last_layer = true);
+  // byp_orig / byp_scale (split modes, EPI_RESADD): bypass_mid in the epilogue
   void linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
-              const char* cls = "enc_gemm");
+              const char* cls = "enc_gemm", const float* byp_orig = nullptr,
+              const float* byp_scale = nullptr);
   // bf16 mode only: A and/or C in bf16 (GEMM -> GEMM intermediates; the GEMM rounds A to
   // bf16 on load anyway, so storing it rounded changes nothing numerically)
   void linear_h(const DLin& l, const void* A, bool a_bf16, int lda, int M, void* C, bool c_bf16,

@@ -75,7 +75,7 @@ struct GemmParams {
   const GemmSlice* slices;  // nullptr => single problem with the fields above
   int num_slices;
   int max_M;                // max M over slices (grid sizing)
-  // EPI_RESADD in gemm_bf16 only (nullable): after the residual add, the layer's mid bypass
+  // EPI_RESADD in gemm_bf16 and gemm_x3 (nullable): after the residual add, the layer's mid bypass
   // C = orig + (C - orig) * scale[n] (orig row stride ldc)
   const float* byp_orig = nullptr;
   const float* byp_scale = nullptr;

@@ -46,6 +46,19 @@ __device__ __forceinline__ void split8(const float4 x0, const float4 x1, bf16x8 
 // native exp2 / log forms (common.h; ~1e-7 absolute from the libm forms, below the f32
 // rounding of the values they feed): the libm log1pf(expf()) pair made the SwooshL-epilogue
 // shapes 2-3x slower than the plain ones (profiles/r03/x3_shape_table.json)
+// EPI_RESADD with p.byp_orig: the layer's bypass_mid folded in after the residual add,
+// launch_bypass's formula (orig + (x - orig) * scale), the same f32 operations in the same
+// order, so the result is bit-identical to the separate pass
+__device__ __forceinline__ void x3_bypass(const GemmParams& p, float4& v, int row, int col) {
+  if (p.byp_orig == nullptr) return;
+  const float4 b0 = *reinterpret_cast<const float4*>(p.byp_orig + (long)row * p.ldc + col);
+  const float4 k = *reinterpret_cast<const float4*>(p.byp_scale + col);
+  v.x = b0.x + (v.x - b0.x) * k.x;
+  v.y = b0.y + (v.y - b0.y) * k.y;
+  v.z = b0.z + (v.z - b0.z) * k.z;
+  v.w = b0.w + (v.w - b0.w) * k.w;
+}
+
 template <int EPI>
 __device__ __forceinline__ float x3_act(float v) {
   if constexpr (EPI == EPI_SWOOSHL) return swooshl_fast(v);
@@ -342,6 +355,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N,
           v.w = x3_act<EPI>(v.w + bias.w);
           if constexpr (EPI == EPI_RESADD) {
             v.x += side[q].x; v.y += side[q].y; v.z += side[q].z; v.w += side[q].w;
+            x3_bypass(p, v, row, col);
           }
           if constexpr (EPI == EPI_MULAUX) {
             v.x *= side[q].x; v.y *= side[q].y; v.z *= side[q].z; v.w *= side[q].w;
@@ -429,6 +443,7 @@ __device__ __forceinline__ void h3_epilogue(const GemmParams& p, float* sE,
           v.w = x3_act<EPI>(v.w + bias.w);
           if constexpr (EPI == EPI_RESADD) {
             v.x += side[q].x; v.y += side[q].y; v.z += side[q].z; v.w += side[q].w;
+            x3_bypass(p, v, row, col);
           }
           if constexpr (EPI == EPI_MULAUX) {
             v.x *= side[q].x; v.y *= side[q].y; v.z *= side[q].z; v.w *= side[q].w;
@@ -605,6 +620,14 @@ void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
       return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
     }
   }
+  // NonlinAttention's per-sequence GEMM (z-slices; A = head 0's f32 weights, K = the
+  // sequence length): every column tile re-reads the L x L A panel, so N = 144 (d = 192) takes
+  // one 160-wide tile instead of five 32-wide ones and N = 288 three 96-wide instead of five
+  // 64-wide (4 x 1 waves, FN = 5 / 3)
+  if (p.slices && p.N > 128 && p.N <= 160)
+    return launch_x3_t<128, 160, 4, 1, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
+  if (p.slices && p.N > 256 && p.N <= 288)
+    return launch_x3_t<128, 96, 4, 1, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
   const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
   const int BN = (pad128 * 100 <= pad32 * 115) ? 128 : (pad64 * 100 <= pad32 * 115 ? 64 : 32);
   const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);
