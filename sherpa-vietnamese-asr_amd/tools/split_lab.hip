@@ -96,6 +96,7 @@ int main(int argc, char** argv) {
       // "hi only": the glds loop with one MFMA per product instead of three (timing
       // diagnostic; its output differs by design)
       const V vars[] = {ZG(2, 128), ZV(128, 128, 2, 2, 32), ZG(2, 64), ZG4(2, 64),
+                        ZV(64, 192, 2, 2, 16), ZV(64, 192, 2, 2, 32),
                         {"glds ns2 bn128 hi only", [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) {
                            if (q.N % 128 || q.K % 32) return;
                            launch_glds_h3<2, EPI_NONE, 128, 2, 1>(q, b, lo, st); }}};
