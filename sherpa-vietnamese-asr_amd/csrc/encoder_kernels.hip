@@ -612,7 +612,9 @@ __device__ __forceinline__ float4 ld4(const __bf16* p) {
 __device__ __forceinline__ void st1(float* p, float v) { *p = v; }
 __device__ __forceinline__ void st1(__bf16* p, float v) { *p = (__bf16)v; }
 
-template <int K, typename TI, typename TO>
+// GLU = false: x2 is already the GLU output, [rows][d] (split modes: the in_proj GEMM's
+// EPI_GLU epilogue applied it, with the same sigmoid_fast)
+template <int K, typename TI, typename TO, bool GLU = true>
 __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
     const TI* __restrict__ x2, const int* __restrict__ off, const int* __restrict__ map,
     int total_rows, int d, int Kr, const float* __restrict__ w, const float* __restrict__ bias,
@@ -658,8 +660,12 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
       int r = r0 - half + rr;
       r = r < 0 ? 0 : (r >= total_rows ? total_rows - 1 : r);
       const int cc = c0 + 4 * c4 < d ? c0 + 4 * c4 : d - 4;
-      a[q] = ld4(x2 + (long)r * 2 * d + cc);
-      g[q] = ld4(x2 + (long)r * 2 * d + d + cc);
+      if constexpr (GLU) {
+        a[q] = ld4(x2 + (long)r * 2 * d + cc);
+        g[q] = ld4(x2 + (long)r * 2 * d + d + cc);
+      } else {
+        a[q] = ld4(x2 + (long)r * d + cc);
+      }
     }
 #pragma unroll
     for (int q = 0; q < kIt; ++q) {
@@ -667,8 +673,10 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
       const int c4 = e & 15, rr = e >> 4;
       const int r = r0 - half + rr;
       const bool ok = e < nf4 && r >= 0 && r < total_rows && c0 + 4 * c4 < d;
-      float4 v = make_float4(a[q].x * sigmoid_fast(g[q].x), a[q].y * sigmoid_fast(g[q].y),
-                             a[q].z * sigmoid_fast(g[q].z), a[q].w * sigmoid_fast(g[q].w));
+      float4 v = a[q];
+      if constexpr (GLU)
+        v = make_float4(a[q].x * sigmoid_fast(g[q].x), a[q].y * sigmoid_fast(g[q].y),
+                        a[q].z * sigmoid_fast(g[q].z), a[q].w * sigmoid_fast(g[q].w));
       if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < nf4) *reinterpret_cast<float4*>(&tile[rr * 64 + 4 * c4]) = v;
     }
@@ -725,7 +733,7 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
   }
 }
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool GLU = true>
 static void launch_glu_dwconv1d_t(const TI* x2, const int* off, const int* map, int total_rows,
                                   int d, int K, const float* w, const float* b, TO* out,
                                   hipStream_t st) {
@@ -734,11 +742,17 @@ static void launch_glu_dwconv1d_t(const TI* x2, const int* off, const int* map, 
   dim3 grid(cdiv(total_rows, kDw1T), cdiv(d, 64));
   ZASR_REQUIRE(K >= 1 && K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
   if (K <= 7)
-    hipLaunchKernelGGL((glu_dwconv1d_kernel<7, TI, TO>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    hipLaunchKernelGGL((glu_dwconv1d_kernel<7, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
   else if (K <= 15)
-    hipLaunchKernelGGL((glu_dwconv1d_kernel<15, TI, TO>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    hipLaunchKernelGGL((glu_dwconv1d_kernel<15, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
   else
-    hipLaunchKernelGGL((glu_dwconv1d_kernel<31, TI, TO>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    hipLaunchKernelGGL((glu_dwconv1d_kernel<31, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+}
+
+void launch_dwconv1d_post_glu(const float* g, const int* off, const int* map, int total_rows,
+                              int d, int K, const float* w, const float* b, float* out,
+                              hipStream_t st) {
+  launch_glu_dwconv1d_t<float, float, false>(g, off, map, total_rows, d, K, w, b, out, st);
 }
 
 void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,

@@ -516,8 +516,26 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
       model_.joiner_packed = p;
       model_.joiner_plane = pe;
     }
+    // the conv modules' in_proj: rows interleaved (a_c, s_c) for the GLU epilogue (EPI_GLU)
+    auto glu_interleave = [&](DLin& l) {
+      const int d = l.N / 2, K = l.K;
+      std::vector<float> w((size_t)l.N * K), wi((size_t)l.N * K), b(l.N), bi(l.N);
+      ZASR_HIP_CHECK(hipMemcpy(w.data(), l.w, w.size() * 4, hipMemcpyDeviceToHost));
+      if (l.b) ZASR_HIP_CHECK(hipMemcpy(b.data(), l.b, b.size() * 4, hipMemcpyDeviceToHost));
+      for (int c = 0; c < d; ++c)
+        for (int h = 0; h < 2; ++h) {
+          std::memcpy(&wi[(size_t)(2 * c + h) * K], &w[(size_t)(h * d + c) * K], (size_t)K * 4);
+          bi[2 * c + h] = b[h * d + c];
+        }
+      float* pw = dev(wi.data(), wi.size());
+      float* pb = l.b ? dev(bi.data(), bi.size()) : nullptr;
+      l.w = pw;
+      l.b = pb;
+      l.glu = true;
+    };
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
+        for (int a = 0; a < 2; ++a) glu_interleave(L.cv_in[a]);
         for (DLin* l : {&L.attn_in, &L.na_in, &L.na_out}) mkx(*l);
         for (int a = 0; a < 2; ++a)
           for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mkx(*l);
@@ -1076,12 +1094,20 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
       linear_h(Ly.cv_out[k], dc, true, d, R, X, false, d, EPI_RESADD);
       return;
     }
-    float* g2 = ws<float>("ly_g2", (size_t)R * 2 * d);
     float* dc = ws<float>("ly_dc", (size_t)R * d);
-    linear(Ly.cv_in[k], X, d, R, g2, 2 * d, EPI_NONE);
-    prof_begin("dwconv1d");
-    launch_glu_dwconv1d(g2, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
-    prof_end();
+    if (Ly.cv_in[k].glu) {  // split modes: the GLU in the in_proj epilogue, d columns out
+      float* g = ws<float>("ly_glu", (size_t)R * d);
+      linear(Ly.cv_in[k], X, d, R, g, d, EPI_GLU);
+      prof_begin("dwconv1d");
+      launch_dwconv1d_post_glu(g, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+      prof_end();
+    } else {
+      float* g2 = ws<float>("ly_g2", (size_t)R * 2 * d);
+      linear(Ly.cv_in[k], X, d, R, g2, 2 * d, EPI_NONE);
+      prof_begin("dwconv1d");
+      launch_glu_dwconv1d(g2, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+      prof_end();
+    }
     linear(Ly.cv_out[k], dc, d, R, X, d, EPI_RESADD);
   };
   // 1. feed_forward1

@@ -23,6 +23,8 @@ enum GemmEpi : int {
   EPI_MULAUX16 = 5, // C = v * aux[m, n], aux bf16 (gemm_bf16 only)
   EPI_RELU = 6,     // C = max(v, 0)  (gemm_f32 only: CAM++ TDNN layers, BN folded in)
   EPI_GELU = 7,     // C = v * Phi(v) = 0.5 v (1 + erf(v / sqrt 2))  (gemm_f32 only: ViBERT FFN)
+  EPI_GLU = 8,      // C[m, n / 2] = v[2c] * sigmoid(v[2c + 1]) (gemm_x3 only: the conv modules'
+                    // in_proj with interleaved weight rows; N = 2 x the output width, ldc = N / 2)
 };
 
 enum GemmALoad : int {

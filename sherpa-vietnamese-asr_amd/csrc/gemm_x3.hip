@@ -360,7 +360,12 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N,
           if constexpr (EPI == EPI_MULAUX) {
             v.x *= side[q].x; v.y *= side[q].y; v.z *= side[q].z; v.w *= side[q].w;
           }
-          *reinterpret_cast<float4*>(C + (long)row * p.ldc + col) = v;
+          if constexpr (EPI == EPI_GLU) {  // columns (2c, 2c + 1) -> channel c
+            *reinterpret_cast<float2*>(C + (long)row * p.ldc + col / 2) =
+                make_float2(v.x * sigmoid_fast(v.y), v.z * sigmoid_fast(v.w));
+          } else {
+            *reinterpret_cast<float4*>(C + (long)row * p.ldc + col) = v;
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -448,7 +453,12 @@ __device__ __forceinline__ void h3_epilogue(const GemmParams& p, float* sE,
           if constexpr (EPI == EPI_MULAUX) {
             v.x *= side[q].x; v.y *= side[q].y; v.z *= side[q].z; v.w *= side[q].w;
           }
-          *reinterpret_cast<float4*>(C + (long)row * p.ldc + col) = v;
+          if constexpr (EPI == EPI_GLU) {  // columns (2c, 2c + 1) -> channel c
+            *reinterpret_cast<float2*>(C + (long)row * p.ldc + col / 2) =
+                make_float2(v.x * sigmoid_fast(v.y), v.z * sigmoid_fast(v.w));
+          } else {
+            *reinterpret_cast<float4*>(C + (long)row * p.ldc + col) = v;
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -684,6 +694,7 @@ void gemm_split_dispatch(const GemmParams& p, const __bf16* B, long b_lo, int ep
       case EPI_SWOOSHR: ZASR_X3(ALOAD_DENSE, EPI_SWOOSHR);
       case EPI_RESADD: ZASR_X3(ALOAD_DENSE, EPI_RESADD);
       case EPI_MULAUX: ZASR_X3(ALOAD_DENSE, EPI_MULAUX);
+      case EPI_GLU: ZASR_X3(ALOAD_DENSE, EPI_GLU);
       default: break;
     }
   } else if (aload == ALOAD_CONV2 && epi == EPI_SWOOSHR) {
@@ -723,6 +734,8 @@ void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload,
   if (p.max_M <= 0) return;
   ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (epi != EPI_MULAUX || p.ldaux % 4 == 0),
                "gemm_x3: N and the C / aux row strides must be multiples of 4");
+  ZASR_REQUIRE(epi != EPI_GLU || (p.ldc * 2 >= p.N && p.ldc % 2 == 0),
+               "gemm_x3: EPI_GLU writes N / 2 columns");
   ZASR_REQUIRE(p.slices != nullptr || (p.K % 8 == 0 && p.lda % 4 == 0),
                "gemm_x3: K must be a multiple of 8 and lda of 4");
   ZASR_REQUIRE(pieces == 2 || pieces == 3 || pieces == kPiecesF16,

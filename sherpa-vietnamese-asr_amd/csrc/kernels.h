@@ -168,6 +168,11 @@ void launch_bypass(float* x, const float* orig, const float* s, long rows, int d
 void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st);
 // g = x2[:, :d] * sigmoid(x2[:, d:]);  out[t][c] = SwooshR(b[c] + sum_k w[c][k] g[t+k-K/2][c]),
 // zero padding per sequence
+// the same depthwise conv + bias + SwooshR on an input that is already the GLU output
+// ([rows][d], split modes: EPI_GLU in the in_proj GEMM)
+void launch_dwconv1d_post_glu(const float* g, const int* off, const int* map, int total_rows,
+                              int d, int K, const float* w, const float* b, float* out,
+                              hipStream_t st);
 void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
                          int K, const float* w, const float* b, float* out, hipStream_t st);
 // bf16 in (the conv in_proj output) / bf16 out (the conv out_proj input), bf16 mode

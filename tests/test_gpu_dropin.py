@@ -89,6 +89,37 @@ def test_two_worker_loop_routed_equals_per_chunk(dropin_rec, feats):
     assert got == want
 
 
+def test_failed_plan_decode_falls_back_per_chunk(dropin_rec):
+    """the plan's batched decode raising (e.g. out of HBM) must not break
+    the caller -- every decode_chunk of the two-worker loop then takes the per-chunk path and
+    returns the per-chunk words."""
+    from zasr.plan import best_split, plan_chunks, silent_regions
+    from zasr.synth_audio import synth_speech
+    ae, rec = dropin_rec
+    concat = synth_speech(120.0, 57)
+    plan = plan_chunks(concat)
+    assert len(plan) >= 3
+    h = rec["handle"]
+    want = [ae.decode_chunk(rec, concat[s:e].copy(), s / 16000.0) for s, e, _ in plan]
+    d0 = h.decode
+    calls = {"batched": 0, "single": 0}
+
+    def failing(chunks, beam=0):
+        if len(chunks) > 1:  # the plan's batched pass
+            calls["batched"] += 1
+            raise RuntimeError("injected: HIP out of memory in the plan decode")
+        calls["single"] += 1
+        return d0(chunks, beam=beam)
+    h.decode = failing
+    try:
+        assert ae.register_plan_from_regions(concat, silent_regions(concat), best_split)
+        got = _loop(ae, rec, concat, plan)
+    finally:
+        del h.decode
+    assert calls["batched"] == 1 and calls["single"] == len(plan), calls
+    assert got == want
+
+
 def test_decode_sharded_real_recognizer_nccl_world1(dropin_rec):
     """zasr.shard.decode_sharded with a real Recognizer under an initialised RCCL ("nccl")
     process group of size 1: the LPT split, the decode and the all_gather_object of the word
