@@ -755,6 +755,14 @@ void launch_dwconv1d_post_glu(const float* g, const int* off, const int* map, in
   launch_glu_dwconv1d_t<float, float, false>(g, off, map, total_rows, d, K, w, b, out, st);
 }
 
+void launch_dwconv1d_post_glu_bf16(const void* g, const int* off, const int* map,
+                                   int total_rows, int d, int K, const float* w, const float* b,
+                                   void* out, hipStream_t st) {
+  launch_glu_dwconv1d_t<__bf16, __bf16, false>(reinterpret_cast<const __bf16*>(g), off, map,
+                                               total_rows, d, K, w, b,
+                                               reinterpret_cast<__bf16*>(out), st);
+}
+
 void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
                          int K, const float* w, const float* b, float* out, hipStream_t st) {
   launch_glu_dwconv1d_t(x2, off, map, total_rows, d, K, w, b, out, st);

@@ -469,6 +469,23 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
   model_.dec_proj = lin("decoder_proj", cfg.joiner_dim, D);
   model_.joiner = lin("joiner.output_linear", cfg.V, cfg.joiner_dim);
   ensure_pos_tables(2048);
+  // the conv modules' in_proj: rows interleaved (a_c, s_c) for the GLU epilogue (EPI_GLU)
+  auto glu_interleave = [&](DLin& l) {
+    const int d = l.N / 2, K = l.K;
+    std::vector<float> w((size_t)l.N * K), wi((size_t)l.N * K), b(l.N), bi(l.N);
+    ZASR_HIP_CHECK(hipMemcpy(w.data(), l.w, w.size() * 4, hipMemcpyDeviceToHost));
+    if (l.b) ZASR_HIP_CHECK(hipMemcpy(b.data(), l.b, b.size() * 4, hipMemcpyDeviceToHost));
+    for (int c = 0; c < d; ++c)
+      for (int h = 0; h < 2; ++h) {
+        std::memcpy(&wi[(size_t)(2 * c + h) * K], &w[(size_t)(h * d + c) * K], (size_t)K * 4);
+        bi[2 * c + h] = b[h * d + c];
+      }
+    float* pw = dev(wi.data(), wi.size());
+    float* pb = l.b ? dev(bi.data(), bi.size()) : nullptr;
+    l.w = pw;
+    l.b = pb;
+    l.glu = true;
+  };
   if (split_pieces() > 0) {  // split-bf16 pieces of every encoder projection weight
     auto mkx = [&](DLin& l) {
       void* p = nullptr;
@@ -516,23 +533,6 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
       model_.joiner_packed = p;
       model_.joiner_plane = pe;
     }
-    // the conv modules' in_proj: rows interleaved (a_c, s_c) for the GLU epilogue (EPI_GLU)
-    auto glu_interleave = [&](DLin& l) {
-      const int d = l.N / 2, K = l.K;
-      std::vector<float> w((size_t)l.N * K), wi((size_t)l.N * K), b(l.N), bi(l.N);
-      ZASR_HIP_CHECK(hipMemcpy(w.data(), l.w, w.size() * 4, hipMemcpyDeviceToHost));
-      if (l.b) ZASR_HIP_CHECK(hipMemcpy(b.data(), l.b, b.size() * 4, hipMemcpyDeviceToHost));
-      for (int c = 0; c < d; ++c)
-        for (int h = 0; h < 2; ++h) {
-          std::memcpy(&wi[(size_t)(2 * c + h) * K], &w[(size_t)(h * d + c) * K], (size_t)K * 4);
-          bi[2 * c + h] = b[h * d + c];
-        }
-      float* pw = dev(wi.data(), wi.size());
-      float* pb = l.b ? dev(bi.data(), bi.size()) : nullptr;
-      l.w = pw;
-      l.b = pb;
-      l.glu = true;
-    };
     for (auto& s : model_.stacks)
       for (auto& L : s.layers) {
         for (int a = 0; a < 2; ++a) glu_interleave(L.cv_in[a]);
@@ -545,6 +545,9 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   if (precision_ == 1 || precision_ == 2) {  // bf16 copies of every dense projection weight
+    for (auto& s : model_.stacks)
+      for (auto& L : s.layers)
+        for (int a = 0; a < 2; ++a) glu_interleave(L.cv_in[a]);
     auto mk = [&](DLin& l) {
       void* p = nullptr;
       ZASR_HIP_CHECK(hipMalloc(&p, (size_t)l.N * l.K * 2));
@@ -1085,12 +1088,20 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   };
   auto conv = [&](int k) {
     if (Ly.cv_in[k].wh) {  // bf16 mode: in_proj output and out_proj input in bf16
-      __bf16* g2 = ws<__bf16>("ly_g2_h", (size_t)R * 2 * d);
       __bf16* dc = ws<__bf16>("ly_dc_h", (size_t)R * d);
-      linear_h(Ly.cv_in[k], X, false, d, R, g2, true, 2 * d, EPI_NONE);
-      prof_begin("dwconv1d");
-      launch_glu_dwconv1d_bf16(g2, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
-      prof_end();
+      if (Ly.cv_in[k].glu) {  // the GLU in the in_proj epilogue (f32, then bf16), d columns
+        __bf16* g = ws<__bf16>("ly_glu_h", (size_t)R * d);
+        linear_h(Ly.cv_in[k], X, false, d, R, g, true, d, EPI_GLU);
+        prof_begin("dwconv1d");
+        launch_dwconv1d_post_glu_bf16(g, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+        prof_end();
+      } else {
+        __bf16* g2 = ws<__bf16>("ly_g2_h", (size_t)R * 2 * d);
+        linear_h(Ly.cv_in[k], X, false, d, R, g2, true, 2 * d, EPI_NONE);
+        prof_begin("dwconv1d");
+        launch_glu_dwconv1d_bf16(g2, d_off, d_map, R, d, S.K, Ly.cv_dw_w[k], Ly.cv_dw_b[k], dc, st_);
+        prof_end();
+      }
       linear_h(Ly.cv_out[k], dc, true, d, R, X, false, d, EPI_RESADD);
       return;
     }

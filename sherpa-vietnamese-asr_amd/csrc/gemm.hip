@@ -332,7 +332,7 @@ __attribute__((amdgpu_waves_per_eu(WAVES_M * WAVES_N >= 8 ? 4 : 1))) void gemm_b
   // every row segment is one 128-byte line written by 8 lanes x 16 bytes (one fragment alone
   // gives 64-byte half lines of 8-byte stores)
   constexpr bool PAIR = std::is_same<TC, __bf16>::value && FN % 2 == 0 && EPI != EPI_MULAUX &&
-                        EPI != EPI_MULAUX16 && EPI != EPI_RESADD && BM <= 128;
+                        EPI != EPI_MULAUX16 && EPI != EPI_RESADD && EPI != EPI_GLU && BM <= 128;
   constexpr int LDE2 = 72;                // paired epilogue row stride (floats)
   constexpr int OPER_BYTES = 2 * STAGE * 2;
   constexpr int EPI_BYTES = (NT / 64) * 32 * (PAIR ? LDE2 : LDE) * 4;
@@ -660,6 +660,18 @@ __attribute__((amdgpu_waves_per_eu(WAVES_M * WAVES_N >= 8 ? 4 : 1))) void gemm_b
             const bf16x4 x = *reinterpret_cast<const bf16x4*>(aux16 + (long)row * p.ldaux + col);
             v.x *= (float)x[0]; v.y *= (float)x[1]; v.z *= (float)x[2]; v.w *= (float)x[3];
           }
+          if constexpr (EPI == EPI_GLU) {  // columns (2c, 2c + 1) -> channel c
+            const float g0 = v.x * sigmoid_fast(v.y), g1 = v.z * sigmoid_fast(v.w);
+            TC* dst = C + (long)row * p.ldc + col / 2;
+            if constexpr (std::is_same<TC, float>::value) {
+              *reinterpret_cast<float2*>(dst) = make_float2(g0, g1);
+            } else {
+              bf16x2 h;
+              h[0] = (__bf16)g0; h[1] = (__bf16)g1;
+              *reinterpret_cast<bf16x2*>(dst) = h;
+            }
+            continue;
+          }
           TC* dst = C + (long)row * p.ldc + col;
           if constexpr (std::is_same<TC, float>::value) {
             if constexpr (EPI == EPI_RESADD) {
@@ -952,6 +964,18 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
             const bf16x4 x = *reinterpret_cast<const bf16x4*>(aux16 + (long)row * p.ldaux + col);
             v.x *= (float)x[0]; v.y *= (float)x[1]; v.z *= (float)x[2]; v.w *= (float)x[3];
           }
+          if constexpr (EPI == EPI_GLU) {  // columns (2c, 2c + 1) -> channel c
+            const float g0 = v.x * sigmoid_fast(v.y), g1 = v.z * sigmoid_fast(v.w);
+            TC* dst = C + (long)row * p.ldc + col / 2;
+            if constexpr (std::is_same<TC, float>::value) {
+              *reinterpret_cast<float2*>(dst) = make_float2(g0, g1);
+            } else {
+              bf16x2 h;
+              h[0] = (__bf16)g0; h[1] = (__bf16)g1;
+              *reinterpret_cast<bf16x2*>(dst) = h;
+            }
+            continue;
+          }
           TC* dst = C + (long)row * p.ldc + col;
           if constexpr (std::is_same<TC, float>::value) {
             if constexpr (EPI == EPI_RESADD) {
@@ -1170,6 +1194,7 @@ void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStrea
     switch (epi) {
       case EPI_NONE: return launch_bk_h<ALOAD_DENSE, EPI_NONE, float, __bf16>(p, B, st);
       case EPI_SWOOSHL: return launch_bk_h<ALOAD_DENSE, EPI_SWOOSHL, float, __bf16>(p, B, st);
+      case EPI_GLU: return launch_bk_h<ALOAD_DENSE, EPI_GLU, float, __bf16>(p, B, st);
       default: break;
     }
   } else if (aload == ALOAD_DENSE && a_bf16 && !c_bf16) {

@@ -8,6 +8,7 @@ namespace zasr {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // A operand, 4 consecutive k of row gm.  Loads are unconditional (clamped into the valid
 // range, zero selected afterwards): a guarded load compiles to a branch with a vmcnt(0) wait,

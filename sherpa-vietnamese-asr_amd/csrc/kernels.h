@@ -173,6 +173,9 @@ void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st);
 void launch_dwconv1d_post_glu(const float* g, const int* off, const int* map, int total_rows,
                               int d, int K, const float* w, const float* b, float* out,
                               hipStream_t st);
+void launch_dwconv1d_post_glu_bf16(const void* g, const int* off, const int* map,
+                                   int total_rows, int d, int K, const float* w, const float* b,
+                                   void* out, hipStream_t st);
 void launch_glu_dwconv1d(const float* x2, const int* off, const int* map, int total_rows, int d,
                          int K, const float* w, const float* b, float* out, hipStream_t st);
 // bf16 in (the conv in_proj output) / bf16 out (the conv out_proj input), bf16 mode
