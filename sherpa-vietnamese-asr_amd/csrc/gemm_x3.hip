@@ -468,10 +468,15 @@ __device__ __forceinline__ void h3_epilogue(const GemmParams& p, float* sE,
 
 // PR = 1: the hi x hi product only (a diagnostic of the split_lab: what the loop costs
 // without the two correction MFMAs; not numerically a split GEMM)
-template <int NS, int EPI, int BN, int WM = 2, int PR = 3>
+// ALD = ALOAD_CONV3 (Conv2dSubsampling's conv.7 as an implicit GEMM, K = 9 taps x 32
+// channels): k-tile kt is tap kt, so every A row segment is 32 contiguous channels of the
+// conv.4 output at a row-independent tap offset -- the same 128-byte LDS-DMA pieces as the
+// dense case from gathered row bases (load_a4<ALOAD_CONV3>'s addresses)
+template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(GemmParams p,
                                                                           const __bf16* Bw,
-                                                                          long blo, int tiles_n) {
+                                                                          long blo, int tiles_n,
+                                                                          int tiles_m) {
   constexpr int BM = 128, BK = 32;
   // WM x WN waves: WM = 4 gives each wave all BN columns of 32 rows, so every A element is
   // split by one wave (WM = 2: by two)
@@ -491,12 +496,28 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
   static_assert(B_BYTES % 4096 == 0, "BN must be a multiple of 64");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS_BYTES];
 
-  const float* A = p.A;
-  float* C = p.C;
-  const int M = p.M, K = p.K, lda = p.lda, N = p.N;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  // z-slices (per-sequence GEMMs, e.g. conv.7): tiles_n x tiles_m tiles per slice, the
+  // slice's operand offsets and M / K / lda applied to a local copy of the parameters
+  GemmParams q = p;
+  const int lin = xcd_tile(blockIdx.x, gridDim.x);
+  const int per = tiles_n * tiles_m;
+  const int zs = lin / per;
+  const int tile = lin - zs * per;
+  if (q.slices) {
+    const GemmSlice sl = q.slices[zs];
+    q.A += sl.a_off;
+    q.C += sl.c_off;
+    if (q.aux) q.aux += sl.aux_off;
+    q.M = sl.M;
+    q.K = sl.K;
+    q.lda = sl.lda;
+    Bw += sl.b_off;
+  }
+  const float* A = q.A;
+  const int M = q.M, K = q.K, lda = q.lda, N = q.N;
   const int m_tile = tile / tiles_n;
   const int m0 = m_tile * BM;
+  if (m0 >= M) return;  // a slice shorter than the longest (whole block)
   const int n0 = (tile - m_tile * tiles_n) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -509,7 +530,12 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
     const int row = (wid * GA + g) * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ ((row >> 1) & 7);
     const int gr = m0 + row < M ? m0 + row : M - 1;
-    asrc[g] = A + (long)gr * lda + 4 * lc;
+    if constexpr (ALD == ALOAD_CONV3) {
+      const int t = gr / 19, f = gr - t * 19;
+      asrc[g] = A + ((long)t * 39 + 2 * f) * 32 + 4 * lc;
+    } else {
+      asrc[g] = A + (long)gr * lda + 4 * lc;
+    }
   }
 #pragma unroll
   for (int g = 0; g < GB; ++g) {
@@ -521,9 +547,11 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
   auto issue = [&](int kt) {
     unsigned char* st = smem + (kt % NS) * STAGE;
     const int k0 = kt * BK;
+    // A offset of k-tile kt: dense k0; conv.7 tap kt = (kt / 3, kt % 3) of (time, freq)
+    const long ak = ALD == ALOAD_CONV3 ? ((long)(kt / 3) * 39 + kt % 3) * 32 : k0;
 #pragma unroll
     for (int g = 0; g < GA; ++g)
-      __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[g] + k0),
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[g] + ak),
                                        (h3_lds_t)(st + (wid * GA + g) * 1024), 16, 0, 0);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -592,15 +620,16 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
   }
   __syncthreads();
 
-  h3_epilogue<EPI, FM, FN>(p, reinterpret_cast<float*>(smem) + wid * (32 * LDE), acc, accl,
+  h3_epilogue<EPI, FM, FN>(q, reinterpret_cast<float*>(smem) + wid * (32 * LDE), acc, accl,
                            m0 + wm * WTM, n0 + wn * WTN, lane);
 }
 
-template <int NS, int EPI, int BN, int WM = 2, int PR = 3>
+template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE>
 void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
-  const int tn = cdiv(p.N, BN), tm = cdiv(p.M, 128);
-  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN, WM, PR>), dim3(tn * tm), dim3(256), 0, st,
-                     p, Bw, blo, tn);
+  const int tn = cdiv(p.N, BN), tm = cdiv(p.slices ? p.max_M : p.M, 128);
+  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN, WM, PR, ALD>),
+                     dim3(tn * tm * (p.slices ? p.num_slices : 1)), dim3(256), 0, st, p, Bw, blo,
+                     tn, tm);
 }
 
 // ZASR_H3_GLDS: 0 = the register-staged kernel only; 2 / 3 = LDS-DMA stages, 2x2 waves;
@@ -614,6 +643,12 @@ int h3_glds_mode() {
 // fp16 pieces (FMT 1): BK = 16 keeps two stages at 41 KB of LDS (3 blocks per CU)
 template <int ALOAD, int EPI>
 void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
+  if constexpr (ALOAD == ALOAD_CONV3) {
+    // (z-sliced launches carry K in the slices; the conv.7 loader's K is 9 taps x 32 = 288)
+    if (h3_glds_mode() != 0 && (p.slices ? p.max_M > 0 : p.K == 288 && p.M >= 128) &&
+        p.N % 128 == 0 && p.sbn == 288)
+      return launch_glds_h3<2, EPI, 128, 2, 3, ALOAD_CONV3>(p, Bw, blo, st);
+  }
   if constexpr (ALOAD == ALOAD_DENSE) {
     const int mode = h3_glds_mode();
     if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
