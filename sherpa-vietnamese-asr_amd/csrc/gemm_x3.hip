@@ -472,7 +472,7 @@ __device__ __forceinline__ void h3_epilogue(const GemmParams& p, float* sE,
 // channels): k-tile kt is tap kt, so every A row segment is 32 contiguous channels of the
 // conv.4 output at a row-independent tap offset -- the same 128-byte LDS-DMA pieces as the
 // dense case from gathered row bases (load_a4<ALOAD_CONV3>'s addresses)
-template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE>
+template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE, int RB = 0>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(GemmParams p,
                                                                           const __bf16* Bw,
                                                                           long blo, int tiles_n,
@@ -583,12 +583,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nkt) issue(kt + NS - 1);  // the stage every wave finished reading
     const unsigned char* st = smem + (kt % NS) * STAGE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    // fragments of k-step ks (16 deep): A rows split into fp16 hi / lo, B pieces as stored
+    auto frags = [&](int ks, bf16x8 (&a)[FM][2], bf16x8 (&b)[FN][2]) {
       const int ch = 2 * ks + h;
-      bf16x8 a[FM][2], b[FN][2];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * WTM + i * 32 + r32;
@@ -605,6 +603,8 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
         b[j][0] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + off);
         b[j][1] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + B_BYTES + off);
       }
+    };
+    auto products = [&](const bf16x8 (&a)[FM][2], const bf16x8 (&b)[FN][2]) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -616,6 +616,25 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
           else
             mfma_h3(a[i], b[j], acc[i][j], accl[i][j]);
         }
+    };
+    if constexpr (RB) {
+      // every fragment of the stage read before the next stage's DMA goes out: an LDS read
+      // behind an LDS-DMA makes the compiler wait for the DMA (vmcnt(0)), which put a full
+      // memory round trip in front of every k-tile's MFMAs
+      bf16x8 a[2][FM][2], b[2][FN][2];
+      frags(0, a[0], b[0]);
+      frags(1, a[1], b[1]);
+      if (kt + NS - 1 < nkt) issue(kt + NS - 1);
+      products(a[0], b[0]);
+      products(a[1], b[1]);
+    } else {
+      if (kt + NS - 1 < nkt) issue(kt + NS - 1);  // the stage every wave finished reading
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 a[FM][2], b[FN][2];
+        frags(ks, a, b);
+        products(a, b);
+      }
     }
   }
   __syncthreads();
@@ -624,10 +643,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
                            m0 + wm * WTM, n0 + wn * WTN, lane);
 }
 
-template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE>
+template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE, int RB = 0>
 void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.slices ? p.max_M : p.M, 128);
-  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN, WM, PR, ALD>),
+  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN, WM, PR, ALD, RB>),
                      dim3(tn * tm * (p.slices ? p.num_slices : 1)), dim3(256), 0, st, p, Bw, blo,
                      tn, tm);
 }
@@ -647,22 +666,22 @@ void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
     // (z-sliced launches carry K in the slices; the conv.7 loader's K is 9 taps x 32 = 288)
     if (h3_glds_mode() != 0 && (p.slices ? p.max_M > 0 : p.K == 288 && p.M >= 128) &&
         p.N % 128 == 0 && p.sbn == 288)
-      return launch_glds_h3<2, EPI, 128, 2, 3, ALOAD_CONV3>(p, Bw, blo, st);
+      return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_CONV3, 1>(p, Bw, blo, st);
   }
   if constexpr (ALOAD == ALOAD_DENSE) {
     const int mode = h3_glds_mode();
     if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
         p.M >= 128 && p.N % 64 == 0) {
       const bool w128 = p.N % 128 == 0;
-      if (mode == 4 && w128) return launch_glds_h3<2, EPI, 128, 4>(p, Bw, blo, st);
-      if (mode == 3) {
-        if (w128) return launch_glds_h3<3, EPI, 128>(p, Bw, blo, st);
-        return launch_glds_h3<3, EPI, 64>(p, Bw, blo, st);
+      if (mode == 1) {  // the round-4 layouts before the read-before-issue loop (A/B runs)
+        if (w128) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
+        return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
       }
-      // N % 128 != 0: the 64-wide tile with 4 x 1 waves (split_lab_tiles_v4: 0.22-0.26 vs
-      // 0.21-0.24 of the 2 x 2 layout on the same shapes)
-      if (w128) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
-      return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
+      // 4 x 1 waves (each A element split by one wave), the stage's fragments read before
+      // the next stage's DMA (split_lab_tiles_v7: 0.28-0.34 of the fp16 peak on the FFN /
+      // projection shapes vs 0.24-0.27 for the 2 x 2 loop that issued first)
+      if (w128) return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
+      return launch_glds_h3<2, EPI, 64, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
     }
   }
   // NonlinAttention's per-sequence GEMM (z-slices; A = head 0's f32 weights, K = the

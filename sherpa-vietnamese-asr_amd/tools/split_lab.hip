@@ -93,15 +93,20 @@ int main(int argc, char** argv) {
   {"glds ns" #NS " bn" #BN " w4x1", [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
      if (q.N % BN || q.K % 32) return; \
      launch_glds_h3<NS, EPI_NONE, BN, 4>(q, b, lo, st); }}
+#define ZGR(NS, BN, WM) \
+  {"glds ns" #NS " bn" #BN " wm" #WM " rb", [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) { \
+     if (q.N % BN || q.K % 32) return; \
+     launch_glds_h3<NS, EPI_NONE, BN, WM, 3, ALOAD_DENSE, 1>(q, b, lo, st); }}
       // "hi only": the glds loop with one MFMA per product instead of three (timing
       // diagnostic; its output differs by design)
-      const V vars[] = {ZG(2, 128), ZV(128, 128, 2, 2, 32), ZG(2, 64), ZG4(2, 64),
-                        ZV(64, 192, 2, 2, 16), ZV(64, 192, 2, 2, 32),
+      const V vars[] = {ZG(2, 128), ZV(128, 128, 2, 2, 32), ZGR(2, 128, 2), ZGR(3, 128, 2),
+                        ZGR(2, 64, 4), ZGR(2, 128, 4), ZGR(3, 64, 2), ZG(2, 64), ZG4(2, 64),
                         {"glds ns2 bn128 hi only", [](const GemmParams& q, const __bf16* b, long lo, hipStream_t st) {
                            if (q.N % 128 || q.K % 32) return;
                            launch_glds_h3<2, EPI_NONE, 128, 2, 1>(q, b, lo, st); }}};
 #undef ZG
 #undef ZG4
+#undef ZGR
 #undef ZV
       std::vector<float> ref0;
       for (const V& v : vars) {
