@@ -670,12 +670,14 @@ void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
   }
   if constexpr (ALOAD == ALOAD_DENSE) {
     const int mode = h3_glds_mode();
+    // any N % 4 == 0: the B rows past N are clamped loads, the epilogue stores col < N only
+    // (the attention in-projections: N = 68 H = 272 / 544, the value projection 12 H = 48)
     if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
-        p.M >= 128 && p.N % 64 == 0) {
-      const bool w128 = p.N % 128 == 0;
+        p.M >= 128 && p.N % 4 == 0) {
+      const bool w128 = cdiv(p.N, 128) * 128 * 10 <= cdiv(p.N, 64) * 64 * 11;
       if (mode == 1) {  // the round-4 layouts before the read-before-issue loop (A/B runs)
-        if (w128) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
-        return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
+        if (p.N % 128 == 0) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
+        if (p.N % 64 == 0) return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
       }
       // 4 x 1 waves (each A element split by one wave), the stage's fragments read before
       // the next stage's DMA (split_lab_tiles_v7: 0.28-0.34 of the fp16 peak on the FFN /
