@@ -5,13 +5,16 @@
 # stages, and the bench lines of BASELINE configs 3, 4 and 5 (and their token-exact f16x3
 # forms).  Profiled passes run with --parity-precision none (the parity line is a child
 # process of the bench; it is measured in the plain runs).
-# Usage (from the repo root, via gpurun): bash sherpa-vietnamese-asr_amd/tools/profile_round.sh TAG
+# Usage (from the repo root, via gpurun): bash sherpa-vietnamese-asr_amd/tools/profile_round.sh TAG [PART]
+# PART 1 / 2 runs the first / second half (each within one gpurun call's limit); default both.
 set -e
 TAG=${1:-r}
+PART=${2:-all}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
+if [ "$PART" != 2 ]; then
 timeout -k 10 400 python3 $R/bench.py > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 $R/bench.py --no-cpu-baseline --parity-precision none --steps 3 --warmup 1 > $OUT/stats_bench.json 2> $OUT/stats.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --parity-precision none --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1
@@ -21,6 +24,8 @@ for st in campp vad; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_$st -o run -- python3 $R/bench.py --stage $st --no-cpu-baseline --steps 3 --warmup 1 > $OUT/stats_$st.json 2> $OUT/stats_$st.err
 done
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords.json 2> $OUT/bench_beam8.err
+fi
+if [ "$PART" != 1 ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_f16x3 -o run -- python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --steps 3 --warmup 1 > $OUT/stats_f16x3.json 2> $OUT/stats_f16x3.err
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_f16x3.json 2> $OUT/bench_beam8_f16x3.err
 timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwords-file default > $OUT/bench_rover.json 2> $OUT/bench_rover.err
@@ -32,4 +37,5 @@ timeout -k 10 300 python3 $R/bench.py --stage dropin --precision bf16 --steps 3 
 # DESIGN §9's single-GPU proxies of the 8-rank shard plan (largest LPT share of the hour)
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --parity-precision none --proxy-ranks 8 > $OUT/bench_proxy8.json 2> $OUT/bench_proxy8.err
 timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwords-file default --no-cpu-baseline --proxy-ranks 8 > $OUT/bench_rover_proxy8.json 2> $OUT/bench_rover_proxy8.err
+fi
 echo done
