@@ -385,6 +385,19 @@ __global__ __launch_bounds__(256, 1) void convnext_mlp_h3_kernel(
   const long p0 = (long)blockIdx.x * kMlpM;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int col = lane & 31, half = lane >> 5;
+  auto w1frag = [&](int pc, int g, int ks) {
+    return *reinterpret_cast<const bf16x8*>(w1 + pc * W1P + (((long)g * 8 + ks) * 64 + lane) * 8);
+  };
+  auto w2frag = [&](int pc, int g, int ks) {
+    return *reinterpret_cast<const bf16x8*>(w2 + pc * W2P + (((long)g * 24 + ks) * 64 + lane) * 8);
+  };
+  // slice 0's W1 set, in flight under the Y tile's loads and split
+  bf16x8 wf[8][2];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    wf[ks][0] = w1frag(0, wid, ks);
+    wf[ks][1] = w1frag(1, wid, ks);
+  }
   // ---- Y tile: 128 positions x 128 channels f32 = 2048 groups of 8, 8 per thread ----
   {
     float4 v0[8], v1[8];
@@ -420,20 +433,9 @@ __global__ __launch_bounds__(256, 1) void convnext_mlp_h3_kernel(
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[t][r] = acc2l[t][r] = 0.f;
-  auto w1frag = [&](int pc, int g, int ks) {
-    return *reinterpret_cast<const bf16x8*>(w1 + pc * W1P + (((long)g * 8 + ks) * 64 + lane) * 8);
-  };
-  auto w2frag = [&](int pc, int g, int ks) {
-    return *reinterpret_cast<const bf16x8*>(w2 + pc * W2P + (((long)g * 24 + ks) * 64 + lane) * 8);
-  };
-  // one weight-fragment set live at a time (two sets + both accumulator pairs spill)
-  bf16x8 wf[8][2];
+  // one weight-fragment set live at a time (two sets + both accumulator pairs spill); the
+  // next slice's W1 set is loaded into the W2 registers pw2 has consumed
   for (int n3 = 0; n3 < 3; ++n3) {
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      wf[ks][0] = w1frag(0, n3 * 4 + wid, ks);
-      wf[ks][1] = w1frag(1, n3 * 4 + wid, ks);
-    }
     f32x16 acc1[4], acc1l[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -475,6 +477,7 @@ __global__ __launch_bounds__(256, 1) void convnext_mlp_h3_kernel(
         *reinterpret_cast<f16x4*>(Hs[1] + o) = ll;
       }
     lds_barrier_cx();
+    const int nn = n3 < 2 ? n3 + 1 : n3;  // (the last slice re-loads its own W1: unused)
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
@@ -483,6 +486,10 @@ __global__ __launch_bounds__(256, 1) void convnext_mlp_h3_kernel(
         mfma_h3_cx(wf[ks][0], wf[ks][1], *reinterpret_cast<const bf16x8*>(Hs[0] + o),
                    *reinterpret_cast<const bf16x8*>(Hs[1] + o), acc2[t], acc2l[t]);
       }
+      // W2 set ks is consumed: its registers take the next slice's W1 set ks, in flight
+      // under the remaining pw2 MFMAs
+      wf[ks][0] = w1frag(0, nn * 4 + wid, ks);
+      wf[ks][1] = w1frag(1, nn * 4 + wid, ks);
     }
   }
 
