@@ -685,6 +685,14 @@ void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) 
       if (w128) return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
       return launch_glds_h3<2, EPI, 64, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
     }
+    // z-sliced (NonlinAttention's A0 @ t1 per sequence): every slice's K and lda are its
+    // L rounded up to 32 (engine.cpp's sl_nl), its offsets 32-element aligned
+    if (mode != 0 && p.slices && p.sbn % 8 == 0 && p.N % 4 == 0 && p.max_M > 0 &&
+        getenv("ZASR_NONLIN_X3") == nullptr) {
+      const bool w128 = cdiv(p.N, 128) * 128 * 10 <= cdiv(p.N, 64) * 64 * 11;
+      if (w128) return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
+      return launch_glds_h3<2, EPI, 64, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
+    }
   }
   // NonlinAttention's per-sequence GEMM (z-slices; A = head 0's f32 weights, K = the
   // sequence length): every column tile re-reads the L x L A panel, so N = 144 (d = 192) takes
