@@ -66,10 +66,16 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 // FMT 1 (the f16x3 mode, NP = 2): the pieces are fp16 hi + lo * 2^-11 (gemm_dev.h split_h8)
 // and every product is hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16 MFMAs, the lo products in a
 // second accumulator (scores: combined per key block; O: at the end, and rescaled with O).
-template <int MODE, int NP, int FMT = 0>
+// MODE 3 (bf16, NF = value fragments per block): NonlinAttention, z = (A0 @ t1) * y.  Mode 0's
+// two passes over head 0; pass 2 multiplies the normalised weights P^T (the score registers as
+// they stand, as in modes 1 / 2) into V^T = this block's NF x 32 rows of t1t (grid.z = chunks of
+// hid), so head 0's L x L weights never reach HBM (mode 0 + the z-sliced GEMM wrote and read them).
+template <int MODE, int NP, int FMT = 0, int NF = 1>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;
   static_assert(FMT == 0 || NP == 2, "fp16 pieces: NP = 2");
+  static_assert(MODE != 3 || NP == 1, "fused NonlinAttention: the bf16 mode");
+  constexpr bool W0 = MODE == 0 || MODE == 3;  // head 0, two passes
   using T = typename std::conditional<SPLIT, float, __bf16>::type;
   // positional rows of this head, x = xlo + t for t < L + kPosPad, one plane per pos dim
   // (structure of arrays: the rows of two adjacent keys are adjacent floats in each plane,
@@ -77,8 +83,11 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   extern __shared__ float sPos[];
   __shared__ __attribute__((aligned(16))) __bf16 sK[NP][2][32 * kKLd];
   __shared__ __attribute__((aligned(16))) __bf16 sVt[NP][2][12 * kKLd];
+  // mode 3: V^T = t1t rows [fz NF 32, +NF 32) x 32 keys, keys permuted like sVt's
+  __shared__ __attribute__((aligned(16))) __bf16 sVn[2][MODE == 3 ? NF * 32 * kKLd : 8];
   const int b = blockIdx.y;
-  const int h = MODE == 0 ? 0 : blockIdx.z;
+  const int h = W0 ? 0 : blockIdx.z;
+  const int fz = MODE == 3 ? blockIdx.z : 0;
   const int r0 = a.row_off[b];
   const int L = a.row_off[b + 1] - r0;
   const int i0b = blockIdx.x * 128;
@@ -144,7 +153,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   // staging roles: threads 0..127 load K (key tid>>2, 8 dims 8 (tid&3)); threads 128..223
   // load V (key (tid-128)/3, 4 dims (tid-128)%3); MODE 0 needs no V
   const T* kbase = qkp + (long)r0 * ldq + 32 * H + 32 * h;
-  const T* vbase = MODE == 0 ? nullptr : reinterpret_cast<const T*>(a.v) + (long)r0 * ldv + 12 * h;
+  const T* vbase = W0 ? nullptr : reinterpret_cast<const T*>(a.v) + (long)r0 * ldv + 12 * h;
   const int vt = tid - 128;
   const int vkey = vt / 3, vq = vt - 3 * (vt / 3);
   // two register sets: key block kb + 2's global loads are in flight while block kb is
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   // row), so the wait before storing a set can count the newer set's loads still in flight
   // (divergent load sites made the compiler wait for everything)
   const bool kt = tid < 128;
-  const bool vrole = MODE != 0 && vt >= 0 && vt < 96;
+  const bool vrole = !W0 && vt >= 0 && vt < 96;
   auto gload = [&](int kb, auto set) {
     constexpr int S = decltype(set)::value;
     const int j0 = kb * 32;
@@ -187,7 +196,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       } else {
         *reinterpret_cast<bf16x8*>(d) = kv[S];
       }
-    } else if (MODE != 0 && vt < 96) {
+    } else if (!W0 && vt < 96) {
       // key jj sits in score register r = (jj&3) + 4 (jj>>3) of lane half (jj>>2)&1, which
       // the PV MFMA m = r >> 3 takes in k-slot 8 half + (r & 7)
       const int jj = vkey;
@@ -216,6 +225,45 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) sVt[0][buf][(4 * vq + e) * kKLd + slot] = kv[S][e];
+      }
+    }
+  };
+  // mode 3: V^T staging, NF 32 rows x 32 keys per key block = NF * 128 16-byte pieces (8 keys
+  // of one t1 row), NV per thread, loaded with the K rows' cadence (two sets in flight)
+  constexpr int NV = MODE == 3 ? (NF * 128 + 255) / 256 : 1;
+  bf16x8 v3[2][NV];
+  const __bf16* t1b = MODE == 3 ? reinterpret_cast<const __bf16*>(a.t1t) + a.o8[b] : nullptr;
+  auto gload3 = [&](int kb, auto set) {
+    constexpr int S = decltype(set)::value;
+    if constexpr (MODE == 3) {
+      const int j0 = (kb < nkb ? kb : nkb - 1) * 32;  // (clamped: the tail loads re-read)
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const int e = tid + 256 * u;
+        const int dr = (e >> 2) < NF * 32 ? (e >> 2) : NF * 32 - 1;
+        int dg = fz * NF * 32 + dr;
+        dg = dg < a.hid ? dg : a.hid - 1;
+        v3[S][u] = *reinterpret_cast<const bf16x8*>(t1b + (long)dg * a.ldt + j0 + 8 * (e & 3));
+      }
+    }
+  };
+  auto sstore3 = [&](int buf, auto set) {
+    constexpr int S = decltype(set)::value;
+    if constexpr (MODE == 3) {
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const int e = tid + 256 * u;
+        if (NV * 256 == NF * 128 || e < NF * 128) {
+          const int dr = e >> 2, g8 = e & 3;
+          // keys 8 g8 + q: q < 4 -> slot s0 + q, q >= 4 -> s0 + 8 + (q - 4) (see sstore)
+          const int s0 = 16 * (g8 >> 1) + 4 * (g8 & 1);
+          const bool live_row = fz * NF * 32 + dr < a.hid;  // rows past hid stay zero
+          bf16x8 v = v3[S][u];
+          if (!live_row) v = (bf16x8){};
+          __bf16* d = &sVn[buf][dr * kKLd + s0];
+          *reinterpret_cast<bf16x4*>(d) = (bf16x4){v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<bf16x4*>(d + 8) = (bf16x4){v[4], v[5], v[6], v[7]};
+        }
       }
     }
   };
@@ -298,11 +346,19 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) vf[mm][t][e] = (__bf16)0.f;
 
-  constexpr int NPASS = MODE == 0 ? 2 : 1;
+  constexpr int NPASS = W0 ? 2 : 1;
+  f32x16 o3[MODE == 3 ? NF : 1];  // mode 3: O^T per 32-row value fragment
+#pragma unroll
+  for (int f = 0; f < (MODE == 3 ? NF : 1); ++f)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o3[f][r] = 0.f;
   T* const a0 = MODE == 0 ? reinterpret_cast<T*>(a.attn) + a.a_off[b] : nullptr;
-#pragma unroll 1
+  // (mode 3: both passes unrolled, so the V^T staging and o3 exist in pass 2's code only)
+  constexpr int kPassUnroll = MODE == 3 ? 2 : 1;
+#pragma unroll kPassUnroll
   for (int pass = 0; pass < NPASS; ++pass) {
-    if (MODE == 0 && pass == 1) {
+    const bool vp = MODE == 3 && pass == 1;  // mode 3's V^T staging
+    if (W0 && pass == 1) {
       // row statistic from the two lane halves (same query, disjoint keys)
       const float mo = __shfl_xor(m, 32, 64), lo = __shfl_xor(l, 32, 64);
       const float M = fmaxf(m, mo);
@@ -312,9 +368,14 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     gload(0, I0{});
-    if (nkb > 1) gload(1, I1{});
+    if (vp) gload3(0, I0{});
+    if (nkb > 1) {
+      gload(1, I1{});
+      if (vp) gload3(1, I1{});
+    }
     __syncthreads();  // previous pass's readers are done with buffer 0 (and sPos is staged)
     sstore(0, I0{});
+    if (vp) sstore3(0, I0{});
     __syncthreads();
     // one key block: its loads went out two blocks ago (set S), block kb + 2's go out now
     // into the same set, block kb + 1 (set 1 - S) is stored for the next step
@@ -322,10 +383,42 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       constexpr int S = decltype(set)::value;
       const int cur = kb & 1;
       gload(kb + 2, set);  // unconditional (clamped rows past the end): see gload
+      if (vp) gload3(kb + 2, set);
       if (live) {
         f32x16 s;
         scores(kb, cur, s);
-        if constexpr (MODE == 0) {
+        if constexpr (MODE == 3) {
+          if (pass == 0) {
+            float bm = s[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) bm = fmaxf(bm, s[r]);
+            const float mn = fmaxf(m, bm);
+            if (mn != -INFINITY) {
+              const f32x2 nm = {-mn, -mn};
+              f32x2 acc = {0.f, 0.f};
+#pragma unroll
+              for (int r = 0; r < 16; r += 2) {
+                const f32x2 d = (f32x2){s[r], s[r + 1]} + nm;
+                acc += (f32x2){fexp2(d.x), fexp2(d.y)};
+              }
+              l = l * fexp2(m - mn) + (acc.x + acc.y);
+              m = mn;
+            }
+          } else {
+#pragma unroll
+            for (int mm = 0; mm < 2; ++mm) {
+              bf16x8 pf;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) pf[q] = (__bf16)fexp2(s[8 * mm + q] - cst);
+#pragma unroll
+              for (int f = 0; f < NF; ++f) {
+                const bf16x8 vf3 =
+                    *reinterpret_cast<const bf16x8*>(&sVn[cur][(f * 32 + c) * kKLd + 16 * mm + 8 * h2]);
+                o3[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf3, pf, o3[f], 0, 0, 0);
+              }
+            }
+          }
+        } else if constexpr (MODE == 0) {
           if (pass == 0) {
             float bm = s[0];
 #pragma unroll
@@ -442,7 +535,10 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           }
         }
       }
-      if (kb + 1 < nkb) sstore(cur ^ 1, std::integral_constant<int, 1 - S>{});
+      if (kb + 1 < nkb) {
+        sstore(cur ^ 1, std::integral_constant<int, 1 - S>{});
+        if (vp) sstore3(cur ^ 1, std::integral_constant<int, 1 - S>{});
+      }
       __syncthreads();
     };
 #pragma unroll 1
@@ -451,7 +547,26 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       if (kb + 1 < nkb) block(kb + 1, I1{});
     }
   }
-  if constexpr (MODE != 0) {
+  if constexpr (MODE == 3) {
+    if (!live || i >= L) return;
+    // z[i][c] = O^T[c][i] * y[i][c]: rows c = (r & 3) + 8 (r >> 2) + 4 h2 of each fragment
+    const __bf16* yrow = reinterpret_cast<const __bf16*>(a.y) + (long)(r0 + i) * a.ldy;
+    __bf16* zrow = reinterpret_cast<__bf16*>(a.z) + (long)(r0 + i) * a.hid;
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c0 = fz * NF * 32 + f * 32 + 8 * g + 4 * h2;
+        if (c0 < a.hid) {
+          const bf16x4 yv = *reinterpret_cast<const bf16x4*>(yrow + c0);
+          bf16x4 zv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) zv[e] = (__bf16)(o3[f][4 * g + e] * (float)yv[e]);
+          *reinterpret_cast<bf16x4*>(zrow + c0) = zv;
+        }
+      }
+  }
+  if constexpr (MODE == 1 || MODE == 2) {
     if (!live || i >= L) return;
     float inv = 1.f;
     if constexpr (MODE == 1) {
@@ -496,6 +611,22 @@ void launch_flash_np(const AttnFlashArgs& a, int mode, size_t lds, hipStream_t s
 
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
+  if (mode == 3) {
+    ZASR_REQUIRE(a.pieces == 1 && a.t1t && a.o8 && a.y && a.z && a.hid > 0 && a.hid % 4 == 0 &&
+                     a.ldt % 8 == 0 && a.ldy % 4 == 0,
+                 "attention mode 3: bf16 t1t / y / z with hid % 4 == 0");
+    const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
+    ZASR_REQUIRE(lds <= 120 * 1024, "attention: sequence too long for the flash kernel's LDS");
+    // 5 fragments for hid = 144 (one chunk) and 288 (two), 6 for 192 (one) and 384 (two)
+    const int nft = cdiv(a.hid, 32);
+    const int nf = (nft % 5 == 0 || nft == 9) ? 5 : 6;
+    const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, nf));
+    if (nf == 5)
+      hipLaunchKernelGGL((attn_flash_kernel<3, 1, 0, 5>), grid, dim3(256), lds, st, a);
+    else
+      hipLaunchKernelGGL((attn_flash_kernel<3, 1, 0, 6>), grid, dim3(256), lds, st, a);
+    return;
+  }
   ZASR_REQUIRE(a.H % 2 == 0, "attention: the bf16 kernels need an even head count (16-byte q/k rows)");
   const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
   ZASR_REQUIRE(lds <= 120 * 1024, "attention: sequence too long for the flash kernel's LDS");

@@ -859,6 +859,13 @@ std::string Engine::shape_key(const char* cls, int M, int K, int N, bool w16, bo
 // ------------------------------------------------------------------------------------
 // building blocks
 // ------------------------------------------------------------------------------------
+// bf16 mode: NonlinAttention as attention mode 3 (head 0's weights consumed in the flash
+// kernel) unless ZASR_NONLIN_UNFUSED is set (mode 0 + the z-sliced GEMM, the A/B reference)
+static bool nonlin_fused() {
+  static const bool f = getenv("ZASR_NONLIN_UNFUSED") == nullptr;
+  return f;
+}
+
 void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
                     const char* cls, const float* byp_orig, const float* byp_scale) {
   GemmParams p{};
@@ -997,9 +1004,11 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
     fa = AttnFlashArgs{qkp16, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A16,
                        nullptr, nullptr, stats, stats};
-    prof_begin("attn_softmax");
-    launch_attn_flash(fa, 0, st_);
-    prof_end();
+    if (!nonlin_fused()) {  // else head 0's weights are consumed inside the fused kernel
+      prof_begin("attn_softmax");
+      launch_attn_flash(fa, 0, st_);
+      prof_end();
+    }
   } else if (np) {
     // split-bf16 modes: the same flash kernels on f32 q / k / v, every MFMA product split
     // into np bf16 pieces per operand; head 0's weights in f32 (L8 row stride)
@@ -1135,6 +1144,20 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("elementwise");
     launch_nonlin_prep_t(h3, true, d_off, d_o8, d_map, R, hid, R8, t1t, st_);
     prof_end();
+    if (nonlin_fused()) {
+      // z = (A0 @ t1) * y in the flash kernel (mode 3): head 0's weights never reach HBM
+      AttnFlashArgs a = fa;
+      a.t1t = t1t;
+      a.o8 = d_o8;
+      a.ldt = R8;
+      a.hid = hid;
+      a.y = h3 + 2 * hid;
+      a.ldy = 3 * hid;
+      a.z = z;
+      prof_begin("attn_nonlin");
+      launch_attn_flash(a, 3, st_);
+      prof_end();
+    } else {
     GemmParams p{};
     p.A = reinterpret_cast<const float*>(A16);
     p.B = nullptr;
@@ -1153,6 +1176,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("attn_nonlin");
     gemm_nonlin_bf16(p, t1t, st_);
     prof_end();
+    }
     linear_h(Ly.na_out, z, true, hid, R, X, false, d, EPI_RESADD);
   } else if (np) {
     // z = (A0 @ t1) * y on the split-bf16 GEMM: A0 [L][L8] f32 (split while staging),
@@ -1427,8 +1451,8 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   prof_end();
 
   // ---------------- encoder stacks ----------------
-  if (bf16)
-    ws<__bf16>("ly_attn_h", std::max<size_t>(attn_floats, 1));
+  if (bf16)  // (the fused NonlinAttention never materialises head 0's weights)
+    ws<__bf16>("ly_attn_h", nonlin_fused() ? 1 : std::max<size_t>(attn_floats, 1));
   else
     ws<float>("ly_attn", std::max<size_t>(attn_floats, 1));
   const int Dm = cfg.max_dim();
