@@ -74,7 +74,8 @@ template <int MODE, int NP, int FMT = 0, int NF = 1>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;
   static_assert(FMT == 0 || NP == 2, "fp16 pieces: NP = 2");
-  static_assert(MODE != 3 || NP == 1, "fused NonlinAttention: the bf16 mode");
+  static_assert(MODE != 3 || NP == 1 || (NP == 2 && FMT == 1),
+                "fused NonlinAttention: the bf16 and f16x3 modes");
   constexpr bool W0 = MODE == 0 || MODE == 3;  // head 0, two passes
   using T = typename std::conditional<SPLIT, float, __bf16>::type;
   // positional rows of this head, x = xlo + t for t < L + kPosPad, one plane per pos dim
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 sK[NP][2][32 * kKLd];
   __shared__ __attribute__((aligned(16))) __bf16 sVt[NP][2][12 * kKLd];
   // mode 3: V^T = t1t rows [fz NF 32, +NF 32) x 32 keys, keys permuted like sVt's
-  __shared__ __attribute__((aligned(16))) __bf16 sVn[2][MODE == 3 ? NF * 32 * kKLd : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 sVn[NP][2][MODE == 3 ? NF * 32 * kKLd : 8];
   const int b = blockIdx.y;
   const int h = W0 ? 0 : blockIdx.z;
   const int fz = MODE == 3 ? blockIdx.z : 0;
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   // mode 3: V^T staging, NF 32 rows x 32 keys per key block = NF * 128 16-byte pieces (8 keys
   // of one t1 row), NV per thread, loaded with the K rows' cadence (two sets in flight)
   constexpr int NV = MODE == 3 ? (NF * 128 + 255) / 256 : 1;
-  bf16x8 v3[2][NV];
+  bf16x8 v3[2][NV][NP];  // (NP = 2: t1t's hi / lo piece images, hid x ldt apart)
   const __bf16* t1b = MODE == 3 ? reinterpret_cast<const __bf16*>(a.t1t) + a.o8[b] : nullptr;
   auto gload3 = [&](int kb, auto set) {
     constexpr int S = decltype(set)::value;
@@ -243,7 +244,9 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
         const int dr = (e >> 2) < NF * 32 ? (e >> 2) : NF * 32 - 1;
         int dg = fz * NF * 32 + dr;
         dg = dg < a.hid ? dg : a.hid - 1;
-        v3[S][u] = *reinterpret_cast<const bf16x8*>(t1b + (long)dg * a.ldt + j0 + 8 * (e & 3));
+#pragma unroll
+        for (int t = 0; t < NP; ++t)
+          v3[S][u][t] = *reinterpret_cast<const bf16x8*>(t1b + ((long)t * a.hid + dg) * a.ldt + j0 + 8 * (e & 3));
       }
     }
   };
@@ -258,11 +261,14 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           // keys 8 g8 + q: q < 4 -> slot s0 + q, q >= 4 -> s0 + 8 + (q - 4) (see sstore)
           const int s0 = 16 * (g8 >> 1) + 4 * (g8 & 1);
           const bool live_row = fz * NF * 32 + dr < a.hid;  // rows past hid stay zero
-          bf16x8 v = v3[S][u];
-          if (!live_row) v = (bf16x8){};
-          __bf16* d = &sVn[buf][dr * kKLd + s0];
-          *reinterpret_cast<bf16x4*>(d) = (bf16x4){v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<bf16x4*>(d + 8) = (bf16x4){v[4], v[5], v[6], v[7]};
+#pragma unroll
+          for (int t = 0; t < NP; ++t) {
+            bf16x8 v = v3[S][u][t];
+            if (!live_row) v = (bf16x8){};
+            __bf16* d = &sVn[t][buf][dr * kKLd + s0];
+            *reinterpret_cast<bf16x4*>(d) = (bf16x4){v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<bf16x4*>(d + 8) = (bf16x4){v[4], v[5], v[6], v[7]};
+          }
         }
       }
     }
@@ -347,11 +353,12 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       for (int e = 0; e < 8; ++e) vf[mm][t][e] = (__bf16)0.f;
 
   constexpr int NPASS = W0 ? 2 : 1;
-  f32x16 o3[MODE == 3 ? NF : 1];  // mode 3: O^T per 32-row value fragment
+  // mode 3: O^T per 32-row value fragment (FMT 1: o3l, the lo products)
+  f32x16 o3[MODE == 3 ? NF : 1], o3l[MODE == 3 && FMT == 1 ? NF : 1];
 #pragma unroll
   for (int f = 0; f < (MODE == 3 ? NF : 1); ++f)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o3[f][r] = 0.f;
+    for (int r = 0; r < 16; ++r) o3[f][r] = o3l[FMT == 1 ? f : 0][r] = 0.f;
   T* const a0 = MODE == 0 ? reinterpret_cast<T*>(a.attn) + a.a_off[b] : nullptr;
   // (mode 3: both passes unrolled, so the V^T staging and o3 exist in pass 2's code only)
   constexpr int kPassUnroll = MODE == 3 ? 2 : 1;
@@ -407,14 +414,26 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           } else {
 #pragma unroll
             for (int mm = 0; mm < 2; ++mm) {
-              bf16x8 pf;
+              bf16x8 pf[NP];
+              if constexpr (FMT == 1) {
+                float pv[8];
 #pragma unroll
-              for (int q = 0; q < 8; ++q) pf[q] = (__bf16)fexp2(s[8 * mm + q] - cst);
+                for (int q = 0; q < 8; ++q) pv[q] = fexp2(s[8 * mm + q] - cst);
+                split_fx<FMT, NP>(pv, pf);
+              } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) pf[0][q] = (__bf16)fexp2(s[8 * mm + q] - cst);
+              }
 #pragma unroll
               for (int f = 0; f < NF; ++f) {
-                const bf16x8 vf3 =
-                    *reinterpret_cast<const bf16x8*>(&sVn[cur][(f * 32 + c) * kKLd + 16 * mm + 8 * h2]);
-                o3[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf3, pf, o3[f], 0, 0, 0);
+                bf16x8 vf3[NP];
+#pragma unroll
+                for (int t = 0; t < NP; ++t)
+                  vf3[t] = *reinterpret_cast<const bf16x8*>(&sVn[t][cur][(f * 32 + c) * kKLd + 16 * mm + 8 * h2]);
+                if constexpr (FMT == 1)
+                  mfma_h3(vf3, pf, o3[f], o3l[f]);
+                else
+                  o3[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf3[0], pf[0], o3[f], 0, 0, 0);
               }
             }
           }
@@ -550,19 +569,30 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   if constexpr (MODE == 3) {
     if (!live || i >= L) return;
     // z[i][c] = O^T[c][i] * y[i][c]: rows c = (r & 3) + 8 (r >> 2) + 4 h2 of each fragment
-    const __bf16* yrow = reinterpret_cast<const __bf16*>(a.y) + (long)(r0 + i) * a.ldy;
-    __bf16* zrow = reinterpret_cast<__bf16*>(a.z) + (long)(r0 + i) * a.hid;
+    // (y / z: bf16 in the bf16 mode, f32 in f16x3)
+    const T* yrow = reinterpret_cast<const T*>(a.y) + (long)(r0 + i) * a.ldy;
+    T* zrow = reinterpret_cast<T*>(a.z) + (long)(r0 + i) * a.hid;
 #pragma unroll
     for (int f = 0; f < NF; ++f)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c0 = fz * NF * 32 + f * 32 + 8 * g + 4 * h2;
         if (c0 < a.hid) {
-          const bf16x4 yv = *reinterpret_cast<const bf16x4*>(yrow + c0);
-          bf16x4 zv;
+          float ov[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) zv[e] = (__bf16)(o3[f][4 * g + e] * (float)yv[e]);
-          *reinterpret_cast<bf16x4*>(zrow + c0) = zv;
+          for (int e = 0; e < 4; ++e)
+            ov[e] = FMT == 1 ? o3[f][4 * g + e] + o3l[f][4 * g + e] * kF16LoInv : o3[f][4 * g + e];
+          if constexpr (SPLIT) {
+            const float4 yv = *reinterpret_cast<const float4*>(yrow + c0);
+            *reinterpret_cast<float4*>(zrow + c0) =
+                make_float4(ov[0] * yv.x, ov[1] * yv.y, ov[2] * yv.z, ov[3] * yv.w);
+          } else {
+            const bf16x4 yv = *reinterpret_cast<const bf16x4*>(yrow + c0);
+            bf16x4 zv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) zv[e] = (__bf16)(ov[e] * (float)yv[e]);
+            *reinterpret_cast<bf16x4*>(zrow + c0) = zv;
+          }
         }
       }
   }
@@ -612,13 +642,24 @@ void launch_flash_np(const AttnFlashArgs& a, int mode, size_t lds, hipStream_t s
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
   if (mode == 3) {
-    ZASR_REQUIRE(a.pieces == 1 && a.t1t && a.o8 && a.y && a.z && a.hid > 0 && a.hid % 4 == 0 &&
-                     a.ldt % 8 == 0 && a.ldy % 4 == 0,
-                 "attention mode 3: bf16 t1t / y / z with hid % 4 == 0");
+    ZASR_REQUIRE((a.pieces == 1 || a.pieces == kPiecesF16) && a.t1t && a.o8 && a.y && a.z &&
+                     a.hid > 0 && a.hid % 4 == 0 && a.ldt % 8 == 0 && a.ldy % 4 == 0,
+                 "attention mode 3: the bf16 or f16x3 mode, hid % 4 == 0");
     const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
     ZASR_REQUIRE(lds <= 120 * 1024, "attention: sequence too long for the flash kernel's LDS");
     // 5 fragments for hid = 144 (one chunk) and 288 (two), 6 for 192 (one) and 384 (two)
     const int nft = cdiv(a.hid, 32);
+    if (a.pieces == kPiecesF16) {  // f16x3: two accumulators and two V^T images per fragment
+      static const int nf16 = getenv("ZASR_NL_NF") ? atoi(getenv("ZASR_NL_NF")) : 3;
+      if (nf16 == 3) {
+        const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, 3));
+        hipLaunchKernelGGL((attn_flash_kernel<3, 2, 1, 3>), grid, dim3(256), lds, st, a);
+      } else {
+        const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, 2));
+        hipLaunchKernelGGL((attn_flash_kernel<3, 2, 1, 2>), grid, dim3(256), lds, st, a);
+      }
+      return;
+    }
     const int nf = (nft % 5 == 0 || nft == 9) ? 5 : 6;
     const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, nf));
     if (nf == 5)

@@ -865,6 +865,14 @@ static bool nonlin_fused() {
   static const bool f = getenv("ZASR_NONLIN_UNFUSED") == nullptr;
   return f;
 }
+// f16x3: the fused form is opt-in (ZASR_NONLIN_FUSED_F16=1): its per-chunk score recomputation
+// (two-piece scores, f32 positional term) costs more than the L x L weights' round trip
+// (attn_softmax + attn_nonlin 4.7 ms per hour unfused vs 5.5 / 6.9 ms fused at 3 / 2 value
+// fragments per block)
+static bool nonlin_fused_f16() {
+  static const bool f = getenv("ZASR_NONLIN_FUSED_F16") != nullptr;
+  return f;
+}
 
 void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
                     const char* cls, const float* byp_orig, const float* byp_scale) {
@@ -1018,9 +1026,11 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
     fa = AttnFlashArgs{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A,
                        nullptr, nullptr, stats, stats, np};
-    prof_begin("attn_softmax");
-    launch_attn_flash(fa, 0, st_);
-    prof_end();
+    if (!(np == kPiecesF16 && nonlin_fused_f16())) {  // else consumed in the fused kernel
+      prof_begin("attn_softmax");
+      launch_attn_flash(fa, 0, st_);
+      prof_end();
+    }
   } else {
     // head 0 only: its normalised weights feed nonlin_attention; every head's statistics
     // come from self_attn1's online softmax
@@ -1188,6 +1198,20 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("elementwise");
     launch_nonlin_prep_t(h3, false, d_off, d_o8, d_map, R, hid, R8, t1t, st_, np);
     prof_end();
+    if (np == kPiecesF16 && nonlin_fused_f16()) {
+      // f16x3: z = (A0 @ t1) * y in the flash kernel (mode 3, fp16 pieces of P and t1)
+      AttnFlashArgs a = fa;
+      a.t1t = t1t;
+      a.o8 = d_o8;
+      a.ldt = R8;
+      a.hid = hid;
+      a.y = h3 + 2 * hid;
+      a.ldy = 3 * hid;
+      a.z = z;
+      prof_begin("attn_nonlin");
+      launch_attn_flash(a, 3, st_);
+      prof_end();
+    } else {
     GemmParams p{};
     p.A = A;
     p.B = nullptr;
@@ -1205,6 +1229,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("attn_nonlin");
     gemm_x3(p, t1t, (long)hid * R8, EPI_MULAUX, ALOAD_DENSE, st_, np);
     prof_end();
+    }
     linear(Ly.na_out, z, hid, R, X, d, EPI_RESADD);
   } else {
     float* h3 = ws<float>("ly_h3", (size_t)R * 3 * hid);
@@ -1454,7 +1479,8 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   if (bf16)  // (the fused NonlinAttention never materialises head 0's weights)
     ws<__bf16>("ly_attn_h", nonlin_fused() ? 1 : std::max<size_t>(attn_floats, 1));
   else
-    ws<float>("ly_attn", std::max<size_t>(attn_floats, 1));
+    ws<float>("ly_attn", split_pieces() == kPiecesF16 && nonlin_fused_f16()
+                             ? 1 : std::max<size_t>(attn_floats, 1));
   const int Dm = cfg.max_dim();
   float* full = ws<float>("st_full", (size_t)mL.total * Dm);
   // stack i's input (50 Hz, width d_i): stack 0 takes the embed output, every later one is
