@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   static_assert(FMT == 0 || NP == 2, "fp16 pieces: NP = 2");
   static_assert(MODE != 3 || NP == 1 || (NP == 2 && FMT == 1),
                 "fused NonlinAttention: the bf16 and f16x3 modes");
-  constexpr bool W0 = MODE == 0 || MODE == 3;  // head 0, two passes
+  constexpr bool W0 = MODE == 0 || MODE == 3;  // head 0
   using T = typename std::conditional<SPLIT, float, __bf16>::type;
   // positional rows of this head, x = xlo + t for t < L + kPosPad, one plane per pos dim
   // (structure of arrays: the rows of two adjacent keys are adjacent floats in each plane,
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) vf[mm][t][e] = (__bf16)0.f;
 
-  constexpr int NPASS = W0 ? 2 : 1;
+  constexpr int NPASS = MODE == 0 ? 2 : 1;
   // mode 3: O^T per 32-row value fragment (FMT 1: o3l, the lo products)
   f32x16 o3[MODE == 3 ? NF : 1], o3l[MODE == 3 && FMT == 1 ? NF : 1];
 #pragma unroll
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr int kPassUnroll = MODE == 3 ? 2 : 1;
 #pragma unroll kPassUnroll
   for (int pass = 0; pass < NPASS; ++pass) {
-    const bool vp = MODE == 3 && pass == 1;  // mode 3's V^T staging
+    constexpr bool vp = MODE == 3;  // mode 3's V^T staging
     if (W0 && pass == 1) {
       // row statistic from the two lane halves (same query, disjoint keys)
       const float mo = __shfl_xor(m, 32, 64), lo = __shfl_xor(l, 32, 64);
@@ -395,46 +395,63 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
         f32x16 s;
         scores(kb, cur, s);
         if constexpr (MODE == 3) {
-          if (pass == 0) {
-            float bm = s[0];
+          // one pass, online: running max / sum as mode 1, O rescaled when the max moves, the
+          // unnormalised weights (<= 1) in the MFMA, 1 / sum in the epilogue
+          float bm = s[0];
 #pragma unroll
-            for (int r = 1; r < 16; ++r) bm = fmaxf(bm, s[r]);
-            const float mn = fmaxf(m, bm);
-            if (mn != -INFINITY) {
-              const f32x2 nm = {-mn, -mn};
-              f32x2 acc = {0.f, 0.f};
+          for (int r = 1; r < 16; ++r) bm = fmaxf(bm, s[r]);
+          bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+          const float mn = fmaxf(m, bm);
+          if (__any(mn > m)) {
+            const float sc = fexp2(m - mn);  // m = -inf -> 0
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
 #pragma unroll
               for (int r = 0; r < 16; r += 2) {
-                const f32x2 d = (f32x2){s[r], s[r + 1]} + nm;
-                acc += (f32x2){fexp2(d.x), fexp2(d.y)};
+                const f32x2 v = (f32x2){o3[f][r], o3[f][r + 1]} * (f32x2){sc, sc};
+                o3[f][r] = v.x;
+                o3[f][r + 1] = v.y;
+                if constexpr (FMT == 1) {
+                  const f32x2 w = (f32x2){o3l[f][r], o3l[f][r + 1]} * (f32x2){sc, sc};
+                  o3l[f][r] = w.x;
+                  o3l[f][r + 1] = w.y;
+                }
               }
-              l = l * fexp2(m - mn) + (acc.x + acc.y);
-              m = mn;
+            l *= sc;
+            m = mn;
+          }
+          const f32x2 nm = {-m, -m};
+          f32x2 acc = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const f32x2 dd = (f32x2){s[r], s[r + 1]} + nm;
+            s[r] = fexp2(dd.x);
+            s[r + 1] = fexp2(dd.y);
+            acc += (f32x2){s[r], s[r + 1]};
+          }
+          l += acc.x + acc.y;
+#pragma unroll
+          for (int mm = 0; mm < 2; ++mm) {
+            bf16x8 pf[NP];
+            if constexpr (FMT == 1) {
+              float pv[8];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) pv[q] = s[8 * mm + q];
+              split_fx<FMT, NP>(pv, pf);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) pf[0][q] = (__bf16)s[8 * mm + q];
             }
-          } else {
 #pragma unroll
-            for (int mm = 0; mm < 2; ++mm) {
-              bf16x8 pf[NP];
-              if constexpr (FMT == 1) {
-                float pv[8];
+            for (int f = 0; f < NF; ++f) {
+              bf16x8 vf3[NP];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) pv[q] = fexp2(s[8 * mm + q] - cst);
-                split_fx<FMT, NP>(pv, pf);
-              } else {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) pf[0][q] = (__bf16)fexp2(s[8 * mm + q] - cst);
-              }
-#pragma unroll
-              for (int f = 0; f < NF; ++f) {
-                bf16x8 vf3[NP];
-#pragma unroll
-                for (int t = 0; t < NP; ++t)
-                  vf3[t] = *reinterpret_cast<const bf16x8*>(&sVn[t][cur][(f * 32 + c) * kKLd + 16 * mm + 8 * h2]);
-                if constexpr (FMT == 1)
-                  mfma_h3(vf3, pf, o3[f], o3l[f]);
-                else
-                  o3[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf3[0], pf[0], o3[f], 0, 0, 0);
-              }
+              for (int t = 0; t < NP; ++t)
+                vf3[t] = *reinterpret_cast<const bf16x8*>(&sVn[t][cur][(f * 32 + c) * kKLd + 16 * mm + 8 * h2]);
+              if constexpr (FMT == 1)
+                mfma_h3(vf3, pf, o3[f], o3l[f]);
+              else
+                o3[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf3[0], pf[0], o3[f], 0, 0, 0);
             }
           }
         } else if constexpr (MODE == 0) {
@@ -568,6 +585,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   }
   if constexpr (MODE == 3) {
     if (!live || i >= L) return;
+    const float inv = 1.f / (l + __shfl_xor(l, 32, 64));
     // z[i][c] = O^T[c][i] * y[i][c]: rows c = (r & 3) + 8 (r >> 2) + 4 h2 of each fragment
     // (y / z: bf16 in the bf16 mode, f32 in f16x3)
     const T* yrow = reinterpret_cast<const T*>(a.y) + (long)(r0 + i) * a.ldy;
@@ -581,7 +599,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           float ov[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            ov[e] = FMT == 1 ? o3[f][4 * g + e] + o3l[f][4 * g + e] * kF16LoInv : o3[f][4 * g + e];
+            ov[e] = (FMT == 1 ? o3[f][4 * g + e] + o3l[f][4 * g + e] * kF16LoInv : o3[f][4 * g + e]) * inv;
           if constexpr (SPLIT) {
             const float4 yv = *reinterpret_cast<const float4*>(yrow + c0);
             *reinterpret_cast<float4*>(zrow + c0) =
@@ -660,6 +678,8 @@ void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
       }
       return;
     }
+    // (one pass, online: 5-6 fragments at one wave per SIMD beat 4 fragments at two, 1.63 vs
+    // 2.08 ms per hour; the two-pass form took 2.02)
     const int nf = (nft % 5 == 0 || nft == 9) ? 5 : 6;
     const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, nf));
     if (nf == 5)
