@@ -859,21 +859,13 @@ std::string Engine::shape_key(const char* cls, int M, int K, int N, bool w16, bo
 // ------------------------------------------------------------------------------------
 // building blocks
 // ------------------------------------------------------------------------------------
-// bf16 mode: NonlinAttention as attention mode 3 (head 0's weights consumed in the flash
-// kernel) unless ZASR_NONLIN_UNFUSED is set (mode 0 + the z-sliced GEMM, the A/B reference)
+// bf16 and f16x3 modes: NonlinAttention as attention mode 3 (head 0's weights consumed in the
+// flash kernel) unless ZASR_NONLIN_UNFUSED is set (mode 0 + the z-sliced GEMM, the A/B
+// reference; the bf16x3 / bf16x6 modes always take that pair)
 static bool nonlin_fused() {
   static const bool f = getenv("ZASR_NONLIN_UNFUSED") == nullptr;
   return f;
 }
-// f16x3: the fused form is opt-in (ZASR_NONLIN_FUSED_F16=1): its per-chunk score recomputation
-// (two-piece scores, f32 positional term) costs more than the L x L weights' round trip
-// (attn_softmax + attn_nonlin 4.7 ms per hour unfused vs 5.5 / 6.9 ms fused at 3 / 2 value
-// fragments per block)
-static bool nonlin_fused_f16() {
-  static const bool f = getenv("ZASR_NONLIN_FUSED_F16") != nullptr;
-  return f;
-}
-
 void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
                     const char* cls, const float* byp_orig, const float* byp_scale) {
   GemmParams p{};
@@ -1026,7 +1018,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
     fa = AttnFlashArgs{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A,
                        nullptr, nullptr, stats, stats, np};
-    if (!(np == kPiecesF16 && nonlin_fused_f16())) {  // else consumed in the fused kernel
+    if (!(np == kPiecesF16 && nonlin_fused())) {  // else consumed in the fused kernel
       prof_begin("attn_softmax");
       launch_attn_flash(fa, 0, st_);
       prof_end();
@@ -1198,7 +1190,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("elementwise");
     launch_nonlin_prep_t(h3, false, d_off, d_o8, d_map, R, hid, R8, t1t, st_, np);
     prof_end();
-    if (np == kPiecesF16 && nonlin_fused_f16()) {
+    if (np == kPiecesF16 && nonlin_fused()) {
       // f16x3: z = (A0 @ t1) * y in the flash kernel (mode 3, fp16 pieces of P and t1)
       AttnFlashArgs a = fa;
       a.t1t = t1t;
@@ -1479,7 +1471,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
   if (bf16)  // (the fused NonlinAttention never materialises head 0's weights)
     ws<__bf16>("ly_attn_h", nonlin_fused() ? 1 : std::max<size_t>(attn_floats, 1));
   else
-    ws<float>("ly_attn", split_pieces() == kPiecesF16 && nonlin_fused_f16()
+    ws<float>("ly_attn", split_pieces() == kPiecesF16 && nonlin_fused()
                              ? 1 : std::max<size_t>(attn_floats, 1));
   const int Dm = cfg.max_dim();
   float* full = ws<float>("st_full", (size_t)mL.total * Dm);
