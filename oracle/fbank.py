@@ -13,10 +13,16 @@ Restated kaldi semantics:
               mel: 80 triangles linear in mel = 1127 ln(1 + f/700) over FFT bins 0..255,
               log(max(e, FLT_EPSILON)).
 
-PARITY: unpinned against kaldi-native-fbank itself (the library is absent and the
-reference holds no fbank fixtures).  The reference's own second restatement
-(`offline_pwa/static/js/pure-ort-asr-worker.js:351-519`) builds its triangles in Hz and is
-only a loose cross-check (tests/test_fbank_oracle.py).
+PARITY: kaldi-native-fbank itself is absent, but the reference ships a second, executable
+fbank -- `computeFbank`, `offline_pwa/static/js/pure-ort-asr-worker.js:470-519` -- and
+tests/golden/make_golden_fbank_js.py runs it under node.  `fbank_js` below restates that
+function (f64 framing / FFT / power / mel sums, f32 window and triangle weights, triangles
+linear in Hz incl. the Nyquist bin, log floor 2^-23) and is pinned to its outputs within 1e-5
+(tests/test_fbank_oracle.py).  `fbank` (the GPU's target, knf's semantics) shares every step
+with it except the two documented ones: triangles linear in mel over bins 0..255 (knf's
+MelBanks) and the f32 DC removal / pre-emphasis / window / power of knf's float pipeline; the
+tests bound that difference on the same fixtures.  The mel-vs-Hz triangle choice is the one
+step no reference-run output pins.
 """
 from __future__ import annotations
 
@@ -81,8 +87,10 @@ def frame_indices(n: int) -> np.ndarray:
     return idx
 
 
-def fbank(audio: np.ndarray) -> np.ndarray:
-    """audio float32 [N] in [-1, 1] -> float32 [T, 80] log-mel (kaldi semantics)."""
+def fbank(audio: np.ndarray, banks: np.ndarray = None) -> np.ndarray:
+    """audio float32 [N] in [-1, 1] -> float32 [T, 80] log-mel (kaldi semantics).  `banks`
+    (checker use): other (80, 257) triangles in place of mel_banks(), e.g. mel_banks_js() to
+    isolate the triangle difference against the reference's executable fbank."""
     audio = np.asarray(audio, dtype=np.float32)
     n = audio.shape[0]
     T = num_frames(n)
@@ -98,5 +106,50 @@ def fbank(audio: np.ndarray) -> np.ndarray:
     re = spec.real.astype(np.float32)
     im = spec.imag.astype(np.float32)
     power = re * re + im * im  # (T, 257) float32
-    mel = power[:, : NFFT // 2] @ mel_banks().T.astype(np.float32)
+    if banks is None:
+        mel = power[:, : NFFT // 2] @ mel_banks().T.astype(np.float32)
+    else:
+        mel = power @ banks.T.astype(np.float32)
     return np.log(np.maximum(mel, FLT_EPS)).astype(np.float32)
+
+
+def _hz_of_mel(m):
+    return 700.0 * (np.exp(m / 1127.0) - 1.0)
+
+
+def mel_banks_js() -> np.ndarray:
+    """(80, 257) float32: pure-ort-asr-worker.js:369-397 -- centres evenly spaced in mel,
+    triangles linear in Hz over bins 0..256 (f64 arithmetic, Float32Array storage)."""
+    mel = lambda f: 1127.0 * np.log(1.0 + f / 700.0)
+    lo, hi = mel(LOW_FREQ), mel(HIGH_FREQ)
+    delta = (hi - lo) / (NUM_BINS + 1)
+    centers = _hz_of_mel(lo + np.arange(NUM_BINS + 2, dtype=np.float64) * delta)
+    freqs = np.arange(NFFT // 2 + 1, dtype=np.float64) * 16000.0 / NFFT
+    W = np.zeros((NUM_BINS, NFFT // 2 + 1), dtype=np.float64)
+    for m in range(NUM_BINS):
+        left, center, right = centers[m], centers[m + 1], centers[m + 2]
+        up = (freqs > left) & (freqs <= center)
+        dn = (freqs > center) & (freqs < right)
+        W[m, up] = (freqs[up] - left) / max(center - left, 1e-12)
+        W[m, dn] = (right - freqs[dn]) / max(right - center, 1e-12)
+    return W.astype(np.float32)
+
+
+def fbank_js(audio: np.ndarray) -> np.ndarray:
+    """The reference's executable fbank (pure-ort-asr-worker.js:470-519) restated: frames of
+    reflected samples (:460-468, :485-491), f64 DC removal and pre-emphasis times the f32
+    window (:494-500), f64 FFT power (:502-505), f64 sums over the f32 Hz triangles and
+    log(max(e, 2^-23)) stored as f32 (:507-515)."""
+    audio = np.asarray(audio, dtype=np.float32)
+    n = audio.shape[0]
+    T = num_frames(n)
+    if T == 0:
+        return np.zeros((0, NUM_BINS), dtype=np.float32)
+    fr = audio[frame_indices(n)].astype(np.float64)
+    fr = fr - fr.sum(axis=1, keepdims=True) / FRAME_LEN
+    prev = np.concatenate([fr[:, :1], fr[:, :-1]], axis=1)
+    x = (fr - 0.97 * prev) * povey_window().astype(np.float64)[None, :]
+    spec = np.fft.rfft(x, n=NFFT, axis=1)
+    power = spec.real * spec.real + spec.imag * spec.imag
+    e = power @ mel_banks_js().astype(np.float64).T
+    return np.log(np.maximum(e, 1.1920928955078125e-7)).astype(np.float32)
