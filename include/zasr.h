@@ -192,6 +192,11 @@ void zasr_result_free(zasr_result* r);
                                    zasr_result_* for one chunk (valid until the stream is
                                    destroyed) */
 typedef struct zasr_stream zasr_stream;
+/* the symbol table zasr_stream_result_json's "tokens" / "text" use: sherpa-onnx's
+   OfflineModelConfig.tokens (sherpa-onnx-asr.js:1719 tokens field; the reference passes
+   tokens.txt beside its model files, core/asr_engine.py:980-986).  Default: model_dir/tokens.txt.
+   ZASR_ERR_NOT_FOUND if the file does not exist. */
+int zasr_set_tokens(zasr_recognizer* h, const char* tokens_path);
 int zasr_create_stream(zasr_recognizer* h, zasr_stream** out);
 void zasr_destroy_stream(zasr_stream* s);
 int zasr_stream_accept_waveform(zasr_stream* s, int32_t sample_rate, const float* samples,

@@ -1,5 +1,7 @@
-// bf16-mode kernels of NonlinAttention (icefall zipformer.py NonlinAttention, 3P; the
-// reference runs it inside the exported encoder, core/asr_engine.py:1045-1049):
+// Attention kernels of the Zipformer2 encoder (icefall zipformer.py
+// RelPositionMultiheadAttentionWeights / SelfAttention / NonlinAttention, 3P; the reference
+// runs them inside the exported encoder, core/asr_engine.py:1045-1049): the flash-style
+// kernel below (modes 0-3), and the kernels of the unfused NonlinAttention route:
 //
 //   z = (A0 @ (tanh(s) * x)) * y,   (s, x, y) = chunk(in_proj(src), 3),
 //   A0 = softmax over keys of head 0 of RelPositionMultiheadAttentionWeights.
@@ -10,7 +12,10 @@
 //   B = t1 transposed in bf16, [hid][R32] (sequence b in columns [o32_b, o32_b + L32_b), zero
 //       padded), i.e. the [N][K] "weight" layout the GEMM streams with 16-byte loads,
 // and the `* y` factor in its epilogue.  The kernels here produce A0 and t1^T.
+#include <mutex>
+#include <string>
 #include <type_traits>
+#include <unordered_map>
 
 #include "common.h"
 #include "gemm.h"
@@ -66,10 +71,13 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 // FMT 1 (the f16x3 mode, NP = 2): the pieces are fp16 hi + lo * 2^-11 (gemm_dev.h split_h8)
 // and every product is hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16 MFMAs, the lo products in a
 // second accumulator (scores: combined per key block; O: at the end, and rescaled with O).
-// MODE 3 (bf16, NF = value fragments per block): NonlinAttention, z = (A0 @ t1) * y.  Mode 0's
-// two passes over head 0; pass 2 multiplies the normalised weights P^T (the score registers as
-// they stand, as in modes 1 / 2) into V^T = this block's NF x 32 rows of t1t (grid.z = chunks of
-// hid), so head 0's L x L weights never reach HBM (mode 0 + the z-sliced GEMM wrote and read them).
+// MODE 3 (NF = value fragments per block): NonlinAttention, z = (A0 @ t1) * y, in ONE online
+// pass over head 0: running max / sum as in mode 1, the unnormalised weights P^T (<= 1; the
+// score registers as they stand) multiplied into V^T = this block's NF x 32 rows of t1t
+// (grid.z = chunks of hid), the value accumulators rescaled when the max moves, 1 / sum and
+// * y in the epilogue -- head 0's L x L weights never reach HBM (mode 0 + the z-sliced GEMM
+// wrote and read them).  bf16 mode: y / z bf16; f16x3 (FMT 1): two fp16 pieces of the weights
+// and of t1, hi / lo value accumulators, y / z f32.
 template <int MODE, int NP, int FMT = 0, int NF = 1>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;
@@ -646,15 +654,46 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   }
 }
 
+// gfx950: one workgroup may hold all 160 KiB of a CU's LDS, static + dynamic together
+constexpr size_t kLdsPerCu = 160 * 1024;
+
+// the static LDS of a kernel instantiation (hipFuncGetAttributes, memoised per function)
+static size_t kernel_static_lds(const void* fn) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> memo;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = memo.find(fn);
+  if (it != memo.end()) return it->second;
+  hipFuncAttributes at{};
+  ZASR_HIP_CHECK(hipFuncGetAttributes(&at, fn));
+  return memo[fn] = at.sharedSizeBytes;
+}
+
+// launch one flash-attention instantiation: its positional stage (dynamic LDS) must fit beside
+// the template's static key / value staging, and a failed launch must not leave the output
+// holding stale workspace data (checked right after the launch)
+template <int MODE, int NP, int FMT, int NF>
+static void launch_flash_one(const AttnFlashArgs& a, dim3 grid, size_t lds, hipStream_t st) {
+  const void* fn = reinterpret_cast<const void*>(&attn_flash_kernel<MODE, NP, FMT, NF>);
+  const size_t stat = kernel_static_lds(fn);
+  if (lds + stat > kLdsPerCu)
+    throw std::runtime_error("attention: sequence of " + std::to_string(a.max_len) +
+                             " frames needs " + std::to_string(lds + stat) +
+                             " B of LDS (positional stage + static staging), over the " +
+                             std::to_string(kLdsPerCu) + " B of a gfx950 CU");
+  hipLaunchKernelGGL((attn_flash_kernel<MODE, NP, FMT, NF>), grid, dim3(256), lds, st, a);
+  ZASR_HIP_CHECK(hipGetLastError());
+}
+
 template <int NP, int FMT = 0>
 void launch_flash_np(const AttnFlashArgs& a, int mode, size_t lds, hipStream_t st) {
   const dim3 grid(cdiv(a.max_len, 128), a.nseq, mode == 0 ? 1 : a.H);
   if (mode == 0)
-    hipLaunchKernelGGL((attn_flash_kernel<0, NP, FMT>), grid, dim3(256), lds, st, a);
+    launch_flash_one<0, NP, FMT, 1>(a, grid, lds, st);
   else if (mode == 1)
-    hipLaunchKernelGGL((attn_flash_kernel<1, NP, FMT>), grid, dim3(256), lds, st, a);
+    launch_flash_one<1, NP, FMT, 1>(a, grid, lds, st);
   else
-    hipLaunchKernelGGL((attn_flash_kernel<2, NP, FMT>), grid, dim3(256), lds, st, a);
+    launch_flash_one<2, NP, FMT, 1>(a, grid, lds, st);
 }
 
 void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
@@ -664,17 +703,16 @@ void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
                      a.hid > 0 && a.hid % 4 == 0 && a.ldt % 8 == 0 && a.ldy % 4 == 0,
                  "attention mode 3: the bf16 or f16x3 mode, hid % 4 == 0");
     const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
-    ZASR_REQUIRE(lds <= 120 * 1024, "attention: sequence too long for the flash kernel's LDS");
     // 5 fragments for hid = 144 (one chunk) and 288 (two), 6 for 192 (one) and 384 (two)
     const int nft = cdiv(a.hid, 32);
     if (a.pieces == kPiecesF16) {  // f16x3: two accumulators and two V^T images per fragment
       static const int nf16 = getenv("ZASR_NL_NF") ? atoi(getenv("ZASR_NL_NF")) : 3;
       if (nf16 == 3) {
         const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, 3));
-        hipLaunchKernelGGL((attn_flash_kernel<3, 2, 1, 3>), grid, dim3(256), lds, st, a);
+        launch_flash_one<3, 2, 1, 3>(a, grid, lds, st);
       } else {
         const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, 2));
-        hipLaunchKernelGGL((attn_flash_kernel<3, 2, 1, 2>), grid, dim3(256), lds, st, a);
+        launch_flash_one<3, 2, 1, 2>(a, grid, lds, st);
       }
       return;
     }
@@ -683,14 +721,13 @@ void launch_attn_flash(const AttnFlashArgs& a, int mode, hipStream_t st) {
     const int nf = (nft % 5 == 0 || nft == 9) ? 5 : 6;
     const dim3 grid(cdiv(a.max_len, 128), a.nseq, cdiv(nft, nf));
     if (nf == 5)
-      hipLaunchKernelGGL((attn_flash_kernel<3, 1, 0, 5>), grid, dim3(256), lds, st, a);
+      launch_flash_one<3, 1, 0, 5>(a, grid, lds, st);
     else
-      hipLaunchKernelGGL((attn_flash_kernel<3, 1, 0, 6>), grid, dim3(256), lds, st, a);
+      launch_flash_one<3, 1, 0, 6>(a, grid, lds, st);
     return;
   }
   ZASR_REQUIRE(a.H % 2 == 0, "attention: the bf16 kernels need an even head count (16-byte q/k rows)");
   const size_t lds = (size_t)(a.max_len + kPosPad) * sizeof(float4);
-  ZASR_REQUIRE(lds <= 120 * 1024, "attention: sequence too long for the flash kernel's LDS");
   if (a.pieces == 1)
     launch_flash_np<1>(a, mode, lds, st);
   else if (a.pieces == 2)

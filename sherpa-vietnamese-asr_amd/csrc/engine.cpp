@@ -1857,9 +1857,13 @@ std::vector<TokenResult> Engine::collect_search(SearchJob& job) {
   const int* h_tok = reinterpret_cast<const int*>(h + 24 * n);
   const int* h_fr = reinterpret_cast<const int*>(h + 28 * n);
   const int* h_cnt = reinterpret_cast<const int*>(h + 32 * n);
-  if (job.check_finite && h_cnt[S] != 0)
+  if (job.check_finite && h_cnt[S] != 0) {
+    // drain every engine stream (later batches' encoders, the other search job) before the
+    // error leaves the pipeline: the next call reuses the workspaces and pinned arenas
+    ZASR_HIP_CHECK(hipDeviceSynchronize());
     throw std::runtime_error("precision f16x3: non-finite encoder output (an activation exceeded "
                              "the fp16 range of the split operands); decode with bf16x6 or fp32");
+  }
   if (job.stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
     const int Tmax = job.Tmax;
     std::vector<unsigned long long> hs((size_t)Tmax * 16);

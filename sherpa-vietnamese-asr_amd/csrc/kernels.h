@@ -226,7 +226,10 @@ void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
 //           [L, L8) zero; L8 = L rounded up to 8), the NonlinAttention GEMM operand
 //   mode 1: self-attention with running statistics; writes out and stats_out
 //   mode 2: self-attention with the statistics of mode 1 (stats_in)
-//   mode 3: mode 0's two passes with pass 2 multiplying the weights into t1 (NonlinAttention)
+//   mode 3: NonlinAttention fused, one online pass over head 0: running max / sum, the
+//           unnormalised weights multiplied into t1 as they are computed (value accumulators
+//           rescaled when the max moves), 1 / sum and * y in the epilogue; bf16 or f16x3
+//           (pieces == kPiecesF16: two fp16 pieces of the weights and of t1)
 // stats: [R][H] c = row max + log2(row sum), log2 domain
 struct AttnFlashArgs {
   const void* qkp;         // [R][68 H]: bf16 (pieces == 1) or f32
@@ -246,10 +249,11 @@ struct AttnFlashArgs {
   // 2 / 3: f32 storage, every MFMA product split into 2 / 3 bf16 pieces per operand (the
   // bf16x3 / bf16x6 modes; q and p unscaled)
   int pieces = 1;
-  // mode 3 (bf16): NonlinAttention fused -- z = (A0 @ t1) * y with head 0's normalised
-  // weights A0 consumed where they are computed (never written): t1 as launch_nonlin_prep_t's
-  // transposed image t1t[c][o8_b + j] (row stride ldt, zero-padded to L32), y [R][ldy] bf16,
-  // z [R][hid] bf16
+  // mode 3: NonlinAttention fused -- z = (A0 @ t1) * y with head 0's weights A0 consumed
+  // where they are computed (never written): t1 as launch_nonlin_prep_t's transposed image
+  // t1t[c][o8_b + j] (row stride ldt, zero-padded to L32; pieces == kPiecesF16: the fp16 hi
+  // image, then the lo image at + hid * ldt), y [R][ldy] and z [R][hid]: bf16 in the bf16
+  // mode (pieces == 1), f32 in the f16x3 mode
   const void* t1t = nullptr;
   const int* o8 = nullptr;
   int ldt = 0;

@@ -933,6 +933,9 @@ std::string load_stage_dir(const std::string& dir, const std::string& kind, Safe
   else if (kind == "campp") cfg = "campp_config.json", st = "campp.safetensors";
   else if (kind == "vibert") cfg = "vibert_config.json", st = "vibert.safetensors";
   else throw std::invalid_argument("unknown model kind " + kind);
+  // the file itself, as the reference's create_ort_session callers name it
+  // (core/speaker_diarization_senko_campp_optimized.py:322-325, core/gec_model.py:133-140)
+  if (ends_with(dir, ".onnx") && file_exists(dir)) return load_stage_onnx(dir, kind, out);
   if (file_exists(dir + "/" + cfg) && file_exists(dir + "/" + st)) {
     out.load(dir + "/" + st);
     return read_file(dir + "/" + cfg);

@@ -23,8 +23,10 @@ using zasr::TokenResult;
 struct zasr_recognizer {
   std::unique_ptr<Engine> eng;
   std::string model_dir;
-  // tokens.txt of model_dir, loaded on the first JSON result (sherpa-onnx SymbolTable: a
+  // the symbol table (sherpa-onnx OfflineModelConfig.tokens; zasr_set_tokens, default
+  // model_dir/tokens.txt), loaded on the first JSON result (sherpa-onnx SymbolTable: a
   // leading "\u2581" becomes a space)
+  std::string tokens_path;
   std::mutex sym_mu;
   std::vector<std::string> syms;
   bool syms_loaded = false;
@@ -122,8 +124,9 @@ void decode_streams_impl(zasr_recognizer* h, zasr_stream* const* ss, int n) {
 const std::vector<std::string>& symbols(zasr_recognizer* h) {
   std::lock_guard<std::mutex> lk(h->sym_mu);
   if (!h->syms_loaded) {
-    std::ifstream f(h->model_dir + "/tokens.txt");
-    if (!f) throw std::invalid_argument("tokens.txt not found in " + h->model_dir);
+    const std::string path = h->tokens_path.empty() ? h->model_dir + "/tokens.txt" : h->tokens_path;
+    std::ifstream f(path);
+    if (!f) throw std::invalid_argument("symbol table not found: " + path);
     std::string line;
     while (std::getline(f, line)) {
       std::istringstream ls(line);
@@ -616,6 +619,19 @@ int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float t
 }
 
 // ---- offline streams (sherpa-onnx OfflineStream surface) ----
+int zasr_set_tokens(zasr_recognizer* h, const char* tokens_path) {
+  if (!h || !tokens_path) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    std::ifstream f(tokens_path);
+    if (!f) return fail(ZASR_ERR_NOT_FOUND, std::string("tokens file not found: ") + tokens_path);
+    std::lock_guard<std::mutex> lk(h->sym_mu);
+    h->tokens_path = tokens_path;
+    h->syms.clear();
+    h->syms_loaded = false;
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_create_stream(zasr_recognizer* h, zasr_stream** out) {
   if (!h || !out) return fail(ZASR_ERR_INVALID, "null argument");
   return guarded([&]() {

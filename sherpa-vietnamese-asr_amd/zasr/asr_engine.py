@@ -57,9 +57,13 @@ BLANK_ID = 0
 UNK_ID = 2
 CONTEXT_SIZE = 2
 
-# the precision create_recognizer (and zasr.offline) use unless told otherwise: the
-# token-exact split-bf16 mode (exact-f32 quality products), the mode
-# bench.py reports as parity_mode and times the drop-in stage in; ZASR_PRECISION overrides
+# the precision create_recognizer (and zasr.offline) use unless told otherwise: f16x3, the
+# fastest token-exact mode -- every f32 operand as two fp16 pieces (hi + lo * 2^-11), three
+# fp16 MFMAs per product, ~2^-22 relative per product; operands must
+# stay below fp16's 65504: a batch whose encoder output goes non-finite is re-decoded by a
+# bf16x6 engine (three bf16 pieces: exact-f32 quality at f32 range; binding.Recognizer).
+# bench.py reports it as parity_mode and times the drop-in stage in it; ZASR_PRECISION
+# overrides
 DEFAULT_PRECISION = "f16x3"
 
 _recognizer_cache: Dict[tuple, dict] = {}

@@ -33,7 +33,7 @@ EXPORTS = (
     "zasr_decode_stream", "zasr_decode_streams", "zasr_stream_is_decoded",
     "zasr_stream_num_tokens", "zasr_stream_num_frames", "zasr_stream_tokens",
     "zasr_stream_frames", "zasr_stream_log_probs", "zasr_stream_token_stats",
-    "zasr_stream_result_json",
+    "zasr_stream_result_json", "zasr_set_tokens",
 )
 
 
@@ -197,6 +197,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_stream_token_stats.restype = fp
     lib.zasr_stream_result_json.argtypes = [P, C.c_char_p, I64, C.POINTER(I64)]
     lib.zasr_stream_result_json.restype = C.c_int
+    lib.zasr_set_tokens.argtypes = [P, C.c_char_p]
+    lib.zasr_set_tokens.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -288,13 +290,41 @@ class Recognizer:
             raise ZasrError(msg)
         self.handle = h
         self.device_id = int(device_id)
+        self.precision = precision
         self.vocab_size = self.lib.zasr_vocab_size(h)
         self.joiner_dim = self.lib.zasr_joiner_dim(h)
+        self._args = (model_dir, decoding_method, max_active_paths, hotwords, scores, device_id,
+                      lib_path)
+        self._fallback = None
 
     def close(self):
         if getattr(self, "handle", None):
             self.lib.zasr_destroy(self.handle)
             self.handle = None
+        fb = getattr(self, "_fallback", None)
+        if fb is not None:
+            fb.close()
+            self._fallback = None
+
+    # f16x3 stores the split operands as fp16 pieces (|x| < 65504); an activation beyond that
+    # range makes the encoder output non-finite, which the engine detects per batch (after
+    # draining every stream) and reports.  The decode is then redone by a bf16x6 engine of the
+    # same model: the other exact-f32-quality mode, whose bf16 pieces have f32's range
+    # (DESIGN.md §6), so the caller still gets the token-exact transcript.
+    FALLBACK_PRECISION = "bf16x6"
+
+    def _retry(self, e: "ZasrError", name: str, *args, **kw):
+        if self.precision != "f16x3" or "non-finite encoder output" not in str(e):
+            raise e
+        if self._fallback is None:
+            import logging
+            logging.getLogger("zasr").warning(
+                "[zasr] f16x3 operand range exceeded; re-decoding with %s", self.FALLBACK_PRECISION)
+            md, method, beam, hw, sc, dev, lp = self._args
+            self._fallback = Recognizer(md, method, beam, hotwords=hw, hotword_scores=sc,
+                                        device_id=dev, precision=self.FALLBACK_PRECISION,
+                                        lib_path=lp)
+        return getattr(self._fallback, name)(*args, **kw)
 
     def __del__(self):
         try:
@@ -344,16 +374,22 @@ class Recognizer:
         arrs = [_f32(c) for c in chunks]
         ns = (C.c_int64 * len(arrs))(*[a.shape[0] for a in arrs])
         res = C.c_void_p()
-        self._check(self.lib.zasr_decode_batch(self.handle, _ptr_array(arrs), ns, len(arrs),
-                                               beam, C.byref(res)))
+        try:
+            self._check(self.lib.zasr_decode_batch(self.handle, _ptr_array(arrs), ns, len(arrs),
+                                                   beam, C.byref(res)))
+        except ZasrError as e:
+            return self._retry(e, "decode", arrs, beam=beam)
         return self._collect(res)
 
     def decode_features(self, feats: Sequence, beam: int = 0) -> List[SearchResult]:
         arrs = [_f32(f) for f in feats]
         ns = (C.c_int64 * len(arrs))(*[a.shape[0] for a in arrs])
         res = C.c_void_p()
-        self._check(self.lib.zasr_decode_features(self.handle, _ptr_array(arrs), ns, len(arrs),
-                                                  beam, C.byref(res)))
+        try:
+            self._check(self.lib.zasr_decode_features(self.handle, _ptr_array(arrs), ns,
+                                                      len(arrs), beam, C.byref(res)))
+        except ZasrError as e:
+            return self._retry(e, "decode_features", arrs, beam=beam)
         return self._collect(res)
 
     def decode_device(self, d_wav_ptr: int, offsets: Sequence[int], lengths: Sequence[int],
@@ -362,8 +398,12 @@ class Recognizer:
         off = (C.c_int64 * n)(*offsets)
         ln = (C.c_int64 * n)(*lengths)
         res = C.c_void_p()
-        self._check(self.lib.zasr_decode_device(self.handle, C.c_void_p(d_wav_ptr), off, ln, n,
-                                                beam, C.c_void_p(stream), C.byref(res)))
+        try:
+            self._check(self.lib.zasr_decode_device(self.handle, C.c_void_p(d_wav_ptr), off, ln,
+                                                    n, beam, C.c_void_p(stream), C.byref(res)))
+        except ZasrError as e:
+            return self._retry(e, "decode_device", d_wav_ptr, offsets, lengths, beam=beam,
+                               stream=stream)
         return self._collect(res)
 
     def decode_device_batches(self, d_wav_ptr: int, offsets: Sequence[int],
@@ -376,9 +416,13 @@ class Recognizer:
         ln = (C.c_int64 * n)(*lengths)
         bs = (C.c_int32 * len(batch_sizes))(*batch_sizes)
         res = C.c_void_p()
-        self._check(self.lib.zasr_decode_device_batches(
-            self.handle, C.c_void_p(d_wav_ptr), off, ln, n, bs, len(batch_sizes), beam,
-            C.c_void_p(stream), C.byref(res)))
+        try:
+            self._check(self.lib.zasr_decode_device_batches(
+                self.handle, C.c_void_p(d_wav_ptr), off, ln, n, bs, len(batch_sizes), beam,
+                C.c_void_p(stream), C.byref(res)))
+        except ZasrError as e:
+            return self._retry(e, "decode_device_batches", d_wav_ptr, offsets, lengths,
+                               batch_sizes, beam=beam, stream=stream)
         return self._collect(res)
 
     def encode_features(self, feats: Sequence) -> List[np.ndarray]:

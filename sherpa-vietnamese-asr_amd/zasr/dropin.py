@@ -22,10 +22,13 @@ What is rebound (the ASR hot path, core/asr_engine.py:698-1326):
                   (:2137-2161) is registered, its batched decode starts at once for the
                   loaded recognizers, and the per-chunk decode_chunk calls of the two
                   workers are served from that ONE decode (zasr.asr_engine, plan-ahead)
-  hardware_accel  configure_gpu_addon_paths only (the DirectML / OpenVINO add-on dispatch is
+  hardware_accel  configure_gpu_addon_paths (the DirectML / OpenVINO add-on dispatch is
                   removed per the north star); create_ort_session, is_gpu_provider and
-                  auto_batch_size stay the reference's, so the stages outside ASR (diarization,
-                  punctuation, DNSMOS) keep running on onnxruntime as before
+                  auto_batch_size wrapped: the "CAM++ speaker embedding" and "ViBERT
+                  punctuation" sessions (core/speaker_diarization_senko_campp_optimized.py:
+                  364-368, core/gec_model.py:168-172) are libzasr.so engines with the
+                  onnxruntime run() surface their callers use; every other stage (pyannote,
+                  DNSMOS, ...) gets the reference's own onnxruntime session
   calibration     detect_calibration_status / run_device_calibration (the provider picker is
                   removed per the north star; ASR always runs on MI355X)
   vad_utils       (only when vad_module is given) _get_vad_session, unload_vad_model,
@@ -47,6 +50,9 @@ from typing import List, Optional
 ENGINE_NAMES = ("compute_fbank_ort", "_log_add", "create_recognizer", "_ort_beam_search",
                 "_compute_token_entropy", "_finalize_word_entropy", "decode_chunk")
 ACCEL_NAMES = ("configure_gpu_addon_paths",)
+WRAPPED_ACCEL = {"create_ort_session": "make_create_ort_session",
+                 "is_gpu_provider": "make_is_gpu_provider",
+                 "auto_batch_size": "make_auto_batch_size"}
 CALIBRATION_NAMES = ("detect_calibration_status", "run_device_calibration")
 VAD_NAMES = ("_get_vad_session", "unload_vad_model", "get_cached_vad_probs",
              "_run_vad_inference", "get_vad_segments")
@@ -115,6 +121,12 @@ def install(engine_module: ModuleType, accel_module: Optional[ModuleType] = None
         for n in ACCEL_NAMES:
             setattr(accel_module, n, getattr(ours_hw, n))
             done.append("hardware_accel." + n)
+        # CAM++ / ViBERT sessions from libzasr.so, everything else the reference's own
+        for n, make in WRAPPED_ACCEL.items():
+            orig = getattr(accel_module, n, None)
+            if orig is not None and not getattr(orig, "_zasr_wrapped", False):
+                setattr(accel_module, n, getattr(ours_hw, make)(orig))
+                done.append("hardware_accel." + n)
     if calibration_module is not None:
         for n in CALIBRATION_NAMES:
             setattr(calibration_module, n, getattr(ours_cal, n))

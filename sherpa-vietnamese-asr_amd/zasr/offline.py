@@ -137,6 +137,9 @@ class OfflineRecognizer:
                                   hotwords=seqs, hotword_scores=scores, device_id=dev,
                                   precision=prec)
         self._lib = self._handle.lib
+        # the JSON result (zasr_stream_result_json) reads the same symbol table as .result
+        self._handle._check(self._lib.zasr_set_tokens(self._handle.handle,
+                                                      os.path.abspath(tokens).encode()))
         self._syms = _load_symbols(tokens)
         self.config = {"model_dir": model_dir, "tokens": tokens, "decoding_method": decoding_method,
                        "max_active_paths": int(max_active_paths), "precision": prec,

@@ -9,8 +9,10 @@ then ours, then the other order in a second process), imports the reference's ow
 `core.asr_engine`, `core.hardware_accel` and `core.calibration`, runs install(), and asserts:
   * the hot-path names of the reference module object are now this build's functions;
   * the names this build must NOT take over (get_ort, TranscriberPipeline, rover_merge_words,
-    merge_chunks_with_overlap, create_ort_session, is_gpu_provider, auto_batch_size) are
-    still the reference's;
+    merge_chunks_with_overlap) are still the reference's; create_ort_session, is_gpu_provider
+    and auto_batch_size are wrapped: the reference's own diarizer initialize() gets its CAM++
+    session from libzasr.so (its pyannote session stays onnxruntime's), the ViBERT stage
+    likewise, and the reference's provider checks accept it (check_session_routing);
   * clear_model_cache is wrapped: this build's cache is dropped AND the reference's own
     function still runs (it unloads the punctuation restorer / diarizer);
   * create_recognizer's hotword route goes through the reference's get_hotwords_config
@@ -33,6 +35,9 @@ import io
 import os
 import subprocess
 import sys
+import types
+
+import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(os.path.dirname(os.path.dirname(HERE)), "sherpa-vietnamese-asr_amd")
@@ -54,7 +59,7 @@ def check(ref_root: str, ours_first: bool) -> None:
 
     keep = {n: getattr(ref, n) for n in ("get_ort", "TranscriberPipeline", "rover_merge_words",
                                           "merge_chunks_with_overlap")}
-    keep_hw = {n: getattr(ref_hw, n) for n in ("create_ort_session", "is_gpu_provider",
+    orig_hw = {n: getattr(ref_hw, n) for n in ("create_ort_session", "is_gpu_provider",
                                                 "auto_batch_size")}
     orig_clear = ref.clear_model_cache
     done = install(ref, ref_hw, ref_cal)
@@ -67,9 +72,10 @@ def check(ref_root: str, ours_first: bool) -> None:
         assert getattr(ref_cal, n) is getattr(ours_cal, n), n
     for n, f in keep.items():
         assert getattr(ref, n) is f, n
-    for n, f in keep_hw.items():
-        assert getattr(ref_hw, n) is f, n
+    for n, f in orig_hw.items():  # wrapped, not replaced: other stages reach the reference's
+        assert getattr(ref_hw, n) is not f and getattr(ref_hw, n)._zasr_wrapped, n
     assert "asr_engine.create_recognizer" in done and "asr_engine.decode_chunk" in done
+    check_session_routing(ref_root, ref_hw, ours_hw, orig_hw)
 
     # clear_model_cache: ours drops its cache, the reference's still runs
     assert ref.clear_model_cache is not orig_clear
@@ -115,6 +121,79 @@ def check(ref_root: str, ours_first: bool) -> None:
     done += [d for d in done_vad if d.startswith("vad_utils.")]
     print("dropin install ok (%s first): %d names rebound, %d hotword phrases via "
           "get_hotwords_config" % ("zasr" if ours_first else "reference", len(done), len(phrases)))
+
+
+def check_session_routing(ref_root, ref_hw, ours_hw, orig_hw) -> None:
+    """The reference's own diarizer initialize() (core/speaker_diarization_senko_campp_
+    optimized.py:344-398) and GecBERTModel's session call (core/gec_model.py:168-191) over the
+    installed factory: CAM++ / ViBERT sessions are libzasr.so engines (a recording stand-in
+    here: no GPU in this container), the pyannote segmentation session the diarizer builds
+    directly stays onnxruntime's, and the reference's provider checks accept the engine.
+    onnxruntime is absent here: a recording stand-in module takes its place."""
+    made, ort_made = [], []
+
+    class Standin:
+        def __init__(self, model_path, device_id=0):
+            made.append(model_path)
+            self.calls = []
+
+        def run(self, names, feeds):
+            self.calls.append((names, {k: np.asarray(v).shape for k, v in feeds.items()}))
+            n = np.asarray(feeds["feats"]).shape[0]
+            return [np.ones((n, 192), np.float32)]
+
+    class FakeOrt(types.ModuleType):
+        class SessionOptions:
+            pass
+
+        class GraphOptimizationLevel:
+            ORT_ENABLE_ALL = 99
+
+        class ExecutionMode:
+            ORT_SEQUENTIAL = 0
+
+        @staticmethod
+        def set_default_logger_severity(level):
+            pass
+
+        @staticmethod
+        def get_available_providers():
+            return ["CPUExecutionProvider"]
+
+        @staticmethod
+        def InferenceSession(path, opts=None, providers=None):
+            ort_made.append((path, providers))
+            return types.SimpleNamespace(get_providers=lambda: ["CPUExecutionProvider"])
+
+    saved = (ours_hw.CamppOrtSession, ours_hw.VibertOrtSession, sys.modules.get("onnxruntime"))
+    ours_hw.CamppOrtSession = ours_hw.VibertOrtSession = Standin
+    sys.modules["onnxruntime"] = FakeOrt("onnxruntime")
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            from core.speaker_diarization_senko_campp_optimized import SenkoCamppDiarizerOptimized
+            dz = SenkoCamppDiarizerOptimized(model_dir="/models/campp-3dspeaker",
+                                             execution_provider="rocm")
+            dz.initialize()
+        assert made == ["/models/campp-3dspeaker/campplus_cn_en_common_200k.onnx"], made
+        assert dz.emb_sess.calls == [(["embs"], {"feats": (1, 150, 80)})], dz.emb_sess.calls
+        assert dz.batch_size == ours_hw.CAMPP_BATCH, dz.batch_size
+        assert [p for p, _ in ort_made] == [dz.seg_path], ort_made  # segmentation: onnxruntime
+        vib = os.path.join("/models/vibert-capu", "vibert-capu.onnx")
+        sess, info = ref_hw.create_ort_session(sys.modules["onnxruntime"], vib, object(),
+                                               policy="rocm", stage="ViBERT punctuation")
+        assert made[-1] == vib and ref_hw.is_gpu_provider(info.get("actual_provider"))
+        assert ref_hw.auto_batch_size("ViBERT punctuation", 32,
+                                      info["actual_provider"]) == ours_hw.VIBERT_BATCH
+        # the reference's own functions still answer for their providers
+        assert ref_hw.is_gpu_provider("ROCMExecutionProvider") == orig_hw["is_gpu_provider"](
+            "ROCMExecutionProvider")
+        assert ref_hw.auto_batch_size("DNSMOS", 8, "CPUExecutionProvider") == 8
+    finally:
+        ours_hw.CamppOrtSession, ours_hw.VibertOrtSession = saved[:2]
+        if saved[2] is None:
+            sys.modules.pop("onnxruntime", None)
+        else:
+            sys.modules["onnxruntime"] = saved[2]
 
 
 def check_pipeline(ref_root: str) -> None:

@@ -118,3 +118,24 @@ def test_stream_errors(onnx_dir):
         kw = _kwargs(d)
         kw["encoder"] = os.path.join(d, "missing-encoder.onnx")
         OfflineRecognizer.from_transducer(**kw)
+
+
+def test_json_result_uses_the_given_symbol_table(onnx_dir, tmp_path):
+    """the JSON result reads the tokens file the recognizer was given (sherpa-onnx
+    OfflineModelConfig.tokens), not model_dir/tokens.txt."""
+    from zasr.offline import OfflineRecognizer
+    _, d = onnx_dir
+    other = tmp_path / "renamed_tokens.txt"
+    with open(os.path.join(d, "tokens.txt"), encoding="utf-8") as f:
+        rows = [ln.split() for ln in f if ln.strip()]
+    with open(other, "w", encoding="utf-8") as f:
+        f.write("".join(f"{'X' + s if int(i) > 2 else s} {i}\n" for s, i in rows))
+    kw = _kwargs(d)
+    kw["tokens"] = str(other)
+    recognizer = OfflineRecognizer.from_transducer(**kw, precision="fp32")
+    s = recognizer.create_stream()
+    s.accept_waveform(16000, _speech(6.0, 4243))
+    recognizer.decode_stream(s)
+    js = json.loads(s.as_json_string())
+    assert s.result.tokens and all(t.startswith("X") for t in s.result.tokens)
+    assert js["tokens"] == s.result.tokens and js["text"] == s.result.text
