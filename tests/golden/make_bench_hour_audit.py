@@ -9,7 +9,10 @@ For every differing chunk it reruns the oracle (numpy fbank -> torch fp32 encode
 reference's _ort_beam_search restated, core/asr_engine.py:1023-1153) and records:
   greedy    the first frame where the two decodes part, the oracle's log-prob margin there
             (its own token's log-prob minus the GPU's token's) -- a rounding-level tie sits far
-            below the logits' scale -- and whether the oracle itself changes its tokens when its
+            below the logits' scale; the search adds every candidate's log-prob to the
+            hypothesis score in f32 (core/asr_engine.py:1099-1100), whose ulp at the scores of
+            a 30 s chunk (|score| ~ 500-2000) is 3e-5-1.2e-4, so margins of that size are
+            decided by rounding -- and whether the oracle itself changes its tokens when its
             encoder output is perturbed by ~1e-6 relative (two seeds; two f32 encoders, torch
             on the CPU and MFMA on the GPU, differ by ~3e-6 on these chunks);
   beam 8    the same perturbation test, and the frames where the oracle meets an EXACT f32 tie

@@ -536,7 +536,8 @@ def test_f16x3_range_guards(need_gpu, tmp_path):
     """f16x3 carries operands as fp16 pieces: a weight at or beyond 65504 is refused when the
     model loads, and an activation that overflows the pieces (here: layer 0's feed_forward1
     output scaled so the residual stream reaches ~1e5) makes the decode fail loudly with the
-    non-finite guard instead of returning tokens; fp32 decodes the same model."""
+    non-finite guard (and the public decode then re-runs the batch in bf16x6); fp32 decodes the
+    same model."""
     from model_fixtures import tiny_model
     from zasr.binding import Recognizer, ZasrError
     from zasr.model import save_model_dir, synth_tokens
@@ -554,7 +555,15 @@ def test_f16x3_range_guards(need_gpu, tmp_path):
     save_model_dir(p2, cfg, hot, synth_tokens(cfg.vocab_size))
     chunks = [_speech(4.0, 3100)]
     Recognizer(p2, "greedy_search", 1, precision="fp32").decode(chunks)
+    # the engine reports the overflow; the public decode re-runs the batch in bf16x6
+    # (zasr.binding.Recognizer._retry) and returns its tokens instead of failing
+    want = Recognizer(p2, "greedy_search", 1, precision="bf16x6").decode(chunks)
     rec = Recognizer(p2, "greedy_search", 1, precision="f16x3")
+    rec._retry = lambda e, *a, **k: (_ for _ in ()).throw(e)  # the engine's own error
     with pytest.raises(ZasrError, match="non-finite"):
         rec.decode(chunks)
+    del rec._retry
+    got = rec.decode(chunks)
+    assert rec._fallback is not None
+    assert [r.token_ids.tolist() for r in got] == [r.token_ids.tolist() for r in want]
     rec.close()
