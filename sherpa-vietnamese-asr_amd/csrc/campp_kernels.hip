@@ -305,10 +305,9 @@ void campp_conv2d_permute_weights(const float* w, int ks, float* out) {
 
 void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st) {
   ZASR_REQUIRE(a.ci <= 32 && (ks == 1 || ks == 3), "campp conv2d: Ci <= 32, kernel 1 or 3");
-  static const bool direct = getenv("ZASR_CAMPP_DIRECT_CONV") != nullptr;
   // the 3 x 3 convolutions take the MFMA kernel; the 1 x 1 shortcut (a quarter of the
   // rows' work, no reuse across taps) stays on the direct kernel, which measured faster
-  if (!direct && ks == 3 && a.wk && a.ci == 32 && !a.in_tf && a.T <= 160 &&
+  if (ks == 3 && a.wk && a.ci == 32 && !a.in_tf && a.T <= 160 &&
       (a.sf == 1 || a.sf == 2)) {
     // rows per block: about 2048 blocks per launch, an even row count, at least 2
     const int pairs = cdiv(a.fo, 2);

@@ -33,7 +33,6 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 constexpr int kDwT = 16;                // output frames per block
 constexpr int kDwH = kDwT + 6;          // staged frames
 constexpr int kDwC = 64;                // channels per block
-constexpr int kDwItems = 2 * 19 * 32;   // (segment, freq, channel pair) work items
 
 }  // namespace
 

@@ -384,77 +384,6 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const i
                        c1_off, c1_map, total_rows, w, b, out);
 }
 
-// =====================================================================================
-// ConvNeXt depthwise Conv2d(128, 7x7, padding 3) over [L][19][128] per sequence.
-// Block tile: 16 packed time rows x 19 freq x 32 channels, staged with a 3-row halo in
-// LDS; zero padding outside each row's own sequence (so ragged batches == batch 1).
-// =====================================================================================
-constexpr int kDw2T = 16;
-
-__global__ __launch_bounds__(256) void dwconv2d_kernel(const float* __restrict__ x,
-                                                       const int* __restrict__ L_off,
-                                                       const int* __restrict__ L_map,
-                                                       int total_rows, const float* __restrict__ w,
-                                                       const float* __restrict__ bias,
-                                                       float* __restrict__ out) {
-  __shared__ float tile[(kDw2T + 6) * 19 * 32];
-  __shared__ int sLo[kDw2T], sHi[kDw2T];
-  const int r0 = blockIdx.x * kDw2T;
-  const int c0 = blockIdx.y * 32;
-  const int tid = threadIdx.x;
-  if (tid < kDw2T) {
-    const int r = r0 + tid;
-    if (r < total_rows) {
-      const int b = L_map[r];
-      sLo[tid] = L_off[b] - r;
-      sHi[tid] = L_off[b + 1] - 1 - r;
-    }
-  }
-  // stage rows r0-3 .. r0+kDw2T+2 (packed), channels c0..c0+31
-  for (int e = tid; e < (kDw2T + 6) * 19 * 8; e += 256) {
-    const int c4 = e & 7;
-    const int rf = e >> 3;
-    const int rr = rf / 19, f = rf - rr * 19;
-    const int r = r0 - 3 + rr;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r >= 0 && r < total_rows)
-      v = *reinterpret_cast<const float4*>(x + ((long)r * 19 + f) * 128 + c0 + 4 * c4);
-    *reinterpret_cast<float4*>(&tile[(rr * 19 + f) * 32 + 4 * c4]) = v;
-  }
-  __syncthreads();
-  const int c = tid & 31;
-  float wr[49];
-#pragma unroll
-  for (int k = 0; k < 49; ++k) wr[k] = w[(c0 + c) * 49 + k];
-  const float bc = bias[c0 + c];
-  for (int p = tid >> 5; p < kDw2T * 19; p += 8) {
-    const int tr = p / 19, f = p - tr * 19;
-    const int r = r0 + tr;
-    if (r >= total_rows) break;
-    const int lo = sLo[tr], hi = sHi[tr];  // allowed time offsets
-    float acc = bc;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int dt = i - 3;
-      if (dt < lo || dt > hi) continue;
-#pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        const int ff = f + j - 3;
-        if (ff < 0 || ff >= 19) continue;
-        acc = fmaf(wr[i * 7 + j], tile[((tr + 3 + dt) * 19 + ff) * 32 + c], acc);
-      }
-    }
-    out[((long)r * 19 + f) * 128 + c0 + c] = acc;
-  }
-}
-
-void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
-                     const float* w, const float* b, float* out, hipStream_t st) {
-  if (total_rows <= 0) return;
-  dim3 grid(cdiv(total_rows, kDw2T), 4);
-  hipLaunchKernelGGL(dwconv2d_kernel, grid, dim3(256), 0, st, x, L_off, L_map, total_rows, w, b,
-                     out);
-}
 
 // =====================================================================================
 // BiasNorm (+ optional bypass): one wave per row.

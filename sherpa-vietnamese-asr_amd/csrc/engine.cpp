@@ -859,13 +859,6 @@ std::string Engine::shape_key(const char* cls, int M, int K, int N, bool w16, bo
 // ------------------------------------------------------------------------------------
 // building blocks
 // ------------------------------------------------------------------------------------
-// bf16 and f16x3 modes: NonlinAttention as attention mode 3 (head 0's weights consumed in the
-// flash kernel) unless ZASR_NONLIN_UNFUSED is set (mode 0 + the z-sliced GEMM, the A/B
-// reference; the bf16x3 / bf16x6 modes always take that pair)
-static bool nonlin_fused() {
-  static const bool f = getenv("ZASR_NONLIN_UNFUSED") == nullptr;
-  return f;
-}
 void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int ldc, int epi,
                     const char* cls, const float* byp_orig, const float* byp_scale) {
   GemmParams p{};
@@ -1004,11 +997,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
     fa = AttnFlashArgs{qkp16, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A16,
                        nullptr, nullptr, stats, stats};
-    if (!nonlin_fused()) {  // else head 0's weights are consumed inside the fused kernel
-      prof_begin("attn_softmax");
-      launch_attn_flash(fa, 0, st_);
-      prof_end();
-    }
+    // (head 0's weights are consumed inside the fused NonlinAttention kernel, mode 3)
   } else if (np) {
     // split-bf16 modes: the same flash kernels on f32 q / k / v, every MFMA product split
     // into np bf16 pieces per operand; head 0's weights in f32 (L8 row stride)
@@ -1018,7 +1007,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     stats = ws<float>("ly_attn_stats", (size_t)R * h);
     fa = AttnFlashArgs{qkp, h, Ly.pos_tab, model_.pmax, d_off, d_aoff, B, maxL, A,
                        nullptr, nullptr, stats, stats, np};
-    if (!(np == kPiecesF16 && nonlin_fused())) {  // else consumed in the fused kernel
+    if (np != kPiecesF16) {  // f16x3: consumed in the fused NonlinAttention kernel
       prof_begin("attn_softmax");
       launch_attn_flash(fa, 0, st_);
       prof_end();
@@ -1035,14 +1024,13 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     launch_attn_softmax(a, st_);
     prof_end();
   }
-  static const bool ffn_unfused = getenv("ZASR_FFN_UNFUSED") != nullptr;
   // bf16 mode: feed_forward2's residual epilogue also applies bypass_mid (same formula as
   // launch_bypass, one pass over X fewer)
   auto ff = [&](int k) {
     const DLin& fi = Ly.ff_in[k];
     const float* bo = (bf16 && k == 1) ? O : nullptr;
     const float* bs = (bf16 && k == 1) ? Ly.bypass_mid : nullptr;
-    if (fi.wh && !ffn_unfused && ffn_fused_supported(d) && (d < 256 || fi.wp)) {
+    if (fi.wh && ffn_fused_supported(d) && (d < 256 || fi.wp)) {
       // bf16 mode: in_proj -> SwooshL -> out_proj + residual in one kernel, hidden on chip
       // (d >= 256: the fragment-packed weights of ffn_wide_kernel)
       prof_begin("ffn_fused");
@@ -1136,9 +1124,8 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
   ff(0);
   // 2. nonlin_attention (attention head 0 only)
   if (bf16) {
-    // z = (A0 @ t1) * y on bf16 MFMA: A0 [L][L32] bf16, t1^T [hid][R32] bf16, z bf16
-    // (s, x, y) = chunk(in_proj(src), 3) in bf16: read by the transpose kernel (s, x) and
-    // by the GEMM epilogue (y)
+    // z = (A0 @ t1) * y with t1^T [hid][R8] bf16, z bf16; (s, x, y) = chunk(in_proj(src), 3)
+    // in bf16: s, x read by the transpose kernel, y by the fused kernel's epilogue
     __bf16* h3 = ws<__bf16>("ly_h3_h", (size_t)R * 3 * hid);
     __bf16* t1t = ws<__bf16>("ly_t1t", (size_t)hid * R8);
     __bf16* z = ws<__bf16>("ly_z_h", (size_t)R * hid);
@@ -1146,39 +1133,18 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("elementwise");
     launch_nonlin_prep_t(h3, true, d_off, d_o8, d_map, R, hid, R8, t1t, st_);
     prof_end();
-    if (nonlin_fused()) {
-      // z = (A0 @ t1) * y in the flash kernel (mode 3): head 0's weights never reach HBM
-      AttnFlashArgs a = fa;
-      a.t1t = t1t;
-      a.o8 = d_o8;
-      a.ldt = R8;
-      a.hid = hid;
-      a.y = h3 + 2 * hid;
-      a.ldy = 3 * hid;
-      a.z = z;
-      prof_begin("attn_nonlin");
-      launch_attn_flash(a, 3, st_);
-      prof_end();
-    } else {
-    GemmParams p{};
-    p.A = reinterpret_cast<const float*>(A16);
-    p.B = nullptr;
-    p.sbk = 1;
-    p.sbn = R8;
-    p.C = reinterpret_cast<float*>(z);
-    p.ldc = hid;
-    p.N = hid;
-    p.alpha = 1.f;
-    p.aux = reinterpret_cast<const float*>(h3 + 2 * hid);  // bf16 (EPI_MULAUX16)
-    p.ldaux = 3 * hid;
-    p.slices = reinterpret_cast<const GemmSlice*>(d_slices_nl);
-    p.num_slices = B;
-    p.max_M = maxL;
-    p.ldaux = 3 * hid;
+    // z = (A0 @ t1) * y in the flash kernel (mode 3): head 0's weights never reach HBM
+    AttnFlashArgs a = fa;
+    a.t1t = t1t;
+    a.o8 = d_o8;
+    a.ldt = R8;
+    a.hid = hid;
+    a.y = h3 + 2 * hid;
+    a.ldy = 3 * hid;
+    a.z = z;
     prof_begin("attn_nonlin");
-    gemm_nonlin_bf16(p, t1t, st_);
+    launch_attn_flash(a, 3, st_);
     prof_end();
-    }
     linear_h(Ly.na_out, z, true, hid, R, X, false, d, EPI_RESADD);
   } else if (np) {
     // z = (A0 @ t1) * y on the split-bf16 GEMM: A0 [L][L8] f32 (split while staging),
@@ -1190,7 +1156,7 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
     prof_begin("elementwise");
     launch_nonlin_prep_t(h3, false, d_off, d_o8, d_map, R, hid, R8, t1t, st_, np);
     prof_end();
-    if (np == kPiecesF16 && nonlin_fused()) {
+    if (np == kPiecesF16) {
       // f16x3: z = (A0 @ t1) * y in the flash kernel (mode 3, fp16 pieces of P and t1)
       AttnFlashArgs a = fa;
       a.t1t = t1t;
@@ -1442,14 +1408,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       prof_end();
       float* y3 = ws<float>("fe_y3", (size_t)mL.total * 19 * 128);
       prof_begin("frontend_conv");
-      static const bool dw_old = getenv("ZASR_DWCONV_OLD") != nullptr;
-      if (dw_old)
-        launch_dwconv2d(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
-      else
-        launch_dwconv2d_tiled(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
+      launch_dwconv2d_tiled(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
       prof_end();
-      static const bool cx_unfused = getenv("ZASR_CONVNEXT_UNFUSED") != nullptr;
-      if (model_.pw1.wp && model_.pw2.wp && split_pieces() == kPiecesF16 && !cx_unfused) {
+      if (model_.pw1.wp && model_.pw2.wp && split_pieces() == kPiecesF16) {
         // f16x3: pw1 -> SwooshL -> pw2 + residual in one kernel, the hidden layer on chip
         prof_begin("frontend_conv");
         launch_convnext_mlp_h3(y3, x3, (long)mL.total * 19, model_.pw1.wp, model_.pw1.b,
@@ -1469,10 +1430,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
 
   // ---------------- encoder stacks ----------------
   if (bf16)  // (the fused NonlinAttention never materialises head 0's weights)
-    ws<__bf16>("ly_attn_h", nonlin_fused() ? 1 : std::max<size_t>(attn_floats, 1));
+    ws<__bf16>("ly_attn_h", 1);
   else
-    ws<float>("ly_attn", split_pieces() == kPiecesF16 && nonlin_fused()
-                             ? 1 : std::max<size_t>(attn_floats, 1));
+    ws<float>("ly_attn", split_pieces() == kPiecesF16 ? 1 : std::max<size_t>(attn_floats, 1));
   const int Dm = cfg.max_dim();
   float* full = ws<float>("st_full", (size_t)mL.total * Dm);
   // stack i's input (50 Hz, width d_i): stack 0 takes the embed output, every later one is
@@ -1591,12 +1551,6 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   st.node_lp = ws<double>("se_nlp", ncap);
   st.node_stats = ws<float4>("se_nst", ncap);
   st.node_count = ws<int>("se_ncnt", S);
-  st.stamps = nullptr;
-  const bool stamps = getenv("ZASR_STAMPS") != nullptr;
-  if (stamps) {
-    st.stamps = ws<unsigned long long>("se_stamps", (size_t)Tmax * 16);
-    ZASR_HIP_CHECK(hipMemsetAsync(st.stamps, 0, (size_t)Tmax * 16 * 8, st_));
-  }
   float* logits = ws<float>("se_logits", slots * V);
   // split-bf16 modes: J written once as `np` packed bf16 pieces (store_j4), the joiner on the
   // packed W pieces; bf16: one packed bf16 image
@@ -1604,8 +1558,7 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   const bool bf16 = model_.joiner.wh != nullptr;
   // bf16 with the decoder-context table: J in fragment order for the packed joiner (every
   // J writer goes through store_j4); without the table decjoin writes row-major J
-  static const bool no_pack = getenv("ZASR_JOINER_UNPACKED") != nullptr;
-  const bool packed = (bf16 || jnp > 0) && model_.joiner_packed && model_.dec_table && !no_pack;
+  const bool packed = (bf16 || jnp > 0) && model_.joiner_packed && model_.dec_table;
   const int jpc = packed && jnp > 0 ? stored_pieces(jnp) : 1;  // packed images of J
   const bool j16 = bf16 || packed;              // J buffer in bf16 elements
   const size_t jrows = (size_t)joiner_packed_rows((long)slots);
@@ -1697,8 +1650,7 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   // frame; two chains interleave their launch and scheduling waits).  Group g holds the
   // streams order[g], order[g + G], ... (each group sorted by T' descending, active streams
   // a prefix), laid out contiguously; the search final runs over all of them.
-  static const int env_groups = getenv("ZASR_SEARCH_GROUPS") ? atoi(getenv("ZASR_SEARCH_GROUPS")) : 2;
-  const int G = split_groups ? std::max(1, std::min({env_groups, 2, S})) : 1;
+  const int G = split_groups ? std::min(2, S) : 1;
   if (G > 1) {
     std::vector<int> reord;
     for (int g = 0; g < G; ++g)
@@ -1732,7 +1684,6 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
     q.st.hw += so; q.st.node += so; q.st.nh += q.s0;
     q.st.node_tok += no; q.st.node_frame += no; q.st.node_parent += no; q.st.node_lp += no;
     q.st.node_stats += no; q.st.node_count += q.s0;
-    if (g > 0) q.st.stamps = nullptr;
     q.stream = g == 0 ? st_ : stream3_;
     if (g == 0) {
       q.J = J;
@@ -1809,8 +1760,6 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
   job.cap = cap;
   job.Tmax = Tmax;
   job.order = order;
-  job.stamps = stamps;
-  job.d_stamps = st.stamps;
   int* o_tok = ws<int>("so_tok", (size_t)S * cap);
   int* o_fr = ws<int>("so_fr", (size_t)S * cap);
   double* o_lp = ws<double>("so_lp", (size_t)S * cap);
@@ -1863,28 +1812,6 @@ std::vector<TokenResult> Engine::collect_search(SearchJob& job) {
     ZASR_HIP_CHECK(hipDeviceSynchronize());
     throw std::runtime_error("precision f16x3: non-finite encoder output (an activation exceeded "
                              "the fp16 range of the split operands); decode with bf16x6 or fp32");
-  }
-  if (job.stamps) {  // diagnostic: mean phase cycles of the search step (block 0)
-    const int Tmax = job.Tmax;
-    std::vector<unsigned long long> hs((size_t)Tmax * 16);
-    ZASR_HIP_CHECK(hipMemcpy(hs.data(), job.d_stamps, hs.size() * 8, hipMemcpyDeviceToHost));
-    const int seq[] = {0, 6, 7, 8, 10, 1, 2, 3, 4, 5};
-    const char* name[] = {"nh", "row0_max", "row0_stats", "row0_topk", "rows_decode", "barrier",
-                          "rank", "tail", "J"};
-    const int NS = 9;
-    double acc[16] = {0};
-    int cnt = 0;
-    for (int t = 0; t < Tmax; ++t) {
-      const unsigned long long* p = &hs[(size_t)t * 16];
-      bool ok = true;
-      for (int k = 0; k <= NS; ++k) ok = ok && p[seq[k]] != 0;
-      if (!ok) continue;
-      for (int k = 0; k < NS; ++k) acc[k] += (double)(p[seq[k + 1]] - p[seq[k]]);
-      ++cnt;
-    }
-    fprintf(stderr, "[zasr stamps] frames=%d mean cycles:", cnt);
-    for (int k = 0; k < NS; ++k) fprintf(stderr, " %s %.0f", name[k], cnt ? acc[k] / cnt : 0.0);
-    fprintf(stderr, "\n");
   }
   for (int i = 0; i < S; ++i) {
     TokenResult& r = res[job.order[i]];
@@ -2010,9 +1937,8 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
   const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
   // L: batches whose encoders are queued ahead of the search in flight, one more than the
   // encoder streams (at most kMaxEnc: L + 1 output slots): 111.8-113.1k -> 113.5-114.3k xRT
-  // on one box (profiles/r03/enc_ahead/); ZASR_ENC_AHEAD overrides
-  static const int env_ahead = getenv("ZASR_ENC_AHEAD") ? atoi(getenv("ZASR_ENC_AHEAD")) : 0;
-  const int L = std::max(E, std::min({env_ahead > 0 ? env_ahead : E + 1, (int)kMaxEnc, nb}));
+  // on one box (profiles/r03/enc_ahead/)
+  const int L = std::max(E, std::min({E + 1, (int)kMaxEnc, nb}));
   // encoder stream 0 is the caller's stream, or (CU-partitioned) the engine's masked stream
   hipStream_t enc_st[kMaxEnc] = {search_cus_ > 0 ? stream_ : main_st};
   for (int e = 1; e < kMaxEnc; ++e) enc_st[e] = enc_extra_[e - 1];

@@ -192,9 +192,7 @@ class Engine {
   struct SearchJob {
     int S_all = 0, S = 0, cap = 0, set = 0, Tmax = 0;
     std::vector<int> order, t_out;
-    bool stamps = false;
     bool check_finite = false;  // f16x3: the encoder output's fp16-range guard
-    unsigned long long* d_stamps = nullptr;
     hipStream_t stream = nullptr;
   };
   void launch_search(const float* d_enc, const std::vector<int>& t_out, int beam, int set,

@@ -93,10 +93,6 @@ void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream
 // A = f32 activations rounded to bf16 while staging (or bf16 when a_bf16: p.A then points
 // at __bf16 data); f32 accumulate and epilogue; C written as f32 (or bf16 when c_bf16).
 // Requires N, ldc (and ldaux for EPI_MULAUX) to be multiples of 4.
-// The NonlinAttention product z = (A0 @ t1) * y per sequence (z-slices): A0 bf16 [L][L32],
-// t1^T bf16 [hid][R32] (every slice's K = L32 a multiple of 32, zero-padded), y bf16 aux, z
-// bf16; the multi-stage LDS-DMA kernel (K = L-deep panels, several slabs in flight).
-void gemm_nonlin_bf16(const GemmParams& p, const void* Bw, hipStream_t st);
 
 void gemm_bf16(const GemmParams& p, const void* Bw, int epi, int aload, hipStream_t stream,
                bool a_bf16 = false, bool c_bf16 = false);

@@ -213,13 +213,13 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_f32_kernel(GemmPar
   }
 }
 
-int g_gemm_f32_deep = -1;  // ZASR_GEMM_DEEP (shared with the bf16 kernel's switch)
+int g_gemm_f32_deep = -1;  // the two-slab prefetch (gemm_set_deep: the labs' A/B switch)
 
 template <int BM, int BN, int WM, int WN, int ALOAD, bool BNC, int EPI>
 void launch_t(const GemmParams& p, hipStream_t st) {
   dim3 grid(cdiv(p.N, BN), cdiv(p.max_M, BM), p.slices ? p.num_slices : 1);
   if (g_gemm_f32_deep < 0)
-    g_gemm_f32_deep = getenv("ZASR_GEMM_DEEP") ? atoi(getenv("ZASR_GEMM_DEEP")) : 1;
+    g_gemm_f32_deep = 1;
   if (g_gemm_f32_deep && !p.slices && p.K % (2 * BK) == 0) {
     hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, true>), grid,
                        dim3(64 * WM * WN), 0, st, p);
@@ -698,7 +698,7 @@ __attribute__((amdgpu_waves_per_eu(WAVES_M * WAVES_N >= 8 ? 4 : 1))) void gemm_b
   }
 }
 
-// ZASR_GEMM_DEEP=0 turns the two-slab register prefetch off (gemm_set_deep for the labs)
+// gemm_set_deep(0) turns the two-slab register prefetch off (the labs' A/B switch)
 static int g_gemm_deep = -1;
 void gemm_set_deep(int on) { g_gemm_deep = g_gemm_f32_deep = on; }
 
@@ -706,7 +706,7 @@ template <int BM, int BN, int BK, int WM, int WN, int ALOAD, int EPI, typename T
 void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
-  if (g_gemm_deep < 0) g_gemm_deep = getenv("ZASR_GEMM_DEEP") ? atoi(getenv("ZASR_GEMM_DEEP")) : 1;
+  if (g_gemm_deep < 0) g_gemm_deep = 1;
   if (g_gemm_deep && ALOAD == ALOAD_DENSE && !p.slices && p.K % (2 * BK) == 0 && p.lda % 8 == 0) {
     hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, true>), grid,
                        dim3(64 * WM * WN), 0, st, p, Bw, tn, tm);
@@ -729,22 +729,10 @@ void launch_tile_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   // wide tiles: 128 x 256 on 8 waves (2 x 4, 64 x 64 each) for N >= 256 -- twice the MFMAs
   // per A slab and per barrier of the 128 x 128 kernel, each A row panel read by half as many
   // blocks; measured -5 % enc_gemm time at the bench's shapes (profiles/r01/v15_gemm_tiles.txt).
-  // ZASR_GEMM_TILE: 0 = 128 x 128 only, 1 = 256 x 128 (8 waves), 2 = 128 x 256 (default),
-  // 4 = 128 x 256 for N >= 512 else 256 x 128 (256 x 256 measured 7 % slower: removed).
-  // A two-slab register prefetch (two K slabs in flight in two register sets behind the LDS
-  // slab) measured enc_gemm 16.7 -> 21.1 ms per step and was dropped (v17)
-  static const int tile_mode = getenv("ZASR_GEMM_TILE") ? atoi(getenv("ZASR_GEMM_TILE")) : 2;
-  if (BN == 128 && big && tile_mode == 1 && blocks128 >= 1024) {
-    launch_h<256, 128, BK, 4, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
-    return;
-  }
-  if (BN == 128 && big && tile_mode == 4) {
-    if (p.N >= 512) launch_h<128, 256, BK, 2, 4, ALOAD, EPI, TA, TC>(p, Bw, st);
-    else if (blocks128 >= 1024) launch_h<256, 128, BK, 4, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
-    else launch_h<128, 128, BK, 2, 2, ALOAD, EPI, TA, TC>(p, Bw, st);
-    return;
-  }
-  if (BN == 128 && big && tile_mode == 2 && p.N >= 256) {
+  // (256 x 128 on 8 waves, and 128 x 256 for N >= 512 only, measured slower; 256 x 256 7 %
+  // slower.)  A two-slab register prefetch (two K slabs in flight in two register sets behind
+  // the LDS slab) measured enc_gemm 16.7 -> 21.1 ms per step and was dropped (v17)
+  if (BN == 128 && big && p.N >= 256) {
     launch_h<128, 256, BK, 2, 4, ALOAD, EPI, TA, TC>(p, Bw, st);
     return;
   }
@@ -1009,19 +997,14 @@ void launch_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
                      tn);
 }
 
-int glds_mode() {  // ZASR_GEMM_GLDS=0 selects the register-staged kernel (A/B runs)
-  const char* e = getenv("ZASR_GEMM_GLDS");
-  return e ? atoi(e) : 1;
-}
 
 // the multi-stage kernel for the long-K / wide-N projections (dense, K % 32 == 0)
 template <int EPI, typename TA, typename TC>
 bool try_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   // measured (tools/rp_bench.hip): ahead of the register-staged kernel only on the long-K
   // bf16-A output projections (K >= 1024: +11 %); behind it on the short-K / f32-A shapes
-  const int mode = glds_mode();
-  if (mode == 0 || p.slices != nullptr || p.K % 32 != 0 || p.K < 128 || p.M < 128) return false;
-  if (mode == 1 && (std::is_same<TA, float>::value || p.K < 1024)) return false;
+  if (p.slices != nullptr || p.K % 32 != 0 || p.K < 128 || p.M < 128) return false;
+  if (std::is_same<TA, float>::value || p.K < 1024) return false;
   if (p.lda % (std::is_same<TA, float>::value ? 4 : 8) != 0 || p.sbn % 8 != 0) return false;
   if (std::is_same<TA, float>::value)
     launch_glds<3, EPI, TA, TC>(p, Bw, st);
@@ -1100,36 +1083,6 @@ void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
 }
 
 }  // namespace
-
-void gemm_nonlin_bf16(const GemmParams& p, const void* Bw, hipStream_t st) {
-  ZASR_REQUIRE(p.slices != nullptr && p.num_slices > 0, "gemm_nonlin_bf16: needs z-slices");
-  ZASR_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && p.ldaux % 4 == 0 && p.sbn % 8 == 0,
-               "gemm_nonlin_bf16: N, ldc, ldaux multiples of 4 and sbn of 8");
-  if (p.max_M <= 0) return;
-  // BN 64 when it wastes fewer padded columns (hid 144 / 192 / 288 -> 192 / 192 / 320)
-  const int pad64 = cdiv(p.N, 64) * 64, pad128 = cdiv(p.N, 128) * 128;
-  const int tm = cdiv(p.max_M, 128);
-  const __bf16* B = reinterpret_cast<const __bf16*>(Bw);
-  // BN 192: one column tile for hid 144 / 192 (and two for 384), so each sequence's K = L-deep
-  // weight panel is streamed once per row tile instead of 2-3x: attn_nonlin 1.71 -> 1.58 ms
-  // per step (profiles/r03/nonlin_bn192/; ZASR_NONLIN_BN=0 restores the 64 / 128 tiles)
-  static const int nl_bn = getenv("ZASR_NONLIN_BN") ? atoi(getenv("ZASR_NONLIN_BN")) : 192;
-  if (nl_bn == 192 && (p.N <= 192 || p.N % 192 == 0)) {
-    const int tn = cdiv(p.N, 192);
-    hipLaunchKernelGGL((gemm_glds_kernel<4, EPI_MULAUX16, __bf16, __bf16, 192, true>),
-                       dim3(tn * tm * p.num_slices), dim3(256), 0, st, p, B, tn, tm);
-    return;
-  }
-  if (pad64 < pad128) {
-    const int tn = cdiv(p.N, 64);
-    hipLaunchKernelGGL((gemm_glds_kernel<4, EPI_MULAUX16, __bf16, __bf16, 64, true>),
-                       dim3(tn * tm * p.num_slices), dim3(256), 0, st, p, B, tn, tm);
-  } else {
-    const int tn = cdiv(p.N, 128);
-    hipLaunchKernelGGL((gemm_glds_kernel<4, EPI_MULAUX16, __bf16, __bf16, 128, true>),
-                       dim3(tn * tm * p.num_slices), dim3(256), 0, st, p, B, tn, tm);
-  }
-}
 
 void gemm_f32(const GemmParams& p, int epi, int aload, bool b_ncontig, hipStream_t st) {
   ZASR_REQUIRE(p.N > 0, "gemm: N must be positive");

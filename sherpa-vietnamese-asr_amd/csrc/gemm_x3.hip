@@ -651,57 +651,31 @@ void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t
                      tn, tm);
 }
 
-// ZASR_H3_GLDS: 0 = the register-staged kernel only; 2 / 3 = LDS-DMA stages, 2x2 waves;
-// 4 = two stages, 4x1 waves (A/B runs; the register-A and deep-ring variants measured in
-// round 4 are gone)
-int h3_glds_mode() {
-  const char* e = getenv("ZASR_H3_GLDS");
-  return e ? atoi(e) : 2;
-}
-
-// fp16 pieces (FMT 1): BK = 16 keeps two stages at 41 KB of LDS (3 blocks per CU)
+// fp16 pieces (FMT 1).  The LDS-DMA kernel wherever its operand layout fits; the register-
+// staged kernel (BK = 16: two stages at 41 KB of LDS, 3 blocks per CU) for the rest.  (The
+// round-4 2 x 2-wave LDS-DMA layouts, the register-A and deep-ring variants measured slower and
+// are gone; NonlinAttention runs fused in the attention kernel in this mode, so
+// no z-sliced dense GEMM reaches here.)
 template <int ALOAD, int EPI>
 void launch_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   if constexpr (ALOAD == ALOAD_CONV3) {
     // (z-sliced launches carry K in the slices; the conv.7 loader's K is 9 taps x 32 = 288)
-    if (h3_glds_mode() != 0 && (p.slices ? p.max_M > 0 : p.K == 288 && p.M >= 128) &&
-        p.N % 128 == 0 && p.sbn == 288)
+    if ((p.slices ? p.max_M > 0 : p.K == 288 && p.M >= 128) && p.N % 128 == 0 && p.sbn == 288)
       return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_CONV3, 1>(p, Bw, blo, st);
   }
   if constexpr (ALOAD == ALOAD_DENSE) {
-    const int mode = h3_glds_mode();
     // any N % 4 == 0: the B rows past N are clamped loads, the epilogue stores col < N only
     // (the attention in-projections: N = 68 H = 272 / 544, the value projection 12 H = 48)
-    if (mode != 0 && !p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 &&
-        p.M >= 128 && p.N % 4 == 0) {
-      const bool w128 = cdiv(p.N, 128) * 128 * 10 <= cdiv(p.N, 64) * 64 * 11;
-      if (mode == 1) {  // the round-4 layouts before the read-before-issue loop (A/B runs)
-        if (p.N % 128 == 0) return launch_glds_h3<2, EPI, 128>(p, Bw, blo, st);
-        if (p.N % 64 == 0) return launch_glds_h3<2, EPI, 64, 4>(p, Bw, blo, st);
-      }
+    if (!p.slices && p.K % 32 == 0 && p.lda % 4 == 0 && p.sbn % 8 == 0 && p.M >= 128 &&
+        p.N % 4 == 0) {
       // 4 x 1 waves (each A element split by one wave), the stage's fragments read before
       // the next stage's DMA (split_lab_tiles_v7: 0.28-0.34 of the fp16 peak on the FFN /
       // projection shapes vs 0.24-0.27 for the 2 x 2 loop that issued first)
-      if (w128) return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
-      return launch_glds_h3<2, EPI, 64, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
-    }
-    // z-sliced (NonlinAttention's A0 @ t1 per sequence): every slice's K and lda are its
-    // L rounded up to 32 (engine.cpp's sl_nl), its offsets 32-element aligned
-    if (mode != 0 && p.slices && p.sbn % 8 == 0 && p.N % 4 == 0 && p.max_M > 0 &&
-        getenv("ZASR_NONLIN_X3") == nullptr) {
       const bool w128 = cdiv(p.N, 128) * 128 * 10 <= cdiv(p.N, 64) * 64 * 11;
       if (w128) return launch_glds_h3<2, EPI, 128, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
       return launch_glds_h3<2, EPI, 64, 4, 3, ALOAD_DENSE, 1>(p, Bw, blo, st);
     }
   }
-  // NonlinAttention's per-sequence GEMM (z-slices; A = head 0's f32 weights, K = the
-  // sequence length): every column tile re-reads the L x L A panel, so N = 144 (d = 192) takes
-  // one 160-wide tile instead of five 32-wide ones and N = 288 three 96-wide instead of five
-  // 64-wide (4 x 1 waves, FN = 5 / 3)
-  if (p.slices && p.N > 128 && p.N <= 160)
-    return launch_x3_t<128, 160, 4, 1, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
-  if (p.slices && p.N > 256 && p.N <= 288)
-    return launch_x3_t<128, 96, 4, 1, ALOAD, EPI, 2, 16, 1>(p, Bw, blo, st);
   const int pad128 = cdiv(p.N, 128) * 128, pad64 = cdiv(p.N, 64) * 64, pad32 = cdiv(p.N, 32) * 32;
   const int BN = (pad128 * 100 <= pad32 * 115) ? 128 : (pad64 * 100 <= pad32 * 115 ? 64 : 32);
   const long blocks128 = (long)cdiv(p.max_M, 128) * cdiv(p.N, BN) * (p.slices ? p.num_slices : 1);

@@ -152,8 +152,6 @@ void launch_convnext_mlp_h3(const float* y, const float* x, long npos, const voi
 // channels per block, staged values reused by up to 7 output frames); same FMA order per output
 void launch_dwconv2d_tiled(const float* x, const int* L_off, const int* L_map, int total_rows,
                            const float* w, const float* b, float* out, hipStream_t st);
-void launch_dwconv2d(const float* x, const int* L_off, const int* L_map, int total_rows,
-                     const float* w /*[128][49]*/, const float* b, float* out, hipStream_t st);
 
 // ---- Zipformer2 encoder elementwise / per-sequence kernels ----
 // y = x * exp(log_scale) * rsqrt(mean((x - bias)^2));  optionally y = orig + (y - orig) * s
@@ -316,7 +314,6 @@ struct SearchState {
   float4* node_stats;   // (entropy, sum p^(1/3), top1, top2) of the emitting joiner row
   int* node_count;      // [S]
   int node_cap;
-  unsigned long long* stamps;  // diagnostic phase timestamps of block 0 ([frame][8]) or null
 };
 struct HotwordTables {
   int num_states;       // 0 => no hotwords
@@ -382,7 +379,7 @@ struct DecTable {
   void* J;                  // [S*H][D] joiner input of the next frame (bf16 if j_bf16)
   int D;
   int j_bf16;
-  int j_packed = 0;         // bf16 J in MFMA-fragment order (joiner_packed_kernel's A operand)
+  int j_packed = 0;         // bf16 J in MFMA-fragment order (the packed joiner's A operand)
   // split-bf16 modes with j_packed: J = tanh() in f32 written as j_pieces bf16 pieces
   // (p0 = bf16(x), p1 = bf16(x - p0), ...), piece t at element offset t * j_plane
   int j_pieces = 0;

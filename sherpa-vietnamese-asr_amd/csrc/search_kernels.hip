@@ -164,12 +164,6 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp_f<kDppRor8>(v);
   return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
-__device__ __forceinline__ float row_max_dpp(float v) {  // every lane: its 16-lane row's max
-  v = fmaxf(v, dpp_f<kDppQuad1>(v));
-  v = fmaxf(v, dpp_f<kDppQuad2>(v));
-  v = fmaxf(v, dpp_f<kDppRor4>(v));
-  return fmaxf(v, dpp_f<kDppRor8>(v));
-}
 __device__ __forceinline__ float wave_min_dpp(float v) {
   v = fminf(v, dpp_f<kDppQuad1>(v));
   v = fminf(v, dpp_f<kDppQuad2>(v));
@@ -196,29 +190,10 @@ __device__ __forceinline__ void wave_max2_dpp(float& m1, float& m2) {
   m1 = r1;
   m2 = r2;
 }
-template <int CTRL>
-__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
-  const int lo = dpp_i<CTRL>((int)(unsigned)v), hi = dpp_i<CTRL>((int)(unsigned)(v >> 32));
-  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
 __device__ __forceinline__ unsigned long long lane_u64(unsigned long long v, int l) {
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
   return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ unsigned long long wave_max_u64_dpp(unsigned long long v) {
-  unsigned long long o;
-  o = dpp_u64<kDppQuad1>(v); v = o > v ? o : v;
-  o = dpp_u64<kDppQuad2>(v); v = o > v ? o : v;
-  o = dpp_u64<kDppRor4>(v); v = o > v ? o : v;
-  o = dpp_u64<kDppRor8>(v); v = o > v ? o : v;
-  unsigned long long r = lane_u64(v, 0);
-#pragma unroll
-  for (int l = 16; l < 64; l += 16) {
-    const unsigned long long x = lane_u64(v, l);
-    r = x > r ? x : r;
-  }
-  return r;
 }
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_f<kDppQuad1>(v));
@@ -246,13 +221,6 @@ __device__ __forceinline__ int wave_min_i_dpp(int v) {
 
 // tanh(x) = 1 - 2 / (exp(2x) + 1): saturates correctly at +-inf (bf16 joiner input only)
 __device__ __forceinline__ float fast_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
-
-// diagnostic phase stamp (block 0, thread 0 only; st.stamps null in normal runs)
-#define ZASR_STAMP(slot)                                                                  \
-  do {                                                                                    \
-    if (st.stamps && blockIdx.x == 0 && threadIdx.x == 0)                                 \
-      st.stamps[(long)t * 16 + (slot)] = __builtin_amdgcn_s_memtime();                     \
-  } while (0)
 
 }  // namespace
 
@@ -587,61 +555,12 @@ void launch_joiner_split(const JoinerArgs& j, hipStream_t st) {
 }
 
 // --------------------------------------------------------------------------------------
-// speculative-greedy joiner on fragment-packed J / W (kernels.h JoinerPackedArgs)
-template <int QK>
-__global__ __launch_bounds__(256) void joiner_packed_kernel(JoinerPackedArgs j) {
-  // one LDS array: [J tile: 2 row tiles][W tile: 2 column groups], each QK x 1 KB
-  __shared__ __attribute__((aligned(1024))) bf16x8 sOp[4 * QK * 64];
-  bf16x8* const sJ = sOp;
-  bf16x8* const sW = sOp + 2 * QK * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int m0 = blockIdx.y * 64;
-  if (tile_done(j.live_t, j.live_len, j.live_f, m0, j.M) &&
-      (m0 + 32 >= j.M || tile_done(j.live_t, j.live_len, j.live_f, m0 + 32, j.M)))
-    return;  // block-uniform: every stream of these 64 rows has finished
-  const int g0 = blockIdx.x * 2;
-  const bf16x8* srcJ = reinterpret_cast<const bf16x8*>(j.Jp) + (long)(m0 >> 5) * QK * 64;
-  const bf16x8* srcW = reinterpret_cast<const bf16x8*>(j.Wp) + (long)g0 * QK * 64;
-  // both tiles are lane-linear 1 KB fragments: LDS-DMA (global_load_lds, 16 B per lane), no
-  // VGPR staging and no ds_write pass; wave w moves chunks [w * 2QK/4, (w + 1) * 2QK/4)
-  constexpr int CPW = 2 * QK / 4;
-#pragma unroll
-  for (int c = 0; c < CPW; ++c) {
-    const int ch = wid * CPW + c;
-    __builtin_amdgcn_global_load_lds(const_cast<bf16x8*>(srcJ + ch * 64 + lane),
-                                     (__attribute__((address_space(3))) void*)(sJ + ch * 64), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(const_cast<bf16x8*>(srcW + ch * 64 + lane),
-                                     (__attribute__((address_space(3))) void*)(sW + ch * 64), 16, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int rt = wid >> 1, gc = wid & 1;
-  const int row0 = m0 + 32 * rt;
-  if (row0 >= j.M) return;
-  f32x16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-  for (int q = 0; q < QK; ++q)
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sJ[(rt * QK + q) * 64 + lane],
-                                                  sW[(gc * QK + q) * 64 + lane], acc, 0, 0, 0);
-  const int col = (g0 + gc) * 32 + (lane & 31);
-  if (col >= j.V) return;
-  const float bb = j.bias[col];
-  const int h = lane >> 5;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (row < j.M) j.out[(long)row * j.V + col] = acc[r] + bb;
-  }
-}
-
-// Register-staged variant: no LDS.  Each wave streams its own J row tile and W column group
-// (1 KB coalesced fragment loads, 8 fragments of each in flight ahead of the MFMAs) -- twice
-// the L2 reads of the LDS-shared kernel, but a block needs no LDS and few VGPRs, so under the
-// batch pipeline it co-resides with the next batch's encoder GEMM blocks instead of waiting
-// for whole CUs to drain (the LDS kernel's 128 KB per block fits only on an empty CU).
-// Same fragments, same MFMA order: bit-identical logits.
+// speculative-greedy / beam joiner on fragment-packed J / W (kernels.h JoinerPackedArgs).
+// Register-staged: no LDS.  Each wave streams its own J row tile and W column group (1 KB
+// coalesced fragment loads, 8 fragments of each in flight ahead of the MFMAs) -- twice the L2
+// reads of an LDS-shared tile, but a block needs no LDS and few VGPRs, so under the batch
+// pipeline it co-resides with the next batch's encoder GEMM blocks instead of waiting for whole
+// CUs to drain.
 template <int QK>
 __global__ __launch_bounds__(256) void joiner_reg_kernel(JoinerPackedArgs j) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -784,17 +703,11 @@ void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st) {
     }
     return;
   }
-  // ZASR_JOINER_LDS=1: the LDS-shared kernel (lowest latency on an idle GPU)
-  static const bool lds = getenv("ZASR_JOINER_LDS") != nullptr && atoi(getenv("ZASR_JOINER_LDS")) != 0;
+  // (an LDS-shared variant, every operand by LDS-DMA, measured 12 % slower under the batch
+  // pipeline: it needs whole CUs)
   switch (j.D) {
-    case 256:
-      if (lds) hipLaunchKernelGGL(joiner_packed_kernel<16>, grid, dim3(256), 0, st, j);
-      else hipLaunchKernelGGL(joiner_reg_kernel<16>, grid, dim3(256), 0, st, j);
-      break;
-    case 512:
-      if (lds) hipLaunchKernelGGL(joiner_packed_kernel<32>, grid, dim3(256), 0, st, j);
-      else hipLaunchKernelGGL(joiner_reg_kernel<32>, grid, dim3(256), 0, st, j);
-      break;
+    case 256: hipLaunchKernelGGL(joiner_reg_kernel<16>, grid, dim3(256), 0, st, j); break;
+    case 512: hipLaunchKernelGGL(joiner_reg_kernel<32>, grid, dim3(256), 0, st, j); break;
     default: throw std::runtime_error("packed joiner: joiner dim must be 256 or 512");
   }
 }
@@ -937,7 +850,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
   __shared__ int sKK;
   __shared__ unsigned long long sFmask;
 
-  ZASR_STAMP(0);
   const int V4 = V >> 2;
   const float4* rows4 = reinterpret_cast<const float4*>(logits + (long)base * V);
   // this wave's first row, issued before anything else (rows >= nh hold stale but valid data)
@@ -969,7 +881,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
   }
   const int node_base = st.node_count[s];
   const int n = st.nh[s];
-  if (n != 12345) ZASR_STAMP(6);
   const bool use_hw = hw.num_states > 0;
   // the next frame's encoder row (every wave writes J rows of candidates in step 4)
   float4 ev[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
@@ -1012,7 +923,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       upd(xa[q].z);
       upd(xa[q].w);
     }
-    if (h == 0 && m1 != 12345.f) ZASR_STAMP(7);
     // candidate threshold: lane groups (DPP): KB >= 16: the 16 quads; KB = 8: overlapping
     // quad pairs (q, q - 1), of which the 8 pairs (2i, 2i + 1) are disjoint, so the minimum
     // over all of them is still a bound; KB <= 4: the four 16-lane rows
@@ -1041,7 +951,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     e1 = wave_sum_dpp(e1);
     e3 = wave_sum_dpp(e3);
     const float ls = logf(se);
-    if (h == 0 && ls != 12345.f) ZASR_STAMP(8);
     if (lane == 0)
       sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
                               __expf(m2 - m1) / se);
@@ -1100,7 +1009,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       // exact unless an element below the threshold can tie the KB-th lp
       fast = kth != 0ull && lane_f(val, __ffsll((long long)kth) - 1) != score(thr_x);
     }
-    if (h == 0 && total != 12345) ZASR_STAMP(10);
     if (!fast) {
       // slow path: pop in (x desc, index asc) order -- per lane the head and second of its
       // elements, the popped lane promoting its second or rescanning what follows -- until
@@ -1224,9 +1132,7 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       }
     }
   }
-  ZASR_STAMP(1);
   __syncthreads();
-  ZASR_STAMP(2);
   // ---- 3. expansion (:1110-1138): ranking and duplicate merge in wave 0 ----
   const int total_c = n * V;
   const int k = beam < total_c ? beam : total_c;
@@ -1247,7 +1153,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     if (lane == 0) sKK = kk;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    ZASR_STAMP(3);
     // 3b. duplicates of the full sequence merge into their first occurrence, in candidate
     //     order, with an f64 log-add (:1133-1138)
     const bool lv = lane < kk;
@@ -1309,7 +1214,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       sFmask = fmask;
     }
   }
-  ZASR_STAMP(4);
   // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]),
   //         candidate c by wave c % 8 ----
   if constexpr (TABLE) {
@@ -1331,7 +1235,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       }
     }
   }
-  ZASR_STAMP(5);
 }
 
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
@@ -1564,11 +1467,8 @@ __global__ __launch_bounds__(256) void greedy_spec_kernel(SearchState st, const 
       break;
     }
   const int t_new = t0 + (fe >= 0 ? fe + 1 : nf);
-  int ny1 = y1, ny2 = y2;
   if (fe >= 0) {
     const int tok = sTok[fe];
-    ny2 = y1;
-    ny1 = tok;
     if ((fe & 3) == wid) {
       // owner wave: the entropy terms of row fe (search_step_kernel's statistics)
       // row r = fe >> 2 of this wave, chosen by selects (a dynamic register-array index
