@@ -81,6 +81,12 @@ def parse_args(argv=None):
                          "chunks_identical_to_fp32 is measured against")
     ap.add_argument("--parity-steps", type=int, default=0,
                     help="timed steps of the parity-mode line (default: --steps)")
+    ap.add_argument("--weights", default="greedy-calibrated",
+                    choices=["greedy-calibrated", "beam-calibrated"],
+                    help="synthetic weight variant (zasr.model.WEIGHT_VARIANTS): greedy-calibrated "
+                         "(default; ~18 %% of frames emit under greedy, ~6 %% under beam 8) or "
+                         "beam-calibrated (peaked non-blank joiner rows: beam 8 emits at the greedy "
+                         "rate, ~18 %%, as a trained model does; 68M only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5,
                     help="CPU baseline: 1 warm-up then the mean of this many repeats "
@@ -213,7 +219,10 @@ def hour_golden(args, beam, hotwords, chunks):
     encoder -> the reference's _ort_beam_search restated, core/asr_engine.py:1023-1153), or
     None when this run's workload is not the one the file holds.  Data only: nothing of the
     oracle runs here."""
-    if args.model != "zipformer-68m" or args.audio_sec != 3600.0 or not os.path.exists(HOUR_GOLDEN):
+    variant = getattr(args, "weights", "greedy-calibrated")
+    path = HOUR_GOLDEN if variant == "greedy-calibrated" else \
+        HOUR_GOLDEN.replace(".json", f"_{variant}.json")
+    if args.model != "zipformer-68m" or args.audio_sec != 3600.0 or not os.path.exists(path):
         return None
     if beam == 1:
         key = "greedy"
@@ -221,7 +230,7 @@ def hour_golden(args, beam, hotwords, chunks):
         key = "beam8_hw"
     else:
         return None
-    with open(HOUR_GOLDEN) as f:
+    with open(path) as f:
         g = json.load(f)
     if [int(c.shape[0]) for c in chunks] != g["chunk_samples"]:
         return None
@@ -231,13 +240,13 @@ def hour_golden(args, beam, hotwords, chunks):
         h.update(np.ascontiguousarray(c, dtype=np.float32).tobytes())
     if h.hexdigest()[:32] != g["audio_sha256_32"]:
         return None
-    return key, g[key]
+    return key, g[key], path.replace("bench_hour_oracle", "bench_hour_audit")
 
 
 HOUR_AUDIT = os.path.join(REPO, "tests", "golden", "bench_hour_audit.json")
 
 
-def oracle_agreement(key, ref, got_steps):
+def oracle_agreement(key, ref, got_steps, audit_path=HOUR_AUDIT):
     """Token agreement of every timed step's decode (a list of per-chunk token lists per step)
     with the oracle golden: chunks identical (worst step), token error rate of the last step,
     and whether every differing chunk is one of the audited f32 ties of
@@ -250,13 +259,14 @@ def oracle_agreement(key, ref, got_steps):
     nref = sum(len(t) for t in ref)
     diff = [i for i, (a, b) in enumerate(zip(last, ref)) if a != b]
     audited = None
-    if os.path.exists(HOUR_AUDIT):
-        with open(HOUR_AUDIT) as f:
+    if os.path.exists(audit_path):
+        with open(audit_path) as f:
             au = json.load(f).get({"greedy": "greedy", "beam8_hw": "beam8_hw"}[key], {})
         ok = set(au.get("allowed_chunks", []))
         audited = all(i in ok and got[i] in au["chunks"][str(i)]["gpu_tokens"].values()
                       for got in got_steps for i, (a, b) in enumerate(zip(got, ref)) if a != b)
-    return {"golden": f"tests/golden/bench_hour_oracle.json[{key}]",
+    gname = os.path.basename(audit_path).replace("bench_hour_audit", "bench_hour_oracle")
+    return {"golden": f"tests/golden/{gname}[{key}]",
             "chunks_identical_to_oracle": f"{min(same)}/{len(ref)}",
             "per_timed_step": same if len(same) <= 32 else same[:32],
             "oracle_tokens": nref, "token_errors": errs,
@@ -380,14 +390,14 @@ def pmc_traffic(kernel_class, args):
 _CPU = {}
 
 
-def _cpu_worker_init(model, seed, threads, hotwords):
+def _cpu_worker_init(model, seed, threads, hotwords, variant="greedy-calibrated"):
     import torch
     from oracle.search import HotwordGraph
     from oracle.zipformer import ZipformerOracle
-    from zasr.model import PRESETS, synth_weights
+    from zasr.model import PRESETS, variant_weights
     torch.set_num_threads(threads)
     cfg = PRESETS[model]()
-    _CPU["orc"] = ZipformerOracle(cfg, synth_weights(cfg, seed))
+    _CPU["orc"] = ZipformerOracle(cfg, variant_weights(cfg, seed, variant))
     _CPU["graph"] = HotwordGraph(*hotwords) if hotwords and hotwords[0] else None
 
 
@@ -427,7 +437,7 @@ def cpu_baseline(args, chunks, beam, hotwords, n_chunks=4):
     jobs = [(sample[w::workers], beam) for w in range(workers)]
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers, initializer=_cpu_worker_init,
-                  initargs=(args.model, WEIGHT_SEED, threads, hotwords)) as pool:
+                  initargs=(args.model, WEIGHT_SEED, threads, hotwords, args.weights)) as pool:
         pool.map(_cpu_worker_run, [([c[: SR * 4] for c in j[0][:1]], j[1]) for j in jobs])
         times = []
         for _ in range(max(1, args.cpu_repeats)):
@@ -1203,7 +1213,7 @@ def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
     if golden is not None:
         ocheck = oracle_agreement(golden[0], golden[1],
                                   [[r.token_ids.tolist() for r in res[st * n:(st + 1) * n]]
-                                   for st in range(k)])
+                                   for st in range(k)], golden[2])
     if dist:
         from zasr.shard import max_over_ranks
         el = max_over_ranks(el, device=dev)
@@ -1276,7 +1286,7 @@ def bench_dropin(args):
     import torch
     from zasr import asr_engine as ae
     from zasr.merge import merge_chunks_with_overlap
-    from zasr.model import PRESETS, save_model_dir, synth_tokens, synth_weights
+    from zasr.model import PRESETS, save_model_dir, synth_tokens, variant_weights
     from zasr.plan import best_split, concat_to_original, silent_regions
     from zasr.synth_audio import synth_speech
     rank = int(os.environ.get("RANK", "0"))
@@ -1292,7 +1302,8 @@ def bench_dropin(args):
     hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
     hotwords = load_hotwords(hw_path, cfg.vocab_size) if hw_path else ([], [])
     mdir = os.path.join(tempfile.gettempdir(), f"zasr_dropin_{args.model}_{os.getpid()}")
-    save_model_dir(mdir, cfg, synth_weights(cfg, WEIGHT_SEED), synth_tokens(cfg.vocab_size))
+    save_model_dir(mdir, cfg, variant_weights(cfg, WEIGHT_SEED, args.weights),
+                   synth_tokens(cfg.vocab_size))
     # the drop-in's own default precision (zasr.asr_engine.DEFAULT_PRECISION: what install()
     # users get) unless --precision is given explicitly
     prec = args.precision if any(a.startswith("--precision") for a in sys.argv[1:]) \
@@ -1412,7 +1423,7 @@ def parity_child_main(args):
     """--parity-child: the bench workload (same chunks, same weights) in the parity precision
     only; prints one PARITY_JSON line for the parent (run_parity_child)."""
     import torch
-    from zasr.model import PRESETS, chunk_flops, save_model_dir, synth_tokens, synth_weights
+    from zasr.model import PRESETS, chunk_flops, save_model_dir, synth_tokens, variant_weights
     cfg = PRESETS[args.model]()
     beam = 1 if args.method == "greedy_search" else args.beam
     hw_path = DEFAULT_HOTWORDS if args.hotwords_file == "default" else args.hotwords_file
@@ -1423,7 +1434,8 @@ def parity_child_main(args):
     torch.cuda.set_device(0)
     dev = "cuda:0"
     mdir = os.path.join(tempfile.gettempdir(), f"zasr_parity_{args.model}_{os.getpid()}")
-    save_model_dir(mdir, cfg, synth_weights(cfg, WEIGHT_SEED), synth_tokens(cfg.vocab_size))
+    save_model_dir(mdir, cfg, variant_weights(cfg, WEIGHT_SEED, args.weights),
+                   synth_tokens(cfg.vocab_size))
     d_wav = torch.from_numpy(np.concatenate(chunks)).to(dev)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream().cuda_stream
@@ -1500,8 +1512,8 @@ def main():
         torch.cuda.set_device(local)
         dev = f"cuda:{local}"
         from zasr.binding import Recognizer
-        from zasr.model import save_model_dir, synth_tokens, synth_weights
-        weights = synth_weights(cfg, WEIGHT_SEED)
+        from zasr.model import save_model_dir, synth_tokens, variant_weights
+        weights = variant_weights(cfg, WEIGHT_SEED, args.weights)
         mdir = os.path.join(tempfile.gettempdir(), f"zasr_bench_{args.model}_{os.getpid()}")
         save_model_dir(mdir, cfg, weights, synth_tokens(cfg.vocab_size))
         del weights
@@ -1662,7 +1674,8 @@ def main():
     if rec is not None and rank == 0 and not args.shard_plan:
         golden = hour_golden(args, beam, hotwords, chunks)
         if golden is not None:
-            ocheck = oracle_agreement(golden[0], golden[1], [[r.token_ids.tolist() for r in res]])
+            ocheck = oracle_agreement(golden[0], golden[1], [[r.token_ids.tolist() for r in res]],
+                                      golden[2])
             ocheck["note"] = ("the headline precision's tokens vs the oracle (fp32); bf16 is "
                               "BASELINE config 2's arithmetic, not a token-exact mode -- the "
                               "token-exact figure is parity_mode")
@@ -1685,7 +1698,9 @@ def main():
             "config": {"workload": f"{args.model} {args.method}"
                                    f"{'' if beam == 1 else ' beam %d' % beam}{hw_tag}"
                                    ", batched planner chunks, 1 h per GPU",
-                       "model": args.model, "chunks_per_gpu": len(chunks),
+                       "model": args.model, "weights": args.weights,
+                       "emitting_frame_fraction": round(emitted / max(1, tprime), 4),
+                       "chunks_per_gpu": len(chunks),
                        "chunk_sec_min_max": [round(min(lens) / SR, 2), round(max(lens) / SR, 2)],
                        "audio_sec_per_gpu": args.audio_sec,
                        "decoded_sec_per_gpu_incl_overlap": round(sum(lens) / SR, 1),

@@ -24,10 +24,13 @@ for st in campp vad; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_$st -o run -- python3 $R/bench.py --stage $st --no-cpu-baseline --steps 3 --warmup 1 > $OUT/stats_$st.json 2> $OUT/stats_$st.err
 done
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords.json 2> $OUT/bench_beam8.err
+# config 3 on the beam-calibrated weights (beam 8 emits at the greedy rate) and its f16x3 form
+timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --weights beam-calibrated --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_beamcal.json 2> $OUT/bench_beam8_beamcal.err
 fi
 if [ "$PART" != 1 ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_f16x3 -o run -- python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --steps 3 --warmup 1 > $OUT/stats_f16x3.json 2> $OUT/stats_f16x3.err
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_f16x3.json 2> $OUT/bench_beam8_f16x3.err
+timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --weights beam-calibrated --precision f16x3 --parity-precision none --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_f16x3_beamcal.json 2> $OUT/bench_beam8_f16x3_beamcal.err
 timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwords-file default > $OUT/bench_rover.json 2> $OUT/bench_rover.err
 timeout -k 10 300 python3 $R/bench.py --stage pipe --steps 4 --warmup 1 > $OUT/bench_pipe.json 2> $OUT/bench_pipe.err
 timeout -k 10 300 python3 $R/bench.py --stage campp > $OUT/bench_campp.json 2> $OUT/bench_campp.err

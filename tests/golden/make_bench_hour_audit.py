@@ -3,7 +3,7 @@ differ from the oracle's (tests/golden/bench_hour_oracle.json) -- test infrastru
 the build container on the GPU's token lists (gpurun_out/hour_tokens_<prec>_<method>.json,
 written by tests/test_gpu_hour.py):
 
-    python tests/golden/make_bench_hour_audit.py [gpurun_out]
+    python tests/golden/make_bench_hour_audit.py [gpurun_out] [--weights VARIANT]
 
 For every differing chunk it reruns the oracle (numpy fbank -> torch fp32 encoder -> the
 reference's _ort_beam_search restated, core/asr_engine.py:1023-1153) and records:
@@ -72,14 +72,20 @@ def main():
     from oracle.fbank import fbank
     from oracle.search import HotwordGraph, beam_search
     from oracle.zipformer import ZipformerOracle
-    from zasr.model import PRESETS, synth_weights
-    src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out")
+    from zasr.model import PRESETS, variant_weights
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src", nargs="?", default=os.path.join(REPO, "gpurun_out"))
+    ap.add_argument("--weights", default="greedy-calibrated")
+    a = ap.parse_args()
+    src, variant = a.src, a.weights
+    tag = "" if variant == "greedy-calibrated" else f"_{variant}"
     torch.set_num_threads(8)
-    with open(os.path.join(HERE, "bench_hour_oracle.json")) as f:
+    with open(os.path.join(HERE, f"bench_hour_oracle{tag}.json")) as f:
         gold = json.load(f)
     chunks = bench.make_chunks(3600.0, bench.AUDIO_SEED)
     cfg = PRESETS["zipformer-68m"]()
-    orc = ZipformerOracle(cfg, synth_weights(cfg, bench.WEIGHT_SEED))
+    orc = ZipformerOracle(cfg, variant_weights(cfg, bench.WEIGHT_SEED, variant))
     phrases, scores = bench.load_hotwords(bench.DEFAULT_HOTWORDS, cfg.vocab_size)
     graph = HotwordGraph(phrases, scores)
     out = {"what": "chunks of the benched hour where the GPU's fp32 / f16x3 decodes differ from "
@@ -88,7 +94,7 @@ def main():
     for method, key, beam, g in (("greedy", "greedy", 1, None), ("beam8_hw", "beam8_hw", 8, graph)):
         got, frames = {}, {}
         for prec in ("fp32", "f16x3"):
-            path = os.path.join(src, f"hour_tokens_{prec}_{method}.json")
+            path = os.path.join(src, f"hour_tokens_{prec}_{method}{tag}.json")
             if os.path.exists(path):
                 with open(path) as f:
                     d = json.load(f)
@@ -121,7 +127,9 @@ def main():
                 beam_search(enc, orc.decoder, orc.joiner, beam, g, ties=ties)
                 e["oracle_exact_boundary_tie_frames"] = ties[:32]
                 ok = ok or bool(ties)
-            encs = os.path.join(src, "hour_enc_fp32.npz")
+            encs = os.path.join(src, f"hour_enc_fp32_{method}{tag}.npz")
+            if not os.path.exists(encs) and method == "greedy" and not tag:
+                encs = os.path.join(src, "hour_enc_fp32.npz")  # round-5 first runs
             if os.path.exists(encs):
                 with np.load(encs) as z:
                     if f"chunk{i}" in z.files:
@@ -140,9 +148,11 @@ def main():
             entries[str(i)] = e
             print(method, i, json.dumps({k: v for k, v in e.items() if k != "gpu_tokens"}), flush=True)
         out[method] = {"differing_chunks": diff, "allowed_chunks": allowed, "chunks": entries}
-    with open(OUT, "w") as f:
+    out["weights"] = variant
+    path = OUT.replace(".json", f"{tag}.json")
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
-    print("wrote", OUT)
+    print("wrote", path)
 
 
 if __name__ == "__main__":

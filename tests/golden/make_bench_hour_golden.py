@@ -17,7 +17,7 @@ file; no GPU-side code reads the oracle.
 
 Deterministic (seeded audio and weights, fp32 torch on the CPU with a fixed thread count per
 worker).  Takes a few minutes on 8 cores:
-    python tests/golden/make_bench_hour_golden.py [--workers 4 --threads 2]
+    python tests/golden/make_bench_hour_golden.py [--workers 4 --threads 2] [--weights VARIANT]
 """
 from __future__ import annotations
 
@@ -36,6 +36,11 @@ for p in (REPO, os.path.join(REPO, "sherpa-vietnamese-asr_amd")):
         sys.path.insert(0, p)
 
 OUT = os.path.join(REPO, "tests", "golden", "bench_hour_oracle.json")
+
+
+def golden_path(variant: str) -> str:
+    """bench_hour_oracle.json for the default weights, bench_hour_oracle_<variant>.json else."""
+    return OUT if variant == "greedy-calibrated" else OUT.replace(".json", f"_{variant}.json")
 _W = {}
 
 
@@ -46,15 +51,15 @@ def audio_digest(chunks) -> str:
     return h.hexdigest()[:32]
 
 
-def _init(threads):
+def _init(threads, variant):
     import torch
     import bench
     from oracle.search import HotwordGraph
     from oracle.zipformer import ZipformerOracle
-    from zasr.model import PRESETS, synth_weights
+    from zasr.model import PRESETS, variant_weights
     torch.set_num_threads(threads)
     cfg = PRESETS["zipformer-68m"]()
-    _W["orc"] = ZipformerOracle(cfg, synth_weights(cfg, bench.WEIGHT_SEED))
+    _W["orc"] = ZipformerOracle(cfg, variant_weights(cfg, bench.WEIGHT_SEED, variant))
     phrases, scores = bench.load_hotwords(bench.DEFAULT_HOTWORDS, cfg.vocab_size)
     _W["graph"] = HotwordGraph(phrases, scores)
 
@@ -77,6 +82,8 @@ def main():
     ap.add_argument("--workers", type=int, default=4)
     ap.add_argument("--threads", type=int, default=2)
     ap.add_argument("--limit", type=int, default=0, help="first N chunks only (a dry run)")
+    ap.add_argument("--weights", default="greedy-calibrated",
+                    help="zasr.model.WEIGHT_VARIANTS name (bench.py --weights)")
     a = ap.parse_args()
     import multiprocessing as mp
     import bench
@@ -87,14 +94,16 @@ def main():
     res = [None] * len(chunks)
     # longest chunks first so the pool drains evenly
     order = sorted(range(len(chunks)), key=lambda i: -chunks[i].shape[0])
-    with mp.get_context("spawn").Pool(a.workers, initializer=_init, initargs=(a.threads,)) as pool:
+    with mp.get_context("spawn").Pool(a.workers, initializer=_init,
+                                      initargs=(a.threads, a.weights)) as pool:
         for n, (i, r) in enumerate(pool.imap_unordered(_run, [(i, chunks[i]) for i in order])):
             res[i] = r
             if n % 10 == 0:
                 print(f"{n + 1}/{len(chunks)} chunks, {time.time() - t0:.0f} s", flush=True)
     out = {
         "what": "oracle decode of bench.py's hour (make_chunks(3600, AUDIO_SEED), "
-                "zipformer-68m synth_weights(WEIGHT_SEED)): greedy and beam 8 + hotword.txt",
+                f"zipformer-68m weights {a.weights} (WEIGHT_SEED)): greedy and beam 8 + hotword.txt",
+        "weights": a.weights,
         "generator": "tests/golden/make_bench_hour_golden.py",
         "audio_sha256_32": audio_digest(chunks),
         "chunk_samples": [int(c.shape[0]) for c in chunks],
@@ -106,7 +115,9 @@ def main():
         "tokens": {"greedy": sum(len(r["greedy"]) for r in res),
                    "beam8_hw": sum(len(r["beam8_hw"]) for r in res)},
     }
-    path = OUT if not a.limit else OUT.replace(".json", f"_first{a.limit}.json")
+    path = golden_path(a.weights)
+    if a.limit:
+        path = path.replace(".json", f"_first{a.limit}.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))
     print(f"wrote {path}: {out['tokens']} tokens, {time.time() - t0:.0f} s")

@@ -17,7 +17,9 @@ Bars (tolerances stated as the north star asks):
   bf16          BASELINE config 2's arithmetic, not a token-exact mode: its TER is measured and
                 written to gpurun_out/hour_agreement.json, bounded by 0.2 greedy / 0.3 beam
                 (measured 0.142 / 0.223; the bound catches a broken path).
-Every mode's per-chunk tokens go to gpurun_out/hour_tokens_<mode>_<method>.json for the audit.
+Every mode's per-chunk tokens go to gpurun_out/hour_tokens_<mode>_<method>[_<weights>].json for
+the audit.  The beam-calibrated weight variant (bench.py --weights beam-calibrated, config 3 at
+the greedy emission rate) is checked the same way against its own golden and audit.
 """
 import json
 import os
@@ -34,30 +36,46 @@ AUDIT = os.path.join(REPO, "tests", "golden", "bench_hour_audit.json")
 OUT = os.path.join(REPO, "gpurun_out")
 
 
-@pytest.fixture(scope="module")
-def hour():
+def _hour(variant):
     if not gpu_available():
         pytest.skip("no GPU")
     import torch
 
     import bench
-    from model_fixtures import m_model
+    from model_fixtures import model_dir
+    from zasr.model import PRESETS, variant_weights
     chunks = bench.make_chunks(3600.0, bench.AUDIO_SEED)
-    with open(GOLDEN) as f:
+    gpath = GOLDEN if variant == "greedy-calibrated" else GOLDEN.replace(".json", f"_{variant}.json")
+    apath = gpath.replace("bench_hour_oracle", "bench_hour_audit")
+    with open(gpath) as f:
         g = json.load(f)
     assert [int(c.shape[0]) for c in chunks] == g["chunk_samples"]
-    cfg, _, path = m_model(bench.WEIGHT_SEED)
+    cfg = PRESETS["zipformer-68m"]()
+    path = model_dir(f"m_{bench.WEIGHT_SEED}" + ("" if variant == "greedy-calibrated" else f"_{variant}"),
+                     cfg, variant_weights(cfg, bench.WEIGHT_SEED, variant))
     lens = [int(c.shape[0]) for c in chunks]
     offs = np.cumsum([0] + lens[:-1]).tolist()
     d_wav = torch.from_numpy(np.concatenate(chunks)).to("cuda:0")
     torch.cuda.synchronize()
     phrases, scores = bench.load_hotwords(bench.DEFAULT_HOTWORDS, cfg.vocab_size)
     audit = {}
-    if os.path.exists(AUDIT):
-        with open(AUDIT) as f:
+    if os.path.exists(apath):
+        with open(apath) as f:
             audit = json.load(f)
     return {"g": g, "path": path, "d_wav": d_wav, "offs": offs, "lens": lens,
-            "hot": (phrases, scores), "audit": audit}
+            "hot": (phrases, scores), "audit": audit, "variant": variant}
+
+
+@pytest.fixture(scope="module")
+def hour():
+    return _hour("greedy-calibrated")
+
+
+@pytest.fixture(scope="module")
+def hour_bc():
+    """The beam-calibrated weights (zasr.model.WEIGHT_VARIANTS: beam 8 emits at the greedy
+    rate, bench.py --weights beam-calibrated) against their own oracle golden."""
+    return _hour("beam-calibrated")
 
 
 def _decode(h, prec, method):
@@ -81,37 +99,41 @@ def _agree(h, prec, method):
     got, frames = _decode(h, prec, method)
     ref = h["g"][key]
     rec = bench.oracle_agreement(key, ref, [got])
+    rec["emitting_frame_fraction"] = round(sum(map(len, got)) / max(1, sum(h["g"]["frames"])), 4)
     rec["tokens"] = got
     os.makedirs(OUT, exist_ok=True)
-    with open(os.path.join(OUT, f"hour_tokens_{prec}_{method}.json"), "w") as f:
+    tag = "" if h["variant"] == "greedy-calibrated" else f"_{h['variant']}"
+    with open(os.path.join(OUT, f"hour_tokens_{prec}_{method}{tag}.json"), "w") as f:
         json.dump({"tokens": got, "frames": frames}, f, separators=(",", ":"))
     path = os.path.join(OUT, "hour_agreement.json")
     allrec = {}
     if os.path.exists(path):
         with open(path) as f:
             allrec = json.load(f)
-    allrec[f"{prec}_{method}"] = {k: v for k, v in rec.items() if k != "tokens"}
+    allrec[f"{prec}_{method}{tag}"] = {k: v for k, v in rec.items() if k != "tokens"}
     with open(path, "w") as f:
         json.dump(allrec, f, indent=1)
     return rec
 
 
-def _dump_encoder_out(h, chunks_idx):
-    """The GPU fp32 encoder output of the given chunks -> gpurun_out/hour_enc_fp32.npz, so the
-    audit can run the oracle's search on it (is the difference the encoder's rounding?)."""
+def _dump_encoder_out(h, chunks_idx, tag=""):
+    """The GPU fp32 encoder output of the given chunks -> gpurun_out/hour_enc_fp32<tag>.npz, so
+    the audit can run the oracle's search on it (is the difference the encoder's rounding?)."""
     import bench
     from zasr.binding import Recognizer
     rec = Recognizer(h["path"], "greedy_search", 1, precision="fp32")
     chunks = bench.make_chunks(3600.0, bench.AUDIO_SEED)
     enc = rec.encode_features([rec.fbank(chunks[i]) for i in chunks_idx])
     rec.close()
-    np.savez(os.path.join(OUT, "hour_enc_fp32.npz"), **{f"chunk{i}": e for i, e in zip(chunks_idx, enc)})
+    np.savez(os.path.join(OUT, f"hour_enc_fp32{tag}.npz"),
+             **{f"chunk{i}": e for i, e in zip(chunks_idx, enc)})
 
 
 def _check_exact(h, prec, method, ter_bound):
     rec = _agree(h, prec, method)
-    if prec == "fp32" and method == "greedy" and rec["differing_chunks"]:
-        _dump_encoder_out(h, rec["differing_chunks"])
+    if prec == "fp32" and rec["differing_chunks"]:
+        tag = "" if h["variant"] == "greedy-calibrated" else f"_{h['variant']}"
+        _dump_encoder_out(h, rec["differing_chunks"], f"_{method}{tag}")
     audit = h["audit"].get(method, {})
     allowed = set(audit.get("allowed_chunks", []))
     unexplained = [c for c in rec["differing_chunks"] if c not in allowed]
@@ -138,3 +160,12 @@ def test_hour_beam8_hotwords_matches_oracle(hour, prec):
 def test_hour_bf16_token_error_rate(hour, method, bound):
     rec = _agree(hour, "bf16", method)
     assert rec["ter"] <= bound, {k: v for k, v in rec.items() if k != "tokens"}
+
+
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+@pytest.mark.parametrize("method,bound", [("greedy", 0.002), ("beam8_hw", 0.01)])
+def test_hour_beam_calibrated_matches_oracle(hour_bc, prec, method, bound):
+    """Config 3 made representative: with the beam-calibrated weights beam 8
+    + hotword.txt emits at the greedy rate; the exact-f32-quality modes still equal the oracle
+    except at audited f32 ties (tests/golden/bench_hour_audit_beam-calibrated.json)."""
+    _check_exact(hour_bc, prec, method, bound)
