@@ -520,6 +520,32 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
         l->wp = p;
       }
     }
+    const char* ffn_h3_env = getenv("ZASR_FFN_H3");  // "0": the GEMM pair (A/B)
+    if (split_pieces() == kPiecesF16 && !(ffn_h3_env && ffn_h3_env[0] == '0')) {
+      // the fused f16x3 FFN (model dims 256..512) reads W1 / W2 as fp16 piece images in
+      // MFMA-fragment order; a layer whose weights reach 31 in magnitude keeps the GEMM pair
+      for (auto& s : model_.stacks)
+        for (auto& L : s.layers)
+          for (int a = 0; a < 3; ++a) {
+            const int F = L.ff_in[a].N, d = L.ff_in[a].K;
+            if (!ffn_h3_supported(d, F)) continue;
+            std::vector<float> w1((size_t)F * d), w2((size_t)F * d);
+            ZASR_HIP_CHECK(hipMemcpy(w1.data(), L.ff_in[a].w, w1.size() * 4, hipMemcpyDeviceToHost));
+            ZASR_HIP_CHECK(hipMemcpy(w2.data(), L.ff_out[a].w, w2.size() * 4, hipMemcpyDeviceToHost));
+            if (!ffn_h3_weights_ok(w1.data(), (long)w1.size()) || !ffn_h3_weights_ok(w2.data(), (long)w2.size()))
+              continue;
+            for (auto [l, w] : {std::pair<DLin*, std::vector<float>*>{&L.ff_in[a], &w1},
+                                std::pair<DLin*, std::vector<float>*>{&L.ff_out[a], &w2}}) {
+              std::vector<__bf16> pk(2 * w->size());
+              ffn_pack_h3_host(w->data(), l->N, l->K, pk.data());
+              void* p = nullptr;
+              ZASR_HIP_CHECK(hipMalloc(&p, pk.size() * 2));
+              model_.allocations.push_back(p);
+              ZASR_HIP_CHECK(hipMemcpy(p, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+              l->wp = p;
+            }
+          }
+    }
     if (cfg.joiner_dim == 256 || cfg.joiner_dim == 512) {
       // the joiner's W pieces in MFMA-fragment order (one packed image per piece) for
       // joiner_split_packed_kernel; J is written in the same order, already split, by store_j4
@@ -1043,6 +1069,13 @@ void Engine::layer_forward(const DStack& S, const DLayer& Ly, float* X, int R, c
       __bf16* H = ws<__bf16>("ly_hid_h", (size_t)R * fi.N);
       linear_h(fi, X, false, d, R, H, true, fi.N, EPI_SWOOSHL);
       linear_h(Ly.ff_out[k], H, true, fi.N, R, X, false, d, EPI_RESADD, bo, bs);
+    } else if (fi.wp && np == kPiecesF16) {
+      // f16x3 mode: the same fusion at f32 quality, the hidden layer on chip as fp16 pieces;
+      // feed_forward2 folds bypass_mid as the GEMM pair's residual epilogue does
+      prof_begin("ffn_fused");
+      launch_ffn_fused_h3(X, R, d, fi.N, fi.wp, fi.b, Ly.ff_out[k].wp, Ly.ff_out[k].b, st_,
+                          k == 1 ? O : nullptr, k == 1 ? Ly.bypass_mid : nullptr);
+      prof_end();
     } else {
       // split modes: feed_forward2's epilogue applies bypass_mid too (fp32: launch_bypass)
       const bool byp = k == 1 && Ly.ff_out[k].wx != nullptr;

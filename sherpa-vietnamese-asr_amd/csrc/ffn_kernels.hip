@@ -15,7 +15,10 @@
 // 4 waves (128 tokens), double-buffered: the next chunk's global loads are in flight while the
 // current chunk computes.  Epilogue: X[token][d] += O^T + b2 (f32 read-modify-write).
 // Bytes per token: D * 4 read + D * 4 written; the 2 F D bf16 weight bytes are L2-resident.
+#include <cmath>
+#include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -407,6 +410,324 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
       *reinterpret_cast<float4*>(xr + ch) = v;
     }
   }
+}
+
+// ---- f16x3 wide FFN (the token-exact mode) ----
+// The same FeedforwardModule at f32 quality: every product on fp16 MFMAs over the two pieces
+// x = hi + lo 2^-11 (gemm_dev.h split_h8), here in the one-accumulator form -- the weight's hi
+// piece scaled by 2^11 in registers (v_pk_mul_f16, exact for |w| < 32: ffn_h3_weights_ok),
+// so the three products w_lo x_hi + w_hi x_lo + (w_hi 2^11) x_hi land on one 2^11-scaled
+// accumulator (one register set per output fragment, as in the bf16 kernel).  The unfused
+// f16x3 path writes the f32 hidden activation to HBM and reads it back (R F 8 bytes per FFN);
+// here it stays on chip as fp16 pieces.  Structure of ffn_wide_kernel: 8 waves, one block per
+// CU, a TT-token tile held once in LDS (two fp16 piece images, split once per block), 128
+// hidden units per chunk:
+//   phase A  H^T = W1_c X^T   wave w: hidden units 16 w .. 16 w + 15 x TT tokens
+//                             (v_mfma_f32_16x16x32_f16; A = W1 pieces from L2, B = X pieces
+//                             from LDS)
+//   + b1, SwooshL, split -> the chunk's H pieces in LDS
+//   phase B  O^T += W2_c H^T  wave w: output channels [w D/8, (w + 1) D/8) x TT tokens
+// Weight fragments stream through small register rings (too many pieces to hold a chunk's
+// set): W1 P1 k-steps ahead within phase A (the next chunk's first P1 issued in phase B), W2
+// two k-steps ahead (the chunk's first two issued at the top of its phase A).
+// W1 / W2 pieces: ffn_pack_host per piece, piece 1 at + F D elements.
+namespace {
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr float kF16Lo = 2048.f, kF16LoInv = 1.f / 2048.f;  // gemm_dev.h's piece scale
+
+// acc (2^11 scale) += w_lo x_hi + w_hi x_lo + w_s x_hi, w_s = w_hi 2^11; smallest terms first
+__device__ __forceinline__ void mfma16_h3(f32x4v& acc, const f16x8& wh, const f16x8& wl,
+                                          const f16x8& ws, const f16x8& xh, const f16x8& xl) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ws, xh, acc, 0, 0, 0);
+}
+}  // namespace
+
+template <int D, int TUM, int NB>
+__global__ __launch_bounds__(512, 1) void ffn_wide_h3_kernel(float* __restrict__ X, int R, int F,
+                                                             const __bf16* __restrict__ W1,
+                                                             const float* __restrict__ b1,
+                                                             const __bf16* __restrict__ W2,
+                                                             const float* __restrict__ b2,
+                                                             const float* __restrict__ byp_orig,
+                                                             const float* __restrict__ byp_scale,
+                                                             int rpb) {
+  constexpr int HC = 128, NW = 8, TTM = 16 * TUM;
+  constexpr int XLD = D + 16, HLD = HC + 16;  // 16 (8 k + 2)-byte rows, as ffn_wide_kernel
+  constexpr int KS = D / 32;
+  constexpr int OW = D / NW, OT = OW / 16;
+  constexpr int P1 = KS < 3 ? KS : 3;
+  static_assert(OW % 16 == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) _Float16 sX[2][TTM * XLD];
+  __shared__ __attribute__((aligned(16))) _Float16 sH[NB][2][TTM * HLD];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  // this block's rows [r0, r1): rpb (a multiple of 16) per block, one block per CU, so every
+  // CU gets the same share instead of a last round of a few TTM-row tiles
+  const long r0 = (long)blockIdx.x * rpb;
+  const long r1 = r0 + rpb < R ? r0 + rpb : R;
+  const long PC = (long)F * D;  // elements per piece image (W1 and W2 alike)
+  const int S2 = F / 32;
+  const int nch = (F + HC - 1) / HC;
+  const f16x8 kS = {(_Float16)2048.f, (_Float16)2048.f, (_Float16)2048.f, (_Float16)2048.f,
+                    (_Float16)2048.f, (_Float16)2048.f, (_Float16)2048.f, (_Float16)2048.f};
+
+  // ---- weight rings (unconditional, clamped loads: rows / k-steps past F meet zero H) ----
+  f16x8 w1r[P1][2];
+  auto load_w1 = [&](int c, int s, int slot) {
+    const int rg = min((c * HC) / 16 + wid, F / 16 - 1);
+    const __bf16* p = W1 + ((long)rg * KS + s) * 512 + lane * 8;
+    w1r[slot][0] = *reinterpret_cast<const f16x8*>(p);
+    w1r[slot][1] = *reinterpret_cast<const f16x8*>(p + PC);
+  };
+  f16x8 w2r[2][OT][2];
+  auto load_w2 = [&](int c, int s, int slot) {
+    const int ks = min(c * (HC / 32) + s, S2 - 1);
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      const __bf16* p = W2 + (((long)(wid * OT + t) * S2 + ks) * 64 + lane) * 8;
+      w2r[slot][t][0] = *reinterpret_cast<const f16x8*>(p);
+      w2r[slot][t][1] = *reinterpret_cast<const f16x8*>(p + PC);
+    }
+  };
+  FFN_STAMP(0)
+#pragma unroll
+  for (int s = 0; s < P1; ++s) load_w1(0, s, s);
+
+  // one tile of TU x 16 rows from t0 (the block's whole tiles at TUM, its last one at what is
+  // left); the weight rings run on across tiles (the last chunk prefetches chunk 0)
+  auto tile = [&](auto tu_c, const long t0) {
+  constexpr int TU = decltype(tu_c)::value, TT = 16 * TU;
+  // ---- X tile -> two fp16 piece images (rows past R: a clamped duplicate, never written) ----
+  {
+    constexpr int NE = TT * D / 4 / (64 * NW);
+    static_assert(NE * 64 * NW * 4 == TT * D, "X tile split");
+    constexpr int NH = NE % 2 == 0 ? NE / 2 : NE;  // in two halves (registers)
+#pragma unroll
+    for (int i0 = 0; i0 < NE; i0 += NH) {
+    float4 v[NH];
+#pragma unroll
+    for (int i = i0; i < i0 + NH; ++i) {
+      const int e = tid + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
+      const long r = t0 + row < R ? t0 + row : R - 1;
+      v[i - i0] = *reinterpret_cast<const float4*>(X + r * D + 4 * c4);
+    }
+#pragma unroll
+    for (int i = i0; i < i0 + NH; ++i) {
+      const int e = tid + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
+      const float x4[4] = {v[i - i0].x, v[i - i0].y, v[i - i0].z, v[i - i0].w};
+      f16x4 hh, ll;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        hh[q] = (_Float16)x4[q];
+        ll[q] = (_Float16)((x4[q] - (float)hh[q]) * kF16Lo);
+      }
+      *reinterpret_cast<f16x4*>(&sX[0][row * XLD + 4 * c4]) = hh;
+      *reinterpret_cast<f16x4*>(&sX[1][row * XLD + 4 * c4]) = ll;
+    }
+    }
+  }
+  lds_barrier();
+  FFN_STAMP(1)
+
+  f32x4v o[OT][TU];
+#pragma unroll
+  for (int t = 0; t < OT; ++t)
+#pragma unroll
+    for (int u = 0; u < TU; ++u) o[t][u] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  for (int c = 0; c < nch; ++c) {
+    const int hid0 = c * HC + wid * 16;
+    const bool hvalid = hid0 < F;  // F % 16 == 0: a wave's 16 units are all valid or none
+    // this chunk's first two W2 k-steps (their ring slots were consumed by the last phase B)
+    // b1 of the wave's 16 units (4 per lane group g4): a volatile load keeps its place ahead
+    // of phase A (a plain one is sunk next to its use, behind a full wait)
+    const f32x4v bb = *reinterpret_cast<const volatile f32x4v*>(b1 + min(hid0, F - 16) + 4 * g4);
+    load_w2(c, 0, 0);
+    load_w2(c, 1, 1);
+    // loads stay where they are issued (the scheduler would sink them next to their use)
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase A: step s + 1's X fragments are read before step s's MFMAs ----
+    f32x4v ha[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) ha[u] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    f16x8 xf[2][TU][2];
+    auto read_x = [&](int s, int buf) {
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int xo = (16 * u + r16) * XLD + 32 * s + 8 * g4;
+        xf[buf][u][0] = *reinterpret_cast<const f16x8*>(&sX[0][xo]);
+        xf[buf][u][1] = *reinterpret_cast<const f16x8*>(&sX[1][xo]);
+      }
+    };
+    FFN_STAMP(8 + 4 * c)
+    read_x(0, 0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int slot = s % P1;
+      if (s + 1 < KS) read_x(s + 1, (s + 1) & 1);
+      const f16x8 wh = w1r[slot][0], wl = w1r[slot][1];
+      const f16x8 ws = wh * kS;
+#pragma unroll
+      for (int u = 0; u < TU; ++u) mfma16_h3(ha[u], wh, wl, ws, xf[s & 1][u][0], xf[s & 1][u][1]);
+      if (s + P1 < KS) load_w1(c, s + P1, slot);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    FFN_STAMP(9 + 4 * c)
+    // ---- + b1, SwooshL, split -> H pieces ----
+    _Float16* sH0 = sH[NB == 2 ? (c & 1) : 0][0];
+    _Float16* sH1 = sH[NB == 2 ? (c & 1) : 0][1];
+    if constexpr (NB == 1) lds_barrier();  // the previous chunk's phase B is done with sH
+    {
+      const float bv[4] = {bb[0], bb[1], bb[2], bb[3]};
+      const float hm = hvalid ? 1.f : 0.f;  // hidden units past F: zero H (no branch: its
+                                            // waits would drain the weight loads in flight)
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        f16x4 hh, ll;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = swooshl_fast(ha[u][q] * kF16LoInv + bv[q]) * hm;
+          hh[q] = (_Float16)v;
+          ll[q] = (_Float16)((v - (float)hh[q]) * kF16Lo);
+        }
+        const int ho = (16 * u + r16) * HLD + wid * 16 + 4 * g4;
+        *reinterpret_cast<f16x4*>(&sH0[ho]) = hh;
+        *reinterpret_cast<f16x4*>(&sH1[ho]) = ll;
+      }
+    }
+    lds_barrier();
+    FFN_STAMP(10 + 4 * c)
+    // ---- phase B: step s + 1's H fragments are read before step s's MFMAs ----
+    f16x8 hf[2][TU][2];
+    auto read_h = [&](int s, int buf) {
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int ho = (16 * u + r16) * HLD + 32 * s + 8 * g4;
+        hf[buf][u][0] = *reinterpret_cast<const f16x8*>(&sH0[ho]);
+        hf[buf][u][1] = *reinterpret_cast<const f16x8*>(&sH1[ho]);
+      }
+    };
+    read_h(0, 0);
+#pragma unroll
+    for (int s = 0; s < HC / 32; ++s) {
+      if (s + 1 < HC / 32) read_h(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int t = 0; t < OT; ++t) {
+        const f16x8 wh = w2r[s & 1][t][0], wl = w2r[s & 1][t][1];
+        const f16x8 ws = wh * kS;
+#pragma unroll
+        for (int u = 0; u < TU; ++u) mfma16_h3(o[t][u], wh, wl, ws, hf[s & 1][u][0], hf[s & 1][u][1]);
+      }
+      if (s + 2 < HC / 32) load_w2(c, s + 2, s & 1);
+      if (s == 1) {  // the next chunk's first W1 k-steps (in-order vmcnt: after W2 step 3)
+        const int cn = c + 1 < nch ? c + 1 : 0;  // (the next tile's first chunk)
+#pragma unroll
+        for (int q = 0; q < P1; ++q) load_w1(cn, q, q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    FFN_STAMP(11 + 4 * c)
+  }
+
+  // ---- X[tok][ch] += O^T 2^-11 + b2 (+ bypass_mid) ----
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const long tok = t0 + 16 * u + r16;
+    if (tok >= r1) continue;
+    float* xr = X + tok * D;
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      const int ch = wid * OW + 16 * t + 4 * g4;
+      const float4 bv = *reinterpret_cast<const float4*>(b2 + ch);
+      float4 v = *reinterpret_cast<const float4*>(xr + ch);
+      v.x += o[t][u][0] * kF16LoInv + bv.x;
+      v.y += o[t][u][1] * kF16LoInv + bv.y;
+      v.z += o[t][u][2] * kF16LoInv + bv.z;
+      v.w += o[t][u][3] * kF16LoInv + bv.w;
+      if (byp_orig != nullptr) {
+        const float4 b0 = *reinterpret_cast<const float4*>(byp_orig + tok * D + ch);
+        const float4 k = *reinterpret_cast<const float4*>(byp_scale + ch);
+        v.x = b0.x + (v.x - b0.x) * k.x;
+        v.y = b0.y + (v.y - b0.y) * k.y;
+        v.z = b0.z + (v.z - b0.z) * k.z;
+        v.w = b0.w + (v.w - b0.w) * k.w;
+      }
+      *reinterpret_cast<float4*>(xr + ch) = v;
+    }
+  }
+  };  // tile
+
+  using T1 = std::integral_constant<int, 1>;
+  using T2 = std::integral_constant<int, 2>;
+  using T3 = std::integral_constant<int, 3>;
+  using TM = std::integral_constant<int, TUM>;
+  long t0 = r0;
+  for (; t0 + TTM <= r1; t0 += TTM) tile(TM{}, t0);
+  const int tail = (int)((r1 - t0 + 15) / 16);  // 0 .. TUM - 1 16-row tiles left
+  if (tail == 1) tile(T1{}, t0);
+  if constexpr (TUM > 2) if (tail == 2) tile(T2{}, t0);
+  if constexpr (TUM > 3) if (tail == 3) tile(T3{}, t0);
+}
+
+bool ffn_h3_supported(int D, int F) {
+  return (D == 256 || D == 384 || D == 512) && F % 32 == 0 && F >= 32;
+}
+
+// the one-accumulator form scales the weight's fp16 hi piece by 2^11: exact below 32
+bool ffn_h3_weights_ok(const float* w, long n) {
+  for (long i = 0; i < n; ++i)
+    if (!(std::fabs(w[i]) < 31.f)) return false;
+  return true;
+}
+
+// W [rows][cols] f32 -> the two fp16 pieces (hi, lo 2^11), each in ffn_pack_host's order
+void ffn_pack_h3_host(const float* w, int rows, int cols, __bf16* out) {
+  const size_t n = (size_t)rows * cols;
+  std::vector<__bf16> piece(n);
+  for (int t = 0; t < 2; ++t) {
+    for (size_t i = 0; i < n; ++i) {
+      const _Float16 hi = (_Float16)w[i];
+      const _Float16 v = t == 0 ? hi : (_Float16)((w[i] - (float)hi) * 2048.f);
+      std::memcpy(&piece[i], &v, 2);
+    }
+    ffn_pack_host(piece.data(), rows, cols, out + t * n);
+  }
+}
+
+void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const float* b1,
+                         const void* W2, const float* b2, hipStream_t st, const float* byp_orig,
+                         const float* byp_scale) {
+  if (R <= 0) return;
+  ZASR_REQUIRE(ffn_h3_supported(D, F), "ffn_fused_h3: unsupported model / feed-forward dim");
+  const __bf16* w1 = reinterpret_cast<const __bf16*>(W1);
+  const __bf16* w2 = reinterpret_cast<const __bf16*>(W2);
+  // one block per CU, rpb rows each (a multiple of 16)
+  static int cus[64] = {0};
+  int dev = 0;
+  ZASR_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    ZASR_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    cus[dev] = n > 0 ? n : 256;
+  }
+  const int rpb = 16 * cdiv(cdiv(R, cus[dev]), 16);
+  const dim3 grid(cdiv(R, rpb));
+#define ZASR_FFNH3(DV, TUV, NBV)                                                                   \
+  hipLaunchKernelGGL((ffn_wide_h3_kernel<DV, TUV, NBV>), grid, dim3(512), 0, st, X, R, F, w1, b1, w2, \
+                     b2, byp_orig, byp_scale, rpb)
+  switch (D) {
+    case 256: ZASR_FFNH3(256, 4, 2); break;
+    case 384: ZASR_FFNH3(384, 4, 1); break;
+    default: ZASR_FFNH3(512, 3, 2); break;
+  }
+#undef ZASR_FFNH3
 }
 
 // D = 256 in the one-wave-per-32-tokens design compiles to one wave per SIMD (384

@@ -1,0 +1,123 @@
+// ffn_wide_h3_kernel check + timing (development tool): random f32 X / W1 / W2, the f16x3 fused
+// FFN vs a host double reference on sampled rows (exact f32 inputs: the error is the f16x3
+// format's plus swooshl_fast's), then the mean time of 20 launches on the bench's shapes,
+// beside the bf16 ffn_wide_kernel on the same shape.  make -C tools ffnh3_lab && ./tools/ffnh3_lab
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#ifndef NO_STAMPS
+#define ZASR_FFN_STAMPS 1
+#endif
+#include "../csrc/ffn_kernels.hip"
+
+using namespace zasr;
+
+static double swl(double x) { double y = x - 4.0; return (y > 20 ? y : std::log1p(std::exp(y))) - 0.08 * x - 0.035; }
+
+static float time_launch(const std::function<void()>& f) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  for (int i = 0; i < 3; ++i) f();
+  hipEventRecord(e0);
+  for (int i = 0; i < 20; ++i) f();
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0); hipEventDestroy(e1);
+  return 1000.f * ms / 20;
+}
+
+static void run(int D, int F, int R) {
+  std::mt19937 g(D * 7919 + F);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  std::vector<float> x((size_t)R * D), b1(F), b2(D), w1((size_t)F * D), w2((size_t)D * F);
+  for (auto& v : x) v = nd(g);
+  for (auto& v : b1) v = 0.1f * nd(g);
+  for (auto& v : b2) v = 0.1f * nd(g);
+  for (auto& v : w1) v = nd(g) / std::sqrt((float)D);
+  for (auto& v : w2) v = nd(g) / std::sqrt((float)F);
+  float *dX, *db1, *db2;
+  __bf16 *dW1, *dW2, *dH1, *dH2;
+  hipMalloc(&dX, x.size() * 4); hipMalloc(&db1, F * 4); hipMalloc(&db2, D * 4);
+  hipMalloc(&dW1, w1.size() * 4); hipMalloc(&dW2, w2.size() * 4);
+  hipMalloc(&dH1, w1.size() * 2); hipMalloc(&dH2, w2.size() * 2);
+  hipMemcpy(dX, x.data(), x.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db1, b1.data(), F * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db2, b2.data(), D * 4, hipMemcpyHostToDevice);
+  {
+    std::vector<__bf16> p1(2 * w1.size()), p2(2 * w2.size());
+    ffn_pack_h3_host(w1.data(), F, D, p1.data());
+    ffn_pack_h3_host(w2.data(), D, F, p2.data());
+    hipMemcpy(dW1, p1.data(), p1.size() * 2, hipMemcpyHostToDevice);
+    hipMemcpy(dW2, p2.data(), p2.size() * 2, hipMemcpyHostToDevice);
+    std::vector<__bf16> h1(w1.size()), h2(w2.size()), q1(w1.size()), q2(w2.size());
+    for (size_t i = 0; i < w1.size(); ++i) h1[i] = (__bf16)w1[i];
+    for (size_t i = 0; i < w2.size(); ++i) h2[i] = (__bf16)w2[i];
+    ffn_pack_host(h1.data(), F, D, q1.data());
+    ffn_pack_host(h2.data(), D, F, q2.data());
+    hipMemcpy(dH1, q1.data(), q1.size() * 2, hipMemcpyHostToDevice);
+    hipMemcpy(dH2, q2.data(), q2.size() * 2, hipMemcpyHostToDevice);
+  }
+  launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) { printf("launch failed: %s\n", hipGetErrorString(e)); exit(1); }
+  std::vector<float> y(x.size());
+  hipMemcpy(y.data(), dX, y.size() * 4, hipMemcpyDeviceToHost);
+  double err = 0, ref2 = 0;
+  int rows = 0;
+  for (int r = 0; r < R; r += (r < 130 ? 1 : 997)) {
+    ++rows;
+    std::vector<double> h(F);
+    for (int j = 0; j < F; ++j) {
+      double a = b1[j];
+      for (int k = 0; k < D; ++k) a += (double)x[(size_t)r * D + k] * w1[(size_t)j * D + k];
+      h[j] = swl(a);
+    }
+    for (int d = 0; d < D; ++d) {
+      double o = b2[d];
+      for (int j = 0; j < F; ++j) o += h[j] * w2[(size_t)d * F + j];
+      const double ref = x[(size_t)r * D + d] + o;
+      err = std::fmax(err, std::fabs(ref - y[(size_t)r * D + d]));
+      ref2 += o * o;
+    }
+  }
+  // last row (tail tile) too
+  const double rms = std::sqrt(ref2 / ((double)rows * D));
+  const float ub = time_launch([&] { launch_ffn_fused(dX, R, D, F, dH1, db1, dH2, db2, 0, nullptr, nullptr); });
+  const float us = time_launch([&] { launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr); });
+  const double fl = 4.0 * R * D * F;
+#ifdef ZASR_FFN_STAMPS
+  {
+    long long st[80];
+    hipMemcpyFromSymbol(st, HIP_SYMBOL(g_ffn_stamps), sizeof(st));
+    printf("  block 0 (shader cycles): X tile %lld", st[1] - st[0]);
+    for (int c = 0; c < (F + 127) / 128 && c < 16; ++c)
+      printf(" | c%d A %lld swl %lld B %lld", c, st[9 + 4 * c] - st[8 + 4 * c], st[10 + 4 * c] - st[9 + 4 * c],
+             st[11 + 4 * c] - st[10 + 4 * c]);
+    printf("\n");
+  }
+#endif
+  printf("D %d F %d R %d: max|err| %.3e (out rms %.3f, rel %.2e, rows %d)  h3 %.1f us = %.3f of the fp16 peak "
+         "(3 MFMA / product)  | bf16 %.1f us (%.3f)  ratio %.2f\n",
+         D, F, R, err, rms, err / rms, rows, us, 3 * fl / us / 1e6 / 2500.0, ub, fl / ub / 1e6 / 2500.0, us / ub);
+  fflush(stdout);
+  hipFree(dX); hipFree(db1); hipFree(db2); hipFree(dW1); hipFree(dW2); hipFree(dH1); hipFree(dH2);
+}
+
+int main(int argc, char** argv) {
+  run(384, 1280, 100);
+  run(384, 1280, 49442);
+  run(384, 1024, 49442);
+  run(384, 768, 49442);
+  run(256, 960, 98813);
+  run(256, 576, 98813);
+  run(256, 768, 98813);
+  run(512, 1920, 24753);
+  run(512, 1536, 24753);
+  run(512, 1152, 24753);
+  return 0;
+}
