@@ -446,8 +446,8 @@ __device__ __forceinline__ void mfma16_h3(f32x4v& acc, const f16x8& wh, const f1
 }
 }  // namespace
 
-template <int D, int TUM, int NB>
-__global__ __launch_bounds__(512, 1) void ffn_wide_h3_kernel(float* __restrict__ X, int R, int F,
+template <int D, int TUM, int NB, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __restrict__ X, int R, int F,
                                                              const __bf16* __restrict__ W1,
                                                              const float* __restrict__ b1,
                                                              const __bf16* __restrict__ W2,
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_h3_kernel(float* __restrict__
                                                              const float* __restrict__ byp_orig,
                                                              const float* __restrict__ byp_scale,
                                                              int rpb) {
-  constexpr int HC = 128, NW = 8, TTM = 16 * TUM;
+  constexpr int HC = 16 * NW, TTM = 16 * TUM;  // NW waves: 8 (one block per CU), 4 (two)
   constexpr int XLD = D + 16, HLD = HC + 16;  // 16 (8 k + 2)-byte rows, as ffn_wide_kernel
   constexpr int KS = D / 32;
   constexpr int OW = D / NW, OT = OW / 16;
@@ -676,7 +676,8 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_h3_kernel(float* __restrict__
 }
 
 bool ffn_h3_supported(int D, int F) {
-  return (D == 256 || D == 384 || D == 512) && F % 32 == 0 && F >= 32;
+  return ((D == 256 || D == 384 || D == 512) && F % 32 == 0 && F >= 32) ||
+         (D == 192 && F % 64 == 0 && F >= 64);
 }
 
 // the one-accumulator form scales the weight's fp16 hi piece by 2^11: exact below 32
@@ -717,15 +718,18 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
     ZASR_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
     cus[dev] = n > 0 ? n : 256;
   }
-  const int rpb = 16 * cdiv(cdiv(R, cus[dev]), 16);
+  // D = 192: 4 waves (48 output channels each), two blocks per CU
+  const int bpc = D == 192 ? 2 : 1;
+  const int rpb = 16 * cdiv(cdiv(R, bpc * cus[dev]), 16);
   const dim3 grid(cdiv(R, rpb));
-#define ZASR_FFNH3(DV, TUV, NBV)                                                                   \
-  hipLaunchKernelGGL((ffn_wide_h3_kernel<DV, TUV, NBV>), grid, dim3(512), 0, st, X, R, F, w1, b1, w2, \
-                     b2, byp_orig, byp_scale, rpb)
+#define ZASR_FFNH3(DV, TUV, NBV, NWV)                                                              \
+  hipLaunchKernelGGL((ffn_wide_h3_kernel<DV, TUV, NBV, NWV>), grid, dim3(64 * NWV), 0, st, X, R, F, w1, \
+                     b1, w2, b2, byp_orig, byp_scale, rpb)
   switch (D) {
-    case 256: ZASR_FFNH3(256, 4, 2); break;
-    case 384: ZASR_FFNH3(384, 4, 1); break;
-    default: ZASR_FFNH3(512, 3, 2); break;
+    case 192: ZASR_FFNH3(192, 3, 2, 4); break;
+    case 256: ZASR_FFNH3(256, 4, 2, 8); break;
+    case 384: ZASR_FFNH3(384, 4, 1, 8); break;
+    default: ZASR_FFNH3(512, 3, 2, 8); break;
   }
 #undef ZASR_FFNH3
 }

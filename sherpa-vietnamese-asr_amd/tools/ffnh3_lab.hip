@@ -95,7 +95,7 @@ static void run(int D, int F, int R) {
     long long st[80];
     hipMemcpyFromSymbol(st, HIP_SYMBOL(g_ffn_stamps), sizeof(st));
     printf("  block 0 (shader cycles): X tile %lld", st[1] - st[0]);
-    for (int c = 0; c < (F + 127) / 128 && c < 16; ++c)
+    for (int c = 0; c < (F + 127) / 128 && c < 12; ++c)
       printf(" | c%d A %lld swl %lld B %lld", c, st[9 + 4 * c] - st[8 + 4 * c], st[10 + 4 * c] - st[9 + 4 * c],
              st[11 + 4 * c] - st[10 + 4 * c]);
     printf("\n");
@@ -109,6 +109,10 @@ static void run(int D, int F, int R) {
 }
 
 int main(int argc, char** argv) {
+  run(192, 512, 100);
+  run(192, 384, 197614);
+  run(192, 512, 197614);
+  run(192, 640, 197614);
   run(384, 1280, 100);
   run(384, 1280, 49442);
   run(384, 1024, 49442);
