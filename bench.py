@@ -284,7 +284,12 @@ def ffn_fused(d: int, f: int) -> bool:
     return d in FFN_FUSED_DIMS and (d < 256 or (f % 32 == 0 and f <= 2048))
 
 
-def gemm_class_work(cfg, L_list, bf16: bool):
+def ffn_fused_h3(d: int, f: int) -> bool:
+    """The f16x3 mode's fused FFN (ffn_kernels.hip ffn_h3_supported)."""
+    return (d in (256, 384, 512) and f % 32 == 0 and f >= 32) or (d == 192 and f % 64 == 0)
+
+
+def gemm_class_work(cfg, L_list, bf16: bool, h3: bool = False):
     """Algorithmic work per step of the GEMM-class launches, mirroring Engine::run_encoder /
     layer_forward: {"enc_gemm": (flops, bytes), "ffn_fused": (flops, bytes)}.
 
@@ -293,7 +298,8 @@ def gemm_class_work(cfg, L_list, bf16: bool):
     + C write (+ C read for the residual epilogue), each at the dtype the launch really uses
     (bf16 mode: GEMM -> GEMM intermediates, q/k/v and the hidden activations in bf16; the
     residual stream f32).  ffn_fused (bf16 mode, model dim in FFN_FUSED_DIMS) = X read + X
-    written (f32) + both weight matrices (bf16), 4 R d F flops."""
+    written (f32) + both weight matrices (bf16), 4 R d F flops.  h3: the f16x3 mode, whose
+    FFNs (ffn_fused_h3 dims) are the fused f16x3 kernel (weights as two fp16 pieces)."""
     wb = 2 if bf16 else 4
     acc = {"enc_gemm": [0.0, 0.0], "ffn_fused": [0.0, 0.0]}
 
@@ -323,6 +329,9 @@ def gemm_class_work(cfg, L_list, bf16: bool):
                 if bf16 and ffn_fused(d, f):
                     acc["ffn_fused"][0] += 4.0 * R * d * f
                     acc["ffn_fused"][1] += 8.0 * R * d + 2 * 2.0 * f * d
+                elif h3 and ffn_fused_h3(d, f):
+                    acc["ffn_fused"][0] += 4.0 * R * d * f
+                    acc["ffn_fused"][1] += 8.0 * R * d + 2 * 4.0 * f * d
                 else:
                     lin(R, d, f, c=h16)
                     lin(R, f, d, a=h16, resadd=True)
@@ -1254,8 +1263,8 @@ def parity_mode_line(args, cfg, mdir, hotwords, beam, d_wav, offs, lens, stream,
     if classes:
         dom, (cnt, ms) = max(classes.items(), key=lambda kv: kv[1][1])
         per = ms / cnt * 1e-3
-        if dom == "enc_gemm":
-            f_cls = gemm_class_work(cfg, L_list, False)["enc_gemm"][0]
+        if dom in ("enc_gemm", "ffn_fused"):
+            f_cls = gemm_class_work(cfg, L_list, False, h3=prec == "f16x3")[dom][0]
             tf = f_cls / cnt / per / 1e12
             out["roofline"] = {"kernel": dom, "bound": "mfma", "avg_launch_ms": round(per * 1e3, 4),
                                "launches_per_step": cnt, "f32_equivalent_tflops": round(tf, 2),
@@ -1613,7 +1622,11 @@ def main():
            "achieved": round(fl_step / t_step / 1e12, 2), "unit": "TFLOP/s", "peak": peak_mfma,
            "frac": round(fl_step / t_step / 1e12 / peak_mfma, 4)}
 
-    work = gemm_class_work(cfg, L_list, bf16)
+    # bf16 / bf16_enc store the GEMM intermediates in bf16; the split modes in f32 (their MFMA
+    # work is nprod executed products per f32-equivalent one)
+    work = gemm_class_work(cfg, L_list, args.precision in ("bf16", "bf16_enc"),
+                           h3=args.precision == "f16x3")
+    nprod = SPLIT_PRODUCTS.get(args.precision, 1)
     f_join = 2.0 * beam * tprime * cfg.joiner_dim * cfg.vocab_size  # per step
     dom = max(classes.items(), key=lambda kv: kv[1][1])[0] if classes else None
     roof = None
@@ -1623,7 +1636,7 @@ def main():
         if dom in work:
             # the binding roof is the larger of bytes / HBM peak and flops / MFMA peak
             f_cls, b_cls = work[dom]
-            fl, by = f_cls * nprof / cnt, b_cls * nprof / cnt  # per launch (class mean)
+            fl, by = nprod * f_cls * nprof / cnt, b_cls * nprof / cnt  # per launch (class mean)
             if by / (HBM_PEAK_GBS * 1e9) >= fl / (peak_mfma * 1e12):
                 ach = by / per_launch_s / 1e9
                 roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1),
@@ -1638,6 +1651,9 @@ def main():
                         "frac": round(ach / peak_mfma, 4), "traffic": None,
                         "algorithmic_flops_per_launch": round(fl),
                         "hbm_gbs": round(by / per_launch_s / 1e9, 1)}
+                if nprod > 1:  # executed MFMA flops: nprod products per f32-equivalent one
+                    roof["mfma_per_product"] = nprod
+                    roof["f32_equivalent_tflops"] = round(ach / nprod, 2)
         elif dom == "joiner":
             ach = f_join * nprof / cnt / per_launch_s / 1e12
             roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2),
