@@ -569,6 +569,30 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
           for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mkx(*l);
       }
     ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
+    const char* h3r_env = getenv("ZASR_GEMM_H3R");  // "0": the tiled gemm_x3 kernel (A/B)
+    if (split_pieces() == kPiecesF16 && !(h3r_env && h3r_env[0] == '0')) {
+      // the layer projections the row-resident f16x3 GEMM takes (K, N within its shapes and
+      // every |w| < 31; the others keep gemm_x3)
+      auto mkr = [&](DLin& l) {
+        if (!gemm_h3r_supported(l.K, l.N, EPI_NONE)) return;
+        std::vector<float> w((size_t)l.N * l.K);
+        ZASR_HIP_CHECK(hipMemcpy(w.data(), l.w, w.size() * 4, hipMemcpyDeviceToHost));
+        if (!ffn_h3_weights_ok(w.data(), (long)w.size())) return;
+        std::vector<__bf16> pk(2 * w.size());
+        ffn_pack_h3_host(w.data(), l.N, l.K, pk.data());
+        void* p = nullptr;
+        ZASR_HIP_CHECK(hipMalloc(&p, pk.size() * 2));
+        model_.allocations.push_back(p);
+        ZASR_HIP_CHECK(hipMemcpy(p, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+        l.wr = p;
+      };
+      for (auto& s : model_.stacks)
+        for (auto& L : s.layers) {
+          for (DLin* l : {&L.attn_in, &L.na_in, &L.na_out}) mkr(*l);
+          for (int a = 0; a < 2; ++a)
+            for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mkr(*l);
+        }
+    }
   }
   if (precision_ == 1 || precision_ == 2) {  // bf16 copies of every dense projection weight
     for (auto& s : model_.stacks)
@@ -908,7 +932,9 @@ void Engine::linear(const DLin& l, const float* A, int lda, int M, float* C, int
     prof_begin(shape_key(cls, M, l.K, l.N, l.wh != nullptr, false, false, epi));
   else
     prof_begin(cls);
-  if (l.wx)
+  if (l.wr && lda == l.K && byp_orig == nullptr && gemm_h3r_supported(l.K, l.N, epi))
+    gemm_h3r(A, l.wr, l.b, C, ldc, M, l.N, l.K, epi, st_);
+  else if (l.wx)
     gemm_x3(p, l.wx, (long)l.N * l.K, epi, ALOAD_DENSE, st_, split_pieces());
   else if (l.wh)
     gemm_bf16(p, l.wh, epi, ALOAD_DENSE, st_);

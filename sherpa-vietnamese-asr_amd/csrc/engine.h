@@ -34,6 +34,7 @@ struct DLin {
   float* bh = nullptr; // bias of the bf16 path when it differs from b (folded row scales)
   void* wp = nullptr;  // bf16 in MFMA-fragment order (ffn_pack_host), the wide fused FFN's operand
   void* wx = nullptr;  // split bf16 of w (precision mode bf16x3): hi [N][K], then lo [N][K]
+  void* wr = nullptr;  // f16x3: the two fp16 pieces in MFMA-fragment order (gemm_h3r)
   // split modes, the conv modules' in_proj: rows (and bias) interleaved so output columns
   // 2c / 2c + 1 are the GLU halves of channel c -- the GEMM epilogue applies the GLU (EPI_GLU)
   bool glu = false;

@@ -122,6 +122,13 @@ constexpr int kPiecesF16 = 4;
 inline int stored_pieces(int pieces) { return pieces == kPiecesF16 ? 2 : pieces; }
 void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload, hipStream_t stream,
              int pieces);
+// f16x3 projection GEMM with the A row tile resident on chip (gemm_h3r.hip): A f32 [M][K]
+// (lda = K), W as two fp16 pieces in MFMA-fragment order (ffn_pack_h3_host, every |w| < 31),
+// C f32; epilogues NONE, RESADD, GLU (ldc = N / 2).  K in {96, 192, 256, 288, 384, 512},
+// N >= 128, N % 16 == 0.
+bool gemm_h3r_supported(int K, int N, int epi);
+void gemm_h3r(const float* A, const void* Wp, const float* bias, float* C, int ldc, int M, int N,
+              int K, int epi, hipStream_t stream);
 // dst[t * n + i] = piece t of src[i]: bf16(src[i] - sum of the previous pieces), t < pieces
 void split_to_bf16(const float* src, void* dst, long n, int pieces, hipStream_t stream);
 
