@@ -346,14 +346,16 @@ def gemm_class_work(cfg, L_list, bf16: bool, h3: bool = False):
     return {k: (v[0], v[1]) for k, v in acc.items()}
 
 
-EPI_NAMES = ["none", "swooshl", "swooshr", "resadd", "mulaux", "mulaux16"]
+EPI_NAMES = ["none", "swooshl", "swooshr", "resadd", "mulaux", "mulaux16", "relu", "gelu", "glu"]  # gemm.h
 
 
-def shape_table(prof: dict, nprof: int, bf16_peak: float, f32_peak: float):
+def shape_table(prof: dict, nprof: int, bf16_peak: float, f32_peak: float, nprod: int = 1):
     """Per-shape roofline rows from profile mode 2's "enc_gemm|M|K|N|w16|a16|c16|epi" classes:
     algorithmic bytes (A + W + C [+ C read for EPI_RESADD] at the launch's dtypes) and flops,
     the binding roof (larger of bytes / HBM peak and flops / MFMA peak), and the fraction of
-    that roof the measured mean launch time reaches."""
+    that roof the measured mean launch time reaches.  nprod > 1 (the split modes): the MFMA
+    work is nprod executed bf16 / fp16 products per f32-equivalent one, priced at the dense
+    bf16 / fp16 peak (the weight pieces take as many bytes as f32)."""
     rows = []
     for name, (cnt, ms) in prof.items():
         parts = name.split("|")
@@ -362,9 +364,9 @@ def shape_table(prof: dict, nprof: int, bf16_peak: float, f32_peak: float):
         M, K, N, w16, a16, c16, epi = map(int, parts[1:])
         by = (2 if a16 else 4) * M * K + (2 if w16 else 4) * N * K + \
             (2 if c16 else 4) * M * N * (2 if epi == 3 else 1)
-        fl = 2.0 * M * K * N
+        fl = 2.0 * M * K * N * nprod
         t = ms / cnt * 1e-3
-        peak_f = bf16_peak if w16 else f32_peak
+        peak_f = bf16_peak if (w16 or nprod > 1) else f32_peak
         t_hbm, t_mfma = by / (HBM_PEAK_GBS * 1e9), fl / (peak_f * 1e12)
         bound = "hbm" if t_hbm >= t_mfma else "mfma"
         rows.append({"M": M, "K": K, "N": N, "a": "bf16" if a16 else "f32",
@@ -375,6 +377,8 @@ def shape_table(prof: dict, nprof: int, bf16_peak: float, f32_peak: float):
                      "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
                      "frac": round(max(t_hbm, t_mfma) / t, 4),
                      "ms_per_step": round(ms / nprof, 4)})
+        if nprod > 1:
+            rows[-1]["mfma_per_product"] = nprod
     rows.sort(key=lambda r: -r["ms_per_step"])
     return rows
 
@@ -1598,7 +1602,7 @@ def main():
             step()
             sync()
             shapes = shape_table(rec.profile_report(), 1, MFMA_BF16_PEAK_TFLOPS,
-                                 MFMA_F32_PEAK_TFLOPS)
+                                 MFMA_F32_PEAK_TFLOPS, SPLIT_PRODUCTS.get(args.precision, 1))
         rec.profile(0)
 
     # weak: every rank its own hour; strong (--shard-plan): one hour for the whole job
