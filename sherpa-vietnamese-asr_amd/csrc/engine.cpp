@@ -592,6 +592,25 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
           for (int a = 0; a < 2; ++a)
             for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mkr(*l);
         }
+      // the ConvNeXt MLP (pw1 [384][128], pw2 [128][384]) as the fused f16x3 FFN
+      const char* cnx_env = getenv("ZASR_CNX_FFN");  // "0": convnext_mlp_h3_kernel (A/B)
+      if (!(cnx_env && cnx_env[0] == '0') && model_.pw1.K == 128 && model_.pw2.N == 128 &&
+          ffn_h3_supported(128, model_.pw1.N)) {
+        std::vector<float> w1((size_t)model_.pw1.N * 128), w2(w1.size());
+        ZASR_HIP_CHECK(hipMemcpy(w1.data(), model_.pw1.w, w1.size() * 4, hipMemcpyDeviceToHost));
+        ZASR_HIP_CHECK(hipMemcpy(w2.data(), model_.pw2.w, w2.size() * 4, hipMemcpyDeviceToHost));
+        if (ffn_h3_weights_ok(w1.data(), (long)w1.size()) && ffn_h3_weights_ok(w2.data(), (long)w2.size()))
+          for (auto [l, w] : {std::pair<DLin*, std::vector<float>*>{&model_.pw1, &w1},
+                              std::pair<DLin*, std::vector<float>*>{&model_.pw2, &w2}}) {
+            std::vector<__bf16> pk(2 * w->size());
+            ffn_pack_h3_host(w->data(), l->N, l->K, pk.data());
+            void* p = nullptr;
+            ZASR_HIP_CHECK(hipMalloc(&p, pk.size() * 2));
+            model_.allocations.push_back(p);
+            ZASR_HIP_CHECK(hipMemcpy(p, pk.data(), pk.size() * 2, hipMemcpyHostToDevice));
+            l->wr = p;
+          }
+      }
     }
   }
   if (precision_ == 1 || precision_ == 2) {  // bf16 copies of every dense projection weight
@@ -1471,7 +1490,13 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       prof_begin("frontend_conv");
       launch_dwconv2d_tiled(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
       prof_end();
-      if (model_.pw1.wp && model_.pw2.wp && split_pieces() == kPiecesF16) {
+      if (model_.pw1.wr && model_.pw2.wr) {
+        // f16x3: the ConvNeXt MLP as the fused f16x3 FFN (d = 128, 384 hidden): x3 += MLP(y3)
+        prof_begin("frontend_conv");
+        launch_ffn_fused_h3(x3, mL.total * 19, 128, 384, model_.pw1.wr, model_.pw1.b,
+                            model_.pw2.wr, model_.pw2.b, st_, nullptr, nullptr, y3);
+        prof_end();
+      } else if (model_.pw1.wp && model_.pw2.wp && split_pieces() == kPiecesF16) {
         // f16x3: pw1 -> SwooshL -> pw2 + residual in one kernel, the hidden layer on chip
         prof_begin("frontend_conv");
         launch_convnext_mlp_h3(y3, x3, (long)mL.total * 19, model_.pw1.wp, model_.pw1.b,

@@ -454,7 +454,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
                                                              const float* __restrict__ b2,
                                                              const float* __restrict__ byp_orig,
                                                              const float* __restrict__ byp_scale,
-                                                             int rpb) {
+                                                             int rpb, const float* __restrict__ Y) {
   constexpr int HC = 16 * NW, TTM = 16 * TUM;  // NW waves: 8 (one block per CU), 4 (two)
   constexpr int XLD = D + 16, HLD = HC + 16;  // 16 (8 k + 2)-byte rows, as ffn_wide_kernel
   constexpr int KS = D / 32;
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
     for (int i = i0; i < i0 + NH; ++i) {
       const int e = tid + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
       const long r = t0 + row < R ? t0 + row : R - 1;
-      v[i - i0] = *reinterpret_cast<const float4*>(X + r * D + 4 * c4);
+      v[i - i0] = *reinterpret_cast<const float4*>(Y + r * D + 4 * c4);
     }
 #pragma unroll
     for (int i = i0; i < i0 + NH; ++i) {
@@ -669,14 +669,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   using TM = std::integral_constant<int, TUM>;
   long t0 = r0;
   for (; t0 + TTM <= r1; t0 += TTM) tile(TM{}, t0);
-  const int tail = (int)((r1 - t0 + 15) / 16);  // 0 .. TUM - 1 16-row tiles left
+  // 16-row groups left: 0 .. TUM - 1 in every block (rpb is a multiple of 16), up to TUM in
+  // the last one (R need not be): a TUM-group remainder runs as a whole tile whose rows past
+  // R are clamped on load and dropped on store
+  const int tail = (int)((r1 - t0 + 15) / 16);
   if (tail == 1) tile(T1{}, t0);
   if constexpr (TUM > 2) if (tail == 2) tile(T2{}, t0);
   if constexpr (TUM > 3) if (tail == 3) tile(T3{}, t0);
+  if (tail == TUM) tile(TM{}, t0);
 }
 
 bool ffn_h3_supported(int D, int F) {
-  return ((D == 256 || D == 384 || D == 512) && F % 32 == 0 && F >= 32) ||
+  return ((D == 128 || D == 256 || D == 384 || D == 512) && F % 32 == 0 && F >= 32) ||
          (D == 192 && F % 64 == 0 && F >= 64);
 }
 
@@ -703,8 +707,9 @@ void ffn_pack_h3_host(const float* w, int rows, int cols, __bf16* out) {
 
 void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const float* b1,
                          const void* W2, const float* b2, hipStream_t st, const float* byp_orig,
-                         const float* byp_scale) {
+                         const float* byp_scale, const float* Y) {
   if (R <= 0) return;
+  if (Y == nullptr) Y = X;
   ZASR_REQUIRE(ffn_h3_supported(D, F), "ffn_fused_h3: unsupported model / feed-forward dim");
   const __bf16* w1 = reinterpret_cast<const __bf16*>(W1);
   const __bf16* w2 = reinterpret_cast<const __bf16*>(W2);
@@ -724,8 +729,9 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
   const dim3 grid(cdiv(R, rpb));
 #define ZASR_FFNH3(DV, TUV, NBV, NWV)                                                              \
   hipLaunchKernelGGL((ffn_wide_h3_kernel<DV, TUV, NBV, NWV>), grid, dim3(64 * NWV), 0, st, X, R, F, w1, \
-                     b1, w2, b2, byp_orig, byp_scale, rpb)
+                     b1, w2, b2, byp_orig, byp_scale, rpb, Y)
   switch (D) {
+    case 128: ZASR_FFNH3(128, 4, 2, 8); break;
     case 192: ZASR_FFNH3(192, 3, 2, 4); break;
     case 256: ZASR_FFNH3(256, 4, 2, 8); break;
     case 384: ZASR_FFNH3(384, 4, 1, 8); break;

@@ -188,10 +188,14 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
   long t0 = r0;
   bool first = true;
   for (; t0 + TTM <= r1; t0 += TTM, first = false) tile(TM{}, t0, first);
+  // 16-row groups left: 0 .. TUM - 1 in every block (rpb is a multiple of 16), up to TUM in
+  // the last one (M need not be): a TUM-group remainder runs as a whole tile whose rows past
+  // M are clamped on load and dropped on store
   const int tail = (int)((r1 - t0 + 15) / 16);
   if (tail == 1) tile(T1{}, t0, first);
   if (tail == 2) tile(T2{}, t0, first);
   if (tail == 3) tile(T3{}, t0, first);
+  if (tail == TUM) tile(TM{}, t0, first);
 }
 
 }  // namespace

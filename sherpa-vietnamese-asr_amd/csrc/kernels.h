@@ -293,14 +293,18 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
                       const void* W2, const float* b2, hipStream_t st,
                       const float* byp_orig = nullptr, const float* byp_scale = nullptr);
 // f16x3 mode (f32-quality products, the hidden layer on chip as fp16 pieces): W1 / W2 as
-// ffn_pack_h3_host images; D in {256, 384, 512}, F % 32 == 0; every |w| < 31
+// ffn_pack_h3_host images; D in {128, 256, 384, 512} with F % 32 == 0 or D = 192 with
+// F % 64 == 0; every |w| < 31
 // (ffn_h3_weights_ok: the kernel scales the weights' fp16 hi piece by 2^11)
 bool ffn_h3_supported(int D, int F);
 bool ffn_h3_weights_ok(const float* w, long n);
 void ffn_pack_h3_host(const float* w, int rows, int cols, __bf16* out);
+// Y (nullable): the rows the FFN reads when they are not X's own -- X += FFN(Y) (the ConvNeXt
+// block's pointwise MLP on the depthwise conv's output, D = 128)
 void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const float* b1,
                          const void* W2, const float* b2, hipStream_t st,
-                         const float* byp_orig = nullptr, const float* byp_scale = nullptr);
+                         const float* byp_orig = nullptr, const float* byp_scale = nullptr,
+                         const float* Y = nullptr);
 
 // ---- transducer search (core/asr_engine.py:1023-1153) ----
 struct SearchState {

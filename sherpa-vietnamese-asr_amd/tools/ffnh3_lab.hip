@@ -31,7 +31,7 @@ static float time_launch(const std::function<void()>& f) {
   return 1000.f * ms / 20;
 }
 
-static void run(int D, int F, int R) {
+static void run(int D, int F, int R, bool sepY = false) {
   std::mt19937 g(D * 7919 + F);
   std::normal_distribution<float> nd(0.f, 1.f);
   std::vector<float> x((size_t)R * D), b1(F), b2(D), w1((size_t)F * D), w2((size_t)D * F);
@@ -62,25 +62,39 @@ static void run(int D, int F, int R) {
     hipMemcpy(dH1, q1.data(), q1.size() * 2, hipMemcpyHostToDevice);
     hipMemcpy(dH2, q2.data(), q2.size() * 2, hipMemcpyHostToDevice);
   }
-  launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr);
+  // sepY: the rows read (Y) are a second buffer, X only the residual (the ConvNeXt MLP form)
+  float* dY = nullptr;
+  std::vector<float> yv;
+  if (sepY) {
+    yv.resize(x.size());
+    for (auto& v : yv) v = nd(g);
+    hipMalloc(&dY, yv.size() * 4);
+    hipMemcpy(dY, yv.data(), yv.size() * 4, hipMemcpyHostToDevice);
+  }
+  launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr, dY);
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) { printf("launch failed: %s\n", hipGetErrorString(e)); exit(1); }
   std::vector<float> y(x.size());
   hipMemcpy(y.data(), dX, y.size() * 4, hipMemcpyDeviceToHost);
   double err = 0, ref2 = 0;
   int rows = 0;
-  for (int r = 0; r < R; r += (r < 130 ? 1 : 997)) {
+  // every row when the shape is small (the last block's tail included), else a sample
+  const bool all_rows = (double)R * D * F < 4e9;
+  long worst = -1;
+  for (int r = 0; r < R; r += (all_rows || r < 130 || r >= R - 130 ? 1 : 997)) {
     ++rows;
     std::vector<double> h(F);
     for (int j = 0; j < F; ++j) {
       double a = b1[j];
-      for (int k = 0; k < D; ++k) a += (double)x[(size_t)r * D + k] * w1[(size_t)j * D + k];
+      const float* in = sepY ? yv.data() : x.data();
+      for (int k = 0; k < D; ++k) a += (double)in[(size_t)r * D + k] * w1[(size_t)j * D + k];
       h[j] = swl(a);
     }
     for (int d = 0; d < D; ++d) {
       double o = b2[d];
       for (int j = 0; j < F; ++j) o += h[j] * w2[(size_t)d * F + j];
       const double ref = x[(size_t)r * D + d] + o;
+      if (std::fabs(ref - y[(size_t)r * D + d]) > err) worst = r;
       err = std::fmax(err, std::fabs(ref - y[(size_t)r * D + d]));
       ref2 += o * o;
     }
@@ -101,14 +115,40 @@ static void run(int D, int F, int R) {
     printf("\n");
   }
 #endif
-  printf("D %d F %d R %d: max|err| %.3e (out rms %.3f, rel %.2e, rows %d)  h3 %.1f us = %.3f of the fp16 peak "
+  if (dY) hipFree(dY);
+  printf("  worst row %ld of %d\n", worst, R);
+  printf("%sD %d F %d R %d: max|err| %.3e (out rms %.3f, rel %.2e, rows %d)  h3 %.1f us = %.3f of the fp16 peak "
          "(3 MFMA / product)  | bf16 %.1f us (%.3f)  ratio %.2f\n",
-         D, F, R, err, rms, err / rms, rows, us, 3 * fl / us / 1e6 / 2500.0, ub, fl / ub / 1e6 / 2500.0, us / ub);
+         sepY ? "(Y) " : "", D, F, R, err, rms, err / rms, rows, us, 3 * fl / us / 1e6 / 2500.0, ub, fl / ub / 1e6 / 2500.0, us / ub);
   fflush(stdout);
   hipFree(dX); hipFree(db1); hipFree(db2); hipFree(dW1); hipFree(dW2); hipFree(dH1); hipFree(dH2);
 }
 
 int main(int argc, char** argv) {
+  run(128, 384, 100, true);
+  run(128, 384, 100);
+  // the last block's remainder a whole TUM-group tile (rows past R clamped): rpb 224, 60 left
+  run(128, 384, 57180, true);
+  run(384, 1280, 57180);
+  run(512, 1536, 24680);        // rpb 112 on 48-row tiles, 40 left
+  run(192, 512, 39960);         // rpb 80 on 48-row tiles (two blocks per CU), 40 left
+  run(128, 384, 7068, true);    // rpb 32: every block one 32-row tile
+  run(128, 384, 11000, true);   // rpb 48: one 48-row tile
+  run(384, 1280, 7068);
+  run(256, 768, 7068);
+  run(128, 384, 57503, true);   // an M-set-like row count (not a multiple of 16)
+  run(128, 384, 57503);
+  run(384, 1280, 3029);
+  run(128, 384, 45056, true);   // rpb 176: two 64-row tiles + a 48-row tail
+  run(128, 384, 36864, true);   // rpb 144: two 64-row tiles + a 16-row tail
+  run(128, 384, 28672, true);   // rpb 112: one 64-row tile + a 48-row tail
+  run(384, 1280, 45056);        // rpb 176: 48-row tail
+  run(384, 1280, 20480);        // rpb 80: 64 + 16
+  run(256, 768, 24576);         // rpb 96: 64 + 32
+  run(512, 1536, 20480);        // rpb 80 (48-row tiles): 48 + 32
+  run(192, 512, 40960);         // two blocks per CU: rpb 80 = 48 + 32
+  run(128, 384, 3753659, true);
+  if (argc > 1) return 0;
   run(192, 512, 100);
   run(192, 384, 197614);
   run(192, 512, 197614);
