@@ -60,6 +60,47 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
+// ---- the f16x3 mode's one-accumulator products (FMT 1) ----
+// x = (x0, x1) = fp16 pieces (hi, lo 2^11) of the A operand (V^T or t1^T, staged in LDS); the
+// B operand (the weights P^T <= 1) carries three pieces: ys = hi 2^11 (exact in fp16), yh = hi,
+// yl = lo 2^11.  acc (scaled by 2^11) += x1 yh + x0 yl + x0 ys, smallest terms first:
+// the same three fp16 MFMAs as the two-accumulator form on one accumulator, so no lo
+// accumulator to hold, rescale and fold back (16 VGPRs per output fragment)
+typedef _Float16 f16x8a __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void mfma_h3s(const bf16x8 (&x)[2], const f16x8a& ys, const f16x8a& yh,
+                                         const f16x8a& yl, f32x16& acc) {
+  const f16x8a x0 = __builtin_bit_cast(f16x8a, x[0]), x1 = __builtin_bit_cast(f16x8a, x[1]);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, yh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, yl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, ys, acc, 0, 0, 0);
+}
+
+// pieces of 8 weights from e = 2^11 p (the exp2 argument carries the + 11; p <= 1, e <= 2048):
+// ys = fp16(e), yh = ys 2^-11, yl = fp16(e - ys) = (p - yh) 2^11 (e - ys is exact in f32)
+__device__ __forceinline__ void split_e8(const float* e, f16x8a& ys, f16x8a& yh, f16x8a& yl) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 sp, lp;
+#pragma unroll
+  for (int q = 0; q < 8; q += 2) {
+    const f16x2 h2 = {(_Float16)e[q], (_Float16)e[q + 1]};
+    const unsigned hs = __builtin_bit_cast(unsigned, h2);
+    // lo pieces e - fp16(e), exact in f32 and rounded once to fp16, by v_fma_mix (the fp16
+    // operand widened inside the instruction): 2 instructions a pair where widen / subtract /
+    // pack take 4 (the compiler does not form it from the C expression)
+    unsigned lo;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(lo) : "v"(hs), "v"(e[q]), "v"(e[q + 1]));
+    sp[q / 2] = hs;
+    lp[q / 2] = lo;
+  }
+  ys = __builtin_bit_cast(f16x8a, sp);
+  yl = __builtin_bit_cast(f16x8a, lp);
+  const _Float16 k = (_Float16)(1.f / 2048.f);
+  yh = ys * (f16x8a){k, k, k, k, k, k, k, k};
+}
+
 }  // namespace
 
 // NP = 1: bf16 storage (the bf16 mode).  NP = 2 / 3: q / k / p / v / out / the head-0 weights
@@ -69,8 +110,11 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 // (the bf16x3 / bf16x6 modes).  In these modes q and p carry no log2(e) factor: the score is
 // scaled into the log2 domain after the positional term.
 // FMT 1 (the f16x3 mode, NP = 2): the pieces are fp16 hi + lo * 2^-11 (gemm_dev.h split_h8)
-// and every product is hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16 MFMAs, the lo products in a
-// second accumulator (scores: combined per key block; O: at the end, and rescaled with O).
+// and every product is hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16 MFMAs: the scores with the lo
+// products in a second accumulator (combined per key block), the PV products in the
+// one-accumulator form (mfma_h3s): the weights enter as e = 2^11 p straight from the exp2
+// (p <= 1, so e's hi piece is exact in fp16), O accumulates 2^11-scaled on one register set
+// and the row sum, which carries the same 2^11, cancels it.
 // MODE 3 (NF = value fragments per block): NonlinAttention, z = (A0 @ t1) * y, in ONE online
 // pass over head 0: running max / sum as in mode 1, the unnormalised weights P^T (<= 1; the
 // score registers as they stand) multiplied into V^T = this block's NF x 32 rows of t1t
@@ -81,6 +125,8 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 template <int MODE, int NP, int FMT = 0, int NF = 1>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   constexpr bool SPLIT = NP > 1;
+  // FMT 1: the PV products in the one-accumulator form (mode 0 has no PV products)
+  constexpr bool P1 = FMT == 1;
   static_assert(FMT == 0 || NP == 2, "fp16 pieces: NP = 2");
   static_assert(MODE != 3 || NP == 1 || (NP == 2 && FMT == 1),
                 "fused NonlinAttention: the bf16 and f16x3 modes");
@@ -112,6 +158,9 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   const int i = i0 + c;
   const int ic = i < L ? i : L - 1;
   constexpr float kSc = SPLIT ? 1.4426950408889634f : 1.f;  // log2(e) applied in-kernel
+  // FMT 1: the weights enter the PV products as e = 2^11 p (exp2 argument + 11); the row sum
+  // then carries 2^11, which the normalisation cancels (mode 1's statistic subtracts the 11)
+  constexpr float kE = P1 ? 11.f : 0.f;
 
   // ---- positional rows: x in [xlo, xlo + L + kPosPad) ----
   {
@@ -292,6 +341,8 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
     if constexpr (FMT == 1) {
+      // (the scores keep two accumulators: their one-accumulator form needs |q| < 32 and
+      // measured slower in modes 1 / 2)
       f32x16 sl;
 #pragma unroll
       for (int r = 0; r < 16; ++r) sl[r] = 0.f;
@@ -347,9 +398,9 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
   // ---- key-block loop(s) ----
   float m = -INFINITY, l = 0.f, cst = 0.f;
   if constexpr (MODE == 2) cst = a.stats_in[(long)(r0 + ic) * H + h];
-  f32x16 o, ol;  // ol: the lo products of O (FMT 1)
+  f32x16 o;  // (P1: scaled by 2^11, the weights entering as e = 2^11 p)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = ol[r] = 0.f;
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
   // V^T fragments of the PV MFMAs; value dims d >= 12 (lanes c >= 12) stay zero
   bf16x8 vf[2][NP];
 #pragma unroll
@@ -360,12 +411,12 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
       for (int e = 0; e < 8; ++e) vf[mm][t][e] = (__bf16)0.f;
 
   constexpr int NPASS = MODE == 0 ? 2 : 1;
-  // mode 3: O^T per 32-row value fragment (FMT 1: o3l, the lo products)
-  f32x16 o3[MODE == 3 ? NF : 1], o3l[MODE == 3 && FMT == 1 ? NF : 1];
+  // mode 3: O^T per 32-row value fragment
+  f32x16 o3[MODE == 3 ? NF : 1];
 #pragma unroll
   for (int f = 0; f < (MODE == 3 ? NF : 1); ++f)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o3[f][r] = o3l[FMT == 1 ? f : 0][r] = 0.f;
+    for (int r = 0; r < 16; ++r) o3[f][r] = 0.f;
   T* const a0 = MODE == 0 ? reinterpret_cast<T*>(a.attn) + a.a_off[b] : nullptr;
   // (mode 3: both passes unrolled, so the V^T staging and o3 exist in pass 2's code only)
   constexpr int kPassUnroll = MODE == 3 ? 2 : 1;
@@ -418,16 +469,11 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
                 const f32x2 v = (f32x2){o3[f][r], o3[f][r + 1]} * (f32x2){sc, sc};
                 o3[f][r] = v.x;
                 o3[f][r + 1] = v.y;
-                if constexpr (FMT == 1) {
-                  const f32x2 w = (f32x2){o3l[f][r], o3l[f][r + 1]} * (f32x2){sc, sc};
-                  o3l[f][r] = w.x;
-                  o3l[f][r + 1] = w.y;
-                }
               }
             l *= sc;
             m = mn;
           }
-          const f32x2 nm = {-m, -m};
+          const f32x2 nm = {kE - m, kE - m};
           f32x2 acc = {0.f, 0.f};
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
@@ -440,11 +486,12 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
             bf16x8 pf[NP];
-            if constexpr (FMT == 1) {
-              float pv[8];
+            f16x8a ps3, ph3, pl3;  // P1: the weights' three pieces
+            if constexpr (P1) {
+              float ev[8];
 #pragma unroll
-              for (int q = 0; q < 8; ++q) pv[q] = s[8 * mm + q];
-              split_fx<FMT, NP>(pv, pf);
+              for (int q = 0; q < 8; ++q) ev[q] = s[8 * mm + q];
+              split_e8(ev, ps3, ph3, pl3);
             } else {
 #pragma unroll
               for (int q = 0; q < 8; ++q) pf[0][q] = (__bf16)s[8 * mm + q];
@@ -455,8 +502,8 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
               for (int t = 0; t < NP; ++t)
                 vf3[t] = *reinterpret_cast<const bf16x8*>(&sVn[t][cur][(f * 32 + c) * kKLd + 16 * mm + 8 * h2]);
-              if constexpr (FMT == 1)
-                mfma_h3(vf3, pf, o3[f], o3l[f]);
+              if constexpr (P1)
+                mfma_h3s(vf3, ps3, ph3, pl3, o3[f]);
               else
                 o3[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf3[0], pf[0], o3[f], 0, 0, 0);
             }
@@ -515,16 +562,11 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
                 const f32x2 v = (f32x2){o[r], o[r + 1]} * (f32x2){sc, sc};
                 o[r] = v.x;
                 o[r + 1] = v.y;
-                if constexpr (FMT == 1) {
-                  const f32x2 w = (f32x2){ol[r], ol[r + 1]} * (f32x2){sc, sc};
-                  ol[r] = w.x;
-                  ol[r + 1] = w.y;
-                }
               }
               l *= sc;
               m = mn;
             }
-            const f32x2 nm = {-m, -m};
+            const f32x2 nm = {kE - m, kE - m};
             f32x2 acc = {0.f, 0.f};
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
@@ -535,7 +577,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
             }
             l += acc.x + acc.y;
           } else {
-            const f32x2 nc = {-cst, -cst};
+            const f32x2 nc = {kE - cst, kE - cst};
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
               const f32x2 d = (f32x2){s[r], s[r + 1]} + nc;
@@ -546,11 +588,12 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
 #pragma unroll
           for (int mm = 0; mm < 2; ++mm) {
             bf16x8 pf[NP];
-            if constexpr (FMT == 1) {
-              float pv[8];
+            f16x8a ps3, ph3, pl3;  // P1: the weights' three pieces
+            if constexpr (P1) {
+              float ev[8];
 #pragma unroll
-              for (int q = 0; q < 8; ++q) pv[q] = s[8 * mm + q];
-              split_fx<FMT, NP>(pv, pf);
+              for (int q = 0; q < 8; ++q) ev[q] = s[8 * mm + q];
+              split_e8(ev, ps3, ph3, pl3);
             } else {
 #pragma unroll
               for (int q = 0; q < 8; ++q) {
@@ -568,10 +611,9 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
               for (int t = 0; t < NP; ++t)
                 vf[mm][t] = *reinterpret_cast<const bf16x8*>(&sVt[t][cur][c * kKLd + 16 * mm + 8 * h2]);
             }
-            if constexpr (FMT == 1) {
+            if constexpr (P1) {
               const bf16x8 x[2] = {vf[mm][0], vf[mm][1]};
-              const bf16x8 y[2] = {pf[0], pf[1]};
-              mfma_h3(x, y, o, ol);
+              mfma_h3s(x, ps3, ph3, pl3, o);
             } else {
               o = mfma_split<NP>(vf[mm], pf, o);
             }
@@ -606,7 +648,7 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
           float ov[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            ov[e] = (FMT == 1 ? o3[f][4 * g + e] + o3l[f][4 * g + e] * kF16LoInv : o3[f][4 * g + e]) * inv;
+            ov[e] = o3[f][4 * g + e] * inv;  // (P1: o3 and l both carry 2^11)
           if constexpr (SPLIT) {
             const float4 yv = *reinterpret_cast<const float4*>(yrow + c0);
             *reinterpret_cast<float4*>(zrow + c0) =
@@ -626,12 +668,10 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnFlashArgs a) {
     float inv = 1.f;
     if constexpr (MODE == 1) {
       const float lt = l + __shfl_xor(l, 32, 64);
-      inv = 1.f / lt;
-      if (h2 == 0) a.stats_out[(long)(r0 + i) * H + h] = m + __log2f(lt);
-    }
-    if constexpr (FMT == 1) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) o[r] += ol[r] * kF16LoInv;
+      inv = 1.f / lt;  // (P1: o and lt both carry 2^11)
+      if (h2 == 0) a.stats_out[(long)(r0 + i) * H + h] = m + __log2f(lt) - kE;
+    } else if constexpr (P1) {
+      inv = 1.f / 2048.f;  // mode 2: o carries 2^11
     }
     // O^T rows = value dims d = (r&3) + 8 (r>>2) + 4 h2; d < 12 valid
     T* dst = reinterpret_cast<T*>(a.out) + (long)(r0 + i) * ldv + 12 * h;

@@ -227,7 +227,8 @@ void launch_attn_softmax(const AttnArgs& a, hipStream_t st);
 //   mode 3: NonlinAttention fused, one online pass over head 0: running max / sum, the
 //           unnormalised weights multiplied into t1 as they are computed (value accumulators
 //           rescaled when the max moves), 1 / sum and * y in the epilogue; bf16 or f16x3
-//           (pieces == kPiecesF16: two fp16 pieces of the weights and of t1)
+//           (pieces == kPiecesF16: fp16 pieces of the weights and of t1, one-accumulator
+//           products, f32 y / z)
 // stats: [R][H] c = row max + log2(row sum), log2 domain
 struct AttnFlashArgs {
   const void* qkp;         // [R][68 H]: bf16 (pieces == 1) or f32
