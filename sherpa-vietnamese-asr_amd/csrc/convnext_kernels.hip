@@ -91,34 +91,33 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
   static_assert(PPR == 8, "eight 16-byte pieces per row");
   typedef T T8 __attribute__((ext_vector_type(EPP)));
   __shared__ __attribute__((aligned(16))) T tile[kDwH * kDwF * C];
+  // the weights pass through the tile's storage before the tile is written (C * 49 floats fit)
+  float* const sW = reinterpret_cast<float*>(tile);
+  static_assert(C * 49 * 4 <= (int)sizeof(tile), "weights staged in the tile buffer");
   __shared__ int sLo[kDwT], sHi[kDwT], sMasked;
   const int t0 = blockIdx.x * kDwT;
   const int c0 = blockIdx.y * C;
   const int tid = threadIdx.x;
   if (tid == 0) sMasked = 0;
-  // every global load of the block is issued before the first wait: this thread's channel
-  // pair weights and bias, the sequence bounds of the tile frames (L_map -> L_off) and the
-  // staged input -- one memory round trip instead of three
+  // every global load of the block is issued before the first wait: the block's channel
+  // weights (staged through LDS with coalesced loads: per-thread loads of its own channels'
+  // rows of dw_w [128][49] would touch one cache line per lane and instruction), the bias,
+  // the sequence bounds of the tile frames (L_map -> L_off) and the staged input -- one memory
+  // round trip
   const int p = tid & (PAIRS - 1);  // channel pair c0 + 2p, c0 + 2p + 1 (fixed per thread)
-  float2 w[49];
+  constexpr int kWIt = (C * 49 + 255) / 256;
+  float wl[kWIt];
 #pragma unroll
-  for (int k = 0; k < 49; ++k)
-    w[k] = make_float2(dw_w[(c0 + 2 * p) * 49 + k], dw_w[(c0 + 2 * p + 1) * 49 + k]);
+  for (int q = 0; q < kWIt; ++q) {
+    const int i = tid + 256 * q;
+    wl[q] = dw_w[c0 * 49 + (i < C * 49 ? i : C * 49 - 1)];
+  }
   const float2 bias = make_float2(dw_b[c0 + 2 * p], dw_b[c0 + 2 * p + 1]);
   int seq_lo = 0, seq_hi = 0;
   if (tid < kDwT && t0 + tid < total_rows) {
     const int b = L_map[t0 + tid];
     seq_lo = L_off[b];
     seq_hi = L_off[b + 1];
-  }
-  // ---- zero freq padding columns (3 + 3 per staged frame, 8 pieces of 16 B each) ----
-  for (int e = tid; e < kDwH * 6 * 8; e += 256) {
-    const int q = e & 7, cf = (e >> 3) % 6, rr = (e >> 3) / 6;
-    const int fcol = cf < 3 ? cf : 19 + cf;
-    T8 z;
-#pragma unroll
-    for (int t = 0; t < EPP; ++t) z[t] = (T)0.f;
-    *reinterpret_cast<T8*>(tile + (rr * kDwF + fcol) * C + EPP * q) = z;
   }
   // ---- stage frames t0-3 .. t0+18, channels c0..c0+C-1: 22 x 19 x 8 16-byte pieces ----
   constexpr int kPieces = kDwH * 19 * 8;  // 3344
@@ -138,6 +137,26 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
 #pragma unroll
       for (int t = 0; t < EPP; ++t) v[k][t] = (T)0.f;
     }
+  }
+  // ---- the weights: loads in flight -> LDS -> this thread's channel pair ----
+#pragma unroll
+  for (int q = 0; q < kWIt; ++q) {
+    const int i = tid + 256 * q;
+    if (i < C * 49) sW[i] = wl[q];
+  }
+  __syncthreads();
+  float2 w[49];
+#pragma unroll
+  for (int k = 0; k < 49; ++k) w[k] = make_float2(sW[2 * p * 49 + k], sW[(2 * p + 1) * 49 + k]);
+  __syncthreads();  // every thread holds its weights before the tile overwrites them
+  // ---- zero freq padding columns (3 + 3 per staged frame, 8 pieces of 16 B each) ----
+  for (int e = tid; e < kDwH * 6 * 8; e += 256) {
+    const int q = e & 7, cf = (e >> 3) % 6, rr = (e >> 3) / 6;
+    const int fcol = cf < 3 ? cf : 19 + cf;
+    T8 z;
+#pragma unroll
+    for (int t = 0; t < EPP; ++t) z[t] = (T)0.f;
+    *reinterpret_cast<T8*>(tile + (rr * kDwF + fcol) * C + EPP * q) = z;
   }
 #pragma unroll
   for (int k = 0; k < kIt; ++k) {

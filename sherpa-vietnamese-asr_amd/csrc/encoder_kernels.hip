@@ -553,24 +553,25 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
   constexpr int nf4 = nrows * 16;
   constexpr int kIt = (nf4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) float tile[nrows * 64];
+  __shared__ float sW[64 * K];
   __shared__ int sLo[kDw1T], sHi[kDw1T], sMasked;
   const int r0 = blockIdx.x * kDw1T;
   const int c0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
   if (tid == 0) sMasked = 0;
-  // every global load of the block is issued before the first wait: this lane's channel
-  // weights and bias, the sequence bounds of the tile rows (map -> off) and the staged
-  // input -- one memory round trip instead of three
+  // every global load of the block is issued before the first wait: the block's channel
+  // weights (staged through LDS: w is [d][Kr], so per-lane loads of a lane's own row would
+  // touch one cache line per lane and instruction), the bias, the sequence bounds of the tile
+  // rows (map -> off) and the staged input -- one memory round trip
   const int c = tid & 63;
   const int cw = c0 + c < d ? c0 + c : d - 1;  // clamped: lanes past d never store
-  float wr[K];
-  const int pad = (K - Kr) / 2;
+  const int nw = (d - c0 < 64 ? d - c0 : 64) * Kr;
+  constexpr int kWIt = (64 * K + 255) / 256;
+  float wl[kWIt];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int kk = k - pad;
-    const bool ok = kk >= 0 && kk < Kr;
-    const float wv = w[(long)cw * Kr + (ok ? kk : 0)];
-    wr[k] = ok ? wv : 0.f;
+  for (int q = 0; q < kWIt; ++q) {
+    const int i = tid + 256 * q;
+    wl[q] = w[(long)c0 * Kr + (i < nw ? i : nw - 1)];
   }
   const float bc = bias[cw];
   int seq_lo = 0, seq_hi = 0;
@@ -610,7 +611,26 @@ __global__ __launch_bounds__(256) void glu_dwconv1d_kernel(
       if (e < nf4) *reinterpret_cast<float4*>(&tile[rr * 64 + 4 * c4]) = v;
     }
   }
+#pragma unroll
+  for (int q = 0; q < kWIt; ++q) {
+    const int i = tid + 256 * q;
+    if (i < nw) sW[i] = wl[q];
+  }
   __syncthreads();
+  // this lane's taps (zero past Kr, centred): row c of the staged [64][Kr] block, an odd
+  // stride, so the 64 lanes' reads fall in distinct banks
+  float wr[K];
+  {
+    const int pad = (K - Kr) / 2;
+    const int cl = c0 + c < d ? c : (d - c0) - 1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int kk = k - pad;
+      const bool ok = kk >= 0 && kk < Kr;
+      const float wv = sW[cl * Kr + (ok ? kk : 0)];
+      wr[k] = ok ? wv : 0.f;
+    }
+  }
   if (tid < kDw1T) {
     const int r = r0 + tid;
     int lo = -half, hi = half;
