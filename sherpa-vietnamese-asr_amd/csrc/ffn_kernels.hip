@@ -437,6 +437,38 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr float kF16Lo = 2048.f, kF16LoInv = 1.f / 2048.f;  // gemm_dev.h's piece scale
 
+// SwooshL of the 2^11-scaled accumulator as its two fp16 pieces (hi, lo 2^11), in 2^11 units
+// throughout: ys = acc + 2^11 (b1 - 4) = 2^11 y with y = x - 4 (bs = that bias), so
+//   2^11 SwooshL(x) = max(ys, 0) + 2^11 ln2 log2(1 + 2^(-|ys| log2(e) 2^-11)) - 0.08 ys - 2^11 0.355
+// (softplus_fast's form), hi = fp16(r 2^-11), lo = fp16(r - 2^11 hi) by v_fma_mix (the fp16
+// operand widened inside the instruction; the compiler does not form it from C): ~9 VALU and
+// 2 transcendentals a value where scaling, shifting, widening and subtracting took ~12
+__device__ __forceinline__ void swooshl_pieces2(float a0, float a1, float bs0, float bs1,
+                                                _Float16& h0, _Float16& h1, _Float16& l0,
+                                                _Float16& l1) {
+  constexpr float kL = -1.4426950408889634f / 2048.f, kLn = 0.6931471805599453f * 2048.f;
+  constexpr float kC = -0.355f * 2048.f;
+  float r[2];
+  const float ys[2] = {a0 + bs0, a1 + bs1};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float l = __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(fabsf(ys[q]) * kL));
+    r[q] = fmaf(ys[q], -0.08f, fmaf(l, kLn, fmaxf(ys[q], 0.f))) + kC;
+  }
+  typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+  const f16x2_t hh = {(_Float16)(r[0] * (1.f / 2048.f)), (_Float16)(r[1] * (1.f / 2048.f))};
+  const unsigned hu = __builtin_bit_cast(unsigned, hh);
+  unsigned lo;
+  asm("v_fma_mixlo_f16 %0, %1, %4, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, %4, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lo) : "v"(hu), "v"(r[0]), "v"(r[1]), "v"(-2048.f));
+  const f16x2_t ll = __builtin_bit_cast(f16x2_t, lo);
+  h0 = hh[0];
+  h1 = hh[1];
+  l0 = ll[0];
+  l1 = ll[1];
+}
+
 // acc (2^11 scale) += w_lo x_hi + w_hi x_lo + w_s x_hi, w_s = w_hi 2^11; smallest terms first
 __device__ __forceinline__ void mfma16_h3(f32x4v& acc, const f16x8& wh, const f16x8& wl,
                                           const f16x8& ws, const f16x8& xh, const f16x8& xl) {
@@ -584,18 +616,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
     _Float16* sH1 = sH[NB == 2 ? (c & 1) : 0][1];
     if constexpr (NB == 1) lds_barrier();  // the previous chunk's phase B is done with sH
     {
-      const float bv[4] = {bb[0], bb[1], bb[2], bb[3]};
-      const float hm = hvalid ? 1.f : 0.f;  // hidden units past F: zero H (no branch: its
-                                            // waits would drain the weight loads in flight)
+      // hidden units past F: zero H, the pieces masked (no branch: its waits would drain the
+      // weight loads in flight)
+      const float bs[4] = {2048.f * (bb[0] - 4.f), 2048.f * (bb[1] - 4.f), 2048.f * (bb[2] - 4.f),
+                           2048.f * (bb[3] - 4.f)};
+      const f16x4 hmk = hvalid ? f16x4{(_Float16)1.f, (_Float16)1.f, (_Float16)1.f, (_Float16)1.f}
+                               : f16x4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
 #pragma unroll
       for (int u = 0; u < TU; ++u) {
-        f16x4 hh, ll;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float v = swooshl_fast(ha[u][q] * kF16LoInv + bv[q]) * hm;
-          hh[q] = (_Float16)v;
-          ll[q] = (_Float16)((v - (float)hh[q]) * kF16Lo);
-        }
+        _Float16 h4[4], l4[4];
+        swooshl_pieces2(ha[u][0], ha[u][1], bs[0], bs[1], h4[0], h4[1], l4[0], l4[1]);
+        swooshl_pieces2(ha[u][2], ha[u][3], bs[2], bs[3], h4[2], h4[3], l4[2], l4[3]);
+        const f16x4 hh = f16x4{h4[0], h4[1], h4[2], h4[3]} * hmk;
+        const f16x4 ll = f16x4{l4[0], l4[1], l4[2], l4[3]} * hmk;
         const int ho = (16 * u + r16) * HLD + wid * 16 + 4 * g4;
         *reinterpret_cast<f16x4*>(&sH0[ho]) = hh;
         *reinterpret_cast<f16x4*>(&sH1[ho]) = ll;
