@@ -328,8 +328,9 @@ void launch_silence_flags(const float* wav, long n, int frame_len, float thresho
 // conv.0: Conv2d(1 -> 8, 3x3, padding (0, 1)) + SwooshR.  One thread per (t, f).
 // =====================================================================================
 // BF16: bf16 output and the native-exp/log SwooshR (the bf16 mode; conv.4 reads it through
-// its bf16 implicit-im2col loader); f32: the libm form (the fp32 parity mode)
-template <bool BF16>
+// its bf16 implicit-im2col loader); f32: the libm form (the fp32 mode), or with FAST the
+// native form (the split modes: their GEMM epilogues' SwooshR is swooshr_fast too)
+template <bool BF16, bool FAST = BF16>
 __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict__ fb_off,
                              const int* __restrict__ c1_off, const int* __restrict__ c1_map,
                              int total,
@@ -356,7 +357,7 @@ __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict
     float acc = bias[o];
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc = fmaf(w[o * 9 + k], xin[k], acc);
-    r[o] = BF16 ? swooshr_fast(acc) : swooshr(acc);
+    r[o] = FAST ? swooshr_fast(acc) : swooshr(acc);
   }
   if constexpr (BF16) {
     typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -373,12 +374,15 @@ __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict
 
 void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const int* c1_map,
                   int total_rows, const float* w, const float* b, void* out, bool out_bf16,
-                  hipStream_t st) {
+                  hipStream_t st, bool fast) {
   if (total_rows <= 0) return;
   long n = (long)total_rows * 80;
   if (out_bf16)
     hipLaunchKernelGGL(conv1_kernel<true>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
                        c1_off, c1_map, total_rows, w, b, out);
+  else if (fast)
+    hipLaunchKernelGGL((conv1_kernel<false, true>), dim3(cdivl(n, 256)), dim3(256), 0, st, fb,
+                       fb_off, c1_off, c1_map, total_rows, w, b, out);
   else
     hipLaunchKernelGGL(conv1_kernel<false>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
                        c1_off, c1_map, total_rows, w, b, out);
