@@ -795,18 +795,33 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict
                                                             const int* __restrict__ map, int R,
                                                             int hid, int R8,
                                                             __bf16* __restrict__ t1t) {
+  // tiled over the OUTPUT: 64 columns of t1t (packed rows of one or two sequences, or their
+  // zero padding up to L32) x 64 channels, so every store is a 32-byte piece of a channel's
+  // contiguous column run and the padding needs no separate pass
   __shared__ float tile[64][65];
-  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  __shared__ int sRow[64];
+  const int col0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const int tid = threadIdx.x;
-  // load: 64 rows x 16 float4 per tile, 4 per thread, all loads in flight first
+  if (tid < 64) {
+    const int col = col0 + tid;
+    int lo = 0, hi = map[R - 1];  // (trailing empty sequences own no columns)  // the sequence owning column col: largest b with o8[b] <= col
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (o8[mid] <= col) lo = mid;
+      else hi = mid - 1;
+    }
+    const int j = col - o8[lo];
+    sRow[tid] = (col < R8 && j < off[lo + 1] - off[lo]) ? off[lo] + j : -1;
+  }
+  __syncthreads();
   float4 sv[4], xv[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int idx = tid + 256 * k;
     const int rl = idx >> 4, c4 = idx & 15;
-    const int r = r0 + rl < R ? r0 + rl : R - 1;
+    const int r = sRow[rl];
     const int cc = c0 + 4 * c4 < hid ? c0 + 4 * c4 : hid - 4;
-    const TH* row = h3 + (long)r * 3 * hid;
+    const TH* row = h3 + (long)(r < 0 ? 0 : r) * 3 * hid;
     sv[k] = h3_load4(row + cc);
     xv[k] = h3_load4(row + hid + cc);
   }
@@ -814,40 +829,49 @@ __global__ __launch_bounds__(256) void nonlin_prep_t_kernel(const TH* __restrict
   for (int k = 0; k < 4; ++k) {
     const int idx = tid + 256 * k;
     const int rl = idx >> 4, c4 = idx & 15;
-    tile[4 * c4 + 0][rl] = tanhf(sv[k].x) * xv[k].x;
-    tile[4 * c4 + 1][rl] = tanhf(sv[k].y) * xv[k].y;
-    tile[4 * c4 + 2][rl] = tanhf(sv[k].z) * xv[k].z;
-    tile[4 * c4 + 3][rl] = tanhf(sv[k].w) * xv[k].w;
+    const float m = sRow[rl] < 0 ? 0.f : 1.f;  // padding columns: zeros
+    tile[4 * c4 + 0][rl] = tanhf(sv[k].x) * xv[k].x * m;
+    tile[4 * c4 + 1][rl] = tanhf(sv[k].y) * xv[k].y * m;
+    tile[4 * c4 + 2][rl] = tanhf(sv[k].z) * xv[k].z * m;
+    tile[4 * c4 + 3][rl] = tanhf(sv[k].w) * xv[k].w * m;
   }
   __syncthreads();
-  const int rl = tid & 63;
-  const int r = r0 + rl;
-  if (r >= R) return;
-  const int b = map[r];
-  const int shift = o8[b] - off[b];
-  const int col = r + shift;
-  const bool last = r == off[b + 1] - 1;
-  const int pad_end = o8[b] + ((off[b + 1] - off[b] + 31) & ~31);
-  for (int cl = tid >> 6; cl < 64; cl += 4) {
-    const int ch = c0 + cl;
-    if (ch >= hid) break;
-    __bf16* dst = t1t + (long)ch * R8;
-    float v = tile[cl][rl];
-    if constexpr (NP == kPiecesF16) {
-      const _Float16 hh = (_Float16)v;
-      dst[col] = __builtin_bit_cast(__bf16, hh);
-      dst[(long)hid * R8 + col] = __builtin_bit_cast(__bf16, (_Float16)((v - (float)hh) * kF16Lo));
-      if (last)
-        for (int z = col + 1; z < pad_end; ++z) dst[z] = dst[(long)hid * R8 + z] = (__bf16)0.f;
-    } else {
+  // channel cl, columns 16 g .. 16 g + 15: reads tile row cl (stride 65: conflict-free)
+  const int cl = tid >> 2, g = tid & 3;
+  const int ch = c0 + cl;
+  const int cs = col0 + 16 * g;
+  if (ch >= hid || cs >= R8) return;  // R8 % 32 == 0: a 16-column group is all in or all out
+  float v[16];
 #pragma unroll
-      for (int t = 0; t < NP; ++t) {
-        const __bf16 hh = (__bf16)v;
-        dst[(long)t * hid * R8 + col] = hh;
-        if (t + 1 < NP) v -= (float)hh;
-        if (last)
-          for (int z = col + 1; z < pad_end; ++z) dst[(long)t * hid * R8 + z] = (__bf16)0.f;
+  for (int i = 0; i < 16; ++i) v[i] = tile[cl][16 * g + i];
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  __bf16* dst = t1t + (long)ch * R8 + cs;
+  if constexpr (NP == kPiecesF16) {
+    typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+    f16x8_t h[2], l[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const _Float16 hh = (_Float16)v[i];
+      h[i >> 3][i & 7] = hh;
+      l[i >> 3][i & 7] = (_Float16)((v[i] - (float)hh) * kF16Lo);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      *reinterpret_cast<f16x8_t*>(dst + 8 * q) = h[q];
+      *reinterpret_cast<f16x8_t*>(dst + (long)hid * R8 + 8 * q) = l[q];
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      bf16x8_t p[2];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const __bf16 hh = (__bf16)v[i];
+        p[i >> 3][i & 7] = hh;
+        if (t + 1 < NP) v[i] -= (float)hh;
       }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) *reinterpret_cast<bf16x8_t*>(dst + (long)t * hid * R8 + 8 * q) = p[q];
     }
   }
 }
@@ -859,7 +883,8 @@ void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const in
   ZASR_REQUIRE(hid % 4 == 0, "nonlin_prep_t: hid must be a multiple of 4");
   ZASR_REQUIRE(pieces == 1 || (!h3_bf16 && (pieces == 2 || pieces == 3 || pieces == kPiecesF16)),
                "nonlin_prep_t: pieces must be 1 (or 2 / 3 / kPiecesF16 for an f32 h3)");
-  const dim3 grid(cdiv(R, 64), cdiv(hid, 64));
+  ZASR_REQUIRE(R8 % 32 == 0, "nonlin_prep_t: t1t columns are 32-padded per sequence");
+  const dim3 grid(cdiv(R8, 64), cdiv(hid, 64));
   __bf16* out = reinterpret_cast<__bf16*>(t1t);
   const float* h3f = reinterpret_cast<const float*>(h3);
   if (h3_bf16)

@@ -328,8 +328,9 @@ void launch_silence_flags(const float* wav, long n, int frame_len, float thresho
 // conv.0: Conv2d(1 -> 8, 3x3, padding (0, 1)) + SwooshR.  One thread per (t, f).
 // =====================================================================================
 // BF16: bf16 output and the native-exp/log SwooshR (the bf16 mode; conv.4 reads it through
-// its bf16 implicit-im2col loader); f32: the libm form (the fp32 mode), or with FAST the
-// native form (the split modes: their GEMM epilogues' SwooshR is swooshr_fast too)
+// its bf16 implicit-im2col loader); f32: the libm form (fp32, bf16x3, bf16x6), or with FAST the
+// native form (f16x3, whose GEMM epilogues' SwooshR is swooshr_fast too; in bf16x6 the native
+// form flipped a near-tie beam chunk of the widened oracle set, so that mode keeps libm)
 template <bool BF16, bool FAST = BF16>
 __global__ void conv1_kernel(const float* __restrict__ fb, const int* __restrict__ fb_off,
                              const int* __restrict__ c1_off, const int* __restrict__ c1_map,

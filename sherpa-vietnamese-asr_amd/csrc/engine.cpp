@@ -1419,7 +1419,7 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
                   : (void*)ws<float>("fe_c1", (size_t)mc1.total * 640);
   prof_begin("frontend_conv");
   launch_conv1(d_feats, I(o_fb), I(o_c1), c1_map, mc1.total, model_.conv0_w, model_.conv0_b, c1,
-               fe16, st_, split_pieces() != 0);
+               fe16, st_, split_pieces() == kPiecesF16);
   prof_end();
   void* c2 = fe16 ? (void*)ws<__bf16>("fe_c2_h", (size_t)mc2.total * 39 * 32)
                   : (void*)ws<float>("fe_c2", (size_t)mc2.total * 39 * 32);

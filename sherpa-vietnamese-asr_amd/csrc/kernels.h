@@ -130,7 +130,7 @@ void launch_vad_lstm(const VadLstmArgs& a, int n_segments, hipStream_t st);
 // ---- Conv2dSubsampling pieces (icefall subsampling.py, 3P) ----
 // conv.0 (1->8, 3x3, pad (0,1)) + SwooshR: fbank rows [T][80] -> [T-2][80][8]
 // (out_bf16: bf16 output, native-exp/log SwooshR -- the bf16 mode; fast: f32 output with the
-// native-exp/log SwooshR -- the split modes, whose GEMM epilogues use the same form)
+// native-exp/log SwooshR -- the f16x3 mode, whose GEMM epilogues use the same form)
 void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const int* c1_map,
                   int total_rows, const float* w /*[8][9]*/, const float* b, void* out,
                   bool out_bf16, hipStream_t st, bool fast = false);
