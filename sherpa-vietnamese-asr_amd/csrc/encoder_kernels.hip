@@ -737,6 +737,9 @@ struct DsW {
 };
 
 // float4 per thread, 32-bit index math (rows * d / 4 < 2^31 at any batch the engine forms)
+// DS = the factor (2, 4, 8): exactly DS loads per output; DS = 0: any factor <= 8 at run time
+// (8 loads per output, the ones past ds duplicates)
+template <int DS>
 __global__ void downsample_kernel(const float* __restrict__ x, const int* __restrict__ off_in,
                                   const int* __restrict__ off_out, const int* __restrict__ map_out,
                                   int total_out,
@@ -749,17 +752,19 @@ __global__ void downsample_kernel(const float* __restrict__ x, const int* __rest
   const int base = off_in[b];
   const int L = off_in[b + 1] - base;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  float4 xv[8];
+  constexpr int NL = DS > 0 ? DS : 8;
+  const int f = DS > 0 ? DS : ds;
+  float4 xv[NL];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {  // all loads in flight (ds <= 8)
-    int t = tp * ds + (u < ds ? u : 0);
+  for (int u = 0; u < NL; ++u) {  // all loads in flight
+    int t = tp * f + (u < f ? u : 0);
     if (t > L - 1) t = L - 1;  // SimpleDownsample pads with the last frame
     xv[u] = x4[(base + t) * d4 + c4];
   }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
-    if (u < ds) {
+  for (int u = 0; u < NL; ++u)
+    if (u < f) {
       acc.x = fmaf(wts.w[u], xv[u].x, acc.x);
       acc.y = fmaf(wts.w[u], xv[u].y, acc.y);
       acc.z = fmaf(wts.w[u], xv[u].z, acc.z);
@@ -776,8 +781,14 @@ void launch_downsample(const float* x, const int* off_in, const int* off_out, co
   ZASR_REQUIRE(d % 4 == 0 && n < (1L << 31), "downsample: width must be a multiple of 4");
   DsW w{};
   for (int i = 0; i < ds && i < 8; ++i) w.w[i] = w_host8[i];
-  hipLaunchKernelGGL(downsample_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in,
-                     off_out, map_out, total_out, d / 4, ds, w, out);
+  ZASR_REQUIRE(ds >= 1 && ds <= 8, "downsample: factor must be in [1, 8]");
+#define ZASR_DS(DSV) hipLaunchKernelGGL((downsample_kernel<DSV>), dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in, \
+                                        off_out, map_out, total_out, d / 4, ds, w, out)
+  if (ds == 2) ZASR_DS(2);
+  else if (ds == 4) ZASR_DS(4);
+  else if (ds == 8) ZASR_DS(8);
+  else ZASR_DS(0);
+#undef ZASR_DS
 }
 
 // The seam between encoder stacks (icefall Zipformer2Encoder / DownsampledZipformer2Encoder,
