@@ -53,6 +53,20 @@ constexpr int kW2Ld = 40;  // W2 chunk row stride (bf16): 80 B
 // slot of hidden index k (0..31) in a permuted W2 chunk row: swap bits 2 and 3
 __device__ __forceinline__ int w2_slot(int k) { return (k & 0x13) | ((k & 4) << 1) | ((k & 8) >> 1); }
 
+// weight fragments by buffer loads: a descriptor over [p, p + bytes) in SGPRs (p and bytes
+// wave-uniform); a fragment's byte offset is wave-uniform too (an SGPR operand) and the lane's
+// 16 bytes a constant VGPR, so a load needs no 64-bit address arithmetic
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, long bytes) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long)p >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long)hi << 32) | lo), 0, n, 0x00020000);
+}
+template <typename V>
+__device__ __forceinline__ V buf_load16(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
 }  // namespace
 
 template <int D>
@@ -469,17 +483,6 @@ __device__ __forceinline__ void swooshl_pieces2(float a0, float a1, float bs0, f
   l1 = ll[1];
 }
 
-// a buffer descriptor over [p, p + bytes) held in SGPRs (p and bytes wave-uniform)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, long bytes) {
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)p);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long)p >> 32));
-  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long)hi << 32) | lo), 0, n, 0x00020000);
-}
-__device__ __forceinline__ f16x8 buf_load16(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-}
-
 // acc (2^11 scale) += w_lo x_hi + w_hi x_lo + w_s x_hi, w_s = w_hi 2^11; smallest terms first
 __device__ __forceinline__ void mfma16_h3(f32x4v& acc, const f16x8& wh, const f16x8& wl,
                                           const f16x8& ws, const f16x8& xh, const f16x8& xl) {
@@ -529,8 +532,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   auto load_w1 = [&](int c, int s, int slot) {
     const int rg = min((c * HC) / 16 + wid, F / 16 - 1);
     const int so = (rg * KS + s) * 1024;
-    w1r[slot][0] = buf_load16(rs1, voff, so);
-    w1r[slot][1] = buf_load16(rs1, voff, so + pcb);
+    w1r[slot][0] = buf_load16<f16x8>(rs1, voff, so);
+    w1r[slot][1] = buf_load16<f16x8>(rs1, voff, so + pcb);
   };
   f16x8 w2r[2][OT][2];
   auto load_w2 = [&](int c, int s, int slot) {
@@ -538,8 +541,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
 #pragma unroll
     for (int t = 0; t < OT; ++t) {
       const int so = ((wid * OT + t) * S2 + ks) * 1024;
-      w2r[slot][t][0] = buf_load16(rs2, voff, so);
-      w2r[slot][t][1] = buf_load16(rs2, voff, so + pcb);
+      w2r[slot][t][0] = buf_load16<f16x8>(rs2, voff, so);
+      w2r[slot][t][1] = buf_load16<f16x8>(rs2, voff, so + pcb);
     }
   };
   FFN_STAMP(0)
