@@ -727,6 +727,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   if (tail == 1) tile(T1{}, t0);
   if constexpr (TUM > 2) if (tail == 2) tile(T2{}, t0);
   if constexpr (TUM > 3) if (tail == 3) tile(T3{}, t0);
+  if constexpr (TUM > 4) if (tail == 4) tile(std::integral_constant<int, 4>{}, t0);
+  if constexpr (TUM > 5) if (tail == 5) tile(std::integral_constant<int, 5>{}, t0);
+  if constexpr (TUM > 6) if (tail == 6) tile(std::integral_constant<int, 6>{}, t0);
+  if constexpr (TUM > 7) if (tail == 7) tile(std::integral_constant<int, 7>{}, t0);
+  static_assert(TUM <= 8, "tail tiles");
   if (tail == TUM) tile(TM{}, t0);
 }
 
@@ -782,9 +787,13 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
   hipLaunchKernelGGL((ffn_wide_h3_kernel<DV, TUV, NBV, NWV>), grid, dim3(64 * NWV), 0, st, X, R, F, w1, \
                      b1, w2, b2, byp_orig, byp_scale, rpb, Y)
   switch (D) {
-    case 128: ZASR_FFNH3(128, 4, 2, 8); break;
-    case 192: ZASR_FFNH3(192, 3, 2, 4); break;
-    case 256: ZASR_FFNH3(256, 4, 2, 8); break;
+    // tile rows (16 TUM) / H buffers: the largest tile the LDS and 256 VGPRs hold -- fewer
+    // weight passes from L2 and barriers per row, for a barrier per chunk with one H buffer
+    // (profiles/r05/ab_s3/ffn_h3_tiles.txt: 4 x 16 rows with two buffers (d = 192: 3 x 16)
+    // cost 0.29 ms per hour on the ConvNeXt MLP (d = 128), 0.15 at d = 256, 0.07 at d = 192)
+    case 128: ZASR_FFNH3(128, 8, 1, 8); break;
+    case 192: ZASR_FFNH3(192, 4, 1, 4); break;
+    case 256: ZASR_FFNH3(256, 5, 1, 8); break;
     case 384: ZASR_FFNH3(384, 4, 1, 8); break;
     default: ZASR_FFNH3(512, 3, 2, 8); break;
   }
