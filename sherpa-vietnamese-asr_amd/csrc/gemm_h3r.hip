@@ -6,7 +6,7 @@
 //
 // The structure is phase A of the fused f16x3 FFN (ffn_kernels.hip ffn_wide_h3_kernel) with an
 // epilogue per column chunk instead of phase B: one 8-wave block per CU owns a per-CU share of
-// the rows; a 64-row tile of A is split once into its two fp16 pieces (hi, lo 2^11) in LDS, and
+// the rows; a 64-128-row tile of A is split once into its two fp16 pieces (hi, lo 2^11) in LDS, and
 // the block walks all N columns in chunks of 128 (16 per wave), W's pieces streaming from L2
 // in MFMA-fragment order (ffn_pack_h3_host) through a register ring that runs on across chunks
 // and tiles.  Products on v_mfma_f32_16x16x32_f16 in the one-accumulator form (w_lo x_hi +
@@ -48,9 +48,14 @@ struct H3RArgs {
 
 template <int K, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
-  constexpr int NW = 8, TUM = 4, TTM = 16 * TUM, CW = 16 * NW;
   // row stride in halves: 16 (8 j + 2)-byte rows keep the 16x16x32 operand reads conflict-free
   constexpr int XLD = K + (K % 64 == 0 ? 16 : 48);
+  // 16-row groups per tile: as many as the LDS (64 XLD bytes per group) and 256 VGPRs hold --
+  // each W pass from L2 feeds more rows (profiles/r05/ab_s3/h3r_tiles.txt: enc_gemm -2.4 %
+  // vs 4 groups at every K; 6 groups at K = 288 / 384 spill)
+  constexpr int TUL = 160 * 1024 / (64 * XLD), TUMAX = K <= 192 ? 8 : K <= 256 ? 6 : 4;
+  constexpr int NW = 8, TUM = TUL < TUMAX ? TUL : TUMAX, TTM = 16 * TUM, CW = 16 * NW;
+  static_assert(TUM >= 1 && TUM <= 8, "tile height");
   constexpr int KS = K / 32;
   // W ring depth, a divisor of KS (twice the k-steps in flight measured no better:
   // profiles/r05/gemm_h3r/)
@@ -181,9 +186,6 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
     }
   };
 
-  using T1 = std::integral_constant<int, 1>;
-  using T2 = std::integral_constant<int, 2>;
-  using T3 = std::integral_constant<int, 3>;
   using TM = std::integral_constant<int, TUM>;
   long t0 = r0;
   bool first = true;
@@ -192,9 +194,13 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
   // the last one (M need not be): a TUM-group remainder runs as a whole tile whose rows past
   // M are clamped on load and dropped on store
   const int tail = (int)((r1 - t0 + 15) / 16);
-  if (tail == 1) tile(T1{}, t0, first);
-  if (tail == 2) tile(T2{}, t0, first);
-  if (tail == 3) tile(T3{}, t0, first);
+  if (tail == 1) tile(std::integral_constant<int, 1>{}, t0, first);
+  if constexpr (TUM > 2) if (tail == 2) tile(std::integral_constant<int, 2>{}, t0, first);
+  if constexpr (TUM > 3) if (tail == 3) tile(std::integral_constant<int, 3>{}, t0, first);
+  if constexpr (TUM > 4) if (tail == 4) tile(std::integral_constant<int, 4>{}, t0, first);
+  if constexpr (TUM > 5) if (tail == 5) tile(std::integral_constant<int, 5>{}, t0, first);
+  if constexpr (TUM > 6) if (tail == 6) tile(std::integral_constant<int, 6>{}, t0, first);
+  if constexpr (TUM > 7) if (tail == 7) tile(std::integral_constant<int, 7>{}, t0, first);
   if (tail == TUM) tile(TM{}, t0, first);
 }
 
