@@ -52,9 +52,11 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
   constexpr int XLD = K + (K % 64 == 0 ? 16 : 48);
   // 16-row groups per tile: as many as the LDS (64 XLD bytes per group) and 256 VGPRs hold --
   // each W pass from L2 feeds more rows (profiles/r05/ab_s3/h3r_tiles.txt: enc_gemm -2.4 %
-  // vs 4 groups at every K; 6 groups at K = 288 / 384 spill)
-  constexpr int TUL = 160 * 1024 / (64 * XLD), TUMAX = K <= 192 ? 8 : K <= 256 ? 6 : 4;
-  constexpr int NW = 8, TUM = TUL < TUMAX ? TUL : TUMAX, TTM = 16 * TUM, CW = 16 * NW;
+  // vs 4 groups at every K, then -0.7 % from 6 at K = 288 / 384 without RESADD, whose side
+  // operands spill there)
+  constexpr int TUL = 160 * 1024 / (64 * XLD);
+  constexpr int TUMX = K <= 192 ? 8 : (K <= 256 || (K <= 384 && EPI != EPI_RESADD)) ? 6 : 4;
+  constexpr int NW = 8, TUM = TUL < TUMX ? TUL : TUMX, TTM = 16 * TUM, CW = 16 * NW;
   static_assert(TUM >= 1 && TUM <= 8, "tile height");
   constexpr int KS = K / 32;
   // W ring depth, a divisor of KS (twice the k-steps in flight measured no better:
