@@ -302,6 +302,25 @@ int zasr_vad_window(zasr_vad* h, const float* input, const float* state, int32_t
 /* model facts */
 int32_t zasr_vocab_size(const zasr_recognizer* h);
 int32_t zasr_joiner_dim(const zasr_recognizer* h);
+/* which kernel each part of the loaded model was routed to, as JSON into buf (cap bytes):
+   {"precision", "ffn_fused_h3", "ffn_gemm_pair", "gemm_h3r", "gemm_x3_range", "cnx_ffn_h3",
+   "dec_table"}.  In f16x3 a layer whose weights reach 31 in magnitude keeps the
+   two-accumulator GEMMs (the one-accumulator kernels scale the weight's fp16 hi piece by
+   2^11); a vocabulary whose V^2 x D decoder-context table exceeds ZASR_DEC_TABLE_MAX_GB
+   (default 24) runs the per-frame decoder instead (dec_table 0).  No reference counterpart:
+   a diagnostic of this build's dispatch, read by the tests. */
+int zasr_model_routes(zasr_recognizer* h, char* buf, int64_t cap);
+/* Replace the fbank's 80 triangular filters: banks row-major [80][n_bins] (n_bins 256, or
+   257 with the Nyquist column zero).  The default is knf's mel-linear triangles
+   (core/asr_engine.py:698-721); the reference's browser worker computes Hz-linear triangles
+   (offline_pwa/static/js/pure-ort-asr-worker.js:369-397), which lets a test hold this kernel
+   to that worker's own outputs.  Applies to later zasr_fbank / decode calls on h. */
+int zasr_fbank_set_mel_banks(zasr_recognizer* h, const float* banks, int32_t n_bins);
+/* Launch a no-op kernel with block_threads threads per block through the library's checked
+   launch path (every kernel launch is followed by the runtime's launch status): a refused
+   configuration (e.g. > 1024 threads) returns ZASR_ERR_RUNTIME with the HIP error in
+   zasr_last_error().  No reference counterpart: a self-test of the error path. */
+int zasr_selftest_launch(int32_t block_threads);
 
 /* profiling: per-kernel-class HIP-event timing on the handle's stream.  on = 0 off,
    1 kernel classes, 2 kernel classes with the encoder GEMMs split by shape

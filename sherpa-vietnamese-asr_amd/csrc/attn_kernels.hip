@@ -720,8 +720,7 @@ static void launch_flash_one(const AttnFlashArgs& a, dim3 grid, size_t lds, hipS
                              " frames needs " + std::to_string(lds + stat) +
                              " B of LDS (positional stage + static staging), over the " +
                              std::to_string(kLdsPerCu) + " B of a gfx950 CU");
-  hipLaunchKernelGGL((attn_flash_kernel<MODE, NP, FMT, NF>), grid, dim3(256), lds, st, a);
-  ZASR_HIP_CHECK(hipGetLastError());
+  ZASR_LAUNCH((attn_flash_kernel<MODE, NP, FMT, NF>), grid, dim3(256), lds, st, a);
 }
 
 template <int NP, int FMT = 0>
@@ -888,19 +887,19 @@ void launch_nonlin_prep_t(const void* h3, bool h3_bf16, const int* off, const in
   __bf16* out = reinterpret_cast<__bf16*>(t1t);
   const float* h3f = reinterpret_cast<const float*>(h3);
   if (h3_bf16)
-    hipLaunchKernelGGL((nonlin_prep_t_kernel<__bf16, 1>), grid, dim3(256), 0, st,
+    ZASR_LAUNCH((nonlin_prep_t_kernel<__bf16, 1>), grid, dim3(256), 0, st,
                        reinterpret_cast<const __bf16*>(h3), off, o8, map, R, hid, R8, out);
   else if (pieces == 1)
-    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 1>), grid, dim3(256), 0, st, h3f, off, o8,
+    ZASR_LAUNCH((nonlin_prep_t_kernel<float, 1>), grid, dim3(256), 0, st, h3f, off, o8,
                        map, R, hid, R8, out);
   else if (pieces == 2)
-    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 2>), grid, dim3(256), 0, st, h3f, off, o8,
+    ZASR_LAUNCH((nonlin_prep_t_kernel<float, 2>), grid, dim3(256), 0, st, h3f, off, o8,
                        map, R, hid, R8, out);
   else if (pieces == kPiecesF16)
-    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, kPiecesF16>), grid, dim3(256), 0, st, h3f,
+    ZASR_LAUNCH((nonlin_prep_t_kernel<float, kPiecesF16>), grid, dim3(256), 0, st, h3f,
                        off, o8, map, R, hid, R8, out);
   else
-    hipLaunchKernelGGL((nonlin_prep_t_kernel<float, 3>), grid, dim3(256), 0, st, h3f, off, o8,
+    ZASR_LAUNCH((nonlin_prep_t_kernel<float, 3>), grid, dim3(256), 0, st, h3f, off, o8,
                        map, R, hid, R8, out);
 }
 

@@ -315,7 +315,7 @@ void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st) {
     const int rb = 2 * cdiv(pairs, chunks);
     const dim3 grid(cdiv(a.fo, rb), a.n);
 #define ZASR_CX(KSV, SFV, RESV) \
-  hipLaunchKernelGGL((campp_conv2d_mfma_kernel<KSV, SFV, RESV>), grid, dim3(256), 0, st, a, rb)
+  ZASR_LAUNCH((campp_conv2d_mfma_kernel<KSV, SFV, RESV>), grid, dim3(256), 0, st, a, rb)
     if (a.sf == 1 && a.res) ZASR_CX(3, 1, true);
     else if (a.sf == 1) ZASR_CX(3, 1, false);
     else if (a.res) ZASR_CX(3, 2, true);
@@ -324,9 +324,9 @@ void launch_campp_conv2d(const CamppConv2d& a, int ks, hipStream_t st) {
     return;
   }
   dim3 grid(cdiv(a.T, 64), a.fo, a.n);
-  if (ks == 3 && a.ci == 1) hipLaunchKernelGGL((campp_conv2d_kernel<3, 1>), grid, dim3(256), 0, st, a);
-  else if (ks == 3) hipLaunchKernelGGL((campp_conv2d_kernel<3, 32>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((campp_conv2d_kernel<1, 32>), grid, dim3(256), 0, st, a);
+  if (ks == 3 && a.ci == 1) ZASR_LAUNCH((campp_conv2d_kernel<3, 1>), grid, dim3(256), 0, st, a);
+  else if (ks == 3) ZASR_LAUNCH((campp_conv2d_kernel<3, 32>), grid, dim3(256), 0, st, a);
+  else ZASR_LAUNCH((campp_conv2d_kernel<1, 32>), grid, dim3(256), 0, st, a);
 }
 
 // y[r][c] = relu(x[r][c] * s[c] + b[c]), c < C (x row stride ldx, y row stride C)
@@ -350,7 +350,7 @@ void launch_campp_bnrelu(const float* x, int ldx, long R, int C, const float* s,
   ZASR_REQUIRE(C % 4 == 0 && ldx % 4 == 0, "campp bnrelu: channels must be multiples of 4");
   const long n = R * (C / 4);
   if (n <= 0) return;
-  hipLaunchKernelGGL(campp_bnrelu_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, x, ldx,
+  ZASR_LAUNCH(campp_bnrelu_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, x, ldx,
                      R, C, s, b, y);
 }
 
@@ -379,7 +379,7 @@ void launch_campp_im2col1d(const float* x, int ldx, int N, int Tin, int Tout, in
   ZASR_REQUIRE(C % 4 == 0 && ldx % 4 == 0, "campp im2col: channels must be multiples of 4");
   const long n = (long)N * Tout * K * (C / 4);
   if (n <= 0) return;
-  hipLaunchKernelGGL(campp_im2col1d_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, x,
+  ZASR_LAUNCH(campp_im2col1d_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, x,
                      ldx, N, Tin, Tout, C, K, stride, dil, pad, out);
 }
 
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(256) void campp_cam_mask_kernel(CamppCamMask a) {
 
 void launch_campp_cam_mask(const CamppCamMask& a, hipStream_t st) {
   const int nseg = cdiv(a.T, a.seg_len);
-  hipLaunchKernelGGL(campp_cam_mask_kernel, dim3(nseg, a.n), dim3(256), 0, st, a);
+  ZASR_LAUNCH(campp_cam_mask_kernel, dim3(nseg, a.n), dim3(256), 0, st, a);
 }
 
 // statistics pooling over T frames of relu(bn(x)) (the out_nonlinear BN-ReLU folded in):
@@ -501,7 +501,7 @@ __global__ void campp_stats_kernel(const float* __restrict__ x, int N, int T, in
 void launch_campp_stats(const float* x, int N, int T, int C, const float* s, const float* b,
                         float* out, hipStream_t st) {
   if (N * C <= 0) return;
-  hipLaunchKernelGGL(campp_stats_kernel, dim3(cdiv(N * C, 128)), dim3(128), 0, st, x, N, T, C, s,
+  ZASR_LAUNCH(campp_stats_kernel, dim3(cdiv(N * C, 128)), dim3(128), 0, st, x, N, T, C, s,
                      b, out);
 }
 
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(960) void campp_cmvn_kernel(float* __restrict__ x,
 
 void launch_campp_cmvn(float* x, const int* fr_off, int nseq, hipStream_t st) {
   if (nseq <= 0) return;
-  hipLaunchKernelGGL(campp_cmvn_kernel, dim3(nseq), dim3(960), 0, st, x, fr_off);
+  ZASR_LAUNCH(campp_cmvn_kernel, dim3(nseq), dim3(960), 0, st, x, fr_off);
 }
 
 // one block per window: 20 float4 per frame, consecutive threads on consecutive float4 of
@@ -563,7 +563,7 @@ __global__ __launch_bounds__(256) void campp_gather_kernel(const float4* __restr
 void launch_campp_gather(const float* rows, const int* win_row, const int* win_n, int nwin,
                          int wf, float* out, hipStream_t st) {
   if (nwin <= 0) return;
-  hipLaunchKernelGGL(campp_gather_kernel, dim3(nwin), dim3(256), 0, st,
+  ZASR_LAUNCH(campp_gather_kernel, dim3(nwin), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(rows), win_row, win_n, wf,
                      reinterpret_cast<float4*>(out));
 }

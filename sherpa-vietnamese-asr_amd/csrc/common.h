@@ -22,7 +22,25 @@
     if (!(cond)) throw std::runtime_error(std::string("zasr: ") + (msg));             \
   } while (0)
 
+// Every kernel launch of the library goes through ZASR_LAUNCH: the launch, then the runtime's
+// launch status (hipGetLastError: host-side, no synchronisation).  A refused launch (grid /
+// block / LDS configuration, missing code object) throws, and the C ABI returns it as
+// ZASR_ERR_RUNTIME with the HIP error in zasr_last_error() -- never a decode that goes on to
+// read the stale workspace the kernel did not write.
+#define ZASR_LAUNCH(...)                                                              \
+  do {                                                                                \
+    hipLaunchKernelGGL(__VA_ARGS__);                                                  \
+    ::zasr::check_launch(__FILE__, __LINE__);                                         \
+  } while (0)
+
 namespace zasr {
+
+inline void check_launch(const char* file, int line) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("HIP kernel launch failed: ") + hipGetErrorString(e) +
+                             " at " + file + ":" + std::to_string(line));
+}
 
 constexpr int kWave = 64;
 

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void convnext_dw_kernel(
 void launch_dwconv2d_tiled(const float* x, const int* L_off, const int* L_map, int total_rows,
                            const float* w, const float* b, float* out, hipStream_t st) {
   if (total_rows <= 0) return;
-  hipLaunchKernelGGL((convnext_dw_kernel<float, 32>), dim3(cdiv(total_rows, kDwT), 128 / 32),
+  ZASR_LAUNCH((convnext_dw_kernel<float, 32>), dim3(cdiv(total_rows, kDwT), 128 / 32),
                      dim3(256), 0, st, x, L_off, L_map, total_rows, w, b, out);
 }
 
@@ -543,7 +543,7 @@ void launch_convnext_mlp_h3(const float* y, const float* x, long npos, const voi
                             const float* b1, const void* w2p, const float* b2, float* out,
                             hipStream_t st) {
   if (npos <= 0) return;
-  hipLaunchKernelGGL(convnext_mlp_h3_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
+  ZASR_LAUNCH(convnext_mlp_h3_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
                      y, x, npos, reinterpret_cast<const __bf16*>(w1p), b1,
                      reinterpret_cast<const __bf16*>(w2p), b2, out);
 }
@@ -555,10 +555,10 @@ void launch_convnext_bf16(const void* x, const int* L_off, const int* L_map, int
   if (total_rows <= 0) return;
   const __bf16* xb = reinterpret_cast<const __bf16*>(x);
   __bf16* yb = reinterpret_cast<__bf16*>(ytmp);
-  hipLaunchKernelGGL((convnext_dw_kernel<__bf16, kDwC>), dim3(cdiv(total_rows, kDwT), 128 / kDwC),
+  ZASR_LAUNCH((convnext_dw_kernel<__bf16, kDwC>), dim3(cdiv(total_rows, kDwT), 128 / kDwC),
                      dim3(256), 0, st, xb, L_off, L_map, total_rows, dw_w, dw_b, yb);
   const long npos = (long)total_rows * 19;
-  hipLaunchKernelGGL(convnext_mlp_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
+  ZASR_LAUNCH(convnext_mlp_kernel, dim3((unsigned)cdivl(npos, kMlpM)), dim3(256), 0, st,
                      yb, xb, npos, reinterpret_cast<const __bf16*>(w1), b1,
                      reinterpret_cast<const __bf16*>(w2), b2, reinterpret_cast<__bf16*>(out));
 }

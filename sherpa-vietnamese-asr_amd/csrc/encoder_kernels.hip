@@ -28,7 +28,7 @@ __global__ void row2seq_kernel(const int* __restrict__ off, int nseq, int total,
 
 void launch_row2seq(const int* off, int nseq, int total, int* map, hipStream_t st) {
   if (total <= 0) return;
-  hipLaunchKernelGGL(row2seq_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, off, nseq, total,
+  ZASR_LAUNCH(row2seq_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, off, nseq, total,
                      map);
 }
 
@@ -230,11 +230,11 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
                   hipStream_t st, bool campp) {
   if (total_frames <= 0) return;
   if (campp)
-    hipLaunchKernelGGL(fbank_kernel<true>, dim3(std::min(cdiv(total_frames, kFbWaves), kFbBlocks)),
+    ZASR_LAUNCH(fbank_kernel<true>, dim3(std::min(cdiv(total_frames, kFbWaves), kFbBlocks)),
                        dim3(64 * kFbWaves), 0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames,
                        tabs, out);
   else
-    hipLaunchKernelGGL(fbank_kernel<false>, dim3(std::min(cdiv(total_frames, kFbWaves), kFbBlocks)),
+    ZASR_LAUNCH(fbank_kernel<false>, dim3(std::min(cdiv(total_frames, kFbWaves), kFbBlocks)),
                        dim3(64 * kFbWaves), 0, st, wav, wav_off, nsamp, fr_off, nseq, total_frames,
                        tabs, out);
 }
@@ -304,6 +304,15 @@ __global__ __launch_bounds__(256) void silence_flags_kernel(const float* __restr
   flags[f] = e < threshold ? 1 : 0;
 }
 
+__global__ void selftest_noop_kernel(int* sink) {
+  if (sink && threadIdx.x == 0xffffff) *sink = 0;
+}
+
+void launch_selftest_noop(int block_threads) {
+  ZASR_LAUNCH(selftest_noop_kernel, dim3(1), dim3(block_threads), 0, nullptr, nullptr);
+  ZASR_HIP_CHECK(hipDeviceSynchronize());
+}
+
 void launch_silence_flags(const float* wav, long n, int frame_len, float threshold,
                           unsigned char* flags, hipStream_t st) {
   ZASR_REQUIRE(frame_len > 0 && frame_len % 4 == 0,
@@ -320,7 +329,7 @@ void launch_silence_flags(const float* wav, long n, int frame_len, float thresho
   }
   const long nframes = n / frame_len;
   if (nframes <= 0) return;
-  hipLaunchKernelGGL(silence_flags_kernel, dim3((unsigned)cdivl(nframes, 256)), dim3(256), 0, st,
+  ZASR_LAUNCH(silence_flags_kernel, dim3((unsigned)cdivl(nframes, 256)), dim3(256), 0, st,
                      wav, nframes, frame_len, n2, threshold, flags);
 }
 
@@ -379,13 +388,13 @@ void launch_conv1(const float* fb, const int* fb_off, const int* c1_off, const i
   if (total_rows <= 0) return;
   long n = (long)total_rows * 80;
   if (out_bf16)
-    hipLaunchKernelGGL(conv1_kernel<true>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
+    ZASR_LAUNCH(conv1_kernel<true>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
                        c1_off, c1_map, total_rows, w, b, out);
   else if (fast)
-    hipLaunchKernelGGL((conv1_kernel<false, true>), dim3(cdivl(n, 256)), dim3(256), 0, st, fb,
+    ZASR_LAUNCH((conv1_kernel<false, true>), dim3(cdivl(n, 256)), dim3(256), 0, st, fb,
                        fb_off, c1_off, c1_map, total_rows, w, b, out);
   else
-    hipLaunchKernelGGL(conv1_kernel<false>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
+    ZASR_LAUNCH(conv1_kernel<false>, dim3(cdivl(n, 256)), dim3(256), 0, st, fb, fb_off,
                        c1_off, c1_map, total_rows, w, b, out);
 }
 
@@ -443,13 +452,13 @@ void launch_bias_norm(float* x, int rows, int d, const float* bias, float log_sc
   ZASR_REQUIRE(d % 4 == 0 && d <= 1024, "BiasNorm width must be a multiple of 4, <= 1024");
   const dim3 grid(cdiv(rows, 4));
   if (d <= 256)
-    hipLaunchKernelGGL(bias_norm_kernel<1>, grid, dim3(256), 0, st, x, rows, d, bias,
+    ZASR_LAUNCH(bias_norm_kernel<1>, grid, dim3(256), 0, st, x, rows, d, bias,
                        expf(log_scale), orig, bypass_scale, copy_out);
   else if (d <= 512)
-    hipLaunchKernelGGL(bias_norm_kernel<2>, grid, dim3(256), 0, st, x, rows, d, bias,
+    ZASR_LAUNCH(bias_norm_kernel<2>, grid, dim3(256), 0, st, x, rows, d, bias,
                        expf(log_scale), orig, bypass_scale, copy_out);
   else
-    hipLaunchKernelGGL(bias_norm_kernel<4>, grid, dim3(256), 0, st, x, rows, d, bias,
+    ZASR_LAUNCH(bias_norm_kernel<4>, grid, dim3(256), 0, st, x, rows, d, bias,
                        expf(log_scale), orig, bypass_scale, copy_out);
 }
 
@@ -475,7 +484,7 @@ void launch_bypass(float* x, const float* orig, const float* s, long rows, int d
                    hipStream_t st) {
   long n4 = rows * d / 4;
   if (n4 <= 0) return;
-  hipLaunchKernelGGL(bypass_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, x, orig, s, n4,
+  ZASR_LAUNCH(bypass_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, x, orig, s, n4,
                      d / 4);
 }
 
@@ -498,7 +507,7 @@ __global__ void glu_kernel(const float* __restrict__ x2, float* __restrict__ g, 
 void launch_glu(const float* x2, float* g, long rows, int d, hipStream_t st) {
   long n4 = rows * d / 4;
   if (n4 <= 0) return;
-  hipLaunchKernelGGL(glu_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, x2, g, n4, d / 4);
+  ZASR_LAUNCH(glu_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, x2, g, n4, d / 4);
 }
 
 __global__ void nonlin_prep_kernel(const float* __restrict__ h3, float* __restrict__ t1, long n4,
@@ -520,7 +529,7 @@ __global__ void nonlin_prep_kernel(const float* __restrict__ h3, float* __restri
 void launch_nonlin_prep(const float* h3, float* t1, long rows, int hid, hipStream_t st) {
   long n4 = rows * hid / 4;
   if (n4 <= 0) return;
-  hipLaunchKernelGGL(nonlin_prep_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, h3, t1, n4,
+  ZASR_LAUNCH(nonlin_prep_kernel, dim3(cdivl(n4, 256)), dim3(256), 0, st, h3, t1, n4,
                      hid / 4);
 }
 
@@ -696,11 +705,11 @@ static void launch_glu_dwconv1d_t(const TI* x2, const int* off, const int* map, 
   dim3 grid(cdiv(total_rows, kDw1T), cdiv(d, 64));
   ZASR_REQUIRE(K >= 1 && K <= 31 && (K & 1), "depthwise kernel size must be odd and <= 31");
   if (K <= 7)
-    hipLaunchKernelGGL((glu_dwconv1d_kernel<7, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    ZASR_LAUNCH((glu_dwconv1d_kernel<7, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
   else if (K <= 15)
-    hipLaunchKernelGGL((glu_dwconv1d_kernel<15, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    ZASR_LAUNCH((glu_dwconv1d_kernel<15, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
   else
-    hipLaunchKernelGGL((glu_dwconv1d_kernel<31, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
+    ZASR_LAUNCH((glu_dwconv1d_kernel<31, TI, TO, GLU>), grid, dim3(256), 0, st, x2, off, map, total_rows, d, K, w, b, out);
 }
 
 void launch_dwconv1d_post_glu(const float* g, const int* off, const int* map, int total_rows,
@@ -782,7 +791,7 @@ void launch_downsample(const float* x, const int* off_in, const int* off_out, co
   DsW w{};
   for (int i = 0; i < ds && i < 8; ++i) w.w[i] = w_host8[i];
   ZASR_REQUIRE(ds >= 1 && ds <= 8, "downsample: factor must be in [1, 8]");
-#define ZASR_DS(DSV) hipLaunchKernelGGL((downsample_kernel<DSV>), dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in, \
+#define ZASR_DS(DSV) ZASR_LAUNCH((downsample_kernel<DSV>), dim3(cdivl(n, 256)), dim3(256), 0, st, x, off_in, \
                                         off_out, map_out, total_out, d / 4, ds, w, out)
   if (ds == 2) ZASR_DS(2);
   else if (ds == 4) ZASR_DS(4);
@@ -836,7 +845,7 @@ void launch_stack_glue(const float* xd, const float* orig, const int* off_in, co
   int shift = 0;
   while ((1 << shift) < ds) ++shift;
   ZASR_REQUIRE((1 << shift) == ds, "stack glue: downsampling factor must be a power of 2");
-  hipLaunchKernelGGL(stack_glue_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig, off_in,
+  ZASR_LAUNCH(stack_glue_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig, off_in,
                      off_ds, map_in, rows, d / 4, shift, s, next, dn / 4, full, ldf / 4, c0 / 4);
 }
 
@@ -862,7 +871,7 @@ void launch_upsample_combine(const float* xd, const float* orig, const int* off_
                              const float* s, float* y, hipStream_t st) {
   long n = (long)total_rows * d;
   if (n <= 0) return;
-  hipLaunchKernelGGL(upsample_combine_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig,
+  ZASR_LAUNCH(upsample_combine_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, xd, orig,
                      off_in, off_ds, map_in, total_rows, d, ds, s, y);
 }
 
@@ -883,7 +892,7 @@ void launch_copy_cols(const float* src, int lds, int c0, float* dst, int ldd, in
   int width = zero_rest ? dst_width : ncols;
   long n = rows * width;
   if (n <= 0) return;
-  hipLaunchKernelGGL(copy_cols_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src, lds, c0, dst,
+  ZASR_LAUNCH(copy_cols_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src, lds, c0, dst,
                      ldd, d0, ncols, rows, zero_rest ? 1 : 0, dst_width);
 }
 
@@ -1292,16 +1301,16 @@ __global__ __launch_bounds__(256) void attn_sa_kernel(AttnSAArgs a) {
 void launch_attn_sa(const AttnSAArgs& a, bool online, bool bf16, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
   dim3 grid(cdiv(a.max_len, 32), a.nseq, a.H);
-  if (online && bf16) hipLaunchKernelGGL((attn_sa_kernel<true, true>), grid, dim3(256), 0, st, a);
-  else if (online) hipLaunchKernelGGL((attn_sa_kernel<true, false>), grid, dim3(256), 0, st, a);
-  else if (bf16) hipLaunchKernelGGL((attn_sa_kernel<false, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_sa_kernel<false, false>), grid, dim3(256), 0, st, a);
+  if (online && bf16) ZASR_LAUNCH((attn_sa_kernel<true, true>), grid, dim3(256), 0, st, a);
+  else if (online) ZASR_LAUNCH((attn_sa_kernel<true, false>), grid, dim3(256), 0, st, a);
+  else if (bf16) ZASR_LAUNCH((attn_sa_kernel<false, true>), grid, dim3(256), 0, st, a);
+  else ZASR_LAUNCH((attn_sa_kernel<false, false>), grid, dim3(256), 0, st, a);
 }
 
 void launch_attn_softmax(const AttnArgs& a, hipStream_t st) {
   if (a.nseq <= 0 || a.max_len <= 0) return;
   dim3 grid(cdiv(a.max_len, 32), a.nseq, a.write_heads < a.H ? a.write_heads : a.H);
-  hipLaunchKernelGGL(attn_softmax_kernel, grid, dim3(256), 0, st, a);
+  ZASR_LAUNCH(attn_softmax_kernel, grid, dim3(256), 0, st, a);
 }
 
 }  // namespace zasr

@@ -520,8 +520,7 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
         l->wp = p;
       }
     }
-    const char* ffn_h3_env = getenv("ZASR_FFN_H3");  // "0": the GEMM pair (A/B)
-    if (split_pieces() == kPiecesF16 && !(ffn_h3_env && ffn_h3_env[0] == '0')) {
+    if (split_pieces() == kPiecesF16) {
       // the fused f16x3 FFN (model dims 256..512) reads W1 / W2 as fp16 piece images in
       // MFMA-fragment order; a layer whose weights reach 31 in magnitude keeps the GEMM pair
       for (auto& s : model_.stacks)
@@ -532,8 +531,11 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
             std::vector<float> w1((size_t)F * d), w2((size_t)F * d);
             ZASR_HIP_CHECK(hipMemcpy(w1.data(), L.ff_in[a].w, w1.size() * 4, hipMemcpyDeviceToHost));
             ZASR_HIP_CHECK(hipMemcpy(w2.data(), L.ff_out[a].w, w2.size() * 4, hipMemcpyDeviceToHost));
-            if (!ffn_h3_weights_ok(w1.data(), (long)w1.size()) || !ffn_h3_weights_ok(w2.data(), (long)w2.size()))
+            if (!ffn_h3_weights_ok(w1.data(), (long)w1.size()) || !ffn_h3_weights_ok(w2.data(), (long)w2.size())) {
+              ++routes_.ffn_gemm_pair;
               continue;
+            }
+            ++routes_.ffn_fused_h3;
             for (auto [l, w] : {std::pair<DLin*, std::vector<float>*>{&L.ff_in[a], &w1},
                                 std::pair<DLin*, std::vector<float>*>{&L.ff_out[a], &w2}}) {
               std::vector<__bf16> pk(2 * w->size());
@@ -569,15 +571,18 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
           for (DLin* l : {&L.ff_in[a], &L.ff_out[a]}) mkx(*l);
       }
     ZASR_HIP_CHECK(hipStreamSynchronize(stream_));
-    const char* h3r_env = getenv("ZASR_GEMM_H3R");  // "0": the tiled gemm_x3 kernel (A/B)
-    if (split_pieces() == kPiecesF16 && !(h3r_env && h3r_env[0] == '0')) {
+    if (split_pieces() == kPiecesF16) {
       // the layer projections the row-resident f16x3 GEMM takes (K, N within its shapes and
       // every |w| < 31; the others keep gemm_x3)
       auto mkr = [&](DLin& l) {
         if (!gemm_h3r_supported(l.K, l.N, EPI_NONE)) return;
         std::vector<float> w((size_t)l.N * l.K);
         ZASR_HIP_CHECK(hipMemcpy(w.data(), l.w, w.size() * 4, hipMemcpyDeviceToHost));
-        if (!ffn_h3_weights_ok(w.data(), (long)w.size())) return;
+        if (!ffn_h3_weights_ok(w.data(), (long)w.size())) {
+          ++routes_.gemm_x3_range;
+          return;
+        }
+        ++routes_.gemm_h3r;
         std::vector<__bf16> pk(2 * w.size());
         ffn_pack_h3_host(w.data(), l.N, l.K, pk.data());
         void* p = nullptr;
@@ -593,13 +598,13 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
             for (DLin* l : {&L.sa_in[a], &L.sa_out[a], &L.cv_in[a], &L.cv_out[a]}) mkr(*l);
         }
       // the ConvNeXt MLP (pw1 [384][128], pw2 [128][384]) as the fused f16x3 FFN
-      const char* cnx_env = getenv("ZASR_CNX_FFN");  // "0": convnext_mlp_h3_kernel (A/B)
-      if (!(cnx_env && cnx_env[0] == '0') && model_.pw1.K == 128 && model_.pw2.N == 128 &&
-          ffn_h3_supported(128, model_.pw1.N)) {
+      if (model_.pw1.K == 128 && model_.pw2.N == 128 && ffn_h3_supported(128, model_.pw1.N)) {
         std::vector<float> w1((size_t)model_.pw1.N * 128), w2(w1.size());
         ZASR_HIP_CHECK(hipMemcpy(w1.data(), model_.pw1.w, w1.size() * 4, hipMemcpyDeviceToHost));
         ZASR_HIP_CHECK(hipMemcpy(w2.data(), model_.pw2.w, w2.size() * 4, hipMemcpyDeviceToHost));
-        if (ffn_h3_weights_ok(w1.data(), (long)w1.size()) && ffn_h3_weights_ok(w2.data(), (long)w2.size()))
+        const bool ok = ffn_h3_weights_ok(w1.data(), (long)w1.size()) && ffn_h3_weights_ok(w2.data(), (long)w2.size());
+        routes_.cnx_ffn_h3 = ok ? 1 : 0;
+        if (ok)
           for (auto [l, w] : {std::pair<DLin*, std::vector<float>*>{&model_.pw1, &w1},
                               std::pair<DLin*, std::vector<float>*>{&model_.pw2, &w2}}) {
             std::vector<__bf16> pk(2 * w->size());
@@ -723,33 +728,21 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
     for (int i = 0; i < 400; ++i)
       win[i] = (float)std::pow(0.5 - 0.5 * std::cos(2.0 * M_PI / 399.0 * i), 0.85);
     d_window_ = dev(win.data(), 400);
+    // knf's triangles: mel-linear between 20 Hz and 7600 Hz over the bins 0 .. 255
     auto mel = [](float f) { return 1127.0f * logf(1.0f + f / 700.0f); };
     const float mlo = mel(20.0f), mhi = mel(7600.0f);
     const float delta = (mhi - mlo) / 81.0f;
-    std::vector<int> meta(240);
-    std::vector<float> wts;
+    std::vector<float> banks(80 * 256, 0.f);
     for (int b = 0; b < 80; ++b) {
       float left = mlo + (float)b * delta, center = mlo + (float)(b + 1) * delta,
             right = mlo + (float)(b + 2) * delta;
-      int st = -1, en = -1;
-      std::vector<float> row(256, 0.f);
       for (int i = 0; i < 256; ++i) {
         float m = mel(31.25f * (float)i);
-        if (m > left && m < right) {
-          row[i] = (m <= center) ? (m - left) / (center - left) : (right - m) / (right - center);
-          if (st < 0) st = i;
-          en = i;
-        }
+        if (m > left && m < right)
+          banks[b * 256 + i] = (m <= center) ? (m - left) / (center - left) : (right - m) / (right - center);
       }
-      if (st < 0) st = en = 0;
-      meta[b] = st;
-      meta[80 + b] = en - st + 1;
-      meta[160 + b] = (int)wts.size();
-      for (int i = st; i <= en; ++i) wts.push_back(row[i]);
     }
-    ZASR_HIP_CHECK(hipMalloc(&d_mel_meta_, 240 * sizeof(int)));
-    ZASR_HIP_CHECK(hipMemcpy(d_mel_meta_, meta.data(), 240 * sizeof(int), hipMemcpyHostToDevice));
-    d_mel_w_ = dev(wts.data(), wts.size());
+    set_mel_banks(banks.data(), 256);
   }
   // ---- hotwords ----
   hw_.num_states = hw_host_.num_states;
@@ -778,6 +771,45 @@ Engine::Engine(const std::string& dir, int device, int beam, bool greedy,
   ZASR_HIP_CHECK(hipDeviceSynchronize());
 }
 
+void Engine::set_mel_banks(const float* banks, int n_bins) {
+  ZASR_REQUIRE(n_bins == 256 || n_bins == 257, "mel banks: 256 or 257 bins per filter");
+  // sparse rows: first nonzero bin, run length, offset into the packed weights
+  std::vector<int> meta(240);
+  std::vector<float> wts;
+  for (int b = 0; b < 80; ++b) {
+    const float* row = banks + (size_t)b * n_bins;
+    if (n_bins == 257)
+      ZASR_REQUIRE(row[256] == 0.f, "mel banks: the Nyquist bin must carry no weight");
+    int st = -1, en = -1;
+    for (int i = 0; i < 256; ++i)
+      if (row[i] != 0.f) {
+        if (st < 0) st = i;
+        en = i;
+      }
+    if (st < 0) st = en = 0;
+    meta[b] = st;
+    meta[80 + b] = en - st + 1;
+    meta[160 + b] = (int)wts.size();
+    for (int i = st; i <= en; ++i) wts.push_back(row[i]);
+  }
+  ZASR_HIP_CHECK(hipDeviceSynchronize());  // no fbank in flight reads the old tables
+  if (!d_mel_meta_) ZASR_HIP_CHECK(hipMalloc(&d_mel_meta_, 240 * sizeof(int)));
+  ZASR_HIP_CHECK(hipMemcpy(d_mel_meta_, meta.data(), 240 * sizeof(int), hipMemcpyHostToDevice));
+  if (d_mel_w_) ZASR_HIP_CHECK(hipFree(d_mel_w_));
+  d_mel_w_ = nullptr;
+  ZASR_HIP_CHECK(hipMalloc(&d_mel_w_, wts.size() * sizeof(float)));
+  ZASR_HIP_CHECK(hipMemcpy(d_mel_w_, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice));
+}
+
+std::string Engine::routes_json() const {
+  std::ostringstream os;
+  os << "{\"precision\": " << precision_ << ", \"ffn_fused_h3\": " << routes_.ffn_fused_h3
+     << ", \"ffn_gemm_pair\": " << routes_.ffn_gemm_pair << ", \"gemm_h3r\": " << routes_.gemm_h3r
+     << ", \"gemm_x3_range\": " << routes_.gemm_x3_range << ", \"cnx_ffn_h3\": " << routes_.cnx_ffn_h3
+     << ", \"dec_table\": " << (model_.dec_table ? 1 : 0) << "}";
+  return os.str();
+}
+
 Engine::~Engine() {
   // best-effort teardown: errors here cannot be reported to the caller
   (void)hipSetDevice(device_);
@@ -790,6 +822,7 @@ Engine::~Engine() {
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (d_twiddle_) (void)hipFree(d_twiddle_);
   if (d_mel_meta_) (void)hipFree(d_mel_meta_);
+  if (d_mel_w_) (void)hipFree(d_mel_w_);
   for (auto e : event_pool_) (void)hipEventDestroy(e);
   for (auto& pe : prof_pending_) {
     (void)hipEventDestroy(pe.a);
@@ -1491,9 +1524,9 @@ void Engine::run_encoder(const float* d_feats, const std::vector<int>& T, float*
       launch_dwconv2d_tiled(x3, I(o_L), L_map, mL.total, model_.dw_w, model_.dw_b, y3, st_);
       prof_end();
       if (model_.pw1.wr && model_.pw2.wr) {
-        // f16x3: the ConvNeXt MLP as the fused f16x3 FFN (d = 128, 384 hidden): x3 += MLP(y3)
+        // f16x3: the ConvNeXt MLP as the fused f16x3 FFN (d = 128, pw1.N hidden): x3 += MLP(y3)
         prof_begin("frontend_conv");
-        launch_ffn_fused_h3(x3, mL.total * 19, 128, 384, model_.pw1.wr, model_.pw1.b,
+        launch_ffn_fused_h3(x3, mL.total * 19, 128, model_.pw1.N, model_.pw1.wr, model_.pw1.b,
                             model_.pw2.wr, model_.pw2.b, st_, nullptr, nullptr, y3);
         prof_end();
       } else if (model_.pw1.wp && model_.pw2.wp && split_pieces() == kPiecesF16) {

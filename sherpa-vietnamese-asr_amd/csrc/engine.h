@@ -137,6 +137,16 @@ class Engine {
   void profile_reset();
   std::string profile_report();
 
+  // which kernel each part of the model was routed to at load (JSON; zasr_model_routes): in
+  // f16x3 a layer whose weights reach 31 in magnitude keeps the two-accumulator GEMMs
+  // (ffn_h3_weights_ok), and a vocabulary whose V^2 D decoder table exceeds the size limit runs
+  // the per-frame decoder (decjoin_kernel)
+  std::string routes_json() const;
+  // replace the fbank's 80 triangular filters (row-major [80][n_bins] weights over the FFT's
+  // power bins, n_bins 256 or 257 with bin 256 zero): the reference's browser fbank uses Hz
+  // triangles (offline_pwa/static/js/pure-ort-asr-worker.js:369-397) where knf uses mel ones
+  void set_mel_banks(const float* banks, int n_bins);
+
   std::mutex mu;
 
  private:
@@ -237,6 +247,12 @@ class Engine {
   hipEvent_t take_event();
 
   DModel model_;
+  struct Routes {
+    int ffn_fused_h3 = 0, ffn_gemm_pair = 0;  // f16x3 FFNs (d 128..512): fused / GEMM pair
+    int gemm_h3r = 0, gemm_x3_range = 0;      // f16x3 layer projections the row-resident GEMM
+                                              // shapes admit: taken / refused by the range check
+    int cnx_ffn_h3 = -1;                      // f16x3 ConvNeXt MLP fused (1) or not (0); -1 n/a
+  } routes_;
   int device_ = 0;
   int beam_ = 8;
   [[maybe_unused]] bool greedy_ = false;

@@ -784,7 +784,7 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
   const int rpb = 16 * cdiv(cdiv(R, bpc * cus[dev]), 16);
   const dim3 grid(cdiv(R, rpb));
 #define ZASR_FFNH3(DV, TUV, NBV, NWV)                                                              \
-  hipLaunchKernelGGL((ffn_wide_h3_kernel<DV, TUV, NBV, NWV>), grid, dim3(64 * NWV), 0, st, X, R, F, w1, \
+  ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV>), grid, dim3(64 * NWV), 0, st, X, R, F, w1, \
                      b1, w2, b2, byp_orig, byp_scale, rpb, Y)
   switch (D) {
     // tile rows (16 TUM) / H buffers: the largest tile the LDS and 256 VGPRs hold -- fewer
@@ -830,7 +830,7 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
     ZASR_REQUIRE(F % 32 == 0 && F >= 32 && F <= kMaxF,
                  "ffn_fused: feed-forward dim must be a multiple of 32 in [32, 2048] for D >= 256");
     const dim3 grid(cdiv(R, 64));
-#define ZASR_FFNW(DV) hipLaunchKernelGGL(ffn_wide_kernel<DV>, grid, dim3(512), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
+#define ZASR_FFNW(DV) ZASR_LAUNCH(ffn_wide_kernel<DV>, grid, dim3(512), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
     switch (D) {
       case 256: ZASR_FFNW(256); break;
       case 384: ZASR_FFNW(384); break;
@@ -840,7 +840,7 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
     return;
   }
   const dim3 grid(cdiv(R, kTok));
-#define ZASR_FFN(DV) hipLaunchKernelGGL(ffn_fused_kernel<DV>, grid, dim3(256), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
+#define ZASR_FFN(DV) ZASR_LAUNCH(ffn_fused_kernel<DV>, grid, dim3(256), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
   switch (D) {
     case 64: ZASR_FFN(64); break;
     case 96: ZASR_FFN(96); break;

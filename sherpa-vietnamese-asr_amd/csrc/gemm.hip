@@ -221,11 +221,11 @@ void launch_t(const GemmParams& p, hipStream_t st) {
   if (g_gemm_f32_deep < 0)
     g_gemm_f32_deep = 1;
   if (g_gemm_f32_deep && !p.slices && p.K % (2 * BK) == 0) {
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, true>), grid,
+    ZASR_LAUNCH((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, true>), grid,
                        dim3(64 * WM * WN), 0, st, p);
     return;
   }
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, false>), grid,
+  ZASR_LAUNCH((gemm_f32_kernel<BM, BN, WM, WN, ALOAD, BNC, EPI, false>), grid,
                      dim3(64 * WM * WN), 0, st, p);
 }
 
@@ -708,11 +708,11 @@ void launch_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
   if (g_gemm_deep < 0) g_gemm_deep = 1;
   if (g_gemm_deep && ALOAD == ALOAD_DENSE && !p.slices && p.K % (2 * BK) == 0 && p.lda % 8 == 0) {
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, true>), grid,
+    ZASR_LAUNCH((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, true>), grid,
                        dim3(64 * WM * WN), 0, st, p, Bw, tn, tm);
     return;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, false>), grid,
+  ZASR_LAUNCH((gemm_bf16_kernel<BM, BN, BK, WM, WN, ALOAD, EPI, TA, TC, false>), grid,
                      dim3(64 * WM * WN), 0, st, p, Bw, tn, tm);
 }
 
@@ -993,7 +993,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmParams p, const __bf
 template <int NS, int EPI, typename TA, typename TC>
 void launch_glds(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
   const int tn = cdiv(p.N, 128), tm = cdiv(p.M, 128);
-  hipLaunchKernelGGL((gemm_glds_kernel<NS, EPI, TA, TC>), dim3(tn * tm), dim3(256), 0, st, p, Bw,
+  ZASR_LAUNCH((gemm_glds_kernel<NS, EPI, TA, TC>), dim3(tn * tm), dim3(256), 0, st, p, Bw,
                      tn);
 }
 
@@ -1065,7 +1065,7 @@ void launch_bk_h(const GemmParams& p, const __bf16* Bw, hipStream_t st) {
       case TT_GLDS3_192:
         if (p.K % 32 == 0 && p.K >= 128 && p.lda % 8 == 0 && p.N % 192 == 0) {
           const int tn = p.N / 192, tm = cdiv(p.M, 128);
-          hipLaunchKernelGGL((gemm_glds_kernel<3, EPI, TA, TC, 192, false>), dim3(tn * tm), dim3(256),
+          ZASR_LAUNCH((gemm_glds_kernel<3, EPI, TA, TC, 192, false>), dim3(tn * tm), dim3(256),
                              0, st, p, Bw, tn);
           return;
         }
@@ -1193,12 +1193,12 @@ void convert_rows_to_bf16(const float* src, const float* row_scale, void* dst, l
                           hipStream_t st) {
   const long n = N * K;
   if (n <= 0) return;
-  hipLaunchKernelGGL(rows_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src, row_scale,
+  ZASR_LAUNCH(rows_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src, row_scale,
                      reinterpret_cast<__bf16*>(dst), n, K);
 }
 void convert_to_bf16(const float* src, void* dst, long n, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
+  ZASR_LAUNCH(f32_to_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
                      reinterpret_cast<__bf16*>(dst), n);
 }
 }  // namespace zasr

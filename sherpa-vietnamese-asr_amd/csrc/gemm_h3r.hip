@@ -237,9 +237,9 @@ void gemm_h3r(const float* A, const void* Wp, const float* bias, float* C, int l
   const dim3 grid(cdiv(M, a.rpb));
 #define ZASR_H3R(KV)                                                                      \
   switch (epi) {                                                                          \
-    case EPI_RESADD: hipLaunchKernelGGL((gemm_h3r_kernel<KV, EPI_RESADD>), grid, dim3(512), 0, st, a); break; \
-    case EPI_GLU: hipLaunchKernelGGL((gemm_h3r_kernel<KV, EPI_GLU>), grid, dim3(512), 0, st, a); break; \
-    default: hipLaunchKernelGGL((gemm_h3r_kernel<KV, EPI_NONE>), grid, dim3(512), 0, st, a); break; \
+    case EPI_RESADD: ZASR_LAUNCH((gemm_h3r_kernel<KV, EPI_RESADD>), grid, dim3(512), 0, st, a); break; \
+    case EPI_GLU: ZASR_LAUNCH((gemm_h3r_kernel<KV, EPI_GLU>), grid, dim3(512), 0, st, a); break; \
+    default: ZASR_LAUNCH((gemm_h3r_kernel<KV, EPI_NONE>), grid, dim3(512), 0, st, a); break; \
   }
   switch (K) {
     case 96: ZASR_H3R(96); break;

@@ -233,7 +233,7 @@ template <int K, typename TA, typename TC, int EPI>
 void launch(const void* A, int lda, const void* Bp, const float* bias, void* C, int ldc, int M,
             int N, hipStream_t st) {
   const int nchunks = cdiv(N, CHUNK);
-  hipLaunchKernelGGL((gemm_rp_kernel<K, TA, TC, EPI>), dim3(cdiv(M, BM)), dim3(256), 0, st,
+  ZASR_LAUNCH((gemm_rp_kernel<K, TA, TC, EPI>), dim3(cdiv(M, BM)), dim3(256), 0, st,
                      reinterpret_cast<const TA*>(A), lda, reinterpret_cast<const bf16x8*>(Bp),
                      bias, reinterpret_cast<TC*>(C), ldc, M, N, nchunks);
 }
@@ -274,7 +274,7 @@ void gemm_rp_pack_weights(const void* W, int N, int K, void* out, hipStream_t st
   ZASR_REQUIRE(K % 16 == 0, "gemm_rp: K must be a multiple of 16");
   const int ngroups = cdiv(N, rp::CHUNK) * (rp::CHUNK / 32);
   const long n = (long)ngroups * (K / 16) * 64;
-  hipLaunchKernelGGL(rp::permute_rp_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st,
+  ZASR_LAUNCH(rp::permute_rp_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st,
                      reinterpret_cast<const __bf16*>(W), N, K, ngroups,
                      reinterpret_cast<rp::bf16x8*>(out));
 }

@@ -379,11 +379,11 @@ void launch_x3_t(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st
   const int tn = cdiv(p.N, BN), tm = cdiv(p.max_M, BM);
   dim3 grid(tn * tm * (p.slices ? p.num_slices : 1));
   if (ALOAD == ALOAD_DENSE && !p.slices && p.K % (2 * BK) == 0 && p.lda % 4 == 0) {
-    hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP, BK, FMT>), grid,
+    ZASR_LAUNCH((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, true, NP, BK, FMT>), grid,
                        dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
     return;
   }
-  hipLaunchKernelGGL((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP, BK, FMT>), grid,
+  ZASR_LAUNCH((gemm_x3_kernel<BM, BN, WM, WN, ALOAD, EPI, false, NP, BK, FMT>), grid,
                      dim3(64 * WM * WN), 0, st, p, Bw, blo, tn, tm);
 }
 
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_glds_h3_kernel(Gemm
 template <int NS, int EPI, int BN, int WM = 2, int PR = 3, int ALD = ALOAD_DENSE, int RB = 0>
 void launch_glds_h3(const GemmParams& p, const __bf16* Bw, long blo, hipStream_t st) {
   const int tn = cdiv(p.N, BN), tm = cdiv(p.slices ? p.max_M : p.M, 128);
-  hipLaunchKernelGGL((gemm_glds_h3_kernel<NS, EPI, BN, WM, PR, ALD, RB>),
+  ZASR_LAUNCH((gemm_glds_h3_kernel<NS, EPI, BN, WM, PR, ALD, RB>),
                      dim3(tn * tm * (p.slices ? p.num_slices : 1)), dim3(256), 0, st, p, Bw, blo,
                      tn, tm);
 }
@@ -789,7 +789,7 @@ void gemm_x3(const GemmParams& p, const void* Bw, long b_lo, int epi, int aload,
 
 void split_to_bf16(const float* src, void* dst, long n, int pieces, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(split_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
+  ZASR_LAUNCH(split_bf16_kernel, dim3(cdivl(n, 256)), dim3(256), 0, st, src,
                      reinterpret_cast<__bf16*>(dst), n, pieces);
 }
 

@@ -31,6 +31,9 @@ void launch_fbank(const float* wav, const long* wav_off, const int* nsamp, const
 void launch_silence_flags(const float* wav, long n, int frame_len, float threshold,
                           unsigned char* flags, hipStream_t st);
 
+// a no-op kernel of block_threads threads through ZASR_LAUNCH, synchronised (zasr_selftest_launch)
+void launch_selftest_noop(int block_threads);
+
 // ---- CAM++ speaker embedding (campp_kernels.hip) ----
 struct CamppConv2d {
   const float* x;      // [n][ci][fi][T]

@@ -246,7 +246,7 @@ __global__ void search_init_kernel(SearchState s, int S, int Hmax) {
 void launch_search_init(const SearchState& s, int S, int Hmax, hipStream_t st) {
   int n = S * Hmax;
   if (n <= 0) return;
-  hipLaunchKernelGGL(search_init_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, s, S, Hmax);
+  ZASR_LAUNCH(search_init_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, s, S, Hmax);
 }
 
 // --------------------------------------------------------------------------------------
@@ -299,10 +299,10 @@ void launch_decjoin(const DecJoinArgs& a, hipStream_t st) {
   dim3 grid(a.dw.D / 32, cdiv(a.M, 32));
   size_t lds = (32 * (a.dw.D + 4) + 3 * 16 * 64) * sizeof(float);
   switch (a.dw.D / 32) {
-    case 2: hipLaunchKernelGGL(decjoin_kernel<2>, grid, dim3(256), lds, st, a); break;
-    case 4: hipLaunchKernelGGL(decjoin_kernel<4>, grid, dim3(256), lds, st, a); break;
-    case 8: hipLaunchKernelGGL(decjoin_kernel<8>, grid, dim3(256), lds, st, a); break;
-    case 16: hipLaunchKernelGGL(decjoin_kernel<16>, grid, dim3(256), lds, st, a); break;
+    case 2: ZASR_LAUNCH(decjoin_kernel<2>, grid, dim3(256), lds, st, a); break;
+    case 4: ZASR_LAUNCH(decjoin_kernel<4>, grid, dim3(256), lds, st, a); break;
+    case 8: ZASR_LAUNCH(decjoin_kernel<8>, grid, dim3(256), lds, st, a); break;
+    case 16: ZASR_LAUNCH(decjoin_kernel<16>, grid, dim3(256), lds, st, a); break;
     default: throw std::runtime_error("decoder dim must be 64, 128, 256 or 512");
   }
 }
@@ -354,10 +354,10 @@ void launch_dec_table(const DecoderW& dw, const float* wp, int V, float* table, 
   dim3 grid((unsigned)cdivl(M, 32), dw.D / 32);
   size_t lds = (32 * (dw.D + 4) + 3 * 16 * 64) * sizeof(float);
   switch (dw.D / 32) {
-    case 2: hipLaunchKernelGGL(dec_table_kernel<2>, grid, dim3(256), lds, st, dw, wp, V, table); break;
-    case 4: hipLaunchKernelGGL(dec_table_kernel<4>, grid, dim3(256), lds, st, dw, wp, V, table); break;
-    case 8: hipLaunchKernelGGL(dec_table_kernel<8>, grid, dim3(256), lds, st, dw, wp, V, table); break;
-    case 16: hipLaunchKernelGGL(dec_table_kernel<16>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 2: ZASR_LAUNCH(dec_table_kernel<2>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 4: ZASR_LAUNCH(dec_table_kernel<4>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 8: ZASR_LAUNCH(dec_table_kernel<8>, grid, dim3(256), lds, st, dw, wp, V, table); break;
+    case 16: ZASR_LAUNCH(dec_table_kernel<16>, grid, dim3(256), lds, st, dw, wp, V, table); break;
     default: throw std::runtime_error("decoder dim must be 64, 128, 256 or 512");
   }
 }
@@ -421,10 +421,10 @@ void launch_joiner(const JoinerArgs& j, hipStream_t st) {
   dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
   size_t lds = (32 * (j.D + 4) + 3 * 16 * 64) * sizeof(float);
   switch (j.D / 32) {
-    case 2: hipLaunchKernelGGL(joiner_kernel<2>, grid, dim3(256), lds, st, j); break;
-    case 4: hipLaunchKernelGGL(joiner_kernel<4>, grid, dim3(256), lds, st, j); break;
-    case 8: hipLaunchKernelGGL(joiner_kernel<8>, grid, dim3(256), lds, st, j); break;
-    case 16: hipLaunchKernelGGL(joiner_kernel<16>, grid, dim3(256), lds, st, j); break;
+    case 2: ZASR_LAUNCH(joiner_kernel<2>, grid, dim3(256), lds, st, j); break;
+    case 4: ZASR_LAUNCH(joiner_kernel<4>, grid, dim3(256), lds, st, j); break;
+    case 8: ZASR_LAUNCH(joiner_kernel<8>, grid, dim3(256), lds, st, j); break;
+    case 16: ZASR_LAUNCH(joiner_kernel<16>, grid, dim3(256), lds, st, j); break;
     default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
   }
 }
@@ -474,10 +474,10 @@ void launch_joiner_bf16(const JoinerBf16Args& j, hipStream_t st) {
   if (j.M <= 0) return;
   dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
   switch (j.D) {
-    case 64: hipLaunchKernelGGL(joiner_bf16_kernel<1>, grid, dim3(256), 0, st, j); break;
-    case 128: hipLaunchKernelGGL(joiner_bf16_kernel<2>, grid, dim3(256), 0, st, j); break;
-    case 256: hipLaunchKernelGGL(joiner_bf16_kernel<4>, grid, dim3(256), 0, st, j); break;
-    case 512: hipLaunchKernelGGL(joiner_bf16_kernel<8>, grid, dim3(256), 0, st, j); break;
+    case 64: ZASR_LAUNCH(joiner_bf16_kernel<1>, grid, dim3(256), 0, st, j); break;
+    case 128: ZASR_LAUNCH(joiner_bf16_kernel<2>, grid, dim3(256), 0, st, j); break;
+    case 256: ZASR_LAUNCH(joiner_bf16_kernel<4>, grid, dim3(256), 0, st, j); break;
+    case 512: ZASR_LAUNCH(joiner_bf16_kernel<8>, grid, dim3(256), 0, st, j); break;
     default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
   }
 }
@@ -546,10 +546,10 @@ template <int NP, int FMT>
 void launch_joiner_split(const JoinerArgs& j, hipStream_t st) {
   dim3 grid(cdiv(j.V, 32), cdiv(j.M, 32));
   switch (j.D) {
-    case 64: hipLaunchKernelGGL((joiner_split_kernel<1, NP, FMT>), grid, dim3(256), 0, st, j); break;
-    case 128: hipLaunchKernelGGL((joiner_split_kernel<2, NP, FMT>), grid, dim3(256), 0, st, j); break;
-    case 256: hipLaunchKernelGGL((joiner_split_kernel<4, NP, FMT>), grid, dim3(256), 0, st, j); break;
-    case 512: hipLaunchKernelGGL((joiner_split_kernel<8, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 64: ZASR_LAUNCH((joiner_split_kernel<1, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 128: ZASR_LAUNCH((joiner_split_kernel<2, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 256: ZASR_LAUNCH((joiner_split_kernel<4, NP, FMT>), grid, dim3(256), 0, st, j); break;
+    case 512: ZASR_LAUNCH((joiner_split_kernel<8, NP, FMT>), grid, dim3(256), 0, st, j); break;
     default: throw std::runtime_error("joiner dim must be 64, 128, 256 or 512");
   }
 }
@@ -692,22 +692,22 @@ void launch_joiner_packed(const JoinerPackedArgs& j, hipStream_t st) {
     ZASR_REQUIRE(j.D == 256 || j.D == 512, "packed split joiner: joiner dim must be 256 or 512");
     const int qk = j.D / 16;
     if (j.pieces == kPiecesF16) {
-      if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 2, 4, 1>), grid, dim3(256), 0, st, j);
-      else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 2, 4, 1>), grid, dim3(256), 0, st, j);
+      if (qk == 16) ZASR_LAUNCH((joiner_split_packed_kernel<16, 2, 4, 1>), grid, dim3(256), 0, st, j);
+      else ZASR_LAUNCH((joiner_split_packed_kernel<32, 2, 4, 1>), grid, dim3(256), 0, st, j);
     } else if (j.pieces == 2) {
-      if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 2, 4>), grid, dim3(256), 0, st, j);
-      else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 2, 4>), grid, dim3(256), 0, st, j);
+      if (qk == 16) ZASR_LAUNCH((joiner_split_packed_kernel<16, 2, 4>), grid, dim3(256), 0, st, j);
+      else ZASR_LAUNCH((joiner_split_packed_kernel<32, 2, 4>), grid, dim3(256), 0, st, j);
     } else {
-      if (qk == 16) hipLaunchKernelGGL((joiner_split_packed_kernel<16, 3, 4>), grid, dim3(256), 0, st, j);
-      else hipLaunchKernelGGL((joiner_split_packed_kernel<32, 3, 4>), grid, dim3(256), 0, st, j);
+      if (qk == 16) ZASR_LAUNCH((joiner_split_packed_kernel<16, 3, 4>), grid, dim3(256), 0, st, j);
+      else ZASR_LAUNCH((joiner_split_packed_kernel<32, 3, 4>), grid, dim3(256), 0, st, j);
     }
     return;
   }
   // (an LDS-shared variant, every operand by LDS-DMA, measured 12 % slower under the batch
   // pipeline: it needs whole CUs)
   switch (j.D) {
-    case 256: hipLaunchKernelGGL(joiner_reg_kernel<16>, grid, dim3(256), 0, st, j); break;
-    case 512: hipLaunchKernelGGL(joiner_reg_kernel<32>, grid, dim3(256), 0, st, j); break;
+    case 256: ZASR_LAUNCH(joiner_reg_kernel<16>, grid, dim3(256), 0, st, j); break;
+    case 512: ZASR_LAUNCH(joiner_reg_kernel<32>, grid, dim3(256), 0, st, j); break;
     default: throw std::runtime_error("packed joiner: joiner dim must be 256 or 512");
   }
 }
@@ -784,7 +784,7 @@ void launch_nonfinite_check(const float* x, long n, int* flag, hipStream_t st) {
   if (n <= 0) return;
   const long n4 = n / 4;
   const int blocks = (int)std::min<long>(cdivl(n4, 256), 2048);
-  hipLaunchKernelGGL(nonfinite_kernel, dim3(blocks), dim3(256), 0, st,
+  ZASR_LAUNCH(nonfinite_kernel, dim3(blocks), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(x), n4, flag);
 }
 
@@ -804,7 +804,7 @@ void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st) {
   if (S <= 0) return;
   ZASR_REQUIRE(dt.D % 4 == 0, "joiner dim must be a multiple of 4");
   const long n = (long)S * (dt.D / 4);
-  hipLaunchKernelGGL(table_init_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, dt, S, Hmax);
+  ZASR_LAUNCH(table_init_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st, dt, S, Hmax);
 }
 
 // --------------------------------------------------------------------------------------
@@ -1250,10 +1250,10 @@ void launch_search_step(const SearchState& s, const float* logits, int V, int S,
 #define ZASR_STEP3(KBV, QV)                                                                 \
   do {                                                                                      \
     if (dt)                                                                                 \
-      hipLaunchKernelGGL((search_step_kernel<KBV, QV, true>), grid, block, 0, st, s, logits, \
+      ZASR_LAUNCH((search_step_kernel<KBV, QV, true>), grid, block, 0, st, s, logits, \
                          V, Hmax, beam, t, enc_len, hw, d);                                 \
     else                                                                                    \
-      hipLaunchKernelGGL((search_step_kernel<KBV, QV, false>), grid, block, 0, st, s,        \
+      ZASR_LAUNCH((search_step_kernel<KBV, QV, false>), grid, block, 0, st, s,        \
                          logits, V, Hmax, beam, t, enc_len, hw, d);                         \
   } while (0)
 #define ZASR_STEP(KBV)             \
@@ -1301,7 +1301,7 @@ void launch_greedy_spec_init(const DecTable& dt, int S, int F, int* t_cur, int* 
   if (S <= 0) return;
   ZASR_REQUIRE(dt.D % 4 == 0, "joiner dim must be a multiple of 4");
   const long n = std::max<long>((long)S * F * (dt.D / 4), 2);
-  hipLaunchKernelGGL(greedy_spec_init_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st,
+  ZASR_LAUNCH(greedy_spec_init_kernel, dim3((unsigned)cdivl(n, 256)), dim3(256), 0, st,
                      dt, S, F, t_cur, active);
 }
 
@@ -1571,7 +1571,7 @@ void launch_greedy_spec(const SearchState& s, const float* logits, int V, int S,
   ZASR_REQUIRE(V % 4 == 0 && V <= 4096, "vocabulary size must be a multiple of 4, <= 4096");
   ZASR_REQUIRE(dt.D % 4 == 0 && dt.D <= 512, "joiner dim must be a multiple of 4, <= 512");
 #define ZASR_GS(FV, QV)                                                                      \
-  hipLaunchKernelGGL((greedy_spec_kernel<FV, QV>), dim3(S), dim3(256), 0, st, s, logits, V, \
+  ZASR_LAUNCH((greedy_spec_kernel<FV, QV>), dim3(S), dim3(256), 0, st, s, logits, V, \
                      t_cur, enc_len, hw, dt, active, parity)
   if (F == 4) {
     if (V <= 512) ZASR_GS(4, 2); else if (V <= 2048) ZASR_GS(4, 8); else ZASR_GS(4, 16);
@@ -1624,7 +1624,7 @@ void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTab
                          int out_cap, int* out_tok, int* out_frame, double* out_lp,
                          float4* out_stats, int* out_count, hipStream_t st) {
   if (S <= 0) return;
-  hipLaunchKernelGGL(search_final_kernel, dim3(cdiv(S, 64)), dim3(64), 0, st, s, S, Hmax, hw,
+  ZASR_LAUNCH(search_final_kernel, dim3(cdiv(S, 64)), dim3(64), 0, st, s, S, Hmax, hw,
                      out_cap, out_tok, out_frame, out_lp, out_stats, out_count);
 }
 

@@ -193,31 +193,31 @@ __global__ __launch_bounds__(512) void vad_lstm_kernel(VadLstmArgs a) {
 void launch_vad_maxabs(const float* audio, const long* off, const long* len, int n_files,
                        unsigned* mx, hipStream_t st) {
   if (n_files <= 0) return;
-  hipLaunchKernelGGL(vad_maxabs_kernel, dim3(64, n_files), dim3(256), 0, st, audio, off, len, mx);
+  ZASR_LAUNCH(vad_maxabs_kernel, dim3(64, n_files), dim3(256), 0, st, audio, off, len, mx);
 }
 
 void launch_vad_frames(const VadFramesArgs& a, long n_windows, hipStream_t st) {
   if (n_windows <= 0) return;
-  hipLaunchKernelGGL(vad_frames_kernel, dim3((unsigned)n_windows), dim3(256), 0, st, a);
+  ZASR_LAUNCH(vad_frames_kernel, dim3((unsigned)n_windows), dim3(256), 0, st, a);
 }
 
 void launch_vad_mag_im2col(const float* S, int ldS, int bins, int Kp, long n_windows, float* A,
                            hipStream_t st) {
   if (n_windows <= 0) return;
-  hipLaunchKernelGGL(vad_mag_im2col_kernel, dim3((unsigned)(n_windows * VFR)), dim3(128), 0, st, S,
+  ZASR_LAUNCH(vad_mag_im2col_kernel, dim3((unsigned)(n_windows * VFR)), dim3(128), 0, st, S,
                      ldS, bins, Kp, A);
 }
 
 void launch_vad_im2col(const float* Y, long N, int T, int C, int stride, int Tout, float* A,
                        hipStream_t st) {
   if (N <= 0) return;
-  hipLaunchKernelGGL(vad_im2col_kernel, dim3((unsigned)(N * Tout)), dim3(128), 0, st, Y, T, C,
+  ZASR_LAUNCH(vad_im2col_kernel, dim3((unsigned)(N * Tout)), dim3(128), 0, st, Y, T, C,
                      stride, Tout, A);
 }
 
 void launch_vad_lstm(const VadLstmArgs& a, int n_segments, hipStream_t st) {
   if (n_segments <= 0) return;
-  hipLaunchKernelGGL(vad_lstm_kernel, dim3(n_segments), dim3(512), 0, st, a);
+  ZASR_LAUNCH(vad_lstm_kernel, dim3(n_segments), dim3(512), 0, st, a);
 }
 
 }  // namespace zasr

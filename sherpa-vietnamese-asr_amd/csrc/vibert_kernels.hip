@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void vibert_embed_kernel(VibertEmbedArgs a) {
 void launch_vibert_embed(const VibertEmbedArgs& a, long rows, hipStream_t st) {
   ZASR_REQUIRE(a.H <= 1024, "ViBERT: hidden size must be <= 1024");
   if (rows <= 0) return;
-  hipLaunchKernelGGL(vibert_embed_kernel, dim3((unsigned)rows), dim3(256), 0, st, a);
+  ZASR_LAUNCH(vibert_embed_kernel, dim3((unsigned)rows), dim3(256), 0, st, a);
 }
 
 __global__ __launch_bounds__(256) void vibert_ln_kernel(float* x, int H, const float* g,
@@ -77,7 +77,7 @@ void launch_vibert_layernorm(float* x, long rows, int H, const float* g, const f
                              hipStream_t st) {
   ZASR_REQUIRE(H <= 1024, "ViBERT: hidden size must be <= 1024");
   if (rows <= 0) return;
-  hipLaunchKernelGGL(vibert_ln_kernel, dim3((unsigned)rows), dim3(256), 0, st, x, H, g, b, eps);
+  ZASR_LAUNCH(vibert_ln_kernel, dim3((unsigned)rows), dim3(256), 0, st, x, H, g, b, eps);
 }
 
 // self-attention of one (sequence, head): K (row stride D + 1: conflict-free per-lane rows)
@@ -175,11 +175,11 @@ void launch_vibert_attention(const VibertAttnArgs& a, int B, int heads, hipStrea
     attr = true;
   }
   if (D == 64)
-    hipLaunchKernelGGL(vibert_attn_kernel<64>, dim3(heads, B), dim3(256), lds, st, a);
+    ZASR_LAUNCH(vibert_attn_kernel<64>, dim3(heads, B), dim3(256), lds, st, a);
   else if (D == 32)
-    hipLaunchKernelGGL(vibert_attn_kernel<32>, dim3(heads, B), dim3(256), lds, st, a);
+    ZASR_LAUNCH(vibert_attn_kernel<32>, dim3(heads, B), dim3(256), lds, st, a);
   else
-    hipLaunchKernelGGL(vibert_attn_kernel<16>, dim3(heads, B), dim3(256), lds, st, a);
+    ZASR_LAUNCH(vibert_attn_kernel<16>, dim3(heads, B), dim3(256), lds, st, a);
 }
 
 // g[b * W + w] = x[b * L + offsets[b][w]]
@@ -194,7 +194,7 @@ __global__ void vibert_gather_kernel(const float* __restrict__ x, const long* __
 void launch_vibert_gather(const float* x, const long* offsets, int B, int L, int W, int H, float* g,
                           hipStream_t st) {
   if (B * W <= 0) return;
-  hipLaunchKernelGGL(vibert_gather_kernel, dim3((unsigned)(B * W)), dim3(256), 0, st, x, offsets,
+  ZASR_LAUNCH(vibert_gather_kernel, dim3((unsigned)(B * W)), dim3(256), 0, st, x, offsets,
                      L, W, H, g);
 }
 

@@ -28,8 +28,9 @@ struct zasr_recognizer {
   // leading "\u2581" becomes a space)
   std::string tokens_path;
   std::mutex sym_mu;
-  std::vector<std::string> syms;
-  bool syms_loaded = false;
+  // immutable once published: a reader copies the pointer under sym_mu and keeps its table
+  // alive across a concurrent zasr_set_tokens, which only swaps the pointer
+  std::shared_ptr<const std::vector<std::string>> syms;
 };
 
 // an offline stream (sherpa-onnx OfflineStream): the samples accepted so far and, once
@@ -121,12 +122,13 @@ void decode_streams_impl(zasr_recognizer* h, zasr_stream* const* ss, int n) {
   }
 }
 
-const std::vector<std::string>& symbols(zasr_recognizer* h) {
+std::shared_ptr<const std::vector<std::string>> symbols(zasr_recognizer* h) {
   std::lock_guard<std::mutex> lk(h->sym_mu);
-  if (!h->syms_loaded) {
+  if (!h->syms) {
     const std::string path = h->tokens_path.empty() ? h->model_dir + "/tokens.txt" : h->tokens_path;
     std::ifstream f(path);
     if (!f) throw std::invalid_argument("symbol table not found: " + path);
+    auto tab = std::make_shared<std::vector<std::string>>();
     std::string line;
     while (std::getline(f, line)) {
       std::istringstream ls(line);
@@ -135,10 +137,10 @@ const std::vector<std::string>& symbols(zasr_recognizer* h) {
       const long id = std::stol(id_s);
       if (id < 0) continue;
       if (sym.compare(0, 3, "\xe2\x96\x81") == 0) sym.replace(0, 3, " ");
-      if ((long)h->syms.size() <= id) h->syms.resize(id + 1);
-      h->syms[id] = sym;
+      if ((long)tab->size() <= id) tab->resize(id + 1);
+      (*tab)[id] = sym;
     }
-    h->syms_loaded = true;
+    h->syms = std::move(tab);
   }
   return h->syms;
 }
@@ -607,13 +609,40 @@ int zasr_profile_report(zasr_recognizer* h, char* buf, int64_t cap) {
   });
 }
 
+int zasr_model_routes(zasr_recognizer* h, char* buf, int64_t cap) {
+  if (!h || !buf || cap <= 0) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    const std::string s = h->eng->routes_json();
+    if ((int64_t)s.size() + 1 > cap) return fail(ZASR_ERR_INVALID, "routes buffer too small");
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_fbank_set_mel_banks(zasr_recognizer* h, const float* banks, int32_t n_bins) {
+  if (!h || !banks) return fail(ZASR_ERR_INVALID, "null argument");
+  if (n_bins != 256 && n_bins != 257) return fail(ZASR_ERR_INVALID, "n_bins must be 256 or 257");
+  return guarded([&]() {
+    std::lock_guard<std::mutex> lk(h->eng->mu);
+    h->eng->set_mel_banks(banks, n_bins);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_selftest_launch(int32_t block_threads) {
+  if (block_threads <= 0) return fail(ZASR_ERR_INVALID, "block_threads must be positive");
+  return guarded([&]() {
+    zasr::launch_selftest_noop(block_threads);
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float threshold,
                        uint8_t* d_flags, void* stream) {
   if (n < 0 || (n > 0 && (!d_wav || !d_flags))) return fail(ZASR_ERR_INVALID, "null argument");
   return guarded([&]() {
     zasr::launch_silence_flags(d_wav, (long)n, (int)frame_len, threshold, d_flags,
                                reinterpret_cast<hipStream_t>(stream));
-    ZASR_HIP_CHECK(hipGetLastError());
     return (int)ZASR_OK;
   });
 }
@@ -626,8 +655,7 @@ int zasr_set_tokens(zasr_recognizer* h, const char* tokens_path) {
     if (!f) return fail(ZASR_ERR_NOT_FOUND, std::string("tokens file not found: ") + tokens_path);
     std::lock_guard<std::mutex> lk(h->sym_mu);
     h->tokens_path = tokens_path;
-    h->syms.clear();
-    h->syms_loaded = false;
+    h->syms.reset();  // readers holding the old table keep it alive
     return (int)ZASR_OK;
   });
 }
@@ -689,7 +717,8 @@ int zasr_stream_result_json(const zasr_stream* s, char* buf, int64_t cap, int64_
   if (!s || !needed) return fail(ZASR_ERR_INVALID, "null argument");
   if (!s->decoded) return fail(ZASR_ERR_INVALID, "stream not decoded");
   return guarded([&]() {
-    const std::vector<std::string>& sym = symbols(s->rec);
+    const std::shared_ptr<const std::vector<std::string>> tab = symbols(s->rec);
+    const std::vector<std::string>& sym = *tab;
     const TokenResult& r = s->res;
     std::ostringstream os;
     std::string text;

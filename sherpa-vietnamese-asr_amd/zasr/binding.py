@@ -33,7 +33,8 @@ EXPORTS = (
     "zasr_decode_stream", "zasr_decode_streams", "zasr_stream_is_decoded",
     "zasr_stream_num_tokens", "zasr_stream_num_frames", "zasr_stream_tokens",
     "zasr_stream_frames", "zasr_stream_log_probs", "zasr_stream_token_stats",
-    "zasr_stream_result_json", "zasr_set_tokens",
+    "zasr_stream_result_json", "zasr_set_tokens", "zasr_model_routes",
+    "zasr_fbank_set_mel_banks", "zasr_selftest_launch",
 )
 
 
@@ -199,6 +200,12 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_stream_result_json.restype = C.c_int
     lib.zasr_set_tokens.argtypes = [P, C.c_char_p]
     lib.zasr_set_tokens.restype = C.c_int
+    lib.zasr_model_routes.argtypes = [P, C.c_char_p, I64]
+    lib.zasr_model_routes.restype = C.c_int
+    lib.zasr_fbank_set_mel_banks.argtypes = [P, fp, I32]
+    lib.zasr_fbank_set_mel_banks.restype = C.c_int
+    lib.zasr_selftest_launch.argtypes = [I32]
+    lib.zasr_selftest_launch.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -231,6 +238,15 @@ def convert_stage_model(kind: str, model_dir: str, out_dir: str,
         if rc == 2:
             raise FileNotFoundError(msg)
         raise ZasrError(msg)
+
+
+def selftest_launch(block_threads: int, lib_path: Optional[str] = None) -> None:
+    """A no-op kernel of block_threads threads through the library's checked launch path
+    (include/zasr.h zasr_selftest_launch): an invalid configuration raises ZasrError."""
+    lib = load_library(lib_path)
+    rc = lib.zasr_selftest_launch(int(block_threads))
+    if rc != 0:
+        raise ZasrError(lib.zasr_last_error().decode())
 
 
 def silence_flags(d_wav_ptr: int, n: int, frame_len: int, threshold: float, d_flags_ptr: int,
@@ -358,6 +374,22 @@ class Recognizer:
         finally:
             self.lib.zasr_result_free(res)
         return out
+
+    def routes(self) -> dict:
+        """Which kernel each part of the loaded model was routed to (zasr_model_routes)."""
+        import json
+        buf = C.create_string_buffer(1024)
+        self._check(self.lib.zasr_model_routes(self.handle, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+    def set_mel_banks(self, banks) -> None:
+        """Replace the fbank's 80 triangular filters ([80][256] or [80][257] weights;
+        zasr_fbank_set_mel_banks)."""
+        b = _f32(banks)
+        if b.ndim != 2 or b.shape[0] != 80 or b.shape[1] not in (256, 257):
+            raise ValueError("mel banks must be [80][256] or [80][257]")
+        self._check(self.lib.zasr_fbank_set_mel_banks(
+            self.handle, b.ctypes.data_as(C.POINTER(C.c_float)), b.shape[1]))
 
     def fbank(self, audio) -> np.ndarray:
         a = _f32(audio)
@@ -497,6 +529,22 @@ class CamppEmbedder:
     def _check(self, rc):
         if rc != 0:
             raise ZasrError(self.lib.zasr_last_error().decode())
+
+    def routes(self) -> dict:
+        """Which kernel each part of the loaded model was routed to (zasr_model_routes)."""
+        import json
+        buf = C.create_string_buffer(1024)
+        self._check(self.lib.zasr_model_routes(self.handle, buf, len(buf)))
+        return json.loads(buf.value.decode())
+
+    def set_mel_banks(self, banks) -> None:
+        """Replace the fbank's 80 triangular filters ([80][256] or [80][257] weights;
+        zasr_fbank_set_mel_banks)."""
+        b = _f32(banks)
+        if b.ndim != 2 or b.shape[0] != 80 or b.shape[1] not in (256, 257):
+            raise ValueError("mel banks must be [80][256] or [80][257]")
+        self._check(self.lib.zasr_fbank_set_mel_banks(
+            self.handle, b.ctypes.data_as(C.POINTER(C.c_float)), b.shape[1]))
 
     def fbank(self, audio) -> np.ndarray:
         a = _f32(audio)

@@ -77,15 +77,23 @@ class OfflineStream:
         self._h = h
         self._result: Optional[OfflineRecognitionResult] = None
         self._fin = weakref.finalize(self, self._lib.zasr_destroy_stream, h)
+        # f16x3: the samples stay on the host side too, so that a stream whose decode meets
+        # the fp16 operand range can be re-decoded by the bf16x6 fallback engine
+        self._samples: Optional[List[np.ndarray]] = [] if recognizer._can_fall_back else None
+        self._delegate: Optional["OfflineStream"] = None  # the fallback engine's stream
 
     def accept_waveform(self, sample_rate: int, waveform) -> None:
         a = np.ascontiguousarray(np.asarray(waveform, dtype=np.float32).reshape(-1))
         fp = C.POINTER(C.c_float)
         self._rec._check(self._lib.zasr_stream_accept_waveform(
             self._h, int(sample_rate), a.ctypes.data_as(fp), int(a.shape[0])))
+        if self._samples is not None:
+            self._samples.append(a.copy())
 
     @property
     def result(self) -> OfflineRecognitionResult:
+        if self._delegate is not None:
+            return self._delegate.result
         if self._result is None:
             r = OfflineRecognitionResult()
             if self._lib.zasr_stream_is_decoded(self._h):
@@ -95,6 +103,8 @@ class OfflineStream:
 
     def as_json_string(self) -> str:
         """zasr_stream_result_json (SherpaOnnxGetOfflineStreamResultAsJson)."""
+        if self._delegate is not None:
+            return self._delegate.as_json_string()
         need = C.c_int64()
         self._lib.zasr_stream_result_json(self._h, None, 0, C.byref(need))
         if need.value <= 0:
@@ -141,6 +151,10 @@ class OfflineRecognizer:
         self._handle._check(self._lib.zasr_set_tokens(self._handle.handle,
                                                       os.path.abspath(tokens).encode()))
         self._syms = _load_symbols(tokens)
+        self._can_fall_back = prec == "f16x3"
+        self._fallback: Optional["OfflineRecognizer"] = None
+        self._ctor = (model_dir, tokens, decoding_method, int(max_active_paths), hotwords_file,
+                      float(hotwords_score), dev)
         self.config = {"model_dir": model_dir, "tokens": tokens, "decoding_method": decoding_method,
                        "max_active_paths": int(max_active_paths), "precision": prec,
                        "num_hotwords": len(seqs)}
@@ -181,16 +195,48 @@ class OfflineRecognizer:
         return OfflineStream(self)
 
     def decode_stream(self, s: OfflineStream) -> None:
-        self._check(self._lib.zasr_decode_stream(self._handle.handle, s._h))
+        try:
+            self._check(self._lib.zasr_decode_stream(self._handle.handle, s._h))
+        except ZasrError as e:
+            self._fall_back(e, [s])
         s._result = None
 
     def decode_streams(self, ss: Sequence[OfflineStream]) -> None:
         """All streams in ONE batched GPU pass (SherpaOnnxDecodeMultipleOfflineStreams)."""
         ss = list(ss)
         arr = (C.c_void_p * max(len(ss), 1))(*[s._h.value for s in ss])
-        self._check(self._lib.zasr_decode_streams(self._handle.handle, arr, len(ss)))
+        try:
+            self._check(self._lib.zasr_decode_streams(self._handle.handle, arr, len(ss)))
+        except ZasrError as e:
+            self._fall_back(e, ss)
         for s in ss:
             s._result = None
+
+    # the stream path's form of zasr.binding.Recognizer._retry: an f16x3 decode whose encoder
+    # output left the fp16 operand range (the engine reports it after draining its streams) is
+    # redone by a bf16x6 engine of the same model, so the caller still gets the token-exact
+    # result; each stream's result is then read from its twin on that engine
+    def _fall_back(self, e: ZasrError, ss: Sequence[OfflineStream]) -> None:
+        if not self._can_fall_back or "non-finite encoder output" not in str(e):
+            raise e
+        if self._fallback is None:
+            import logging
+            logging.getLogger("zasr").warning(
+                "[zasr] f16x3 operand range exceeded; re-decoding with %s",
+                Recognizer.FALLBACK_PRECISION)
+            md, tok, method, beam, hwf, hws, dev = self._ctor
+            self._fallback = OfflineRecognizer(md, tok, method, beam, hwf, hws,
+                                               precision=Recognizer.FALLBACK_PRECISION,
+                                               device_id=dev)
+        twins = []
+        for s in ss:
+            t = self._fallback.create_stream()
+            t.accept_waveform(16000, np.concatenate(s._samples) if s._samples
+                              else np.zeros(0, np.float32))
+            twins.append(t)
+        self._fallback.decode_streams(twins)
+        for s, t in zip(ss, twins):
+            s._delegate = t
 
     def _result_of(self, h) -> OfflineRecognitionResult:
         lib = self._lib

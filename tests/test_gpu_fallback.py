@@ -54,3 +54,34 @@ def test_f16x3_out_of_range_falls_back_to_bf16x6(hot_model, method, beam):
         assert a.token_ids.tolist() == b.token_ids.tolist() == c.token_ids.tolist()
         assert a.T == b.T
         np.testing.assert_array_equal(a.log_probs, b.log_probs)
+
+
+@pytest.mark.parametrize("method,beam", [("greedy_search", 1), ("modified_beam_search", 4)])
+def test_offline_stream_out_of_range_falls_back_to_bf16x6(hot_model, method, beam):
+    """The sherpa-onnx stream surface (core/audio_analyzer.py:345-361, streaming_asr.py:358):
+    OfflineRecognizer at its f16x3 default decodes through zasr_decode_stream(s), not through
+    Recognizer.decode, so it carries the same fallback -- decode_stream and decode_streams
+    re-decode on a bf16x6 engine, and result / as_json_string read the re-decoded streams."""
+    import json
+    import os
+    from zasr.binding import Recognizer
+    from zasr.offline import OfflineRecognizer
+    from zasr.synth_audio import synth_speech
+    audio = [synth_speech(6.0, 81), synth_speech(3.5, 82), synth_speech(2.0, 83)]
+    ref = Recognizer(hot_model, method, beam, precision="bf16x6")
+    want = [r.token_ids.tolist() for r in ref.decode(audio)]
+    ref.close()
+    assert sum(len(w) for w in want) > 0
+    rec = OfflineRecognizer(hot_model, os.path.join(hot_model, "tokens.txt"),
+                            decoding_method=method, max_active_paths=beam, precision="f16x3")
+    ss = [rec.create_stream() for _ in audio]
+    for s, a in zip(ss, audio):
+        s.accept_waveform(16000, a[: len(a) // 2])
+        s.accept_waveform(16000, a[len(a) // 2:])
+    rec.decode_streams(ss[:2])
+    rec.decode_stream(ss[2])
+    assert rec._fallback is not None, "the f16x3 engine did not report the range overflow"
+    for s, w in zip(ss, want):
+        assert s.result.token_ids == w
+        assert s.result.text == "".join(rec._syms.get(t, "") for t in w)
+        assert json.loads(s.as_json_string())["text"] == s.result.text
