@@ -149,6 +149,17 @@ int zasr_decode_device_batches(zasr_recognizer* h, const float* d_wav, const int
                                const int64_t* n, int32_t count, const int32_t* batch_sizes,
                                int32_t n_batches, int32_t beam, void* stream, zasr_result** out);
 
+/* zasr_decode_device_batches from HOST waveforms (wav: host memory, pinned for an
+   asynchronous copy, e.g. hipHostMalloc / torch pin_memory): each batch's span of samples is
+   copied into the engine's device buffer for that pipeline slot on its own copy stream, and
+   the batch's fbank waits for that copy alone, so batch k+1's upload runs under batch k's
+   encoder and search.  Results identical to uploading the signal and calling
+   zasr_decode_device_batches.  The reference's unit of work starts from the host waveform
+   (core/asr_engine.py:2068). */
+int zasr_decode_host_batches(zasr_recognizer* h, const float* wav, const int64_t* wav_off,
+                             const int64_t* n, int32_t count, const int32_t* batch_sizes,
+                             int32_t n_batches, int32_t beam, void* stream, zasr_result** out);
+
 /* Encoder only: features -> encoder_out rows [T'_i][joiner_dim], packed in chunk order
    into out (cap floats); t_out[i] receives T'_i. */
 int zasr_encode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,

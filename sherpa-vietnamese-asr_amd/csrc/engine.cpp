@@ -828,6 +828,10 @@ Engine::~Engine() {
     (void)hipEventDestroy(pe.a);
     (void)hipEventDestroy(pe.b);
   }
+  if (copy_st_) (void)hipStreamSynchronize(copy_st_);
+  for (auto e : upload_ev_)
+    if (e) (void)hipEventDestroy(e);
+  if (copy_st_) (void)hipStreamDestroy(copy_st_);
   (void)hipStreamSynchronize(stream2_);
   (void)hipStreamSynchronize(stream3_);
   if (stream4_) (void)hipStreamSynchronize(stream4_);
@@ -1704,9 +1708,16 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
     const size_t jrs = (size_t)joiner_packed_rows((long)S * F);
     void* Js = j16 ? (void*)ws<__bf16>("gs_joinin_h", jrs * D * jpc)
                    : (void*)ws<float>("gs_joinin", (size_t)S * F * D);
-    float* lg = ws<float>("gs_logits", (size_t)S * F * V);
+    // one launch per super-step (joiner_greedy_kernel) for the packed bf16 / f16x3 joiner at
+    // F = 4; the other modes run the joiner and greedy_spec as two launches
+    static const bool fused_env = !(getenv("ZASR_GREEDY_FUSED") && getenv("ZASR_GREEDY_FUSED")[0] == '0');
+    const bool fused = fused_env && packed && F == 4 && (jnp == 0 || jnp == kPiecesF16) &&
+                       (D == 256 || D == 512) && V % 4 == 0 && V <= 2048;
+    const int ldo = fused ? joiner_greedy_ldo(V) : V;
+    float* lg = ws<float>("gs_logits", (size_t)S * F * ldo);
     int* d_t = ws<int>("gs_t", S);
     int* d_active = ws<int>("gs_active", 2);
+    int* d_cnt = fused ? ws<int>("gs_cnt", (size_t)cdiv(S, 8)) : nullptr;
     DecTable ds{model_.dec_table, V, d_enc, d_eo, d_el, Js, D, bf16 ? 1 : 0};
     ds.j_packed = packed ? 1 : 0;
     ds.j_pieces = packed ? jnp : 0;
@@ -1714,6 +1725,7 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
     prof_begin("search");
     launch_search_init(st, S, 1, st_);
     launch_greedy_spec_init(ds, S, F, d_t, d_active, st_);
+    if (fused) ZASR_HIP_CHECK(hipMemsetAsync(d_cnt, 0, (size_t)cdiv(S, 8) * sizeof(int), st_));
     prof_end();
     // every super-step advances each live stream by >= 1 frame: Tmax steps at most; the
     // host checks the live-stream count every kSync steps (one small D2H copy)
@@ -1725,6 +1737,24 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
     bool have_prev = false;
     while (k < Tmax) {
       for (int b = 0; b < kSync && k < Tmax; ++b, ++k) {
+        if (fused) {
+          GreedyFusedArgs ga{};
+          ga.j = packed_args(Js, ds.j_plane, lg, S * F);
+          ga.ldo = ldo;
+          ga.st = st;
+          ga.t_cur = d_t;
+          ga.enc_len = d_el;
+          ga.hw = hw_;
+          ga.dt = ds;
+          ga.active = d_active;
+          ga.parity = k & 1;
+          ga.cnt = d_cnt;
+          ga.S = S;
+          prof_begin("joiner_search");
+          launch_joiner_greedy(ga, st_);
+          prof_end();
+          continue;
+        }
         prof_begin("joiner");
         if (packed) {
           JoinerPackedArgs ja = packed_args(Js, ds.j_plane, lg, S * F);
@@ -1961,7 +1991,30 @@ void Engine::encode_stage(const float* d_wav, const std::vector<long>& wav_off,
   long total_frames = 0;
   for (int b = 0; b < B; ++b) total_frames += n[b] > 0 ? (n[b] + 80) / 160 : 0;
   float* feats = ws<float>("feats", (size_t)std::max<long>(total_frames, 1) * 80);
-  run_fbank(d_wav, wav_off, n, feats, frames);
+  std::vector<long> off_dev(wav_off);
+  if (host_wav_) {
+    // this batch's span of the host signal -> the output slot's device buffer, on the copy
+    // stream; the slot's previous batch has been searched, so its fbank is done with the buffer
+    long lo = -1, hi = 0;
+    for (int b = 0; b < B; ++b)
+      if (n[b] > 0) {
+        lo = lo < 0 ? wav_off[b] : std::min(lo, wav_off[b]);
+        hi = std::max(hi, wav_off[b] + n[b]);
+      }
+    if (lo >= 0) {
+      float* buf = ws<float>("wav_in" + std::to_string(out_slot), (size_t)(hi - lo));
+      if (!copy_st_) ZASR_HIP_CHECK(hipStreamCreateWithFlags(&copy_st_, hipStreamNonBlocking));
+      if (!upload_ev_[out_slot])
+        ZASR_HIP_CHECK(hipEventCreateWithFlags(&upload_ev_[out_slot], hipEventDisableTiming));
+      ZASR_HIP_CHECK(hipMemcpyAsync(buf, host_wav_ + lo, (size_t)(hi - lo) * sizeof(float),
+                                    hipMemcpyHostToDevice, copy_st_));
+      ZASR_HIP_CHECK(hipEventRecord(upload_ev_[out_slot], copy_st_));
+      ZASR_HIP_CHECK(hipStreamWaitEvent(st_, upload_ev_[out_slot], 0));
+      for (int b = 0; b < B; ++b) off_dev[b] = n[b] > 0 ? wav_off[b] - lo : 0;
+      d_wav = buf;
+    }
+  }
+  run_fbank(d_wav, off_dev, n, feats, frames);
   // chunks too short for the encoder produce empty results (T' = 0)
   std::vector<int> T;
   std::vector<long> foff(B + 1, 0);
@@ -2015,6 +2068,19 @@ std::vector<TokenResult> Engine::decode_device(const float* d_wav, const std::ve
                                                const std::vector<long>& n, int beam,
                                                hipStream_t st) {
   return decode_device_batches(d_wav, wav_off, n, {(int)n.size()}, beam, st);
+}
+
+std::vector<TokenResult> Engine::decode_host_batches(const float* h_wav,
+                                                     const std::vector<long>& wav_off,
+                                                     const std::vector<long>& n,
+                                                     const std::vector<int>& batch_sizes,
+                                                     int beam, hipStream_t st) {
+  struct Reset {
+    const float** p;
+    ~Reset() { *p = nullptr; }
+  } reset{&host_wav_};
+  host_wav_ = h_wav;
+  return decode_device_batches(nullptr, wav_off, n, batch_sizes, beam, st);
 }
 
 std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,

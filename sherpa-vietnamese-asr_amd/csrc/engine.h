@@ -120,6 +120,15 @@ class Engine {
                                                  const std::vector<long>& n,
                                                  const std::vector<int>& batch_sizes, int beam,
                                                  hipStream_t st);
+  // the same pipeline from HOST waveforms (h_wav: pinned memory for an asynchronous copy):
+  // each batch's span of samples is copied into its encoder slot's device buffer on the
+  // engine's copy stream and its fbank waits on that copy only, so batch k + 1's upload runs
+  // under batch k's encoder / search (the reference's unit of work starts from host audio,
+  // core/asr_engine.py:2068)
+  std::vector<TokenResult> decode_host_batches(const float* h_wav, const std::vector<long>& wav_off,
+                                               const std::vector<long>& n,
+                                               const std::vector<int>& batch_sizes, int beam,
+                                               hipStream_t st);
   std::vector<TokenResult> decode_features(const std::vector<const float*>& feats,
                                            const std::vector<long>& frames, int beam);
   void fbank_host(const float* wav, long n, float* out);
@@ -275,6 +284,11 @@ class Engine {
   // kMaxEnc + 3: beam groups; kMaxEnc + 4 + set: search job `set` complete
   hipEvent_t part_ev_[kMaxEnc + 4 + kMaxJobs] = {};
   hipStream_t st_ = nullptr;  // stream of the current call
+  // decode_host_batches: the call's waveforms are host memory; encode_stage uploads each
+  // batch's span on copy_st_ (upload_ev_[slot]: that slot's copy done)
+  const float* host_wav_ = nullptr;
+  hipStream_t copy_st_ = nullptr;
+  hipEvent_t upload_ev_[kMaxEnc + 1] = {};
   std::map<std::string, Buf> ws_;
   // fbank tables
   double* d_twiddle_ = nullptr;

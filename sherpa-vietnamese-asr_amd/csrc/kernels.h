@@ -454,6 +454,28 @@ void launch_greedy_spec_init(const DecTable& dt, int S, int F, int* t_cur, int* 
 void launch_greedy_spec(const SearchState& s, const float* logits, int V, int S, int F,
                         int* t_cur, const int* enc_len, const HotwordTables& hw,
                         const DecTable& dt, int* active, int parity, hipStream_t st);
+// One launch per super-step (joiner_greedy_kernel): the packed joiner over row tiles of 8
+// streams x 4 frames, and in each row tile's last-arriving block (an agent-scope arrival
+// counter; logits handed over by write-through stores and loads) that tile's greedy step,
+// one wave per stream -- the same logits bit for bit (same MFMA sequence per 32 x 32 tile)
+// and the same per-frame arithmetic as joiner + greedy_spec, without the second launch and
+// its boundary.  F = 4.  `out` rows have stride ldo (>= V, a multiple of 32); cnt: one int
+// per row tile, zero before the first launch (each tile's last block re-zeroes it).
+struct GreedyFusedArgs {
+  JoinerPackedArgs j;  // j.out = logits [S * 4][ldo], j.M = S * 4
+  int ldo;
+  SearchState st;
+  int* t_cur;
+  const int* enc_len;
+  HotwordTables hw;
+  DecTable dt;
+  int* active;
+  int parity;
+  int* cnt;
+  int S;
+};
+void launch_joiner_greedy(const GreedyFusedArgs& a, hipStream_t st);
+inline int joiner_greedy_ldo(int V) { return (V + 31) / 32 * 32; }
 void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTables& hw,
                          int out_cap, int* out_tok, int* out_frame, double* out_lp,
                          float4* out_stats, int* out_count, hipStream_t st);

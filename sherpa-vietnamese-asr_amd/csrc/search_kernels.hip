@@ -1584,17 +1584,375 @@ void launch_greedy_spec(const SearchState& s, const float* logits, int V, int S,
 }
 
 // --------------------------------------------------------------------------------------
-// finalize (:1142-1148), length-normalised pick (:1151), backtrack the emission chain
-__global__ void search_final_kernel(SearchState st, int S, int Hmax, HotwordTables hw,
-                                    int out_cap, int* out_tok, int* out_frame, double* out_lp,
-                                    float4* out_stats, int* out_count) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
+// speculative greedy in ONE launch per super-step (kernels.h GreedyFusedArgs).
+//
+// Block (x, rt) = 8 waves over the joiner rows of row tile rt (32 rows = streams 8 rt ..
+// 8 rt + 7, frames t_cur .. t_cur + 3) and the 256 vocabulary columns 256 x .. : wave w
+// computes the 32 x 32 tile of column group 8 x + w over all of D with exactly the MFMA
+// sequence of joiner_reg_kernel (bf16) / joiner_split_packed_kernel (f16x3), so the logits are
+// those of the two-launch path bit for bit.  The logits leave by write-through (sc1) stores;
+// after every wave's stores have completed, lane 0 adds one to the tile's arrival counter
+// (agent scope) and the block that draws the last ticket runs the tile's greedy step, the
+// logits read back by sc1 loads (MI355X_MICROARCH.md, inter-workgroup hand-off: sc1 stores +
+// one agent-scope counter + sc1 loads, no fence).  No block waits for another, so the grid
+// has no residency requirement.
+//
+// The greedy step of one stream is one wave (greedy_spec_kernel's four waves' work, the same
+// operations in the same order per row): row statistics, the all-blank score recurrence, the
+// top-1 of every window row, the first emission (node, state, hotword transition) and the
+// next window's joiner input from the new context's table row.
+namespace {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t srch_rsrc(const void* p, long bytes) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long)p >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long)hi << 32) | lo), 0, n, 0x00020000);
+}
+constexpr int kCpolSc1 = 16;  // buffer cache-policy bit of sc1 (write-through / L1 bypass)
+}  // namespace
+
+template <int QK, int FMT, int Q>
+__global__ __launch_bounds__(512) void joiner_greedy_kernel(GreedyFusedArgs a) {
+  constexpr int F = 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rt = blockIdx.y, nct = gridDim.x;
+  const JoinerPackedArgs& j = a.j;
+  if (blockIdx.x == 0 && rt == 0 && tid == 0) a.active[a.parity ^ 1] = 0;  // the next step's count
+  const int m0 = rt * 32;
+  if (tile_done(a.t_cur, a.enc_len, F, m0, j.M)) return;  // block-uniform: all 8 streams done
+  const __amdgpu_buffer_rsrc_t rso = srch_rsrc(j.out, (long)j.M * a.ldo * 4);
+
+  // ---- joiner: wave w, column group g (32 columns), all 32 rows ----
+  const int g = blockIdx.x * 8 + wid;
+  if (g * 32 < j.V) {
+    const bf16x8* srcJ = reinterpret_cast<const bf16x8*>(j.Jp) + (long)rt * QK * 64 + lane;
+    const bf16x8* srcW = reinterpret_cast<const bf16x8*>(j.Wp) + (long)g * QK * 64 + lane;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if constexpr (FMT == 0) {  // bf16: joiner_reg_kernel's loop
+      constexpr int CH = 8, NCH = QK / CH;
+      bf16x8 aa[2][CH], bb[2][CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        aa[0][c] = srcJ[c * 64];
+        bb[0][c] = srcW[c * 64];
+      }
+#pragma unroll
+      for (int h = 0; h < NCH; ++h) {
+        const int cur = h & 1;
+        if (h + 1 < NCH) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c) {
+            aa[cur ^ 1][c] = srcJ[((h + 1) * CH + c) * 64];
+            bb[cur ^ 1][c] = srcW[((h + 1) * CH + c) * 64];
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aa[cur][c], bb[cur][c], acc, 0, 0, 0);
+      }
+    } else {  // f16x3: joiner_split_packed_kernel<QK, 2, 4, 1>'s loop
+      constexpr int CH = 4, NCH = QK / CH;
+      const long jp = j.j_plane / 8, wp = j.w_plane / 8;
+      bf16x8 aa[2][CH][2], bb[2][CH][2];
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          aa[0][c][t] = srcJ[t * jp + c * 64];
+          bb[0][c][t] = srcW[t * wp + c * 64];
+        }
+      f32x16 accl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accl[r] = 0.f;
+#pragma unroll
+      for (int h = 0; h < NCH; ++h) {
+        const int cur = h & 1;
+        if (h + 1 < NCH) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              aa[cur ^ 1][c][t] = srcJ[t * jp + ((h + 1) * CH + c) * 64];
+              bb[cur ^ 1][c][t] = srcW[t * wp + ((h + 1) * CH + c) * 64];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const bf16x8 x[2] = {aa[cur][c][0], aa[cur][c][1]};
+          const bf16x8 y[2] = {bb[cur][c][0], bb[cur][c][1]};
+          mfma_h3(x, y, acc, accl);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += accl[r] * kF16LoInv;
+    }
+    const int col = g * 32 + (lane & 31);
+    if (col < j.V) {
+      const float bv = j.bias[col];
+      const int hh = lane >> 5;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (row < j.M)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[r] + bv), rso,
+                                                (row * a.ldo + col) * 4, 0, kCpolSc1);
+      }
+    }
+  }
+  // ---- arrival: every wave's stores complete, then one ticket per block ----
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(a.cnt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == nct - 1;
+    if (last) __hip_atomic_store(a.cnt + rt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  // ---- the row tile's greedy step: wave w = stream 8 rt + w ----
+  const int s = rt * 8 + wid;
+  if (s >= a.S) return;
+  const SearchState& st = a.st;
+  const DecTable& dt = a.dt;
+  const HotwordTables& hw = a.hw;
+  const int V = j.V;
+  const int T_s = a.enc_len[s];
+  const int t0 = a.t_cur[s];
+  if (t0 >= T_s) return;
+  const int nf = T_s - t0 < F ? T_s - t0 : F;
+  const int V4 = V >> 2;
+  const int D = dt.D, d4 = D >> 2;
+  const int base = s;  // Hmax = 1
+  const int y1 = st.y1[base], y2 = st.y2[base];
+  float4 x[F][Q];
+#pragma unroll
+  for (int r = 0; r < F; ++r)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = lane + 64 * q;
+      const int ii = i < V4 ? i : V4 - 1;
+      const float4 v = __builtin_bit_cast(
+          float4, __builtin_amdgcn_raw_buffer_load_b128(rso, ((s * F + r) * a.ldo + 4 * ii) * 4, 0,
+                                                        kCpolSc1));
+      x[r][q] = (r < nf && i < V4) ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    }
+  double lp = st.lp[base];
+  // ---- A + B: row statistics; the all-blank score recurrence (greedy_spec steps A, B) ----
+  float m1r[F], m2r[F], lsr[F], ser[F], lfr[F];
+  double lpr[F + 1];
+  lpr[0] = lp;
+#pragma unroll
+  for (int r = 0; r < F; ++r) {
+    float m1 = -INFINITY, m2 = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float4 v = x[r][q];
+      m2 = fmaxf(m2, fminf(m1, v.x)); m1 = fmaxf(m1, v.x);
+      m2 = fmaxf(m2, fminf(m1, v.y)); m1 = fmaxf(m1, v.y);
+      m2 = fmaxf(m2, fminf(m1, v.z)); m1 = fmaxf(m1, v.z);
+      m2 = fmaxf(m2, fminf(m1, v.w)); m1 = fmaxf(m1, v.w);
+    }
+    wave_max2_dpp(m1, m2);
+    float se = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      se += __expf(x[r][q].x - m1);
+      se += __expf(x[r][q].y - m1);
+      se += __expf(x[r][q].z - m1);
+      se += __expf(x[r][q].w - m1);
+    }
+    se = wave_sum_dpp(se);
+    const float ls = logf(se);
+    m1r[r] = m1;
+    m2r[r] = m2;
+    lsr[r] = ls;
+    ser[r] = se;
+    // blank = token 0 = lane 0's first element
+    const float d0 = lane_f(x[r][0].x, 0) - m1;
+    const float lf = (float)lp;
+    lfr[r] = lf;
+    if (r < nf) lp = (double)((d0 - ls) + lf);
+    lpr[r + 1] = lp;
+  }
+  // ---- C: top-1 per row; D: the first emission of the window ----
+  int fe = -1, tok = 0;
+#pragma unroll
+  for (int r = 0; r < F; ++r) {
+    if (r >= nf || fe >= 0) continue;  // wave-uniform
+    const float lf = lfr[r], m1 = m1r[r], ls = lsr[r];
+    const float vmax = (0.f - ls) + lf;
+    int bq = 0x7fffffff;
+#pragma unroll
+    for (int q = Q - 1; q >= 0; --q) {
+      const int i = 4 * (lane + 64 * q);
+      const float4 v = x[r][q];
+      const int c = (((v.x - m1) - ls) + lf == vmax) ? i
+                  : (((v.y - m1) - ls) + lf == vmax) ? i + 1
+                  : (((v.z - m1) - ls) + lf == vmax) ? i + 2
+                  : (((v.w - m1) - ls) + lf == vmax) ? i + 3 : 0x7fffffff;
+      bq = c < bq ? c : bq;
+    }
+    const int bm = wave_min_i_dpp(bq);
+    const int best = bm < V ? bm : 0;
+    if (best != 0) {
+      fe = r;
+      tok = best;
+    }
+  }
+  const int t_new = t0 + (fe >= 0 ? fe + 1 : nf);
+  // the next window's rows and context row go out before the emission bookkeeping
+  const bool more = t_new < T_s;
+  const int nf2 = T_s - t_new < F ? T_s - t_new : F;
+  const int ny2 = fe >= 0 ? y1 : y2, ny1 = fe >= 0 ? tok : y1;
+  float4 tv[2], ev[F][2];
+  if (more) {
+    const float4* tab4 = reinterpret_cast<const float4*>(dt.table + ((long)ny2 * dt.V + ny1) * D);
+    const float4* enc4 = reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + t_new) * D);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int c4 = lane + 64 * jj < d4 ? lane + 64 * jj : d4 - 1;
+      tv[jj] = tab4[c4];
+#pragma unroll
+      for (int f = 0; f < F; ++f) ev[f][jj] = enc4[(long)(f < nf2 ? f : 0) * d4 + c4];
+    }
+  }
+  if (fe >= 0) {
+    float m1 = m1r[0], m2 = m2r[0], se = ser[0], ls = lsr[0], lf = lfr[0];
+    double lpb = lpr[0];
+#pragma unroll
+    for (int rr = 1; rr < F; ++rr) {
+      m1 = rr == fe ? m1r[rr] : m1;
+      m2 = rr == fe ? m2r[rr] : m2;
+      se = rr == fe ? ser[rr] : se;
+      ls = rr == fe ? lsr[rr] : ls;
+      lf = rr == fe ? lfr[rr] : lf;
+      lpb = rr == fe ? lpr[rr] : lpb;
+    }
+    float e1 = 0.f, e3 = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      float4 v = x[0][q];
+#pragma unroll
+      for (int rr = 1; rr < F; ++rr) v = rr == fe ? x[rr][q] : v;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float d = vv[c] - m1;
+        const float e = __expf(d);
+        e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+        e3 += __expf(d * (1.0f / 3.0f));
+      }
+    }
+    e1 = wave_sum_dpp(e1);
+    e3 = wave_sum_dpp(e3);
+    if (lane == 0) {
+      const float val = (0.f - ls) + lf;
+      double score = (double)val;
+      int nhw = st.hw[base];
+      if (hw.num_states > 0 && tok != 2) {
+        const int cls = hw.tok2cls[tok];
+        if (cls < 0) {
+          score += -hw.node_score[nhw];
+          nhw = 0;
+        } else {
+          const long e = (long)nhw * hw.num_cls + cls;
+          score += hw.delta[e];
+          nhw = hw.next[e];
+        }
+      }
+      const int nid = st.node_count[s];
+      const long gi = (long)s * st.node_cap + nid;
+      st.node_tok[gi] = tok;
+      st.node_frame[gi] = t0 + fe;
+      st.node_parent[gi] = st.node[base];
+      st.node_lp[gi] = (double)val - lpb;
+      st.node_stats[gi] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)),
+                                      1.0f / se, __expf(m2 - m1) / se);
+      st.node_count[s] = nid + 1;
+      st.lp[base] = score;
+      st.lpf[base] = 0;
+      st.hash[base] = hash_push(st.hash[base], tok);
+      st.len[base] = st.len[base] + 1;
+      st.y2[base] = y1;
+      st.y1[base] = tok;
+      st.hw[base] = nhw;
+      st.node[base] = nid;
+    }
+  } else if (lane == 0) {
+    st.lp[base] = lpr[nf];
+    st.lpf[base] = 0;
+  }
+  if (lane == 0) {
+    a.t_cur[s] = t_new;
+    if (more) atomicAdd(&a.active[a.parity], 1);
+  }
+  // ---- the next window's joiner input: J[s][f] = tanh(enc[t_new + f] + table[ny2, ny1]) ----
+  if (!more) return;
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int c4 = lane + 64 * jj;
+    if (c4 >= d4) continue;
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+      if (f < nf2) store_j4(dt, (long)s * F + f, 4 * c4, ev[f][jj], tv[jj]);
+  }
+}
+
+void launch_joiner_greedy(const GreedyFusedArgs& a, hipStream_t st) {
+  if (a.S <= 0) return;
+  const JoinerPackedArgs& j = a.j;
+  ZASR_REQUIRE(j.M == a.S * 4, "joiner_greedy: 4 window rows per stream");
+  ZASR_REQUIRE(j.V % 4 == 0 && j.V <= 2048, "joiner_greedy: vocabulary a multiple of 4, <= 2048");
+  ZASR_REQUIRE(a.ldo >= j.V && a.ldo % 32 == 0, "joiner_greedy: logits row stride");
+  ZASR_REQUIRE(j.D == 256 || j.D == 512, "joiner_greedy: joiner dim must be 256 or 512");
+  ZASR_REQUIRE(a.dt.D == j.D && a.dt.j_packed, "joiner_greedy: packed J of the joiner's dim");
+  ZASR_REQUIRE(j.pieces == 0 || j.pieces == kPiecesF16, "joiner_greedy: bf16 or f16x3 operands");
+  ZASR_REQUIRE((long)j.M * a.ldo * 4 < 0x7fffffffL, "joiner_greedy: logits beyond 2 GB");
+  const dim3 grid(cdiv(j.V, 256), cdiv(a.S, 8));
+  const int qk = j.D / 16;
+#define ZASR_JG(QKV, FMTV, QV) \
+  ZASR_LAUNCH((joiner_greedy_kernel<QKV, FMTV, QV>), grid, dim3(512), 0, st, a)
+  if (j.pieces == kPiecesF16) {
+    if (j.V <= 512) { if (qk == 16) ZASR_JG(16, 1, 2); else ZASR_JG(32, 1, 2); }
+    else { if (qk == 16) ZASR_JG(16, 1, 8); else ZASR_JG(32, 1, 8); }
+  } else {
+    if (j.V <= 512) { if (qk == 16) ZASR_JG(16, 0, 2); else ZASR_JG(32, 0, 2); }
+    else { if (qk == 16) ZASR_JG(16, 0, 8); else ZASR_JG(32, 0, 8); }
+  }
+#undef ZASR_JG
+}
+
+// --------------------------------------------------------------------------------------
+// finalize (:1142-1148), length-normalised pick (:1151), backtrack the emission chain.
+// One wave per stream: the stream's parent pointers are staged into LDS by coalesced loads
+// (one HBM round trip instead of one per emission: a thread walking the chain in global
+// memory paid ~1 us per token), lane 0 walks the chain in LDS recording the node of every
+// output position, and the 64 lanes gather the nodes' fields into the outputs.  A stream
+// with more nodes than the stage holds walks in global memory as before.
+constexpr int kFinalStage = 8192;  // nodes staged per stream (32 KB of parents)
+constexpr int kFinalPath = 2048;   // output positions recorded in LDS (8 KB)
+__global__ __launch_bounds__(64) void search_final_kernel(SearchState st, int S, int Hmax,
+                                                          HotwordTables hw, int out_cap,
+                                                          int* out_tok, int* out_frame,
+                                                          double* out_lp, float4* out_stats,
+                                                          int* out_count) {
+  __shared__ int sPar[kFinalStage];
+  __shared__ int sPath[kFinalPath + 1];
+  const int s = blockIdx.x, lane = threadIdx.x;
   if (s >= S) return;
   const int base = s * Hmax;
   const int n = st.nh[s];
   int best = 0;
   double best_v = -INFINITY;
-  for (int h = 0; h < n; ++h) {
+  for (int h = 0; h < n; ++h) {  // every lane the same pick (uniform loads)
     double lp = st.lp[base + h];
     if (hw.num_states > 0) lp += -hw.node_score[st.hw[base + h]];
     double v = lp / (double)(st.len[base + h] > 1 ? st.len[base + h] : 1);
@@ -1603,29 +1961,68 @@ __global__ void search_final_kernel(SearchState st, int S, int Hmax, HotwordTabl
       best = h;
     }
   }
-  int cnt = 0;
-  for (int nd = st.node[base + best]; nd >= 0; nd = st.node_parent[(long)s * st.node_cap + nd])
-    ++cnt;
-  if (cnt > out_cap) cnt = out_cap;
-  int pos = cnt - 1;
-  for (int nd = st.node[base + best]; nd >= 0 && pos >= 0;
-       nd = st.node_parent[(long)s * st.node_cap + nd], --pos) {
-    const long g = (long)s * st.node_cap + nd;
-    const long o = (long)s * out_cap + pos;
-    out_tok[o] = st.node_tok[g];
-    out_frame[o] = st.node_frame[g];
-    out_lp[o] = st.node_lp[g];
-    out_stats[o] = st.node_stats[g];
+  const long pool = (long)s * st.node_cap;
+  const int nodes = st.node_count[s];
+  const int start = st.node[base + best];
+  if (nodes > kFinalStage) {  // the chain walked in global memory (one lane)
+    if (lane != 0) return;
+    int cnt = 0;
+    for (int nd = start; nd >= 0; nd = st.node_parent[pool + nd]) ++cnt;
+    if (cnt > out_cap) cnt = out_cap;
+    int pos = cnt - 1;
+    for (int nd = start; nd >= 0 && pos >= 0; nd = st.node_parent[pool + nd], --pos) {
+      const long g = pool + nd, o = (long)s * out_cap + pos;
+      out_tok[o] = st.node_tok[g];
+      out_frame[o] = st.node_frame[g];
+      out_lp[o] = st.node_lp[g];
+      out_stats[o] = st.node_stats[g];
+    }
+    out_count[s] = cnt;
+    return;
   }
-  out_count[s] = cnt;
+  for (int i = lane; i < nodes; i += 64) sPar[i] = st.node_parent[pool + i];
+  __syncthreads();
+  // lane 0: the chain's length, then its nodes newest first into sPath (the newest out_cap
+  // nodes when the chain is longer, as the two-walk form kept)
+  if (lane == 0) {
+    int cnt = 0;
+    for (int nd = start; nd >= 0; nd = sPar[nd]) ++cnt;
+    if (cnt > out_cap) cnt = out_cap;
+    sPath[kFinalPath] = cnt;
+    if (cnt <= kFinalPath) {
+      int pos = cnt - 1;
+      for (int nd = start; nd >= 0 && pos >= 0; nd = sPar[nd], --pos) sPath[pos] = nd;
+    }
+  }
+  __syncthreads();
+  const int cnt = sPath[kFinalPath];
+  if (cnt <= kFinalPath) {
+    for (int pos = lane; pos < cnt; pos += 64) {
+      const long g = pool + sPath[pos], o = (long)s * out_cap + pos;
+      out_tok[o] = st.node_tok[g];
+      out_frame[o] = st.node_frame[g];
+      out_lp[o] = st.node_lp[g];
+      out_stats[o] = st.node_stats[g];
+    }
+  } else if (lane == 0) {
+    int pos = cnt - 1;
+    for (int nd = start; nd >= 0 && pos >= 0; nd = sPar[nd], --pos) {
+      const long g = pool + nd, o = (long)s * out_cap + pos;
+      out_tok[o] = st.node_tok[g];
+      out_frame[o] = st.node_frame[g];
+      out_lp[o] = st.node_lp[g];
+      out_stats[o] = st.node_stats[g];
+    }
+  }
+  if (lane == 0) out_count[s] = cnt;
 }
 
 void launch_search_final(const SearchState& s, int S, int Hmax, const HotwordTables& hw,
                          int out_cap, int* out_tok, int* out_frame, double* out_lp,
                          float4* out_stats, int* out_count, hipStream_t st) {
   if (S <= 0) return;
-  ZASR_LAUNCH(search_final_kernel, dim3(cdiv(S, 64)), dim3(64), 0, st, s, S, Hmax, hw,
-                     out_cap, out_tok, out_frame, out_lp, out_stats, out_count);
+  ZASR_LAUNCH(search_final_kernel, dim3(S), dim3(64), 0, st, s, S, Hmax, hw, out_cap, out_tok,
+              out_frame, out_lp, out_stats, out_count);
 }
 
 }  // namespace zasr

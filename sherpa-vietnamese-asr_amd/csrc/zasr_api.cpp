@@ -514,6 +514,34 @@ int zasr_decode_device_batches(zasr_recognizer* h, const float* d_wav, const int
   });
 }
 
+int zasr_decode_host_batches(zasr_recognizer* h, const float* wav, const int64_t* wav_off,
+                             const int64_t* n, int32_t count, const int32_t* batch_sizes,
+                             int32_t n_batches, int32_t beam, void* stream, zasr_result** out) {
+  if (!h || !out || count < 0 || n_batches < 0 || (n_batches > 0 && !batch_sizes) ||
+      (count > 0 && (!wav || !wav_off || !n)))
+    return fail(ZASR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  long total = 0;
+  for (int32_t i = 0; i < n_batches; ++i) {
+    if (batch_sizes[i] < 0) return fail(ZASR_ERR_INVALID, "negative batch size");
+    total += batch_sizes[i];
+  }
+  if (total != count) return fail(ZASR_ERR_INVALID, "batch sizes must sum to count");
+  for (int32_t i = 0; i < count; ++i)
+    if (wav_off[i] < 0 || n[i] < 0) return fail(ZASR_ERR_INVALID, "negative offset or length");
+  return guarded([&]() {
+    Engine* e = h->eng.get();
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<long> off(wav_off, wav_off + count), len(n, n + count);
+    std::vector<int> bs(batch_sizes, batch_sizes + n_batches);
+    auto r = std::make_unique<zasr_result>();
+    r->items = e->decode_host_batches(wav, off, len, bs, resolve_beam(h, beam),
+                                      reinterpret_cast<hipStream_t>(stream));
+    *out = r.release();
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_encode_features(zasr_recognizer* h, const float* const* feats, const int64_t* n_frames,
                          int32_t count, float* out, int64_t cap, int64_t* t_out) {
   if (!h || !feats || !n_frames || !out || !t_out || count <= 0) return fail(ZASR_ERR_INVALID, "null argument");

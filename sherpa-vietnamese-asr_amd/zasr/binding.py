@@ -34,7 +34,7 @@ EXPORTS = (
     "zasr_stream_num_tokens", "zasr_stream_num_frames", "zasr_stream_tokens",
     "zasr_stream_frames", "zasr_stream_log_probs", "zasr_stream_token_stats",
     "zasr_stream_result_json", "zasr_set_tokens", "zasr_model_routes",
-    "zasr_fbank_set_mel_banks", "zasr_selftest_launch",
+    "zasr_fbank_set_mel_banks", "zasr_selftest_launch", "zasr_decode_host_batches",
 )
 
 
@@ -98,6 +98,9 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_decode_device_batches.argtypes = [P, P, C.POINTER(I64), C.POINTER(I64), I32,
                                                C.POINTER(I32), I32, I32, P, C.POINTER(P)]
     lib.zasr_decode_device_batches.restype = C.c_int
+    lib.zasr_decode_host_batches.argtypes = [P, P, C.POINTER(I64), C.POINTER(I64), I32,
+                                             C.POINTER(I32), I32, I32, P, C.POINTER(P)]
+    lib.zasr_decode_host_batches.restype = C.c_int
     lib.zasr_encode_features.argtypes = [P, C.POINTER(fp), C.POINTER(I64), I32, fp, I64,
                                          C.POINTER(I64)]
     lib.zasr_encode_features.restype = C.c_int
@@ -454,6 +457,26 @@ class Recognizer:
                 C.c_void_p(stream), C.byref(res)))
         except ZasrError as e:
             return self._retry(e, "decode_device_batches", d_wav_ptr, offsets, lengths,
+                               batch_sizes, beam=beam, stream=stream)
+        return self._collect(res)
+
+    def decode_host_batches(self, h_wav_ptr: int, offsets: Sequence[int],
+                            lengths: Sequence[int], batch_sizes: Sequence[int],
+                            beam: int = 0, stream: int = 0) -> List[SearchResult]:
+        """decode_device_batches from HOST waveforms at h_wav_ptr (pinned for an asynchronous
+        upload): each batch's samples are copied on the engine's copy stream under the
+        previous batch's work (zasr_decode_host_batches)."""
+        n = len(lengths)
+        off = (C.c_int64 * n)(*offsets)
+        ln = (C.c_int64 * n)(*lengths)
+        bs = (C.c_int32 * len(batch_sizes))(*batch_sizes)
+        res = C.c_void_p()
+        try:
+            self._check(self.lib.zasr_decode_host_batches(
+                self.handle, C.c_void_p(h_wav_ptr), off, ln, n, bs, len(batch_sizes), beam,
+                C.c_void_p(stream), C.byref(res)))
+        except ZasrError as e:
+            return self._retry(e, "decode_host_batches", h_wav_ptr, offsets, lengths,
                                batch_sizes, beam=beam, stream=stream)
         return self._collect(res)
 

@@ -69,9 +69,9 @@ def test_offline_stream_out_of_range_falls_back_to_bf16x6(hot_model, method, bea
     from zasr.synth_audio import synth_speech
     audio = [synth_speech(6.0, 81), synth_speech(3.5, 82), synth_speech(2.0, 83)]
     ref = Recognizer(hot_model, method, beam, precision="bf16x6")
-    want = [r.token_ids.tolist() for r in ref.decode(audio)]
+    wres = ref.decode(audio)
     ref.close()
-    assert sum(len(w) for w in want) > 0
+    want = [r.token_ids.tolist() for r in wres]
     rec = OfflineRecognizer(hot_model, os.path.join(hot_model, "tokens.txt"),
                             decoding_method=method, max_active_paths=beam, precision="f16x3")
     ss = [rec.create_stream() for _ in audio]
@@ -81,7 +81,8 @@ def test_offline_stream_out_of_range_falls_back_to_bf16x6(hot_model, method, bea
     rec.decode_streams(ss[:2])
     rec.decode_stream(ss[2])
     assert rec._fallback is not None, "the f16x3 engine did not report the range overflow"
-    for s, w in zip(ss, want):
+    for s, w, r in zip(ss, want, wres):
+        assert s.result.num_frames == r.T > 0
         assert s.result.token_ids == w
         assert s.result.text == "".join(rec._syms.get(t, "") for t in w)
         assert json.loads(s.as_json_string())["text"] == s.result.text

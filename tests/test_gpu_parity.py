@@ -447,7 +447,8 @@ def check_pipelined_batches(method, beam):
 @pytest.mark.parametrize("env,method,beam", [
     ({"ZASR_SEARCH_JOBS": "3", "ZASR_ENC_STREAMS": "2"}, "modified_beam_search", 4),
     ({"ZASR_SEARCH_CUS": "32"}, "greedy_search", 1),
-], ids=["three_jobs_two_enc_streams", "cu_masked_search"])
+    ({"ZASR_GREEDY_FUSED": "0"}, "greedy_search", 1),
+], ids=["three_jobs_two_enc_streams", "cu_masked_search", "two_launch_greedy"])
 def test_pipelined_batches_env_variants(need_gpu, env, method, beam):
     """The pipeline variants the engine reads from the environment at first use (three beam
     searches in flight + two encoder streams; the CU-partitioned search stream, whose encoder
@@ -494,6 +495,50 @@ def test_pipelined_workspace_growth_mid_pipeline(need_gpu):
         assert a.token_ids.tolist() == p.token_ids.tolist()
         assert a.frames.tolist() == p.frames.tolist()
         np.testing.assert_array_equal(a.log_probs, p.log_probs)
+
+
+def check_greedy_out(out_path, prec):
+    """Greedy decode of 14 chunks (1.5-33 s) in one batch -> .npz of tokens / frames /
+    log-probs / stats (the fused joiner + greedy step vs the two-launch path)."""
+    from model_fixtures import m_model
+    from zasr.binding import Recognizer
+    cfg, w, path = m_model()
+    rec = Recognizer(path, "greedy_search", 1, precision=prec)
+    secs = [33.0, 1.5, 20.0, 7.0, 29.5, 0.2, 12.0, 31.0, 4.0, 25.0, 9.5, 2.5, 17.0, 30.0]
+    res = rec.decode([_speech(x, 2600 + i) for i, x in enumerate(secs)])
+    rec.close()
+    np.savez(out_path, tok=np.concatenate([r.token_ids for r in res]),
+             fr=np.concatenate([r.frames for r in res]), lp=np.concatenate([r.log_probs for r in res]),
+             st=np.concatenate([r.stats for r in res]), n=np.array([r.token_ids.size for r in res]),
+             T=np.array([r.T for r in res]))
+
+
+@pytest.mark.parametrize("prec", ["bf16", "f16x3"])
+def test_fused_greedy_bit_identical_to_two_launches(need_gpu, tmp_path, prec):
+    """joiner_greedy_kernel (one launch per super-step: the joiner's tiles, then the row
+    tile's greedy step in its last-arriving block, logits handed over by write-through stores)
+    returns exactly what the joiner + greedy_spec launches return (ZASR_GREEDY_FUSED=0): the
+    same MFMA sequence per logits tile and the same per-frame arithmetic, so every token,
+    frame, log-prob and statistic is bit-identical (a fresh process each: the switch is read
+    once)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    outs = []
+    for fused in ("1", "0"):
+        out = str(tmp_path / f"greedy_{fused}.npz")
+        code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_parity as t; "
+                "t.check_greedy_out(%r, %r); print('ok')"
+                % (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "sherpa-vietnamese-asr_amd"),
+                   out, prec))
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "ZASR_GREEDY_FUSED": fused},
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
+        outs.append(np.load(out))
+    a, b = outs
+    assert int(a["n"].sum()) > 100
+    for k in ("tok", "fr", "lp", "st", "n", "T"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 def check_encoder_out(out_path):

@@ -56,11 +56,11 @@ HOT = 40.0  # >= 31: outside the one-accumulator kernels' exact range
 
 HOT_TENSORS = [
     # a fused-FFN layer (stack 2, d = 384) -> the GEMM pair
-    ("encoder.encoders.2.layers.0.feed_forward1.in_proj.weight", (3, 5)),
+    ("encoder.encoders.2.encoder.layers.0.feed_forward1.in_proj.weight", (3, 5)),
     # projections the row-resident GEMM takes at K = 384 -> the tiled gemm_x3
-    ("encoder.encoders.2.layers.0.self_attn_weights.in_proj.weight", (7, 11)),
-    ("encoder.encoders.2.layers.0.conv_module1.out_proj.weight", (2, 9)),
-    ("encoder.encoders.2.layers.0.nonlin_attention.in_proj.weight", (300, 17)),
+    ("encoder.encoders.2.encoder.layers.0.self_attn_weights.in_proj.weight", (7, 11)),
+    ("encoder.encoders.2.encoder.layers.0.conv_module1.out_proj.weight", (2, 9)),
+    ("encoder.encoders.2.encoder.layers.0.nonlin_attention.in_proj.weight", (300, 17)),
     # the ConvNeXt MLP -> convnext_mlp_h3_kernel (two accumulators)
     ("encoder_embed.convnext.pointwise_conv1.weight", (10, 20, 0, 0)),
 ]
