@@ -88,6 +88,9 @@ def parse_args(argv=None):
                          "beam-calibrated (peaked non-blank joiner rows: beam 8 emits at the greedy "
                          "rate, ~18 %%, as a trained model does; 68M only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub-lines", action="store_true",
+                    help="skip the config-3 / config-4 f16x3 lines run in child processes beside "
+                         "the default (config 2) line")
     ap.add_argument("--cpu-repeats", type=int, default=5,
                     help="CPU baseline: 1 warm-up then the mean of this many repeats "
                          "(core/calibration.py:822-830)")
@@ -244,6 +247,29 @@ def hour_golden(args, beam, hotwords, chunks):
 
 
 HOUR_AUDIT = os.path.join(REPO, "tests", "golden", "bench_hour_audit.json")
+ROVER_GOLDEN = os.path.join(REPO, "tests", "golden", "bench_hour_oracle_rover.json")
+
+
+def rover_golden_checks(args, beam, phrases, chunks, toks):
+    """Config 4: each ROVER model's tokens of every timed pass vs the oracle's decode of the
+    hour (data only: the golden file), or None when this run is not the golden's workload."""
+    if (args.audio_sec != 3600.0 or beam != 8 or args.hotwords_file != "default" or
+            not os.path.exists(ROVER_GOLDEN)):
+        return None
+    with open(ROVER_GOLDEN) as f:
+        g = json.load(f)
+    if [int(c.shape[0]) for c in chunks] != g["chunk_samples"]:
+        return None
+    import hashlib
+    h = hashlib.sha256()
+    for c in chunks:
+        h.update(np.ascontiguousarray(c, dtype=np.float32).tobytes())
+    if h.hexdigest()[:32] != g["audio_sha256_32"]:
+        return None
+    audit = ROVER_GOLDEN.replace("bench_hour_oracle", "bench_hour_audit")
+    return {m: oracle_agreement(f"{m}_beam8_hw", g[f"{m}_beam8_hw"], [t[i] for t in toks], audit)
+            for i, m in enumerate(("rover30m", "rover68m"))}
+
 
 
 def oracle_agreement(key, ref, got_steps, audit_path=HOUR_AUDIT):
@@ -261,7 +287,7 @@ def oracle_agreement(key, ref, got_steps, audit_path=HOUR_AUDIT):
     audited = None
     if os.path.exists(audit_path):
         with open(audit_path) as f:
-            au = json.load(f).get({"greedy": "greedy", "beam8_hw": "beam8_hw"}[key], {})
+            au = json.load(f).get(key, {})
         ok = set(au.get("allowed_chunks", []))
         audited = all(i in ok and got[i] in au["chunks"][str(i)]["gpu_tokens"].values()
                       for got in got_steps for i, (a, b) in enumerate(zip(got, ref)) if a != b)
@@ -1054,12 +1080,14 @@ def bench_rover(args):
     d_wav = torch.from_numpy(np.concatenate(chunks)).cuda()
     torch.cuda.synchronize()
     last = {}
+    toks = []  # per timed pass: (30M token ids per chunk, 68M token ids per chunk)
 
-    def steps(k):
+    def steps(k, keep=False):
         r = rover_device_many(recs[0], recs[1], recds[0], recds[1], d_wav.data_ptr(), offs, lens,
                               k, beam, phrases, args.rover_sub_batches,
                               args.rover_passes_per_call, mine=mine,
-                              gather=not (args.proxy_ranks > 1 and world == 1))[-1]
+                              gather=not (args.proxy_ranks > 1 and world == 1),
+                              tokens_out=toks if keep else None)[-1]
         last.update(words=len(r[0]), disagree_blocks=sum(r[1]), tokens_a=r[2], tokens_b=r[3])
 
     if args.warmup:
@@ -1069,12 +1097,15 @@ def bench_rover(args):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    steps(args.steps)
+    steps(args.steps, keep=mine is None and rank == 0)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if dist:
         from zasr.shard import max_over_ranks
         el = max_over_ranks(el, device=f"cuda:{local}")
+    # both models' tokens of every timed pass against the oracle's decode of this hour
+    # (tests/golden/bench_hour_oracle_rover.json, make_bench_hour_golden.py --set rover)
+    ochecks = rover_golden_checks(args, beam, phrases, chunks, toks) if toks else None
     # each model alone (decode only, HIP work + result copies) for the breakdown
     alone = {}
     sel = list(range(len(lens))) if mine is None else mine
@@ -1115,6 +1146,11 @@ def bench_rover(args):
                                            f"host object gather, merged there; strong scaling)"
                                            if args.shard_plan else
                                            f"dp{world} (each rank its own hour; weak scaling)")},
+                "oracle_check": ochecks,
+                "token_exact": (all(c["chunks_identical_to_oracle"].split("/")[0] ==
+                                    c["chunks_identical_to_oracle"].split("/")[1] or
+                                    bool(c["differing_chunks_all_audited_f32_ties"])
+                                    for c in ochecks.values()) if ochecks else None),
                 "roofline": {"kernel": "both encoders + joiners (algorithmic flops / step time)",
                              "bound": "mfma", "unit": "TFLOP/s",
                              "achieved": round(fl / t_step / 1e12, 2), "peak": peak,
@@ -1432,6 +1468,35 @@ def run_parity_child():
     raise RuntimeError(f"parity-mode child failed (rc {r.returncode})")
 
 
+def run_sub_bench(argv, timeout=900):
+    """Another bench.py workload in a CHILD process (own HIP context and hardware queues; this
+    process has initialised the GPU, so it starts a child and never execs): its JSON line."""
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    for line in reversed(r.stdout.splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    sys.stderr.write(r.stdout[-2000:] + r.stderr[-4000:])
+    raise RuntimeError(f"sub-bench {' '.join(argv)} failed (rc {r.returncode})")
+
+
+def sub_line(d):
+    """The fields of a child bench line the parent carries."""
+    keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config",
+            "oracle_check", "token_exact", "roofline", "kernel_classes_ms_per_step")
+    out = {k: d[k] for k in keep if k in d}
+    if "config" in out:
+        out["config"] = {k: v for k, v in out["config"].items()
+                         if k in ("workload", "weights", "single_batch_latency_ms",
+                                  "emitting_frame_fraction", "tokens_30m", "tokens_68m",
+                                  "decode_alone_ms")}
+    if out.get("oracle_check") and "token_exact" not in out:
+        oc = out["oracle_check"]
+        n = oc["chunks_identical_to_oracle"].split("/")
+        out["token_exact"] = n[0] == n[1] or bool(oc["differing_chunks_all_audited_f32_ties"])
+    return out
+
+
 def parity_child_main(args):
     """--parity-child: the bench workload (same chunks, same weights) in the parity precision
     only; prints one PARITY_JSON line for the parent (run_parity_child)."""
@@ -1699,10 +1764,64 @@ def main():
             ocheck["note"] = ("the headline precision's tokens vs the oracle (fp32); bf16 is "
                               "BASELINE config 2's arithmetic, not a token-exact mode -- the "
                               "token-exact figure is parity_mode")
+    # the same K steps from HOST audio: pinned host memory, each batch's samples uploaded on the
+    # engine's copy stream under the previous batch's work (zasr_decode_host_batches) -- the
+    # reference's unit of work starts from the host waveform (core/asr_engine.py:2068)
+    host_line = None
+    if rec is not None and not args.no_pipeline and not args.shard_plan and lens:
+        h_wav = torch.from_numpy(np.concatenate(chunks)).pin_memory()
+        n = len(lens)
+
+        def hsteps(k):
+            return rec.decode_host_batches(h_wav.data_ptr(), offs * k, lens * k, [n] * k,
+                                           beam=beam, stream=stream)
+        hsteps(1)
+        sync()
+        if dist:
+            dist.barrier()
+        sync()
+        t1 = time.perf_counter()
+        hres = hsteps(args.steps)
+        sync()
+        el_h = time.perf_counter() - t1
+        if dist:
+            from zasr.shard import max_over_ranks
+            el_h = max_over_ranks(el_h, device=dev)
+        host_line = {"value": round(args.audio_sec * world * args.steps / el_h, 2),
+                     "unit": "audio-sec/sec", "ms_per_step": round(1000 * el_h / args.steps, 3),
+                     "steps": args.steps, "pinned_host_audio_bytes": int(h_wav.numel() * 4),
+                     "tokens_equal_resident": all(a.token_ids.tolist() == b.token_ids.tolist()
+                                                  for a, b in zip(hres[-n:], res[-n:])),
+                     "note": "same workload with the waveforms in pinned host memory: each "
+                             "batch's upload (PCIe) inside the timed region, on the engine's "
+                             "copy stream under the previous batch's work"}
+        del h_wav
     parity = None
     if (rec is not None and world == 1 and args.parity_precision != "none"
             and args.parity_precision != args.precision):
         parity = run_parity_child()
+    # configs 3 and 4 in the token-exact mode, each in its own child process, beside the
+    # default config-2 line (bounded: a few steps each)
+    subs = None
+    if (rec is not None and world == 1 and not args.no_sub_lines and beam == 1 and
+            args.model == "zipformer-68m" and args.audio_sec == 3600.0 and not args.shard_plan
+            and args.parity_precision not in ("none",)):
+        k_sub = str(max(1, min(args.steps, 5)))
+        subs = {}
+        try:
+            subs["config3_f16x3"] = sub_line(run_sub_bench(
+                ["--method", "modified_beam_search", "--beam", "8", "--hotwords-file", "default",
+                 "--precision", args.parity_precision, "--parity-precision", "none",
+                 "--no-cpu-baseline", "--no-sub-lines", "--steps", k_sub, "--warmup", "1"]))
+        except Exception as e:  # reported, never fatal to the headline line
+            subs["config3_f16x3"] = {"error": str(e)[:400]}
+        try:
+            subs["config4_rover_f16x3"] = sub_line(run_sub_bench(
+                ["--stage", "rover", "--beam", "8", "--hotwords-file", "default",
+                 "--precision", args.parity_precision, "--no-cpu-baseline", "--steps", k_sub,
+                 "--warmup", "1"]))
+        except Exception as e:
+            subs["config4_rover_f16x3"] = {"error": str(e)[:400]}
 
     if rank == 0:
         hw_tag = (f" + hotwords ({len(hotwords[0])} phrases of {os.path.basename(hw_path)})"
@@ -1744,6 +1863,8 @@ def main():
             "cpu_baseline": cpu,
             "oracle_check": ocheck,
             "parity_mode": parity,
+            "host_audio": host_line,
+            "token_exact_lines": subs,
         }
         if args.cpu_dry_run:
             line["dry_run"] = True

@@ -157,7 +157,7 @@ def decode_chunks_rover(rec_a, rec_b, chunks, time_offsets, hotword_phrases: Seq
 def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths, k: int,
                       beam: int, hotword_phrases: Sequence[str] = (), sub_batches: int = 1,
                       passes_per_call: int = 1, mine: Optional[Sequence[int]] = None,
-                      gather: bool = True):
+                      gather: bool = True, tokens_out: Optional[list] = None):
     """k passes of one file's chunk plan (waveforms in HBM) through the ROVER pair on one GPU
     (BASELINE config 4): model A (primary, 30M) and model B (68M) decode every chunk
     (`zasr_decode_device`, each on its own engine streams, concurrently: two worker threads,
@@ -178,7 +178,9 @@ def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths
     rank), the voted chunks are gathered to every rank in chunk order (a host object gather,
     zasr.shard.gather_chunks: the vote is per chunk, so the only exchange is its result) and
     every rank merges the whole file; disagreements / tokens are this rank's.  gather=False
-    (bench.py --proxy-ranks, one process standing in for one rank): merge this share alone."""
+    (bench.py --proxy-ranks, one process standing in for one rank): merge this share alone.
+    tokens_out: if a list, each pass appends (A's token ids per chunk, B's token ids per chunk)
+    of the chunks this call decoded (bench.py's oracle agreement)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from zasr.asr_engine import result_words
@@ -224,6 +226,9 @@ def rover_device_many(rec_a, rec_b, recd_a, recd_b, d_wav: int, offsets, lengths
                     chunks.append({"words": merged, "audio_start_abs": t0,
                                    "audio_end_abs": (off + ln) / 16000.0})
                     dis.append(len(d))
+                if tokens_out is not None:
+                    tokens_out.append(([x.token_ids.tolist() for x in ra],
+                                       [x.token_ids.tolist() for x in rb]))
                 if mine is not None and gather:
                     chunks = gather_chunks(list(zip(mine, chunks)), n_all)
                 words, _ = merge_chunks_with_overlap(chunks)

@@ -77,7 +77,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src", nargs="?", default=os.path.join(REPO, "gpurun_out"))
     ap.add_argument("--weights", default="greedy-calibrated")
+    ap.add_argument("--set", default="hour", choices=["hour", "rover"],
+                    help="rover: the config-4 pair against bench_hour_oracle_rover.json")
     a = ap.parse_args()
+    if a.set == "rover":
+        return main_rover(a.src)
     src, variant = a.src, a.weights
     tag = "" if variant == "greedy-calibrated" else f"_{variant}"
     torch.set_num_threads(8)
@@ -150,6 +154,61 @@ def main():
         out[method] = {"differing_chunks": diff, "allowed_chunks": allowed, "chunks": entries}
     out["weights"] = variant
     path = OUT.replace(".json", f"{tag}.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", path)
+
+
+def main_rover(src):
+    """--set rover: the ROVER pair's beam 8 + hotword.txt decodes (tests/test_gpu_hour.py
+    test_hour_rover_pair_matches_oracle token lists) against bench_hour_oracle_rover.json; the
+    beam-8 evidence of main() (the oracle's perturbation flip, exact boundary ties)."""
+    import torch
+
+    import bench
+    from oracle.fbank import fbank
+    from oracle.search import HotwordGraph, beam_search
+    from oracle.zipformer import ZipformerOracle
+    from zasr.model import PRESETS, synth_weights
+    torch.set_num_threads(8)
+    with open(os.path.join(HERE, "bench_hour_oracle_rover.json")) as f:
+        gold = json.load(f)
+    chunks = bench.make_chunks(3600.0, bench.AUDIO_SEED)
+    out = {"what": "chunks of bench.py --stage rover's hour where the GPU's fp32 / f16x3 decodes "
+                   "of either ROVER model differ from the oracle, each with the oracle-side "
+                   "evidence that it is an f32 tie",
+           "generator": "tests/golden/make_bench_hour_audit.py --set rover"}
+    for model, name, ds in (("rover30m", "zipformer-30m", 1), ("rover68m", "zipformer-68m", 0)):
+        key = f"{model}_beam8_hw"
+        cfg = PRESETS[name]()
+        orc = ZipformerOracle(cfg, synth_weights(cfg, bench.WEIGHT_SEED + ds))
+        graph = HotwordGraph(*bench.load_hotwords(bench.DEFAULT_HOTWORDS, cfg.vocab_size))
+        got = {}
+        for prec in ("fp32", "f16x3"):
+            path = os.path.join(src, f"hour_tokens_{prec}_{model}.json")
+            if os.path.exists(path):
+                with open(path) as f:
+                    got[prec] = json.load(f)["tokens"]
+        ref = gold[key]
+        diff = sorted({i for toks in got.values() for i, (a, b) in enumerate(zip(toks, ref)) if a != b})
+        entries, allowed = {}, []
+        for i in diff:
+            enc = orc.encoder(fbank(chunks[i]))
+            flips = [beam_search(perturbed(enc, sd), orc.decoder, orc.joiner, 8, graph)[0] != ref[i]
+                     for sd in (1, 2)]
+            ties = []
+            beam_search(enc, orc.decoder, orc.joiner, 8, graph, ties=ties)
+            e = {"gpu_tokens": {p: t[i] for p, t in got.items() if t[i] != ref[i]},
+                 "oracle_tokens": len(ref[i]),
+                 "oracle_flips_under_1e-6_perturbation": flips,
+                 "oracle_exact_boundary_tie_frames": ties[:32]}
+            e["allowed"] = any(flips) or bool(ties)
+            if e["allowed"]:
+                allowed.append(i)
+            entries[str(i)] = e
+            print(key, i, json.dumps({k: v for k, v in e.items() if k != "gpu_tokens"}), flush=True)
+        out[key] = {"differing_chunks": diff, "allowed_chunks": allowed, "chunks": entries}
+    path = OUT.replace(".json", "_rover.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print("wrote", path)

@@ -3,7 +3,9 @@
 The reference ships a second, executable fbank besides its kaldi-native-fbank call
 (`core/asr_engine.py:698-721`, knf absent here): `computeFbank` in
 `offline_pwa/static/js/pure-ort-asr-worker.js:470-519`.  This script runs that function under
-node (`tests/golden/run_reference_fbank.js`, which evaluates the worker file in a vm context)
+node (`tests/golden/run_reference_fbank.js`, which cuts the fbank's constants and functions out
+of the worker file's text and evaluates only those, in a bare vm context, in a child process
+with an empty environment)
 on seeded inputs and commits its outputs to `tests/golden/fbank_js.npz`:
 
   lengths 1, 399, 400, 401, 1599, 16000*7 + 123 and 480000 samples of seeded synthetic speech
@@ -53,7 +55,8 @@ def main():
         np.concatenate([x for _, x in ins]).astype(np.float32).tofile(fin)
         lens = ",".join(str(x.shape[0]) for _, x in ins)
         r = subprocess.run(["node", os.path.join(HERE, "run_reference_fbank.js"), WORKER, fin,
-                            lens, fout], capture_output=True, text=True, check=True)
+                            lens, fout], capture_output=True, text=True, check=True, cwd=td,
+                           env={"PATH": "/usr/bin:/bin"}, timeout=600)
         info = json.loads(r.stdout.strip().splitlines()[-1])
         flat = np.fromfile(fout, dtype=np.float32)
     arrays, off = {}, 0
@@ -65,7 +68,7 @@ def main():
     node = subprocess.run(["node", "--version"], capture_output=True, text=True).stdout.strip()
     meta = {"generator": "tests/golden/make_golden_fbank_js.py + run_reference_fbank.js",
             "reference": "offline_pwa/static/js/pure-ort-asr-worker.js:470-519 computeFbank",
-            "node": node, "worker_messages": info["posted"],
+            "node": node, "extracted_functions": info["functions"],
             "names": [n for n, _ in ins]}
     np.savez_compressed(OUT, meta=np.array(json.dumps(meta)), **arrays)
     print(f"wrote {OUT}: {len(ins)} inputs, {off // 80} frames; {meta}")

@@ -169,3 +169,75 @@ def test_hour_beam_calibrated_matches_oracle(hour_bc, prec, method, bound):
     + hotword.txt emits at the greedy rate; the exact-f32-quality modes still equal the oracle
     except at audited f32 ties (tests/golden/bench_hour_audit_beam-calibrated.json)."""
     _check_exact(hour_bc, prec, method, bound)
+
+
+# ------------------------------------------------------------------ config 4 (ROVER pair)
+ROVER_GOLDEN = os.path.join(REPO, "tests", "golden", "bench_hour_oracle_rover.json")
+ROVER_AUDIT = os.path.join(REPO, "tests", "golden", "bench_hour_audit_rover.json")
+ROVER_MODELS = {"rover30m": ("zipformer-30m", 1), "rover68m": ("zipformer-68m", 0)}
+
+
+@pytest.fixture(scope="module")
+def hour_rover():
+    """bench.py --stage rover's hour and pair: Zipformer-30M (synth_weights, WEIGHT_SEED + 1) and
+    Zipformer-68M (synth_weights, WEIGHT_SEED), each beam 8 + hotword.txt, against the oracle's
+    decode of the same hour (tests/golden/make_bench_hour_golden.py --set rover)."""
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+
+    import bench
+    chunks = bench.make_chunks(3600.0, bench.AUDIO_SEED)
+    with open(ROVER_GOLDEN) as f:
+        g = json.load(f)
+    assert [int(c.shape[0]) for c in chunks] == g["chunk_samples"]
+    lens = [int(c.shape[0]) for c in chunks]
+    offs = np.cumsum([0] + lens[:-1]).tolist()
+    d_wav = torch.from_numpy(np.concatenate(chunks)).to("cuda:0")
+    torch.cuda.synchronize()
+    audit = {}
+    if os.path.exists(ROVER_AUDIT):
+        with open(ROVER_AUDIT) as f:
+            audit = json.load(f)
+    return {"g": g, "d_wav": d_wav, "offs": offs, "lens": lens, "audit": audit}
+
+
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+@pytest.mark.parametrize("model", sorted(ROVER_MODELS))
+def test_hour_rover_pair_matches_oracle(hour_rover, model, prec):
+    """BASELINE config 4's two decodes of the hour in the exact-f32-quality modes: every chunk
+    identical to the oracle's except audited f32 ties (tests/golden/bench_hour_audit_rover.json,
+    made by make_bench_hour_audit.py --set rover from these runs' token lists)."""
+    import torch
+
+    import bench
+    from model_fixtures import model_dir
+    from zasr.binding import Recognizer
+    from zasr.model import PRESETS, synth_weights
+    name, ds = ROVER_MODELS[model]
+    cfg = PRESETS[name]()
+    path = model_dir(f"{model}_{bench.WEIGHT_SEED + ds}", cfg, synth_weights(cfg, bench.WEIGHT_SEED + ds))
+    phrases, scores = bench.load_hotwords(bench.DEFAULT_HOTWORDS, cfg.vocab_size)
+    h = hour_rover
+    rec = Recognizer(path, "modified_beam_search", 8, hotwords=phrases, hotword_scores=scores,
+                     precision=prec)
+    res = rec.decode_device(h["d_wav"].data_ptr(), h["offs"], h["lens"], beam=8,
+                            stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rec.close()
+    got = [r.token_ids.tolist() for r in res]
+    key = f"{model}_beam8_hw"
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, f"hour_tokens_{prec}_{model}.json"), "w") as f:
+        json.dump({"tokens": got, "frames": [r.frames.tolist() for r in res]}, f,
+                  separators=(",", ":"))
+    ref = h["g"][key]
+    agree = bench.oracle_agreement(key, ref, [got], ROVER_AUDIT)
+    audit = h["audit"].get(key, {})
+    allowed = set(audit.get("allowed_chunks", []))
+    diff = [i for i, (a, b) in enumerate(zip(got, ref)) if a != b]
+    unexplained = [c for c in diff if c not in allowed]
+    assert not unexplained, (prec, model, agree, sorted(allowed))
+    for c in diff:
+        assert got[c] in audit["chunks"][str(c)]["gpu_tokens"].values(), (prec, model, c)
+    assert agree["ter"] <= 0.01, agree
