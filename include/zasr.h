@@ -332,6 +332,19 @@ int zasr_fbank_set_mel_banks(zasr_recognizer* h, const float* banks, int32_t n_b
    configuration (e.g. > 1024 threads) returns ZASR_ERR_RUNTIME with the HIP error in
    zasr_last_error().  No reference counterpart: a self-test of the error path. */
 int zasr_selftest_launch(int32_t block_threads);
+/* Kernel self-tests of the f16x3 one-accumulator kernels on host operands (device 0,
+   synchronous; no reference counterpart: test infrastructure that reaches the shapes and row
+   counts the decode meets only incidentally).  gemm_h3r: C[M][N'] = epi(A[M][K] W[N][K]^T +
+   bias), epi 0 (none), 3 (C += ..., C is read) or 8 (GLU over interleaved rows, N' = N / 2);
+   K in {96, 192, 256, 288, 384, 512}, N >= 128, N % 16 == 0.  ffn_h3: X[R][D] += W2
+   SwooshL(W1 Y + b1) + b2, then X = byp_orig + (X - byp_orig) * byp_scale when byp_orig is
+   given (the bypass_mid epilogue); D in {128, 256, 384, 512} (F % 32 == 0) or 192
+   (F % 64 == 0).  Every |w| must be below 31 (the kernels scale the fp16 hi piece by 2^11). */
+int zasr_selftest_gemm_h3r(int32_t M, int32_t K, int32_t N, int32_t epi, const float* A,
+                           const float* W, const float* bias, float* C);
+int zasr_selftest_ffn_h3(int32_t R, int32_t D, int32_t F, const float* Y, const float* W1,
+                         const float* b1, const float* W2, const float* b2,
+                         const float* byp_orig, const float* byp_scale, float* X);
 
 /* profiling: per-kernel-class HIP-event timing on the handle's stream.  on = 0 off,
    1 kernel classes, 2 kernel classes with the encoder GEMMs split by shape

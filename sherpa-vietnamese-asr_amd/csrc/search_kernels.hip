@@ -1751,9 +1751,10 @@ __global__ __launch_bounds__(512) void joiner_greedy_kernel(GreedyFusedArgs a) {
   const int D = dt.D, d4 = D >> 2;
   const int base = s;  // Hmax = 1
   const int y1 = st.y1[base], y2 = st.y2[base];
-  float4 x[F][Q];
-#pragma unroll
-  for (int r = 0; r < F; ++r)
+  // rows in a 3-deep register ring (rows 0..2 loaded at once, row r + 3 once row r is done):
+  // greedy needs the rows only up to the window's first emission, and with all four rows live
+  // beside the emitting row's entropy work the wave would need more than 256 registers
+  auto load_row = [&](float4 (&x)[Q], int r) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int i = lane + 64 * q;
@@ -1761,115 +1762,86 @@ __global__ __launch_bounds__(512) void joiner_greedy_kernel(GreedyFusedArgs a) {
       const float4 v = __builtin_bit_cast(
           float4, __builtin_amdgcn_raw_buffer_load_b128(rso, ((s * F + r) * a.ldo + 4 * ii) * 4, 0,
                                                         kCpolSc1));
-      x[r][q] = (r < nf && i < V4) ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      x[q] = (r < nf && i < V4) ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     }
+  };
+  float4 xr[3][Q];
+  load_row(xr[0], 0);
+  load_row(xr[1], 1);
+  load_row(xr[2], 2);
   double lp = st.lp[base];
-  // ---- A + B: row statistics; the all-blank score recurrence (greedy_spec steps A, B) ----
-  float m1r[F], m2r[F], lsr[F], ser[F], lfr[F];
-  double lpr[F + 1];
-  lpr[0] = lp;
-#pragma unroll
-  for (int r = 0; r < F; ++r) {
-    float m1 = -INFINITY, m2 = -INFINITY;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const float4 v = x[r][q];
-      m2 = fmaxf(m2, fminf(m1, v.x)); m1 = fmaxf(m1, v.x);
-      m2 = fmaxf(m2, fminf(m1, v.y)); m1 = fmaxf(m1, v.y);
-      m2 = fmaxf(m2, fminf(m1, v.z)); m1 = fmaxf(m1, v.z);
-      m2 = fmaxf(m2, fminf(m1, v.w)); m1 = fmaxf(m1, v.w);
-    }
-    wave_max2_dpp(m1, m2);
-    float se = 0.f;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      se += __expf(x[r][q].x - m1);
-      se += __expf(x[r][q].y - m1);
-      se += __expf(x[r][q].z - m1);
-      se += __expf(x[r][q].w - m1);
-    }
-    se = wave_sum_dpp(se);
-    const float ls = logf(se);
-    m1r[r] = m1;
-    m2r[r] = m2;
-    lsr[r] = ls;
-    ser[r] = se;
-    // blank = token 0 = lane 0's first element
-    const float d0 = lane_f(x[r][0].x, 0) - m1;
-    const float lf = (float)lp;
-    lfr[r] = lf;
-    if (r < nf) lp = (double)((d0 - ls) + lf);
-    lpr[r + 1] = lp;
-  }
-  // ---- C: top-1 per row; D: the first emission of the window ----
+  // per row in frame order (greedy_spec steps A-D): statistics, the score before the frame
+  // under the all-blank hypothesis (lf), the top-1; the first non-blank top-1 is the emission
   int fe = -1, tok = 0;
+  float m1 = 0.f, m2 = 0.f, se = 1.f, ls = 0.f, lf = 0.f, e1 = 0.f, e3 = 0.f;
+  double lpb = 0.0;
 #pragma unroll
   for (int r = 0; r < F; ++r) {
-    if (r >= nf || fe >= 0) continue;  // wave-uniform
-    const float lf = lfr[r], m1 = m1r[r], ls = lsr[r];
-    const float vmax = (0.f - ls) + lf;
+    if (r >= nf) break;  // wave-uniform
+    float4 (&x)[Q] = xr[r % 3];
+    float rm1 = -INFINITY, rm2 = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float4 v = x[q];
+      rm2 = fmaxf(rm2, fminf(rm1, v.x)); rm1 = fmaxf(rm1, v.x);
+      rm2 = fmaxf(rm2, fminf(rm1, v.y)); rm1 = fmaxf(rm1, v.y);
+      rm2 = fmaxf(rm2, fminf(rm1, v.z)); rm1 = fmaxf(rm1, v.z);
+      rm2 = fmaxf(rm2, fminf(rm1, v.w)); rm1 = fmaxf(rm1, v.w);
+    }
+    wave_max2_dpp(rm1, rm2);
+    float rse = 0.f;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      rse += __expf(x[q].x - rm1);
+      rse += __expf(x[q].y - rm1);
+      rse += __expf(x[q].z - rm1);
+      rse += __expf(x[q].w - rm1);
+    }
+    rse = wave_sum_dpp(rse);
+    const float rls = logf(rse);
+    const float d0 = lane_f(x[0].x, 0) - rm1;  // blank = token 0 = lane 0's first element
+    const float rlf = (float)lp;
+    const float vmax = (0.f - rls) + rlf;
     int bq = 0x7fffffff;
 #pragma unroll
     for (int q = Q - 1; q >= 0; --q) {
       const int i = 4 * (lane + 64 * q);
-      const float4 v = x[r][q];
-      const int c = (((v.x - m1) - ls) + lf == vmax) ? i
-                  : (((v.y - m1) - ls) + lf == vmax) ? i + 1
-                  : (((v.z - m1) - ls) + lf == vmax) ? i + 2
-                  : (((v.w - m1) - ls) + lf == vmax) ? i + 3 : 0x7fffffff;
+      const float4 v = x[q];
+      const int c = (((v.x - rm1) - rls) + rlf == vmax) ? i
+                  : (((v.y - rm1) - rls) + rlf == vmax) ? i + 1
+                  : (((v.z - rm1) - rls) + rlf == vmax) ? i + 2
+                  : (((v.w - rm1) - rls) + rlf == vmax) ? i + 3 : 0x7fffffff;
       bq = c < bq ? c : bq;
     }
     const int bm = wave_min_i_dpp(bq);
     const int best = bm < V ? bm : 0;
-    if (best != 0) {
+    if (best != 0) {  // the emission: this row's entropy terms (search_step_kernel's statistics)
       fe = r;
       tok = best;
+      m1 = rm1;
+      m2 = rm2;
+      se = rse;
+      ls = rls;
+      lf = rlf;
+      lpb = lp;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float vv[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float d = vv[c] - m1;
+          const float e = __expf(d);
+          e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
+          e3 += __expf(d * (1.0f / 3.0f));
+        }
+      }
+      break;
     }
+    lp = (double)((d0 - rls) + rlf);
+    if (r + 3 < F) load_row(xr[r % 3], r + 3);
   }
   const int t_new = t0 + (fe >= 0 ? fe + 1 : nf);
-  // the next window's rows and context row go out before the emission bookkeeping
-  const bool more = t_new < T_s;
-  const int nf2 = T_s - t_new < F ? T_s - t_new : F;
-  const int ny2 = fe >= 0 ? y1 : y2, ny1 = fe >= 0 ? tok : y1;
-  float4 tv[2], ev[F][2];
-  if (more) {
-    const float4* tab4 = reinterpret_cast<const float4*>(dt.table + ((long)ny2 * dt.V + ny1) * D);
-    const float4* enc4 = reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + t_new) * D);
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int c4 = lane + 64 * jj < d4 ? lane + 64 * jj : d4 - 1;
-      tv[jj] = tab4[c4];
-#pragma unroll
-      for (int f = 0; f < F; ++f) ev[f][jj] = enc4[(long)(f < nf2 ? f : 0) * d4 + c4];
-    }
-  }
   if (fe >= 0) {
-    float m1 = m1r[0], m2 = m2r[0], se = ser[0], ls = lsr[0], lf = lfr[0];
-    double lpb = lpr[0];
-#pragma unroll
-    for (int rr = 1; rr < F; ++rr) {
-      m1 = rr == fe ? m1r[rr] : m1;
-      m2 = rr == fe ? m2r[rr] : m2;
-      se = rr == fe ? ser[rr] : se;
-      ls = rr == fe ? lsr[rr] : ls;
-      lf = rr == fe ? lfr[rr] : lf;
-      lpb = rr == fe ? lpr[rr] : lpb;
-    }
-    float e1 = 0.f, e3 = 0.f;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      float4 v = x[0][q];
-#pragma unroll
-      for (int rr = 1; rr < F; ++rr) v = rr == fe ? x[rr][q] : v;
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float d = vv[c] - m1;
-        const float e = __expf(d);
-        e1 = (e > 0.f) ? fmaf(e, d, e1) : e1;
-        e3 += __expf(d * (1.0f / 3.0f));
-      }
-    }
     e1 = wave_sum_dpp(e1);
     e3 = wave_sum_dpp(e3);
     if (lane == 0) {
@@ -1906,8 +1878,25 @@ __global__ __launch_bounds__(512) void joiner_greedy_kernel(GreedyFusedArgs a) {
       st.node[base] = nid;
     }
   } else if (lane == 0) {
-    st.lp[base] = lpr[nf];
+    st.lp[base] = lp;  // the score after the window's nf blank frames
     st.lpf[base] = 0;
+  }
+  // the next window's rows and the new context's table row (issued once the window's rows are
+  // dead: with them live beside these the wave would need more than 256 registers)
+  const bool more = t_new < T_s;
+  const int nf2 = T_s - t_new < F ? T_s - t_new : F;
+  const int ny2 = fe >= 0 ? y1 : y2, ny1 = fe >= 0 ? tok : y1;
+  float4 tv[2], ev[F][2];
+  if (more) {
+    const float4* tab4 = reinterpret_cast<const float4*>(dt.table + ((long)ny2 * dt.V + ny1) * D);
+    const float4* enc4 = reinterpret_cast<const float4*>(dt.enc + (long)(dt.enc_off[s] + t_new) * D);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int c4 = lane + 64 * jj < d4 ? lane + 64 * jj : d4 - 1;
+      tv[jj] = tab4[c4];
+#pragma unroll
+      for (int f = 0; f < F; ++f) ev[f][jj] = enc4[(long)(f < nf2 ? f : 0) * d4 + c4];
+    }
   }
   if (lane == 0) {
     a.t_cur[s] = t_new;

@@ -665,6 +665,25 @@ int zasr_selftest_launch(int32_t block_threads) {
   });
 }
 
+int zasr_selftest_gemm_h3r(int32_t M, int32_t K, int32_t N, int32_t epi, const float* A,
+                           const float* W, const float* bias, float* C) {
+  if (!A || !W || !C) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    zasr::selftest_gemm_h3r(M, K, N, epi, A, W, bias, C);
+    return (int)ZASR_OK;
+  });
+}
+
+int zasr_selftest_ffn_h3(int32_t R, int32_t D, int32_t F, const float* Y, const float* W1,
+                         const float* b1, const float* W2, const float* b2,
+                         const float* byp_orig, const float* byp_scale, float* X) {
+  if (!Y || !W1 || !b1 || !W2 || !b2 || !X) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    zasr::selftest_ffn_h3(R, D, F, Y, W1, b1, W2, b2, byp_orig, byp_scale, X);
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float threshold,
                        uint8_t* d_flags, void* stream) {
   if (n < 0 || (n > 0 && (!d_wav || !d_flags))) return fail(ZASR_ERR_INVALID, "null argument");

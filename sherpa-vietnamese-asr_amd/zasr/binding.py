@@ -35,6 +35,7 @@ EXPORTS = (
     "zasr_stream_frames", "zasr_stream_log_probs", "zasr_stream_token_stats",
     "zasr_stream_result_json", "zasr_set_tokens", "zasr_model_routes",
     "zasr_fbank_set_mel_banks", "zasr_selftest_launch", "zasr_decode_host_batches",
+    "zasr_selftest_gemm_h3r", "zasr_selftest_ffn_h3",
 )
 
 
@@ -42,6 +43,9 @@ EXPORTS = (
 # "bf16x3" / "bf16x6" = f32 storage, split-bf16 products (2 / 3 pieces per operand) on the
 # bf16 MFMA
 PRECISIONS = {"fp32": 0, "bf16": 1, "bf16_enc": 2, "bf16x3": 3, "bf16x6": 4, "f16x3": 5}
+
+
+C_FP = C.POINTER(C.c_float)
 
 
 class ZasrError(RuntimeError):
@@ -209,6 +213,10 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_fbank_set_mel_banks.restype = C.c_int
     lib.zasr_selftest_launch.argtypes = [I32]
     lib.zasr_selftest_launch.restype = C.c_int
+    lib.zasr_selftest_gemm_h3r.argtypes = [I32, I32, I32, I32, fp, fp, fp, fp]
+    lib.zasr_selftest_gemm_h3r.restype = C.c_int
+    lib.zasr_selftest_ffn_h3.argtypes = [I32, I32, I32, fp, fp, fp, fp, fp, fp, fp, fp]
+    lib.zasr_selftest_ffn_h3.restype = C.c_int
     if path is None:
         _lib = lib
     return lib
@@ -250,6 +258,37 @@ def selftest_launch(block_threads: int, lib_path: Optional[str] = None) -> None:
     rc = lib.zasr_selftest_launch(int(block_threads))
     if rc != 0:
         raise ZasrError(lib.zasr_last_error().decode())
+
+
+def selftest_gemm_h3r(A, W, bias, C, epi: int = 0, lib_path: Optional[str] = None) -> np.ndarray:
+    """gemm_h3r_kernel alone on host operands (zasr_selftest_gemm_h3r): returns C after
+    C = epi(A W^T + bias) (epi 3: C += ..., 8: GLU over interleaved rows)."""
+    lib = load_library(lib_path)
+    A, W, C = _f32(A), _f32(W), _f32(C).copy()
+    b = None if bias is None else _f32(bias)
+    p = lambda x: None if x is None else x.ctypes.data_as(C_FP)
+    rc = lib.zasr_selftest_gemm_h3r(A.shape[0], A.shape[1], W.shape[0], int(epi), p(A), p(W),
+                                    p(b), p(C))
+    if rc != 0:
+        raise ZasrError(lib.zasr_last_error().decode())
+    return C
+
+
+def selftest_ffn_h3(Y, W1, b1, W2, b2, X, byp_orig=None, byp_scale=None,
+                    lib_path: Optional[str] = None) -> np.ndarray:
+    """ffn_wide_h3_kernel alone on host operands (zasr_selftest_ffn_h3): returns
+    X + W2 SwooshL(W1 Y + b1) + b2 (then the bypass_mid blend when byp_orig is given)."""
+    lib = load_library(lib_path)
+    Y, W1, b1, W2, b2, X = (_f32(v) for v in (Y, W1, b1, W2, b2, X))
+    X = X.copy()
+    bo = None if byp_orig is None else _f32(byp_orig)
+    bs = None if byp_scale is None else _f32(byp_scale)
+    p = lambda x: None if x is None else x.ctypes.data_as(C_FP)
+    rc = lib.zasr_selftest_ffn_h3(Y.shape[0], Y.shape[1], W1.shape[0], p(Y), p(W1), p(b1), p(W2),
+                                  p(b2), p(bo), p(bs), p(X))
+    if rc != 0:
+        raise ZasrError(lib.zasr_last_error().decode())
+    return X
 
 
 def silence_flags(d_wav_ptr: int, n: int, frame_len: int, threshold: float, d_flags_ptr: int,

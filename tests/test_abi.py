@@ -14,7 +14,7 @@ HDR = os.path.join(REPO, "include", "zasr.h")
 def header_functions():
     text = open(HDR).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(zasr_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(zasr_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_built():
