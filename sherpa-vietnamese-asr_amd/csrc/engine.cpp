@@ -1708,9 +1708,13 @@ void Engine::launch_search(const float* d_enc, const std::vector<int>& t_out, in
     const size_t jrs = (size_t)joiner_packed_rows((long)S * F);
     void* Js = j16 ? (void*)ws<__bf16>("gs_joinin_h", jrs * D * jpc)
                    : (void*)ws<float>("gs_joinin", (size_t)S * F * D);
-    // one launch per super-step (joiner_greedy_kernel) for the packed bf16 / f16x3 joiner at
-    // F = 4; the other modes run the joiner and greedy_spec as two launches
-    static const bool fused_env = !(getenv("ZASR_GREEDY_FUSED") && getenv("ZASR_GREEDY_FUSED")[0] == '0');
+    // ZASR_GREEDY_FUSED=1: one launch per super-step (joiner_greedy_kernel, packed bf16 / f16x3
+    // joiner, F = 4), bit-identical to the two launches but measured slower: per super-step
+    // 22.8 vs 21.0 us of kernel time, and its 8-wave blocks at 219 VGPRs crowd the next batch's
+    // encoder out (pipelined bf16 hour 104.7k vs 120.8k xRT, profiles/r06/fused_greedy/,
+    // DESIGN.md §11) -- the write-through hand-off and the last-arriver's one wave per stream
+    // cost what the launch boundary did.  Default: joiner + greedy_spec
+    static const bool fused_env = getenv("ZASR_GREEDY_FUSED") && getenv("ZASR_GREEDY_FUSED")[0] == '1';
     const bool fused = fused_env && packed && F == 4 && (jnp == 0 || jnp == kPiecesF16) &&
                        (D == 256 || D == 512) && V % 4 == 0 && V <= 2048;
     const int ldo = fused ? joiner_greedy_ldo(V) : V;

@@ -447,8 +447,8 @@ def check_pipelined_batches(method, beam):
 @pytest.mark.parametrize("env,method,beam", [
     ({"ZASR_SEARCH_JOBS": "3", "ZASR_ENC_STREAMS": "2"}, "modified_beam_search", 4),
     ({"ZASR_SEARCH_CUS": "32"}, "greedy_search", 1),
-    ({"ZASR_GREEDY_FUSED": "0"}, "greedy_search", 1),
-], ids=["three_jobs_two_enc_streams", "cu_masked_search", "two_launch_greedy"])
+    ({"ZASR_GREEDY_FUSED": "1"}, "greedy_search", 1),
+], ids=["three_jobs_two_enc_streams", "cu_masked_search", "fused_greedy"])
 def test_pipelined_batches_env_variants(need_gpu, env, method, beam):
     """The pipeline variants the engine reads from the environment at first use (three beam
     searches in flight + two encoder streams; the CU-partitioned search stream, whose encoder
@@ -517,7 +517,7 @@ def check_greedy_out(out_path, prec):
 def test_fused_greedy_bit_identical_to_two_launches(need_gpu, tmp_path, prec):
     """joiner_greedy_kernel (one launch per super-step: the joiner's tiles, then the row
     tile's greedy step in its last-arriving block, logits handed over by write-through stores)
-    returns exactly what the joiner + greedy_spec launches return (ZASR_GREEDY_FUSED=0): the
+    returns exactly what the joiner + greedy_spec launches (the default) return: the
     same MFMA sequence per logits tile and the same per-frame arithmetic, so every token,
     frame, log-prob and statistic is bit-identical (a fresh process each: the switch is read
     once)."""
