@@ -896,6 +896,10 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     }
   }
 
+  // step 2c's table-row prefetches land here (read only by the empty asm of step 4)
+  float pf[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) pf[l] = 0.f;
   // ---- 1 + 2. per row: statistics (:1096-1098, :1159-1181) and the row's top candidates ----
   //   max / second max; S = sum e, E1 = sum e d, E3 = sum exp(d / 3) (d = x - max):
   //   entropy = log S - E1 / S, sum p^(1/3) = S^(-1/3) E3, top1 = 1 / S, top2 = e^(m2-m1) / S
@@ -1129,10 +1133,25 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
         dLen[slot] = klen;
         dY1[slot] = ny1;
         dY2[slot] = ny2;
+        if constexpr (TABLE) {
+          // the candidate's decoder-table row (step 4 reads it if the candidate survives): one
+          // dword per 128-byte line pulls the row into this XCD's L2 while wave 0 ranks, so
+          // step 4's reads hit L2 instead of paying an HBM round trip (the table is V^2 rows,
+          // gigabytes: a cold row every frame).  The values are only kept live (pf) until
+          // step 4, so the loads complete under step 3.
+          if (next) {
+            const float* row = dt.table + ((long)ny2 * dt.V + ny1) * dt.D;
+#pragma unroll
+            for (int l = 0; l < 16; ++l) pf[l] = row[32 * (l < dt.D / 32 ? l : 0)];
+          }
+        }
       }
     }
   }
-  __syncthreads();
+  // LDS-only barrier (s_waitcnt lgkmcnt(0) + s_barrier): __syncthreads() would also drain the
+  // table-row prefetches above (vmcnt(0)); step 4's barrier waits for them
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   // ---- 3. expansion (:1110-1138): ranking and duplicate merge in wave 0 ----
   const int total_c = n * V;
   const int k = beam < total_c ? beam : total_c;
@@ -1217,6 +1236,10 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
   // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]),
   //         candidate c by wave c % 8 ----
   if constexpr (TABLE) {
+    // the prefetches are complete before step 4 (their registers stay untouched until here)
+    asm volatile("" ::"v"(pf[0]), "v"(pf[1]), "v"(pf[2]), "v"(pf[3]), "v"(pf[4]), "v"(pf[5]),
+                 "v"(pf[6]), "v"(pf[7]), "v"(pf[8]), "v"(pf[9]), "v"(pf[10]), "v"(pf[11]),
+                 "v"(pf[12]), "v"(pf[13]), "v"(pf[14]), "v"(pf[15]));
     if (next) {
       __syncthreads();  // sFmask, sKK, cSrc
       const unsigned long long fm = sFmask;
