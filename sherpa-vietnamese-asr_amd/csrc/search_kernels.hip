@@ -824,6 +824,14 @@ void launch_table_init(const DecTable& dt, int S, int Hmax, hipStream_t st) {
 //      slots h * KB + rank, so the hotword table loads overlap the other rows.
 // After one block barrier wave 0 ranks the n * KB slots, merges duplicates and writes the new
 // hypotheses; then every wave writes the next frame's joiner input of its candidates.
+#ifdef ZASR_SEARCH_STAMPS  // development: per-phase shader cycles of block 0, wave 0
+__device__ unsigned long long g_ss_sum[12];
+__device__ unsigned long long g_ss_n;
+#define SS_STAMP(i) \
+  if (ss_on) ss_t[i] = __builtin_amdgcn_s_memtime();
+#else
+#define SS_STAMP(i)
+#endif
 template <int KB, int Q, bool TABLE>
 __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const float* logits,
                                                           int V, int Hmax, int beam, int t,
@@ -838,6 +846,11 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int base = s * Hmax;
+#ifdef ZASR_SEARCH_STAMPS
+  const bool ss_on = s == 0 && tid == 0;
+  unsigned long long ss_t[12];
+#endif
+  SS_STAMP(0)
 
   __shared__ float4 sStats[kMaxBeam];
   __shared__ unsigned long long cK[NKS], dHash[NKS];
@@ -896,10 +909,6 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     }
   }
 
-  // step 2c's table-row prefetches land here (read only by the empty asm of step 4)
-  float pf[16];
-#pragma unroll
-  for (int l = 0; l < 16; ++l) pf[l] = 0.f;
   // ---- 1 + 2. per row: statistics (:1096-1098, :1159-1181) and the row's top candidates ----
   //   max / second max; S = sum e, E1 = sum e d, E3 = sum exp(d / 3) (d = x - max):
   //   entropy = log S - E1 / S, sum p^(1/3) = S^(-1/3) E3, top1 = 1 / S, top2 = e^(m2-m1) / S
@@ -936,6 +945,7 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     if constexpr (KB <= 4) thr_x = fmaxf(thr_x, dpp_f<kDppRor8>(thr_x));
     thr_x = wave_min_dpp(thr_x);
     wave_max2_dpp(m1, m2);
+    SS_STAMP(1)
     float se = 0.f, e1 = 0.f, e3 = 0.f;
     auto acc = [&](float x) {
       const float d = x - m1;  // -inf past V -> e = 0
@@ -958,6 +968,7 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     if (lane == 0)
       sStats[h] = make_float4(ls - e1 / se, e3 * exp2f(-log2f(se) * (1.0f / 3.0f)), 1.0f / se,
                               __expf(m2 - m1) / se);
+    SS_STAMP(2)
     const double ld = ld_cur;
     const bool f64 = lpf_cur != 0;
     const float lf = (float)ld;
@@ -995,10 +1006,17 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     float val = -INFINITY;
     int ncand = total;
     bool fast = total <= 64;
+    // the hotword class of this lane's candidate token, fetched now so that the dependent
+    // transition loads of step 2c are the only hotword round trip left behind the ranking
+    int pcls = -1;
     if (fast) {
       if (lane < total) {
+        const int col = wI[wid][lane];
         val = score(wX[wid][lane]);
-        key = make_key(val, h * V + wI[wid][lane]);
+        key = make_key(val, h * V + col);
+#ifndef ZASR_NO_CLS_PREFETCH  // (A/B builds: tools/ab_variant.sh)
+        if (use_hw) pcls = hw.tok2cls[col];
+#endif
       }
     }
     int rank = 64;
@@ -1083,6 +1101,7 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       ncand = got;
       rank_keys();
     }
+    SS_STAMP(3)
     // 2c. the row's KB best -> slots h * KB + rank, decoded (:1116-1131): blank keeps the
     //     sequence, non-blank appends and steps the hotword graph (blank and UNK skip it,
     //     :1129); every lane < KB writes its slot (empty: key 0)
@@ -1108,7 +1127,12 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
           ny2 = py2;
         } else {
           if (use_hw && tok != 2) {
+#ifndef ZASR_NO_CLS_PREFETCH
+            // the fast path kept each candidate in the lane that fetched its class
+            const int cls = fast ? pcls : hw.tok2cls[tok];
+#else
             const int cls = hw.tok2cls[tok];
+#endif
             if (cls < 0) {
               sc += -hw.node_score[nhw];
               nhw = 0;
@@ -1133,25 +1157,12 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
         dLen[slot] = klen;
         dY1[slot] = ny1;
         dY2[slot] = ny2;
-        if constexpr (TABLE) {
-          // the candidate's decoder-table row (step 4 reads it if the candidate survives): one
-          // dword per 128-byte line pulls the row into this XCD's L2 while wave 0 ranks, so
-          // step 4's reads hit L2 instead of paying an HBM round trip (the table is V^2 rows,
-          // gigabytes: a cold row every frame).  The values are only kept live (pf) until
-          // step 4, so the loads complete under step 3.
-          if (next) {
-            const float* row = dt.table + ((long)ny2 * dt.V + ny1) * dt.D;
-#pragma unroll
-            for (int l = 0; l < 16; ++l) pf[l] = row[32 * (l < dt.D / 32 ? l : 0)];
-          }
-        }
       }
     }
   }
-  // LDS-only barrier (s_waitcnt lgkmcnt(0) + s_barrier): __syncthreads() would also drain the
-  // table-row prefetches above (vmcnt(0)); step 4's barrier waits for them
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  SS_STAMP(4)
+  __syncthreads();
+  SS_STAMP(5)
   // ---- 3. expansion (:1110-1138): ranking and duplicate merge in wave 0 ----
   const int total_c = n * V;
   const int k = beam < total_c ? beam : total_c;
@@ -1170,6 +1181,7 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
     }
     const int kk = k < nz ? k : nz;
     if (lane == 0) sKK = kk;
+    SS_STAMP(6)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // 3b. duplicates of the full sequence merge into their first occurrence, in candidate
@@ -1232,16 +1244,14 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       st.node_count[s] = node_base + __popcll(emask);
       sFmask = fmask;
     }
+    SS_STAMP(7)
   }
   // ---- 4. the next frame's joiner input J[slot] = tanh(enc[s, t + 1] + table[context]),
   //         candidate c by wave c % 8 ----
   if constexpr (TABLE) {
-    // the prefetches are complete before step 4 (their registers stay untouched until here)
-    asm volatile("" ::"v"(pf[0]), "v"(pf[1]), "v"(pf[2]), "v"(pf[3]), "v"(pf[4]), "v"(pf[5]),
-                 "v"(pf[6]), "v"(pf[7]), "v"(pf[8]), "v"(pf[9]), "v"(pf[10]), "v"(pf[11]),
-                 "v"(pf[12]), "v"(pf[13]), "v"(pf[14]), "v"(pf[15]));
     if (next) {
       __syncthreads();  // sFmask, sKK, cSrc
+      SS_STAMP(8)
       const unsigned long long fm = sFmask;
       const int kk_all = sKK;
       for (int cc = wid; cc < kk_all; cc += NW) {
@@ -1258,6 +1268,23 @@ __global__ __launch_bounds__(512) void search_step_kernel(SearchState st, const 
       }
     }
   }
+#ifdef ZASR_SEARCH_STAMPS
+  if (ss_on) {
+    ss_t[9] = __builtin_amdgcn_s_memtime();
+    if (next) {
+      for (int q = 1; q < 10; ++q) atomicAdd(&g_ss_sum[q], ss_t[q] - ss_t[q - 1]);
+      atomicAdd(&g_ss_n, 1ull);
+    } else {
+      const unsigned long long n = g_ss_n > 0 ? g_ss_n : 1;
+      printf("[search stamps] frames %llu mean cycles: max %llu stats %llu topk %llu decode %llu "
+             "barrier %llu rank %llu tail %llu barrier2 %llu J %llu\n", g_ss_n, g_ss_sum[1] / n,
+             g_ss_sum[2] / n, g_ss_sum[3] / n, g_ss_sum[4] / n, g_ss_sum[5] / n, g_ss_sum[6] / n,
+             g_ss_sum[7] / n, g_ss_sum[8] / n, g_ss_sum[9] / n);
+      for (int q = 0; q < 12; ++q) g_ss_sum[q] = 0;
+      g_ss_n = 0;
+    }
+  }
+#endif
 }
 
 void launch_search_step(const SearchState& s, const float* logits, int V, int S, int Hmax,
