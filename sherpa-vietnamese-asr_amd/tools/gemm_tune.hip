@@ -25,8 +25,11 @@ static float* dA;
 static __bf16 *dA16, *dB, *dC16, *dRef16;
 static float *dC, *dRef, *dbias;
 
+struct SweepResult { float def_us = 0.f, best_us = 1e30f; const char* best = ""; };
+
 template <typename TA, typename TC, int EPI>
-static void sweep(const Shape& s) {
+static SweepResult sweep(const Shape& s) {
+  SweepResult res;
   GemmParams p{};
   p.A = std::is_same<TA, float>::value ? dA : reinterpret_cast<const float*>(dA16);
   p.lda = s.K;
@@ -117,14 +120,52 @@ static void sweep(const Shape& s) {
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
     printf("  %s %.1f%s", v.first, ms * 100.f, same ? "" : "(DIFF)");
+    if (!strcmp(v.first, "default")) res.def_us = ms * 100.f;
+    if (same && ms * 100.f < res.best_us) { res.best_us = ms * 100.f; res.best = v.first; }
     hipEventDestroy(e0);
     hipEventDestroy(e1);
   }
   printf("\n");
   fflush(stdout);
+  return res;
 }
 
-int main() {
+// in-projections of the bf16 step (A = the f32 residual stream today) with A read as f32 (as
+// now) and as a bf16 image of the same values: default and best tile of each, weighted by the
+// launches per step (bench.py --shape-table, profiles/r05/gemm_h3r/shapes_bf16.json)
+struct InProj { int M, K, N, epi, launches; };
+static int a16_mode() {
+  const std::vector<InProj> v = {
+      {49442, 384, 768, EPI_GLU, 12},  {98813, 256, 512, EPI_GLU, 8},   {24753, 512, 1024, EPI_GLU, 8},
+      {197561, 192, 384, EPI_GLU, 4},  {49442, 384, 864, EPI_NONE, 6},  {98813, 256, 576, EPI_NONE, 4},
+      {197561, 192, 432, EPI_NONE, 2}, {24753, 512, 1152, EPI_NONE, 4}, {49442, 384, 272, EPI_NONE, 6},
+      {98813, 256, 272, EPI_NONE, 4},  {197561, 192, 272, EPI_NONE, 2}, {24753, 512, 544, EPI_NONE, 4},
+      {49442, 384, 48, EPI_NONE, 12},  {98813, 256, 48, EPI_NONE, 8},   {197561, 192, 48, EPI_NONE, 4},
+      {24753, 512, 96, EPI_NONE, 8},
+  };
+  double t32d = 0, t32b = 0, t16d = 0, t16b = 0, wr = 0;
+  for (const InProj& q : v) {
+    SweepResult r32, r16;
+    if (q.epi == EPI_GLU) {
+      r32 = sweep<float, __bf16, EPI_GLU>({q.M, q.K, q.N, false, true, EPI_GLU});
+      r16 = sweep<__bf16, __bf16, EPI_GLU>({q.M, q.K, q.N, true, true, EPI_GLU});
+    } else {
+      r32 = sweep<float, __bf16, EPI_NONE>({q.M, q.K, q.N, false, true, EPI_NONE});
+      r16 = sweep<__bf16, __bf16, EPI_NONE>({q.M, q.K, q.N, true, true, EPI_NONE});
+    }
+    printf("  => M %d K %d N %d epi %d x%d: f32-A default %.1f best %.1f (%s) | bf16-A default %.1f best %.1f (%s)\n",
+           q.M, q.K, q.N, q.epi, q.launches, r32.def_us, r32.best_us, r32.best, r16.def_us, r16.best_us, r16.best);
+    t32d += q.launches * r32.def_us; t32b += q.launches * r32.best_us;
+    t16d += q.launches * r16.def_us; t16b += q.launches * r16.best_us;
+    wr += q.launches * (double)q.M * q.K * 2;  // the producer's extra bf16 image write
+  }
+  printf("per step: f32-A default %.3f ms best %.3f ms | bf16-A default %.3f ms best %.3f ms | "
+         "producer bf16 image writes %.1f MB (%.3f ms at 5 TB/s)\n",
+         t32d / 1e3, t32b / 1e3, t16d / 1e3, t16b / 1e3, wr / 1e6, wr / 5e12 * 1e3);
+  return 0;
+}
+
+int main(int argc, char** argv) {
   // bench.py --shape-table, bf16 mode, 68M, 1 h per step (profiles/r03/ffn_w2sets/)
   std::vector<Shape> shapes = {
       {49442, 384, 768, false, true, EPI_NONE},   {49442, 384, 384, true, false, EPI_RESADD},
@@ -171,6 +212,7 @@ int main() {
   hipMemcpy(dA16, hA16.data(), maxA * 2, hipMemcpyHostToDevice);
   hipMemcpy(dB, hB16.data(), maxB * 2, hipMemcpyHostToDevice);
   hipMemcpy(dbias, hbias.data(), 4096 * 4, hipMemcpyHostToDevice);
+  if (argc > 1 && !strcmp(argv[1], "a16")) return a16_mode();
   for (auto& s : shapes) {
     if (!s.a16 && s.c16 && s.epi == EPI_NONE) sweep<float, __bf16, EPI_NONE>(s);
     else if (s.a16 && !s.c16 && s.epi == EPI_RESADD) sweep<__bf16, float, EPI_RESADD>(s);
