@@ -877,9 +877,11 @@ def bench_pipe(args):
 
     def steps(k):
         # k steps = k passes of the hour through the pipe, pipelined (FullPipe.run_many)
-        r = pipe.run_many(k, args.rover_passes_per_call)[-1]
+        rs = pipe.run_many(k, args.rover_passes_per_call)
+        r = rs[-1]
         out.update(windows=len(r["windows"]), words=len(r["words"]), rows=r["vibert_rows"],
-                   vibert_runs=r["vibert_runs"], tokens=r["tokens"])
+                   vibert_runs=r["vibert_runs"], tokens=r["tokens"],
+                   token_ids=[o["token_ids"] for o in rs])
 
     if args.warmup:
         steps(args.warmup)
@@ -919,6 +921,15 @@ def bench_pipe(args):
     fl = f_dec + f_cam + f_vib
     p_dec = MFMA_BF16_PEAK_TFLOPS if args.precision != "fp32" else MFMA_F32_PEAK_TFLOPS
     t_roof = f_dec / (p_dec * 1e12) + (f_cam + f_vib) / (MFMA_F32_PEAK_TFLOPS * 1e12)
+    # the decode stage's tokens of every timed pass vs the oracle's decode of the hour (the
+    # pipe cuts and weights the bench hour exactly as the config-2 / 3 lines do; data only)
+    ocheck = None
+    if (world == 1 and not args.shard_plan and
+            getattr(args, "weights", "greedy-calibrated") == "greedy-calibrated"):
+        chunks_h = [audio[a:a + n] for a, n in zip(pipe.c_off_all, pipe.c_len_all)]
+        golden = hour_golden(args, beam, hotwords[0] if hotwords else None, chunks_h)
+        if golden is not None:
+            ocheck = oracle_agreement(golden[0], golden[1], out["token_ids"], golden[2])
     if rank == 0:
         line = {"metric": "audio-sec/sec full pipe (decode + CAM++ embeddings + ViBERT punctuation)",
                 "value": round(args.audio_sec * (1 if args.shard_plan else world) * args.steps / el, 2),
@@ -961,6 +972,8 @@ def bench_pipe(args):
                                      "peak (exact f32, their reference tolerances); per-stage "
                                      "roofs in the asr / campp stage lines"},
                 "cpu_baseline": cpu}
+        if ocheck is not None:
+            line["oracle_check"] = ocheck
         print(json.dumps(line))
         if args.profile_out:
             with open(args.profile_out, "w") as f:
@@ -1800,7 +1813,7 @@ def main():
     if (rec is not None and world == 1 and args.parity_precision != "none"
             and args.parity_precision != args.precision):
         parity = run_parity_child()
-    # configs 3 and 4 in the token-exact mode, each in its own child process, beside the
+    # configs 3, 4 and 5 in the token-exact mode, each in its own child process, beside the
     # default config-2 line (bounded: a few steps each)
     subs = None
     if (rec is not None and world == 1 and not args.no_sub_lines and beam == 1 and
@@ -1822,6 +1835,12 @@ def main():
                  "--warmup", "1"]))
         except Exception as e:
             subs["config4_rover_f16x3"] = {"error": str(e)[:400]}
+        try:
+            subs["config5_pipe_f16x3"] = sub_line(run_sub_bench(
+                ["--stage", "pipe", "--precision", args.parity_precision, "--no-cpu-baseline",
+                 "--steps", k_sub, "--warmup", "1"]))
+        except Exception as e:
+            subs["config5_pipe_f16x3"] = {"error": str(e)[:400]}
 
     if rank == 0:
         hw_tag = (f" + hotwords ({len(hotwords[0])} phrases of {os.path.basename(hw_path)})"

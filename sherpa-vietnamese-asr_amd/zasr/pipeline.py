@@ -263,7 +263,9 @@ class FullPipe:
                         embs, win = self._gather_windows(embs, win)
                     outs.append({"words": words, "tokens": tokens, "text": text,
                                  "vibert_runs": runs, "vibert_rows": rows, "embeddings": embs,
-                                 "windows": win})
+                                 "windows": win,
+                                 "token_ids": [r.token_ids.tolist()
+                                               for r in res_all[p * n:(p + 1) * n]]})
         return outs
 
     def _gather_windows(self, embs: np.ndarray, win: np.ndarray):

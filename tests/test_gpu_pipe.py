@@ -61,6 +61,72 @@ def test_pipe_words_equal_host_decode_and_merge(pipe):
     assert out["tokens"] == sum(int(r.token_ids.size) for r in res) > 0
 
 
+def test_pipe_tokens_match_oracle(pipe):
+    """The pipe's ASR stage pinned to the oracle, not only to its own stage run alone: every
+    planner chunk of the file decoded by the oracle (numpy fbank, fp32 encoder restatement,
+    the reference's search at beam 1 = greedy) gives the pipe's tokens, frames and log-probs.
+    The model emits sparsely and with several token ids (25-36 tokens of 465-796 frames per
+    chunk, 4-5 ids), so the check sees blank / non-blank decisions and token choice."""
+    from oracle.fbank import fbank
+    from oracle.search import beam_search
+    from oracle.zipformer import ZipformerOracle
+    from zasr.model import synth_weights, zipformer_tiny
+    p, audio, out, _ = pipe
+    cfg = zipformer_tiny(64)
+    orc = ZipformerOracle(cfg, synth_weights(cfg, 5, blank_bias=-1.5))
+    chunks = [audio[a:a + n] for a, n in zip(p.c_off, p.c_len)]
+    res = p.rec.decode(chunks, beam=1)
+    ids = set()
+    for r, c in zip(res, chunks):
+        toks, frames, lps, T, _ = beam_search(orc.encoder(fbank(c)), orc.decoder, orc.joiner, 1)
+        assert r.T == T
+        assert r.token_ids.tolist() == toks
+        assert r.frames.tolist() == list(frames)
+        np.testing.assert_allclose(r.log_probs, lps, rtol=0, atol=1e-3)
+        assert 0 < len(toks) < T // 4
+        ids |= set(toks)
+    assert len(ids) >= 3
+    assert out["tokens"] == sum(int(r.token_ids.size) for r in res)
+
+
+def test_pipe_embeddings_match_oracle(pipe):
+    """The pipe's speaker embeddings against the CAM++ oracle (oracle/campplus.py, f64: the
+    random-init network is ill-conditioned, tests/test_gpu_campp.py) on the same windows: the
+    device fbank + CMVN of each region (pinned to the reference's fbank on its own,
+    test_campp_fbank_matches_reference) cut by the window plan, L2-normalised as the pipe
+    does.  Bound: the reference's CAM++ acceptance, rel_l2 <= 2e-4 over the batch
+    (core/calibration.py:71-78), or 1.5x the f32 oracle's own distance from the f64 result
+    where that is larger (test_campp_embedding_matches_oracle_large_batch's observation)."""
+    from oracle.campplus import CamppOracle
+    from zasr.campp import CamppConfig, window_plan
+    from zasr.campp import synth_weights as campp_weights
+    from zasr.pipeline import l2_normalise
+    p, audio, out, _ = pipe
+    ccfg = CamppConfig()
+    feats = []
+    for a, n in zip(p.r_off, p.r_len):
+        fb = p.emb.fbank(audio[a:a + n])
+        for s, k in window_plan(fb.shape[0]):
+            x = np.zeros((150, 80), np.float32)
+            x[:k] = fb[s:s + k]
+            feats.append(x)
+    assert len(feats) == out["embeddings"].shape[0] >= 2
+    cw = campp_weights(ccfg, 3)
+    x = np.stack(feats)
+    ref = l2_normalise(CamppOracle(ccfg, cw, dtype=np.float64).embed(x).astype(np.float64))
+    f32 = l2_normalise(CamppOracle(ccfg, cw).embed(x).astype(np.float64))
+    got = out["embeddings"].astype(np.float64)
+
+    def rel(a):
+        return float(np.linalg.norm(a - ref) / np.linalg.norm(ref))
+    per = np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    print(f"pipe embeddings vs oracle (f64): rel_l2 {rel(got):.2e} (worst window "
+          f"{per.max():.2e}; the f32 oracle {rel(f32):.2e}) over {len(per)} windows")
+    # the acceptance number, or f32 quality where the f32 oracle itself misses it on this
+    # batch (the random-init network amplifies f32 rounding in a few windows)
+    assert rel(got) <= max(2e-4, 1.5 * rel(f32)), (rel(got), rel(f32), per.max())
+
+
 def test_pipe_embeddings_equal_host_windows(pipe):
     from zasr.campp import window_plan
     from zasr.pipeline import l2_normalise
@@ -126,3 +192,4 @@ def test_pipelined_passes_equal_single_pass(pipe):
         assert [w["text"] for w in o["words"]] == [w["text"] for w in out["words"]]
         assert np.array_equal(o["embeddings"], out["embeddings"])
         assert o["text"] == out["text"] and o["vibert_rows"] == out["vibert_rows"]
+        assert o["token_ids"] == out["token_ids"]
