@@ -249,8 +249,10 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
     const __bf16* __restrict__ yin, const __bf16* __restrict__ x, long npos,
     const __bf16* __restrict__ w1, const float* __restrict__ b1, const __bf16* __restrict__ w2,
     const float* __restrict__ b2, __bf16* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) __bf16 Ys[kMlpM * kMlpLd];
-  __shared__ __attribute__((aligned(16))) __bf16 Hs[kMlpM * kMlpLd];
+  // Y and H tiles in one array: the epilogue stages O + b2 over both
+  __shared__ __attribute__((aligned(16))) __bf16 YH[2 * kMlpM * kMlpLd];
+  __bf16* const Ys = YH;
+  __bf16* const Hs = YH + kMlpM * kMlpLd;
   __shared__ float sB1[384];
   const long p0 = (long)blockIdx.x * kMlpM;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -339,31 +341,48 @@ __global__ __launch_bounds__(256, 2) void convnext_mlp_kernel(
     }
   }
 
-  // ---- out = x + O + b2: lane holds position t*32 + col, channels 32 wid + 8 g + 4 half + e ----
-  // residual loads unconditional (clamped) and all in flight together; stores guarded
-  bf16x4 xr[4][4];
+  // ---- out = x + (O + b2) through LDS: O + b2 staged [position][channel] f32 over the Y / H
+  // tiles, then each lane owns 16-byte pieces of whole 256-byte output rows (the fragment layout
+  // would store 8-byte pieces of 32 rows per instruction: 1.43 -> 1.25 ms per hour,
+  // tools/cnx_lab.hip, bit-identical) ----
+  constexpr int OLD = 132;  // f32 row stride: 528 B
+  static_assert(kMlpM * OLD * 4 <= 2 * kMlpM * kMlpLd * 2, "O staging fits the Y / H tiles");
+  float* Os = reinterpret_cast<float*>(YH);
+  bf16x8 xr8[8];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      long pp = p0 + t * 32 + col;
-      pp = pp < npos ? pp : npos - 1;
-      xr[g][t] = *reinterpret_cast<const bf16x4*>(x + pp * 128 + wid * 32 + 8 * g + 4 * half);
-    }
+  for (int k = 0; k < 8; ++k) {  // residual pieces in flight under the staging
+    const int e = tid + 256 * k;
+    long pp = p0 + (e >> 4);
+    pp = pp < npos ? pp : npos - 1;
+    xr8[k] = *reinterpret_cast<const bf16x8*>(x + pp * 128 + 8 * (e & 15));
+  }
+  lds_barrier_cx();  // every wave's last pw2 is done reading Hs
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int ch = wid * 32 + 8 * g + 4 * half;
     const float4 bo = *reinterpret_cast<const float4*>(b2 + ch);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const long pp = p0 + t * 32 + col;
-      bf16x4 o;
-      o[0] = (__bf16)((float)xr[g][t][0] + (acc2[t][4 * g + 0] + bo.x));
-      o[1] = (__bf16)((float)xr[g][t][1] + (acc2[t][4 * g + 1] + bo.y));
-      o[2] = (__bf16)((float)xr[g][t][2] + (acc2[t][4 * g + 2] + bo.z));
-      o[3] = (__bf16)((float)xr[g][t][3] + (acc2[t][4 * g + 3] + bo.w));
-      if (pp < npos) *reinterpret_cast<bf16x4*>(out + pp * 128 + ch) = o;
+      float4 v;
+      v.x = acc2[t][4 * g + 0] + bo.x;
+      v.y = acc2[t][4 * g + 1] + bo.y;
+      v.z = acc2[t][4 * g + 2] + bo.z;
+      v.w = acc2[t][4 * g + 3] + bo.w;
+      *reinterpret_cast<float4*>(Os + (t * 32 + col) * OLD + ch) = v;
     }
+  }
+  lds_barrier_cx();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int e = tid + 256 * k, pl = e >> 4, c8 = 8 * (e & 15);
+    const long pp = p0 + pl;
+    const float4 a = *reinterpret_cast<const float4*>(Os + pl * OLD + c8);
+    const float4 b = *reinterpret_cast<const float4*>(Os + pl * OLD + c8 + 4);
+    const float ov[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (__bf16)((float)xr8[k][q] + ov[q]);
+    if (pp < npos) *reinterpret_cast<bf16x8*>(out + pp * 128 + c8) = o;
   }
 }
 
