@@ -26,9 +26,9 @@
 namespace zasr {
 
 #ifdef ZASR_FFN_STAMPS  // development: per-phase wall clock of block 0 (tools/ffnw_lab.hip)
-__device__ long long g_ffn_stamps[4096];
+__device__ long long g_ffn_stamps[4896];
 #define FFN_STAMP(i) \
-  if (blockIdx.x == 0 && threadIdx.x == 0 && (i) < 4096) g_ffn_stamps[(i)] = clock64();
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (i) < 4896) g_ffn_stamps[(i)] = clock64();
 #else
 #define FFN_STAMP(i)
 #endif
@@ -68,6 +68,16 @@ __device__ __forceinline__ V buf_load16(__amdgpu_buffer_rsrc_t rs, int voff, int
 }
 
 }  // namespace
+
+// split barriers (SB, the wide kernels below): cumulative per-wave counters in LDS, polled
+__device__ __forceinline__ void lds_wait_ge(int* p, int target) {
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+    __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void lds_signal(int* p, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's H stores / reads are done
+  if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 template <int D>
 __global__ __launch_bounds__(256, (D <= 192 ? 2 : 1)) void ffn_fused_kernel(float* __restrict__ X, int R, int F,
@@ -492,7 +502,16 @@ __device__ __forceinline__ void mfma16_h3(f32x4v& acc, const f16x8& wh, const f1
 }
 }  // namespace
 
-template <int D, int TUM, int NB, int NW>
+// SB (split barrier; NB == 1): the chunk's two block barriers become LDS counters per half of
+// the hidden chunk.  Waves 0 .. NW/2 - 1 own units [0, HC/2), the others [HC/2, HC); phase B's
+// first HC/64 k-steps read only the low half.  A wave writes its half of H(c) once every wave
+// has finished reading that half of H(c - 1), announces it, waits for the LOW half to be
+// complete, runs the low k-steps, announces them read, and waits for the high half only
+// before its high k-steps -- so the waves that finish phase A first (waves 0 .. 3 issue ahead
+// of their SIMD partners) run their low phase-B MFMAs while the partners are still in
+// SwooshL, instead of idling at a block barrier (per-wave stamps: profiles/r06/ffn_pp/).
+// Same products in the same order: bit-identical to the barrier form.
+template <int D, int TUM, int NB, int NW, bool SB = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __restrict__ X, int R, int F,
                                                              const __bf16* __restrict__ W1,
                                                              const float* __restrict__ b1,
@@ -509,10 +528,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   static_assert(OW % 16 == 0, "tile shape");
   __shared__ __attribute__((aligned(16))) _Float16 sX[2][TTM * XLD];
   __shared__ __attribute__((aligned(16))) _Float16 sH[NB][2][TTM * HLD];
+  // SB: waves that wrote H low / high, waves done reading H low / high (cumulative counts)
+  __shared__ int sFlag[4];
+  static_assert(!SB || NB == 1, "split barriers: one H buffer");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g4 = lane >> 4;
+  if (SB && tid < 4) sFlag[tid] = 0;  // visible after the first tile's X barrier
+  const bool lo_half = wid < NW / 2;
+  int gc = 0;  // chunks done by this block (all tiles): the counters' targets
   // this block's rows [r0, r1): rpb (a multiple of 16) per block, one block per CU, so every
   // CU gets the same share instead of a last round of a few TTM-row tiles
   const long r0 = (long)blockIdx.x * rpb;
@@ -551,8 +576,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
 
   // one tile of TU x 16 rows from t0 (the block's whole tiles at TUM, its last one at what is
   // left); the weight rings run on across tiles (the last chunk prefetches chunk 0)
+#ifdef ZASR_FFN_STAMPS
+  int kt = 0;  // development: per-tile stamps at 1000 + 100 kt (tools/ffnh3_lab.hip)
+#define FFN_TSTAMP(i) FFN_STAMP(1000 + 100 * (kt < 30 ? kt : 30) + (i))
+  // every wave of block 0, tile 1: 4000 + 100 wave + 4 c + phase
+#define FFN_WSTAMP(i) \
+  if (blockIdx.x == 0 && lane == 0 && kt == 1) g_ffn_stamps[4000 + 100 * wid + (i)] = clock64();
+#else
+#define FFN_TSTAMP(i)
+#define FFN_WSTAMP(i)
+#endif
   auto tile = [&](auto tu_c, const long t0) {
   constexpr int TU = decltype(tu_c)::value, TT = 16 * TU;
+  FFN_TSTAMP(0)
   // ---- X tile -> two fp16 piece images (rows past R: a clamped duplicate, never written) ----
   {
     constexpr int NE = TT * D / 4 / (64 * NW);
@@ -584,6 +620,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   }
   lds_barrier();
   FFN_STAMP(1)
+  FFN_TSTAMP(1)
 
   f32x4v o[OT][TU];
 #pragma unroll
@@ -616,6 +653,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
       }
     };
     FFN_STAMP(8 + 4 * c)
+    FFN_TSTAMP(2 + 4 * (c & 15))
+    FFN_WSTAMP(4 * (c & 15) + 0)
     read_x(0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -629,10 +668,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
       __builtin_amdgcn_sched_barrier(0);
     }
     FFN_STAMP(9 + 4 * c)
+    FFN_TSTAMP(3 + 4 * (c & 15))
+    FFN_WSTAMP(4 * (c & 15) + 1)
     // ---- + b1, SwooshL, split -> H pieces ----
     _Float16* sH0 = sH[NB == 2 ? (c & 1) : 0][0];
     _Float16* sH1 = sH[NB == 2 ? (c & 1) : 0][1];
-    if constexpr (NB == 1) lds_barrier();  // the previous chunk's phase B is done with sH
+    if constexpr (SB) {  // every wave has read this wave's half of H(c - 1)
+      if (gc > 0) lds_wait_ge(&sFlag[lo_half ? 2 : 3], NW * gc);
+    } else if constexpr (NB == 1) {
+      lds_barrier();  // the previous chunk's phase B is done with sH
+    }
     {
       // hidden units past F: zero H, the pieces masked (no branch: its waits would drain the
       // weight loads in flight)
@@ -652,8 +697,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
         *reinterpret_cast<f16x4*>(&sH1[ho]) = ll;
       }
     }
-    lds_barrier();
+    if constexpr (SB) {
+      lds_signal(&sFlag[lo_half ? 0 : 1], lane);
+      lds_wait_ge(&sFlag[0], (NW / 2) * (gc + 1));  // the low half of H(c) is complete
+    } else {
+      lds_barrier();
+    }
     FFN_STAMP(10 + 4 * c)
+    FFN_TSTAMP(4 + 4 * (c & 15))
+    FFN_WSTAMP(4 * (c & 15) + 2)
     // ---- phase B: step s + 1's H fragments are read before step s's MFMAs ----
     f16x8 hf[2][TU][2];
     auto read_h = [&](int s, int buf) {
@@ -664,10 +716,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
         hf[buf][u][1] = *reinterpret_cast<const f16x8*>(&sH1[ho]);
       }
     };
+    constexpr int SL = HC / 64;  // the first k-step over the high half of the chunk
     read_h(0, 0);
 #pragma unroll
     for (int s = 0; s < HC / 32; ++s) {
-      if (s + 1 < HC / 32) read_h(s + 1, (s + 1) & 1);
+      if (s + 1 < HC / 32 && !(SB && s + 1 == SL)) read_h(s + 1, (s + 1) & 1);
 #pragma unroll
       for (int t = 0; t < OT; ++t) {
         const f16x8 wh = w2r[s & 1][t][0], wl = w2r[s & 1][t][1];
@@ -681,9 +734,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
 #pragma unroll
         for (int q = 0; q < P1; ++q) load_w1(cn, q, q);
       }
+      if constexpr (SB) {
+        if (s == SL - 1) {  // low half read; the high half once its writers are done
+          lds_signal(&sFlag[2], lane);
+          lds_wait_ge(&sFlag[1], (NW / 2) * (gc + 1));
+          read_h(SL, SL & 1);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (SB) lds_signal(&sFlag[3], lane);
+    ++gc;
     FFN_STAMP(11 + 4 * c)
+    FFN_TSTAMP(5 + 4 * (c & 15))
+    FFN_WSTAMP(4 * (c & 15) + 3)
   }
 
   // ---- X[tok][ch] += O^T 2^-11 + b2 (+ bypass_mid) ----
@@ -712,6 +776,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
       *reinterpret_cast<float4*>(xr + ch) = v;
     }
   }
+  FFN_TSTAMP(90)
+#ifdef ZASR_FFN_STAMPS
+  ++kt;
+#endif
   };  // tile
 
   using T1 = std::integral_constant<int, 1>;
@@ -734,6 +802,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   static_assert(TUM <= 8, "tail tiles");
   if (tail == TUM) tile(TM{}, t0);
 }
+
+// split barriers in the one-H-buffer instances but d = 128 (default; there the variant spills
+// and measured 4 % slower, d = 192 / 256 / 384 3-4 % faster: profiles/r06/ffn_pp/sb.txt);
+// ffn_h3_set_split(0): block barriers everywhere (the labs' A/B switch)
+static int g_ffn_split = 1;
+void ffn_h3_set_split(int on) { g_ffn_split = on; }
 
 bool ffn_h3_supported(int D, int F) {
   return ((D == 128 || D == 256 || D == 384 || D == 512) && F % 32 == 0 && F >= 32) ||
@@ -783,9 +857,13 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
   const int bpc = D == 192 ? 2 : 1;
   const int rpb = 16 * cdiv(cdiv(R, bpc * cus[dev]), 16);
   const dim3 grid(cdiv(R, rpb));
-#define ZASR_FFNH3(DV, TUV, NBV, NWV)                                                              \
-  ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV>), grid, dim3(64 * NWV), 0, st, X, R, F, w1, \
-                     b1, w2, b2, byp_orig, byp_scale, rpb, Y)
+#define ZASR_FFNH3(DV, TUV, NBV, NWV)                                                                \
+  if (NBV == 1 && g_ffn_split && DV != 128)                                                       \
+    ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV, NBV == 1>), grid, dim3(64 * NWV), 0, st, X, \
+                R, F, w1, b1, w2, b2, byp_orig, byp_scale, rpb, Y);                                \
+  else                                                                                             \
+    ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV, false>), grid, dim3(64 * NWV), 0, st, X, R, \
+                F, w1, b1, w2, b2, byp_orig, byp_scale, rpb, Y)
   switch (D) {
     // tile rows (16 TUM) / H buffers: the largest tile the LDS and 256 VGPRs hold -- fewer
     // weight passes from L2 and barriers per row, for a barrier per chunk with one H buffer

@@ -308,6 +308,8 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
 // F % 64 == 0; every |w| < 31
 // (ffn_h3_weights_ok: the kernel scales the weights' fp16 hi piece by 2^11)
 bool ffn_h3_supported(int D, int F);
+// development A/B switch of the f16x3 FFN's split barriers (default 1; 0: block barriers)
+void ffn_h3_set_split(int on);
 bool ffn_h3_weights_ok(const float* w, long n);
 void ffn_pack_h3_host(const float* w, int rows, int cols, __bf16* out);
 // Y (nullable): the rows the FFN reads when they are not X's own -- X += FFN(Y) (the ConvNeXt

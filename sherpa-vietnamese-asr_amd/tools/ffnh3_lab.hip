@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -102,7 +103,30 @@ static void run(int D, int F, int R, bool sepY = false) {
   // last row (tail tile) too
   const double rms = std::sqrt(ref2 / ((double)rows * D));
   const float ub = time_launch([&] { launch_ffn_fused(dX, R, D, F, dH1, db1, dH2, db2, 0, nullptr, nullptr); });
-  const float us = time_launch([&] { launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr); });
+  // split barriers (default) against block barriers: bit-identical outputs, interleaved
+  // timings (the clock state drifts between back-to-back timings), best of 3 each
+  bool same_sb = true;
+  {
+    float* dX2;
+    hipMalloc(&dX2, x.size() * 4);
+    hipMemcpy(dX2, x.data(), x.size() * 4, hipMemcpyHostToDevice);
+    ffn_h3_set_split(0);
+    launch_ffn_fused_h3(dX2, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr, dY);
+    ffn_h3_set_split(1);
+    std::vector<float> y0(x.size());
+    hipMemcpy(y0.data(), dX2, y0.size() * 4, hipMemcpyDeviceToHost);
+    same_sb = memcmp(y0.data(), y.data(), y.size() * 4) == 0;
+    hipFree(dX2);
+  }
+  float us_bar = 1e30f, us = 1e30f;
+  for (int rep = 0; rep < 3; ++rep) {
+    ffn_h3_set_split(0);
+    us_bar = std::min(us_bar, time_launch([&] { launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr); }));
+    ffn_h3_set_split(1);
+    us = std::min(us, time_launch([&] { launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr); }));
+  }
+  printf("  block barriers %.1f us -> split barriers %.1f us (%s)\n", us_bar, us,
+         same_sb ? "bit-identical" : "OUTPUTS DIFFER");
   const double fl = 4.0 * R * D * F;
 #ifdef ZASR_FFN_STAMPS
   {
@@ -113,6 +137,38 @@ static void run(int D, int F, int R, bool sepY = false) {
       printf(" | c%d A %lld swl %lld B %lld", c, st[9 + 4 * c] - st[8 + 4 * c], st[10 + 4 * c] - st[9 + 4 * c],
              st[11 + 4 * c] - st[10 + 4 * c]);
     printf("\n");
+    // per tile of block 0: X staging, chunk phases summed, epilogue (shader cycles)
+    static long long ts[4896];
+    hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_ffn_stamps), sizeof(ts));
+    const int nch = (F + 127) / 128;
+    for (int k = 0; k < 30; ++k) {
+      const long long* t = ts + 1000 + 100 * k;
+      if (t[0] == 0 || t[90] == 0 || t[90] < t[0]) break;
+      long long a = 0, w = 0, b = 0;
+      for (int c = 0; c < nch && c < 16; ++c) {
+        a += t[3 + 4 * c] - t[2 + 4 * c];
+        w += t[4 + 4 * c] - t[3 + 4 * c];
+        b += t[5 + 4 * c] - t[4 + 4 * c];
+      }
+      const long long last = t[5 + 4 * ((nch - 1) & 15)];
+      printf("    tile %d: total %lld | X %lld | A %lld swl %lld B %lld | epilogue %lld | gap to next %lld\n", k,
+             t[90] - t[0], t[1] - t[0], a, w, b, t[90] - last,
+             (k + 1 < 30 && ts[1000 + 100 * (k + 1)] > t[90]) ? ts[1000 + 100 * (k + 1)] - t[90] : -1);
+    }
+    // every wave of block 0, tile 1: A start / A end / H barrier passed / B end, per chunk,
+    // relative to the earliest A start of the chunk
+    for (int c = 0; c < nch && c < 4; ++c) {
+      long long t0w = 1LL << 62;
+      for (int w = 0; w < 8; ++w) t0w = std::min(t0w, ts[4000 + 100 * w + 4 * c]);
+      printf("    tile 1 chunk %d per wave (A start, A end, H ready, B end):", c);
+      for (int w = 0; w < 8; ++w) {
+        const long long* q = ts + 4000 + 100 * w + 4 * c;
+        printf(" w%d %lld/%lld/%lld/%lld", w, q[0] - t0w, q[1] - t0w, q[2] - t0w, q[3] - t0w);
+      }
+      printf("\n");
+    }
+    memset(ts, 0, sizeof(ts));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_ffn_stamps), ts, sizeof(ts));
   }
 #endif
   if (dY) hipFree(dY);
@@ -125,6 +181,28 @@ static void run(int D, int F, int R, bool sepY = false) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "sb")) {  // the bench's shapes
+    run(384, 1024, 49442);
+    run(384, 1280, 49442);
+    run(384, 768, 49442);
+    run(256, 768, 98813);
+    run(256, 960, 98813);
+    run(256, 576, 98813);
+    run(192, 512, 197614);
+    run(128, 384, 3753659, true);
+    run(512, 1536, 24753);  // control: two H buffers, block barriers in both arms
+    run(384, 1280, 3029);   // small shapes: tails, one tile
+    run(128, 384, 100, true);
+    run(192, 512, 100);
+    return 0;
+  }
+  if (argc > 1 && !strcmp(argv[1], "tiles")) {  // the bench's largest shapes, per-tile stamps
+    run(384, 1024, 49442);
+    run(256, 768, 98813);
+    run(512, 1536, 24753);
+    run(128, 384, 3753659, true);
+    return 0;
+  }
   run(128, 384, 100, true);
   run(128, 384, 100);
   // the last block's remainder a whole TUM-group tile (rows past R clamped): rpb 224, 60 left
