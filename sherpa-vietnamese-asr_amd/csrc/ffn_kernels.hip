@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256, (D <= 192 ? 2 : 1)) void ffn_fused_kernel(floa
 // phase ahead: the chunk's W2 fragments are issued before its phase A, the next chunk's W1
 // fragments right after this chunk's phase A.  Two barriers per chunk around the H write.
 // Epilogue as above: X += O^T + b2 (+ bypass_mid).
-template <int D>
+template <int D, bool EB = true>
 __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X, int R, int F,
                                                           const __bf16* __restrict__ W1,
                                                           const float* __restrict__ b1,
@@ -409,6 +409,56 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
   }
 
   // ---- X[tok][ch] += O^T + b2 (+ bypass_mid): lane's token, 4 consecutive channels ----
+  if constexpr (EB) {
+    // the residual (and bypass) pieces of two row groups loaded together, rows past R clamped
+    // (loaded, never stored): two memory round trips instead of one per row group
+    float4 bv[OT], kv[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      const int ch = wid * OW + 16 * t + 4 * g4;
+      bv[t] = *reinterpret_cast<const float4*>(b2 + ch);
+      if (byp_orig != nullptr) kv[t] = *reinterpret_cast<const float4*>(byp_scale + ch);
+    }
+#pragma unroll
+    for (int u0 = 0; u0 < 4; u0 += 2) {
+    float4 xv[2][OT], b0v[2][OT];
+#pragma unroll
+    for (int du = 0; du < 2; ++du) {
+      const long tok = min(t0 + 16 * (u0 + du) + r16, (long)R - 1);
+#pragma unroll
+      for (int t = 0; t < OT; ++t) {
+        const int ch = wid * OW + 16 * t + 4 * g4;
+        xv[du][t] = *reinterpret_cast<const float4*>(X + tok * D + ch);
+        if (byp_orig != nullptr) b0v[du][t] = *reinterpret_cast<const float4*>(byp_orig + tok * D + ch);
+      }
+    }
+#pragma unroll
+    for (int du = 0; du < 2; ++du) {
+      const int u = u0 + du;
+      const long tok = t0 + 16 * u + r16;
+      if (tok >= R) continue;
+      float* xr = X + tok * D;
+#pragma unroll
+      for (int t = 0; t < OT; ++t) {
+        const int ch = wid * OW + 16 * t + 4 * g4;
+        float4 v = xv[du][t];
+        v.x += o[t][u][0] + bv[t].x;
+        v.y += o[t][u][1] + bv[t].y;
+        v.z += o[t][u][2] + bv[t].z;
+        v.w += o[t][u][3] + bv[t].w;
+        if (byp_orig != nullptr) {
+          const float4 b0 = b0v[du][t], k = kv[t];
+          v.x = b0.x + (v.x - b0.x) * k.x;
+          v.y = b0.y + (v.y - b0.y) * k.y;
+          v.z = b0.z + (v.z - b0.z) * k.z;
+          v.w = b0.w + (v.w - b0.w) * k.w;
+        }
+        *reinterpret_cast<float4*>(xr + ch) = v;
+      }
+    }
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const long tok = t0 + 16 * u + r16;
@@ -511,7 +561,7 @@ __device__ __forceinline__ void mfma16_h3(f32x4v& acc, const f16x8& wh, const f1
 // of their SIMD partners) run their low phase-B MFMAs while the partners are still in
 // SwooshL, instead of idling at a block barrier (per-wave stamps: profiles/r06/ffn_pp/).
 // Same products in the same order: bit-identical to the barrier form.
-template <int D, int TUM, int NB, int NW, bool SB = false>
+template <int D, int TUM, int NB, int NW, bool SB = false, bool EB = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __restrict__ X, int R, int F,
                                                              const __bf16* __restrict__ W1,
                                                              const float* __restrict__ b1,
@@ -751,6 +801,59 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
   }
 
   // ---- X[tok][ch] += O^T 2^-11 + b2 (+ bypass_mid) ----
+  if constexpr (EB) {
+    // the residual (and bypass) rows of up to two 16-row groups loaded together, rows past r1
+    // clamped (loaded, never stored): one memory round trip per group pair instead of one
+    // per (group, channel tile) behind each row guard (the tile's epilogue was ~9 % of it)
+    float4 bv[OT], kv[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      const int ch = wid * OW + 16 * t + 4 * g4;
+      bv[t] = *reinterpret_cast<const float4*>(b2 + ch);
+      if (byp_orig != nullptr) kv[t] = *reinterpret_cast<const float4*>(byp_scale + ch);
+    }
+#pragma unroll
+    for (int u0 = 0; u0 < TU; u0 += 2) {
+      constexpr int UB = TU >= 2 ? 2 : 1;
+      float4 xv[UB][OT], b0v[UB][OT];
+#pragma unroll
+      for (int du = 0; du < UB; ++du) {
+        if (u0 + du >= TU) break;
+        const long tok = min(t0 + 16 * (u0 + du) + r16, r1 - 1);
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+          const int ch = wid * OW + 16 * t + 4 * g4;
+          xv[du][t] = *reinterpret_cast<const float4*>(X + tok * D + ch);
+          if (byp_orig != nullptr) b0v[du][t] = *reinterpret_cast<const float4*>(byp_orig + tok * D + ch);
+        }
+      }
+#pragma unroll
+      for (int du = 0; du < UB; ++du) {
+        const int u = u0 + du;
+        if (u >= TU) break;
+        const long tok = t0 + 16 * u + r16;
+        if (tok >= r1) continue;
+        float* xr = X + tok * D;
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+          const int ch = wid * OW + 16 * t + 4 * g4;
+          float4 v = xv[du][t];
+          v.x += o[t][u][0] * kF16LoInv + bv[t].x;
+          v.y += o[t][u][1] * kF16LoInv + bv[t].y;
+          v.z += o[t][u][2] * kF16LoInv + bv[t].z;
+          v.w += o[t][u][3] * kF16LoInv + bv[t].w;
+          if (byp_orig != nullptr) {
+            const float4 b0 = b0v[du][t], k = kv[t];
+            v.x = b0.x + (v.x - b0.x) * k.x;
+            v.y = b0.y + (v.y - b0.y) * k.y;
+            v.z = b0.z + (v.z - b0.z) * k.z;
+            v.w = b0.w + (v.w - b0.w) * k.w;
+          }
+          *reinterpret_cast<float4*>(xr + ch) = v;
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int u = 0; u < TU; ++u) {
     const long tok = t0 + 16 * u + r16;
@@ -775,6 +878,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void ffn_wide_h3_kernel(float* __r
       }
       *reinterpret_cast<float4*>(xr + ch) = v;
     }
+  }
   }
   FFN_TSTAMP(90)
 #ifdef ZASR_FFN_STAMPS
@@ -857,13 +961,15 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
   const int bpc = D == 192 ? 2 : 1;
   const int rpb = 16 * cdiv(cdiv(R, bpc * cus[dev]), 16);
   const dim3 grid(cdiv(R, rpb));
+// SB (split barriers) with one H buffer, EB (batched epilogue loads) but at d = 128: the
+// ConvNeXt instance spills with either and measured 4 % / 1.4 % slower (profiles/r06/ffn_pp/)
 #define ZASR_FFNH3(DV, TUV, NBV, NWV)                                                                \
   if (NBV == 1 && g_ffn_split && DV != 128)                                                       \
-    ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV, NBV == 1>), grid, dim3(64 * NWV), 0, st, X, \
-                R, F, w1, b1, w2, b2, byp_orig, byp_scale, rpb, Y);                                \
+    ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV, NBV == 1, DV != 128>), grid, dim3(64 * NWV), \
+                0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale, rpb, Y);                       \
   else                                                                                             \
-    ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV, false>), grid, dim3(64 * NWV), 0, st, X, R, \
-                F, w1, b1, w2, b2, byp_orig, byp_scale, rpb, Y)
+    ZASR_LAUNCH((ffn_wide_h3_kernel<DV, TUV, NBV, NWV, false, DV != 128>), grid, dim3(64 * NWV), 0, \
+                st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale, rpb, Y)
   switch (D) {
     // tile rows (16 TUM) / H buffers: the largest tile the LDS and 256 VGPRs hold -- fewer
     // weight passes from L2 and barriers per row, for a barrier per chunk with one H buffer
@@ -908,7 +1014,10 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
     ZASR_REQUIRE(F % 32 == 0 && F >= 32 && F <= kMaxF,
                  "ffn_fused: feed-forward dim must be a multiple of 32 in [32, 2048] for D >= 256");
     const dim3 grid(cdiv(R, 64));
-#define ZASR_FFNW(DV) ZASR_LAUNCH(ffn_wide_kernel<DV>, grid, dim3(512), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
+// EB (batched epilogue loads) at d = 384: 1.5-2 % (profiles/r06/ffn_pp/ffnw_eb.txt); d = 512
+// neutral, and at d = 256 it takes the kernel past 128 VGPRs (one block per CU instead of two)
+#define ZASR_FFNW(DV) \
+  ZASR_LAUNCH((ffn_wide_kernel<DV, DV == 384>), grid, dim3(512), 0, st, X, R, F, w1, b1, w2, b2, byp_orig, byp_scale)
     switch (D) {
       case 256: ZASR_FFNW(256); break;
       case 384: ZASR_FFNW(384); break;

@@ -7,6 +7,7 @@
 # process of the bench; it is measured in the plain runs).
 # Usage (from the repo root, via gpurun): bash sherpa-vietnamese-asr_amd/tools/profile_round.sh TAG [PART]
 # PART 1 / 2 runs the first / second half (each within one gpurun call's limit); default both.
+# PART 3: the f16x3 line's PMC passes and config 5 in f16x3.
 set -e
 TAG=${1:-r}
 PART=${2:-all}
@@ -14,7 +15,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-if [ "$PART" != 2 ]; then
+if [ "$PART" != 2 ] && [ "$PART" != 3 ]; then
 timeout -k 10 400 python3 $R/bench.py > $OUT/bench.json 2> $OUT/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 $R/bench.py --no-cpu-baseline --parity-precision none --steps 3 --warmup 1 > $OUT/stats_bench.json 2> $OUT/stats.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --parity-precision none --steps 1 --warmup 1 > $OUT/pmc_fetch.log 2>&1
@@ -27,7 +28,7 @@ timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --method modified_beam_s
 # config 3 on the beam-calibrated weights (beam 8 emits at the greedy rate) and its f16x3 form
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --weights beam-calibrated --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_beamcal.json 2> $OUT/bench_beam8_beamcal.err
 fi
-if [ "$PART" != 1 ]; then
+if [ "$PART" != 1 ] && [ "$PART" != 3 ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats_f16x3 -o run -- python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --steps 3 --warmup 1 > $OUT/stats_f16x3.json 2> $OUT/stats_f16x3.err
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_f16x3.json 2> $OUT/bench_beam8_f16x3.err
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --weights beam-calibrated --precision f16x3 --parity-precision none --method modified_beam_search --beam 8 --hotwords-file default > $OUT/bench_beam8_hotwords_f16x3_beamcal.json 2> $OUT/bench_beam8_f16x3_beamcal.err
@@ -40,5 +41,12 @@ timeout -k 10 300 python3 $R/bench.py --stage dropin --precision bf16 --steps 3 
 # DESIGN §9's single-GPU proxies of the 8-rank shard plan (largest LPT share of the hour)
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline --parity-precision none --proxy-ranks 8 > $OUT/bench_proxy8.json 2> $OUT/bench_proxy8.err
 timeout -k 10 300 python3 $R/bench.py --stage rover --steps 4 --warmup 1 --hotwords-file default --no-cpu-baseline --proxy-ranks 8 > $OUT/bench_rover_proxy8.json 2> $OUT/bench_rover_proxy8.err
+fi
+if [ "$PART" = 3 ]; then
+# the token-exact f16x3 line's PMC passes (HBM bytes, MFMA busy) and config 5 in f16x3
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_f16x3_fetch -o run -- python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --no-sub-lines --steps 1 --warmup 1 > $OUT/pmc_f16x3_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_f16x3_write -o run -- python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --no-sub-lines --steps 1 --warmup 1 > $OUT/pmc_f16x3_write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_f16x3_mfma -o run -- python3 $R/bench.py --no-cpu-baseline --precision f16x3 --parity-precision none --no-sub-lines --steps 1 --warmup 1 > $OUT/pmc_f16x3_mfma.log 2>&1
+timeout -k 10 300 python3 $R/bench.py --stage pipe --precision f16x3 --steps 4 --warmup 1 > $OUT/bench_pipe_f16x3.json 2> $OUT/bench_pipe_f16x3.err
 fi
 echo done
