@@ -10,7 +10,8 @@ gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads (MI355X_MICROAR
 Kernel classes: enc_gemm = gemm_bf16_kernel / gemm_f32_kernel with the dense A loader
 (template argument ALOAD = 0) and a [N][K] weight operand, the launches Engine::linear /
 linear_h make (the NonlinAttention GEMM, EPI_MULAUX, is class attn_nonlin); any other class
-name matches kernels whose name contains it (e.g. ffn_fused).
+name matches kernels whose name contains it; ffn_fused = the fused FeedforwardModule kernels
+(bf16 ffn_fused / ffn_wide, f16x3 ffn_wide_h3 but its d = 128 ConvNeXt instance).
 """
 import argparse
 import csv
@@ -32,8 +33,23 @@ def gemm_args(name: str):
     return None, None
 
 
+def _int_args(name: str, kernel: str):
+    m = re.search(kernel + r"<([^>]*)>", name)
+    return [a.strip() for a in m.group(1).split(",")] if m else None
+
+
 def in_class(name: str, cls: str) -> bool:
     if cls == "enc_gemm":
+        # f16x3 projections: the row-resident kernel, and the dense-A instances of the LDS-DMA
+        # and register-tile kernels (ALOAD 0; the others are the subsampling convolutions)
+        if "gemm_h3r_kernel" in name:
+            return True
+        a = _int_args(name, "gemm_glds_h3_kernel")
+        if a is not None:
+            return a[5] == "0" and a[1] not in ("4", "5")
+        a = _int_args(name, "gemm_x3_kernel")
+        if a is not None:
+            return a[4] == "0" and a[5] not in ("4", "5")
         if "gemm_glds_kernel" in name:  # multi-stage LDS-DMA variant: its EPI_MULAUX(16)
             # z-sliced instances are the NonlinAttention product (class attn_nonlin)
             m = re.search(r"gemm_glds_kernel(?:<\s*\d+,\s*(\d+)|ILi\d+ELi(\d+)E)", name)
@@ -47,6 +63,11 @@ def in_class(name: str, cls: str) -> bool:
             return args[5] == "0" and args[6] != "4"  # EPI_MULAUX = the NonlinAttention GEMM
         return args[4] == "0" and args[5] == "false"  # B n-contiguous = nonlin_attention
 
+    if cls == "ffn_fused":  # the fused FeedforwardModule launches: bf16 ffn_fused / ffn_wide,
+        # f16x3 ffn_wide_h3 except its d = 128 instance (the ConvNeXt MLP, class frontend_conv)
+        if "ffn_wide_h3_kernel" in name:
+            return "ffn_wide_h3_kernelILi128E" not in name and "ffn_wide_h3_kernel<128" not in name
+        return "ffn_wide_kernel" in name or "ffn_fused_kernel" in name
     return cls in name
 
 
