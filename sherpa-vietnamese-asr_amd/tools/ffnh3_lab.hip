@@ -180,7 +180,77 @@ static void run(int D, int F, int R, bool sepY = false) {
   hipFree(dX); hipFree(db1); hipFree(db2); hipFree(dW1); hipFree(dW2); hipFree(dH1); hipFree(dH2);
 }
 
+// the ConvNeXt MLP (d = 128, F = 384, Y separate) at other tile heights / split barriers /
+// batched epilogue, against the engine's instance: bit-identical outputs, interleaved timings
+template <int TU, bool SB, bool EB>
+static float cnx_variant(float* X, int R, const __bf16* w1, const float* b1, const __bf16* w2,
+                         const float* b2, const float* Y, bool time_it) {
+  const int rpb = 16 * cdiv(cdiv(R, 256), 16);
+  const dim3 grid(cdiv(R, rpb));
+  auto go = [&] {
+    hipLaunchKernelGGL((ffn_wide_h3_kernel<128, TU, 1, 8, SB, EB>), grid, dim3(512), 0, 0, X, R, 384, w1,
+                       b1, w2, b2, nullptr, nullptr, rpb, Y);
+  };
+  if (!time_it) { go(); hipDeviceSynchronize(); return 0.f; }
+  return time_launch(go);
+}
+
+static void cnx_mode() {
+  const int D = 128, F = 384, R = 3753659;
+  std::mt19937 g(5);
+  std::normal_distribution<float> nd(0.f, 1.f);
+  std::vector<float> x((size_t)R * D), y((size_t)R * D), b1(F), b2(D), w1((size_t)F * D), w2((size_t)D * F);
+  for (auto& v : x) v = nd(g);
+  for (auto& v : y) v = nd(g);
+  for (auto& v : b1) v = 0.1f * nd(g);
+  for (auto& v : b2) v = 0.1f * nd(g);
+  for (auto& v : w1) v = nd(g) / std::sqrt((float)D);
+  for (auto& v : w2) v = nd(g) / std::sqrt((float)F);
+  std::vector<__bf16> p1(2 * w1.size()), p2(2 * w2.size());
+  ffn_pack_h3_host(w1.data(), F, D, p1.data());
+  ffn_pack_h3_host(w2.data(), D, F, p2.data());
+  float *dX, *dY, *db1, *db2;
+  __bf16 *dW1, *dW2;
+  hipMalloc(&dX, x.size() * 4); hipMalloc(&dY, y.size() * 4); hipMalloc(&db1, F * 4); hipMalloc(&db2, D * 4);
+  hipMalloc(&dW1, p1.size() * 2); hipMalloc(&dW2, p2.size() * 2);
+  hipMemcpy(dY, y.data(), y.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db1, b1.data(), F * 4, hipMemcpyHostToDevice);
+  hipMemcpy(db2, b2.data(), D * 4, hipMemcpyHostToDevice);
+  hipMemcpy(dW1, p1.data(), p1.size() * 2, hipMemcpyHostToDevice);
+  hipMemcpy(dW2, p2.data(), p2.size() * 2, hipMemcpyHostToDevice);
+  std::vector<float> ref(x.size()), got(x.size());
+  auto fresh = [&] { hipMemcpy(dX, x.data(), x.size() * 4, hipMemcpyHostToDevice); };
+  fresh();
+  launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr, dY);
+  hipMemcpy(ref.data(), dX, ref.size() * 4, hipMemcpyDeviceToHost);
+  struct V { const char* name; std::function<float(bool)> f; float best; };
+  std::vector<V> vs = {
+      {"engine (TU 8, block barriers)", [&](bool t) { return t ? time_launch([&] { launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr, dY); }) : (launch_ffn_fused_h3(dX, R, D, F, dW1, db1, dW2, db2, 0, nullptr, nullptr, dY), 0.f); }, 1e30f},
+      {"TU 8 SB", [&](bool t) { return cnx_variant<8, true, false>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+      {"TU 8 EB", [&](bool t) { return cnx_variant<8, false, true>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+      {"TU 7", [&](bool t) { return cnx_variant<7, false, false>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+      {"TU 7 SB", [&](bool t) { return cnx_variant<7, true, false>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+      {"TU 6 SB", [&](bool t) { return cnx_variant<6, true, false>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+      {"TU 6 SB EB", [&](bool t) { return cnx_variant<6, true, true>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+      {"TU 5 SB EB", [&](bool t) { return cnx_variant<5, true, true>(dX, R, dW1, db1, dW2, db2, dY, t); }, 1e30f},
+  };
+  for (auto& v : vs) {
+    fresh();
+    v.f(false);
+    hipMemcpy(got.data(), dX, got.size() * 4, hipMemcpyDeviceToHost);
+    printf("  %-32s %s\n", v.name, memcmp(got.data(), ref.data(), got.size() * 4) ? "OUTPUTS DIFFER" : "bit-identical");
+  }
+  for (int rep = 0; rep < 3; ++rep)
+    for (auto& v : vs) v.best = std::min(v.best, v.f(true));
+  for (auto& v : vs) printf("  %-32s %.1f us\n", v.name, v.best);
+  fflush(stdout);
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "cnx")) {
+    cnx_mode();
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "sb")) {  // the bench's shapes
     run(384, 1024, 49442);
     run(384, 1280, 49442);
