@@ -46,6 +46,14 @@ struct H3RArgs {
   int rpb;                  // rows per block (multiple of 16)
 };
 
+#ifdef ZASR_H3R_STAMPS  // development: per-wave stamps of block 0 (tools/h3r_lab.hip)
+__device__ long long g_h3r_stamps[8 * 64 * 4];
+#define H3R_STAMP(k, i)                                                                        \
+  if (blockIdx.x == 0 && lane == 0 && (k) < 64) g_h3r_stamps[(wid * 64 + (k)) * 4 + (i)] = clock64();
+#else
+#define H3R_STAMP(k, i)
+#endif
+
 template <int K, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
   // row stride in halves: 16 (8 j + 2)-byte rows keep the 16x16x32 operand reads conflict-free
@@ -86,9 +94,12 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
 #pragma unroll
   for (int s = 0; s < P1; ++s) load_w(0, s, s);
 
+  int kt = 0;  // tiles done (stamps)
   auto tile = [&](auto tu_c, const long t0, bool first) {
     constexpr int TU = decltype(tu_c)::value, TT = 16 * TU;
+    H3R_STAMP(kt, 0)
     if (!first) lds_barrier_h3r();  // every wave is done reading the previous tile
+    H3R_STAMP(kt, 1)
     // ---- A tile -> two fp16 piece images (rows past M: a clamped duplicate, never written)
     {
       constexpr int NQ = TT * K / 4, NE = (NQ + 64 * NW - 1) / (64 * NW);  // float4 per thread
@@ -115,6 +126,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
       }
     }
     lds_barrier_h3r();
+    H3R_STAMP(kt, 2)
 
     f16x8 xf[2][TU][2];
     auto read_x = [&](int s, int buf) {
@@ -186,6 +198,8 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
         }
       }
     }
+    H3R_STAMP(kt, 3)
+    ++kt;
   };
 
   using TM = std::integral_constant<int, TUM>;
