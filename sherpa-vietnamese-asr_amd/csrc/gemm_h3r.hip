@@ -94,7 +94,9 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
 #pragma unroll
   for (int s = 0; s < P1; ++s) load_w(0, s, s);
 
+#ifdef ZASR_H3R_STAMPS
   int kt = 0;  // tiles done (stamps)
+#endif
   auto tile = [&](auto tu_c, const long t0, bool first) {
     constexpr int TU = decltype(tu_c)::value, TT = 16 * TU;
     H3R_STAMP(kt, 0)
@@ -199,7 +201,9 @@ __global__ __launch_bounds__(512, 1) void gemm_h3r_kernel(H3RArgs a) {
       }
     }
     H3R_STAMP(kt, 3)
+#ifdef ZASR_H3R_STAMPS
     ++kt;
+#endif
   };
 
   using TM = std::integral_constant<int, TUM>;
