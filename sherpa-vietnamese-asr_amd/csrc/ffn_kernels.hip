@@ -486,6 +486,223 @@ __global__ __launch_bounds__(512, 1) void ffn_wide_kernel(float* __restrict__ X,
   }
 }
 
+// ffn_wide_kernel over a per-CU share of the rows ("rows" form, d = 384): one block per CU
+// walks rpb rows (a multiple of 16) in 64-token tiles and a 16-48-token tail tile.  One block
+// per 64-token tile ran d = 384's 773 tiles in 4 rounds of the 256 CUs for 3.02 rounds of
+// work: the rows form measured 1.08-1.10x at F = 768 / 1024 / 1280, bit-identical
+// (tools/ffnw_lab.hip, profiles/r06/ffn_rows/).  Not at d = 256 (0.82-0.87x: one block per
+// tile runs two blocks per CU whose X staging and epilogues overlap each other's chunks; the
+// rows form at two blocks per CU spills) nor d = 512 (0.95x, spills).
+template <int D, bool EB>
+__global__ __launch_bounds__(512, 2) void ffn_rows_kernel(float* __restrict__ X, int R, int F,
+                                                          const __bf16* W1,
+                                                          const float* __restrict__ b1,
+                                                          const __bf16* W2,
+                                                          const float* __restrict__ b2,
+                                                          const float* __restrict__ byp_orig,
+                                                          const float* __restrict__ byp_scale,
+                                                          int rpb) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int TUM = 4, HC = 128, NW = 8;
+  constexpr int XLD = D + 16, HLD = HC + 16;  // as ffn_wide_kernel
+  constexpr int KS = D / 32;
+  constexpr int OW = D / NW, OT = OW / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 sX[16 * TUM * XLD];
+  constexpr int NB = D >= 384 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) __bf16 sH[NB][16 * TUM * HLD];
+  __shared__ __attribute__((aligned(16))) float sB1[kMaxF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const long r0 = (long)blockIdx.x * rpb;
+  const long r1 = r0 + rpb < R ? r0 + rpb : R;
+  const int nch = (F + HC - 1) / HC;
+  const int S2 = F / 32;
+  bf16x8 w1f[KS];
+  auto load_w1 = [&](int c) {
+    const int rg = min((c * HC) / 16 + wid, F / 16 - 1);
+    const __bf16* p = W1 + ((long)rg * KS * 64 + lane) * 8;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) w1f[s] = *reinterpret_cast<const bf16x8*>(p + s * 512);
+  };
+  constexpr int W2S = ZASR_FFN_W2SETS;
+  bf16x8 w2f[W2S][4][OT];
+  auto load_w2 = [&](int c, auto set) {
+    constexpr int S = decltype(set)::value;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ks = min(c * (HC / 32) + s, S2 - 1);
+#pragma unroll
+      for (int t = 0; t < OT; ++t)
+        w2f[S][s][t] = *reinterpret_cast<const bf16x8*>(W2 + (((long)(wid * OW / 16 + t) * S2 + ks) * 64 + lane) * 8);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, W2S - 1>;
+  for (int e = tid; e < F; e += 64 * NW) sB1[e] = b1[e];  // published by the first X barrier
+
+  auto tile = [&](auto tu_c, const long t0) __attribute__((always_inline)) {
+    constexpr int TU = decltype(tu_c)::value, TT = 16 * TU;
+    // the X tile's element indices and addresses from a per-tile copy of tid: hoisted out of
+    // the tile loop they stay live through it (24+ VGPRs at d = 384: spills)
+    int tix = tid;
+    asm volatile("" : "+v"(tix));
+    // ---- X tile -> bf16 LDS (rows past R: a clamped duplicate, never written back); every
+    // wave read the previous tile's sX (its last phase A) before the last H barrier ----
+    {
+      static_assert(TT * D / 4 % (64 * NW) == 0, "X tile staging");
+      constexpr int NE = TT * D / 4 / (64 * NW);
+      float4 v[NE];
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = tix + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
+        const long r = t0 + row < R ? t0 + row : R - 1;
+        v[i] = *reinterpret_cast<const float4*>(X + r * D + 4 * c4);
+      }
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = tix + 64 * NW * i, row = e / (D / 4), c4 = e - row * (D / 4);
+        bf16x4 b;
+        b[0] = (__bf16)v[i].x; b[1] = (__bf16)v[i].y; b[2] = (__bf16)v[i].z; b[3] = (__bf16)v[i].w;
+        *reinterpret_cast<bf16x4*>(&sX[row * XLD + 4 * c4]) = b;
+      }
+    }
+    // the first chunk's weights, behind the X tile (a prefetch from the previous tile's last
+    // chunk, or ahead of the X loads, holds the weight registers live through the epilogue /
+    // the X conversion: 256 VGPRs and scratch; W1 / W2 are not __restrict__, whose invariant
+    // loads the compiler hoists out of the tile loop for the same effect)
+    load_w1(0);
+    load_w2(0, I0{});
+    lds_barrier();  // (also: every wave is done with the previous tile's H buffers)
+
+    f32x4 o[OT][TU];
+#pragma unroll
+    for (int t = 0; t < OT; ++t)
+#pragma unroll
+      for (int u = 0; u < TU; ++u) o[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto chunk = [&](int c, auto set) __attribute__((always_inline)) {
+      constexpr int S = decltype(set)::value;
+      const int hid0 = c * HC + wid * 16;
+      const bool hvalid = hid0 < F;
+      __bf16* sHc = sH[NB == 2 ? (c & 1) : 0];
+      f32x4 ha[TU];
+#pragma unroll
+      for (int u = 0; u < TU; ++u) ha[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+          const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&sX[(16 * u + r16) * XLD + 32 * s + 8 * g4]);
+          ha[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[s], xb, ha[u], 0, 0, 0);
+        }
+      }
+      if constexpr (NB == 1) lds_barrier();
+      if (hvalid) {
+        const float4 bb = *reinterpret_cast<const float4*>(&sB1[hid0 + 4 * g4]);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+          bf16x4 p;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p[q] = (__bf16)swooshl_fast(ha[u][q] + bv[q]);
+          *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = p;
+        }
+      } else {
+        const bf16x4 z = {(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+#pragma unroll
+        for (int u = 0; u < TU; ++u) *reinterpret_cast<bf16x4*>(&sHc[(16 * u + r16) * HLD + wid * 16 + 4 * g4]) = z;
+      }
+      lds_barrier();
+      // the next chunk's weights (unconditional: the last chunk's re-load is dead code)
+      const int cn = min(c + 1, nch - 1);
+      load_w1(cn);
+      if constexpr (W2S == 2) load_w2(cn, std::integral_constant<int, 1 - S>{});
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 hf[TU];
+#pragma unroll
+        for (int u = 0; u < TU; ++u) hf[u] = *reinterpret_cast<const bf16x8*>(&sHc[(16 * u + r16) * HLD + 32 * s + 8 * g4]);
+#pragma unroll
+        for (int t = 0; t < OT; ++t)
+#pragma unroll
+          for (int u = 0; u < TU; ++u) o[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[S][s][t], hf[u], o[t][u], 0, 0, 0);
+      }
+      if constexpr (W2S == 1) load_w2(cn, I0{});
+    };
+    for (int c = 0; c < nch; c += W2S) {
+      chunk(c, I0{});
+      if constexpr (W2S == 2) {
+        if (c + 1 < nch) chunk(c + 1, I1{});
+      }
+    }
+
+    // ---- X[tok][ch] += O^T + b2 (+ bypass_mid): lane's token, 4 consecutive channels ----
+    int g4e = g4;  // (per tile, as tix: the epilogue's b2 / scale loads and addresses)
+    asm volatile("" : "+v"(g4e));
+    float4 bv[OT], kv[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      const int ch = wid * OW + 16 * t + 4 * g4e;
+      bv[t] = *reinterpret_cast<const float4*>(b2 + ch);
+      if (byp_orig != nullptr) kv[t] = *reinterpret_cast<const float4*>(byp_scale + ch);
+    }
+    // EB: the residual (and bypass) pieces of two row groups loaded together
+    constexpr int UB = EB ? 2 : 1;
+#pragma unroll
+    for (int u0 = 0; u0 < TU; u0 += UB) {
+      float4 xv[UB][OT], b0v[UB][OT];
+#pragma unroll
+      for (int du = 0; du < UB; ++du) {
+        if (u0 + du >= TU) break;
+        const long tok = min(t0 + 16 * (u0 + du) + r16, (long)R - 1);
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+          const int ch = wid * OW + 16 * t + 4 * g4e;
+          xv[du][t] = *reinterpret_cast<const float4*>(X + tok * D + ch);
+          if (byp_orig != nullptr) b0v[du][t] = *reinterpret_cast<const float4*>(byp_orig + tok * D + ch);
+        }
+      }
+#pragma unroll
+      for (int du = 0; du < UB; ++du) {
+        const int u = u0 + du;
+        if (u >= TU) break;
+        const long tok = t0 + 16 * u + r16;
+        if (tok >= r1) continue;
+        float* xr = X + tok * D;
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+          const int ch = wid * OW + 16 * t + 4 * g4e;
+          float4 v = xv[du][t];
+          v.x += o[t][u][0] + bv[t].x;
+          v.y += o[t][u][1] + bv[t].y;
+          v.z += o[t][u][2] + bv[t].z;
+          v.w += o[t][u][3] + bv[t].w;
+          if (byp_orig != nullptr) {
+            const float4 b0 = b0v[du][t], k = kv[t];
+            v.x = b0.x + (v.x - b0.x) * k.x;
+            v.y = b0.y + (v.y - b0.y) * k.y;
+            v.z = b0.z + (v.z - b0.z) * k.z;
+            v.w = b0.w + (v.w - b0.w) * k.w;
+          }
+          *reinterpret_cast<float4*>(xr + ch) = v;
+        }
+      }
+    }
+  };
+
+  using TM = std::integral_constant<int, TUM>;
+  long t0 = r0;
+  for (; t0 + 16 * TUM <= r1; t0 += 16 * TUM) tile(TM{}, t0);
+  // 0-3 row groups left (rpb is a multiple of 16), up to 4 in the last block (R need not be)
+  const int tail = (int)((r1 - t0 + 15) / 16);
+  if (tail == 1) tile(std::integral_constant<int, 1>{}, t0);
+  if (tail == 2) tile(std::integral_constant<int, 2>{}, t0);
+  if (tail == 3) tile(std::integral_constant<int, 3>{}, t0);
+  if (tail == 4) tile(TM{}, t0);
+}
+
 // ---- f16x3 wide FFN (the token-exact mode) ----
 // The same FeedforwardModule at f32 quality: every product on fp16 MFMAs over the two pieces
 // x = hi + lo 2^-11 (gemm_dev.h split_h8), here in the one-accumulator form -- the weight's hi
@@ -998,6 +1215,9 @@ void ffn_pack_host(const __bf16* w, int rows, int cols, __bf16* out) {
               w[(size_t)(16 * g + (l & 15)) * cols + 32 * s + 8 * (l >> 4) + j];
 }
 
+// development A/B switch: ffn_rows_kernel vs ffn_wide_kernel (tools/ffnw_lab.hip)
+static int g_ffnw_rows = 1;
+
 bool ffn_fused_supported(int D) {
   return D == 64 || D == 96 || D == 128 || D == 192 || D == 256 || D == 384 || D == 512;
 }
@@ -1014,6 +1234,21 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
     ZASR_REQUIRE(F % 32 == 0 && F >= 32 && F <= kMaxF,
                  "ffn_fused: feed-forward dim must be a multiple of 32 in [32, 2048] for D >= 256");
     const dim3 grid(cdiv(R, 64));
+    static int cus[64] = {0};
+    int dev = 0;
+    ZASR_HIP_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+      int n = 0;
+      ZASR_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+      cus[dev] = n > 0 ? n : 256;
+    }
+    if (D == 384 && g_ffnw_rows) {
+      const int rpb = 16 * cdiv(cdiv(R, cus[dev]), 16);
+      ZASR_LAUNCH((ffn_rows_kernel<384, true>), dim3(cdiv(R, rpb)), dim3(512), 0, st, X, R, F, w1, b1, w2, b2,
+                  byp_orig, byp_scale, rpb);
+      return;
+    }
 // EB (batched epilogue loads) at d = 384: 1.5-2 % (profiles/r06/ffn_pp/ffnw_eb.txt); d = 512
 // neutral, and at d = 256 it takes the kernel past 128 VGPRs (one block per CU instead of two)
 #define ZASR_FFNW(DV) \

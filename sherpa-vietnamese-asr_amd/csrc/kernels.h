@@ -33,12 +33,14 @@ void launch_silence_flags(const float* wav, long n, int frame_len, float thresho
 
 // a no-op kernel of block_threads threads through ZASR_LAUNCH, synchronised (zasr_selftest_launch)
 void launch_selftest_noop(int block_threads);
-// kernel self-tests on host operands (selftest.cpp; zasr_selftest_gemm_h3r / _ffn_h3)
+// kernel self-tests on host operands (selftest.cpp; zasr_selftest_gemm_h3r / _ffn_h3 / _ffn_bf16)
 void selftest_gemm_h3r(int M, int K, int N, int epi, const float* A, const float* W,
                        const float* bias, float* C);
 void selftest_ffn_h3(int R, int D, int F, const float* Y, const float* W1, const float* b1,
                      const float* W2, const float* b2, const float* byp_orig,
                      const float* byp_scale, float* X);
+void selftest_ffn_bf16(int R, int D, int F, const float* W1, const float* b1, const float* W2,
+                       const float* b2, const float* byp_orig, const float* byp_scale, float* X);
 
 // ---- CAM++ speaker embedding (campp_kernels.hip) ----
 struct CamppConv2d {

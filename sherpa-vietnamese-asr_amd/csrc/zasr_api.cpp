@@ -684,6 +684,16 @@ int zasr_selftest_ffn_h3(int32_t R, int32_t D, int32_t F, const float* Y, const 
   });
 }
 
+int zasr_selftest_ffn_bf16(int32_t R, int32_t D, int32_t F, const float* W1, const float* b1,
+                           const float* W2, const float* b2, const float* byp_orig,
+                           const float* byp_scale, float* X) {
+  if (!W1 || !b1 || !W2 || !b2 || !X) return fail(ZASR_ERR_INVALID, "null argument");
+  return guarded([&]() {
+    zasr::selftest_ffn_bf16(R, D, F, W1, b1, W2, b2, byp_orig, byp_scale, X);
+    return (int)ZASR_OK;
+  });
+}
+
 int zasr_silence_flags(const float* d_wav, int64_t n, int32_t frame_len, float threshold,
                        uint8_t* d_flags, void* stream) {
   if (n < 0 || (n > 0 && (!d_wav || !d_flags))) return fail(ZASR_ERR_INVALID, "null argument");
