@@ -348,10 +348,11 @@ int zasr_selftest_ffn_h3(int32_t R, int32_t D, int32_t F, const float* Y, const 
 /* The bf16 mode's fused FeedforwardModule alone on host operands (same conventions):
    X[R][D] += W2 SwooshL(W1 bf16(X) + b1) + b2 with W1 [F][D], W2 [D][F] rounded to bf16 and
    the hidden activation in bf16 (then the bypass_mid blend when byp_orig is given);
-   D in {64, 96, 128, 192, 256, 384, 512}; D >= 256: F % 32 == 0, F <= 2048. */
+   D in {64, 96, 128, 192, 256, 384, 512}; D >= 256: F % 32 == 0, F <= 2048.  form 0: the
+   decode's route; 1: the opt-in per-CU rows form at D = 384 (ZASR_FFN_ROWS=1). */
 int zasr_selftest_ffn_bf16(int32_t R, int32_t D, int32_t F, const float* W1, const float* b1,
                            const float* W2, const float* b2, const float* byp_orig,
-                           const float* byp_scale, float* X);
+                           const float* byp_scale, float* X, int32_t form);
 
 /* profiling: per-kernel-class HIP-event timing on the handle's stream.  on = 0 off,
    1 kernel classes, 2 kernel classes with the encoder GEMMs split by shape

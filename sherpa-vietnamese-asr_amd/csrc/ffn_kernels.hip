@@ -17,6 +17,7 @@
 // Bytes per token: D * 4 read + D * 4 written; the 2 F D bf16 weight bytes are L2-resident.
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -1215,8 +1216,19 @@ void ffn_pack_host(const __bf16* w, int rows, int cols, __bf16* out) {
               w[(size_t)(16 * g + (l & 15)) * cols + 32 * s + 8 * (l >> 4) + j];
 }
 
-// development A/B switch: ffn_rows_kernel vs ffn_wide_kernel (tools/ffnw_lab.hip)
-static int g_ffnw_rows = 1;
+// The rows form (d = 384) is opt-in: ZASR_FFN_ROWS=1 or ffn_set_rows(1).  The kernel alone
+// is 1.08-1.10x, but in the pipelined step its 238 resident blocks hold the CUs for a whole
+// launch and the search chain on the other stream waits: bench 122.2k vs 123.7k xRT (mean of
+// 7 interleaved runs each, profiles/r06/ffn_rows/step_ab.txt).
+static int g_ffnw_rows = -1;
+void ffn_set_rows(int on) { g_ffnw_rows = on ? 1 : 0; }
+int ffn_rows_on() {
+  if (g_ffnw_rows < 0) {
+    const char* e = getenv("ZASR_FFN_ROWS");
+    g_ffnw_rows = e != nullptr && atoi(e) == 1 ? 1 : 0;
+  }
+  return g_ffnw_rows;
+}
 
 bool ffn_fused_supported(int D) {
   return D == 64 || D == 96 || D == 128 || D == 192 || D == 256 || D == 384 || D == 512;
@@ -1243,7 +1255,7 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
       ZASR_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
       cus[dev] = n > 0 ? n : 256;
     }
-    if (D == 384 && g_ffnw_rows) {
+    if (D == 384 && ffn_rows_on()) {
       const int rpb = 16 * cdiv(cdiv(R, cus[dev]), 16);
       ZASR_LAUNCH((ffn_rows_kernel<384, true>), dim3(cdiv(R, rpb)), dim3(512), 0, st, X, R, F, w1, b1, w2, b2,
                   byp_orig, byp_scale, rpb);

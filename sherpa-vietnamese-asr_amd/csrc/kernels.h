@@ -40,7 +40,8 @@ void selftest_ffn_h3(int R, int D, int F, const float* Y, const float* W1, const
                      const float* W2, const float* b2, const float* byp_orig,
                      const float* byp_scale, float* X);
 void selftest_ffn_bf16(int R, int D, int F, const float* W1, const float* b1, const float* W2,
-                       const float* b2, const float* byp_orig, const float* byp_scale, float* X);
+                       const float* b2, const float* byp_orig, const float* byp_scale, float* X,
+                       int form);
 
 // ---- CAM++ speaker embedding (campp_kernels.hip) ----
 struct CamppConv2d {
@@ -312,6 +313,9 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
 bool ffn_h3_supported(int D, int F);
 // development A/B switch of the f16x3 FFN's split barriers (default 1; 0: block barriers)
 void ffn_h3_set_split(int on);
+// the d = 384 bf16 FFN over per-CU row shares (ffn_rows_kernel): off unless ZASR_FFN_ROWS=1
+void ffn_set_rows(int on);
+int ffn_rows_on();
 bool ffn_h3_weights_ok(const float* w, long n);
 void ffn_pack_h3_host(const float* w, int rows, int cols, __bf16* out);
 // Y (nullable): the rows the FFN reads when they are not X's own -- X += FFN(Y) (the ConvNeXt

@@ -76,7 +76,9 @@ void selftest_ffn_h3(int R, int D, int F, const float* Y, const float* W1, const
 }
 
 void selftest_ffn_bf16(int R, int D, int F, const float* W1, const float* b1, const float* W2,
-                       const float* b2, const float* byp_orig, const float* byp_scale, float* X) {
+                       const float* b2, const float* byp_orig, const float* byp_scale, float* X,
+                       int form) {
+  ZASR_REQUIRE(form == 0 || form == 1, "selftest ffn_bf16: form 0 (default route) or 1 (rows form)");
   ZASR_REQUIRE(R >= 1, "selftest ffn_bf16: R >= 1");
   ZASR_REQUIRE(ffn_fused_supported(D), "selftest ffn_bf16: unsupported model dim");
   // W1 [F][D] and W2 [D][F] in bf16; d >= 256 in MFMA-fragment order (the engine's wp)
@@ -103,8 +105,16 @@ void selftest_ffn_bf16(int R, int D, int F, const float* W1, const float* b1, co
     up(dbo, byp_orig, xb);
     up(dbs, byp_scale, (size_t)D * 4);
   }
-  launch_ffn_fused(dX.as<float>(), R, D, F, d1.p, db1.as<float>(), d2.p, db2.as<float>(), nullptr,
-                   byp_orig ? dbo.as<float>() : nullptr, byp_orig ? dbs.as<float>() : nullptr);
+  const int saved = ffn_rows_on();
+  ffn_set_rows(form);
+  try {
+    launch_ffn_fused(dX.as<float>(), R, D, F, d1.p, db1.as<float>(), d2.p, db2.as<float>(), nullptr,
+                     byp_orig ? dbo.as<float>() : nullptr, byp_orig ? dbs.as<float>() : nullptr);
+  } catch (...) {
+    ffn_set_rows(saved);
+    throw;
+  }
+  ffn_set_rows(saved);
   ZASR_HIP_CHECK(hipDeviceSynchronize());
   ZASR_HIP_CHECK(hipMemcpy(X, dX.p, xb, hipMemcpyDeviceToHost));
 }

@@ -686,10 +686,10 @@ int zasr_selftest_ffn_h3(int32_t R, int32_t D, int32_t F, const float* Y, const 
 
 int zasr_selftest_ffn_bf16(int32_t R, int32_t D, int32_t F, const float* W1, const float* b1,
                            const float* W2, const float* b2, const float* byp_orig,
-                           const float* byp_scale, float* X) {
+                           const float* byp_scale, float* X, int32_t form) {
   if (!W1 || !b1 || !W2 || !b2 || !X) return fail(ZASR_ERR_INVALID, "null argument");
   return guarded([&]() {
-    zasr::selftest_ffn_bf16(R, D, F, W1, b1, W2, b2, byp_orig, byp_scale, X);
+    zasr::selftest_ffn_bf16(R, D, F, W1, b1, W2, b2, byp_orig, byp_scale, X, form);
     return (int)ZASR_OK;
   });
 }

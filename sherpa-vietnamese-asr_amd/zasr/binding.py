@@ -217,7 +217,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.zasr_selftest_gemm_h3r.restype = C.c_int
     lib.zasr_selftest_ffn_h3.argtypes = [I32, I32, I32, fp, fp, fp, fp, fp, fp, fp, fp]
     lib.zasr_selftest_ffn_h3.restype = C.c_int
-    lib.zasr_selftest_ffn_bf16.argtypes = [I32, I32, I32, fp, fp, fp, fp, fp, fp, fp]
+    lib.zasr_selftest_ffn_bf16.argtypes = [I32, I32, I32, fp, fp, fp, fp, fp, fp, fp, I32]
     lib.zasr_selftest_ffn_bf16.restype = C.c_int
     if path is None:
         _lib = lib
@@ -293,11 +293,11 @@ def selftest_ffn_h3(Y, W1, b1, W2, b2, X, byp_orig=None, byp_scale=None,
     return X
 
 
-def selftest_ffn_bf16(W1, b1, W2, b2, X, byp_orig=None, byp_scale=None,
+def selftest_ffn_bf16(W1, b1, W2, b2, X, byp_orig=None, byp_scale=None, form: int = 0,
                       lib_path: Optional[str] = None) -> np.ndarray:
     """The bf16 fused FFN alone on host operands (zasr_selftest_ffn_bf16): returns
     X + W2 SwooshL(W1 bf16(X) + b1) + b2 (bf16 weights and hidden activation; then the
-    bypass_mid blend when byp_orig is given)."""
+    bypass_mid blend when byp_orig is given).  form 1: the opt-in rows form at D = 384."""
     lib = load_library(lib_path)
     W1, b1, W2, b2, X = (_f32(v) for v in (W1, b1, W2, b2, X))
     X = X.copy()
@@ -305,7 +305,7 @@ def selftest_ffn_bf16(W1, b1, W2, b2, X, byp_orig=None, byp_scale=None,
     bs = None if byp_scale is None else _f32(byp_scale)
     p = lambda x: None if x is None else x.ctypes.data_as(C_FP)
     rc = lib.zasr_selftest_ffn_bf16(X.shape[0], X.shape[1], W1.shape[0], p(W1), p(b1), p(W2),
-                                    p(b2), p(bo), p(bs), p(X))
+                                    p(b2), p(bo), p(bs), p(X), int(form))
     if rc != 0:
         raise ZasrError(lib.zasr_last_error().decode())
     return X
