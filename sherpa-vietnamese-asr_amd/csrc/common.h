@@ -1,5 +1,6 @@
 // Shared helpers for libzasr (host + device).  gfx950 / CDNA4 only.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -34,6 +35,29 @@
   } while (0)
 
 namespace zasr {
+
+// Grid of the persistent kernels (gemm_h3r, the fused f16x3 FFN: one block per CU, a per-CU
+// share of the rows each).  While the pipelined greedy decode runs a second encoder stream
+// they take 7/8 of the CUs and leave the rest to that stream's kernels (and the search's):
+// f16x3 greedy 69.9k -> 70.7-70.9k xRT at 208-224 blocks of 256, 71.9k vs 70.4k in the
+// final A/B (profiles/r06/persist_ab/); one encoder stream keeps every CU.
+// ZASR_PERSIST_CUS=N overrides (development A/B).
+inline int& persist_share_flag() {
+  static thread_local int on = 0;
+  return on;
+}
+struct PersistShare {  // scoped: the calling thread's launches leave CUs to other streams
+  int prev;
+  explicit PersistShare(bool on) : prev(persist_share_flag()) { persist_share_flag() = on ? 1 : 0; }
+  ~PersistShare() { persist_share_flag() = prev; }
+  PersistShare(const PersistShare&) = delete;
+  PersistShare& operator=(const PersistShare&) = delete;
+};
+inline int persist_blocks(int cus) {
+  static const int cap = getenv("ZASR_PERSIST_CUS") != nullptr ? atoi(getenv("ZASR_PERSIST_CUS")) : -1;
+  if (cap >= 0) return cap > 0 && cap < cus ? cap : cus;
+  return persist_share_flag() ? cus - cus / 8 : cus;
+}
 
 inline void check_launch(const char* file, int line) {
   const hipError_t e = hipGetLastError();

@@ -2124,6 +2124,8 @@ std::vector<TokenResult> Engine::decode_device_batches(const float* d_wav,
     return decode_batches_two_searches(d_wav, wav_off, n, batch_sizes, beam, main_st);
   const int want_e = env_e ? env_e : (beam > 1 ? 1 : 2);
   const int E = std::max(1, std::min({want_e, (int)kMaxEnc, nb - 1}));
+  // a second encoder stream: the persistent kernels leave 1/8 of the CUs to it (common.h)
+  const PersistShare share(E > 1);
   // L: batches whose encoders are queued ahead of the search in flight, one more than the
   // encoder streams (at most kMaxEnc: L + 1 output slots): 111.8-113.1k -> 113.5-114.3k xRT
   // on one box (profiles/r03/enc_ahead/)
@@ -2185,6 +2187,9 @@ std::vector<TokenResult> Engine::decode_batches_two_searches(const float* d_wav,
   const int J = std::max(2, std::min(env_jobs, (int)kMaxJobs));
   const int L = std::max(1, kMaxEnc + 1 - J);
   const int E = std::max(1, std::min(env_e, 2));
+  // (a second encoder stream only: with J beam searches beside one encoder stream the share
+  // measured +2.2 % on config 3 and -1.5..-3 % on the drop-in phase, profiles/r06/persist_ab/)
+  const PersistShare share(E > 1);
   const int NS = J + L;
   ZASR_REQUIRE(NS <= kMaxEnc + 1, "pipeline slots");
   hipStream_t enc_st[2] = {main_st, enc_extra_[0]};

@@ -1177,7 +1177,7 @@ void launch_ffn_fused_h3(float* X, int R, int D, int F, const void* W1, const fl
   }
   // D = 192: 4 waves (48 output channels each), two blocks per CU
   const int bpc = D == 192 ? 2 : 1;
-  const int rpb = 16 * cdiv(cdiv(R, bpc * cus[dev]), 16);
+  const int rpb = 16 * cdiv(cdiv(R, bpc * persist_blocks(cus[dev])), 16);
   const dim3 grid(cdiv(R, rpb));
 // SB (split barriers) with one H buffer, EB (batched epilogue loads) but at d = 128: the
 // ConvNeXt instance spills with either and measured 4 % / 1.4 % slower (profiles/r06/ffn_pp/)
@@ -1256,7 +1256,7 @@ void launch_ffn_fused(float* X, int R, int D, int F, const void* W1, const float
       cus[dev] = n > 0 ? n : 256;
     }
     if (D == 384 && ffn_rows_on()) {
-      const int rpb = 16 * cdiv(cdiv(R, cus[dev]), 16);
+      const int rpb = 16 * cdiv(cdiv(R, persist_blocks(cus[dev])), 16);
       ZASR_LAUNCH((ffn_rows_kernel<384, true>), dim3(cdiv(R, rpb)), dim3(512), 0, st, X, R, F, w1, b1, w2, b2,
                   byp_orig, byp_scale, rpb);
       return;

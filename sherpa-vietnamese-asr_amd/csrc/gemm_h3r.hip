@@ -251,7 +251,7 @@ void gemm_h3r(const float* A, const void* Wp, const float* bias, float* C, int l
     cus[dev] = n > 0 ? n : 256;
   }
   H3RArgs a{A, reinterpret_cast<const __bf16*>(Wp), (long)N * K, bias, C, ldc, M, N,
-            16 * cdiv(cdiv(M, cus[dev]), 16)};
+            16 * cdiv(cdiv(M, persist_blocks(cus[dev])), 16)};
   const dim3 grid(cdiv(M, a.rpb));
 #define ZASR_H3R(KV)                                                                      \
   switch (epi) {                                                                          \
