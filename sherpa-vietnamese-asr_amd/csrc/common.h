@@ -37,10 +37,11 @@
 namespace zasr {
 
 // Grid of the persistent kernels (gemm_h3r, the fused f16x3 FFN: one block per CU, a per-CU
-// share of the rows each).  While the pipelined greedy decode runs a second encoder stream
-// they take 7/8 of the CUs and leave the rest to that stream's kernels (and the search's):
-// f16x3 greedy 69.9k -> 70.7-70.9k xRT at 208-224 blocks of 256, 71.9k vs 70.4k in the
-// final A/B (profiles/r06/persist_ab/); one encoder stream keeps every CU.
+// share of the rows each).  While the pipelined decode runs other streams beside the encoder
+// (the greedy pipeline's second encoder stream, the beam pipeline's J searches) they take 7/8
+// of the CUs and leave the rest to those streams' kernels: f16x3 greedy 69.9k -> 70.7-70.9k
+// xRT at 208-224 blocks of 256, config 3 in f16x3 58.5k -> 59.2k (profiles/r06/persist_ab/);
+// a decode alone on the device keeps every CU.
 // ZASR_PERSIST_CUS=N overrides (development A/B).
 inline int& persist_share_flag() {
   static thread_local int on = 0;

@@ -2187,9 +2187,10 @@ std::vector<TokenResult> Engine::decode_batches_two_searches(const float* d_wav,
   const int J = std::max(2, std::min(env_jobs, (int)kMaxJobs));
   const int L = std::max(1, kMaxEnc + 1 - J);
   const int E = std::max(1, std::min(env_e, 2));
-  // (a second encoder stream only: with J beam searches beside one encoder stream the share
-  // measured +2.2 % on config 3 and -1.5..-3 % on the drop-in phase, profiles/r06/persist_ab/)
-  const PersistShare share(E > 1);
+  // J searches beside the encoder: the persistent kernels leave 1/8 of the CUs to them
+  // (config 3 in f16x3 58.5k -> 59.2k xRT, the drop-in phase within noise: 36.8k / 36.7k,
+  // three interleaved pairs each, profiles/r06/persist_ab/beam_share.txt)
+  const PersistShare share(true);
   const int NS = J + L;
   ZASR_REQUIRE(NS <= kMaxEnc + 1, "pipeline slots");
   hipStream_t enc_st[2] = {main_st, enc_extra_[0]};
