@@ -405,21 +405,23 @@ def test_rover_shared_fbank_equals_separate_decodes(need_gpu):
         assert [w["start"] for w in m1] == [w["start"] for w in m2]
 
 
-@pytest.mark.parametrize("method,beam", [("greedy_search", 1), ("modified_beam_search", 4)])
-def test_pipelined_batches_equal_per_batch_decode(need_gpu, method, beam):
+@pytest.mark.parametrize("method,beam,prec", [("greedy_search", 1, "bf16"), ("modified_beam_search", 4, "bf16"),
+                                              ("greedy_search", 1, "f16x3"), ("modified_beam_search", 4, "f16x3")])
+def test_pipelined_batches_equal_per_batch_decode(need_gpu, method, beam, prec):
     """zasr_decode_device_batches: batch k+1's encoder overlaps batch k's search on two
     streams; every chunk's result must be bit-identical to decoding its batch alone
     (batches of different sizes, an empty batch, short and empty chunks, a batch whose
-    chunks are all too short)."""
-    check_pipelined_batches(method, beam)
+    chunks are all too short).  f16x3: the pipelines' persistent kernels run on 7/8 of the
+    CUs (other row shares per block, common.h PersistShare), a batch alone on all of them."""
+    check_pipelined_batches(method, beam, prec)
 
 
-def check_pipelined_batches(method, beam):
+def check_pipelined_batches(method, beam, prec="bf16"):
     import torch
     from model_fixtures import m_model
     from zasr.binding import Recognizer
     cfg, w, path = m_model()
-    rec = Recognizer(path, method, beam, precision="bf16")
+    rec = Recognizer(path, method, beam, precision=prec)
     secs = [[2.0, 7.5, 0.3], [], [21.0], [0.0, 0.004], [3.3, 1.1, 12.0, 5.0], [9.0]]
     batches = [[_speech(s, 900 + 10 * i + j) if s > 0 else np.zeros(0, np.float32)
                 for j, s in enumerate(b)] for i, b in enumerate(secs)]
@@ -448,7 +450,8 @@ def check_pipelined_batches(method, beam):
     ({"ZASR_SEARCH_JOBS": "3", "ZASR_ENC_STREAMS": "2"}, "modified_beam_search", 4),
     ({"ZASR_SEARCH_CUS": "32"}, "greedy_search", 1),
     ({"ZASR_GREEDY_FUSED": "1"}, "greedy_search", 1),
-], ids=["three_jobs_two_enc_streams", "cu_masked_search", "fused_greedy"])
+    ({"ZASR_PERSIST_CUS": "200"}, "greedy_search", 1),
+], ids=["three_jobs_two_enc_streams", "cu_masked_search", "fused_greedy", "persistent_grid_200"])
 def test_pipelined_batches_env_variants(need_gpu, env, method, beam):
     """The pipeline variants the engine reads from the environment at first use (three beam
     searches in flight + two encoder streams; the CU-partitioned search stream, whose encoder
@@ -457,9 +460,9 @@ def test_pipelined_batches_env_variants(need_gpu, env, method, beam):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_parity as t; "
-            "t.check_pipelined_batches(%r, %d); print('ok')"
+            "t.check_pipelined_batches(%r, %d, %r); print('ok')"
             % (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "sherpa-vietnamese-asr_amd"),
-               method, beam))
+               method, beam, "f16x3" if "ZASR_PERSIST_CUS" in env else "bf16"))
     r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env},
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
